@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""Benchmark: illumstats + correct throughput (sites/s) on MI355X.
+
+Metric (BASELINE.json): sites/sec for 2160x2560 uint16 site images through
+corilla illumination statistics AND ChannelImage.correct.  One *step* is the
+whole job over one channel's resident batch of sites (configs[1]: 384 wells x
+9 sites = 3,456 sites per GPU):
+
+    reset stats -> Welford + per-site histogram/percentiles over every site
+    (tmh_stats_update_device) -> [N>1: RCCL Welford all-reduce merge + ordered
+    percentile chain] -> finalize mean/std -> smooth both planes (sigma 5)
+    -> correction coefficients -> correct every site (tmh_correct_u16_device)
+
+Inputs are synthetic (counter-hash generator, SURVEY.md §8(d) distribution)
+and resident in HBM before timing starts.  With N GPUs each rank owns its own
+3,456 sites (weak scaling) and the merged statistics are identical on every
+rank.  Prints ONE JSON line on rank 0.
+
+    python bench.py                      # N=1, default steps
+    torchrun --nproc-per-node N bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+
+METRIC = "sites/sec (2160×2560 uint16) illumstats+correct; % of HBM roofline at 1–8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--sites", type=int, default=3456, help="sites per GPU (configs[1])")
+    p.add_argument("--height", type=int, default=2160)
+    p.add_argument("--width", type=int, default=2560)
+    p.add_argument("--cpu-sample", type=int, default=24,
+                   help="sites in the bounded CPU-baseline sample (0 disables)")
+    p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
+                   help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+    return p.parse_args()
+
+
+def cpu_baseline(n_sites, H, W, total_sites):
+    """Bounded sample of the CPU oracle (numpy, 1 process, single-threaded
+    elementwise ops) over the same op sequence: per-site stats update +
+    correct, plus the one-time smoothing amortised over the full job."""
+    from oracle import corilla_oracle as orc
+    from tmlibrary_amd.synth import synth_sites_host
+    sites = synth_sites_host(n_sites, H, W, seed=2024)
+    st = orc.OracleOnlineStatistics((H, W))
+    t0 = time.perf_counter()
+    for s in sites:
+        st.update(s)
+    t1 = time.perf_counter()
+    sm_mean = orc.smooth_reflect(st.mean, 5)
+    sm_std = orc.smooth_reflect(st.std, 5)
+    t2 = time.perf_counter()
+    for s in sites:
+        orc.correct_illumination(s, sm_mean, sm_std)
+    t3 = time.perf_counter()
+    per_site = ((t1 - t0) + (t3 - t2)) / n_sites + (t2 - t1) / total_sites
+    return {
+        "value": round(1.0 / per_site, 4),
+        "unit": "sites/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": "%d synthetic %dx%d sites: oracle OnlineStatistics.update x%d + "
+                  "correct_illumination x%d (numpy, 1 process) + smoothing of 2 planes "
+                  "amortised over %d sites; stats %.1f ms/site, correct %.1f ms/site"
+                  % (n_sites, H, W, n_sites, n_sites, total_sites,
+                     1e3 * (t1 - t0) / n_sites, 1e3 * (t3 - t2) / n_sites),
+    }
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    from tmlibrary_amd import hip
+    from tmlibrary_amd.image import ZERO_LOG10
+    from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
+    from tmlibrary_amd.workflow.corilla.sharded import StatsOps, merge_shards
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    L = hip.lib()
+    hip.check(L.tmh_set_device(local_rank))
+    H, W, S = a.height, a.width, a.sites
+    npx = H * W
+    Q = 100000
+    # one non-null stream for our launches AND torch/RCCL work, so they order
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    sp = C.c_void_p(stream.cuda_stream)
+
+    # resident inputs / outputs (int16 tensors = raw uint16 bytes)
+    sites = torch.empty((S, H, W), dtype=torch.int16, device=dev)
+    out = torch.empty_like(sites)
+    hip.check(L.tmh_synth_sites_device(C.c_void_p(sites.data_ptr()), S, H, W, 12345, 0,
+                                       rank * S, sp))
+    mean = torch.empty(npx, dtype=torch.float64, device=dev)
+    std = torch.empty_like(mean)
+    smean = torch.empty_like(mean)
+    sstd = torch.empty_like(mean)
+    tmp = torch.empty_like(mean)
+
+    lo, hi, gamma = quantile_table(npx, np.linspace(0, 100, Q))
+    lut = stats_log10_lut()
+    flags = hip.TMH_STATS_DEFERRED_PCT if world > 1 else 0
+    h = C.c_void_p()
+    hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma), hip.ptr(lut),
+                                 1, flags, C.byref(h)))
+    hip.check(L.tmh_stats_set_stream(h, sp))
+    corr = C.c_void_p()
+    torch.cuda.synchronize(dev)
+    hip.check(L.tmh_corrector_create_device(C.c_void_p(mean.data_ptr()), C.c_void_p(std.data_ptr()),
+                                            H, W, 1, ZERO_LOG10, sp, C.byref(corr)))
+    ops = StatsOps(L, h, npx, Q, dev)
+
+    def step():
+        hip.check(L.tmh_stats_reset(h))
+        hip.check(L.tmh_stats_update_device(h, C.c_void_p(sites.data_ptr()), S, 1, sp))
+        if world > 1:
+            merge_shards(ops, dist)
+        hip.check(L.tmh_stats_finalize_device(h, C.c_void_p(mean.data_ptr()),
+                                              C.c_void_p(std.data_ptr()), sp))
+        hip.check(L.tmh_smooth_f64_device(C.c_void_p(mean.data_ptr()), C.c_void_p(smean.data_ptr()),
+                                          C.c_void_p(tmp.data_ptr()), H, W, 5.0, sp))
+        hip.check(L.tmh_smooth_f64_device(C.c_void_p(std.data_ptr()), C.c_void_p(sstd.data_ptr()),
+                                          C.c_void_p(tmp.data_ptr()), H, W, 5.0, sp))
+        hip.check(L.tmh_corrector_update_device(corr, C.c_void_p(smean.data_ptr()),
+                                                C.c_void_p(sstd.data_ptr()), sp))
+        hip.check(L.tmh_correct_u16_device(corr, C.c_void_p(sites.data_ptr()),
+                                           C.c_void_p(out.data_ptr()), S, -1, -1, sp))
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    prof = not a.no_profile
+    if prof:
+        L.tmh_profile_enable(1)
+        L.tmh_profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel event timing on the launch stream (live roofline)
+    kern = {}
+    if prof:
+        for name in ("welford", "hist", "pct_acc", "finalize", "smooth", "coeffs", "correct"):
+            ms, k = C.c_double(), C.c_int64()
+            hip.check(L.tmh_profile_read(name.encode(), C.byref(ms), C.byref(k)))
+            if k.value:
+                kern[name] = (ms.value / k.value, k.value)
+        L.tmh_profile_enable(0)
+
+    if rank == 0:
+        site_bytes = npx * 2
+        alg = {  # algorithmic HBM bytes per launch (per-site figure x sites)
+            "welford": S * site_bytes + 4 * 8 * npx,       # sites + mean/M2 read & write
+            "hist": S * site_bytes,                        # sites
+            "correct": S * site_bytes * 2 + 16 * npx,      # sites in + out, coefficients
+            "pct_acc": S * Q * 4,                          # per-site order statistics
+        }
+        kdetail = {}
+        for name, (avg_ms, k) in kern.items():
+            d = {"avg_ms": round(avg_ms, 4), "launches": k}
+            if name in alg:
+                gbs = alg[name] / (avg_ms * 1e-3) / 1e9
+                d["alg_GBs"] = round(gbs, 1)
+                d["frac_of_8TBs"] = round(gbs / HBM_PEAK_GBS, 4)
+            kdetail[name] = d
+        dominant = max((n for n in kern if n in alg), key=lambda n: kern[n][0], default=None)
+        roofline = None
+        if dominant:
+            avg_ms = kern[dominant][0]
+            ach = alg[dominant] / (avg_ms * 1e-3) / 1e9
+            traffic = None
+            try:
+                with open(a.traffic_json) as f:
+                    tj = json.load(f)
+                cfg = tj.get("config", {})
+                if cfg.get("sites") == S and cfg.get("height") == H and cfg.get("width") == W:
+                    traffic = tj.get("kernels", {}).get(dominant, {}).get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                pass
+            roofline = {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                        "traffic": traffic, "alg_bytes_per_launch": alg[dominant]}
+        total_sites = world * S * a.steps
+        value = total_sites / elapsed
+        job_bytes = world * S * 6 * npx  # 6 B/px algorithmic per site-image
+        res = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "sites/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1e3 * elapsed / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (device counter-hash generator, SURVEY.md §8(d) distribution), "
+                    "resident in HBM",
+            "config": {"workload": "illumstats+correct, 1 channel, %d sites/GPU of %dx%d uint16 "
+                                   "(configs[1]: 384 wells x 9 sites)" % (S, H, W),
+                       "sites_per_gpu": S, "height": H, "width": W, "decimals": 3,
+                       "smoothing_sigma": 5, "clip": None,
+                       "parallelism": "sites sharded (contiguous); RCCL all-reduce Welford "
+                                      "merge + ordered percentile chain" if world > 1
+                                      else "single GPU"},
+            "job_hbm_roofline_frac": round(job_bytes * a.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world), 4),
+            "roofline": roofline,
+            "kernels": kdetail,
+        }
+        if world == 1 and a.cpu_sample > 0:
+            res["cpu_baseline"] = cpu_baseline(a.cpu_sample, H, W, S)
+        else:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+
+    L.tmh_corrector_destroy(corr)
+    L.tmh_stats_destroy(h)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,43 @@
+/*
+ * tmh5.h — C-ABI of libtmh5.so: the illumination path's HDF5 files, read and
+ * written through libhdf5 (1.10, /opt/conda) instead of h5py.
+ *
+ * Replaces, with the on-disk layout unchanged:
+ *   tmlib/models/file.py:440-456  IllumstatsFile.put  (DatasetWriter.write x4,
+ *                                 tmlib/writers.py:322-389)
+ *   tmlib/models/file.py:420-438  IllumstatsFile.get  (DatasetReader.read,
+ *                                 tmlib/readers.py:367-389)
+ *   tmlib/models/file.py:353-363  ChannelImageFile.put (gzip /array)
+ *   tmlib/models/file.py:322-351  ChannelImageFile.get
+ * Return 0 on success, negative errno-style code on failure
+ * (-2: dataset missing -> KeyError, -22: bad argument, -5: HDF5 error).
+ */
+#ifndef TMH5_H
+#define TMH5_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* tmh5_last_error(void);
+
+int tmh5_write_illumstats(const char* path, int height, int width, const double* mean,
+                          const double* std_, int64_t n_quantiles, const double* keys,
+                          const int64_t* values);
+int tmh5_illumstats_shape(const char* path, int* height, int* width, int64_t* n_quantiles);
+/* any output may be NULL (that dataset is skipped) */
+int tmh5_read_illumstats(const char* path, double* mean, double* std_, double* keys,
+                         int64_t* values);
+
+/* bits: 8 or 16; gzip_level < 0 writes an uncompressed contiguous dataset */
+int tmh5_write_channel_image(const char* path, int height, int width, int bits, const void* data,
+                             int gzip_level);
+int tmh5_channel_image_shape(const char* path, int* height, int* width, int* bits);
+int tmh5_read_channel_image(const char* path, void* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TMH5_H */

@@ -1,0 +1,181 @@
+/*
+ * tmhip.h — C-ABI of libtmhip.so, the MI355X (gfx950) implementation of
+ * TmLibrary's corilla illumination-statistics path and its apply step.
+ *
+ * The reference (scottberry/TmLibrary) is pure Python and has no FFI; these
+ * entry points are the boundary its Python classes would bind through
+ * ctypes.  Each function names the reference interface it replaces.
+ *
+ * Conventions
+ *   - Every int-returning function returns 0 on success and a negative
+ *     errno-style code on failure; tmh_last_error() holds a thread-local
+ *     message for the last failure on the calling thread.
+ *   - "host" pointers are plain CPU memory owned by the caller; "dev"
+ *     pointers are device (HBM) memory on the handle's device, owned by the
+ *     caller unless stated otherwise.
+ *   - stream arguments are hipStream_t passed as void*; NULL means the
+ *     handle's own stream.  Host-pointer calls are synchronous on return.
+ *   - A handle is not thread-safe; distinct handles may be used from
+ *     distinct threads.  No callbacks.
+ *   - Sites are contiguous [n_sites][height][width] uint16 images in site
+ *     order (the order of batch['channel_image_files_ids'],
+ *     tmlib/workflow/corilla/api.py:125-136).
+ */
+#ifndef TMHIP_H
+#define TMHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TMH_ABI_VERSION 1
+
+#define TMH_OK 0
+#define TMH_EINVAL (-22)  /* bad argument: maps to ValueError / TypeError */
+#define TMH_ENOMEM (-12)  /* device or host allocation failed             */
+#define TMH_EDEVICE (-5)  /* HIP runtime error                            */
+#define TMH_ESTATE (-71)  /* call not valid in the handle's state         */
+
+/* ---- library ---------------------------------------------------------- */
+int tmh_abi_version(void);
+const char* tmh_last_error(void);
+int tmh_device_count(int* n);
+int tmh_set_device(int device);
+int tmh_synchronize(void* stream);
+
+/* ---- illumination statistics ------------------------------------------
+ * Replaces tmlib/workflow/corilla/stats.py:35-121 (OnlineStatistics):
+ *   __init__(image_dimensions, decimals)  -> tmh_stats_create
+ *   update(image, log_transform)           -> tmh_stats_update[_device]
+ *   mean / std / var / percentiles         -> tmh_stats_finalize[_device]
+ *
+ * n_quantiles = 10**(decimals+2).  q_lo/q_hi/q_gamma are numpy 2.2.6's
+ * linear-percentile sorted positions and weights for an image of
+ * height*width pixels (previous/next index after the above/below-bound
+ * substitution, gamma = virtual - previous), computed on the host so they
+ * are bit-identical to np.percentile (stats.py:76).
+ * lut_log10[65536] is the stats log transform of every uint16 value
+ * (np.log10 with 0 -> 0, stats.py:79-85), built by the host's numpy.
+ * batch_capacity is the number of sites the handle stages per launch for
+ * host-pointer updates (device updates of any size are processed in
+ * place).  flags: TMH_STATS_DEFERRED_PCT keeps every site's order
+ * statistics on the device instead of folding them into the accumulator at
+ * each update (needed for the multi-GPU percentile chain).
+ */
+typedef struct tmh_stats tmh_stats;
+
+#define TMH_STATS_DEFERRED_PCT 1u
+
+int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo,
+                     const int64_t* q_hi, const double* q_gamma, const double* lut_log10,
+                     int batch_capacity, unsigned flags, tmh_stats** out);
+void tmh_stats_destroy(tmh_stats* h);
+int tmh_stats_set_stream(tmh_stats* h, void* stream);
+int tmh_stats_reset(tmh_stats* h);
+
+/* update(image) for a run of sites.  zero_counts_out (host, n_sites, may be
+ * NULL): per-site number of zero pixels, for the 'image contains zero
+ * values' warning (stats.py:81-82); non-NULL forces a synchronisation. */
+int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites,
+                     int log_transform, int64_t* zero_counts_out);
+int tmh_stats_update_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
+                            int log_transform, void* stream);
+
+/* Host copies of the results; any output may be NULL.
+ *   n            sites accumulated (stats.py:89)
+ *   mean, std    [height*width] f64; std is NaN where n < 2 (stats.py:94-112)
+ *   pct_sum      [n_quantiles] f64 running sum of per-site percentiles in
+ *                site order (stats.py:76); values = int(pct_sum / n)
+ *   hist         [65536] u64 pooled per-site histogram (sum over sites) */
+int tmh_stats_finalize(tmh_stats* h, int64_t* n, double* mean, double* std, double* pct_sum,
+                       uint64_t* hist);
+/* Device form: writes mean/std planes into caller device buffers. */
+int tmh_stats_finalize_device(tmh_stats* h, double* dev_mean, double* dev_std, void* stream);
+/* Per-site histogram of the most recent update batch (debug/parity). */
+int tmh_stats_site_histogram(tmh_stats* h, int64_t site_in_last_batch, uint32_t* host_hist);
+/* Order statistics at every quantile's previous/next sorted position for one
+ * site (last batch; any stored site in deferred mode) — debug/parity. */
+int tmh_stats_site_order_stats(tmh_stats* h, int64_t site, uint16_t* host_vlo,
+                               uint16_t* host_vhi);
+
+/* ---- multi-GPU merge (one process per GPU; collectives done by the caller
+ * over RCCL on the device buffers these functions fill/consume) --------- */
+int tmh_stats_get_n(tmh_stats* h, int64_t* n);
+/* dev_nmean = n_r * mean_r (input of all_reduce(sum)) */
+int tmh_stats_merge_stage1(tmh_stats* h, double* dev_nmean, void* stream);
+/* mean = dev_sum_nmean / n_total; dev_m2c = M2_r + n_r * (mean_r - mean)^2 */
+int tmh_stats_merge_stage2(tmh_stats* h, const double* dev_sum_nmean, int64_t n_total,
+                           double* dev_m2c, void* stream);
+/* Adopt the merged state: n = n_total, mean from stage 2, M2 = dev_sum_m2c. */
+int tmh_stats_merge_stage3(tmh_stats* h, int64_t n_total, const double* dev_sum_m2c,
+                           void* stream);
+/* Percentile chain: dev_acc[n_quantiles] += each local site's percentiles,
+ * in local site order (deferred mode).  Rank r runs this on the accumulator
+ * received from rank r-1, keeping the reference's sequential summation. */
+int tmh_stats_pct_accumulate(tmh_stats* h, double* dev_acc, void* stream);
+int tmh_stats_set_pct_sum(tmh_stats* h, const double* dev_acc, void* stream);
+
+/* ---- smoothing -----------------------------------------------------------
+ * Replaces tmlib/image.py:287-311 Image.smooth -> mahotas.gaussian_filter
+ * (image.py:303) as used by IllumstatsContainer.smooth (image.py:1172-1193):
+ * separable Gaussian, radius int(4*sigma+0.5), normalised taps, 'reflect'
+ * border, float64, axis 0 then axis 1.  in == out is allowed. */
+int tmh_smooth_f64(const double* host_in, double* host_out, int height, int width, double sigma);
+int tmh_smooth_f64_device(const double* dev_in, double* dev_out, double* dev_tmp, int height,
+                          int width, double sigma, void* stream);
+
+/* ---- correction ------------------------------------------------------------
+ * Replaces tmlib/image.py:599-631 ChannelImage._correct_illumination,
+ * image.py:633-670 correct, and image.py:570-597 clip.
+ * A corrector holds the per-pixel affine form of the correction for one
+ * (mean, std) pair:  log: out = 10**(a*log10(x) + b), a = mean(std)/std,
+ * b = mean(mean) - mean*a, x==0 -> log10(1e-10);  no log: out = a*x + b.
+ * lut_zero_log10 = np.log10(1e-10) from the host numpy.  The float result is
+ * cast with the x86 astype rule (trunc to int32, low bits) and optionally
+ * clipped to [clip_lo, clip_hi] (clip_lo < 0: no clip). */
+typedef struct tmh_corrector tmh_corrector;
+
+int tmh_corrector_create(const double* host_mean, const double* host_std, int height, int width,
+                         int log_transform, double zero_log10, tmh_corrector** out);
+int tmh_corrector_create_device(const double* dev_mean, const double* dev_std, int height,
+                                int width, int log_transform, double zero_log10, void* stream,
+                                tmh_corrector** out);
+void tmh_corrector_destroy(tmh_corrector* c);
+/* Recompute the coefficients in place from new device planes (no allocation,
+ * no synchronisation): one corrector serves every job of the same shape. */
+int tmh_corrector_update_device(tmh_corrector* c, const double* dev_mean, const double* dev_std,
+                                void* stream);
+/* The two global means (np.mean(std), np.mean(mean), image.py:627). */
+int tmh_corrector_means(tmh_corrector* c, double* mean_of_std, double* mean_of_mean);
+int tmh_correct_u16(tmh_corrector* c, const uint16_t* host_in, uint16_t* host_out,
+                    int64_t n_sites, int clip_lo, int clip_hi);
+int tmh_correct_u16_device(tmh_corrector* c, const uint16_t* dev_in, uint16_t* dev_out,
+                           int64_t n_sites, int clip_lo, int clip_hi, void* stream);
+int tmh_correct_u8(tmh_corrector* c, const uint8_t* host_in, uint8_t* host_out, int64_t n_sites,
+                   int clip_lo, int clip_hi);
+/* ChannelImage.clip alone (image.py:589), u16. */
+int tmh_clip_u16(const uint16_t* host_in, uint16_t* host_out, int64_t n, int lo, int hi);
+
+/* ---- synthetic input (imextract stand-in for benchmarks) ----------------- */
+int tmh_synth_sites_device(uint16_t* dev_out, int64_t n_sites, int height, int width,
+                           uint64_t seed, int channel, int64_t first_site, void* stream);
+
+/* ---- device memory helpers for callers without another allocator -------- */
+int tmh_malloc_device(void** dev_ptr, size_t bytes);
+int tmh_free_device(void* dev_ptr);
+int tmh_memcpy(void* dst, const void* src, size_t bytes, int kind /*0 h2d,1 d2h,2 d2d*/,
+               void* stream);
+
+/* ---- timing of the most recent launches (bench/roofline support) ---------
+ * Per-kernel event timing on the handle's stream, enabled by flag. */
+int tmh_profile_enable(int on);
+int tmh_profile_read(const char* kernel, double* total_ms, int64_t* launches);
+int tmh_profile_reset(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TMHIP_H */

@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE itself.
+
+Runs only in the build container, where /root/reference exists.  It imports
+the reference's hot-path modules (tmlib/utils.py, tmlib/metadata.py,
+tmlib/image.py, tmlib/workflow/corilla/stats.py) by file path, with the
+minimal shims SURVEY.md §8(c) lists (numpy-2 aliases, stub modules for the
+unrelated heavy imports, mahotas.gaussian_filter -> scipy), runs them on
+seeded inputs and writes inputs + outputs as .npz data files.  No reference
+source is copied; the fixtures are data only.  Bytecode writing is disabled
+so nothing is written under /root/reference.
+
+    python tests/golden/make_goldens.py            # (re)write all fixtures
+"""
+from __future__ import annotations
+
+import hashlib
+import importlib.util
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
+import scipy.ndimage as ndi  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+
+# ---------------------------------------------------------------------------
+# reference loader (shims per SURVEY.md §8(c))
+# ---------------------------------------------------------------------------
+
+def _stub(name, **attrs):
+    m = types.ModuleType(name)
+    for k, v in attrs.items():
+        setattr(m, k, v)
+    sys.modules[name] = m
+    return m
+
+
+def load_reference():
+    np.float = float  # removed in numpy 2 (stats.py:61, image.py:104/1132)
+    np.bool = bool
+    _stub("decorator", decorator=lambda f: f)
+    _stub("cv2")
+    sk = _stub("skimage")
+    for sub in ("measure", "color", "draw"):
+        setattr(sk, sub, _stub("skimage." + sub))
+    sh = _stub("shapely")
+    sh.geometry = _stub("shapely.geometry")
+    g2 = _stub("geoalchemy2")
+    g2.shape = _stub("geoalchemy2.shape", to_shape=None)
+
+    def gaussian_filter(array, sigma, order=0, mode="reflect", cval=0.0, out=None):
+        # mahotas 1.4.3 is absent: scipy stand-in (same radius int(4s+.5), reflect)
+        return ndi.gaussian_filter(np.asarray(array, dtype=np.float64), sigma,
+                                   order=order, mode=mode, cval=cval, truncate=4.0)
+
+    _stub("mahotas", gaussian_filter=gaussian_filter)
+    for pkg, path in (("tmlib", "tmlib"), ("tmlib.workflow", "tmlib/workflow"),
+                      ("tmlib.workflow.corilla", "tmlib/workflow/corilla")):
+        m = types.ModuleType(pkg)
+        m.__path__ = [os.path.join(REF, path)]
+        sys.modules[pkg] = m
+
+    def load(modname, rel):
+        spec = importlib.util.spec_from_file_location(modname, os.path.join(REF, rel))
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[modname] = mod
+        spec.loader.exec_module(mod)
+        return mod
+
+    utils = load("tmlib.utils", "tmlib/utils.py")
+    utils.assert_type = lambda **kw: (lambda f: f)  # body uses py2 iteritems
+    metadata = load("tmlib.metadata", "tmlib/metadata.py")
+    image = load("tmlib.image", "tmlib/image.py")
+    stats = load("tmlib.workflow.corilla.stats", "tmlib/workflow/corilla/stats.py")
+    return metadata, image, stats
+
+
+# ---------------------------------------------------------------------------
+# inputs
+# ---------------------------------------------------------------------------
+
+def synth(n, h, w, seed, dtype=np.uint16):
+    from tmlibrary_amd.synth import synth_sites_host
+    return synth_sites_host(n, h, w, seed=seed, dtype=dtype)
+
+
+def extremes(n, h, w, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        a = rng.integers(0, 65536, size=(h, w), dtype=np.uint16)
+        a[rng.random((h, w)) < 0.05] = 0
+        a[rng.random((h, w)) < 0.05] = 1
+        a[rng.random((h, w)) < 0.05] = 65535
+        out.append(a)
+    out.append(np.full((h, w), 7, dtype=np.uint16))  # constant site
+    return out
+
+
+def run_stats(stats_mod, image_mod, sites, log_transform=True, decimals=3):
+    st = stats_mod.OnlineStatistics(sites[0].shape, decimals=decimals)
+    for s in sites:
+        st.update(image_mod.ChannelImage(s), log_transform=log_transform)
+    pct = st.percentiles
+    keys = np.array(sorted(pct.keys()), dtype=np.float64)
+    vals = np.array([pct[k] for k in keys], dtype=np.int64)
+    return dict(n=np.int64(st.n), mean=st.mean.array, std=st.std.array,
+                pct_sums=np.asarray(st._percentiles, dtype=np.float64),
+                pct_keys=keys, pct_values=vals)
+
+
+def run_apply(metadata_mod, image_mod, mean, std, img, log_transform=True):
+    md = metadata_mod.IllumstatsImageMetadata(channel_id=1)
+    cont = image_mod.IllumstatsContainer(image_mod.IllumstatsImage(mean.copy(), md),
+                                         image_mod.IllumstatsImage(std.copy(), md), {})
+    cont.smooth()
+    sm_mean, sm_std = cont.mean.array, cont.std.array
+    corr = image_mod.ChannelImage._correct_illumination(img, sm_mean, sm_std,
+                                                        log_transform=log_transform)
+    return sm_mean, sm_std, corr
+
+
+def digest(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def main():
+    metadata, image, stats = load_reference()
+    from oracle import corilla_oracle as orc
+
+    index = {}
+
+    def save(name, **arrays):
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **arrays)
+        index[name] = sorted(arrays.keys())
+        print("wrote", path, os.path.getsize(path), "bytes")
+
+    # --- stats cases ------------------------------------------------------
+    cases = {
+        "stats_small": dict(sites=synth(5, 64, 80, seed=101)),
+        "stats_medium": dict(sites=synth(4, 192, 256, seed=202)),
+        "stats_extremes": dict(sites=extremes(3, 48, 40, seed=303)),
+        "stats_single": dict(sites=synth(1, 40, 56, seed=404)),
+        "stats_odd": dict(sites=synth(4, 37, 53, seed=505)),
+        "stats_nolog": dict(sites=synth(4, 64, 80, seed=606), log=False),
+        "stats_dec1": dict(sites=synth(3, 64, 80, seed=707), decimals=1),
+        "stats_dec0": dict(sites=synth(3, 32, 48, seed=808), decimals=0),
+        "stats_u8": dict(sites=synth(4, 64, 80, seed=909, dtype=np.uint8)),
+    }
+    for name, c in cases.items():
+        sites = c["sites"]
+        log = c.get("log", True)
+        dec = c.get("decimals", 3)
+        ref = run_stats(stats, image, sites, log_transform=log, decimals=dec)
+        # cross-check the oracle restatement now (bit-exact expected)
+        o = orc.run_illumstats(sites, log_transform=log, decimals=dec)
+        assert o.n == ref["n"]
+        assert np.array_equal(o.mean, ref["mean"], equal_nan=True), name
+        assert np.array_equal(o.std, ref["std"], equal_nan=True), name
+        assert np.array_equal(o.percentile_sums, ref["pct_sums"]), name
+        ov = orc.percentile_values(o.percentile_sums, o.n)
+        assert np.array_equal(ov, ref["pct_values"]), name
+        if name not in ("stats_small", "stats_dec1", "stats_dec0"):
+            ref.pop("pct_keys")  # identical for every decimals=3 case: pinned once
+        save(name, sites=np.stack(sites), log_transform=np.bool_(log),
+             decimals=np.int64(dec), **ref)
+
+    # --- apply cases (smooth -> correct), incl. clip + closest percentile --
+    base = synth(6, 96, 128, seed=1111)
+    ref = run_stats(stats, image, base)
+    test_imgs = synth(3, 96, 128, seed=2222)
+    test_imgs[0][0, :8] = 0  # zeros take the 1e-10 branch
+    test_imgs[1][1, :8] = 65535
+    for log in (True, False):
+        sm_mean, sm_std, _ = run_apply(metadata, image, ref["mean"], ref["std"], test_imgs[0], log)
+        corr = np.stack([run_apply(metadata, image, ref["mean"], ref["std"], t, log)[2]
+                         for t in test_imgs])
+        pct = dict(zip(ref["pct_keys"].tolist(), ref["pct_values"].tolist()))
+        lo = orc.get_closest_percentile(pct, 0.001)
+        hi = max(orc.get_closest_percentile(pct, 99.9), 700)
+        cmd = metadata.ChannelImageMetadata(channel_id=1, site_id=1, cycle_id=1, tpoint=0, zplane=0)
+        clipped = np.stack([image.ChannelImage(c.copy(), cmd).clip(lo, hi).array for c in corr])
+        o_corr = np.stack([orc.correct_illumination(t, sm_mean, sm_std, log) for t in test_imgs])
+        assert np.array_equal(o_corr, corr), "oracle correct != reference"
+        o_sm = orc.smooth_reflect(ref["mean"])
+        assert np.allclose(o_sm, sm_mean, rtol=1e-12, atol=1e-14)
+        save("apply_log" if log else "apply_nolog",
+             stats_mean=ref["mean"], stats_std=ref["std"],
+             smooth_mean=sm_mean, smooth_std=sm_std, images=np.stack(test_imgs),
+             corrected=corr, clip_lo=np.int64(lo), clip_hi=np.int64(hi), clipped=clipped)
+
+    # uint8 correct
+    u8 = synth(3, 64, 80, seed=3333, dtype=np.uint8)
+    r8 = run_stats(stats, image, u8)
+    sm_mean, sm_std, c8 = run_apply(metadata, image, r8["mean"], r8["std"], u8[0])
+    save("apply_u8", stats_mean=r8["mean"], stats_std=r8["std"], smooth_mean=sm_mean,
+         smooth_std=sm_std, images=u8[0][None], corrected=c8[None])
+
+    # float -> uint cast rule (image.py:631 astype) on special values
+    specials = np.array([0.0, 0.4, 0.99, 1.0, 65535.0, 65535.9, 65536.0, 70000.0, -0.5, -1.0,
+                         -1.5, 2.0 ** 31 - 1, 2.0 ** 31, 2.0 ** 40, -(2.0 ** 31), -(2.0 ** 31) - 1,
+                         np.inf, -np.inf, np.nan, 1e300, 255.5, 256.0, 300.0], dtype=np.float64)
+    save("cast_rule", values=specials, as_u16=specials.astype(np.uint16),
+         as_u8=specials.astype(np.uint8))
+
+    # --- full-size sites (2160 x 2560): seeds + digests + samples ---------
+    H, W = 2160, 2560
+    full = synth(2, H, W, seed=4242)
+    rf = run_stats(stats, image, full)
+    sm_mean, sm_std, corr0 = run_apply(metadata, image, rf["mean"], rf["std"], full[0])
+    rng = np.random.default_rng(7)
+    iy = rng.integers(0, H, 2048)
+    ix = rng.integers(0, W, 2048)
+    save("fullsize_2site", seed=np.int64(4242), n_sites=np.int64(2), height=np.int64(H),
+         width=np.int64(W), input_digest=np.array([digest(s) for s in full]),
+         sample_y=iy, sample_x=ix, mean_samples=rf["mean"][iy, ix], std_samples=rf["std"][iy, ix],
+         pct_sums=rf["pct_sums"], pct_values=rf["pct_values"], n=rf["n"],
+         mean_digest=np.array(digest(rf["mean"])), std_digest=np.array(digest(rf["std"])),
+         smooth_mean_samples=sm_mean[iy, ix], smooth_std_samples=sm_std[iy, ix],
+         corrected_digest=np.array(digest(corr0)), corrected_samples=corr0[iy, ix],
+         corrected_hist=np.bincount(corr0.ravel(), minlength=65536).astype(np.int64))
+
+    meta = dict(numpy=np.__version__, generator="tests/golden/make_goldens.py",
+                reference="/root/reference (scottberry/TmLibrary, imported with shims)",
+                fixtures=index)
+    with open(os.path.join(HERE, "INDEX.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("done")
+
+
+if __name__ == "__main__":
+    main()

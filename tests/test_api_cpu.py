@@ -1,0 +1,63 @@
+"""CPU: host-side behaviour of the drop-in API (types, errors, metadata flags)."""
+import numpy as np
+import pytest
+
+from util import load_golden
+from tmlibrary_amd.image import ChannelImage, IllumstatsContainer, IllumstatsImage
+from tmlibrary_amd.metadata import ChannelImageMetadata, IllumstatsImageMetadata
+
+
+def test_channel_image_type_checks():
+    ChannelImage(np.zeros((4, 5), np.uint16))
+    ChannelImage(np.zeros((4, 5), np.uint8))
+    with pytest.raises(TypeError):
+        ChannelImage([[1, 2]])
+    with pytest.raises(ValueError):
+        ChannelImage(np.zeros(5, np.uint16))
+    with pytest.raises(ValueError):
+        ChannelImage(np.zeros((4, 5), np.float64))
+    with pytest.raises(ValueError):
+        ChannelImage(np.zeros((4, 5), np.uint32))
+    with pytest.raises(TypeError):
+        ChannelImage(np.zeros((4, 5), np.uint16), metadata=object())
+
+
+def test_illumstats_image_type_checks():
+    IllumstatsImage(np.zeros((3, 3)))
+    with pytest.raises(ValueError):
+        IllumstatsImage(np.zeros((3, 3), np.float32))
+    with pytest.raises(TypeError):
+        IllumstatsImage(np.zeros((3, 3)), metadata=ChannelImageMetadata(1, 1, 1, 0, 0))
+    with pytest.raises(TypeError):
+        IllumstatsContainer(np.zeros((3, 3)), IllumstatsImage(np.zeros((3, 3))), {})
+
+
+def test_metadata_flags_and_types():
+    md = ChannelImageMetadata(channel_id=3, site_id=1, cycle_id=0, tpoint=0, zplane=0)
+    assert md.is_corrected is False and md.is_clipped is False and md.is_rescaled is False
+    with pytest.raises(TypeError):
+        md.channel_id = "3"
+    with pytest.raises(TypeError):
+        md.is_corrected = 1
+    im = IllumstatsImageMetadata(channel_id=3)
+    assert im.is_smoothed is False
+    with pytest.raises(TypeError):
+        im.is_smoothed = "yes"
+
+
+def test_get_closest_percentile_matches_golden():
+    g = load_golden("stats_small")
+    pct = dict(zip(g["pct_keys"].tolist(), g["pct_values"].tolist()))
+    c = IllumstatsContainer(IllumstatsImage(np.zeros((2, 2))), IllumstatsImage(np.ones((2, 2))), pct)
+    assert c.get_closest_percentile(99.9) == pct[99.9]
+    assert c.get_closest_percentile(0.001) == pct[0.001]
+    assert c.get_closest_percentile(-5) == pct[0.0]
+    assert c.get_closest_percentile(500) == pct[100.0]
+
+
+def test_stats_rejects_bad_decimals():
+    from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
+    with pytest.raises(ValueError):
+        OnlineStatistics((4, 4), decimals=4)
+    with pytest.raises(ValueError):
+        OnlineStatistics((4, 4), decimals=-1)

@@ -1,0 +1,118 @@
+"""CPU, world_size 2 (gloo): the multi-GPU merge sequencing of
+tmlibrary_amd/workflow/corilla/sharded.py reproduces the single-process
+statistics — Welford merge within 1e-6, percentile chain bit-exact.
+
+The device kernels are replaced by a host-memory test double with the same
+stage arithmetic; the GPU kernels themselves are covered by
+test_gpu_parity.py::test_deferred_chain_and_merge_single_gpu."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from util import REPO, load_golden
+
+
+class HostOps(object):
+    """Test double of sharded.StatsOps on numpy/torch CPU state."""
+
+    def __init__(self, n, mean, m2, site_pcts):
+        self.n = int(n)
+        self.mean = torch.tensor(np.asarray(mean, dtype=np.float64).ravel())
+        self.m2 = torch.tensor(np.asarray(m2, dtype=np.float64).ravel())
+        self.site_pcts = [np.asarray(p, dtype=np.float64) for p in site_pcts]
+        self.Q = self.site_pcts[0].size
+        self.acc = None
+        self.device = "cpu"
+
+    def n_local(self):
+        return self.n
+
+    def empty_plane(self):
+        return torch.empty(self.mean.numel(), dtype=torch.float64)
+
+    def empty_acc(self):
+        return torch.zeros(self.Q, dtype=torch.float64)
+
+    def stage1(self, buf):
+        buf.copy_(self.n * self.mean)
+
+    def stage2(self, sum_nmean, n_total, m2c):
+        mu = sum_nmean / n_total
+        d = self.mean - mu
+        m2c.copy_(self.m2 + self.n * d * d)
+        self.mean = mu.clone()
+
+    def stage3(self, n_total, sum_m2c):
+        self.m2 = sum_m2c.clone()
+        self.n = n_total
+
+    def pct_accumulate(self, acc):
+        a = acc.numpy().copy()
+        for p in self.site_pcts:
+            a += p  # in site order
+        acc.copy_(torch.from_numpy(a))
+
+    def set_pct_sum(self, acc):
+        self.acc = acc.clone()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, name, out_dir):
+    import sys
+    sys.path.insert(0, REPO)
+    from oracle import corilla_oracle as orc
+    from tmlibrary_amd.workflow.corilla.sharded import merge_shards, shard_bounds
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = load_golden(name)
+    sites = list(g["sites"])
+    a, b = shard_bounds(len(sites), world, rank)
+    mine = sites[a:b]
+    q = np.linspace(0, 100, 10 ** (int(g["decimals"]) + 2))
+    st = orc.OracleOnlineStatistics(sites[0].shape, int(g["decimals"]))
+    for s in mine:
+        st.update(s)
+    ops = HostOps(st.n, st.mean, st._M2, [orc.percentile_linear(s, q) for s in mine])
+    n_total = merge_shards(ops, dist)
+    np.savez(os.path.join(out_dir, "r%d.npz" % rank), n=n_total, mean=ops.mean.numpy(),
+             m2=ops.m2.numpy(), acc=ops.acc.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,name", [(2, "stats_medium"), (2, "stats_small"),
+                                        (3, "stats_small")])
+def test_merge_shards_gloo(tmp_path, world, name):
+    port = _free_port()
+    mp.start_processes(_worker, args=(world, port, name, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    g = load_golden(name)
+    want_var = g["std"] ** 2
+    for r in range(world):
+        z = np.load(tmp_path / ("r%d.npz" % r))
+        assert int(z["n"]) == int(g["n"])
+        assert np.allclose(z["mean"].reshape(g["mean"].shape), g["mean"], rtol=1e-6, atol=1e-12)
+        var = z["m2"].reshape(g["mean"].shape) / (int(z["n"]) - 1)
+        assert np.allclose(var, want_var, rtol=1e-6, atol=1e-12)
+        assert np.array_equal(z["acc"], g["pct_sums"]), "chained percentile sum not bit-exact"
+
+
+def test_shard_bounds_cover_in_order():
+    from tmlibrary_amd.workflow.corilla.sharded import shard_bounds
+    for n in (0, 1, 7, 3456, 13824):
+        for w in (1, 2, 3, 8):
+            spans = [shard_bounds(n, w, r) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))

@@ -1,0 +1,383 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the oracle and the golden
+fixtures.  Bars (BASELINE.json north_star): mean/std 1e-6 relative,
+percentiles and histograms bit-exact, corrected uint16 within +-1 DN."""
+import ctypes as C
+import hashlib
+
+import numpy as np
+import pytest
+
+from util import assert_close_rel, dn_diff, load_golden
+from oracle import corilla_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+STATS_CASES = ["stats_small", "stats_medium", "stats_extremes", "stats_single", "stats_odd",
+               "stats_nolog", "stats_dec1", "stats_dec0", "stats_u8"]
+
+
+@pytest.fixture(scope="module")
+def L():
+    from tmlibrary_amd import hip
+    return hip.lib()
+
+
+class Dev:
+    """Raw device buffer via the C-ABI helpers (no torch needed)."""
+
+    def __init__(self, L, nbytes):
+        self.L = L
+        self.p = C.c_void_p()
+        assert L.tmh_malloc_device(C.byref(self.p), max(int(nbytes), 1)) == 0
+        self.nbytes = nbytes
+
+    def put(self, a):
+        a = np.ascontiguousarray(a)
+        assert self.L.tmh_memcpy(self.p, a.ctypes.data, a.nbytes, 0, None) == 0
+
+    def get(self, dtype, shape):
+        out = np.empty(shape, dtype)
+        assert self.L.tmh_memcpy(out.ctypes.data, self.p, out.nbytes, 1, None) == 0
+        return out
+
+    def free(self):
+        self.L.tmh_free_device(self.p)
+
+
+def run_stats(sites, log=True, decimals=3, batch=3, flags=0):
+    from tmlibrary_amd.image import ChannelImage
+    from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
+    st = OnlineStatistics(sites[0].shape, decimals=decimals, batch_size=batch, flags=flags)
+    for s in sites:
+        st.update(ChannelImage(np.ascontiguousarray(s)), log_transform=log)
+    return st
+
+
+@pytest.mark.parametrize("name", STATS_CASES)
+@pytest.mark.parametrize("batch", [1, 3, 64])
+def test_stats_vs_golden(L, name, batch):
+    g = load_golden(name)
+    st = run_stats(list(g["sites"]), bool(g["log_transform"]), int(g["decimals"]), batch)
+    assert st.n == int(g["n"])
+    assert_close_rel(st.mean.array, g["mean"])
+    assert_close_rel(st.std.array, g["std"])
+    assert np.array_equal(st.percentile_sums, g["pct_sums"]), "percentile sums not bit-exact"
+    pct = st.percentiles
+    vals = np.array([pct[k] for k in sorted(pct)], dtype=np.int64)
+    assert np.array_equal(vals, g["pct_values"])
+    if "pct_keys" in g:
+        assert np.array_equal(np.array(sorted(pct), dtype=np.float64), g["pct_keys"])
+    pooled = sum(orc.histogram_u16(s) for s in g["sites"])
+    assert np.array_equal(st.histogram, pooled), "pooled histogram not bit-exact"
+
+
+def test_site_histograms_bit_exact(L):
+    from tmlibrary_amd import hip
+    g = load_golden("stats_extremes")
+    sites = list(g["sites"])
+    st = run_stats(sites, batch=64, flags=hip.TMH_STATS_KEEP_SITE_HIST)
+    st._finalize()
+    for i, s in enumerate(sites):
+        h = np.empty(65536, np.uint32)
+        hip.check(L.tmh_stats_site_histogram(st._h, i, hip.ptr(h)))
+        assert np.array_equal(h.astype(np.uint64), orc.histogram_u16(s))
+
+
+@pytest.mark.parametrize("kind", ["constant_low", "constant_high", "uniform", "two_values",
+                                  "all_max", "sparse_hi"])
+def test_histogram_stress(L, kind):
+    """Worst cases for the LDS/global histogram split: every pixel in one bin
+    (below and above the LDS range), uniform over all 65,536 values."""
+    rng = np.random.default_rng(11)
+    h, w = 512, 640
+    if kind == "constant_low":
+        sites = [np.full((h, w), 123, np.uint16) for _ in range(3)]
+    elif kind == "constant_high":
+        sites = [np.full((h, w), 50000, np.uint16) for _ in range(3)]
+    elif kind == "uniform":
+        sites = [rng.integers(0, 65536, (h, w), dtype=np.uint16) for _ in range(3)]
+    elif kind == "two_values":
+        sites = [np.where(rng.random((h, w)) < 0.5, 1, 65534).astype(np.uint16) for _ in range(3)]
+    elif kind == "all_max":
+        sites = [np.full((h, w), 65535, np.uint16) for _ in range(2)]
+    else:
+        base = rng.integers(90, 4000, (h, w), dtype=np.uint16)
+        base[rng.random((h, w)) < 1e-3] = 65535
+        base[rng.random((h, w)) < 1e-3] = 40000
+        sites = [base, base[::-1].copy(), base[:, ::-1].copy()]
+    st = run_stats(sites, batch=2)
+    ref = orc.run_illumstats(sites)
+    assert np.array_equal(st.percentile_sums, ref.percentile_sums)
+    assert np.array_equal(st.histogram, sum(orc.histogram_u16(s) for s in sites))
+    assert_close_rel(st.mean.array, ref.mean)
+    assert_close_rel(st.std.array, ref.std)
+
+
+def test_repeatable_bitwise(L):
+    sites = list(load_golden("stats_medium")["sites"])
+    a = run_stats(sites, batch=2)
+    b = run_stats(sites, batch=4)
+    assert np.array_equal(a.percentile_sums, b.percentile_sums)
+    assert np.array_equal(a.histogram, b.histogram)
+    assert np.array_equal(a.std.array, b.std.array)
+
+
+def test_log_transform_switch_and_zero_warning(L, caplog):
+    sites = list(load_golden("stats_small")["sites"])
+    from tmlibrary_amd.image import ChannelImage
+    from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
+    st = OnlineStatistics(sites[0].shape, batch_size=4)
+    ref = orc.OracleOnlineStatistics(sites[0].shape)
+    logs = [True, False, True, True, False]
+    with caplog.at_level("WARNING"):
+        for s, lg in zip(sites, logs):
+            st.update(ChannelImage(s), log_transform=lg)
+            ref.update(s, log_transform=lg)
+        _ = st.mean
+    assert_close_rel(st.mean.array, ref.mean)
+    assert_close_rel(st.std.array, ref.std)
+    assert np.array_equal(st.percentile_sums, ref.percentile_sums)
+    n_warn = sum("image contains zero values" in r.message for r in caplog.records)
+    assert n_warn == ref.zero_sites
+
+
+def test_empty_stats_behaviour(L):
+    from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
+    st = OnlineStatistics((8, 8))
+    assert st.n == 0
+    assert np.all(np.isnan(st.var)) and np.all(np.isnan(st.std.array))
+    assert np.array_equal(st.mean.array, np.zeros((8, 8)))
+    with pytest.raises(ZeroDivisionError):
+        st.percentiles
+    from tmlibrary_amd.image import ChannelImage
+    with pytest.raises(ValueError):
+        st.update(ChannelImage(np.zeros((8, 9), np.uint16)))
+    with pytest.raises(TypeError):
+        st.update(np.zeros((8, 8), np.uint16))
+
+
+@pytest.mark.parametrize("name", ["apply_log", "apply_nolog"])
+def test_smooth_and_correct_vs_golden(L, name):
+    from tmlibrary_amd.image import (ChannelImage, IllumstatsContainer, IllumstatsImage,
+                                     smooth_f64)
+    from tmlibrary_amd.metadata import ChannelImageMetadata, IllumstatsImageMetadata
+    g = load_golden(name)
+    log = name == "apply_log"
+    # smoothing (pinned vs scipy reflect; mahotas itself is unavailable)
+    assert np.allclose(smooth_f64(g["stats_mean"], 5), g["smooth_mean"], rtol=1e-10, atol=1e-13)
+    assert np.allclose(smooth_f64(g["stats_std"], 5), g["smooth_std"], rtol=1e-10, atol=1e-13)
+    md = IllumstatsImageMetadata(channel_id=7)
+    cont = IllumstatsContainer(IllumstatsImage(g["stats_mean"].copy(), md),
+                               IllumstatsImage(g["stats_std"].copy(), md), {})
+    cont.smooth()
+    assert cont.mean.metadata.is_smoothed and cont.std.metadata.is_smoothed
+    for img, want, want_clip in zip(g["images"], g["corrected"], g["clipped"]):
+        got = ChannelImage._correct_illumination(img, g["smooth_mean"], g["smooth_std"], log)
+        assert dn_diff(got, want).max() <= 1
+        assert np.mean(got == want) > 0.999
+        if log:
+            ci = ChannelImage(img.copy(), ChannelImageMetadata(7, 1, 1, 0, 0))
+            ci.correct(cont)
+            assert ci.metadata.is_corrected
+            assert dn_diff(ci.array, want).max() <= 1
+            ci.clip(int(g["clip_lo"]), int(g["clip_hi"]))
+            assert ci.metadata.is_clipped
+            assert dn_diff(ci.array, want_clip).max() <= 1
+        clipped = ChannelImage(want.copy(), ChannelImageMetadata(7, 1, 1, 0, 0)).clip(
+            int(g["clip_lo"]), int(g["clip_hi"]))
+        assert np.array_equal(clipped.array, want_clip)
+
+
+def test_correct_channel_mismatch(L):
+    from tmlibrary_amd.image import ChannelImage, IllumstatsContainer, IllumstatsImage
+    from tmlibrary_amd.metadata import ChannelImageMetadata, IllumstatsImageMetadata
+    md = IllumstatsImageMetadata(channel_id=1)
+    cont = IllumstatsContainer(IllumstatsImage(np.ones((4, 4)), md),
+                               IllumstatsImage(np.ones((4, 4)), md), {})
+    ci = ChannelImage(np.ones((4, 4), np.uint16), ChannelImageMetadata(2, 1, 1, 0, 0))
+    with pytest.raises(ValueError):
+        ci.correct(cont)
+    with pytest.raises(TypeError):
+        ci.correct("stats")
+
+
+def test_correct_u8(L):
+    from tmlibrary_amd.image import ChannelImage
+    g = load_golden("apply_u8")
+    got = ChannelImage._correct_illumination(g["images"][0], g["smooth_mean"], g["smooth_std"])
+    assert got.dtype == np.uint8
+    assert dn_diff(got, g["corrected"][0], bits=8).max() <= 1
+
+
+def test_correct_special_stats(L):
+    """std = 0 / NaN (n < 2) and extreme outputs follow the x86 cast rule."""
+    from tmlibrary_amd.image import ChannelImage
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 65536, (64, 80), dtype=np.uint16)
+    img[0, :4] = [0, 1, 65535, 2]
+    mean = rng.random((64, 80)) * 3
+    std = rng.random((64, 80)) * 0.5 + 0.01
+    std[5, :] = 0.0
+    std[6, :] = np.nan
+    for log in (True, False):
+        got = ChannelImage._correct_illumination(img, mean, std, log)
+        want = orc.correct_illumination(img, mean, std, log)
+        d = dn_diff(got, want)
+        assert d.max() <= 1, (log, int(d.max()))
+
+
+def test_fullsize_two_sites(L):
+    """2160x2560: samples/digests of the reference outputs (fixture)."""
+    from tmlibrary_amd.image import ChannelImage, Corrector, smooth_f64
+    from tmlibrary_amd.synth import synth_sites_host
+    g = load_golden("fullsize_2site")
+    H, W = int(g["height"]), int(g["width"])
+    sites = synth_sites_host(int(g["n_sites"]), H, W, seed=int(g["seed"]))
+    st = run_stats(sites, batch=2)
+    iy, ix = g["sample_y"], g["sample_x"]
+    assert_close_rel(st.mean.array[iy, ix], g["mean_samples"])
+    assert_close_rel(st.std.array[iy, ix], g["std_samples"])
+    assert np.array_equal(st.percentile_sums, g["pct_sums"])
+    pct = st.percentiles
+    assert np.array_equal(np.array([pct[k] for k in sorted(pct)]), g["pct_values"])
+    sm, ss = smooth_f64(st.mean.array, 5), smooth_f64(st.std.array, 5)
+    assert np.allclose(sm[iy, ix], g["smooth_mean_samples"], rtol=1e-9, atol=1e-12)
+    corr = Corrector(sm, ss).apply(sites[0])
+    assert dn_diff(corr[iy, ix], g["corrected_samples"]).max() <= 1
+    h = np.bincount(corr.ravel(), minlength=65536)
+    # +-1 DN: the corrected histogram moves by at most the pixels that flip a bin
+    assert np.abs(h - g["corrected_hist"]).sum() <= 0.002 * corr.size
+    exact = hashlib.sha256(corr.tobytes()).hexdigest() == str(g["corrected_digest"])
+    print("fullsize corrected bit-identical to reference:", exact)
+
+
+def test_device_path_large_batch(L):
+    """Sites generated in HBM, one update_device call, vs the oracle on a copy."""
+    from tmlibrary_amd import hip
+    from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
+    H, W, n = 540, 640, 40
+    npx = H * W
+    d = Dev(L, n * npx * 2)
+    hip.check(L.tmh_synth_sites_device(d.p, n, H, W, 99, 0, 0, None))
+    L.tmh_synchronize(None)
+    sites = d.get(np.uint16, (n, H, W))
+    q = np.linspace(0, 100, 100000)
+    lo, hi, gamma = quantile_table(npx, q)
+    lut = stats_log10_lut()
+    h = C.c_void_p()
+    hip.check(L.tmh_stats_create(H, W, 100000, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
+                                 hip.ptr(lut), 8, 0, C.byref(h)))
+    hip.check(L.tmh_stats_update_device(h, d.p, n, 1, None))
+    mean = np.empty((H, W))
+    std = np.empty((H, W))
+    acc = np.empty(100000)
+    nn = C.c_int64()
+    hip.check(L.tmh_stats_finalize(h, C.byref(nn), hip.ptr(mean), hip.ptr(std), hip.ptr(acc), None))
+    ref = orc.run_illumstats(list(sites))
+    assert nn.value == n
+    assert_close_rel(mean, ref.mean)
+    assert_close_rel(std, ref.std)
+    assert np.array_equal(acc, ref.percentile_sums)
+    L.tmh_stats_destroy(h)
+    d.free()
+
+
+def test_deferred_chain_and_merge_single_gpu(L):
+    """Two handles = two 'ranks' on one GPU: Chan merge + ordered percentile
+    chain reproduce the single-handle result (mean/std 1e-6, pct bit-exact)."""
+    from tmlibrary_amd import hip
+    from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
+    sites = np.stack(load_golden("stats_medium")["sites"])
+    n, H, W = sites.shape
+    npx = H * W
+    q = np.linspace(0, 100, 100000)
+    lo, hi, gamma = quantile_table(npx, q)
+    lut = stats_log10_lut()
+
+    def mk(flags):
+        h = C.c_void_p()
+        hip.check(L.tmh_stats_create(H, W, 100000, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
+                                     hip.ptr(lut), 4, flags, C.byref(h)))
+        return h
+
+    parts = [sites[:1], sites[1:]]
+    hs = [mk(hip.TMH_STATS_DEFERRED_PCT) for _ in parts]
+    for h, p in zip(hs, parts):
+        hip.check(L.tmh_stats_update(h, hip.ptr(np.ascontiguousarray(p)), len(p), 1, None))
+    # all-reduce emulated by host sums of the device buffers
+    bufs = [Dev(L, npx * 8) for _ in hs]
+    for h, b in zip(hs, bufs):
+        hip.check(L.tmh_stats_merge_stage1(h, b.p, None))
+    L.tmh_synchronize(None)
+    s1 = sum(b.get(np.float64, npx) for b in bufs)
+    sum_dev = Dev(L, npx * 8)
+    sum_dev.put(s1)
+    for h, b in zip(hs, bufs):
+        hip.check(L.tmh_stats_merge_stage2(h, sum_dev.p, n, b.p, None))
+    L.tmh_synchronize(None)
+    s2 = sum(b.get(np.float64, npx) for b in bufs)
+    sum_dev.put(s2)
+    for h in hs:
+        hip.check(L.tmh_stats_merge_stage3(h, n, sum_dev.p, None))
+    acc = Dev(L, 100000 * 8)
+    acc.put(np.zeros(100000))
+    for h in hs:  # rank order
+        hip.check(L.tmh_stats_pct_accumulate(h, acc.p, None))
+    for h in hs:
+        hip.check(L.tmh_stats_set_pct_sum(h, acc.p, None))
+    L.tmh_synchronize(None)
+    ref = orc.run_illumstats(list(sites))
+    for h in hs:
+        mean = np.empty((H, W))
+        std = np.empty((H, W))
+        pct = np.empty(100000)
+        nn = C.c_int64()
+        hip.check(L.tmh_stats_finalize(h, C.byref(nn), hip.ptr(mean), hip.ptr(std), hip.ptr(pct),
+                                       None))
+        assert nn.value == n
+        assert_close_rel(mean, ref.mean)
+        assert_close_rel(std, ref.std)
+        assert np.array_equal(pct, ref.percentile_sums)
+        L.tmh_stats_destroy(h)
+    for b in bufs + [sum_dev, acc]:
+        b.free()
+
+
+def test_profile_counters(L):
+    from tmlibrary_amd import hip
+    L.tmh_profile_enable(1)
+    L.tmh_profile_reset()
+    run_stats(list(load_golden("stats_small")["sites"]), batch=8)._finalize()
+    ms, k = C.c_double(), C.c_int64()
+    hip.check(L.tmh_profile_read(b"welford", C.byref(ms), C.byref(k)))
+    assert k.value >= 1 and ms.value > 0
+    L.tmh_profile_enable(0)
+
+
+def test_run_job_end_to_end(L, tmp_path):
+    """IllumstatsCalculator.run_job: gzip HDF5 sites in batch order -> GPU stats
+    -> IllumstatsFile (4 datasets) -> IllumstatsFile.get (smoothed)."""
+    pytest.importorskip("tmlibrary_amd.models.file")
+    from tmlibrary_amd.models import file as h5
+    try:
+        h5.h5lib()
+    except RuntimeError as e:
+        pytest.skip(str(e))
+    from tmlibrary_amd.workflow.corilla.api import IllumstatsCalculator
+    g = load_golden("stats_medium")
+    sites = list(g["sites"])
+    store = h5.ExperimentStore(str(tmp_path), {100 + i: (5, i, 0, 0, 0) for i in range(len(sites))})
+    (tmp_path / "channel_image_files").mkdir()
+    for i, s in enumerate(sites):
+        h5.write_channel_image(store.channel_image_file(100 + i).location, s)
+    batch = {"id": 1, "channel_image_files_ids": [[100 + i] for i in range(len(sites))],
+             "channel_id": 5}
+    IllumstatsCalculator(1, store=store, batch_size=2).run_job(batch)
+    mean, std, keys, vals = h5.read_illumstats(store.illumstats_file(5).location)
+    assert_close_rel(mean, g["mean"])
+    assert_close_rel(std, g["std"])
+    got = dict(zip(keys.tolist(), vals.tolist()))
+    assert [got[k] for k in sorted(got)] == g["pct_values"].tolist()
+    cont = store.illumstats_file(5).get()
+    assert cont.mean.metadata.is_smoothed
+    assert np.allclose(cont.mean.array, orc.smooth_reflect(g["mean"]), rtol=1e-9, atol=1e-12)

@@ -1,0 +1,64 @@
+"""CPU: HDF5 layout of IllumstatsFile / ChannelImageFile (tmlib/models/file.py:420-456,
+:322-363) written and read through libtmh5 (no h5py)."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from util import load_golden
+
+h5 = pytest.importorskip("tmlibrary_amd.models.file")
+try:
+    h5.h5lib()
+except RuntimeError as e:  # libhdf5 absent on this host
+    pytest.skip(str(e), allow_module_level=True)
+
+H5DUMP = shutil.which("h5dump") or "/opt/conda/bin/h5dump"
+
+
+def test_illumstats_roundtrip(tmp_path):
+    g = load_golden("stats_small")
+    pct = dict(zip(g["pct_keys"].tolist(), g["pct_values"].tolist()))
+    path = str(tmp_path / "illumstats_file_3.h5")
+    h5.write_illumstats(path, g["mean"], g["std"], pct)
+    mean, std, keys, vals = h5.read_illumstats(path)
+    assert np.array_equal(mean, g["mean"]) and np.array_equal(std, g["std"])
+    assert dict(zip(keys.tolist(), vals.tolist())) == pct
+    assert keys.dtype == np.float64 and vals.dtype == np.int64
+
+
+@pytest.mark.skipif(not os.path.exists(H5DUMP), reason="h5dump not available")
+def test_illumstats_layout_h5dump(tmp_path):
+    path = str(tmp_path / "illumstats_file_1.h5")
+    h5.write_illumstats(path, np.zeros((4, 6)), np.ones((4, 6)), {0.0: 1, 50.0: 2, 100.0: 3})
+    out = subprocess.run([H5DUMP, "-H", path], capture_output=True, text=True, check=True).stdout
+    for frag in ('DATASET "mean"', 'DATASET "std"', 'GROUP "percentiles"', 'DATASET "keys"',
+                 'DATASET "values"', "H5T_IEEE_F64LE", "H5T_STD_I64LE", "( 4, 6 )", "( 3 )"):
+        assert frag in out, frag
+
+
+def test_channel_image_roundtrip(tmp_path):
+    rng = np.random.default_rng(0)
+    for dt in (np.uint16, np.uint8):
+        a = rng.integers(0, np.iinfo(dt).max, (37, 53), dtype=dt)
+        p = str(tmp_path / ("channel_image_file_%d.h5" % np.dtype(dt).itemsize))
+        h5.write_channel_image(p, a)
+        b = h5.read_channel_image(p)
+        assert b.dtype == dt and np.array_equal(a, b)
+
+
+@pytest.mark.skipif(not os.path.exists(H5DUMP), reason="h5dump not available")
+def test_channel_image_is_gzip(tmp_path):
+    p = str(tmp_path / "channel_image_file_9.h5")
+    h5.write_channel_image(p, np.zeros((64, 80), np.uint16))
+    out = subprocess.run([H5DUMP, "-p", "-H", p], capture_output=True, text=True, check=True).stdout
+    assert "DEFLATE" in out and "H5T_STD_U16LE" in out
+
+
+def test_missing_dataset_is_keyerror(tmp_path):
+    p = str(tmp_path / "channel_image_file_1.h5")
+    h5.write_channel_image(p, np.zeros((4, 4), np.uint16))
+    with pytest.raises((KeyError, IOError)):
+        h5.read_illumstats(p)

@@ -1,0 +1,756 @@
+// C-ABI of libtmhip.so (include/tmhip.h): handles, device memory, launches.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+
+namespace tmh {
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+template <typename F>
+static int guard(F&& f) {
+  try {
+    f();
+    return TMH_OK;
+  } catch (const Error& e) {
+    set_error(e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_error("host allocation failed");
+    return TMH_ENOMEM;
+  } catch (...) {
+    set_error("unknown error");
+    return TMH_EDEVICE;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// per-kernel event timing
+// ---------------------------------------------------------------------------
+struct ProfSlot {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  double total_ms = 0.0;
+  int64_t launches = 0;
+};
+static std::mutex g_prof_mu;
+static bool g_prof_on = false;
+static std::map<std::string, ProfSlot> g_prof;
+
+ProfScope::ProfScope(const char* name, hipStream_t s) : name_(name), s_(s), slot_(nullptr) {
+  if (!g_prof_on) return;
+  hipEvent_t a, b;
+  if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+  (void)hipEventRecord(a, s);
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  auto& slot = g_prof[name];
+  slot.pending.emplace_back(a, b);
+  slot_ = &slot;
+}
+
+ProfScope::~ProfScope() {
+  if (!slot_) return;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  auto* slot = static_cast<ProfSlot*>(slot_);
+  (void)hipEventRecord(slot->pending.back().second, s_);
+}
+
+static void prof_drain(ProfSlot& slot) {
+  for (auto& p : slot.pending) {
+    float ms = 0.f;
+    (void)hipEventSynchronize(p.second);
+    if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) slot.total_ms += ms;
+    slot.launches += 1;
+    (void)hipEventDestroy(p.first);
+    (void)hipEventDestroy(p.second);
+  }
+  slot.pending.clear();
+}
+
+// ---------------------------------------------------------------------------
+// device buffers
+// ---------------------------------------------------------------------------
+template <typename T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count, bool zero = false) {
+    release();
+    if (count == 0) return;
+    if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) {
+      p = nullptr;
+      throw Error{TMH_ENOMEM, "hipMalloc of " + std::to_string(count * sizeof(T)) + " bytes failed"};
+    }
+    n = count;
+    if (zero) {
+      // null-stream memset: our launches run on non-blocking streams, so wait
+      TMH_HIP(hipMemset(p, 0, count * sizeof(T)));
+      TMH_HIP(hipDeviceSynchronize());
+    }
+  }
+  void ensure(size_t count, bool zero = false) {
+    if (count > n) alloc(count, zero);
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~DBuf() { release(); }
+};
+
+}  // namespace tmh
+
+using namespace tmh;
+
+struct tmh_stats {
+  int device = 0;
+  int H = 0, W = 0;
+  int64_t npx = 0;
+  int Q = 0;
+  double scale = 0.0;
+  unsigned flags = 0;
+  int64_t batch_cap = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  int64_t n = 0;              // sites accumulated (Welford count)
+  int64_t n_deferred = 0;     // sites whose order statistics are stored
+  int64_t last_batch = 0;
+  bool pct_sum_external = false;
+  DBuf<double> mean, m2, lut_log, lut_lin, gamma, acc, tmp_mean, tmp_std;
+  DBuf<int32_t> q_lo, q_hi;
+  DBuf<unsigned long long> pooled;
+  DBuf<uint32_t> hist_hi, site_hist;
+  DBuf<uint16_t> vlo, vhi, stage;
+  DBuf<int64_t> zeros;
+};
+
+struct tmh_corrector {
+  int device = 0;
+  int H = 0, W = 0;
+  int64_t npx = 0;
+  int log_transform = 1;
+  hipStream_t stream = nullptr;
+  DBuf<float4> coef;
+  DBuf<float2> lut, mconst;
+  DBuf<double> sums, partial;
+  DBuf<uint16_t> stage_in, stage_out;
+  DBuf<uint8_t> stage8_in, stage8_out;
+};
+
+static hipStream_t pick(hipStream_t own, void* s) { return s ? (hipStream_t)s : own; }
+
+extern "C" {
+
+int tmh_abi_version(void) { return TMH_ABI_VERSION; }
+const char* tmh_last_error(void) { return g_last_error.c_str(); }
+
+int tmh_device_count(int* n) {
+  return guard([&] {
+    TMH_CHECK(n, TMH_EINVAL, "n is NULL");
+    TMH_HIP(hipGetDeviceCount(n));
+  });
+}
+
+int tmh_set_device(int device) { return guard([&] { TMH_HIP(hipSetDevice(device)); }); }
+
+int tmh_synchronize(void* stream) {
+  return guard([&] {
+    if (stream)
+      TMH_HIP(hipStreamSynchronize((hipStream_t)stream));
+    else
+      TMH_HIP(hipDeviceSynchronize());
+  });
+}
+
+// ---------------------------------------------------------------------------
+// stats
+// ---------------------------------------------------------------------------
+
+static void stats_reserve_sites(tmh_stats* h, int64_t n_sites) {
+  // growing frees buffers earlier launches may still be using
+  const bool grow = (size_t)n_sites * kHiBins > h->hist_hi.n || (size_t)n_sites > h->zeros.n ||
+                    ((h->flags & 2u) && (size_t)n_sites * kBins > h->site_hist.n) ||
+                    (!(h->flags & TMH_STATS_DEFERRED_PCT) && (size_t)n_sites * h->Q > h->vlo.n);
+  if (grow) TMH_HIP(hipStreamSynchronize(h->stream));
+  // per-site slabs: hist_hi stays all-zero between launches (the kernel
+  // resets what it touched), so it is zeroed only when (re)allocated.
+  if ((size_t)n_sites * kHiBins > h->hist_hi.n) h->hist_hi.alloc((size_t)n_sites * kHiBins, true);
+  h->zeros.ensure((size_t)n_sites);
+  if (h->flags & 2u) h->site_hist.ensure((size_t)n_sites * kBins);
+  if (!(h->flags & TMH_STATS_DEFERRED_PCT)) {
+    h->vlo.ensure((size_t)n_sites * h->Q);
+    h->vhi.ensure((size_t)n_sites * h->Q);
+  }
+}
+
+static void stats_grow_deferred(tmh_stats* h, int64_t extra) {
+  const size_t need = (size_t)(h->n_deferred + extra) * h->Q;
+  if (need <= h->vlo.n) return;
+  size_t cap = std::max(need, h->vlo.n * 2);
+  for (auto* b : {&h->vlo, &h->vhi}) {
+    DBuf<uint16_t> nb;
+    nb.alloc(cap);
+    if (h->n_deferred)
+      TMH_HIP(hipMemcpyAsync(nb.p, b->p, (size_t)h->n_deferred * h->Q * sizeof(uint16_t),
+                             hipMemcpyDeviceToDevice, h->stream));
+    TMH_HIP(hipStreamSynchronize(h->stream));
+    std::swap(b->p, nb.p);
+    std::swap(b->n, nb.n);
+  }
+}
+
+int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo,
+                     const int64_t* q_hi, const double* q_gamma, const double* lut_log10,
+                     int batch_capacity, unsigned flags, tmh_stats** out) {
+  return guard([&] {
+    TMH_CHECK(out, TMH_EINVAL, "out is NULL");
+    TMH_CHECK(height > 0 && width > 0, TMH_EINVAL, "image dimensions must be positive");
+    const int64_t npx = (int64_t)height * width;
+    TMH_CHECK(npx < (int64_t(1) << 31), TMH_EINVAL, "images must have fewer than 2^31 pixels");
+    TMH_CHECK(n_quantiles > 0 && q_lo && q_hi && q_gamma && lut_log10, TMH_EINVAL,
+              "quantile tables and LUT are required");
+    auto* h = new tmh_stats();
+    try {
+      TMH_HIP(hipGetDevice(&h->device));
+      h->H = height;
+      h->W = width;
+      h->npx = npx;
+      h->Q = n_quantiles;
+      h->scale = (npx > 1) ? (double)(n_quantiles - 1) / (double)(npx - 1) : 0.0;
+      h->flags = flags;
+      h->batch_cap = std::min(4096, batch_capacity > 0 ? batch_capacity : 1);
+      TMH_HIP(hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking));
+      h->stream = h->own_stream;
+      h->mean.alloc(npx, true);
+      h->m2.alloc(npx, true);
+      h->acc.alloc(n_quantiles, true);
+      h->pooled.alloc(kBins, true);
+      h->lut_log.alloc(kBins);
+      h->lut_lin.alloc(kBins);
+      h->gamma.alloc(n_quantiles);
+      h->q_lo.alloc(n_quantiles);
+      h->q_hi.alloc(n_quantiles);
+      std::vector<int32_t> lo(n_quantiles), hi(n_quantiles);
+      for (int i = 0; i < n_quantiles; ++i) {
+        TMH_CHECK(q_lo[i] >= 0 && q_lo[i] < npx && q_hi[i] >= q_lo[i] && q_hi[i] < npx, TMH_EINVAL,
+                  "quantile positions out of range");
+        TMH_CHECK(i == 0 || (q_lo[i] >= q_lo[i - 1] && q_hi[i] >= q_hi[i - 1]), TMH_EINVAL,
+                  "quantile positions must be non-decreasing");
+        lo[i] = (int32_t)q_lo[i];
+        hi[i] = (int32_t)q_hi[i];
+      }
+      std::vector<double> lin(kBins);
+      for (int v = 0; v < kBins; ++v) lin[v] = (double)v;
+      TMH_HIP(hipMemcpy(h->q_lo.p, lo.data(), lo.size() * 4, hipMemcpyHostToDevice));
+      TMH_HIP(hipMemcpy(h->q_hi.p, hi.data(), hi.size() * 4, hipMemcpyHostToDevice));
+      TMH_HIP(hipMemcpy(h->gamma.p, q_gamma, (size_t)n_quantiles * 8, hipMemcpyHostToDevice));
+      TMH_HIP(hipMemcpy(h->lut_log.p, lut_log10, (size_t)kBins * 8, hipMemcpyHostToDevice));
+      TMH_HIP(hipMemcpy(h->lut_lin.p, lin.data(), (size_t)kBins * 8, hipMemcpyHostToDevice));
+    } catch (...) {
+      tmh_stats_destroy(h);
+      throw;
+    }
+    *out = h;
+  });
+}
+
+void tmh_stats_destroy(tmh_stats* h) {
+  if (!h) return;
+  if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
+  if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
+  hipStream_t s = h->own_stream;
+  delete h;
+  if (s) (void)hipStreamDestroy(s);
+}
+
+int tmh_stats_set_stream(tmh_stats* h, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
+    h->stream = stream ? (hipStream_t)stream : h->own_stream;
+  });
+}
+
+int tmh_stats_reset(tmh_stats* h) {
+  return guard([&] {
+    TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
+    TMH_HIP(hipMemsetAsync(h->mean.p, 0, h->npx * 8, h->stream));
+    TMH_HIP(hipMemsetAsync(h->m2.p, 0, h->npx * 8, h->stream));
+    TMH_HIP(hipMemsetAsync(h->acc.p, 0, (size_t)h->Q * 8, h->stream));
+    TMH_HIP(hipMemsetAsync(h->pooled.p, 0, (size_t)kBins * 8, h->stream));
+    h->n = 0;
+    h->n_deferred = 0;
+    h->last_batch = 0;
+    h->pct_sum_external = false;
+  });
+}
+
+static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int log_transform,
+                             hipStream_t s) {
+  if (ns <= 0) return;
+  const double* lut = log_transform ? h->lut_log.p : h->lut_lin.p;
+  launch_welford(d, h->npx, ns, h->n, h->mean.p, h->m2.p, lut, s);
+  // order statistics, in chunks so the per-site slabs stay bounded
+  const int64_t chunk = 4096;
+  for (int64_t c0 = 0; c0 < ns; c0 += chunk) {
+    const int64_t nc = std::min(chunk, ns - c0);
+    stats_reserve_sites(h, nc);
+    uint16_t *vlo, *vhi;
+    if (h->flags & TMH_STATS_DEFERRED_PCT) {
+      stats_grow_deferred(h, nc);
+      vlo = h->vlo.p + (size_t)h->n_deferred * h->Q;
+      vhi = h->vhi.p + (size_t)h->n_deferred * h->Q;
+    } else {
+      vlo = h->vlo.p;
+      vhi = h->vhi.p;
+    }
+    launch_hist_scatter(d + c0 * h->npx, h->npx, nc, h->hist_hi.p, h->q_lo.p, h->q_hi.p, h->Q,
+                        h->scale, vlo, vhi, h->pooled.p, h->zeros.p,
+                        (h->flags & 2u) ? h->site_hist.p : nullptr, s);
+    if (h->flags & TMH_STATS_DEFERRED_PCT)
+      h->n_deferred += nc;
+    else
+      launch_pct_accumulate(vlo, vhi, nc, h->Q, h->gamma.p, h->acc.p, s);
+    h->last_batch = nc;
+  }
+  h->n += ns;
+}
+
+int tmh_stats_update_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
+                            int log_transform, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && (dev_sites || n_sites == 0) && n_sites >= 0, TMH_EINVAL, "bad arguments");
+    stats_update_dev(h, dev_sites, n_sites, log_transform, pick(h->stream, stream));
+  });
+}
+
+int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites, int log_transform,
+                     int64_t* zero_counts_out) {
+  return guard([&] {
+    TMH_CHECK(h && (host_sites || n_sites == 0) && n_sites >= 0, TMH_EINVAL, "bad arguments");
+    if ((size_t)h->batch_cap * h->npx > h->stage.n) {
+      TMH_HIP(hipStreamSynchronize(h->stream));
+      h->stage.ensure((size_t)h->batch_cap * h->npx);
+    }
+    for (int64_t s0 = 0; s0 < n_sites; s0 += h->batch_cap) {
+      const int64_t ns = std::min<int64_t>(h->batch_cap, n_sites - s0);
+      TMH_HIP(hipMemcpyAsync(h->stage.p, host_sites + s0 * h->npx, (size_t)ns * h->npx * 2,
+                             hipMemcpyHostToDevice, h->stream));
+      stats_update_dev(h, h->stage.p, ns, log_transform, h->stream);
+      if (zero_counts_out)
+        TMH_HIP(hipMemcpyAsync(zero_counts_out + s0, h->zeros.p, (size_t)ns * 8,
+                               hipMemcpyDeviceToHost, h->stream));
+      TMH_HIP(hipStreamSynchronize(h->stream));  // the stage buffer is reused
+    }
+  });
+}
+
+static void stats_pct_sum_device(tmh_stats* h) {
+  if ((h->flags & TMH_STATS_DEFERRED_PCT) && !h->pct_sum_external) {
+    TMH_HIP(hipMemsetAsync(h->acc.p, 0, (size_t)h->Q * 8, h->stream));
+    launch_pct_accumulate(h->vlo.p, h->vhi.p, h->n_deferred, h->Q, h->gamma.p, h->acc.p, h->stream);
+  }
+}
+
+int tmh_stats_finalize(tmh_stats* h, int64_t* n, double* mean, double* std, double* pct_sum,
+                       uint64_t* hist) {
+  return guard([&] {
+    TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
+    if (n) *n = h->n;
+    if (mean || std) {
+      h->tmp_std.ensure(h->npx);
+      launch_finalize(h->mean.p, h->m2.p, h->n, h->npx, nullptr, h->tmp_std.p, h->stream);
+      if (mean)
+        TMH_HIP(hipMemcpyAsync(mean, h->mean.p, h->npx * 8, hipMemcpyDeviceToHost, h->stream));
+      if (std)
+        TMH_HIP(hipMemcpyAsync(std, h->tmp_std.p, h->npx * 8, hipMemcpyDeviceToHost, h->stream));
+    }
+    if (pct_sum) {
+      stats_pct_sum_device(h);
+      TMH_HIP(hipMemcpyAsync(pct_sum, h->acc.p, (size_t)h->Q * 8, hipMemcpyDeviceToHost, h->stream));
+    }
+    if (hist)
+      TMH_HIP(hipMemcpyAsync(hist, h->pooled.p, (size_t)kBins * 8, hipMemcpyDeviceToHost, h->stream));
+    TMH_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int tmh_stats_finalize_device(tmh_stats* h, double* dev_mean, double* dev_std, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
+    launch_finalize(h->mean.p, h->m2.p, h->n, h->npx, dev_mean, dev_std, pick(h->stream, stream));
+  });
+}
+
+int tmh_stats_site_histogram(tmh_stats* h, int64_t site, uint32_t* host_hist) {
+  return guard([&] {
+    TMH_CHECK(h && host_hist, TMH_EINVAL, "bad arguments");
+    TMH_CHECK(h->flags & 2u, TMH_ESTATE, "handle was created without TMH_STATS_KEEP_SITE_HIST (2)");
+    TMH_CHECK(site >= 0 && site < h->last_batch, TMH_EINVAL, "site outside the last batch");
+    TMH_HIP(hipMemcpyAsync(host_hist, h->site_hist.p + (size_t)site * kBins, (size_t)kBins * 4,
+                           hipMemcpyDeviceToHost, h->stream));
+    TMH_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int tmh_stats_site_order_stats(tmh_stats* h, int64_t site, uint16_t* host_vlo, uint16_t* host_vhi) {
+  return guard([&] {
+    TMH_CHECK(h && host_vlo && host_vhi, TMH_EINVAL, "bad arguments");
+    const bool deferred = h->flags & TMH_STATS_DEFERRED_PCT;
+    const int64_t avail = deferred ? h->n_deferred : h->last_batch;
+    TMH_CHECK(site >= 0 && site < avail, TMH_EINVAL, "site not available");
+    const size_t off = (size_t)site * h->Q;
+    TMH_HIP(hipMemcpyAsync(host_vlo, h->vlo.p + off, (size_t)h->Q * 2, hipMemcpyDeviceToHost, h->stream));
+    TMH_HIP(hipMemcpyAsync(host_vhi, h->vhi.p + off, (size_t)h->Q * 2, hipMemcpyDeviceToHost, h->stream));
+    TMH_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int tmh_stats_get_n(tmh_stats* h, int64_t* n) {
+  return guard([&] {
+    TMH_CHECK(h && n, TMH_EINVAL, "bad arguments");
+    *n = h->n;
+  });
+}
+
+int tmh_stats_merge_stage1(tmh_stats* h, double* dev_nmean, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && dev_nmean, TMH_EINVAL, "bad arguments");
+    launch_merge1(h->mean.p, h->n, h->npx, dev_nmean, pick(h->stream, stream));
+  });
+}
+
+int tmh_stats_merge_stage2(tmh_stats* h, const double* dev_sum_nmean, int64_t n_total,
+                           double* dev_m2c, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && dev_sum_nmean && dev_m2c && n_total > 0, TMH_EINVAL, "bad arguments");
+    launch_merge2(h->mean.p, h->m2.p, h->n, dev_sum_nmean, n_total, h->npx, dev_m2c,
+                  pick(h->stream, stream));
+  });
+}
+
+int tmh_stats_merge_stage3(tmh_stats* h, int64_t n_total, const double* dev_sum_m2c, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && dev_sum_m2c && n_total >= 0, TMH_EINVAL, "bad arguments");
+    launch_copy_f64(dev_sum_m2c, h->m2.p, h->npx, pick(h->stream, stream));
+    h->n = n_total;
+  });
+}
+
+int tmh_stats_pct_accumulate(tmh_stats* h, double* dev_acc, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && dev_acc, TMH_EINVAL, "bad arguments");
+    TMH_CHECK(h->flags & TMH_STATS_DEFERRED_PCT, TMH_ESTATE,
+              "percentile chain needs a TMH_STATS_DEFERRED_PCT handle");
+    launch_pct_accumulate(h->vlo.p, h->vhi.p, h->n_deferred, h->Q, h->gamma.p, dev_acc,
+                          pick(h->stream, stream));
+  });
+}
+
+int tmh_stats_set_pct_sum(tmh_stats* h, const double* dev_acc, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && dev_acc, TMH_EINVAL, "bad arguments");
+    launch_copy_f64(dev_acc, h->acc.p, h->Q, pick(h->stream, stream));
+    h->pct_sum_external = true;
+  });
+}
+
+// ---------------------------------------------------------------------------
+// smoothing
+// ---------------------------------------------------------------------------
+
+static std::vector<double> gaussian_taps(double sigma) {
+  // mahotas 1.4.3 gaussian_filter1d (order 0): radius int(4 sd + 0.5)
+  const int lw = (int)(4.0 * sigma + 0.5);
+  std::vector<double> w(2 * lw + 1, 0.0);
+  w[lw] = 1.0;
+  double sum = 1.0;
+  const double sd2 = sigma * sigma;
+  for (int ii = 1; ii <= lw; ++ii) {
+    const double t = std::exp(-0.5 * (double)(ii * ii) / sd2);
+    w[lw + ii] = t;
+    w[lw - ii] = t;
+    sum += 2.0 * t;
+  }
+  for (auto& x : w) x /= sum;
+  return w;
+}
+
+// taps per sigma, uploaded once (no allocation or sync on later calls)
+static std::mutex g_taps_mu;
+static std::map<double, std::pair<double*, int>> g_taps;
+
+static std::pair<double*, int> taps_for(double sigma) {
+  std::lock_guard<std::mutex> lk(g_taps_mu);
+  auto it = g_taps.find(sigma);
+  if (it != g_taps.end()) return it->second;
+  const auto w = gaussian_taps(sigma);
+  double* d = nullptr;
+  TMH_HIP(hipMalloc(&d, w.size() * 8));
+  TMH_HIP(hipMemcpy(d, w.data(), w.size() * 8, hipMemcpyHostToDevice));
+  auto v = std::make_pair(d, (int)(w.size() / 2));
+  g_taps[sigma] = v;
+  return v;
+}
+
+int tmh_smooth_f64_device(const double* dev_in, double* dev_out, double* dev_tmp, int height,
+                          int width, double sigma, void* stream) {
+  return guard([&] {
+    TMH_CHECK(dev_in && dev_out && dev_tmp && height > 0 && width > 0, TMH_EINVAL, "bad arguments");
+    TMH_CHECK(sigma >= 0.125, TMH_EINVAL, "sigma must be >= 0.125");
+    TMH_CHECK(dev_tmp != dev_in && dev_tmp != dev_out, TMH_EINVAL, "dev_tmp must be a third buffer");
+    const auto t = taps_for(sigma);
+    launch_smooth(dev_in, dev_out, dev_tmp, height, width, t.first, t.second, (hipStream_t)stream);
+  });
+}
+
+int tmh_smooth_f64(const double* host_in, double* host_out, int height, int width, double sigma) {
+  return guard([&] {
+    TMH_CHECK(host_in && host_out && height > 0 && width > 0, TMH_EINVAL, "bad arguments");
+    const size_t npx = (size_t)height * width;
+    DBuf<double> a, b, t;
+    a.alloc(npx);
+    b.alloc(npx);
+    t.alloc(npx);
+    TMH_HIP(hipMemcpy(a.p, host_in, npx * 8, hipMemcpyHostToDevice));
+    int rc = tmh_smooth_f64_device(a.p, b.p, t.p, height, width, sigma, nullptr);
+    if (rc) throw Error{rc, g_last_error};
+    TMH_HIP(hipDeviceSynchronize());
+    TMH_HIP(hipMemcpy(host_out, b.p, npx * 8, hipMemcpyDeviceToHost));
+  });
+}
+
+// ---------------------------------------------------------------------------
+// correction
+// ---------------------------------------------------------------------------
+
+static void corrector_coeffs(tmh_corrector* c, const double* d_mean, const double* d_std,
+                             hipStream_t s) {
+  ProfScope prof("coeffs", s);
+  const int np = 512;
+  launch_reduce_sum(d_std, c->npx, c->partial.p, np, c->sums.p, s);
+  launch_reduce_sum(d_mean, c->npx, c->partial.p, np, c->sums.p + 1, s);
+  launch_coeffs(d_mean, d_std, c->sums.p, c->npx, c->coef.p, c->mconst.p, s);
+}
+
+static void corrector_init(tmh_corrector* c, const double* d_mean, const double* d_std) {
+  c->sums.alloc(2);
+  c->partial.alloc(512);
+  c->coef.alloc(c->npx);
+  c->mconst.alloc(1);
+  corrector_coeffs(c, d_mean, d_std, c->stream);
+}
+
+int tmh_corrector_create_device(const double* dev_mean, const double* dev_std, int height,
+                                int width, int log_transform, double zero_log10, void* stream,
+                                tmh_corrector** out) {
+  return guard([&] {
+    TMH_CHECK(out && dev_mean && dev_std && height > 0 && width > 0, TMH_EINVAL, "bad arguments");
+    auto* c = new tmh_corrector();
+    try {
+      TMH_HIP(hipGetDevice(&c->device));
+      c->H = height;
+      c->W = width;
+      c->npx = (int64_t)height * width;
+      c->log_transform = log_transform ? 1 : 0;
+      c->stream = (hipStream_t)stream;
+      c->lut.alloc(kBins);
+      launch_build_corr_lut(c->lut.p, c->log_transform, zero_log10, c->stream);
+      corrector_init(c, dev_mean, dev_std);
+    } catch (...) {
+      delete c;
+      throw;
+    }
+    *out = c;
+  });
+}
+
+int tmh_corrector_create(const double* host_mean, const double* host_std, int height, int width,
+                         int log_transform, double zero_log10, tmh_corrector** out) {
+  return guard([&] {
+    TMH_CHECK(out && host_mean && host_std && height > 0 && width > 0, TMH_EINVAL, "bad arguments");
+    const size_t npx = (size_t)height * width;
+    DBuf<double> m, s;
+    m.alloc(npx);
+    s.alloc(npx);
+    TMH_HIP(hipMemcpy(m.p, host_mean, npx * 8, hipMemcpyHostToDevice));
+    TMH_HIP(hipMemcpy(s.p, host_std, npx * 8, hipMemcpyHostToDevice));
+    int rc = tmh_corrector_create_device(m.p, s.p, height, width, log_transform, zero_log10, nullptr,
+                                         out);
+    if (rc) throw Error{rc, g_last_error};
+    TMH_HIP(hipDeviceSynchronize());
+  });
+}
+
+void tmh_corrector_destroy(tmh_corrector* c) {
+  if (!c) return;
+  (void)hipStreamSynchronize(c->stream);
+  delete c;
+}
+
+int tmh_corrector_update_device(tmh_corrector* c, const double* dev_mean, const double* dev_std,
+                                void* stream) {
+  return guard([&] {
+    TMH_CHECK(c && dev_mean && dev_std, TMH_EINVAL, "bad arguments");
+    corrector_coeffs(c, dev_mean, dev_std, pick(c->stream, stream));
+  });
+}
+
+int tmh_corrector_means(tmh_corrector* c, double* mean_of_std, double* mean_of_mean) {
+  return guard([&] {
+    TMH_CHECK(c, TMH_EINVAL, "corrector is NULL");
+    double sums[2];
+    TMH_HIP(hipStreamSynchronize(c->stream));
+    TMH_HIP(hipMemcpy(sums, c->sums.p, 16, hipMemcpyDeviceToHost));
+    if (mean_of_std) *mean_of_std = sums[0] / (double)c->npx;
+    if (mean_of_mean) *mean_of_mean = sums[1] / (double)c->npx;
+  });
+}
+
+static void check_clip(int lo, int hi, int maxv) {
+  if (lo < 0) return;
+  TMH_CHECK(lo <= maxv && hi >= 0 && hi <= maxv, TMH_EINVAL, "clip bounds out of range");
+}
+
+int tmh_correct_u16_device(tmh_corrector* c, const uint16_t* dev_in, uint16_t* dev_out,
+                           int64_t n_sites, int clip_lo, int clip_hi, void* stream) {
+  return guard([&] {
+    TMH_CHECK(c && (dev_in && dev_out || n_sites == 0) && n_sites >= 0, TMH_EINVAL, "bad arguments");
+    check_clip(clip_lo, clip_hi, 65535);
+    launch_correct_u16(dev_in, dev_out, c->npx, n_sites, c->coef.p, c->lut.p, c->mconst.p,
+                       c->log_transform, clip_lo, clip_hi, pick(c->stream, stream));
+  });
+}
+
+int tmh_correct_u16(tmh_corrector* c, const uint16_t* host_in, uint16_t* host_out, int64_t n_sites,
+                    int clip_lo, int clip_hi) {
+  return guard([&] {
+    TMH_CHECK(c && (host_in && host_out || n_sites == 0) && n_sites >= 0, TMH_EINVAL,
+              "bad arguments");
+    check_clip(clip_lo, clip_hi, 65535);
+    const int64_t cap = 64;
+    c->stage_in.ensure((size_t)std::min(cap, std::max<int64_t>(n_sites, 1)) * c->npx);
+    c->stage_out.ensure(c->stage_in.n);
+    const int64_t per = (int64_t)(c->stage_in.n / c->npx);
+    for (int64_t s0 = 0; s0 < n_sites; s0 += per) {
+      const int64_t ns = std::min(per, n_sites - s0);
+      const size_t bytes = (size_t)ns * c->npx * 2;
+      TMH_HIP(hipMemcpyAsync(c->stage_in.p, host_in + s0 * c->npx, bytes, hipMemcpyHostToDevice,
+                             c->stream));
+      launch_correct_u16(c->stage_in.p, c->stage_out.p, c->npx, ns, c->coef.p, c->lut.p,
+                         c->mconst.p, c->log_transform, clip_lo, clip_hi, c->stream);
+      TMH_HIP(hipMemcpyAsync(host_out + s0 * c->npx, c->stage_out.p, bytes, hipMemcpyDeviceToHost,
+                             c->stream));
+      TMH_HIP(hipStreamSynchronize(c->stream));
+    }
+  });
+}
+
+int tmh_correct_u8(tmh_corrector* c, const uint8_t* host_in, uint8_t* host_out, int64_t n_sites,
+                   int clip_lo, int clip_hi) {
+  return guard([&] {
+    TMH_CHECK(c && (host_in && host_out || n_sites == 0) && n_sites >= 0, TMH_EINVAL,
+              "bad arguments");
+    check_clip(clip_lo, clip_hi, 255);
+    const size_t bytes = (size_t)n_sites * c->npx;
+    if (!bytes) return;
+    c->stage8_in.ensure(bytes);
+    c->stage8_out.ensure(bytes);
+    TMH_HIP(hipMemcpyAsync(c->stage8_in.p, host_in, bytes, hipMemcpyHostToDevice, c->stream));
+    launch_correct_u8(c->stage8_in.p, c->stage8_out.p, c->npx, n_sites, c->coef.p, c->lut.p,
+                      c->mconst.p, c->log_transform, clip_lo, clip_hi, c->stream);
+    TMH_HIP(hipMemcpyAsync(host_out, c->stage8_out.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    TMH_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int tmh_clip_u16(const uint16_t* host_in, uint16_t* host_out, int64_t n, int lo, int hi) {
+  return guard([&] {
+    TMH_CHECK((host_in && host_out) || n == 0, TMH_EINVAL, "bad arguments");
+    TMH_CHECK(lo >= 0 && lo <= 65535 && hi >= 0 && hi <= 65535, TMH_EINVAL, "clip bounds out of range");
+    if (n == 0) return;
+    DBuf<uint16_t> a, b;
+    a.alloc(n);
+    b.alloc(n);
+    TMH_HIP(hipMemcpy(a.p, host_in, (size_t)n * 2, hipMemcpyHostToDevice));
+    launch_clip_u16(a.p, b.p, n, lo, hi, nullptr);
+    TMH_HIP(hipMemcpy(host_out, b.p, (size_t)n * 2, hipMemcpyDeviceToHost));
+  });
+}
+
+// ---------------------------------------------------------------------------
+// misc
+// ---------------------------------------------------------------------------
+
+int tmh_synth_sites_device(uint16_t* dev_out, int64_t n_sites, int height, int width, uint64_t seed,
+                           int channel, int64_t first_site, void* stream) {
+  return guard([&] {
+    TMH_CHECK(dev_out && n_sites >= 0 && height > 0 && width > 0, TMH_EINVAL, "bad arguments");
+    launch_synth(dev_out, n_sites, height, width, seed, channel, first_site, (hipStream_t)stream);
+  });
+}
+
+int tmh_malloc_device(void** dev_ptr, size_t bytes) {
+  return guard([&] {
+    TMH_CHECK(dev_ptr, TMH_EINVAL, "dev_ptr is NULL");
+    if (hipMalloc(dev_ptr, bytes) != hipSuccess) {
+      *dev_ptr = nullptr;
+      throw Error{TMH_ENOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed"};
+    }
+  });
+}
+
+int tmh_free_device(void* dev_ptr) { return guard([&] { TMH_HIP(hipFree(dev_ptr)); }); }
+
+int tmh_memcpy(void* dst, const void* src, size_t bytes, int kind, void* stream) {
+  return guard([&] {
+    TMH_CHECK(kind >= 0 && kind <= 2, TMH_EINVAL, "kind must be 0 (h2d), 1 (d2h) or 2 (d2d)");
+    const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
+                          : kind == 1 ? hipMemcpyDeviceToHost
+                                      : hipMemcpyDeviceToDevice;
+    TMH_HIP(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)stream));
+    TMH_HIP(hipStreamSynchronize((hipStream_t)stream));
+  });
+}
+
+int tmh_profile_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof_on = on != 0;
+  return TMH_OK;
+}
+
+int tmh_profile_read(const char* kernel, double* total_ms, int64_t* launches) {
+  return guard([&] {
+    TMH_CHECK(kernel && total_ms && launches, TMH_EINVAL, "bad arguments");
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    auto it = g_prof.find(kernel);
+    if (it == g_prof.end()) {
+      *total_ms = 0.0;
+      *launches = 0;
+      return;
+    }
+    prof_drain(it->second);
+    *total_ms = it->second.total_ms;
+    *launches = it->second.launches;
+  });
+}
+
+int tmh_profile_reset(void) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  for (auto& kv : g_prof) {
+    prof_drain(kv.second);
+    kv.second.total_ms = 0.0;
+    kv.second.launches = 0;
+  }
+  return TMH_OK;
+}
+
+}  // extern "C"

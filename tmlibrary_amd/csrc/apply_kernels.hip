@@ -1,0 +1,374 @@
+// Apply-step kernels for gfx950 (MI355X).
+//
+// Reference: tmlib/image.py
+//   287-311 / 1172-1193  smoothing (mahotas.gaussian_filter, 'reflect', f64)
+//   599-631              ChannelImage._correct_illumination
+//   570-597              ChannelImage.clip
+//
+// Correction is pixel-major: each thread owns 8 pixels, loads their
+// per-pixel coefficients once and walks the sites, so HBM sees 2 B/px read
+// + 2 B/px written per site.  The log10 of the input comes from an f32
+// hi/lo LUT (|err| ~1e-14) staged in LDS, the affine step runs in f32
+// keeping (L - mean) exact to ~1e-7, and 10**t is one v_exp_f32: |rel err|
+// < 1e-6, i.e. < 0.07 DN at 65535 (tolerance +-1 DN).
+#include "common.h"
+
+namespace tmh {
+
+// ---------------------------------------------------------------------------
+// separable Gaussian, 'reflect' border (d c b a | a b c d | d c b a)
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  if (n == 1) return 0;
+  const int p = 2 * n;
+  i %= p;
+  if (i < 0) i += p;
+  return (i < n) ? i : p - 1 - i;
+}
+
+// axis 0 (rows of the plane vary): out[y][x] = sum_j w[j] in[refl(y+j-r)][x]
+__global__ __launch_bounds__(256) void k_smooth_axis0(const double* __restrict__ in,
+                                                      double* __restrict__ out, int H, int W,
+                                                      const double* __restrict__ w, int r) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  const int y = blockIdx.y;
+  if (x >= W) return;
+  double acc = 0.0;
+  for (int j = -r; j <= r; ++j) acc = fma(w[j + r], in[(int64_t)reflect_idx(y + j, H) * W + x], acc);
+  out[(int64_t)y * W + x] = acc;
+}
+
+// axis 1 (along a row), row segment + halo staged in LDS
+constexpr int kSmTile = 256;
+constexpr int kSmMaxR = 128;
+__global__ __launch_bounds__(256) void k_smooth_axis1(const double* __restrict__ in,
+                                                      double* __restrict__ out, int H, int W,
+                                                      const double* __restrict__ w, int r) {
+  __shared__ double tile[kSmTile + 2 * kSmMaxR];
+  const int x0 = blockIdx.x * kSmTile;
+  const int y = blockIdx.y;
+  const double* row = in + (int64_t)y * W;
+  for (int i = threadIdx.x; i < kSmTile + 2 * r; i += 256) tile[i] = row[reflect_idx(x0 - r + i, W)];
+  __syncthreads();
+  const int x = x0 + threadIdx.x;
+  if (x >= W) return;
+  double acc = 0.0;
+  for (int j = 0; j <= 2 * r; ++j) acc = fma(w[j], tile[threadIdx.x + j], acc);
+  out[(int64_t)y * W + x] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_smooth_axis1_wide(const double* __restrict__ in,
+                                                           double* __restrict__ out, int H, int W,
+                                                           const double* __restrict__ w, int r) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  const int y = blockIdx.y;
+  if (x >= W) return;
+  const double* row = in + (int64_t)y * W;
+  double acc = 0.0;
+  for (int j = -r; j <= r; ++j) acc = fma(w[j + r], row[reflect_idx(x + j, W)], acc);
+  out[(int64_t)y * W + x] = acc;
+}
+
+void launch_smooth(const double* in, double* out, double* tmp, int H, int W, const double* d_w,
+                   int radius, hipStream_t s) {
+  ProfScope prof("smooth", s);
+  const dim3 grid((unsigned)cdiv(W, 256), (unsigned)H);
+  hipLaunchKernelGGL(k_smooth_axis0, grid, dim3(256), 0, s, in, tmp, H, W, d_w, radius);
+  if (radius <= kSmMaxR)
+    hipLaunchKernelGGL(k_smooth_axis1, dim3((unsigned)cdiv(W, kSmTile), (unsigned)H), dim3(256), 0,
+                       s, tmp, out, H, W, d_w, radius);
+  else
+    hipLaunchKernelGGL(k_smooth_axis1_wide, grid, dim3(256), 0, s, tmp, out, H, W, d_w, radius);
+  TMH_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// deterministic f64 sum (two fixed-order passes)
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ double block_sum256(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  return red[0];
+}
+
+__global__ __launch_bounds__(256) void k_reduce_partial(const double* __restrict__ x, int64_t n,
+                                                        double* __restrict__ partial) {
+  __shared__ double red[256];
+  const int64_t chunk = cdiv(n, gridDim.x);
+  const int64_t b = (int64_t)blockIdx.x * chunk;
+  const int64_t e = (b + chunk < n) ? b + chunk : n;
+  double acc = 0.0;
+  for (int64_t i = b + threadIdx.x; i < e; i += 256) acc += x[i];
+  const double t = block_sum256(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void k_reduce_final(const double* __restrict__ partial, int n,
+                                                      double* __restrict__ out) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) acc += partial[i];
+  const double t = block_sum256(acc, red);
+  if (threadIdx.x == 0) *out = t;
+}
+
+void launch_reduce_sum(const double* x, int64_t n, double* partial, int n_partial, double* out,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_partial, dim3(n_partial), dim3(256), 0, s, x, n, partial);
+  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(256), 0, s, partial, n_partial, out);
+  TMH_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// correction coefficients
+// ---------------------------------------------------------------------------
+
+// LUT of the correct-path transform of every uint16 value as an f32 hi/lo pair:
+// log: v==0 -> log10(1e-10) (image.py:624-626), else log10(v); no log: v.
+__global__ void k_build_corr_lut(float2* __restrict__ lut, int log_transform, double zero_log10) {
+  const int v = blockIdx.x * 256 + threadIdx.x;
+  if (v >= kBins) return;
+  double L = (double)v;
+  if (log_transform) L = (v == 0) ? zero_log10 : log10((double)v);
+  const float hi = (float)L;
+  lut[v] = make_float2(hi, (float)(L - (double)hi));
+}
+
+void launch_build_corr_lut(float2* lut, int log_transform, double zero_log10, hipStream_t s) {
+  hipLaunchKernelGGL(k_build_corr_lut, dim3(kBins / 256), dim3(256), 0, s, lut, log_transform,
+                     zero_log10);
+  TMH_HIP(hipGetLastError());
+}
+
+// coef[i] = (mean_hi, mean_lo, a = mean(std)/std, 0);  mconst = mean(mean) hi/lo
+__global__ void k_coeffs(const double* __restrict__ mean, const double* __restrict__ std,
+                         const double* __restrict__ sums, int64_t npx, float4* __restrict__ coef,
+                         float2* __restrict__ mconst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const double S = sums[0] / (double)npx;  // np.mean(std)
+  const double M = sums[1] / (double)npx;  // np.mean(mean)
+  if (i == 0) {
+    const float mh = (float)M;
+    mconst[0] = make_float2(mh, (float)(M - (double)mh));
+  }
+  if (i >= npx) return;
+  const double mu = mean[i];
+  const float mh = (float)mu;
+  coef[i] = make_float4(mh, (float)(mu - (double)mh), (float)(S / std[i]), 0.0f);
+}
+
+void launch_coeffs(const double* mean, const double* std, const double* sums, int64_t npx,
+                   float4* coef, float2* mconst, hipStream_t s) {
+  hipLaunchKernelGGL(k_coeffs, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, mean, std, sums,
+                     npx, coef, mconst);
+  TMH_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// fused correct (+ clip)
+// ---------------------------------------------------------------------------
+
+constexpr float kLog2_10 = 3.32192809488736234787f;
+
+template <bool LOG, int BITS>
+__device__ __forceinline__ uint32_t correct1(uint32_t u, const float4 c, const float2* slut,
+                                             const float2* __restrict__ glut, float mh, float ml,
+                                             int clip_lo, int clip_hi) {
+  float Lh, Ll;
+  if (LOG) {
+    float2 l = slut[u < (uint32_t)kLutLds ? u : 0u];
+    if (u >= (uint32_t)kLutLds) l = glut[u];
+    Lh = l.x;
+    Ll = l.y;
+  } else {
+    Lh = (float)u;
+    Ll = 0.0f;
+  }
+  const float d = (Lh - c.x) + (Ll - c.y);       // (img - mean)
+  const float t = fmaf(d, c.z, mh) + ml;          // * mean(std)/std + mean(mean)
+  const float o = LOG ? exp2f(t * kLog2_10) : t;  // 10 ** t
+  // numpy float64 -> uint astype on x86: trunc to int32 (out of range/NaN ->
+  // INT32_MIN), keep the low bits (image.py:631)
+  const int32_t iv = (o >= -2147483648.0f && o < 2147483648.0f) ? (int32_t)o : INT32_MIN;
+  uint32_t r = (uint32_t)iv & ((1u << BITS) - 1u);
+  if (clip_lo >= 0) {
+    r = r < (uint32_t)clip_lo ? (uint32_t)clip_lo : r;
+    r = r > (uint32_t)clip_hi ? (uint32_t)clip_hi : r;
+  }
+  return r;
+}
+
+constexpr int kCorrThreads = 256;
+constexpr int kCorrUnroll = 4;
+
+template <bool LOG>
+__global__ __launch_bounds__(kCorrThreads) void k_correct_u16_vec8(
+    const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
+    const float4* __restrict__ coef, const float2* __restrict__ lut,
+    const float2* __restrict__ mconst, int clip_lo, int clip_hi) {
+  __shared__ float2 slut[kLutLds];
+  if (LOG)
+    for (int i = threadIdx.x; i < kLutLds; i += kCorrThreads) slut[i] = lut[i];
+  __syncthreads();
+  const int64_t ngroups = npx >> 3;
+  const int64_t g = (int64_t)blockIdx.x * kCorrThreads + threadIdx.x;
+  if (g >= ngroups) return;
+  const float2 m = mconst[0];
+  float4 c[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) c[k] = coef[g * 8 + k];
+  const uint4* src = reinterpret_cast<const uint4*>(in) + g;
+  uint4* dst = reinterpret_cast<uint4*>(out) + g;
+  auto one = [&](const uint4 v) -> uint4 {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t lo =
+          correct1<LOG, 16>(w[k] & 0xFFFFu, c[2 * k], slut, lut, m.x, m.y, clip_lo, clip_hi);
+      const uint32_t hi =
+          correct1<LOG, 16>(w[k] >> 16, c[2 * k + 1], slut, lut, m.x, m.y, clip_lo, clip_hi);
+      o[k] = lo | (hi << 16);
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+  };
+  int64_t s = 0;
+  for (; s + kCorrUnroll <= n_sites; s += kCorrUnroll) {
+    uint4 v[kCorrUnroll];
+#pragma unroll
+    for (int k = 0; k < kCorrUnroll; ++k) v[k] = src[(s + k) * ngroups];
+#pragma unroll
+    for (int k = 0; k < kCorrUnroll; ++k) dst[(s + k) * ngroups] = one(v[k]);
+  }
+  for (; s < n_sites; ++s) dst[s * ngroups] = one(src[s * ngroups]);
+}
+
+template <bool LOG, typename T, int BITS>
+__global__ __launch_bounds__(kCorrThreads) void k_correct_scalar(
+    const T* __restrict__ in, T* __restrict__ out, int64_t npx, int64_t n_sites,
+    const float4* __restrict__ coef, const float2* __restrict__ lut,
+    const float2* __restrict__ mconst, int clip_lo, int clip_hi) {
+  __shared__ float2 slut[kLutLds];
+  if (LOG)
+    for (int i = threadIdx.x; i < kLutLds; i += kCorrThreads) slut[i] = lut[i];
+  __syncthreads();
+  const int64_t p = (int64_t)blockIdx.x * kCorrThreads + threadIdx.x;
+  if (p >= npx) return;
+  const float2 m = mconst[0];
+  const float4 c = coef[p];
+  for (int64_t s = 0; s < n_sites; ++s)
+    out[s * npx + p] =
+        (T)correct1<LOG, BITS>(in[s * npx + p], c, slut, lut, m.x, m.y, clip_lo, clip_hi);
+}
+
+void launch_correct_u16(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
+                        const float4* coef, const float2* lut, const float2* mconst,
+                        int log_transform, int clip_lo, int clip_hi, hipStream_t s) {
+  if (n_sites <= 0) return;
+  ProfScope prof("correct", s);
+  const bool vec = (npx & 7) == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  if (vec) {
+    const dim3 grid((unsigned)cdiv(npx >> 3, kCorrThreads));
+    if (log_transform)
+      hipLaunchKernelGGL(k_correct_u16_vec8<true>, grid, dim3(kCorrThreads), 0, s, in, out, npx,
+                         n_sites, coef, lut, mconst, clip_lo, clip_hi);
+    else
+      hipLaunchKernelGGL(k_correct_u16_vec8<false>, grid, dim3(kCorrThreads), 0, s, in, out, npx,
+                         n_sites, coef, lut, mconst, clip_lo, clip_hi);
+  } else {
+    const dim3 grid((unsigned)cdiv(npx, kCorrThreads));
+    if (log_transform)
+      hipLaunchKernelGGL((k_correct_scalar<true, uint16_t, 16>), grid, dim3(kCorrThreads), 0, s, in,
+                         out, npx, n_sites, coef, lut, mconst, clip_lo, clip_hi);
+    else
+      hipLaunchKernelGGL((k_correct_scalar<false, uint16_t, 16>), grid, dim3(kCorrThreads), 0, s,
+                         in, out, npx, n_sites, coef, lut, mconst, clip_lo, clip_hi);
+  }
+  TMH_HIP(hipGetLastError());
+}
+
+void launch_correct_u8(const uint8_t* in, uint8_t* out, int64_t npx, int64_t n_sites,
+                       const float4* coef, const float2* lut, const float2* mconst,
+                       int log_transform, int clip_lo, int clip_hi, hipStream_t s) {
+  if (n_sites <= 0) return;
+  ProfScope prof("correct_u8", s);
+  const dim3 grid((unsigned)cdiv(npx, kCorrThreads));
+  if (log_transform)
+    hipLaunchKernelGGL((k_correct_scalar<true, uint8_t, 8>), grid, dim3(kCorrThreads), 0, s, in,
+                       out, npx, n_sites, coef, lut, mconst, clip_lo, clip_hi);
+  else
+    hipLaunchKernelGGL((k_correct_scalar<false, uint8_t, 8>), grid, dim3(kCorrThreads), 0, s, in,
+                       out, npx, n_sites, coef, lut, mconst, clip_lo, clip_hi);
+  TMH_HIP(hipGetLastError());
+}
+
+__global__ void k_clip_u16(const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t n,
+                           int lo, int hi) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int v = in[i];
+  v = v < lo ? lo : v;
+  v = v > hi ? hi : v;
+  out[i] = (uint16_t)v;
+}
+
+void launch_clip_u16(const uint16_t* in, uint16_t* out, int64_t n, int lo, int hi, hipStream_t s) {
+  hipLaunchKernelGGL(k_clip_u16, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, in, out, n, lo, hi);
+  TMH_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// synthetic sites on device (SURVEY.md §8(d) distribution; counter-based)
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_synth(uint16_t* __restrict__ out, int H, int W,
+                                               uint64_t key, int64_t first_site) {
+  const int64_t npx = (int64_t)H * W;
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t s = blockIdx.y;
+  if (p >= npx) return;
+  const uint64_t z1 = splitmix64(key ^ splitmix64((uint64_t)(first_site + s)) ^ (uint64_t)p);
+  const uint64_t z2 = splitmix64(z1);
+  const float u1 = ((float)(z1 >> 40) + 0.5f) * (1.0f / 16777216.0f);
+  const float u2 = (float)((z1 >> 16) & 0xFFFFFFu) * (1.0f / 16777216.0f);
+  const float u3 = (float)(z2 >> 40) * (1.0f / 16777216.0f);
+  const float rr = sqrtf(-2.0f * logf(u1));
+  const float n1 = rr * cospif(2.0f * u2), n2 = rr * sinpif(2.0f * u2);
+  const int y = (int)(p / W), x = (int)(p % W);
+  const float fy = (y - (H - 1) * 0.5f) / fmaxf(H * 0.5f, 1.0f);
+  const float fx = (x - (W - 1) * 0.5f) / fmaxf(W * 0.5f, 1.0f);
+  const float illum = expf(-1.5f * 0.5f * (fy * fy + fx * fx));
+  float v = 100.0f + illum * expf(6.0f + 0.6f * n1) + 5.0f * n2;
+  v = fminf(fmaxf(rintf(v), 0.0f), 65535.0f);
+  if (u3 < 1e-4f) v = 0.0f;
+  if (u3 > 1.0f - 1e-4f) v = 65535.0f;
+  out[s * npx + p] = (uint16_t)v;
+}
+
+void launch_synth(uint16_t* out, int64_t n_sites, int H, int W, uint64_t seed, int channel,
+                  int64_t first_site, hipStream_t s) {
+  const int64_t npx = (int64_t)H * W;
+  const uint64_t key = seed * 0x100000001B3ull ^ ((uint64_t)channel << 56);
+  for (int64_t s0 = 0; s0 < n_sites; s0 += 65535) {
+    const int64_t ns = (n_sites - s0 < 65535) ? n_sites - s0 : 65535;
+    hipLaunchKernelGGL(k_synth, dim3((unsigned)cdiv(npx, 256), (unsigned)ns), dim3(256), 0, s,
+                       out + s0 * npx, H, W, key, first_site + s0);
+  }
+  TMH_HIP(hipGetLastError());
+}
+
+}  // namespace tmh

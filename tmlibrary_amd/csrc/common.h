@@ -1,0 +1,90 @@
+// Shared definitions for libtmhip (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/tmhip.h"
+
+namespace tmh {
+
+// error plumbing --------------------------------------------------------------
+void set_error(const std::string& msg);
+
+struct Error {
+  int code;
+  std::string msg;
+};
+
+#define TMH_HIP(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      throw ::tmh::Error{TMH_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)}; \
+  } while (0)
+
+#define TMH_CHECK(cond, code, msg)                         \
+  do {                                                     \
+    if (!(cond)) throw ::tmh::Error{(code), (msg)};        \
+  } while (0)
+
+// kernel timing (bench/roofline support) ----------------------------------------
+// When enabled, every launch of a named kernel is bracketed by a pair of HIP
+// events on the stream it runs on; tmh_profile_read sums their durations.
+struct ProfScope {
+  ProfScope(const char* name, hipStream_t s);
+  ~ProfScope();
+  const char* name_;
+  hipStream_t s_;
+  void* slot_;
+};
+
+// histogram geometry ------------------------------------------------------------
+constexpr int kBins = 65536;      // all uint16 values
+constexpr int kLdsBins = 32768;   // bins [0, kLdsBins) counted in LDS (u32)
+constexpr int kHiBins = kBins - kLdsBins;  // counted with global atomics
+constexpr int kHistThreads = 1024;
+constexpr int kBinsPerThread = kBins / kHistThreads;  // 64
+
+// log10 LUT entries staged in LDS by the per-pixel kernels (f64 / f32x2): 32 KB
+constexpr int kLutLds = 4096;
+
+// launches (defined in the .hip files) -------------------------------------------
+void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0,
+                    double* mean, double* m2, const double* lut, hipStream_t s);
+void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
+                         const int32_t* q_lo, const int32_t* q_hi, int Q, double scale,
+                         uint16_t* vlo, uint16_t* vhi, unsigned long long* pooled,
+                         int64_t* zero_counts, uint32_t* site_hist, hipStream_t s);
+void launch_pct_accumulate(const uint16_t* vlo, const uint16_t* vhi, int64_t n_sites, int Q,
+                           const double* gamma, double* acc, hipStream_t s);
+void launch_finalize(const double* mean, const double* m2, int64_t n, int64_t npx, double* out_mean,
+                     double* out_std, hipStream_t s);
+void launch_merge1(const double* mean, int64_t n, int64_t npx, double* nmean, hipStream_t s);
+void launch_merge2(double* mean, const double* m2, int64_t n_r, const double* sum_nmean,
+                   int64_t n_total, int64_t npx, double* m2c, hipStream_t s);
+void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s);
+
+void launch_smooth(const double* in, double* out, double* tmp, int H, int W, const double* d_w,
+                   int radius, hipStream_t s);
+void launch_reduce_sum(const double* x, int64_t n, double* partial, int n_partial, double* out,
+                       hipStream_t s);
+void launch_build_corr_lut(float2* lut, int log_transform, double zero_log10, hipStream_t s);
+void launch_coeffs(const double* mean, const double* std, const double* sums, int64_t npx,
+                   float4* coef, float2* mconst, hipStream_t s);
+void launch_correct_u16(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
+                        const float4* coef, const float2* lut, const float2* mconst,
+                        int log_transform, int clip_lo, int clip_hi, hipStream_t s);
+void launch_correct_u8(const uint8_t* in, uint8_t* out, int64_t npx, int64_t n_sites,
+                       const float4* coef, const float2* lut, const float2* mconst,
+                       int log_transform, int clip_lo, int clip_hi, hipStream_t s);
+void launch_clip_u16(const uint16_t* in, uint16_t* out, int64_t n, int lo, int hi, hipStream_t s);
+void launch_synth(uint16_t* out, int64_t n_sites, int H, int W, uint64_t seed, int channel,
+                  int64_t first_site, hipStream_t s);
+
+__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace tmh

@@ -1,0 +1,447 @@
+// Illumination-statistics kernels for gfx950 (MI355X).
+//
+// Reference: tmlib/workflow/corilla/stats.py:64-121 (OnlineStatistics.update,
+// var/mean/std/percentiles).  Two passes over the resident site images:
+//
+//   k_welford_*      pixel-major: each thread owns 8 pixels and walks the
+//                    sites in order, keeping (mean, M2) in f64 registers
+//                    (stats.py:89-92) — state is read/written once per launch,
+//                    so HBM traffic is the 2 B/px of the sites.  log10 comes
+//                    from the host-numpy LUT (stats.py:79-85), first 4096
+//                    entries staged in LDS.
+//   k_hist_scatter   site-major: one 1024-thread workgroup per site builds the
+//                    exact 65,536-bin histogram (bins < 32768 in LDS, the rest
+//                    with global atomics into a zero-maintained per-site
+//                    slab), scans it, and scatters the value at every
+//                    percentile's previous/next sorted position (np.percentile
+//                    linear, stats.py:76) as u16.
+//   k_pct_acc        thread per quantile: folds each site's interpolated
+//                    percentile into the f64 accumulator in SITE ORDER, without
+//                    FMA, so the sum is bit-identical to the reference's
+//                    sequential `_percentiles +=`.
+#include "common.h"
+
+namespace tmh {
+
+// ---------------------------------------------------------------------------
+// Welford
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ double lut_f64(const double* slut, const double* __restrict__ glut,
+                                          uint32_t u) {
+  double x = slut[u < (uint32_t)kLutLds ? u : 0u];
+  if (u >= (uint32_t)kLutLds) x = glut[u];
+  return x;
+}
+
+__device__ __forceinline__ void welford1(double x, double rn, double& mu, double& m2) {
+  const double d = x - mu;
+  mu = fma(d, rn, mu);          // mean + delta / n
+  m2 = fma(d, x - mu, m2);      // M2 + delta * (x - mean_new)
+}
+
+__device__ __forceinline__ void welford8(const uint4 v, double rn, double (&mu)[8],
+                                         double (&m2)[8], const double* slut,
+                                         const double* __restrict__ glut) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    welford1(lut_f64(slut, glut, w[k] & 0xFFFFu), rn, mu[2 * k], m2[2 * k]);
+    welford1(lut_f64(slut, glut, w[k] >> 16), rn, mu[2 * k + 1], m2[2 * k + 1]);
+  }
+}
+
+constexpr int kWfThreads = 256;
+constexpr int kWfUnroll = 4;
+
+__global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
+    const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites, int64_t n0,
+    double* __restrict__ mean, double* __restrict__ m2, const double* __restrict__ lut) {
+  __shared__ double slut[kLutLds];
+  for (int i = threadIdx.x; i < kLutLds; i += kWfThreads) slut[i] = lut[i];
+  __syncthreads();
+  const int64_t ngroups = npx >> 3;
+  const int64_t g = (int64_t)blockIdx.x * kWfThreads + threadIdx.x;
+  if (g >= ngroups) return;
+
+  double mu[8], q[8];
+  const double2* pm = reinterpret_cast<const double2*>(mean) + g * 4;
+  const double2* pq = reinterpret_cast<const double2*>(m2) + g * 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double2 a = pm[k], b = pq[k];
+    mu[2 * k] = a.x; mu[2 * k + 1] = a.y;
+    q[2 * k] = b.x; q[2 * k + 1] = b.y;
+  }
+  const uint4* src = reinterpret_cast<const uint4*>(sites) + g;
+  int64_t s = 0;
+  for (; s + kWfUnroll <= n_sites; s += kWfUnroll) {
+    uint4 v[kWfUnroll];
+#pragma unroll
+    for (int k = 0; k < kWfUnroll; ++k) v[k] = src[(s + k) * ngroups];
+#pragma unroll
+    for (int k = 0; k < kWfUnroll; ++k)
+      welford8(v[k], 1.0 / (double)(n0 + s + k + 1), mu, q, slut, lut);
+  }
+  for (; s < n_sites; ++s) welford8(src[s * ngroups], 1.0 / (double)(n0 + s + 1), mu, q, slut, lut);
+
+  double2* om = reinterpret_cast<double2*>(mean) + g * 4;
+  double2* oq = reinterpret_cast<double2*>(m2) + g * 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    om[k] = make_double2(mu[2 * k], mu[2 * k + 1]);
+    oq[k] = make_double2(q[2 * k], q[2 * k + 1]);
+  }
+}
+
+// Any shape (npx % 8 != 0 leaves sites unaligned for 16-B loads): 1 px/thread.
+__global__ __launch_bounds__(kWfThreads) void k_welford_scalar(
+    const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites, int64_t n0,
+    double* __restrict__ mean, double* __restrict__ m2, const double* __restrict__ lut) {
+  __shared__ double slut[kLutLds];
+  for (int i = threadIdx.x; i < kLutLds; i += kWfThreads) slut[i] = lut[i];
+  __syncthreads();
+  const int64_t p = (int64_t)blockIdx.x * kWfThreads + threadIdx.x;
+  if (p >= npx) return;
+  double mu = mean[p], q = m2[p];
+  for (int64_t s = 0; s < n_sites; ++s)
+    welford1(lut_f64(slut, lut, sites[s * npx + p]), 1.0 / (double)(n0 + s + 1), mu, q);
+  mean[p] = mu;
+  m2[p] = q;
+}
+
+void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* mean,
+                    double* m2, const double* lut, hipStream_t s) {
+  if (n_sites <= 0) return;
+  ProfScope prof("welford", s);
+  if ((npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0) {
+    const int64_t grid = cdiv(npx >> 3, kWfThreads);
+    hipLaunchKernelGGL(k_welford_vec8, dim3((unsigned)grid), dim3(kWfThreads), 0, s, sites, npx,
+                       n_sites, n0, mean, m2, lut);
+  } else {
+    const int64_t grid = cdiv(npx, kWfThreads);
+    hipLaunchKernelGGL(k_welford_scalar, dim3((unsigned)grid), dim3(kWfThreads), 0, s, sites, npx,
+                       n_sites, n0, mean, m2, lut);
+  }
+  TMH_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// per-site histogram + percentile order statistics
+// ---------------------------------------------------------------------------
+
+// LDS bin address: rotate within each 64-bin group so that thread t reading
+// bin 64t+j (j fixed across the wave) hits bank (j+t)%32: conflict-free scan.
+__device__ __forceinline__ uint32_t bin_slot(uint32_t u) {
+  return (u & ~63u) | ((u + (u >> 6)) & 63u);
+}
+
+__device__ __forceinline__ void count1(uint32_t u, uint32_t* bins, uint32_t* himask,
+                                       uint32_t* __restrict__ hhi) {
+  if (u < (uint32_t)kLdsBins) {
+    atomicAdd(&bins[bin_slot(u)], 1u);
+  } else {
+    const uint32_t h = u - kLdsBins;
+    atomicAdd(&hhi[h], 1u);
+    atomicOr(&himask[h >> 11], 1u << ((h >> 6) & 31u));
+  }
+}
+
+__device__ __forceinline__ void count8(const uint4 v, uint32_t* bins, uint32_t* himask,
+                                       uint32_t* __restrict__ hhi) {
+  count1(v.x & 0xFFFFu, bins, himask, hhi);
+  count1(v.x >> 16, bins, himask, hhi);
+  count1(v.y & 0xFFFFu, bins, himask, hhi);
+  count1(v.y >> 16, bins, himask, hhi);
+  count1(v.z & 0xFFFFu, bins, himask, hhi);
+  count1(v.z >> 16, bins, himask, hhi);
+  count1(v.w & 0xFFFFu, bins, himask, hhi);
+  count1(v.w >> 16, bins, himask, hhi);
+}
+
+// smallest q in [0, Q] with tab[q] >= r (tab non-decreasing, ~linear in q)
+__device__ __forceinline__ int64_t first_q(const int32_t* __restrict__ tab, int Q, double scale,
+                                           int64_t r) {
+  int64_t q = (int64_t)((double)r * scale);
+  if (q > Q) q = Q;
+  if (q < 0) q = 0;
+  while (q > 0 && tab[q - 1] >= r) --q;
+  while (q < Q && tab[q] < r) ++q;
+  return q;
+}
+
+// Writes value b at every quantile whose previous (vlo) / next (vhi) sorted
+// position lies in [start, end).  Kept out of line: it runs only for
+// non-empty bins, and inlining it 64x would bloat the scan loop.
+__device__ __noinline__ void scatter_bin(uint32_t b, int64_t start, int64_t end,
+                                         const int32_t* __restrict__ q_lo,
+                                         const int32_t* __restrict__ q_hi, int Q, double scale,
+                                         uint16_t* __restrict__ vlo, uint16_t* __restrict__ vhi) {
+  const uint16_t v = (uint16_t)b;
+  for (int64_t q = first_q(q_lo, Q, scale, start), q1 = first_q(q_lo, Q, scale, end); q < q1; ++q)
+    vlo[q] = v;
+  for (int64_t q = first_q(q_hi, Q, scale, start), q1 = first_q(q_hi, Q, scale, end); q < q1; ++q)
+    vhi[q] = v;
+}
+
+__global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
+    const uint16_t* __restrict__ sites, int64_t npx, int vec, uint32_t* __restrict__ hist_hi,
+    const int32_t* __restrict__ q_lo, const int32_t* __restrict__ q_hi, int Q, double scale,
+    uint16_t* __restrict__ vlo_all, uint16_t* __restrict__ vhi_all,
+    unsigned long long* __restrict__ pooled, int64_t* __restrict__ zero_counts,
+    uint32_t* __restrict__ site_hist) {
+  __shared__ __attribute__((aligned(16))) uint32_t bins[kLdsBins];
+  __shared__ uint32_t himask[16];
+  __shared__ uint32_t wsum[16];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int64_t s = blockIdx.x;
+
+  for (int i = tid; i < kLdsBins / 4; i += kHistThreads)
+    reinterpret_cast<uint4*>(bins)[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (tid < 16) himask[tid] = 0u;
+  __syncthreads();
+
+  const uint16_t* site = sites + s * npx;
+  uint32_t* hhi = hist_hi + s * (int64_t)kHiBins;
+  if (vec) {
+    const uint4* src = reinterpret_cast<const uint4*>(site);
+    const int64_t n16 = npx >> 3;
+    int64_t i = tid;
+    for (; i + 3 * kHistThreads < n16; i += 4 * kHistThreads) {
+      const uint4 v0 = src[i], v1 = src[i + kHistThreads], v2 = src[i + 2 * kHistThreads],
+                  v3 = src[i + 3 * kHistThreads];
+      count8(v0, bins, himask, hhi);
+      count8(v1, bins, himask, hhi);
+      count8(v2, bins, himask, hhi);
+      count8(v3, bins, himask, hhi);
+    }
+    for (; i < n16; i += kHistThreads) count8(src[i], bins, himask, hhi);
+  } else {
+    for (int64_t i = tid; i < npx; i += kHistThreads) count1(site[i], bins, himask, hhi);
+  }
+  // __syncthreads() orders LDS only: the global atomics into the slab must
+  // have been performed before other waves swap the slab out below.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // thread t owns bins [64t, 64t+64): read them into registers
+  uint32_t cnt[kBinsPerThread];
+  if (tid < kLdsBins / kBinsPerThread) {
+    const uint32_t base = (uint32_t)tid * kBinsPerThread;
+#pragma unroll
+    for (int j = 0; j < kBinsPerThread; ++j) cnt[j] = bins[base + ((j + tid) & 63)];
+  } else {
+    const uint32_t c = (uint32_t)tid - kLdsBins / kBinsPerThread;
+    const bool touched = (himask[c >> 5] >> (c & 31u)) & 1u;
+    if (touched) {
+#pragma unroll
+      for (int j = 0; j < kBinsPerThread; ++j) cnt[j] = atomicExch(&hhi[c * kBinsPerThread + j], 0u);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kBinsPerThread; ++j) cnt[j] = 0u;
+    }
+  }
+  uint32_t tot = 0;
+#pragma unroll
+  for (int j = 0; j < kBinsPerThread; ++j) tot += cnt[j];
+
+  // exclusive scan of per-thread totals over the workgroup
+  uint32_t incl = tot;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  __syncthreads();
+  uint32_t woff = 0;
+  for (int w = 0; w < wid; ++w) woff += wsum[w];
+  const int64_t base_rank = (int64_t)woff + incl - tot;
+
+  const uint32_t b0 = (uint32_t)tid * kBinsPerThread;
+  if (tid == 0 && zero_counts) zero_counts[s] = cnt[0];
+  if (site_hist) {
+#pragma unroll
+    for (int j = 0; j < kBinsPerThread; ++j) site_hist[s * kBins + b0 + j] = cnt[j];
+  }
+  uint16_t* vlo = vlo_all + s * (int64_t)Q;
+  uint16_t* vhi = vhi_all + s * (int64_t)Q;
+  int64_t r = base_rank;
+#pragma unroll
+  for (int j = 0; j < kBinsPerThread; ++j) {
+    const uint32_t c = cnt[j];
+    if (c) {
+      atomicAdd(&pooled[b0 + j], (unsigned long long)c);
+      scatter_bin(b0 + j, r, r + c, q_lo, q_hi, Q, scale, vlo, vhi);
+      r += c;
+    }
+  }
+}
+
+void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
+                         const int32_t* q_lo, const int32_t* q_hi, int Q, double scale,
+                         uint16_t* vlo, uint16_t* vhi, unsigned long long* pooled,
+                         int64_t* zero_counts, uint32_t* site_hist, hipStream_t s) {
+  if (n_sites <= 0) return;
+  ProfScope prof("hist", s);
+  const int vec = ((npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0) ? 1 : 0;
+  hipLaunchKernelGGL(k_hist_scatter, dim3((unsigned)n_sites), dim3(kHistThreads), 0, s, sites, npx,
+                     vec, hist_hi, q_lo, q_hi, Q, scale, vlo, vhi, pooled, zero_counts, site_hist);
+  TMH_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// sequential percentile accumulation
+// ---------------------------------------------------------------------------
+
+// numpy 2.2.6 _lerp on the two order statistics, f64, no contraction:
+//   a + (b-a)*g, or b - (b-a)*(1-g) where g >= 0.5.  Plain operators under a
+// scoped fp-contract(off) (built with -ffp-contract=fast-honor-pragmas); the
+// HIP __dmul_rn/__dadd_rn helpers are header code compiled with contraction
+// on and would still fuse into one v_fma_f64 (1-ulp drift vs numpy).
+__device__ __forceinline__ double lerp_np(uint32_t a, uint32_t b, double g) {
+#pragma clang fp contract(off)
+  const double d = (double)(b - a);
+  return (g >= 0.5) ? (double)b - d * (1.0 - g) : (double)a + d * g;
+}
+
+__device__ __forceinline__ double add_nc(double x, double y) {
+#pragma clang fp contract(off)
+  return x + y;
+}
+
+constexpr int kPctThreads = 256;
+constexpr int kPctUnroll = 8;
+
+// each thread: two consecutive quantiles (one u32 load of each u16 array)
+__global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint16_t* __restrict__ vlo,
+                                                          const uint16_t* __restrict__ vhi,
+                                                          int64_t n_sites, int Q,
+                                                          const double* __restrict__ gamma,
+                                                          double* __restrict__ acc) {
+  const int q0 = ((int)blockIdx.x * kPctThreads + threadIdx.x) * 2;
+  if (q0 >= Q) return;
+  const bool two = q0 + 1 < Q;
+  const double g0 = gamma[q0], g1 = two ? gamma[q0 + 1] : 0.0;
+  double a0 = acc[q0], a1 = two ? acc[q0 + 1] : 0.0;
+  const int64_t stride = Q / 2;  // u32 per site (Q even on this path)
+  const uint32_t* pl = reinterpret_cast<const uint32_t*>(vlo) + q0 / 2;
+  const uint32_t* ph = reinterpret_cast<const uint32_t*>(vhi) + q0 / 2;
+  int64_t s = 0;
+  for (; s + kPctUnroll <= n_sites; s += kPctUnroll) {
+    uint32_t l[kPctUnroll], h[kPctUnroll];
+#pragma unroll
+    for (int k = 0; k < kPctUnroll; ++k) {
+      l[k] = pl[(s + k) * stride];
+      h[k] = ph[(s + k) * stride];
+    }
+#pragma unroll
+    for (int k = 0; k < kPctUnroll; ++k) {
+      a0 = add_nc(a0, lerp_np(l[k] & 0xFFFFu, h[k] & 0xFFFFu, g0));
+      a1 = add_nc(a1, lerp_np(l[k] >> 16, h[k] >> 16, g1));
+    }
+  }
+  for (; s < n_sites; ++s) {
+    const uint32_t l = pl[s * stride], h = ph[s * stride];
+    a0 = add_nc(a0, lerp_np(l & 0xFFFFu, h & 0xFFFFu, g0));
+    a1 = add_nc(a1, lerp_np(l >> 16, h >> 16, g1));
+  }
+  acc[q0] = a0;
+  if (two) acc[q0 + 1] = a1;
+}
+
+__global__ __launch_bounds__(kPctThreads) void k_pct_acc_odd(const uint16_t* __restrict__ vlo,
+                                                              const uint16_t* __restrict__ vhi,
+                                                              int64_t n_sites, int Q,
+                                                              const double* __restrict__ gamma,
+                                                              double* __restrict__ acc) {
+  const int q = (int)blockIdx.x * kPctThreads + threadIdx.x;
+  if (q >= Q) return;
+  const double g = gamma[q];
+  double a = acc[q];
+  for (int64_t s = 0; s < n_sites; ++s) a = add_nc(a, lerp_np(vlo[s * Q + q], vhi[s * Q + q], g));
+  acc[q] = a;
+}
+
+void launch_pct_accumulate(const uint16_t* vlo, const uint16_t* vhi, int64_t n_sites, int Q,
+                           const double* gamma, double* acc, hipStream_t s) {
+  if (n_sites <= 0) return;
+  ProfScope prof("pct_acc", s);
+  if ((Q & 1) == 0) {
+    const int grid = (int)cdiv(Q / 2, kPctThreads);
+    hipLaunchKernelGGL(k_pct_acc, dim3(grid), dim3(kPctThreads), 0, s, vlo, vhi, n_sites, Q, gamma,
+                       acc);
+  } else {
+    const int grid = (int)cdiv(Q, kPctThreads);
+    hipLaunchKernelGGL(k_pct_acc_odd, dim3(grid), dim3(kPctThreads), 0, s, vlo, vhi, n_sites, Q,
+                       gamma, acc);
+  }
+  TMH_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// finalize (stats.py:94-112) and multi-rank merge
+// ---------------------------------------------------------------------------
+
+__global__ void k_finalize(const double* __restrict__ mean, const double* __restrict__ m2, int64_t n,
+                           int64_t npx, double* __restrict__ out_mean, double* __restrict__ out_std) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npx) return;
+  if (out_mean) out_mean[i] = mean[i];
+  if (out_std) out_std[i] = (n < 2) ? __builtin_nan("") : sqrt(m2[i] / (double)(n - 1));
+}
+
+void launch_finalize(const double* mean, const double* m2, int64_t n, int64_t npx, double* out_mean,
+                     double* out_std, hipStream_t s) {
+  ProfScope prof("finalize", s);
+  hipLaunchKernelGGL(k_finalize, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, mean, m2, n, npx,
+                     out_mean, out_std);
+  TMH_HIP(hipGetLastError());
+}
+
+__global__ void k_merge1(const double* __restrict__ mean, double nr, int64_t npx,
+                         double* __restrict__ nmean) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < npx) nmean[i] = nr * mean[i];
+}
+
+// Chan et al. pairwise combine, expressed as two sums so that one RCCL
+// all-reduce per quantity merges any number of ranks:
+//   mean = sum_r n_r mean_r / n,  M2 = sum_r [M2_r + n_r (mean_r - mean)^2]
+__global__ void k_merge2(double* __restrict__ mean, const double* __restrict__ m2, double nr,
+                         const double* __restrict__ sum_nmean, double n_total, int64_t npx,
+                         double* __restrict__ m2c) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npx) return;
+  const double mu = sum_nmean[i] / n_total;
+  const double d = mean[i] - mu;
+  m2c[i] = m2[i] + nr * d * d;
+  mean[i] = mu;
+}
+
+void launch_merge1(const double* mean, int64_t n, int64_t npx, double* nmean, hipStream_t s) {
+  hipLaunchKernelGGL(k_merge1, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, mean, (double)n,
+                     npx, nmean);
+  TMH_HIP(hipGetLastError());
+}
+
+void launch_merge2(double* mean, const double* m2, int64_t n_r, const double* sum_nmean,
+                   int64_t n_total, int64_t npx, double* m2c, hipStream_t s) {
+  hipLaunchKernelGGL(k_merge2, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, mean, m2,
+                     (double)n_r, sum_nmean, (double)n_total, npx, m2c);
+  TMH_HIP(hipGetLastError());
+}
+
+__global__ void k_copy_f64(const double* __restrict__ src, double* __restrict__ dst, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
+void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_copy_f64, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, src, dst, n);
+  TMH_HIP(hipGetLastError());
+}
+
+}  // namespace tmh

@@ -1,0 +1,308 @@
+"""Image classes of the illumination-correction path, computed on MI355X.
+
+Mirrors the hot-path subset of tmlib/image.py:
+  ``Image``                (:35-311; array/metadata checks, ``smooth`` :287-311)
+  ``ChannelImage``         (:455-670; ``clip`` :570-597,
+                            ``_correct_illumination`` :599-631, ``correct`` :633-670)
+  ``IllumstatsImage``      (:1097-1136)
+  ``IllumstatsContainer``  (:1139-1213; ``smooth`` :1172-1193,
+                            ``get_closest_percentile`` :1195-1213)
+
+Smoothing, correction and clipping run in libtmhip.so (no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import hip
+from .metadata import ImageMetadata, IllumstatsImageMetadata
+
+#: np.log10(1e-10) on this host: the log of a zero pixel in the correction
+#: (image.py:624-626 replaces 0 by 10**-10 before the log10)
+ZERO_LOG10 = float(np.log10(np.float64(10 ** -10)))
+
+
+class Image(object):
+    """2-D pixel array + optional metadata (tmlib/image.py:35-311)."""
+
+    __slots__ = ("_array", "_metadata")
+
+    def __init__(self, array, metadata=None):
+        self.array = array
+        self.metadata = metadata
+
+    @property
+    def metadata(self):
+        return self._metadata
+
+    @metadata.setter
+    def metadata(self, value):
+        if value is not None and not isinstance(value, ImageMetadata):
+            raise TypeError('Argument "metadata" must have type tmlib.metadata.ImageMetadata.')
+        self._metadata = value
+
+    @property
+    def array(self):
+        return self._array
+
+    @array.setter
+    def array(self, value):
+        if not isinstance(value, np.ndarray):
+            raise TypeError('Argument "array" must have type numpy.ndarray.')
+        if value.ndim != 2:
+            raise ValueError('Argument "array" must be two dimensional.')
+        self._array = value
+
+    @property
+    def dimensions(self):
+        return self.array.shape
+
+    @property
+    def dtype(self):
+        return self.array.dtype
+
+    @property
+    def is_int(self):
+        return issubclass(self.array.dtype.type, np.integer)
+
+    @property
+    def is_float(self):
+        return issubclass(self.array.dtype.type, np.floating)
+
+    @property
+    def is_uint(self):
+        return issubclass(self.array.dtype.type, np.unsignedinteger)
+
+    @property
+    def is_uint8(self):
+        return self.array.dtype == np.uint8
+
+    @property
+    def is_uint16(self):
+        return self.array.dtype == np.uint16
+
+    def smooth(self, sigma, inplace=True):
+        """Gaussian smoothing (image.py:287-311 -> mahotas.gaussian_filter),
+        'reflect' border, radius int(4*sigma+0.5), float64, on the GPU."""
+        array = smooth_f64(self.array, sigma)
+        if inplace:
+            self.array = array
+            self.metadata.is_smoothed = True
+            return self
+        new_img = self.__class__(array, self.metadata)
+        new_img.metadata.is_smoothed = True
+        return new_img
+
+
+def smooth_f64(array: np.ndarray, sigma) -> np.ndarray:
+    L = hip.lib()
+    a = np.ascontiguousarray(array, dtype=np.float64)
+    if a.ndim != 2:
+        raise ValueError("smoothing needs a 2-D array")
+    out = np.empty_like(a)
+    hip.check(L.tmh_smooth_f64(hip.ptr(a), hip.ptr(out), a.shape[0], a.shape[1], float(sigma)))
+    return out
+
+
+class ChannelImage(Image):
+    """Grayscale uint8/uint16 site image (tmlib/image.py:455-670)."""
+
+    def __init__(self, array, metadata=None):
+        super(ChannelImage, self).__init__(array, metadata)
+        if not self.is_uint:
+            raise TypeError("Image must have unsigned integer type.")
+
+    @property
+    def array(self):
+        return self._array
+
+    @array.setter
+    def array(self, value):
+        if not isinstance(value, np.ndarray):
+            raise TypeError('Argument "array" must have type numpy.ndarray.')
+        if value.ndim != 2:
+            raise ValueError('Argument "array" must be two dimensional.')
+        if not (value.dtype == np.uint16 or value.dtype == np.uint8):
+            raise ValueError('Argument "array" must have numpy.uint8 or numpy.uint16 data type.')
+        self._array = value
+
+    def clip(self, lower, upper, inplace=True):
+        """np.clip of the pixels (image.py:570-597), on the GPU."""
+        array = clip_array(self.array, lower, upper)
+        if inplace:
+            self.array = array
+            self.metadata.is_clipped = True
+            return self
+        new_image = self.__class__(array, self.metadata)
+        new_image.metadata.is_clipped = True
+        return new_image
+
+    @staticmethod
+    def _correct_illumination(img, mean, std, log_transform=True):
+        """image.py:599-631: log10 -> z-score -> rescale by mean(std),
+        mean(mean) -> 10** -> cast to the input dtype (x86 astype rule)."""
+        corr = Corrector(mean, std, log_transform=log_transform)
+        try:
+            return corr.apply(img)
+        finally:
+            corr.close()
+
+    def correct(self, stats, inplace=True):
+        """image.py:633-670: correct with the container's (smoothed) stats."""
+        if not isinstance(stats, IllumstatsContainer):
+            raise TypeError('Argument "stats" must have type tmlib.image.IllumstatsContainer.')
+        if (stats.mean.metadata.channel_id != self.metadata.channel_id or
+                stats.std.metadata.channel_id != self.metadata.channel_id):
+            raise ValueError("Channels don't match!")
+        array = stats.corrector().apply(self.array)
+        if inplace:
+            self.array = array
+            self.metadata.is_corrected = True
+            return self
+        new_object = ChannelImage(array, self.metadata)
+        new_object.metadata.is_corrected = True
+        return new_object
+
+
+def clip_array(array: np.ndarray, lower, upper) -> np.ndarray:
+    info = np.iinfo(array.dtype)
+    for b in (lower, upper):
+        if not (info.min <= int(b) <= info.max):
+            raise OverflowError("Python integer %d out of bounds for %s" % (int(b), array.dtype))
+    L = hip.lib()
+    a = np.ascontiguousarray(array)
+    if a.dtype == np.uint8:
+        wide = a.astype(np.uint16)
+        out = np.empty_like(wide)
+        hip.check(L.tmh_clip_u16(hip.ptr(wide), hip.ptr(out), wide.size, int(lower), int(upper)))
+        return out.astype(np.uint8)
+    out = np.empty_like(a)
+    hip.check(L.tmh_clip_u16(hip.ptr(a), hip.ptr(out), a.size, int(lower), int(upper)))
+    return out
+
+
+class Corrector(object):
+    """Device-resident correction for one (mean, std) pair.
+
+    Holds tmh_corrector: per-pixel coefficients and the two global means
+    (np.mean(std), np.mean(mean), image.py:627) computed once, so a loop of
+    ``correct`` calls (illuminati/api.py:389-405) does not redo them.
+    """
+
+    def __init__(self, mean, std, log_transform=True):
+        L = hip.lib()
+        m = np.ascontiguousarray(mean, dtype=np.float64)
+        s = np.ascontiguousarray(std, dtype=np.float64)
+        if m.shape != s.shape or m.ndim != 2:
+            raise ValueError("mean and std must be 2-D arrays of the same shape")
+        self.shape = m.shape
+        self.log_transform = bool(log_transform)
+        h = C.c_void_p()
+        hip.check(L.tmh_corrector_create(hip.ptr(m), hip.ptr(s), m.shape[0], m.shape[1],
+                                         int(self.log_transform), ZERO_LOG10, C.byref(h)))
+        self._h = h
+
+    def means(self):
+        a, b = C.c_double(), C.c_double()
+        hip.check(hip.lib().tmh_corrector_means(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def apply(self, img: np.ndarray, clip=None) -> np.ndarray:
+        """Correct one image [H,W] or a stack [n,H,W] (uint8/uint16)."""
+        img = np.asarray(img)
+        if img.shape[-2:] != self.shape:
+            raise ValueError("operands could not be broadcast together with shapes %s %s"
+                             % (img.shape, self.shape))
+        a = np.ascontiguousarray(img)
+        out = np.empty_like(a)
+        n = 1 if a.ndim == 2 else int(np.prod(a.shape[:-2]))
+        lo, hi = (-1, -1) if clip is None else (int(clip[0]), int(clip[1]))
+        L = hip.lib()
+        if a.dtype == np.uint16:
+            hip.check(L.tmh_correct_u16(self._h, hip.ptr(a), hip.ptr(out), n, lo, hi))
+        elif a.dtype == np.uint8:
+            hip.check(L.tmh_correct_u8(self._h, hip.ptr(a), hip.ptr(out), n, lo, hi))
+        else:
+            raise TypeError("only uint8/uint16 images can be corrected")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            hip.lib().tmh_corrector_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class IllumstatsImage(Image):
+    """float64 statistics plane (tmlib/image.py:1097-1136)."""
+
+    def __init__(self, array, metadata=None):
+        if metadata is not None and not isinstance(metadata, IllumstatsImageMetadata):
+            raise TypeError('Argument "metadata" must have type '
+                            'tmlib.metadata.IllumstatsImageMetadata.')
+        super(IllumstatsImage, self).__init__(array, metadata)
+        if not self.is_float:
+            raise TypeError("Image must have data type float.")
+
+    @property
+    def array(self):
+        return self._array
+
+    @array.setter
+    def array(self, value):
+        if not isinstance(value, np.ndarray):
+            raise TypeError('Argument "array" must have type numpy.ndarray.')
+        if value.ndim != 2:
+            raise ValueError('Argument "array" must be two dimensional.')
+        if not value.dtype == np.float64:
+            raise ValueError('Argument "array" must have numpy.float data type.')
+        self._array = value
+
+
+class IllumstatsContainer(object):
+    """mean/std planes + percentile dict of one channel (tmlib/image.py:1139-1213)."""
+
+    def __init__(self, mean, std, percentiles):
+        if not isinstance(mean, IllumstatsImage):
+            raise TypeError('Argument "mean" must have type tmlib.image.IllumstatsImage.')
+        if not isinstance(std, IllumstatsImage):
+            raise TypeError('Argument "std" must have type tmlib.image.IllumstatsImage.')
+        self.mean = mean
+        self.std = std
+        self.percentiles = percentiles
+        self._corr = None
+        self._corr_key = None
+
+    def smooth(self, sigma=5):
+        """Gaussian-smooth mean and std in place (image.py:1172-1193)."""
+        self.mean.array = self.mean.smooth(sigma).array
+        self.mean.metadata.is_smoothed = True
+        self.std.array = self.std.smooth(sigma).array
+        self.std.metadata.is_smoothed = True
+        return self
+
+    def get_closest_percentile(self, value):
+        """Value of the percentile whose key is closest to ``value``; the first
+        key (in dict order) wins ties (image.py:1195-1213)."""
+        keys = np.array(list(self.percentiles.keys()))
+        idx = np.abs(keys - value).argmin()
+        return self.percentiles[keys[idx]]
+
+    def corrector(self, log_transform=True) -> Corrector:
+        """Cached device corrector for the current mean/std arrays (rebuilt
+        when either array object is replaced, e.g. by ``smooth``)."""
+        key = (id(self.mean.array), id(self.std.array), bool(log_transform))
+        if self._corr is None or self._corr_key != key:
+            if self._corr is not None:
+                self._corr.close()
+            self._corr = Corrector(self.mean.array, self.std.array, log_transform)
+            self._corr_key = key
+            self._corr_arrays = (self.mean.array, self.std.array)  # keep ids valid
+        return self._corr

@@ -1,0 +1,191 @@
+"""HDF5 files of the illumination path (no h5py, no database).
+
+Mirrors the storage half of tmlib/models/file.py with the on-disk layout
+unchanged:
+  ``ChannelImageFile``  (:207-379) ``/array`` u8/u16, gzip; ``get`` (:322-351),
+                        ``put`` (:353-363); FILENAME_FORMAT ``channel_image_file_{id}.h5``
+  ``IllumstatsFile``    (:383-472) ``/mean``, ``/std`` f64, ``/percentiles/keys`` f64,
+                        ``/percentiles/values`` i64; ``get`` smooths on read
+                        (:420-438), ``put`` (:440-456); FILENAME_FORMAT
+                        ``illumstats_file_{id}.h5``
+
+The SQLAlchemy/PostgreSQL part of the reference models (ids, sessions,
+locations from the channel rows) is out of scope: here a file is addressed by
+its path, and ``ExperimentStore`` maps ids to paths.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+from tmlibrary_amd.image import ChannelImage, IllumstatsContainer, IllumstatsImage
+from tmlibrary_amd.metadata import ChannelImageMetadata, IllumstatsImageMetadata
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "hip",
+                         "libtmh5.so")
+_lib = None
+_lock = threading.Lock()
+
+_SIGS = {
+    "tmh5_last_error": (C.c_char_p, []),
+    "tmh5_write_illumstats": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                        C.c_int64, C.c_void_p, C.c_void_p]),
+    "tmh5_illumstats_shape": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                        C.POINTER(C.c_int64)]),
+    "tmh5_read_illumstats": (C.c_int, [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p]),
+    "tmh5_write_channel_image": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                           C.c_int]),
+    "tmh5_channel_image_shape": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                           C.POINTER(C.c_int)]),
+    "tmh5_read_channel_image": (C.c_int, [C.c_char_p, C.c_void_p]),
+}
+
+
+def h5lib():
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(_LIB_PATH):
+                raise RuntimeError("libtmh5.so not built (make -C tmlibrary_amd/csrc h5; "
+                                   "needs libhdf5)")
+            lib = C.CDLL(_LIB_PATH)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+        return _lib
+
+
+def _check(rc, path):
+    if rc == 0:
+        return
+    msg = h5lib().tmh5_last_error().decode()
+    if rc == -2:
+        raise KeyError(msg)
+    if rc == -22:
+        raise ValueError("%s: %s" % (path, msg))
+    raise IOError("%s: %s" % (path, msg))
+
+
+def _b(path):
+    return os.fsencode(path)
+
+
+def write_illumstats(path, mean, std, percentiles):
+    """The four datasets of IllumstatsFile.put (file.py:451-456).  Keys and
+    values are written in dict order, as ``percentiles.keys()/values()``."""
+    L = h5lib()
+    m = np.ascontiguousarray(mean, dtype=np.float64)
+    s = np.ascontiguousarray(std, dtype=np.float64)
+    keys = np.ascontiguousarray(list(percentiles.keys()), dtype=np.float64)
+    vals = np.ascontiguousarray(list(percentiles.values()), dtype=np.int64)
+    _check(L.tmh5_write_illumstats(_b(path), m.shape[0], m.shape[1], m.ctypes.data, s.ctypes.data,
+                                   keys.size, keys.ctypes.data, vals.ctypes.data), path)
+
+
+def read_illumstats(path):
+    L = h5lib()
+    h, w, q = C.c_int(), C.c_int(), C.c_int64()
+    _check(L.tmh5_illumstats_shape(_b(path), C.byref(h), C.byref(w), C.byref(q)), path)
+    mean = np.empty((h.value, w.value), np.float64)
+    std = np.empty_like(mean)
+    keys = np.empty(q.value, np.float64)
+    vals = np.empty(q.value, np.int64)
+    _check(L.tmh5_read_illumstats(_b(path), mean.ctypes.data, std.ctypes.data, keys.ctypes.data,
+                                  vals.ctypes.data), path)
+    return mean, std, keys, vals
+
+
+def write_channel_image(path, array, gzip_level=4):
+    L = h5lib()
+    a = np.ascontiguousarray(array)
+    if a.dtype not in (np.uint8, np.uint16) or a.ndim != 2:
+        raise ValueError("channel images are 2-D uint8/uint16")
+    _check(L.tmh5_write_channel_image(_b(path), a.shape[0], a.shape[1], 8 * a.itemsize,
+                                      a.ctypes.data, int(gzip_level)), path)
+
+
+def read_channel_image(path):
+    L = h5lib()
+    h, w, bits = C.c_int(), C.c_int(), C.c_int()
+    _check(L.tmh5_channel_image_shape(_b(path), C.byref(h), C.byref(w), C.byref(bits)), path)
+    out = np.empty((h.value, w.value), np.uint8 if bits.value == 8 else np.uint16)
+    _check(L.tmh5_read_channel_image(_b(path), out.ctypes.data), path)
+    return out
+
+
+class ChannelImageFile(object):
+    """One site/channel plane on disk (tmlib/models/file.py:207-379)."""
+
+    FILENAME_FORMAT = "channel_image_file_{id}.h5"
+
+    def __init__(self, location, channel_id=0, site_id=0, cycle_id=0, tpoint=0, zplane=0):
+        self.location = location
+        self.channel_id = channel_id
+        self.site_id = site_id
+        self.cycle_id = cycle_id
+        self.tpoint = tpoint
+        self.zplane = zplane
+
+    def get(self):
+        md = ChannelImageMetadata(channel_id=self.channel_id, site_id=self.site_id,
+                                  tpoint=self.tpoint, zplane=self.zplane, cycle_id=self.cycle_id)
+        return ChannelImage(read_channel_image(self.location), md)
+
+    def put(self, image):
+        if not isinstance(image, ChannelImage):
+            raise TypeError('Argument "image" must have type tmlib.image.ChannelImage.')
+        write_channel_image(self.location, image.array, gzip_level=4)
+
+
+class IllumstatsFile(object):
+    """Illumination statistics of one channel (tmlib/models/file.py:383-472)."""
+
+    FILENAME_FORMAT = "illumstats_file_{id}.h5"
+
+    def __init__(self, location, channel_id=0):
+        self.location = location
+        self.channel_id = channel_id
+
+    def get(self):
+        """Read the four datasets, then smooth (file.py:420-438).  mean and std
+        share ONE metadata object, as in the reference (:431-434)."""
+        mean, std, keys, vals = read_illumstats(self.location)
+        md = IllumstatsImageMetadata(channel_id=self.channel_id)
+        percentiles = dict(zip(keys.tolist(), vals.tolist()))
+        cont = IllumstatsContainer(IllumstatsImage(mean, md), IllumstatsImage(std, md),
+                                   percentiles)
+        return cont.smooth()
+
+    def put(self, data):
+        if not isinstance(data, IllumstatsContainer):
+            raise TypeError('Argument "data" must have type tmlib.image.IllumstatsContainer.')
+        write_illumstats(self.location, data.mean.array, data.std.array, data.percentiles)
+
+
+class ExperimentStore(object):
+    """Id -> file mapping standing in for the experiment database:
+    ``<root>/channel_image_files/channel_image_file_{id}.h5`` and
+    ``<root>/illumstats/illumstats_file_{channel_id}.h5``.  ``file_info``
+    optionally maps a file id to (channel_id, site_id, cycle_id, tpoint, zplane)."""
+
+    def __init__(self, root, file_info=None):
+        self.root = root
+        self.file_info = file_info or {}
+
+    def channel_image_file(self, file_id):
+        info = self.file_info.get(file_id, (0, int(file_id), 0, 0, 0))
+        path = os.path.join(self.root, "channel_image_files",
+                            ChannelImageFile.FILENAME_FORMAT.format(id=file_id))
+        return ChannelImageFile(path, *info)
+
+    def illumstats_file(self, channel_id):
+        d = os.path.join(self.root, "illumstats")
+        os.makedirs(d, exist_ok=True)
+        return IllumstatsFile(os.path.join(d, IllumstatsFile.FILENAME_FORMAT.format(id=channel_id)),
+                              channel_id)

@@ -1,0 +1,91 @@
+"""corilla step: illumination statistics per channel (run phase).
+
+Mirrors tmlib/workflow/corilla/api.py:31-146 ``IllumstatsCalculator``:
+``run_job(batch)`` reads the channel's site images in the order of
+``batch['channel_image_files_ids']``, takes the image dimensions from the
+first file, updates ``OnlineStatistics`` with every site, and writes an
+``IllumstatsFile`` with mean, std and the percentile dict.
+
+Differences by design (database/cluster orchestration is out of scope): files
+are resolved through an ``ExperimentStore`` (tmlibrary_amd/models/file.py)
+instead of SQLAlchemy sessions, and the images are read ahead on a
+background thread so HDF5 decode overlaps the GPU updates.
+"""
+from __future__ import annotations
+
+import logging
+import queue
+import threading
+
+from tmlibrary_amd.image import IllumstatsContainer
+from tmlibrary_amd.models.file import ExperimentStore
+from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
+
+logger = logging.getLogger(__name__)
+
+#: corilla/api.py:69 — sites per channel beyond which the reference subsamples
+SITE_LIMIT = 20000
+
+
+def _file_id(fid):
+    # batch JSON stores SQLAlchemy row tuples as [[id], ...]
+    if isinstance(fid, (list, tuple)):
+        return fid[0]
+    return fid
+
+
+class IllumstatsCalculator(object):
+    """Calculation of illumination statistics (corilla/api.py:31-146)."""
+
+    def __init__(self, experiment_id, store=None, batch_size=32, prefetch=8):
+        self.experiment_id = experiment_id
+        if store is None:
+            raise ValueError("an ExperimentStore is required (no database in this build)")
+        if not isinstance(store, ExperimentStore):
+            raise TypeError('Argument "store" must have type ExperimentStore.')
+        self.store = store
+        self.batch_size = batch_size
+        self.prefetch = prefetch
+
+    def _images(self, file_ids):
+        """Yield (file_id, ChannelImage) in order, decoded one thread ahead."""
+        q = queue.Queue(maxsize=max(1, self.prefetch))
+        stop = object()
+
+        def reader():
+            try:
+                for fid in file_ids:
+                    q.put((fid, self.store.channel_image_file(fid).get()))
+            except BaseException as e:  # surface I/O errors in the caller
+                q.put(e)
+            q.put(stop)
+
+        t = threading.Thread(target=reader, daemon=True)
+        t.start()
+        while True:
+            item = q.get()
+            if item is stop:
+                break
+            if isinstance(item, BaseException):
+                raise item
+            yield item
+        t.join()
+
+    def run_job(self, batch, assume_clean_state=False):
+        """corilla/api.py:115-146."""
+        file_ids = [_file_id(f) for f in batch["channel_image_files_ids"]]
+        logger.info("calculate illumination statistics")
+        first = self.store.channel_image_file(file_ids[0]).get()
+        stats = OnlineStatistics(image_dimensions=first.dimensions[0:2],
+                                 batch_size=self.batch_size)
+        try:
+            for fid, img in self._images(file_ids):
+                logger.info("update statistics for image: %d", fid)
+                stats.update(img)
+            stats_file = self.store.illumstats_file(batch["channel_id"])
+            logger.info("write calculated statistics to file")
+            illumstats = IllumstatsContainer(stats.mean, stats.std, stats.percentiles)
+            stats_file.put(illumstats)
+        finally:
+            stats.close()
+        return illumstats

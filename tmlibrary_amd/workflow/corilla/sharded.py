@@ -1,0 +1,120 @@
+"""Multi-GPU illumination statistics: sites sharded across ranks, one process per GPU.
+
+The reference runs one single-threaded process per channel and never
+exchanges data inside a channel (tmlib/workflow/corilla/api.py:64-105,
+:115-146).  Here one channel's sites are split into contiguous blocks in site
+order, one block per rank; every rank streams its block through the same
+kernels as a single GPU, then the partial states are merged:
+
+  Welford   Chan et al.'s pairwise combine written as two sums, so one RCCL
+            all-reduce per quantity merges any number of ranks, identically
+            on every rank:  mean = sum_r n_r mean_r / n,
+                            M2   = sum_r [M2_r + n_r (mean_r - mean)^2]
+  percentiles  the f64 accumulator travels rank 0 -> 1 -> ... -> N-1 and each
+            rank adds its own sites in order, reproducing the reference's
+            sequential ``_percentiles +=`` bit for bit (a plain all-reduce sum
+            would reassociate it); the last rank broadcasts the result.
+  histogram all-reduce of the pooled u64 counts (exact).
+
+Collectives use ``torch.distributed`` (backend "nccl" = RCCL over xGMI on
+MI355X) on device buffers; the arithmetic runs in libtmhip kernels through
+``StatsOps``.  ``merge_shards`` only sequences collectives, so the same code
+is exercised on CPU with the gloo backend and a host-memory ``ops`` test
+double (tests/test_distributed_gloo.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+
+class StatsOps(object):
+    """libtmhip operations on one rank's ``tmh_stats`` handle (device buffers
+    are torch tensors; launches go on torch's current stream)."""
+
+    def __init__(self, lib, handle, npx, n_quantiles, device):
+        import torch
+        self.torch = torch
+        self.L = lib
+        self.h = handle
+        self.npx = int(npx)
+        self.Q = int(n_quantiles)
+        self.device = device
+
+    def _stream(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _chk(self, rc):
+        from tmlibrary_amd import hip
+        hip.check(rc)
+
+    def empty_plane(self):
+        return self.torch.empty(self.npx, dtype=self.torch.float64, device=self.device)
+
+    def empty_acc(self):
+        return self.torch.zeros(self.Q, dtype=self.torch.float64, device=self.device)
+
+    def n_local(self):
+        n = C.c_int64()
+        self._chk(self.L.tmh_stats_get_n(self.h, C.byref(n)))
+        return n.value
+
+    def stage1(self, buf):
+        self._chk(self.L.tmh_stats_merge_stage1(self.h, C.c_void_p(buf.data_ptr()), self._stream()))
+
+    def stage2(self, sum_nmean, n_total, m2c):
+        self._chk(self.L.tmh_stats_merge_stage2(self.h, C.c_void_p(sum_nmean.data_ptr()), n_total,
+                                                C.c_void_p(m2c.data_ptr()), self._stream()))
+
+    def stage3(self, n_total, sum_m2c):
+        self._chk(self.L.tmh_stats_merge_stage3(self.h, n_total, C.c_void_p(sum_m2c.data_ptr()),
+                                                self._stream()))
+
+    def pct_accumulate(self, acc):
+        self._chk(self.L.tmh_stats_pct_accumulate(self.h, C.c_void_p(acc.data_ptr()),
+                                                  self._stream()))
+
+    def set_pct_sum(self, acc):
+        self._chk(self.L.tmh_stats_set_pct_sum(self.h, C.c_void_p(acc.data_ptr()), self._stream()))
+
+
+def merge_shards(ops, dist, group=None, int_device=None):
+    """Merge every rank's partial statistics into identical global state.
+
+    ``ops`` provides n_local/empty_plane/empty_acc/stage1-3/pct_accumulate/
+    set_pct_sum on this rank's state; ``dist`` is torch.distributed.
+    Returns the global site count.
+    """
+    import torch
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    dev = int_device if int_device is not None else getattr(ops, "device", "cpu")
+    n_t = torch.tensor([ops.n_local()], dtype=torch.int64, device=dev)
+    dist.all_reduce(n_t, group=group)
+    n_total = int(n_t.item())
+    if n_total > 0:
+        buf = ops.empty_plane()
+        ops.stage1(buf)
+        dist.all_reduce(buf, group=group)
+        m2c = ops.empty_plane()
+        ops.stage2(buf, n_total, m2c)
+        dist.all_reduce(m2c, group=group)
+        ops.stage3(n_total, m2c)
+    # ordered percentile chain (bit-exact sequential summation)
+    acc = ops.empty_acc()
+    if rank > 0:
+        dist.recv(acc, src=rank - 1, group=group)
+    ops.pct_accumulate(acc)
+    if rank < world - 1:
+        dist.send(acc, dst=rank + 1, group=group)
+    dist.broadcast(acc, src=world - 1, group=group)
+    ops.set_pct_sum(acc)
+    return n_total
+
+
+def shard_bounds(n_sites, world, rank):
+    """Contiguous block of sites for ``rank`` (site order preserved)."""
+    base, extra = divmod(int(n_sites), int(world))
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
