@@ -125,7 +125,7 @@ struct tmh_stats {
   int64_t n_deferred = 0;     // sites whose order statistics are stored
   int64_t last_batch = 0;
   bool pct_sum_external = false;
-  DBuf<double> mean, m2, lut_log, lut_lin, gamma, acc, tmp_mean, tmp_std;
+  DBuf<double> mean, m2, lut_log, gamma, acc, tmp_mean, tmp_std, rn;
   DBuf<int32_t> q_lo, q_hi;
   DBuf<unsigned long long> pooled;
   DBuf<uint32_t> hist_hi, site_hist;
@@ -235,7 +235,6 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
       h->acc.alloc(n_quantiles, true);
       h->pooled.alloc(kBins, true);
       h->lut_log.alloc(kBins);
-      h->lut_lin.alloc(kBins);
       h->gamma.alloc(n_quantiles);
       h->q_lo.alloc(n_quantiles);
       h->q_hi.alloc(n_quantiles);
@@ -248,13 +247,10 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
         lo[i] = (int32_t)q_lo[i];
         hi[i] = (int32_t)q_hi[i];
       }
-      std::vector<double> lin(kBins);
-      for (int v = 0; v < kBins; ++v) lin[v] = (double)v;
       TMH_HIP(hipMemcpy(h->q_lo.p, lo.data(), lo.size() * 4, hipMemcpyHostToDevice));
       TMH_HIP(hipMemcpy(h->q_hi.p, hi.data(), hi.size() * 4, hipMemcpyHostToDevice));
       TMH_HIP(hipMemcpy(h->gamma.p, q_gamma, (size_t)n_quantiles * 8, hipMemcpyHostToDevice));
       TMH_HIP(hipMemcpy(h->lut_log.p, lut_log10, (size_t)kBins * 8, hipMemcpyHostToDevice));
-      TMH_HIP(hipMemcpy(h->lut_lin.p, lin.data(), (size_t)kBins * 8, hipMemcpyHostToDevice));
     } catch (...) {
       tmh_stats_destroy(h);
       throw;
@@ -296,8 +292,12 @@ int tmh_stats_reset(tmh_stats* h) {
 static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int log_transform,
                              hipStream_t s) {
   if (ns <= 0) return;
-  const double* lut = log_transform ? h->lut_log.p : h->lut_lin.p;
-  launch_welford(d, h->npx, ns, h->n, h->mean.p, h->m2.p, lut, s);
+  if ((size_t)ns > h->rn.n) {
+    TMH_HIP(hipStreamSynchronize(s));
+    h->rn.alloc((size_t)ns);
+  }
+  launch_welford(d, h->npx, ns, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
+                 log_transform, s);
   // order statistics, in chunks so the per-site slabs stay bounded
   const int64_t chunk = 4096;
   for (int64_t c0 = 0; c0 < ns; c0 += chunk) {

@@ -176,14 +176,22 @@ void launch_coeffs(const double* mean, const double* std, const double* sums, in
 
 constexpr float kLog2_10 = 3.32192809488736234787f;
 
+// correct-path log10 of a value >= kLutLds as an f32 hi/lo pair (out of line:
+// rare for microscopy data, and a global LUT load in the pixel loop would make
+// the compiler wait for the prefetched sites)
+__device__ __noinline__ float2 corr_log_slow(uint32_t u) {
+  const double L = log10((double)u);
+  const float hi = (float)L;
+  return make_float2(hi, (float)(L - (double)hi));
+}
+
 template <bool LOG, int BITS>
 __device__ __forceinline__ uint32_t correct1(uint32_t u, const float4 c, const float2* slut,
-                                             const float2* __restrict__ glut, float mh, float ml,
-                                             int clip_lo, int clip_hi) {
+                                             float mh, float ml, int clip_lo, int clip_hi) {
   float Lh, Ll;
   if (LOG) {
     float2 l = slut[u < (uint32_t)kLutLds ? u : 0u];
-    if (u >= (uint32_t)kLutLds) l = glut[u];
+    if (u >= (uint32_t)kLutLds) l = corr_log_slow(u);
     Lh = l.x;
     Ll = l.y;
   } else {
@@ -205,7 +213,7 @@ __device__ __forceinline__ uint32_t correct1(uint32_t u, const float4 c, const f
 }
 
 constexpr int kCorrThreads = 256;
-constexpr int kCorrUnroll = 4;
+constexpr int kCorrGroup = 4;  // sites per pipeline stage (two stages in flight)
 
 template <bool LOG>
 __global__ __launch_bounds__(kCorrThreads) void k_correct_u16_vec8(
@@ -230,23 +238,28 @@ __global__ __launch_bounds__(kCorrThreads) void k_correct_u16_vec8(
     uint32_t o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint32_t lo =
-          correct1<LOG, 16>(w[k] & 0xFFFFu, c[2 * k], slut, lut, m.x, m.y, clip_lo, clip_hi);
-      const uint32_t hi =
-          correct1<LOG, 16>(w[k] >> 16, c[2 * k + 1], slut, lut, m.x, m.y, clip_lo, clip_hi);
+      const uint32_t lo = correct1<LOG, 16>(w[k] & 0xFFFFu, c[2 * k], slut, m.x, m.y, clip_lo, clip_hi);
+      const uint32_t hi = correct1<LOG, 16>(w[k] >> 16, c[2 * k + 1], slut, m.x, m.y, clip_lo, clip_hi);
       o[k] = lo | (hi << 16);
     }
     return make_uint4(o[0], o[1], o[2], o[3]);
   };
-  int64_t s = 0;
-  for (; s + kCorrUnroll <= n_sites; s += kCorrUnroll) {
-    uint4 v[kCorrUnroll];
+  const int64_t last = n_sites - 1;
+  uint4 cur[kCorrGroup], nxt[kCorrGroup];
 #pragma unroll
-    for (int k = 0; k < kCorrUnroll; ++k) v[k] = src[(s + k) * ngroups];
+  for (int k = 0; k < kCorrGroup; ++k) cur[k] = src[(k < last ? k : last) * ngroups];
+  for (int64_t s = 0; s < n_sites; s += kCorrGroup) {
 #pragma unroll
-    for (int k = 0; k < kCorrUnroll; ++k) dst[(s + k) * ngroups] = one(v[k]);
+    for (int k = 0; k < kCorrGroup; ++k) {
+      const int64_t t = s + kCorrGroup + k;
+      nxt[k] = src[(t < last ? t : last) * ngroups];
+    }
+#pragma unroll
+    for (int k = 0; k < kCorrGroup; ++k)
+      if (s + k < n_sites) dst[(s + k) * ngroups] = one(cur[k]);
+#pragma unroll
+    for (int k = 0; k < kCorrGroup; ++k) cur[k] = nxt[k];
   }
-  for (; s < n_sites; ++s) dst[s * ngroups] = one(src[s * ngroups]);
 }
 
 template <bool LOG, typename T, int BITS>
@@ -263,8 +276,7 @@ __global__ __launch_bounds__(kCorrThreads) void k_correct_scalar(
   const float2 m = mconst[0];
   const float4 c = coef[p];
   for (int64_t s = 0; s < n_sites; ++s)
-    out[s * npx + p] =
-        (T)correct1<LOG, BITS>(in[s * npx + p], c, slut, lut, m.x, m.y, clip_lo, clip_hi);
+    out[s * npx + p] = (T)correct1<LOG, BITS>(in[s * npx + p], c, slut, m.x, m.y, clip_lo, clip_hi);
 }
 
 void launch_correct_u16(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,

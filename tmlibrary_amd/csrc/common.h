@@ -53,8 +53,9 @@ constexpr int kBinsPerThread = kBins / kHistThreads;  // 64
 constexpr int kLutLds = 4096;
 
 // launches (defined in the .hip files) -------------------------------------------
-void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0,
-                    double* mean, double* m2, const double* lut, hipStream_t s);
+void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
+                    double* mean, double* m2, const double* lut, int log_transform,
+                    hipStream_t s);
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
                          const int32_t* q_lo, const int32_t* q_hi, int Q, double scale,
                          uint16_t* vlo, uint16_t* vhi, unsigned long long* pooled,

@@ -27,10 +27,17 @@ namespace tmh {
 // Welford
 // ---------------------------------------------------------------------------
 
-__device__ __forceinline__ double lut_f64(const double* slut, const double* __restrict__ glut,
-                                          uint32_t u) {
+// x = stats transform of one pixel value.  LOG: np.log10 with 0 -> 0 from the
+// host-numpy LUT for values < kLutLds (LDS), ocml log10 for the rare larger
+// ones (VALU, no global load: a global load here would make the compiler
+// wait vmcnt(0) for the prefetched sites before every pixel).
+__device__ __noinline__ double log10_slow(uint32_t u) { return log10((double)u); }
+
+template <bool LOG>
+__device__ __forceinline__ double xform(uint32_t u, const double* slut) {
+  if (!LOG) return (double)u;
   double x = slut[u < (uint32_t)kLutLds ? u : 0u];
-  if (u >= (uint32_t)kLutLds) x = glut[u];
+  if (u >= (uint32_t)kLutLds) x = log10_slow(u);
   return x;
 }
 
@@ -40,25 +47,34 @@ __device__ __forceinline__ void welford1(double x, double rn, double& mu, double
   m2 = fma(d, x - mu, m2);      // M2 + delta * (x - mean_new)
 }
 
+template <bool LOG>
 __device__ __forceinline__ void welford8(const uint4 v, double rn, double (&mu)[8],
-                                         double (&m2)[8], const double* slut,
-                                         const double* __restrict__ glut) {
+                                         double (&m2)[8], const double* slut) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    welford1(lut_f64(slut, glut, w[k] & 0xFFFFu), rn, mu[2 * k], m2[2 * k]);
-    welford1(lut_f64(slut, glut, w[k] >> 16), rn, mu[2 * k + 1], m2[2 * k + 1]);
+    welford1(xform<LOG>(w[k] & 0xFFFFu, slut), rn, mu[2 * k], m2[2 * k]);
+    welford1(xform<LOG>(w[k] >> 16, slut), rn, mu[2 * k + 1], m2[2 * k + 1]);
   }
 }
 
 constexpr int kWfThreads = 256;
-constexpr int kWfUnroll = 4;
+constexpr int kWfGroup = 4;  // sites per pipeline stage (two stages in flight)
 
+// 1/n for the sites of one launch (uniform per site: read with scalar loads)
+__global__ void k_rn_table(double* __restrict__ rn, int64_t n0, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) rn[i] = 1.0 / (double)(n0 + i + 1);
+}
+
+template <bool LOG>
 __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
-    const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites, int64_t n0,
-    double* __restrict__ mean, double* __restrict__ m2, const double* __restrict__ lut) {
+    const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites,
+    const double* __restrict__ rn, double* __restrict__ mean, double* __restrict__ m2,
+    const double* __restrict__ lut) {
   __shared__ double slut[kLutLds];
-  for (int i = threadIdx.x; i < kLutLds; i += kWfThreads) slut[i] = lut[i];
+  if (LOG)
+    for (int i = threadIdx.x; i < kLutLds; i += kWfThreads) slut[i] = lut[i];
   __syncthreads();
   const int64_t ngroups = npx >> 3;
   const int64_t g = (int64_t)blockIdx.x * kWfThreads + threadIdx.x;
@@ -74,16 +90,24 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
     q[2 * k] = b.x; q[2 * k + 1] = b.y;
   }
   const uint4* src = reinterpret_cast<const uint4*>(sites) + g;
-  int64_t s = 0;
-  for (; s + kWfUnroll <= n_sites; s += kWfUnroll) {
-    uint4 v[kWfUnroll];
+  const int64_t last = n_sites - 1;
+  // two-stage pipeline: the next group's loads are in flight while the
+  // current group is folded in (tail loads clamp to the last site: harmless)
+  uint4 cur[kWfGroup], nxt[kWfGroup];
 #pragma unroll
-    for (int k = 0; k < kWfUnroll; ++k) v[k] = src[(s + k) * ngroups];
+  for (int k = 0; k < kWfGroup; ++k) cur[k] = src[(k < last ? k : last) * ngroups];
+  for (int64_t s = 0; s < n_sites; s += kWfGroup) {
 #pragma unroll
-    for (int k = 0; k < kWfUnroll; ++k)
-      welford8(v[k], 1.0 / (double)(n0 + s + k + 1), mu, q, slut, lut);
+    for (int k = 0; k < kWfGroup; ++k) {
+      const int64_t t = s + kWfGroup + k;
+      nxt[k] = src[(t < last ? t : last) * ngroups];
+    }
+#pragma unroll
+    for (int k = 0; k < kWfGroup; ++k)
+      if (s + k < n_sites) welford8<LOG>(cur[k], rn[s + k], mu, q, slut);
+#pragma unroll
+    for (int k = 0; k < kWfGroup; ++k) cur[k] = nxt[k];
   }
-  for (; s < n_sites; ++s) welford8(src[s * ngroups], 1.0 / (double)(n0 + s + 1), mu, q, slut, lut);
 
   double2* om = reinterpret_cast<double2*>(mean) + g * 4;
   double2* oq = reinterpret_cast<double2*>(m2) + g * 4;
@@ -95,34 +119,45 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
 }
 
 // Any shape (npx % 8 != 0 leaves sites unaligned for 16-B loads): 1 px/thread.
+template <bool LOG>
 __global__ __launch_bounds__(kWfThreads) void k_welford_scalar(
-    const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites, int64_t n0,
-    double* __restrict__ mean, double* __restrict__ m2, const double* __restrict__ lut) {
+    const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites,
+    const double* __restrict__ rn, double* __restrict__ mean, double* __restrict__ m2,
+    const double* __restrict__ lut) {
   __shared__ double slut[kLutLds];
-  for (int i = threadIdx.x; i < kLutLds; i += kWfThreads) slut[i] = lut[i];
+  if (LOG)
+    for (int i = threadIdx.x; i < kLutLds; i += kWfThreads) slut[i] = lut[i];
   __syncthreads();
   const int64_t p = (int64_t)blockIdx.x * kWfThreads + threadIdx.x;
   if (p >= npx) return;
   double mu = mean[p], q = m2[p];
   for (int64_t s = 0; s < n_sites; ++s)
-    welford1(lut_f64(slut, lut, sites[s * npx + p]), 1.0 / (double)(n0 + s + 1), mu, q);
+    welford1(xform<LOG>(sites[s * npx + p], slut), rn[s], mu, q);
   mean[p] = mu;
   m2[p] = q;
 }
 
-void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* mean,
-                    double* m2, const double* lut, hipStream_t s) {
+void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
+                    double* mean, double* m2, const double* lut, int log_transform,
+                    hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("welford", s);
-  if ((npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0) {
-    const int64_t grid = cdiv(npx >> 3, kWfThreads);
-    hipLaunchKernelGGL(k_welford_vec8, dim3((unsigned)grid), dim3(kWfThreads), 0, s, sites, npx,
-                       n_sites, n0, mean, m2, lut);
-  } else {
-    const int64_t grid = cdiv(npx, kWfThreads);
-    hipLaunchKernelGGL(k_welford_scalar, dim3((unsigned)grid), dim3(kWfThreads), 0, s, sites, npx,
-                       n_sites, n0, mean, m2, lut);
-  }
+  hipLaunchKernelGGL(k_rn_table, dim3((unsigned)cdiv(n_sites, 256)), dim3(256), 0, s, rn, n0,
+                     n_sites);
+  const bool vec = (npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0;
+  const dim3 grid((unsigned)(vec ? cdiv(npx >> 3, kWfThreads) : cdiv(npx, kWfThreads)));
+  if (vec && log_transform)
+    hipLaunchKernelGGL(k_welford_vec8<true>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites, rn,
+                       mean, m2, lut);
+  else if (vec)
+    hipLaunchKernelGGL(k_welford_vec8<false>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites, rn,
+                       mean, m2, lut);
+  else if (log_transform)
+    hipLaunchKernelGGL(k_welford_scalar<true>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
+                       rn, mean, m2, lut);
+  else
+    hipLaunchKernelGGL(k_welford_scalar<false>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
+                       rn, mean, m2, lut);
   TMH_HIP(hipGetLastError());
 }
 
@@ -130,17 +165,11 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
 // per-site histogram + percentile order statistics
 // ---------------------------------------------------------------------------
 
-// LDS bin address: rotate within each 64-bin group so that thread t reading
-// bin 64t+j (j fixed across the wave) hits bank (j+t)%32: conflict-free scan.
-__device__ __forceinline__ uint32_t bin_slot(uint32_t u) {
-  return (u & ~63u) | ((u + (u >> 6)) & 63u);
-}
-
-__device__ __forceinline__ void count1(uint32_t u, uint32_t* bins, uint32_t* himask,
-                                       uint32_t* __restrict__ hhi) {
-  if (u < (uint32_t)kLdsBins) {
-    atomicAdd(&bins[bin_slot(u)], 1u);
-  } else {
+// High values (>= kLdsBins) are rare in microscopy data: they go to global
+// atomics in a per-site slab; the LDS add for them is a harmless +0 so the
+// common path has no per-pixel branch.
+__device__ __forceinline__ void count_hi(uint32_t u, uint32_t* himask, uint32_t* __restrict__ hhi) {
+  if (u >= (uint32_t)kLdsBins) {
     const uint32_t h = u - kLdsBins;
     atomicAdd(&hhi[h], 1u);
     atomicOr(&himask[h >> 11], 1u << ((h >> 6) & 31u));
@@ -149,14 +178,15 @@ __device__ __forceinline__ void count1(uint32_t u, uint32_t* bins, uint32_t* him
 
 __device__ __forceinline__ void count8(const uint4 v, uint32_t* bins, uint32_t* himask,
                                        uint32_t* __restrict__ hhi) {
-  count1(v.x & 0xFFFFu, bins, himask, hhi);
-  count1(v.x >> 16, bins, himask, hhi);
-  count1(v.y & 0xFFFFu, bins, himask, hhi);
-  count1(v.y >> 16, bins, himask, hhi);
-  count1(v.z & 0xFFFFu, bins, himask, hhi);
-  count1(v.z >> 16, bins, himask, hhi);
-  count1(v.w & 0xFFFFu, bins, himask, hhi);
-  count1(v.w >> 16, bins, himask, hhi);
+  const uint32_t u[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
+                         v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
+  const uint32_t any_hi = (v.x | v.y | v.z | v.w) & 0x80008000u;  // kLdsBins == 32768
+#pragma unroll
+  for (int k = 0; k < 8; ++k) atomicAdd(&bins[u[k] & (kLdsBins - 1)], u[k] < (uint32_t)kLdsBins);
+  if (any_hi) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) count_hi(u[k], himask, hhi);
+  }
 }
 
 // smallest q in [0, Q] with tab[q] >= r (tab non-decreasing, ~linear in q)
@@ -171,17 +201,42 @@ __device__ __forceinline__ int64_t first_q(const int32_t* __restrict__ tab, int 
 }
 
 // Writes value b at every quantile whose previous (vlo) / next (vhi) sorted
-// position lies in [start, end).  Kept out of line: it runs only for
-// non-empty bins, and inlining it 64x would bloat the scan loop.
-__device__ __noinline__ void scatter_bin(uint32_t b, int64_t start, int64_t end,
-                                         const int32_t* __restrict__ q_lo,
-                                         const int32_t* __restrict__ q_hi, int Q, double scale,
-                                         uint16_t* __restrict__ vlo, uint16_t* __restrict__ vhi) {
+// position lies in [start, end).
+__device__ __forceinline__ void scatter_bin(uint32_t b, int64_t start, int64_t end,
+                                            const int32_t* __restrict__ q_lo,
+                                            const int32_t* __restrict__ q_hi, int Q, double scale,
+                                            uint16_t* __restrict__ vlo, uint16_t* __restrict__ vhi) {
   const uint16_t v = (uint16_t)b;
-  for (int64_t q = first_q(q_lo, Q, scale, start), q1 = first_q(q_lo, Q, scale, end); q < q1; ++q)
-    vlo[q] = v;
-  for (int64_t q = first_q(q_hi, Q, scale, start), q1 = first_q(q_hi, Q, scale, end); q < q1; ++q)
-    vhi[q] = v;
+  const int64_t l0 = first_q(q_lo, Q, scale, start), l1 = first_q(q_lo, Q, scale, end);
+  const int64_t h0 = first_q(q_hi, Q, scale, start), h1 = first_q(q_hi, Q, scale, end);
+  for (int64_t q = l0; q < l1; ++q) vlo[q] = v;
+  for (int64_t q = h0; q < h1; ++q) vhi[q] = v;
+}
+
+// Exclusive scan of one value per thread over the 1024-thread workgroup.
+// `slots` holds 2 x 16 wave totals (double-buffered by `round` parity, so one
+// barrier per round suffices).  Returns the exclusive prefix; *total = sum.
+__device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, int round,
+                                                 uint32_t* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t incl = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  uint32_t* ws = slots + (round & 1) * 16;
+  if (lane == 63) ws[wid] = incl;
+  __syncthreads();
+  uint32_t woff = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    const uint32_t t = ws[w];
+    woff += (w < wid) ? t : 0u;
+    all += t;
+  }
+  *total = all;
+  return woff + incl - c;
 }
 
 __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
@@ -192,10 +247,8 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
     uint32_t* __restrict__ site_hist) {
   __shared__ __attribute__((aligned(16))) uint32_t bins[kLdsBins];
   __shared__ uint32_t himask[16];
-  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t slots[32];
   const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
   const int64_t s = blockIdx.x;
 
   for (int i = tid; i < kLdsBins / 4; i += kHistThreads)
@@ -219,63 +272,41 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
     }
     for (; i < n16; i += kHistThreads) count8(src[i], bins, himask, hhi);
   } else {
-    for (int64_t i = tid; i < npx; i += kHistThreads) count1(site[i], bins, himask, hhi);
+    for (int64_t i = tid; i < npx; i += kHistThreads) {
+      const uint32_t u = site[i];
+      atomicAdd(&bins[u & (kLdsBins - 1)], u < (uint32_t)kLdsBins);
+      count_hi(u, himask, hhi);
+    }
   }
   // __syncthreads() orders LDS only: the global atomics into the slab must
   // have been performed before other waves swap the slab out below.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // thread t owns bins [64t, 64t+64): read them into registers
-  uint32_t cnt[kBinsPerThread];
-  if (tid < kLdsBins / kBinsPerThread) {
-    const uint32_t base = (uint32_t)tid * kBinsPerThread;
-#pragma unroll
-    for (int j = 0; j < kBinsPerThread; ++j) cnt[j] = bins[base + ((j + tid) & 63)];
-  } else {
-    const uint32_t c = (uint32_t)tid - kLdsBins / kBinsPerThread;
-    const bool touched = (himask[c >> 5] >> (c & 31u)) & 1u;
-    if (touched) {
-#pragma unroll
-      for (int j = 0; j < kBinsPerThread; ++j) cnt[j] = atomicExch(&hhi[c * kBinsPerThread + j], 0u);
-    } else {
-#pragma unroll
-      for (int j = 0; j < kBinsPerThread; ++j) cnt[j] = 0u;
-    }
-  }
-  uint32_t tot = 0;
-#pragma unroll
-  for (int j = 0; j < kBinsPerThread; ++j) tot += cnt[j];
-
-  // exclusive scan of per-thread totals over the workgroup
-  uint32_t incl = tot;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += y;
-  }
-  if (lane == 63) wsum[wid] = incl;
-  __syncthreads();
-  uint32_t woff = 0;
-  for (int w = 0; w < wid; ++w) woff += wsum[w];
-  const int64_t base_rank = (int64_t)woff + incl - tot;
-
-  const uint32_t b0 = (uint32_t)tid * kBinsPerThread;
-  if (tid == 0 && zero_counts) zero_counts[s] = cnt[0];
-  if (site_hist) {
-#pragma unroll
-    for (int j = 0; j < kBinsPerThread; ++j) site_hist[s * kBins + b0 + j] = cnt[j];
-  }
+  // Walk the 65,536 bins in 64 rounds of 1024 consecutive bins, thread t
+  // owning bin 1024*j + t: LDS reads are conflict-free, and the dense part of
+  // a microscopy histogram (a few thousand adjacent values) is spread over
+  // every thread, so the percentile scatter is balanced.
   uint16_t* vlo = vlo_all + s * (int64_t)Q;
   uint16_t* vhi = vhi_all + s * (int64_t)Q;
-  int64_t r = base_rank;
-#pragma unroll
-  for (int j = 0; j < kBinsPerThread; ++j) {
-    const uint32_t c = cnt[j];
+  int64_t base = 0;  // exclusive rank of the current round's first bin
+  for (int j = 0; j < kBins / kHistThreads; ++j) {
+    const uint32_t b = (uint32_t)j * kHistThreads + tid;
+    uint32_t c;
+    if (b < (uint32_t)kLdsBins) {
+      c = bins[b];
+    } else {
+      const uint32_t h = b - kLdsBins;
+      c = ((himask[h >> 11] >> ((h >> 6) & 31u)) & 1u) ? atomicExch(&hhi[h], 0u) : 0u;
+    }
+    uint32_t total;
+    const int64_t r = base + block_exscan(c, slots, j, &total);
+    base += total;
+    if (site_hist) site_hist[s * kBins + b] = c;
+    if (b == 0 && zero_counts) zero_counts[s] = c;
     if (c) {
-      atomicAdd(&pooled[b0 + j], (unsigned long long)c);
-      scatter_bin(b0 + j, r, r + c, q_lo, q_hi, Q, scale, vlo, vhi);
-      r += c;
+      atomicAdd(&pooled[b], (unsigned long long)c);
+      scatter_bin(b, r, r + c, q_lo, q_hi, Q, scale, vlo, vhi);
     }
   }
 }

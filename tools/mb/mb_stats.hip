@@ -1,0 +1,278 @@
+// Microbenchmarks for the stats/apply kernels (development tool, not shipped).
+//
+// Builds against the production kernels (launch_* from libtmhip sources) and
+// adds ablation variants to find each kernel's limiter:
+//   stream_read / copy        HBM roofline of this access pattern
+//   hist_* variants           loads only / LDS atomics only / production
+//   welford variants          production
+// Usage: mb_stats [n_sites] [reps]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <algorithm>
+#include <vector>
+
+#include "../../tmlibrary_amd/csrc/common.h"
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+using namespace tmh;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_nt(uint4* p, uint4 v) {
+  u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+}
+
+__global__ __launch_bounds__(256) void k_stream_read(const uint4* __restrict__ p, int64_t n,
+                                                     uint32_t* __restrict__ sink) {
+  uint32_t acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint4 v = p[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ p, uint4* __restrict__ q,
+                                              int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    q[i] = p[i];
+}
+
+// copy variants: U loads in flight per thread, NT = nontemporal stores
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_copy_u(const uint4* __restrict__ p, uint4* __restrict__ q,
+                                                int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += U * stride) {
+    uint4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = (i + k * stride < n) ? p[i + k * stride] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (i + k * stride < n) {
+        if (NT) st_nt(q + i + k * stride, v[k]);
+        else q[i + k * stride] = v[k];
+      }
+  }
+}
+
+// pixel-major copy (the correct kernel's pattern): thread = 8 px, loop sites
+template <bool NT>
+__global__ __launch_bounds__(256) void k_copy_pm(const uint4* __restrict__ p, uint4* __restrict__ q,
+                                                 int64_t ngroups, int64_t n_sites) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= ngroups) return;
+  for (int64_t s = 0; s < n_sites; s += 4) {
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = (s + k < n_sites) ? p[(s + k) * ngroups + g] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (s + k < n_sites) {
+        if (NT) st_nt(q + (s + k) * ngroups + g, v[k]);
+        else q[(s + k) * ngroups + g] = v[k];
+      }
+  }
+}
+
+// hist ablation: MODE 0 = loads + integer sum only, 1 = LDS atomics (no hi branch),
+// 2 = LDS atomics with 8 loads in flight
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_hist_abl(const uint16_t* __restrict__ sites, int64_t npx,
+                                                   uint32_t* __restrict__ sink) {
+  __shared__ uint32_t bins[32768];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 32768; i += 1024) bins[i] = 0;
+  __syncthreads();
+  const uint4* src = reinterpret_cast<const uint4*>(sites + blockIdx.x * npx);
+  const int64_t n16 = npx >> 3;
+  uint32_t acc = 0;
+  constexpr int U = MODE == 2 ? 8 : 4;
+  for (int64_t i = tid; i < n16; i += U * 1024) {
+    uint4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = (i + k * 1024 < n16) ? src[i + k * 1024] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (MODE == 0) {
+          acc += (w[j] & 0xFFFF) + (w[j] >> 16);
+        } else {
+          atomicAdd(&bins[(w[j] & 0xFFFF) & 32767], 1u);
+          atomicAdd(&bins[(w[j] >> 16) & 32767], 1u);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (MODE != 0) acc = bins[tid];
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+struct Timer {
+  hipEvent_t a, b;
+  Timer() {
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+  }
+  void start() { CK(hipEventRecord(a, 0)); }
+  float stop() {
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms;
+  }
+};
+
+int main(int argc, char** argv) {
+  const int64_t S = argc > 1 ? atoll(argv[1]) : 512;
+  const int reps = argc > 2 ? atoi(argv[2]) : 3;
+  const int H = 2160, W = 2560;
+  const int64_t npx = (int64_t)H * W;
+  const double site_gb = npx * 2 / 1e9;
+  uint16_t *sites, *out;
+  CK(hipMalloc(&sites, S * npx * 2));
+  CK(hipMalloc(&out, S * npx * 2));
+  uint32_t* sink;
+  CK(hipMalloc(&sink, 64));
+  launch_synth(sites, S, H, W, 12345, 0, 0, 0);
+  CK(hipDeviceSynchronize());
+  Timer t;
+  auto report = [&](const char* name, float ms, double gb) {
+    printf("%-28s %9.3f ms  %8.1f GB/s  %6.1f%% of 8 TB/s  %9.0f sites/s\n", name, ms, gb / (ms * 1e-3),
+           100.0 * gb / (ms * 1e-3) / 8000.0, S / (ms * 1e-3));
+  };
+  const int64_t n16 = S * npx / 8;
+  for (int r = 0; r < reps; ++r) {
+    t.start();
+    hipLaunchKernelGGL(k_stream_read, dim3(8192), dim3(256), 0, 0, (const uint4*)sites, n16, sink);
+    report("stream_read (2 B/px)", t.stop(), S * site_gb);
+    t.start();
+    hipLaunchKernelGGL(k_copy, dim3(8192), dim3(256), 0, 0, (const uint4*)sites, (uint4*)out, n16);
+    report("copy (4 B/px)", t.stop(), 2 * S * site_gb);
+  }
+  for (int r = 0; r < reps; ++r) {
+    t.start();
+    hipLaunchKernelGGL((k_copy_u<4, false>), dim3(8192), dim3(256), 0, 0, (const uint4*)sites, (uint4*)out, n16);
+    report("copy u4", t.stop(), 2 * S * site_gb);
+    t.start();
+    hipLaunchKernelGGL((k_copy_u<4, true>), dim3(8192), dim3(256), 0, 0, (const uint4*)sites, (uint4*)out, n16);
+    report("copy u4 nt-store", t.stop(), 2 * S * site_gb);
+    t.start();
+    hipLaunchKernelGGL((k_copy_u<1, true>), dim3(8192), dim3(256), 0, 0, (const uint4*)sites, (uint4*)out, n16);
+    report("copy u1 nt-store", t.stop(), 2 * S * site_gb);
+    t.start();
+    hipLaunchKernelGGL((k_copy_u<4, false>), dim3(2048), dim3(256), 0, 0, (const uint4*)sites, (uint4*)out, n16);
+    report("copy u4 grid2048", t.stop(), 2 * S * site_gb);
+    const int64_t ng = npx / 8;
+    t.start();
+    hipLaunchKernelGGL(k_copy_pm<false>, dim3((unsigned)cdiv(ng, 256)), dim3(256), 0, 0, (const uint4*)sites, (uint4*)out, ng, S);
+    report("copy pixel-major", t.stop(), 2 * S * site_gb);
+    t.start();
+    hipLaunchKernelGGL(k_copy_pm<true>, dim3((unsigned)cdiv(ng, 256)), dim3(256), 0, 0, (const uint4*)sites, (uint4*)out, ng, S);
+    report("copy pixel-major nt", t.stop(), 2 * S * site_gb);
+  }
+  // Infinity-cache probe: re-read a buffer that fits (128 MB) vs one that doesn't
+  for (int64_t mb : {64, 128, 200, 512, 4096}) {
+    const int64_t n = mb * (1 << 20) / 16;
+    if (n > n16) break;
+    hipLaunchKernelGGL(k_stream_read, dim3(8192), dim3(256), 0, 0, (const uint4*)sites, n, sink);
+    float best = 1e9;
+    for (int r = 0; r < 5; ++r) {
+      t.start();
+      hipLaunchKernelGGL(k_stream_read, dim3(8192), dim3(256), 0, 0, (const uint4*)sites, n, sink);
+      best = std::min(best, t.stop());
+    }
+    printf("re-read %5ld MB: %8.1f GB/s\n", (long)mb, n * 16 / (best * 1e-3) / 1e9);
+  }
+  // welford (production)
+  double *mean, *m2, *lut, *rn;
+  CK(hipMalloc(&rn, S * 8));
+  CK(hipMalloc(&mean, npx * 8));
+  CK(hipMalloc(&m2, npx * 8));
+  CK(hipMalloc(&lut, 65536 * 8));
+  std::vector<double> hl(65536);
+  for (int v = 0; v < 65536; ++v) hl[v] = v ? log10((double)v) : 0.0;
+  CK(hipMemcpy(lut, hl.data(), 65536 * 8, hipMemcpyHostToDevice));
+  for (int r = 0; r < reps; ++r) {
+    CK(hipMemset(mean, 0, npx * 8));
+    CK(hipMemset(m2, 0, npx * 8));
+    t.start();
+    launch_welford(sites, npx, S, 0, rn, mean, m2, lut, 1, 0);
+    report("welford (prod)", t.stop(), S * site_gb);
+  }
+  // hist ablations
+  for (int r = 0; r < reps; ++r) {
+    t.start();
+    hipLaunchKernelGGL(k_hist_abl<0>, dim3(S), dim3(1024), 0, 0, sites, npx, sink);
+    report("hist: loads only", t.stop(), S * site_gb);
+    t.start();
+    hipLaunchKernelGGL(k_hist_abl<1>, dim3(S), dim3(1024), 0, 0, sites, npx, sink);
+    report("hist: lds atomics", t.stop(), S * site_gb);
+    t.start();
+    hipLaunchKernelGGL(k_hist_abl<2>, dim3(S), dim3(1024), 0, 0, sites, npx, sink);
+    report("hist: lds atomics, 8 ld", t.stop(), S * site_gb);
+  }
+  // hist production
+  const int Q = 100000;
+  uint32_t* hist_hi;
+  CK(hipMalloc(&hist_hi, S * kHiBins * 4));
+  CK(hipMemset(hist_hi, 0, S * kHiBins * 4));
+  int32_t *qlo, *qhi;
+  CK(hipMalloc(&qlo, Q * 4));
+  CK(hipMalloc(&qhi, Q * 4));
+  std::vector<int32_t> lo(Q), hi(Q);
+  for (int i = 0; i < Q; ++i) {
+    const double vi = (double)(npx - 1) * ((100.0 * i / (Q - 1)) / 100.0);
+    lo[i] = (int32_t)vi;
+    hi[i] = std::min<int64_t>(lo[i] + 1, npx - 1);
+  }
+  CK(hipMemcpy(qlo, lo.data(), Q * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(qhi, hi.data(), Q * 4, hipMemcpyHostToDevice));
+  uint16_t *vlo, *vhi;
+  CK(hipMalloc(&vlo, S * Q * 2));
+  CK(hipMalloc(&vhi, S * Q * 2));
+  unsigned long long* pooled;
+  CK(hipMalloc(&pooled, 65536 * 8));
+  int64_t* zeros;
+  CK(hipMalloc(&zeros, S * 8));
+  for (int r = 0; r < reps; ++r) {
+    t.start();
+    launch_hist_scatter(sites, npx, S, hist_hi, qlo, qhi, Q, (double)(Q - 1) / (npx - 1), vlo, vhi,
+                        pooled, zeros, nullptr, 0);
+    report("hist (prod)", t.stop(), S * site_gb);
+  }
+  // correct (production) with dummy stats
+  float4* coef;
+  float2 *clut, *mconst;
+  double* sums;
+  CK(hipMalloc(&coef, npx * 16));
+  CK(hipMalloc(&clut, 65536 * 8));
+  CK(hipMalloc(&mconst, 8));
+  CK(hipMalloc(&sums, 16));
+  launch_finalize(mean, m2, S, npx, nullptr, m2, 0);
+  launch_build_corr_lut(clut, 1, -10.0, 0);
+  std::vector<double> hs = {1.0 * npx, 2.5 * npx};
+  CK(hipMemcpy(sums, hs.data(), 16, hipMemcpyHostToDevice));
+  launch_coeffs(mean, m2, sums, npx, coef, mconst, 0);
+  for (int r = 0; r < reps; ++r) {
+    t.start();
+    launch_correct_u16(sites, out, npx, S, coef, clut, mconst, 1, -1, -1, 0);
+    report("correct (prod)", t.stop(), 2 * S * site_gb);
+  }
+  CK(hipDeviceSynchronize());
+  printf("done\n");
+  return 0;
+}
