@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=24,
                    help="sites in the bounded CPU-baseline sample (0 disables)")
     p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
+    p.add_argument("--serial-stats", action="store_true",
+                   help="run the histogram pass after Welford instead of concurrently")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     return p.parse_args()
@@ -126,6 +128,8 @@ def main():
     lo, hi, gamma = quantile_table(npx, np.linspace(0, 100, Q))
     lut = stats_log10_lut()
     flags = hip.TMH_STATS_DEFERRED_PCT if world > 1 else 0
+    if a.serial_stats:
+        flags |= hip.TMH_STATS_SERIAL
     h = C.c_void_p()
     hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma), hip.ptr(lut),
                                  1, flags, C.byref(h)))

@@ -68,6 +68,8 @@ int tmh_synchronize(void* stream);
 typedef struct tmh_stats tmh_stats;
 
 #define TMH_STATS_DEFERRED_PCT 1u
+#define TMH_STATS_KEEP_SITE_HIST 2u /* keep per-site histograms (debug/parity) */
+#define TMH_STATS_SERIAL 4u         /* no side stream: histogram after Welford */
 
 int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo,
                      const int64_t* q_hi, const double* q_gamma, const double* lut_log10,

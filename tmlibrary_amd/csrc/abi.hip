@@ -121,6 +121,8 @@ struct tmh_stats {
   int64_t batch_cap = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;   // histogram pass runs here, concurrent with Welford
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t n = 0;              // sites accumulated (Welford count)
   int64_t n_deferred = 0;     // sites whose order statistics are stored
   int64_t last_batch = 0;
@@ -180,7 +182,10 @@ static void stats_reserve_sites(tmh_stats* h, int64_t n_sites) {
   const bool grow = (size_t)n_sites * kHiBins > h->hist_hi.n || (size_t)n_sites > h->zeros.n ||
                     ((h->flags & 2u) && (size_t)n_sites * kBins > h->site_hist.n) ||
                     (!(h->flags & TMH_STATS_DEFERRED_PCT) && (size_t)n_sites * h->Q > h->vlo.n);
-  if (grow) TMH_HIP(hipStreamSynchronize(h->stream));
+  if (grow) {
+    TMH_HIP(hipStreamSynchronize(h->stream));
+    TMH_HIP(hipStreamSynchronize(h->side));
+  }
   // per-site slabs: hist_hi stays all-zero between launches (the kernel
   // resets what it touched), so it is zeroed only when (re)allocated.
   if ((size_t)n_sites * kHiBins > h->hist_hi.n) h->hist_hi.alloc((size_t)n_sites * kHiBins, true);
@@ -203,6 +208,7 @@ static void stats_grow_deferred(tmh_stats* h, int64_t extra) {
       TMH_HIP(hipMemcpyAsync(nb.p, b->p, (size_t)h->n_deferred * h->Q * sizeof(uint16_t),
                              hipMemcpyDeviceToDevice, h->stream));
     TMH_HIP(hipStreamSynchronize(h->stream));
+    TMH_HIP(hipStreamSynchronize(h->side));
     std::swap(b->p, nb.p);
     std::swap(b->n, nb.n);
   }
@@ -229,6 +235,9 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
       h->flags = flags;
       h->batch_cap = std::min(4096, batch_capacity > 0 ? batch_capacity : 1);
       TMH_HIP(hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking));
+      TMH_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+      TMH_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+      TMH_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
       h->stream = h->own_stream;
       h->mean.alloc(npx, true);
       h->m2.alloc(npx, true);
@@ -263,9 +272,13 @@ void tmh_stats_destroy(tmh_stats* h) {
   if (!h) return;
   if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
   if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
-  hipStream_t s = h->own_stream;
+  hipStream_t s = h->own_stream, side = h->side;
+  if (side) (void)hipStreamSynchronize(side);
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   delete h;
   if (s) (void)hipStreamDestroy(s);
+  if (side) (void)hipStreamDestroy(side);
 }
 
 int tmh_stats_set_stream(tmh_stats* h, void* stream) {
@@ -296,16 +309,24 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
     TMH_HIP(hipStreamSynchronize(s));
     h->rn.alloc((size_t)ns);
   }
+  // Both passes only read the sites: run the histogram/percentile pass on a
+  // side stream concurrently with the Welford pass (fork/join by events).
+  const bool serial = (h->flags & TMH_STATS_SERIAL) != 0;
+  hipStream_t hs = serial ? s : h->side;
+  const int64_t chunk = 4096;
+  stats_reserve_sites(h, std::min(chunk, ns));  // (re)allocate before forking
+  if (h->flags & TMH_STATS_DEFERRED_PCT) stats_grow_deferred(h, ns);
+  if (!serial) {
+    TMH_HIP(hipEventRecord(h->ev_fork, s));
+    TMH_HIP(hipStreamWaitEvent(hs, h->ev_fork, 0));
+  }
   launch_welford(d, h->npx, ns, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
                  log_transform, s);
   // order statistics, in chunks so the per-site slabs stay bounded
-  const int64_t chunk = 4096;
   for (int64_t c0 = 0; c0 < ns; c0 += chunk) {
     const int64_t nc = std::min(chunk, ns - c0);
-    stats_reserve_sites(h, nc);
     uint16_t *vlo, *vhi;
     if (h->flags & TMH_STATS_DEFERRED_PCT) {
-      stats_grow_deferred(h, nc);
       vlo = h->vlo.p + (size_t)h->n_deferred * h->Q;
       vhi = h->vhi.p + (size_t)h->n_deferred * h->Q;
     } else {
@@ -314,12 +335,16 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
     }
     launch_hist_scatter(d + c0 * h->npx, h->npx, nc, h->hist_hi.p, h->q_lo.p, h->q_hi.p, h->Q,
                         h->scale, vlo, vhi, h->pooled.p, h->zeros.p,
-                        (h->flags & 2u) ? h->site_hist.p : nullptr, s);
+                        (h->flags & 2u) ? h->site_hist.p : nullptr, hs);
     if (h->flags & TMH_STATS_DEFERRED_PCT)
       h->n_deferred += nc;
     else
-      launch_pct_accumulate(vlo, vhi, nc, h->Q, h->gamma.p, h->acc.p, s);
+      launch_pct_accumulate(vlo, vhi, nc, h->Q, h->gamma.p, h->acc.p, hs);
     h->last_batch = nc;
+  }
+  if (!serial) {
+    TMH_HIP(hipEventRecord(h->ev_join, hs));
+    TMH_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
   }
   h->n += ns;
 }

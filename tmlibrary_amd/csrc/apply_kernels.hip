@@ -185,19 +185,10 @@ __device__ __noinline__ float2 corr_log_slow(uint32_t u) {
   return make_float2(hi, (float)(L - (double)hi));
 }
 
+// the correction of one pixel given its log10 (hi, lo) (or value) L
 template <bool LOG, int BITS>
-__device__ __forceinline__ uint32_t correct1(uint32_t u, const float4 c, const float2* slut,
-                                             float mh, float ml, int clip_lo, int clip_hi) {
-  float Lh, Ll;
-  if (LOG) {
-    float2 l = slut[u < (uint32_t)kLutLds ? u : 0u];
-    if (u >= (uint32_t)kLutLds) l = corr_log_slow(u);
-    Lh = l.x;
-    Ll = l.y;
-  } else {
-    Lh = (float)u;
-    Ll = 0.0f;
-  }
+__device__ __forceinline__ uint32_t correct_l(float Lh, float Ll, const float4 c, float mh, float ml,
+                                              int clip_lo, int clip_hi) {
   const float d = (Lh - c.x) + (Ll - c.y);       // (img - mean)
   const float t = fmaf(d, c.z, mh) + ml;          // * mean(std)/std + mean(mean)
   const float o = LOG ? exp2f(t * kLog2_10) : t;  // 10 ** t
@@ -210,6 +201,19 @@ __device__ __forceinline__ uint32_t correct1(uint32_t u, const float4 c, const f
     r = r > (uint32_t)clip_hi ? (uint32_t)clip_hi : r;
   }
   return r;
+}
+
+template <bool LOG, int BITS>
+__device__ __forceinline__ uint32_t correct1(uint32_t u, const float4 c, const float2* slut,
+                                             float mh, float ml, int clip_lo, int clip_hi) {
+  float2 l;
+  if (LOG) {
+    l = slut[u < (uint32_t)kLutLds ? u : 0u];
+    if (u >= (uint32_t)kLutLds) l = corr_log_slow(u);
+  } else {
+    l = make_float2((float)u, 0.0f);
+  }
+  return correct_l<LOG, BITS>(l.x, l.y, c, mh, ml, clip_lo, clip_hi);
 }
 
 constexpr int kCorrThreads = 256;
@@ -234,15 +238,31 @@ __global__ __launch_bounds__(kCorrThreads) void k_correct_u16_vec8(
   const uint4* src = reinterpret_cast<const uint4*>(in) + g;
   uint4* dst = reinterpret_cast<uint4*>(out) + g;
   auto one = [&](const uint4 v) -> uint4 {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint32_t o[4];
+    const uint32_t u[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
+                           v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
+    float2 l[8];
+    if (LOG) {
+      // one branch per 8 pixels: LDS LUT for all, then patch the rare big ones
+      uint32_t mx = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t lo = correct1<LOG, 16>(w[k] & 0xFFFFu, c[2 * k], slut, m.x, m.y, clip_lo, clip_hi);
-      const uint32_t hi = correct1<LOG, 16>(w[k] >> 16, c[2 * k + 1], slut, m.x, m.y, clip_lo, clip_hi);
-      o[k] = lo | (hi << 16);
+      for (int k = 0; k < 8; ++k) {
+        mx = u[k] > mx ? u[k] : mx;
+        l[k] = slut[u[k] < (uint32_t)kLutLds ? u[k] : 0u];
+      }
+      if (mx >= (uint32_t)kLutLds) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (u[k] >= (uint32_t)kLutLds) l[k] = corr_log_slow(u[k]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) l[k] = make_float2((float)u[k], 0.0f);
     }
-    return make_uint4(o[0], o[1], o[2], o[3]);
+    uint32_t o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = correct_l<LOG, 16>(l[k].x, l[k].y, c[k], m.x, m.y, clip_lo, clip_hi);
+    return make_uint4(o[0] | (o[1] << 16), o[2] | (o[3] << 16), o[4] | (o[5] << 16),
+                      o[6] | (o[7] << 16));
   };
   const int64_t last = n_sites - 1;
   uint4 cur[kCorrGroup], nxt[kCorrGroup];

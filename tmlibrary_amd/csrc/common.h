@@ -60,6 +60,10 @@ void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, ui
                          const int32_t* q_lo, const int32_t* q_hi, int Q, double scale,
                          uint16_t* vlo, uint16_t* vhi, unsigned long long* pooled,
                          int64_t* zero_counts, uint32_t* site_hist, hipStream_t s);
+void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const int32_t* q_lo, const int32_t* q_hi,
+                          int Q, double scale, uint16_t* vlo, uint16_t* vhi,
+                          unsigned long long* pooled, int64_t* zero_counts, uint32_t* site_hist,
+                          hipStream_t s);
 void launch_pct_accumulate(const uint16_t* vlo, const uint16_t* vhi, int64_t n_sites, int Q,
                            const double* gamma, double* acc, hipStream_t s);
 void launch_finalize(const double* mean, const double* m2, int64_t n, int64_t npx, double* out_mean,

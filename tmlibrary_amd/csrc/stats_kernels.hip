@@ -28,16 +28,21 @@ namespace tmh {
 // ---------------------------------------------------------------------------
 
 // x = stats transform of one pixel value.  LOG: np.log10 with 0 -> 0 from the
-// host-numpy LUT for values < kLutLds (LDS), ocml log10 for the rare larger
+// host-numpy LUT for values < kWfLut (LDS), ocml log10 for the rare larger
 // ones (VALU, no global load: a global load here would make the compiler
 // wait vmcnt(0) for the prefetched sites before every pixel).
 __device__ __noinline__ double log10_slow(uint32_t u) { return log10((double)u); }
 
+// LUT entries staged in LDS: 4032 x 8 B leaves room for one Welford
+// workgroup beside a histogram workgroup (131,264 B) in a CU's 160 KiB, so
+// the two passes can run concurrently
+constexpr int kWfLut = 4032;
+
 template <bool LOG>
 __device__ __forceinline__ double xform(uint32_t u, const double* slut) {
   if (!LOG) return (double)u;
-  double x = slut[u < (uint32_t)kLutLds ? u : 0u];
-  if (u >= (uint32_t)kLutLds) x = log10_slow(u);
+  double x = slut[u < (uint32_t)kWfLut ? u : 0u];
+  if (u >= (uint32_t)kWfLut) x = log10_slow(u);
   return x;
 }
 
@@ -47,15 +52,32 @@ __device__ __forceinline__ void welford1(double x, double rn, double& mu, double
   m2 = fma(d, x - mu, m2);      // M2 + delta * (x - mean_new)
 }
 
+// One branch per 8 pixels (not per pixel): gather all 8 from the LDS LUT,
+// then patch the rare values beyond it.
 template <bool LOG>
 __device__ __forceinline__ void welford8(const uint4 v, double rn, double (&mu)[8],
                                          double (&m2)[8], const double* slut) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  const uint32_t u[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
+                         v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
+  double x[8];
+  if (LOG) {
+    uint32_t mx = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    welford1(xform<LOG>(w[k] & 0xFFFFu, slut), rn, mu[2 * k], m2[2 * k]);
-    welford1(xform<LOG>(w[k] >> 16, slut), rn, mu[2 * k + 1], m2[2 * k + 1]);
+    for (int k = 0; k < 8; ++k) {
+      mx = u[k] > mx ? u[k] : mx;
+      x[k] = slut[u[k] < (uint32_t)kWfLut ? u[k] : 0u];
+    }
+    if (mx >= (uint32_t)kWfLut) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (u[k] >= (uint32_t)kWfLut) x[k] = log10_slow(u[k]);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = (double)u[k];
   }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) welford1(x[k], rn, mu[k], m2[k]);
 }
 
 constexpr int kWfThreads = 256;
@@ -72,9 +94,9 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
     const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites,
     const double* __restrict__ rn, double* __restrict__ mean, double* __restrict__ m2,
     const double* __restrict__ lut) {
-  __shared__ double slut[kLutLds];
+  __shared__ double slut[kWfLut];
   if (LOG)
-    for (int i = threadIdx.x; i < kLutLds; i += kWfThreads) slut[i] = lut[i];
+    for (int i = threadIdx.x; i < kWfLut; i += kWfThreads) slut[i] = lut[i];
   __syncthreads();
   const int64_t ngroups = npx >> 3;
   const int64_t g = (int64_t)blockIdx.x * kWfThreads + threadIdx.x;
@@ -124,9 +146,9 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_scalar(
     const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites,
     const double* __restrict__ rn, double* __restrict__ mean, double* __restrict__ m2,
     const double* __restrict__ lut) {
-  __shared__ double slut[kLutLds];
+  __shared__ double slut[kWfLut];
   if (LOG)
-    for (int i = threadIdx.x; i < kLutLds; i += kWfThreads) slut[i] = lut[i];
+    for (int i = threadIdx.x; i < kWfLut; i += kWfThreads) slut[i] = lut[i];
   __syncthreads();
   const int64_t p = (int64_t)blockIdx.x * kWfThreads + threadIdx.x;
   if (p >= npx) return;
@@ -239,6 +261,39 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, in
   return woff + incl - c;
 }
 
+// Walk the 65,536 bins in 64 rounds of 1024 consecutive bins, thread t
+// owning bin 1024*j + t: reads are conflict-free/coalesced, and the dense part
+// of a microscopy histogram (a few thousand adjacent values) is spread over
+// every thread, so the percentile scatter is balanced.  count(b) returns the
+// site's count of value b.
+template <typename CountFn>
+__device__ __forceinline__ void hist_tail(CountFn count, int64_t s,
+                                          const int32_t* __restrict__ q_lo,
+                                          const int32_t* __restrict__ q_hi, int Q, double scale,
+                                          uint16_t* __restrict__ vlo_all,
+                                          uint16_t* __restrict__ vhi_all,
+                                          unsigned long long* __restrict__ pooled,
+                                          int64_t* __restrict__ zero_counts,
+                                          uint32_t* __restrict__ site_hist, uint32_t* slots) {
+  const int tid = threadIdx.x;
+  uint16_t* vlo = vlo_all + s * (int64_t)Q;
+  uint16_t* vhi = vhi_all + s * (int64_t)Q;
+  int64_t base = 0;  // exclusive rank of the current round's first bin
+  for (int j = 0; j < kBins / kHistThreads; ++j) {
+    const uint32_t b = (uint32_t)j * kHistThreads + tid;
+    const uint32_t c = count(b);
+    uint32_t total;
+    const int64_t r = base + block_exscan(c, slots, j, &total);
+    base += total;
+    if (site_hist) site_hist[s * kBins + b] = c;
+    if (b == 0 && zero_counts) zero_counts[s] = c;
+    if (c) {
+      atomicAdd(&pooled[b], (unsigned long long)c);
+      scatter_bin(b, r, r + c, q_lo, q_hi, Q, scale, vlo, vhi);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
     const uint16_t* __restrict__ sites, int64_t npx, int vec, uint32_t* __restrict__ hist_hi,
     const int32_t* __restrict__ q_lo, const int32_t* __restrict__ q_hi, int Q, double scale,
@@ -283,32 +338,44 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // Walk the 65,536 bins in 64 rounds of 1024 consecutive bins, thread t
-  // owning bin 1024*j + t: LDS reads are conflict-free, and the dense part of
-  // a microscopy histogram (a few thousand adjacent values) is spread over
-  // every thread, so the percentile scatter is balanced.
-  uint16_t* vlo = vlo_all + s * (int64_t)Q;
-  uint16_t* vhi = vhi_all + s * (int64_t)Q;
-  int64_t base = 0;  // exclusive rank of the current round's first bin
-  for (int j = 0; j < kBins / kHistThreads; ++j) {
-    const uint32_t b = (uint32_t)j * kHistThreads + tid;
-    uint32_t c;
-    if (b < (uint32_t)kLdsBins) {
-      c = bins[b];
-    } else {
-      const uint32_t h = b - kLdsBins;
-      c = ((himask[h >> 11] >> ((h >> 6) & 31u)) & 1u) ? atomicExch(&hhi[h], 0u) : 0u;
-    }
-    uint32_t total;
-    const int64_t r = base + block_exscan(c, slots, j, &total);
-    base += total;
-    if (site_hist) site_hist[s * kBins + b] = c;
-    if (b == 0 && zero_counts) zero_counts[s] = c;
-    if (c) {
-      atomicAdd(&pooled[b], (unsigned long long)c);
-      scatter_bin(b, r, r + c, q_lo, q_hi, Q, scale, vlo, vhi);
-    }
-  }
+  hist_tail(
+      [&](uint32_t b) -> uint32_t {
+        if (b < (uint32_t)kLdsBins) return bins[b];
+        const uint32_t h = b - kLdsBins;
+        return ((himask[h >> 11] >> ((h >> 6) & 31u)) & 1u) ? atomicExch(&hhi[h], 0u) : 0u;
+      },
+      s, q_lo, q_hi, Q, scale, vlo_all, vhi_all, pooled, zero_counts, site_hist, slots);
+}
+
+// Per-site histogram (65,536 counts, exact) -> order statistics, written from
+// a complete histogram held in global memory (zero-maintained: every count is
+// read and reset), e.g. accumulated by the fused correct+histogram pass.
+__global__ __launch_bounds__(kHistThreads) void k_hist_finalize(
+    uint32_t* __restrict__ hist, const int32_t* __restrict__ q_lo,
+    const int32_t* __restrict__ q_hi, int Q, double scale, uint16_t* __restrict__ vlo_all,
+    uint16_t* __restrict__ vhi_all, unsigned long long* __restrict__ pooled,
+    int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist) {
+  __shared__ uint32_t slots[32];
+  const int64_t s = blockIdx.x;
+  uint32_t* h = hist + s * (int64_t)kBins;
+  hist_tail(
+      [&](uint32_t b) -> uint32_t {
+        const uint32_t c = h[b];
+        if (c) h[b] = 0u;
+        return c;
+      },
+      s, q_lo, q_hi, Q, scale, vlo_all, vhi_all, pooled, zero_counts, site_hist, slots);
+}
+
+void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const int32_t* q_lo, const int32_t* q_hi,
+                          int Q, double scale, uint16_t* vlo, uint16_t* vhi,
+                          unsigned long long* pooled, int64_t* zero_counts, uint32_t* site_hist,
+                          hipStream_t s) {
+  if (n_sites <= 0) return;
+  ProfScope prof("hist_finalize", s);
+  hipLaunchKernelGGL(k_hist_finalize, dim3((unsigned)n_sites), dim3(kHistThreads), 0, s, hist, q_lo,
+                     q_hi, Q, scale, vlo, vhi, pooled, zero_counts, site_hist);
+  TMH_HIP(hipGetLastError());
 }
 
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,

@@ -22,6 +22,7 @@ TMH_EDEVICE = -5
 TMH_ESTATE = -71
 TMH_STATS_DEFERRED_PCT = 1
 TMH_STATS_KEEP_SITE_HIST = 2
+TMH_STATS_SERIAL = 4
 
 _P = C.c_void_p
 _I64 = C.c_int64

@@ -84,6 +84,52 @@ __global__ __launch_bounds__(256) void k_copy_pm(const uint4* __restrict__ p, ui
   }
 }
 
+// welford ablation: MODE 0 = production math, 1 = x = (double)u (no LUT),
+// 2 = LUT gather + plain sum (no Welford), 3 = loads + int sum only
+template <int MODE>
+__global__ __launch_bounds__(256) void k_wf_abl(const uint16_t* __restrict__ sites, int64_t npx,
+                                                int64_t n_sites, const double* __restrict__ rn,
+                                                double* __restrict__ mean, double* __restrict__ m2,
+                                                const double* __restrict__ lut) {
+  __shared__ double slut[4096];
+  for (int i = threadIdx.x; i < 4096; i += 256) slut[i] = lut[i];
+  __syncthreads();
+  const int64_t ngroups = npx >> 3;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= ngroups) return;
+  double mu[8], q[8];
+  for (int k = 0; k < 8; ++k) { mu[k] = mean[g * 8 + k]; q[k] = m2[g * 8 + k]; }
+  const uint4* src = reinterpret_cast<const uint4*>(sites) + g;
+  const int64_t last = n_sites - 1;
+  uint4 cur[4], nxt[4];
+  uint32_t isum = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) cur[k] = src[(k < last ? k : last) * ngroups];
+  for (int64_t s = 0; s < n_sites; s += 4) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { const int64_t t = s + 4 + k; nxt[k] = src[(t < last ? t : last) * ngroups]; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (s + k >= n_sites) continue;
+      const double r = rn[s + k];
+      const uint32_t w[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t u = (j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFF);
+        if (MODE == 3) { isum += u; continue; }
+        double x = (MODE == 1) ? (double)u : slut[u & 4095];
+        if (MODE == 2) { mu[j] += x; continue; }
+        const double d = x - mu[j];
+        mu[j] = fma(d, r, mu[j]);
+        q[j] = fma(d, x - mu[j], q[j]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+  }
+  for (int k = 0; k < 8; ++k) { mean[g * 8 + k] = mu[k] + isum; m2[g * 8 + k] = q[k]; }
+}
+
 // hist ablation: MODE 0 = loads + integer sum only, 1 = LDS atomics (no hi branch),
 // 2 = LDS atomics with 8 loads in flight
 template <int MODE>
@@ -212,6 +258,21 @@ int main(int argc, char** argv) {
     t.start();
     launch_welford(sites, npx, S, 0, rn, mean, m2, lut, 1, 0);
     report("welford (prod)", t.stop(), S * site_gb);
+  }
+  for (int r = 0; r < reps; ++r) {
+    const dim3 gr((unsigned)cdiv(npx / 8, 256));
+    t.start();
+    hipLaunchKernelGGL(k_wf_abl<0>, gr, dim3(256), 0, 0, sites, npx, S, rn, mean, m2, lut);
+    report("welford abl: full", t.stop(), S * site_gb);
+    t.start();
+    hipLaunchKernelGGL(k_wf_abl<1>, gr, dim3(256), 0, 0, sites, npx, S, rn, mean, m2, lut);
+    report("welford abl: no LUT", t.stop(), S * site_gb);
+    t.start();
+    hipLaunchKernelGGL(k_wf_abl<2>, gr, dim3(256), 0, 0, sites, npx, S, rn, mean, m2, lut);
+    report("welford abl: LUT+sum", t.stop(), S * site_gb);
+    t.start();
+    hipLaunchKernelGGL(k_wf_abl<3>, gr, dim3(256), 0, 0, sites, npx, S, rn, mean, m2, lut);
+    report("welford abl: loads only", t.stop(), S * site_gb);
   }
   // hist ablations
   for (int r = 0; r < reps; ++r) {
