@@ -48,6 +48,9 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=24,
                    help="sites in the bounded CPU-baseline sample (0 disables)")
     p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
+    p.add_argument("--pipeline", choices=["fused", "separate"], default="separate",
+                   help="fused: histograms built from the correction's read (6 B/px); "
+                        "separate: Welford || histogram pass, then correct (8 B/px)")
     p.add_argument("--serial-stats", action="store_true",
                    help="run the histogram pass after Welford instead of concurrently")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
@@ -98,7 +101,7 @@ def main():
     from tmlibrary_amd import hip
     from tmlibrary_amd.image import ZERO_LOG10
     from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
-    from tmlibrary_amd.workflow.corilla.sharded import StatsOps, merge_shards
+    from tmlibrary_amd.workflow.corilla.sharded import StatsOps, merge_percentiles, merge_welford
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -140,11 +143,17 @@ def main():
                                             H, W, 1, ZERO_LOG10, sp, C.byref(corr)))
     ops = StatsOps(L, h, npx, Q, dev)
 
+    fused = a.pipeline == "fused"
+    S_ptr, O_ptr = C.c_void_p(sites.data_ptr()), C.c_void_p(out.data_ptr())
+
     def step():
         hip.check(L.tmh_stats_reset(h))
-        hip.check(L.tmh_stats_update_device(h, C.c_void_p(sites.data_ptr()), S, 1, sp))
+        if fused:  # Welford pass; histograms come from the correction's read
+            hip.check(L.tmh_stats_update_welford_device(h, S_ptr, S, 1, sp))
+        else:
+            hip.check(L.tmh_stats_update_device(h, S_ptr, S, 1, sp))
         if world > 1:
-            merge_shards(ops, dist)
+            merge_welford(ops, dist)
         hip.check(L.tmh_stats_finalize_device(h, C.c_void_p(mean.data_ptr()),
                                               C.c_void_p(std.data_ptr()), sp))
         hip.check(L.tmh_smooth_f64_device(C.c_void_p(mean.data_ptr()), C.c_void_p(smean.data_ptr()),
@@ -153,8 +162,12 @@ def main():
                                           C.c_void_p(tmp.data_ptr()), H, W, 5.0, sp))
         hip.check(L.tmh_corrector_update_device(corr, C.c_void_p(smean.data_ptr()),
                                                 C.c_void_p(sstd.data_ptr()), sp))
-        hip.check(L.tmh_correct_u16_device(corr, C.c_void_p(sites.data_ptr()),
-                                           C.c_void_p(out.data_ptr()), S, -1, -1, sp))
+        if fused:
+            hip.check(L.tmh_correct_u16_hist_device(corr, h, S_ptr, O_ptr, S, -1, -1, sp))
+        else:
+            hip.check(L.tmh_correct_u16_device(corr, S_ptr, O_ptr, S, -1, -1, sp))
+        if world > 1:
+            merge_percentiles(ops, dist)
 
     for _ in range(a.warmup):
         step()
@@ -182,7 +195,8 @@ def main():
     # per-kernel event timing on the launch stream (live roofline)
     kern = {}
     if prof:
-        for name in ("welford", "hist", "pct_acc", "finalize", "smooth", "coeffs", "correct"):
+        for name in ("welford", "hist", "pct_acc", "finalize", "smooth", "coeffs", "correct",
+                     "correct_hist", "hist_finalize"):
             ms, k = C.c_double(), C.c_int64()
             hip.check(L.tmh_profile_read(name.encode(), C.byref(ms), C.byref(k)))
             if k.value:
@@ -195,6 +209,7 @@ def main():
             "welford": S * site_bytes + 4 * 8 * npx,       # sites + mean/M2 read & write
             "hist": S * site_bytes,                        # sites
             "correct": S * site_bytes * 2 + 16 * npx,      # sites in + out, coefficients
+            "correct_hist": S * site_bytes * 2 + 8 * npx,  # sites in + out, coefficients
             "pct_acc": S * Q * 4,                          # per-site order statistics
         }
         kdetail = {}
@@ -245,7 +260,8 @@ def main():
                        "smoothing_sigma": 5, "clip": None,
                        "parallelism": "sites sharded (contiguous); RCCL all-reduce Welford "
                                       "merge + ordered percentile chain" if world > 1
-                                      else "single GPU"},
+                                      else "single GPU",
+                       "pipeline": a.pipeline},
             "job_hbm_roofline_frac": round(job_bytes * a.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world), 4),
             "roofline": roofline,
             "kernels": kdetail,

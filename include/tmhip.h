@@ -86,6 +86,17 @@ int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites,
 int tmh_stats_update_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
                             int log_transform, void* stream);
 
+/* Split job pipeline (one read of the sites per pass):
+ *   tmh_stats_update_welford_device  Welford only; the sites' percentile
+ *                                    contributions are left pending
+ *   tmh_correct_u16_hist_device      (below) corrects the SAME sites, in the
+ *                                    same order, and builds their histograms
+ *                                    from that read, completing the pending
+ *                                    percentile state.
+ * Results are identical to tmh_stats_update_device + tmh_correct_u16_device. */
+int tmh_stats_update_welford_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
+                                    int log_transform, void* stream);
+
 /* Host copies of the results; any output may be NULL.
  *   n            sites accumulated (stats.py:89)
  *   mean, std    [height*width] f64; std is NaN where n < 2 (stats.py:94-112)
@@ -156,6 +167,11 @@ int tmh_correct_u16(tmh_corrector* c, const uint16_t* host_in, uint16_t* host_ou
                     int64_t n_sites, int clip_lo, int clip_hi);
 int tmh_correct_u16_device(tmh_corrector* c, const uint16_t* dev_in, uint16_t* dev_out,
                            int64_t n_sites, int clip_lo, int clip_hi, void* stream);
+/* Correct n_sites pending sites of h and fold their histograms/percentiles
+ * into h (see tmh_stats_update_welford_device). */
+int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* dev_in,
+                                uint16_t* dev_out, int64_t n_sites, int clip_lo, int clip_hi,
+                                void* stream);
 int tmh_correct_u8(tmh_corrector* c, const uint8_t* host_in, uint8_t* host_out, int64_t n_sites,
                    int clip_lo, int clip_hi);
 /* ChannelImage.clip alone (image.py:589), u16. */

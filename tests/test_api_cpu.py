@@ -61,3 +61,20 @@ def test_stats_rejects_bad_decimals():
         OnlineStatistics((4, 4), decimals=4)
     with pytest.raises(ValueError):
         OnlineStatistics((4, 4), decimals=-1)
+
+
+def test_create_run_batches(tmp_path, caplog):
+    from tmlibrary_amd.models.file import ExperimentStore
+    from tmlibrary_amd.workflow.corilla.api import SITE_LIMIT, IllumstatsCalculator
+    calc = IllumstatsCalculator(1, store=ExperimentStore(str(tmp_path)))
+    files = {3: list(range(50)), 1: list(range(1000, 1000 + SITE_LIMIT + 7)), 2: []}
+    with caplog.at_level("WARNING"):
+        batches = list(calc.create_run_batches(channel_files=files, seed=0))
+    assert [b["channel_id"] for b in batches] == [1, 3]
+    assert [b["id"] for b in batches] == [1, 2]
+    big = [f[0] for f in batches[0]["channel_image_files_ids"]]
+    assert len(big) == SITE_LIMIT and len(set(big)) == SITE_LIMIT
+    assert set(big) <= set(files[1])
+    assert [f[0] for f in batches[1]["channel_image_files_ids"]] == files[3]
+    msgs = " ".join(r.message for r in caplog.records)
+    assert "only 50 images" in msgs and 'no image files found for channel "2"' in msgs

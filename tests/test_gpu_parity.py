@@ -381,3 +381,75 @@ def test_run_job_end_to_end(L, tmp_path):
     cont = store.illumstats_file(5).get()
     assert cont.mean.metadata.is_smoothed
     assert np.allclose(cont.mean.array, orc.smooth_reflect(g["mean"]), rtol=1e-9, atol=1e-12)
+
+
+def _fused_job(L, sites, clip=(-1, -1)):
+    """Split pipeline through the C-ABI: Welford-only update -> finalize ->
+    smooth -> corrector -> fused correct+histogram.  Returns host results."""
+    from tmlibrary_amd import hip
+    from tmlibrary_amd.image import ZERO_LOG10
+    from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
+    n, H, W = sites.shape
+    npx = H * W
+    lo, hi, gamma = quantile_table(npx, np.linspace(0, 100, 100000))
+    lut = stats_log10_lut()
+    h = C.c_void_p()
+    hip.check(L.tmh_stats_create(H, W, 100000, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
+                                 hip.ptr(lut), 4, hip.TMH_STATS_KEEP_SITE_HIST, C.byref(h)))
+    d_in, d_out = Dev(L, sites.nbytes), Dev(L, sites.nbytes)
+    d_in.put(sites)
+    planes = [Dev(L, npx * 8) for _ in range(5)]
+    mean, std, smean, sstd, tmp = planes
+    hip.check(L.tmh_stats_update_welford_device(h, d_in.p, n, 1, None))
+    hip.check(L.tmh_stats_finalize_device(h, mean.p, std.p, None))
+    L.tmh_synchronize(None)
+    hip.check(L.tmh_smooth_f64_device(mean.p, smean.p, tmp.p, H, W, 5.0, None))
+    hip.check(L.tmh_smooth_f64_device(std.p, sstd.p, tmp.p, H, W, 5.0, None))
+    L.tmh_synchronize(None)
+    c = C.c_void_p()
+    hip.check(L.tmh_corrector_create_device(smean.p, sstd.p, H, W, 1, ZERO_LOG10, None, C.byref(c)))
+    hip.check(L.tmh_correct_u16_hist_device(c, h, d_in.p, d_out.p, n, clip[0], clip[1], None))
+    L.tmh_synchronize(None)
+    acc = np.empty(100000)
+    nn = C.c_int64()
+    m_h = np.empty((H, W))
+    s_h = np.empty((H, W))
+    hist = np.empty(65536, np.uint64)
+    hip.check(L.tmh_stats_finalize(h, C.byref(nn), hip.ptr(m_h), hip.ptr(s_h), hip.ptr(acc),
+                                   hip.ptr(hist)))
+    site_h = []
+    for i in range(n):
+        sh = np.empty(65536, np.uint32)
+        hip.check(L.tmh_stats_site_histogram(h, i, hip.ptr(sh)))
+        site_h.append(sh)
+    out = d_out.get(np.uint16, sites.shape)
+    res = dict(n=nn.value, mean=m_h, std=s_h, acc=acc, hist=hist, site_hist=site_h, out=out,
+               smean=smean.get(np.float64, (H, W)), sstd=sstd.get(np.float64, (H, W)))
+    L.tmh_corrector_destroy(c)
+    L.tmh_stats_destroy(h)
+    for b in planes + [d_in, d_out]:
+        b.free()
+    return res
+
+
+@pytest.mark.parametrize("kind", ["synth", "extremes"])
+def test_fused_correct_hist_pipeline(L, kind):
+    if kind == "synth":
+        from tmlibrary_amd.synth import synth_sites_host
+        sites = np.stack(synth_sites_host(7, 240, 320, seed=31))
+        sites[2, :4, :4] = 65535
+        sites[3, 5, :9] = 40000  # beyond the LDS bins and the LDS LUT
+    else:
+        sites = np.stack(load_golden("stats_extremes")["sites"])
+    r = _fused_job(L, sites)
+    ref = orc.run_illumstats(list(sites))
+    assert r["n"] == len(sites)
+    assert_close_rel(r["mean"], ref.mean)
+    assert_close_rel(r["std"], ref.std)
+    assert np.array_equal(r["acc"], ref.percentile_sums), "fused percentile sums not bit-exact"
+    for s, sh in zip(sites, r["site_hist"]):
+        assert np.array_equal(sh.astype(np.uint64), orc.histogram_u16(s))
+    assert np.array_equal(r["hist"], sum(orc.histogram_u16(s) for s in sites))
+    for s, o in zip(sites, r["out"]):
+        want = orc.correct_illumination(s, r["smean"], r["sstd"])
+        assert dn_diff(o, want).max() <= 1

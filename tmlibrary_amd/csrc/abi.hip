@@ -126,11 +126,12 @@ struct tmh_stats {
   int64_t n = 0;              // sites accumulated (Welford count)
   int64_t n_deferred = 0;     // sites whose order statistics are stored
   int64_t last_batch = 0;
+  int64_t pending = 0;        // Welford-updated sites whose histograms are still to come
   bool pct_sum_external = false;
   DBuf<double> mean, m2, lut_log, gamma, acc, tmp_mean, tmp_std, rn;
   DBuf<int32_t> q_lo, q_hi;
   DBuf<unsigned long long> pooled;
-  DBuf<uint32_t> hist_hi, site_hist;
+  DBuf<uint32_t> hist_hi, site_hist, hist_full;
   DBuf<uint16_t> vlo, vhi, stage;
   DBuf<int64_t> zeros;
 };
@@ -142,7 +143,9 @@ struct tmh_corrector {
   int log_transform = 1;
   hipStream_t stream = nullptr;
   DBuf<float4> coef;
-  DBuf<float2> lut, mconst;
+  DBuf<float2> lut, mconst, coef2;
+  DBuf<int> queues;
+  int n_wg = 256;
   DBuf<double> sums, partial;
   DBuf<uint16_t> stage_in, stage_out;
   DBuf<uint8_t> stage8_in, stage8_out;
@@ -298,6 +301,7 @@ int tmh_stats_reset(tmh_stats* h) {
     h->n = 0;
     h->n_deferred = 0;
     h->last_batch = 0;
+    h->pending = 0;
     h->pct_sum_external = false;
   });
 }
@@ -347,6 +351,22 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
     TMH_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
   }
   h->n += ns;
+}
+
+int tmh_stats_update_welford_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
+                                    int log_transform, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && (dev_sites || n_sites == 0) && n_sites >= 0, TMH_EINVAL, "bad arguments");
+    hipStream_t s = pick(h->stream, stream);
+    if ((size_t)n_sites > h->rn.n) {
+      TMH_HIP(hipStreamSynchronize(s));
+      h->rn.alloc((size_t)n_sites);
+    }
+    launch_welford(dev_sites, h->npx, n_sites, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
+                   log_transform, s);
+    h->n += n_sites;
+    h->pending += n_sites;
+  });
 }
 
 int tmh_stats_update_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
@@ -564,13 +584,17 @@ static void corrector_coeffs(tmh_corrector* c, const double* d_mean, const doubl
   launch_reduce_sum(d_std, c->npx, c->partial.p, np, c->sums.p, s);
   launch_reduce_sum(d_mean, c->npx, c->partial.p, np, c->sums.p + 1, s);
   launch_coeffs(d_mean, d_std, c->sums.p, c->npx, c->coef.p, c->mconst.p, s);
+  launch_coeffs2(d_mean, d_std, c->sums.p, c->npx, c->coef2.p, s);
 }
 
 static void corrector_init(tmh_corrector* c, const double* d_mean, const double* d_std) {
   c->sums.alloc(2);
   c->partial.alloc(512);
   c->coef.alloc(c->npx);
+  c->coef2.alloc(c->npx);
   c->mconst.alloc(1);
+  c->queues.alloc(8, true);
+  TMH_HIP(hipDeviceGetAttribute(&c->n_wg, hipDeviceAttributeMultiprocessorCount, c->device));
   corrector_coeffs(c, d_mean, d_std, c->stream);
 }
 
@@ -694,6 +718,72 @@ int tmh_correct_u8(tmh_corrector* c, const uint8_t* host_in, uint8_t* host_out, 
                       c->mconst.p, c->log_transform, clip_lo, clip_hi, c->stream);
     TMH_HIP(hipMemcpyAsync(host_out, c->stage8_out.p, bytes, hipMemcpyDeviceToHost, c->stream));
     TMH_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* dev_in,
+                                uint16_t* dev_out, int64_t n_sites, int clip_lo, int clip_hi,
+                                void* stream) {
+  return guard([&] {
+    TMH_CHECK(c && h && (dev_in && dev_out || n_sites == 0) && n_sites >= 0, TMH_EINVAL,
+              "bad arguments");
+    TMH_CHECK(c->npx == h->npx, TMH_EINVAL, "corrector and statistics image sizes differ");
+    TMH_CHECK(n_sites <= h->pending, TMH_ESTATE,
+              "more sites than were passed to tmh_stats_update_welford_device");
+    check_clip(clip_lo, clip_hi, 65535);
+    hipStream_t s = pick(c->stream, stream);
+    const bool vec = (h->npx & 7) == 0 && (reinterpret_cast<uintptr_t>(dev_in) & 15) == 0 &&
+                     (reinterpret_cast<uintptr_t>(dev_out) & 15) == 0;
+    const int64_t chunk = 4096;
+    for (int64_t c0 = 0; c0 < n_sites; c0 += chunk) {
+      const int64_t nc = std::min(chunk, n_sites - c0);
+      const uint16_t* din = dev_in + c0 * h->npx;
+      uint16_t* dout = dev_out + c0 * h->npx;
+      // per-site buffers (growing frees memory earlier launches may still use)
+      const bool grow = (size_t)nc * kBins > h->hist_full.n || (size_t)nc > h->zeros.n ||
+                        ((h->flags & 2u) && (size_t)nc * kBins > h->site_hist.n) ||
+                        (!(h->flags & TMH_STATS_DEFERRED_PCT) && (size_t)nc * h->Q > h->vlo.n);
+      if (grow) {
+        TMH_HIP(hipStreamSynchronize(s));
+        TMH_HIP(hipStreamSynchronize(h->stream));
+        TMH_HIP(hipStreamSynchronize(h->side));
+      }
+      if ((size_t)nc * kBins > h->hist_full.n) h->hist_full.alloc((size_t)nc * kBins, true);
+      h->zeros.ensure((size_t)nc);
+      if (h->flags & 2u) h->site_hist.ensure((size_t)nc * kBins);
+      uint16_t *vlo, *vhi;
+      if (h->flags & TMH_STATS_DEFERRED_PCT) {
+        stats_grow_deferred(h, nc);
+        vlo = h->vlo.p + (size_t)h->n_deferred * h->Q;
+        vhi = h->vhi.p + (size_t)h->n_deferred * h->Q;
+      } else {
+        h->vlo.ensure((size_t)nc * h->Q);
+        h->vhi.ensure((size_t)nc * h->Q);
+        vlo = h->vlo.p;
+        vhi = h->vhi.p;
+      }
+      if (vec) {
+        launch_correct_hist(din, dout, c->npx, nc, c->coef2.p, c->lut.p, c->mconst.p,
+                            c->log_transform, clip_lo, clip_hi, h->hist_full.p, c->queues.p,
+                            c->n_wg, s);
+        launch_hist_finalize(h->hist_full.p, nc, h->q_lo.p, h->q_hi.p, h->Q, h->scale, vlo, vhi,
+                             h->pooled.p, h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr,
+                             s);
+      } else {  // odd shapes: correct and histogram in two passes
+        stats_reserve_sites(h, nc);
+        launch_correct_u16(din, dout, c->npx, nc, c->coef.p, c->lut.p, c->mconst.p,
+                           c->log_transform, clip_lo, clip_hi, s);
+        launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->q_lo.p, h->q_hi.p, h->Q, h->scale,
+                            vlo, vhi, h->pooled.p, h->zeros.p,
+                            (h->flags & 2u) ? h->site_hist.p : nullptr, s);
+      }
+      if (h->flags & TMH_STATS_DEFERRED_PCT)
+        h->n_deferred += nc;
+      else
+        launch_pct_accumulate(vlo, vhi, nc, h->Q, h->gamma.p, h->acc.p, s);
+      h->last_batch = nc;
+      h->pending -= nc;
+    }
   });
 }
 

@@ -42,6 +42,7 @@ SIGNATURES = {
     "tmh_stats_reset": (_I, [_P]),
     "tmh_stats_update": (_I, [_P, _P, _I64, _I, _P]),
     "tmh_stats_update_device": (_I, [_P, _P, _I64, _I, _P]),
+    "tmh_stats_update_welford_device": (_I, [_P, _P, _I64, _I, _P]),
     "tmh_stats_finalize": (_I, [_P, _P, _P, _P, _P, _P]),
     "tmh_stats_finalize_device": (_I, [_P, _P, _P, _P]),
     "tmh_stats_site_histogram": (_I, [_P, _I64, _P]),
@@ -61,6 +62,7 @@ SIGNATURES = {
     "tmh_corrector_means": (_I, [_P, C.POINTER(_D), C.POINTER(_D)]),
     "tmh_correct_u16": (_I, [_P, _P, _P, _I64, _I, _I]),
     "tmh_correct_u16_device": (_I, [_P, _P, _P, _I64, _I, _I, _P]),
+    "tmh_correct_u16_hist_device": (_I, [_P, _P, _P, _P, _I64, _I, _I, _P]),
     "tmh_correct_u8": (_I, [_P, _P, _P, _I64, _I, _I]),
     "tmh_clip_u16": (_I, [_P, _P, _I64, _I, _I]),
     "tmh_synth_sites_device": (_I, [_P, _I64, _I, _I, C.c_uint64, _I, _I64, _P]),

@@ -47,6 +47,40 @@ class IllumstatsCalculator(object):
         self.batch_size = batch_size
         self.prefetch = prefetch
 
+    def create_run_batches(self, args=None, channel_files=None, channel_names=None, seed=None):
+        """One job per channel (corilla/api.py:45-105).
+
+        ``channel_files`` maps channel id -> list of channel image file ids
+        (the database query of the reference).  More than SITE_LIMIT files:
+        a random subset of SITE_LIMIT (the reference orders by
+        ``random()``; ``seed`` makes the draw reproducible); fewer than 100:
+        warning; none: warning and no batch.  Yields the batch dicts
+        ``{'id', 'channel_image_files_ids', 'channel_id'}``.
+        """
+        import random
+        channel_files = channel_files if channel_files is not None else {}
+        names = channel_names or {}
+        rng = random.Random(seed)
+        count = 0
+        for ch_id in sorted(channel_files):
+            name = names.get(ch_id, str(ch_id))
+            file_ids = list(channel_files[ch_id])
+            n = len(file_ids)
+            if n > SITE_LIMIT:
+                logger.info('using a subset of image files (n=%d) to calculate '
+                            'illumination statistics for channel "%s"', SITE_LIMIT, name)
+                file_ids = rng.sample(file_ids, SITE_LIMIT)
+            elif n < 100:
+                logger.warning('calculation of illumnation statistics for channel "%s" on '
+                               'only %d images - this may introduce artifacts upon '
+                               'illumination correction', name, n)
+            if not file_ids:
+                logger.warning('no image files found for channel "%s"', name)
+                continue
+            count += 1
+            yield {"id": count, "channel_image_files_ids": [[f] for f in file_ids],
+                   "channel_id": ch_id}
+
     def _images(self, file_ids):
         """Yield (file_id, ChannelImage) in order, decoded one thread ahead."""
         q = queue.Queue(maxsize=max(1, self.prefetch))

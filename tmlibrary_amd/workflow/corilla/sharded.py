@@ -79,16 +79,10 @@ class StatsOps(object):
         self._chk(self.L.tmh_stats_set_pct_sum(self.h, C.c_void_p(acc.data_ptr()), self._stream()))
 
 
-def merge_shards(ops, dist, group=None, int_device=None):
-    """Merge every rank's partial statistics into identical global state.
-
-    ``ops`` provides n_local/empty_plane/empty_acc/stage1-3/pct_accumulate/
-    set_pct_sum on this rank's state; ``dist`` is torch.distributed.
-    Returns the global site count.
-    """
+def merge_welford(ops, dist, group=None, int_device=None):
+    """All-reduce merge of every rank's Welford state (identical on all ranks).
+    Returns the global site count."""
     import torch
-    rank = dist.get_rank(group)
-    world = dist.get_world_size(group)
     dev = int_device if int_device is not None else getattr(ops, "device", "cpu")
     n_t = torch.tensor([ops.n_local()], dtype=torch.int64, device=dev)
     dist.all_reduce(n_t, group=group)
@@ -101,7 +95,15 @@ def merge_shards(ops, dist, group=None, int_device=None):
         ops.stage2(buf, n_total, m2c)
         dist.all_reduce(m2c, group=group)
         ops.stage3(n_total, m2c)
-    # ordered percentile chain (bit-exact sequential summation)
+    return n_total
+
+
+def merge_percentiles(ops, dist, group=None):
+    """Ordered percentile chain: the f64 accumulator travels rank 0 -> N-1,
+    each rank adding its own sites in order (bit-exact sequential sum), and
+    the last rank broadcasts it."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
     acc = ops.empty_acc()
     if rank > 0:
         dist.recv(acc, src=rank - 1, group=group)
@@ -110,6 +112,18 @@ def merge_shards(ops, dist, group=None, int_device=None):
         dist.send(acc, dst=rank + 1, group=group)
     dist.broadcast(acc, src=world - 1, group=group)
     ops.set_pct_sum(acc)
+
+
+def merge_shards(ops, dist, group=None, int_device=None):
+    """Merge every rank's partial statistics into identical global state
+    (Welford all-reduce merge, then the ordered percentile chain).
+
+    ``ops`` provides n_local/empty_plane/empty_acc/stage1-3/pct_accumulate/
+    set_pct_sum on this rank's state; ``dist`` is torch.distributed.
+    Returns the global site count.
+    """
+    n_total = merge_welford(ops, dist, group, int_device)
+    merge_percentiles(ops, dist, group)
     return n_total
 
 
