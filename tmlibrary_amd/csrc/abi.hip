@@ -141,8 +141,9 @@ struct tmh_corrector {
   int H = 0, W = 0;
   int64_t npx = 0;
   int log_transform = 1;
+  double zero_log10 = -10.0;
   hipStream_t stream = nullptr;
-  DBuf<float4> coef;
+  DBuf<float4> coef, mconst2;
   DBuf<float2> lut, mconst, coef2;
   DBuf<int> queues;
   int n_wg = 256;
@@ -584,7 +585,8 @@ static void corrector_coeffs(tmh_corrector* c, const double* d_mean, const doubl
   launch_reduce_sum(d_std, c->npx, c->partial.p, np, c->sums.p, s);
   launch_reduce_sum(d_mean, c->npx, c->partial.p, np, c->sums.p + 1, s);
   launch_coeffs(d_mean, d_std, c->sums.p, c->npx, c->coef.p, c->mconst.p, s);
-  launch_coeffs2(d_mean, d_std, c->sums.p, c->npx, c->coef2.p, s);
+  launch_coeffs2(d_mean, d_std, c->sums.p, c->npx, c->log_transform, c->zero_log10, c->coef2.p,
+                 c->mconst2.p, s);
 }
 
 static void corrector_init(tmh_corrector* c, const double* d_mean, const double* d_std) {
@@ -593,6 +595,7 @@ static void corrector_init(tmh_corrector* c, const double* d_mean, const double*
   c->coef.alloc(c->npx);
   c->coef2.alloc(c->npx);
   c->mconst.alloc(1);
+  c->mconst2.alloc(1);
   c->queues.alloc(8, true);
   TMH_HIP(hipDeviceGetAttribute(&c->n_wg, hipDeviceAttributeMultiprocessorCount, c->device));
   corrector_coeffs(c, d_mean, d_std, c->stream);
@@ -610,6 +613,7 @@ int tmh_corrector_create_device(const double* dev_mean, const double* dev_std, i
       c->W = width;
       c->npx = (int64_t)height * width;
       c->log_transform = log_transform ? 1 : 0;
+      c->zero_log10 = zero_log10;
       c->stream = (hipStream_t)stream;
       c->lut.alloc(kBins);
       launch_build_corr_lut(c->lut.p, c->log_transform, zero_log10, c->stream);
@@ -763,9 +767,8 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         vhi = h->vhi.p;
       }
       if (vec) {
-        launch_correct_hist(din, dout, c->npx, nc, c->coef2.p, c->lut.p, c->mconst.p,
-                            c->log_transform, clip_lo, clip_hi, h->hist_full.p, c->queues.p,
-                            c->n_wg, s);
+        launch_correct_hist(din, dout, c->npx, nc, c->coef2.p, c->mconst2.p, c->log_transform,
+                            clip_lo, clip_hi, h->hist_full.p, c->queues.p, c->n_wg, s);
         launch_hist_finalize(h->hist_full.p, nc, h->q_lo.p, h->q_hi.p, h->Q, h->scale, vlo, vhi,
                              h->pooled.p, h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr,
                              s);

@@ -87,11 +87,12 @@ void launch_correct_u8(const uint8_t* in, uint8_t* out, int64_t npx, int64_t n_s
                        const float4* coef, const float2* lut, const float2* mconst,
                        int log_transform, int clip_lo, int clip_hi, hipStream_t s);
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
-                         const float2* coef2, const float2* lut, const float2* mconst,
-                         int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
-                         int* queues, int n_wg, hipStream_t s);
+                         const float2* coef2, const float4* mconst2, int log_transform,
+                         int clip_lo, int clip_hi, uint32_t* hist, int* queues, int n_wg,
+                         hipStream_t s);
 void launch_coeffs2(const double* mean, const double* std, const double* sums, int64_t npx,
-                    float2* coef2, hipStream_t s);
+                    int log_transform, double zero_log10, float2* coef2, float4* mconst2,
+                    hipStream_t s);
 void launch_clip_u16(const uint16_t* in, uint16_t* out, int64_t n, int lo, int hi, hipStream_t s);
 void launch_synth(uint16_t* out, int64_t n_sites, int H, int W, uint64_t seed, int channel,
                   int64_t first_site, hipStream_t s);

@@ -236,8 +236,9 @@ __device__ __forceinline__ void scatter_bin(uint32_t b, int64_t start, int64_t e
 }
 
 // Exclusive scan of one value per thread over the 1024-thread workgroup.
-// `slots` holds 2 x 16 wave totals (double-buffered by `round` parity, so one
-// barrier per round suffices).  Returns the exclusive prefix; *total = sum.
+// `slots` holds 2 x 16 wave totals (double-buffered by the parity of the
+// caller's scan counter, so one barrier per scan suffices).  Returns the
+// exclusive prefix; *total = sum.
 __device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, int round,
                                                  uint32_t* total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -261,35 +262,69 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, in
   return woff + incl - c;
 }
 
+constexpr int kTailChunk = 8;  // rounds whose counts are loaded together
+
 // Walk the 65,536 bins in 64 rounds of 1024 consecutive bins, thread t
 // owning bin 1024*j + t: reads are conflict-free/coalesced, and the dense part
 // of a microscopy histogram (a few thousand adjacent values) is spread over
 // every thread, so the percentile scatter is balanced.  count(b) returns the
-// site's count of value b.
-template <typename CountFn>
-__device__ __forceinline__ void hist_tail(CountFn count, int64_t s,
+// site's count of value b.  Counts are fetched kTailChunk rounds at a time
+// (the next chunk's loads in flight while the current one is scanned) and
+// rounds that are empty for the whole workgroup are skipped, so a typical
+// microscopy site (values < ~10,000 plus saturation) scans ~12 rounds.
+// `cmask` is 3 words of LDS (chunk masks, triple-buffered).  done(b, c) is
+// called once per bin after its count has been used (e.g. to reset it).
+template <typename CountFn, typename DoneFn>
+__device__ __forceinline__ void hist_tail(CountFn count, DoneFn done, int64_t s,
                                           const int32_t* __restrict__ q_lo,
                                           const int32_t* __restrict__ q_hi, int Q, double scale,
                                           uint16_t* __restrict__ vlo_all,
                                           uint16_t* __restrict__ vhi_all,
                                           unsigned long long* __restrict__ pooled,
                                           int64_t* __restrict__ zero_counts,
-                                          uint32_t* __restrict__ site_hist, uint32_t* slots) {
+                                          uint32_t* __restrict__ site_hist, uint32_t* slots,
+                                          uint32_t* cmask) {
   const int tid = threadIdx.x;
   uint16_t* vlo = vlo_all + s * (int64_t)Q;
   uint16_t* vhi = vhi_all + s * (int64_t)Q;
   int64_t base = 0;  // exclusive rank of the current round's first bin
-  for (int j = 0; j < kBins / kHistThreads; ++j) {
-    const uint32_t b = (uint32_t)j * kHistThreads + tid;
-    const uint32_t c = count(b);
-    uint32_t total;
-    const int64_t r = base + block_exscan(c, slots, j, &total);
-    base += total;
-    if (site_hist) site_hist[s * kBins + b] = c;
-    if (b == 0 && zero_counts) zero_counts[s] = c;
-    if (c) {
-      atomicAdd(&pooled[b], (unsigned long long)c);
-      scatter_bin(b, r, r + c, q_lo, q_hi, Q, scale, vlo, vhi);
+  int nscan = 0;
+  uint32_t cn[kTailChunk];
+#pragma unroll
+  for (int k = 0; k < kTailChunk; ++k) cn[k] = count((uint32_t)k * kHistThreads + tid);
+  for (int jc = 0; jc < kBins / kHistThreads; jc += kTailChunk) {
+    uint32_t c[kTailChunk];
+#pragma unroll
+    for (int k = 0; k < kTailChunk; ++k) c[k] = cn[k];
+    if (jc + kTailChunk < kBins / kHistThreads) {
+#pragma unroll
+      for (int k = 0; k < kTailChunk; ++k)
+        cn[k] = count((uint32_t)(jc + kTailChunk + k) * kHistThreads + tid);
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < kTailChunk; ++k) m |= (c[k] != 0u ? 1u : 0u) << k;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m |= (uint32_t)__shfl_xor((int)m, off, 64);
+    const int slot = (jc / kTailChunk) % 3;
+    if (tid == 0) cmask[(slot + 1) % 3] = 0u;
+    if ((tid & 63) == 0 && m) atomicOr(&cmask[slot], m);
+    __syncthreads();
+    const uint32_t mask = cmask[slot];
+#pragma unroll
+    for (int k = 0; k < kTailChunk; ++k) {
+      const uint32_t b = (uint32_t)(jc + k) * kHistThreads + tid;
+      if (site_hist) site_hist[s * kBins + b] = c[k];
+      if (b == 0 && zero_counts) zero_counts[s] = c[k];
+      done(b, c[k]);
+      if (!((mask >> k) & 1u)) continue;  // uniform: no counts in this round
+      uint32_t total;
+      const int64_t r = base + block_exscan(c[k], slots, nscan++, &total);
+      base += total;
+      if (c[k]) {
+        atomicAdd(&pooled[b], (unsigned long long)c[k]);
+        scatter_bin(b, r, r + c[k], q_lo, q_hi, Q, scale, vlo, vhi);
+      }
     }
   }
 }
@@ -303,12 +338,14 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
   __shared__ __attribute__((aligned(16))) uint32_t bins[kLdsBins];
   __shared__ uint32_t himask[16];
   __shared__ uint32_t slots[32];
+  __shared__ uint32_t cmask[3];
   const int tid = threadIdx.x;
   const int64_t s = blockIdx.x;
 
   for (int i = tid; i < kLdsBins / 4; i += kHistThreads)
     reinterpret_cast<uint4*>(bins)[i] = make_uint4(0u, 0u, 0u, 0u);
   if (tid < 16) himask[tid] = 0u;
+  if (tid < 3) cmask[tid] = 0u;
   __syncthreads();
 
   const uint16_t* site = sites + s * npx;
@@ -344,7 +381,8 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
         const uint32_t h = b - kLdsBins;
         return ((himask[h >> 11] >> ((h >> 6) & 31u)) & 1u) ? atomicExch(&hhi[h], 0u) : 0u;
       },
-      s, q_lo, q_hi, Q, scale, vlo_all, vhi_all, pooled, zero_counts, site_hist, slots);
+      [](uint32_t, uint32_t) {},
+      s, q_lo, q_hi, Q, scale, vlo_all, vhi_all, pooled, zero_counts, site_hist, slots, cmask);
 }
 
 // Per-site histogram (65,536 counts, exact) -> order statistics, written from
@@ -356,15 +394,17 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_finalize(
     uint16_t* __restrict__ vhi_all, unsigned long long* __restrict__ pooled,
     int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist) {
   __shared__ uint32_t slots[32];
+  __shared__ uint32_t cmask[3];
   const int64_t s = blockIdx.x;
+  if (threadIdx.x < 3) cmask[threadIdx.x] = 0u;
+  __syncthreads();
   uint32_t* h = hist + s * (int64_t)kBins;
   hist_tail(
-      [&](uint32_t b) -> uint32_t {
-        const uint32_t c = h[b];
+      [&](uint32_t b) -> uint32_t { return h[b]; },
+      [&](uint32_t b, uint32_t c) {
         if (c) h[b] = 0u;
-        return c;
       },
-      s, q_lo, q_hi, Q, scale, vlo_all, vhi_all, pooled, zero_counts, site_hist, slots);
+      s, q_lo, q_hi, Q, scale, vlo_all, vhi_all, pooled, zero_counts, site_hist, slots, cmask);
 }
 
 void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const int32_t* q_lo, const int32_t* q_hi,

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../tmlibrary_amd/csrc/common.h"
+#include "../../tmlibrary_amd/csrc/fused_kernels.hip"
 
 #define CK(x)                                                                  \
   do {                                                                         \
@@ -26,7 +27,7 @@
 
 using namespace tmh;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st_nt(uint4* p, uint4 v) {
+__device__ __forceinline__ void mb_st_nt(uint4* p, uint4 v) {
   u32x4 w = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
 }
@@ -59,7 +60,7 @@ __global__ __launch_bounds__(256) void k_copy_u(const uint4* __restrict__ p, uin
 #pragma unroll
     for (int k = 0; k < U; ++k)
       if (i + k * stride < n) {
-        if (NT) st_nt(q + i + k * stride, v[k]);
+        if (NT) mb_st_nt(q + i + k * stride, v[k]);
         else q[i + k * stride] = v[k];
       }
   }
@@ -78,7 +79,7 @@ __global__ __launch_bounds__(256) void k_copy_pm(const uint4* __restrict__ p, ui
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (s + k < n_sites) {
-        if (NT) st_nt(q + (s + k) * ngroups + g, v[k]);
+        if (NT) mb_st_nt(q + (s + k) * ngroups + g, v[k]);
         else q[(s + k) * ngroups + g] = v[k];
       }
   }
@@ -332,6 +333,39 @@ int main(int argc, char** argv) {
     t.start();
     launch_correct_u16(sites, out, npx, S, coef, clut, mconst, 1, -1, -1, 0);
     report("correct (prod)", t.stop(), 2 * S * site_gb);
+  }
+  // fused correct+hist ablations (persistent, 1 WG per CU)
+  {
+    int n_cu = 0;
+    CK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, 0));
+    float2* coef2;
+    float4* mconst2;
+    uint32_t* hist;
+    int* queues;
+    CK(hipMalloc(&coef2, npx * 8));
+    CK(hipMalloc(&mconst2, 16));
+    CK(hipMalloc(&hist, S * kBins * 4));
+    CK(hipMalloc(&queues, 64));
+    CK(hipMemset(hist, 0, S * kBins * 4));
+    launch_coeffs2(mean, m2, sums, npx, 1, -10.0, coef2, mconst2, 0);
+    const int bpx = getenv("MB_BANDS") ? atoi(getenv("MB_BANDS")) : 2;
+    auto run = [&](auto kern, const char* name) {
+      for (int r = 0; r < reps; ++r) {
+        CK(hipMemset(queues, 0, 64));
+        t.start();
+        hipLaunchKernelGGL(kern, dim3(n_cu), dim3(kFThreads), 0, 0, sites, out, npx, S, coef2,
+                           mconst2, -1, -1, hist, queues, bpx);
+        report(name, t.stop(), 2 * S * site_gb);
+      }
+    };
+    run(k_correct_hist<true, 1, 0>, "fused spu1: full");
+    run(k_correct_hist<true, 2, 0>, "fused spu2: full");
+    run(k_correct_hist<true, 4, 0>, "fused spu4: full");
+    run(k_correct_hist<true, 2, 8>, "fused spu2: no flush");
+    run(k_correct_hist<true, 2, 1>, "fused spu2: no hist");
+    run(k_correct_hist<true, 2, 2>, "fused spu2: const coef");
+    run(k_correct_hist<true, 2, 3>, "fused spu2: math only");
+    run(k_correct_hist<true, 1, 3>, "fused spu1: math only");
   }
   CK(hipDeviceSynchronize());
   printf("done\n");
