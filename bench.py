@@ -48,7 +48,7 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=24,
                    help="sites in the bounded CPU-baseline sample (0 disables)")
     p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
-    p.add_argument("--pipeline", choices=["fused", "separate"], default="separate",
+    p.add_argument("--pipeline", choices=["fused", "separate"], default="fused",
                    help="fused: histograms built from the correction's read (6 B/px); "
                         "separate: Welford || histogram pass, then correct (8 B/px)")
     p.add_argument("--serial-stats", action="store_true",

@@ -432,13 +432,21 @@ def _fused_job(L, sites, clip=(-1, -1)):
     return res
 
 
-@pytest.mark.parametrize("kind", ["synth", "extremes"])
+@pytest.mark.parametrize("kind", ["synth", "extremes", "uniform", "tiny", "many"])
 def test_fused_correct_hist_pipeline(L, kind):
+    from tmlibrary_amd.synth import synth_sites_host
+    rng = np.random.default_rng(97)
     if kind == "synth":
-        from tmlibrary_amd.synth import synth_sites_host
         sites = np.stack(synth_sites_host(7, 240, 320, seed=31))
         sites[2, :4, :4] = 65535
         sites[3, 5, :9] = 40000  # beyond the LDS bins and the LDS LUT
+    elif kind == "uniform":  # most values beyond the per-site LDS slices
+        sites = rng.integers(0, 65536, size=(6, 96, 160), dtype=np.uint16)
+    elif kind == "tiny":  # bands far narrower than a workgroup
+        sites = np.stack(synth_sites_host(5, 16, 24, seed=5))
+    elif kind == "many":  # several site groups per band, ragged last group
+        sites = np.stack(synth_sites_host(37, 64, 96, seed=8))
+        sites[::5, 3, :] = 65000
     else:
         sites = np.stack(load_golden("stats_extremes")["sites"])
     r = _fused_job(L, sites)

@@ -35,7 +35,6 @@
 namespace tmh {
 
 constexpr int kBandsPerXcd = 2;  // default; TMH_FUSED_BANDS overrides (experiments)
-constexpr int kFThreads = 1024;
 constexpr double kLog2_10 = 3.32192809488736234787;
 
 __device__ __forceinline__ int xcc_id() {
@@ -85,62 +84,112 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 }
 
 // ABL: development ablations (tools/mb), 0 in production: 1 = no histogram,
-// 2 = constant coefficients, 8 = no flush
-template <bool LOG, int SPU, int ABL = 0>
-__global__ __launch_bounds__(kFThreads) void k_correct_hist(
+// 2 = constant coefficients, 8 = no flush.
+// NT threads per workgroup, LB LDS bins per workgroup (split into SPU slices).
+// Each workgroup reserves its NEXT unit while it streams the current one, and
+// issues the next unit's first loads before it flushes the current unit's
+// histogram slices, so the flush (LDS scan + global atomics + barriers) runs
+// with the next unit's pixels already in flight.
+template <bool LOG, int SPU, int ABL, int NT, int LB>
+__global__ __launch_bounds__(NT, 4) void k_correct_hist(
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
     const float2* __restrict__ coef2, const float4* __restrict__ mconst2, int clip_lo,
     int clip_hi, uint32_t* __restrict__ hist, int* __restrict__ queues, int bands_per_xcd) {
-  constexpr int BINS = kLdsBins / SPU;
-  __shared__ __attribute__((aligned(16))) uint32_t bins[kLdsBins];
+  constexpr int BINS = LB / SPU;
+  __shared__ __attribute__((aligned(16))) uint32_t bins[LB];
   __shared__ int unit_sh;
   __shared__ uint32_t top_sh[SPU];
   const int tid = threadIdx.x;
-  for (int i = tid; i < kLdsBins / 4; i += kFThreads)
+  for (int i = tid; i < LB / 4; i += NT)
     reinterpret_cast<uint4*>(bins)[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (tid < SPU) top_sh[tid] = 0u;
 
   const float4 m = mconst2[0];
-  const int64_t ngroups = npx >> 3;
+  const int ngroups = (int)(npx >> 3);
+  const int site_bytes = (int)(npx * 2);
   const int n_bands = 8 * bands_per_xcd;
-  const int64_t n_groups_s = (n_sites + SPU - 1) / SPU;
-  const int64_t units_per_queue = bands_per_xcd * n_groups_s;
-  const uint4* src = reinterpret_cast<const uint4*>(in);
-  uint4* dst = reinterpret_cast<uint4*>(out);
+  const int n_groups_s = (int)((n_sites + SPU - 1) / SPU);
+  const int upq = bands_per_xcd * n_groups_s;  // units per queue
   // coefficient planes: plane k holds pixels 8g+2k, 8g+2k+1 of group g, so each
   // of a lane's four coefficient loads is one contiguous 1 KiB per wave
-  const float4* cf = reinterpret_cast<const float4*>(coef2);
+  const __amdgpu_buffer_rsrc_t rcf =
+      __builtin_amdgcn_make_buffer_rsrc((void*)coef2, 0, (int)(npx * 8), 0x00020000);
   const float4 cc = make_float4(2.5f, 1.1f, 2.4f, 0.9f);
 
+  // unit = (queue q, index u) -> band q + 8 * (u / n_groups_s), sites from s0
   int q = xcc_id(), exhausted = 0;
-  while (exhausted < 8) {
-    if (tid == 0) unit_sh = atomicAdd(&queues[q], 1);
-    if (tid < SPU) top_sh[tid] = 0u;
-    __syncthreads();
-    const int u = unit_sh;
-    __syncthreads();
-    if (u >= units_per_queue) {  // this queue is drained: steal from the next
-      q = (q + 1) & 7;
+  auto grab = [&]() -> int {
+    while (exhausted < 8) {
+      if (tid == 0) unit_sh = atomicAdd(&queues[q], 1);
+      __syncthreads();
+      const int u = __builtin_amdgcn_readfirstlane(unit_sh);
+      __syncthreads();
+      if (u < upq) {
+        exhausted = 0;
+        return q * upq + u;
+      }
+      q = (q + 1) & 7;  // this queue is drained: steal from the next
       ++exhausted;
-      continue;
     }
-    exhausted = 0;
-    const int band = q + 8 * (int)(u / n_groups_s);
-    const int64_t s0 = (u % n_groups_s) * SPU;
-    const int ns = (int)(n_sites - s0 < SPU ? n_sites - s0 : SPU);
-    const int64_t g0 = band * ngroups / n_bands, g1 = (band + 1) * ngroups / n_bands;
-    const uint4* sp = src + s0 * ngroups;
-    uint4* dp = dst + s0 * ngroups;
-    uint32_t* hs = hist + s0 * (int64_t)kBins;
+    return -1;
+  };
+  struct Unit {
+    int g0, g1, ns;
+    int64_t s0;
+    __amdgpu_buffer_rsrc_t rin, rout;  // the unit's SPU sites; loads past ns read 0
+  };
+  auto decode = [&](int code) -> Unit {
+    const int qq = code / upq, u = code % upq;
+    const int band = qq + 8 * (u / n_groups_s);
+    Unit r;
+    r.s0 = (int64_t)(u % n_groups_s) * SPU;
+    r.ns = (int)(n_sites - r.s0 < SPU ? n_sites - r.s0 : SPU);
+    r.g0 = (int)((int64_t)band * ngroups / n_bands);
+    r.g1 = (int)((int64_t)(band + 1) * ngroups / n_bands);
+    r.rin = __builtin_amdgcn_make_buffer_rsrc((void*)(in + r.s0 * npx), 0, r.ns * site_bytes,
+                                              0x00020000);
+    r.rout = __builtin_amdgcn_make_buffer_rsrc((void*)(out + r.s0 * npx), 0, r.ns * site_bytes,
+                                               0x00020000);
+    return r;
+  };
+  auto load = [&](const Unit& un, int g, uint4 (&v)[SPU], float4& c0, float4& c1, float4& c2,
+                  float4& c3) {
+    const int off = g * 16;
+#pragma unroll
+    for (int k = 0; k < SPU; ++k) {
+      const u32x4_t w = __builtin_amdgcn_raw_buffer_load_b128(un.rin, off, k * site_bytes, 2);
+      v[k] = make_uint4(w.x, w.y, w.z, w.w);
+    }
+    if (!(ABL & 2)) {
+      c0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rcf, off, 0, 0));
+      c1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rcf, off, ngroups * 16, 0));
+      c2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rcf, off, ngroups * 32, 0));
+      c3 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rcf, off, ngroups * 48, 0));
+    }
+  };
+
+  uint4 v[SPU];
+  float4 c0 = cc, c1 = cc, c2 = cc, c3 = cc;
+#pragma unroll
+  for (int k = 0; k < SPU; ++k) v[k] = make_uint4(0, 0, 0, 0);
+  bool pre = false;  // v/c already hold this unit's first group (loaded by the previous unit)
+  int cur = grab();
+  while (cur >= 0) {
+    const int nxt = grab();
+    const Unit un = decode(cur);
+    Unit nu = un;
+    if (nxt >= 0) nu = decode(nxt);
+    uint32_t* hs = hist + un.s0 * (int64_t)kBins;
     uint32_t top[SPU];
 #pragma unroll
     for (int k = 0; k < SPU; ++k) top[k] = 0u;
 
-    auto process = [&](const uint4 v, const int k, const float4 c0, const float4 c1,
-                       const float4 c2, const float4 c3) -> uint4 {
-      const uint32_t px[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
-                              v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
-      const float mu[8] = {c0.x, c0.z, c1.x, c1.z, c2.x, c2.z, c3.x, c3.z};
-      const float a[8] = {c0.y, c0.w, c1.y, c1.w, c2.y, c2.w, c3.y, c3.w};
+    auto process = [&](const uint4 w, const int k, const float4 k0, const float4 k1,
+                       const float4 k2, const float4 k3) -> u32x4_t {
+      const uint32_t px[8] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16,
+                              w.z & 0xFFFFu, w.z >> 16, w.w & 0xFFFFu, w.w >> 16};
+      const float mu[8] = {k0.x, k0.z, k1.x, k1.z, k2.x, k2.z, k3.x, k3.z};
+      const float a[8] = {k0.y, k0.w, k1.y, k1.w, k2.y, k2.w, k3.y, k3.w};
       uint32_t mx = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -158,62 +207,55 @@ __global__ __launch_bounds__(kFThreads) void k_correct_hist(
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         o[j] = fcorrect<LOG>(px[j], mu[j], a[j], m.x, m.y, m.z, clip_lo, clip_hi);
-      return make_uint4(o[0] | (o[1] << 16), o[2] | (o[3] << 16), o[4] | (o[5] << 16),
-                        o[6] | (o[7] << 16));
+      const u32x4_t r = {o[0] | (o[1] << 16), o[2] | (o[3] << 16), o[4] | (o[5] << 16),
+                         o[6] | (o[7] << 16)};
+      return r;
     };
 
-    // two-stage pipeline over the unit's pixel groups
-    int64_t g = g0 + tid;
-    uint4 v[SPU];
-    float4 c0 = cc, c1 = cc, c2 = cc, c3 = cc;
-#pragma unroll
-    for (int k = 0; k < SPU; ++k) v[k] = make_uint4(0, 0, 0, 0);
-    if (g < g1) {
-#pragma unroll
-      for (int k = 0; k < SPU; ++k)
-        if (k < ns) v[k] = ld_nt(sp + k * ngroups + g);
-      if (!(ABL & 2)) {
-        c0 = cf[g]; c1 = cf[ngroups + g]; c2 = cf[2 * ngroups + g]; c3 = cf[3 * ngroups + g];
-      }
-    }
-    while (g < g1) {
-      const int64_t gn = g + kFThreads;
+    int g = un.g0 + tid;
+    if (!pre && g < un.g1) load(un, g, v, c0, c1, c2, c3);
+    pre = false;
+    // two-stage pipeline over the unit's pixel groups; the last stage loads
+    // the next unit's first group
+    while (g < un.g1) {
+      const int gn = g + NT;
       uint4 vn[SPU];
       float4 n0 = cc, n1 = cc, n2 = cc, n3 = cc;
 #pragma unroll
       for (int k = 0; k < SPU; ++k) vn[k] = make_uint4(0, 0, 0, 0);
-      if (gn < g1) {
-#pragma unroll
-        for (int k = 0; k < SPU; ++k)
-          if (k < ns) vn[k] = ld_nt(sp + k * ngroups + gn);
-        if (!(ABL & 2)) {
-          n0 = cf[gn]; n1 = cf[ngroups + gn]; n2 = cf[2 * ngroups + gn]; n3 = cf[3 * ngroups + gn];
-        }
+      if (gn < un.g1) {
+        load(un, gn, vn, n0, n1, n2, n3);
+      } else if (nxt >= 0 && nu.g0 + tid < nu.g1) {
+        load(nu, nu.g0 + tid, vn, n0, n1, n2, n3);
+        pre = true;
       }
 #pragma unroll
       for (int k = 0; k < SPU; ++k)
-        if (k < ns) st_nt(dp + k * ngroups + g, process(v[k], k, c0, c1, c2, c3));
+        if (k < un.ns)
+          __builtin_amdgcn_raw_buffer_store_b128(process(v[k], k, c0, c1, c2, c3), un.rout,
+                                                 g * 16, k * site_bytes, 2);
 #pragma unroll
       for (int k = 0; k < SPU; ++k) v[k] = vn[k];
       c0 = n0; c1 = n1; c2 = n2; c3 = n3;
       g = gn;
     }
+    cur = nxt;
+    if (ABL & 9) continue;
     // largest value per site in this unit bounds the bins worth flushing
 #pragma unroll
     for (int k = 0; k < SPU; ++k) {
       const uint32_t t = wave_max(top[k]);
-      if ((tid & 63) == 0) atomicMax(&top_sh[k], t);
+      if ((tid & 63) == 0 && t) atomicMax(&top_sh[k], t);
     }
     __syncthreads();
-    if (ABL & 9) continue;
     // fold this unit's slices into the sites' histograms (contiguous lanes -> bins)
 #pragma unroll
     for (int k = 0; k < SPU; ++k) {
-      if (k >= ns) break;
+      if (k >= un.ns) break;
       const uint32_t t = top_sh[k];
       const int lim = (int)(t < (uint32_t)BINS ? t : (uint32_t)BINS - 1);
       uint32_t* h = hs + k * (int64_t)kBins;
-      for (int b = tid; b <= lim; b += kFThreads) {
+      for (int b = tid; b <= lim; b += NT) {
         const uint32_t c = bins[k * BINS + b];
         if (c) {
           atomicAdd(&h[b], c);
@@ -222,14 +264,16 @@ __global__ __launch_bounds__(kFThreads) void k_correct_hist(
       }
     }
     __syncthreads();
+    if (tid < SPU) top_sh[tid] = 0u;  // next write is after grab()'s barriers
   }
 }
 
-static int fused_spu() {
+// (SPU, threads, LDS bins) configurations; TMH_FUSED_CFG selects (experiments)
+static int fused_cfg() {
   static const int v = [] {
-    const char* e = getenv("TMH_FUSED_SPU");
-    const int x = e ? atoi(e) : 2;
-    return (x == 1 || x == 2 || x == 4) ? x : 2;
+    const char* e = getenv("TMH_FUSED_CFG");
+    const int x = e ? atoi(e) : 3;
+    return (x >= 0 && x <= 3) ? x : 3;
   }();
   return v;
 }
@@ -246,19 +290,23 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
     return v >= 1 && v <= 16 ? v : kBandsPerXcd;
   }();
   TMH_HIP(hipMemsetAsync(queues, 0, 8 * sizeof(int), s));
-#define TMH_LAUNCH_CH(L_, S_)                                                                  \
-  hipLaunchKernelGGL((k_correct_hist<L_, S_>), dim3(n_wg), dim3(kFThreads), 0, s, in, out, npx, \
-                     n_sites, coef2, mconst2, clip_lo, clip_hi, hist, queues, bpx)
-  const int spu = fused_spu();
-  if (log_transform) {
-    if (spu == 1) TMH_LAUNCH_CH(true, 1);
-    else if (spu == 2) TMH_LAUNCH_CH(true, 2);
-    else TMH_LAUNCH_CH(true, 4);
-  } else {
-    if (spu == 1) TMH_LAUNCH_CH(false, 1);
-    else if (spu == 2) TMH_LAUNCH_CH(false, 2);
-    else TMH_LAUNCH_CH(false, 4);
+#define TMH_LAUNCH_CH(L_, S_, T_, B_)                                                     \
+  hipLaunchKernelGGL((k_correct_hist<L_, S_, 0, T_, B_>), dim3(n_wg * (1024 / T_)), dim3(T_), \
+                     0, s, in, out, npx, n_sites, coef2, mconst2, clip_lo, clip_hi, hist,     \
+                     queues, bpx)
+#define TMH_LAUNCH_CFG(L_)                                 \
+  switch (fused_cfg()) {                                   \
+    case 0: TMH_LAUNCH_CH(L_, 2, 1024, 32768); break;      \
+    case 1: TMH_LAUNCH_CH(L_, 4, 1024, 32768); break;      \
+    case 2: TMH_LAUNCH_CH(L_, 2, 512, 16384); break;       \
+    default: TMH_LAUNCH_CH(L_, 4, 512, 16384); break;      \
   }
+  if (log_transform) {
+    TMH_LAUNCH_CFG(true);
+  } else {
+    TMH_LAUNCH_CFG(false);
+  }
+#undef TMH_LAUNCH_CFG
 #undef TMH_LAUNCH_CH
   TMH_HIP(hipGetLastError());
 }

@@ -28,10 +28,22 @@ namespace tmh {
 // ---------------------------------------------------------------------------
 
 // x = stats transform of one pixel value.  LOG: np.log10 with 0 -> 0 from the
-// host-numpy LUT for values < kWfLut (LDS), ocml log10 for the rare larger
-// ones (VALU, no global load: a global load here would make the compiler
-// wait vmcnt(0) for the prefetched sites before every pixel).
-__device__ __noinline__ double log10_slow(uint32_t u) { return log10((double)u); }
+// host-numpy LUT for values < kWfLut - 1 (LDS, bit-identical to numpy); the
+// rare larger values use the same LUT on their top bits,
+//   log10(u) = log10(a) + k log10(2) + log1p(t) / ln 10,  a = u >> k,
+//   t = (u - (a << k)) / (a << k) < 1/2015,
+// with a 3-term series (truncation < 7e-15 absolute): no transcendental and
+// few registers, so the rare branch does not cost the streaming loop waves.
+__device__ __forceinline__ double log10_slow(uint32_t u, const double* slut) {
+  const int k = u < 64496u ? 4 : 5;  // a <= 4030 < kWfLut - 1
+  const uint32_t a = u >> k;
+  const double den = (double)(a << k);
+  const double t = (double)(u - (a << k)) / den;
+  constexpr double kInvLn10 = 0.43429448190325182765;
+  constexpr double kLog10_2 = 0.30102999566398119521;
+  const double series = t * (kInvLn10 + t * (-0.5 * kInvLn10 + t * (kInvLn10 / 3.0)));
+  return slut[a] + (double)k * kLog10_2 + series;
+}
 
 // LUT entries staged in LDS: 4032 x 8 B leaves room for one Welford
 // workgroup beside a histogram workgroup (131,264 B) in a CU's 160 KiB, so
@@ -41,8 +53,8 @@ constexpr int kWfLut = 4032;
 template <bool LOG>
 __device__ __forceinline__ double xform(uint32_t u, const double* slut) {
   if (!LOG) return (double)u;
-  double x = slut[u < (uint32_t)kWfLut ? u : 0u];
-  if (u >= (uint32_t)kWfLut) x = log10_slow(u);
+  double x = slut[u < (uint32_t)kWfLut - 1 ? u : 0u];
+  if (u >= (uint32_t)kWfLut - 1) x = log10_slow(u, slut);
   return x;
 }
 
@@ -52,8 +64,10 @@ __device__ __forceinline__ void welford1(double x, double rn, double& mu, double
   m2 = fma(d, x - mu, m2);      // M2 + delta * (x - mean_new)
 }
 
-// One branch per 8 pixels (not per pixel): gather all 8 from the LDS LUT,
-// then patch the rare values beyond it.
+// One branch per 8 pixels (not per pixel): gather all 8 from the LDS LUT
+// (index clamped with one v_min), then patch the rare values beyond it one
+// lane-slot at a time, so a single inlined log10 serves all eight slots
+// (eight unrolled copies cost ~30 VGPRs and a wave per SIMD).
 template <bool LOG>
 __device__ __forceinline__ void welford8(const uint4 v, double rn, double (&mu)[8],
                                          double (&m2)[8], const double* slut) {
@@ -61,16 +75,17 @@ __device__ __forceinline__ void welford8(const uint4 v, double rn, double (&mu)[
                          v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
   double x[8];
   if (LOG) {
+    constexpr uint32_t kTop = kWfLut - 1;
     uint32_t mx = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       mx = u[k] > mx ? u[k] : mx;
-      x[k] = slut[u[k] < (uint32_t)kWfLut ? u[k] : 0u];
+      x[k] = slut[u[k] < kTop ? u[k] : kTop];
     }
-    if (mx >= (uint32_t)kWfLut) {
+    if (mx > kTop) {
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        if (u[k] >= (uint32_t)kWfLut) x[k] = log10_slow(u[k]);
+        if (u[k] > kTop) x[k] = log10_slow(u[k], slut);
     }
   } else {
 #pragma unroll

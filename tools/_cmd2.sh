@@ -1,0 +1,5 @@
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+MB_COPY=1 timeout -k 10 300 tools/mb/mb_stats 1024 3 > gpurun_out/mb_r1s2b.txt 2>&1 || exit $?
+echo mb ok

@@ -85,6 +85,156 @@ __global__ __launch_bounds__(256) void k_copy_pm(const uint4* __restrict__ p, ui
   }
 }
 
+
+// block-contiguous copy: one 1024-thread WG streams `chunk` uint4s in order
+template <int U, bool NT>
+__global__ __launch_bounds__(1024) void k_copy_blk(const uint4* __restrict__ p, uint4* __restrict__ q,
+                                                   int64_t chunk, int64_t n) {
+  const int64_t base = (int64_t)blockIdx.x * chunk;
+  const int64_t end = base + chunk < n ? base + chunk : n;
+  for (int64_t i = base + threadIdx.x; i < end; i += U * 1024) {
+    uint4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = (i + k * 1024 < end) ? p[i + k * 1024] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (i + k * 1024 < end) {
+        if (NT) mb_st_nt(q + i + k * 1024, v[k]);
+        else q[i + k * 1024] = v[k];
+      }
+  }
+}
+
+// block-contiguous read
+template <int U>
+__global__ __launch_bounds__(1024) void k_read_blk(const uint4* __restrict__ p, int64_t chunk,
+                                                   int64_t n, uint32_t* __restrict__ sink) {
+  const int64_t base = (int64_t)blockIdx.x * chunk;
+  const int64_t end = base + chunk < n ? base + chunk : n;
+  uint32_t acc = 0;
+  for (int64_t i = base + threadIdx.x; i < end; i += U * 1024) {
+    uint4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = (i + k * 1024 < end) ? p[i + k * 1024] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < U; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// welford over a site chunk (grid.y = chunks), partial states per chunk
+__global__ __launch_bounds__(256) void k_wf_split(const uint16_t* __restrict__ sites, int64_t npx,
+                                                  int64_t n_sites, const double* __restrict__ rn,
+                                                  double* __restrict__ mean, double* __restrict__ m2,
+                                                  const double* __restrict__ lut) {
+  __shared__ double slut[4096];
+  for (int i = threadIdx.x; i < 4096; i += 256) slut[i] = lut[i];
+  __syncthreads();
+  const int64_t ngroups = npx >> 3;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= ngroups) return;
+  const int64_t s0 = n_sites * blockIdx.y / gridDim.y, s1 = n_sites * (blockIdx.y + 1) / gridDim.y;
+  double mu[8], q[8];
+  for (int k = 0; k < 8; ++k) { mu[k] = 0; q[k] = 0; }
+  const uint4* src = reinterpret_cast<const uint4*>(sites) + g;
+  const int64_t last = s1 - 1;
+  uint4 cur[4], nxt[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) cur[k] = src[(s0 + k < last ? s0 + k : last) * ngroups];
+  for (int64_t s = s0; s < s1; s += 4) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { const int64_t t = s + 4 + k; nxt[k] = src[(t < last ? t : last) * ngroups]; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (s + k >= s1) continue;
+      const double r = rn[s + k - s0];
+      const uint32_t w[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+      uint32_t mx = 0;
+      double x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t u = (j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFF);
+        mx = u > mx ? u : mx;
+        x[j] = slut[u & 4095];
+      }
+      if (mx >= 4096) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t u = (j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFF);
+          if (u >= 4096) x[j] = log10((double)u);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const double d = x[j] - mu[j];
+        mu[j] = fma(d, r, mu[j]);
+        q[j] = fma(d, x[j] - mu[j], q[j]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+  }
+  double* om = mean + blockIdx.y * npx;
+  double* oq = m2 + blockIdx.y * npx;
+  for (int k = 0; k < 8; ++k) { om[g * 8 + k] = mu[k]; oq[g * 8 + k] = q[k]; }
+}
+
+
+// production-shaped Welford variants: RARE=0 drops the >=4032 fix-up (timing
+// only), GROUP sites per pipeline stage, WPS min waves/SIMD launch bound
+template <int GROUP, bool RARE, int WPS>
+__global__ __launch_bounds__(256, WPS) void k_wf_var(const uint16_t* __restrict__ sites, int64_t npx,
+                                                     int64_t n_sites, const double* __restrict__ rn,
+                                                     double* __restrict__ mean, double* __restrict__ m2,
+                                                     const double* __restrict__ lut) {
+  constexpr int LUTN = 4032;
+  __shared__ double slut[LUTN];
+  for (int i = threadIdx.x; i < LUTN; i += 256) slut[i] = lut[i];
+  __syncthreads();
+  const int64_t ngroups = npx >> 3;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= ngroups) return;
+  double mu[8], q[8];
+  for (int k = 0; k < 8; ++k) { mu[k] = mean[g * 8 + k]; q[k] = m2[g * 8 + k]; }
+  const uint4* src = reinterpret_cast<const uint4*>(sites) + g;
+  const int64_t last = n_sites - 1;
+  uint4 cur[GROUP], nxt[GROUP];
+#pragma unroll
+  for (int k = 0; k < GROUP; ++k) cur[k] = src[(k < last ? k : last) * ngroups];
+  for (int64_t s = 0; s < n_sites; s += GROUP) {
+#pragma unroll
+    for (int k = 0; k < GROUP; ++k) { const int64_t t = s + GROUP + k; nxt[k] = src[(t < last ? t : last) * ngroups]; }
+#pragma unroll
+    for (int k = 0; k < GROUP; ++k) {
+      if (s + k >= n_sites) continue;
+      const double r = rn[s + k];
+      const uint32_t w[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+      uint32_t u[8], mx = 0;
+      double x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        u[j] = (j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFF);
+        mx = u[j] > mx ? u[j] : mx;
+        x[j] = slut[u[j] < (uint32_t)LUTN ? u[j] : 0u];
+      }
+      if (RARE && mx >= (uint32_t)LUTN) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (u[j] >= (uint32_t)LUTN) x[j] = log10((double)u[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const double d = x[j] - mu[j];
+        mu[j] = fma(d, r, mu[j]);
+        q[j] = fma(d, x[j] - mu[j], q[j]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < GROUP; ++k) cur[k] = nxt[k];
+  }
+  for (int k = 0; k < 8; ++k) { mean[g * 8 + k] = mu[k]; m2[g * 8 + k] = q[k]; }
+}
+
 // welford ablation: MODE 0 = production math, 1 = x = (double)u (no LUT),
 // 2 = LUT gather + plain sum (no Welford), 3 = loads + int sum only
 template <int MODE>
@@ -231,6 +381,55 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(k_copy_pm<true>, dim3((unsigned)cdiv(ng, 256)), dim3(256), 0, 0, (const uint4*)sites, (uint4*)out, ng, S);
     report("copy pixel-major nt", t.stop(), 2 * S * site_gb);
   }
+
+  if (getenv("MB_COPY")) {
+    const int64_t site16 = npx / 8;
+    for (int r = 0; r < reps; ++r) {
+      t.start();
+      hipLaunchKernelGGL((k_read_blk<4>), dim3((unsigned)cdiv(n16, site16)), dim3(1024), 0, 0, (const uint4*)sites, site16, n16, sink);
+      report("read blk site u4", t.stop(), S * site_gb);
+      t.start();
+      hipLaunchKernelGGL((k_read_blk<4>), dim3((unsigned)cdiv(n16, site16 / 16)), dim3(1024), 0, 0, (const uint4*)sites, site16 / 16, n16, sink);
+      report("read blk site/16 u4", t.stop(), S * site_gb);
+      t.start();
+      hipLaunchKernelGGL((k_copy_blk<4, false>), dim3((unsigned)cdiv(n16, site16)), dim3(1024), 0, 0, (const uint4*)sites, (uint4*)out, site16, n16);
+      report("copy blk site u4", t.stop(), 2 * S * site_gb);
+      t.start();
+      hipLaunchKernelGGL((k_copy_blk<4, true>), dim3((unsigned)cdiv(n16, site16)), dim3(1024), 0, 0, (const uint4*)sites, (uint4*)out, site16, n16);
+      report("copy blk site u4 nt", t.stop(), 2 * S * site_gb);
+      t.start();
+      hipLaunchKernelGGL((k_copy_blk<2, true>), dim3((unsigned)cdiv(n16, site16)), dim3(1024), 0, 0, (const uint4*)sites, (uint4*)out, site16, n16);
+      report("copy blk site u2 nt", t.stop(), 2 * S * site_gb);
+      t.start();
+      hipLaunchKernelGGL((k_copy_blk<8, true>), dim3((unsigned)cdiv(n16, site16)), dim3(1024), 0, 0, (const uint4*)sites, (uint4*)out, site16, n16);
+      report("copy blk site u8 nt", t.stop(), 2 * S * site_gb);
+      t.start();
+      hipLaunchKernelGGL((k_copy_blk<4, true>), dim3((unsigned)cdiv(n16, site16 / 16)), dim3(1024), 0, 0, (const uint4*)sites, (uint4*)out, site16 / 16, n16);
+      report("copy blk site/16 u4 nt", t.stop(), 2 * S * site_gb);
+      t.start();
+      hipLaunchKernelGGL((k_copy_blk<4, true>), dim3((unsigned)cdiv(n16, 65536)), dim3(1024), 0, 0, (const uint4*)sites, (uint4*)out, 65536, n16);
+      report("copy blk 1MB u4 nt", t.stop(), 2 * S * site_gb);
+      t.start();
+      hipLaunchKernelGGL((k_copy_blk<4, false>), dim3((unsigned)cdiv(n16, 65536)), dim3(1024), 0, 0, (const uint4*)sites, (uint4*)out, 65536, n16);
+      report("copy blk 1MB u4", t.stop(), 2 * S * site_gb);
+    }
+    double *pm, *pq, *rn2, *lut2;
+    CK(hipMalloc(&pm, 16 * npx * 8));
+    CK(hipMalloc(&pq, 16 * npx * 8));
+    CK(hipMalloc(&rn2, S * 8));
+    CK(hipMalloc(&lut2, 65536 * 8));
+    CK(hipMemset(rn2, 0, S * 8));
+    CK(hipMemset(lut2, 0, 65536 * 8));
+    for (int r = 0; r < reps; ++r) {
+      for (int c : {1, 2, 4, 8, 16}) {
+        t.start();
+        hipLaunchKernelGGL(k_wf_split, dim3((unsigned)cdiv(npx / 8, 256), c), dim3(256), 0, 0, sites, npx, S, rn2, pm, pq, lut2);
+        char nm[64];
+        snprintf(nm, sizeof nm, "welford split %d", c);
+        report(nm, t.stop(), S * site_gb);
+      }
+    }
+  }
   // Infinity-cache probe: re-read a buffer that fits (128 MB) vs one that doesn't
   for (int64_t mb : {64, 128, 200, 512, 4096}) {
     const int64_t n = mb * (1 << 20) / 16;
@@ -259,6 +458,23 @@ int main(int argc, char** argv) {
     t.start();
     launch_welford(sites, npx, S, 0, rn, mean, m2, lut, 1, 0);
     report("welford (prod)", t.stop(), S * site_gb);
+  }
+
+  if (getenv("MB_WF")) {
+    const dim3 gr((unsigned)cdiv(npx / 8, 256));
+    auto runw = [&](auto kern, const char* name) {
+      for (int r = 0; r < reps; ++r) {
+        t.start();
+        hipLaunchKernelGGL(kern, gr, dim3(256), 0, 0, sites, npx, S, rn, mean, m2, lut);
+        report(name, t.stop(), S * site_gb);
+      }
+    };
+    runw(k_wf_var<4, true, 1>, "wfvar g4 rare");
+    runw(k_wf_var<4, false, 1>, "wfvar g4 norare");
+    runw(k_wf_var<2, true, 1>, "wfvar g2 rare");
+    runw(k_wf_var<4, true, 5>, "wfvar g4 rare wps5");
+    runw(k_wf_var<2, true, 6>, "wfvar g2 rare wps6");
+    runw(k_wf_var<8, true, 1>, "wfvar g8 rare");
   }
   for (int r = 0; r < reps; ++r) {
     const dim3 gr((unsigned)cdiv(npx / 8, 256));
@@ -349,23 +565,25 @@ int main(int argc, char** argv) {
     CK(hipMemset(hist, 0, S * kBins * 4));
     launch_coeffs2(mean, m2, sums, npx, 1, -10.0, coef2, mconst2, 0);
     const int bpx = getenv("MB_BANDS") ? atoi(getenv("MB_BANDS")) : 2;
-    auto run = [&](auto kern, const char* name) {
+    auto run = [&](auto kern, int nt, const char* name) {
       for (int r = 0; r < reps; ++r) {
         CK(hipMemset(queues, 0, 64));
         t.start();
-        hipLaunchKernelGGL(kern, dim3(n_cu), dim3(kFThreads), 0, 0, sites, out, npx, S, coef2,
+        hipLaunchKernelGGL(kern, dim3(n_cu * (1024 / nt)), dim3(nt), 0, 0, sites, out, npx, S, coef2,
                            mconst2, -1, -1, hist, queues, bpx);
         report(name, t.stop(), 2 * S * site_gb);
       }
     };
-    run(k_correct_hist<true, 1, 0>, "fused spu1: full");
-    run(k_correct_hist<true, 2, 0>, "fused spu2: full");
-    run(k_correct_hist<true, 4, 0>, "fused spu4: full");
-    run(k_correct_hist<true, 2, 8>, "fused spu2: no flush");
-    run(k_correct_hist<true, 2, 1>, "fused spu2: no hist");
-    run(k_correct_hist<true, 2, 2>, "fused spu2: const coef");
-    run(k_correct_hist<true, 2, 3>, "fused spu2: math only");
-    run(k_correct_hist<true, 1, 3>, "fused spu1: math only");
+    run(k_correct_hist<true, 2, 0, 1024, 32768>, 1024, "fused spu2 t1024: full");
+    run(k_correct_hist<true, 4, 0, 1024, 32768>, 1024, "fused spu4 t1024: full");
+    run(k_correct_hist<true, 2, 0, 512, 16384>, 512, "fused spu2 t512: full");
+    run(k_correct_hist<true, 4, 0, 512, 16384>, 512, "fused spu4 t512: full");
+    run(k_correct_hist<true, 4, 8, 1024, 32768>, 1024, "fused spu4 t1024: no flush");
+    run(k_correct_hist<true, 4, 1, 1024, 32768>, 1024, "fused spu4 t1024: no hist");
+    run(k_correct_hist<true, 4, 2, 1024, 32768>, 1024, "fused spu4 t1024: const coef");
+    run(k_correct_hist<true, 4, 3, 1024, 32768>, 1024, "fused spu4 t1024: math only");
+    run(k_correct_hist<true, 4, 3, 512, 16384>, 512, "fused spu4 t512: math only");
+    run(k_correct_hist<true, 2, 3, 512, 16384>, 512, "fused spu2 t512: math only");
   }
   CK(hipDeviceSynchronize());
   printf("done\n");
