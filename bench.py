@@ -65,7 +65,7 @@ def cpu_baseline(n_sites, H, W, total_sites):
     from oracle import corilla_oracle as orc
     from tmlibrary_amd.synth import synth_sites_host
     sites = synth_sites_host(n_sites, H, W, seed=2024)
-    st = orc.OracleOnlineStatistics((H, W))
+    st = orc.OracleOnlineStatistics((H, W), percentile="numpy")  # stats.py:76 as written
     t0 = time.perf_counter()
     for s in sites:
         st.update(s)
@@ -82,7 +82,8 @@ def cpu_baseline(n_sites, H, W, total_sites):
         "unit": "sites/s",
         "cores": 1,
         "kind": "port",
-        "sample": "%d synthetic %dx%d sites: oracle OnlineStatistics.update x%d + "
+        "sample": "%d synthetic %dx%d sites: oracle OnlineStatistics.update (np.percentile "
+                  "with 100,000 q, log10, Welford) x%d + "
                   "correct_illumination x%d (numpy, 1 process) + smoothing of 2 planes "
                   "amortised over %d sites; stats %.1f ms/site, correct %.1f ms/site"
                   % (n_sites, H, W, n_sites, n_sites, total_sites,

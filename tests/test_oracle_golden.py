@@ -121,3 +121,17 @@ def test_fullsize_inputs_reproducible():
                              seed=int(g["seed"]))
     for s, d in zip(sites, g["input_digest"]):
         assert hashlib.sha256(np.ascontiguousarray(s).tobytes()).hexdigest() == str(d)
+
+
+def test_numpy_percentile_mode_matches_cdf_mode():
+    """The CPU-baseline mode (np.percentile, stats.py:76 as written) and the
+    histogram/CDF restatement give identical sums."""
+    rng = np.random.default_rng(3)
+    sites = [rng.integers(0, 4000, size=(48, 64), dtype=np.uint16) for _ in range(3)]
+    a = orc.OracleOnlineStatistics((48, 64), percentile="numpy")
+    b = orc.OracleOnlineStatistics((48, 64))
+    for s in sites:
+        a.update(s)
+        b.update(s)
+    assert np.array_equal(a.percentile_sums, b.percentile_sums)
+    assert np.array_equal(a.mean, b.mean) and np.array_equal(a.std, b.std)
