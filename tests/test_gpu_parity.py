@@ -383,7 +383,7 @@ def test_run_job_end_to_end(L, tmp_path):
     assert np.allclose(cont.mean.array, orc.smooth_reflect(g["mean"]), rtol=1e-9, atol=1e-12)
 
 
-def _fused_job(L, sites, clip=(-1, -1)):
+def _fused_job(L, sites, clip=(-1, -1), q=None):
     """Split pipeline through the C-ABI: Welford-only update -> finalize ->
     smooth -> corrector -> fused correct+histogram.  Returns host results."""
     from tmlibrary_amd import hip
@@ -391,10 +391,12 @@ def _fused_job(L, sites, clip=(-1, -1)):
     from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
     n, H, W = sites.shape
     npx = H * W
-    lo, hi, gamma = quantile_table(npx, np.linspace(0, 100, 100000))
+    q = np.linspace(0, 100, 100000) if q is None else q
+    Q = len(q)
+    lo, hi, gamma = quantile_table(npx, q)
     lut = stats_log10_lut()
     h = C.c_void_p()
-    hip.check(L.tmh_stats_create(H, W, 100000, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
+    hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
                                  hip.ptr(lut), 4, hip.TMH_STATS_KEEP_SITE_HIST, C.byref(h)))
     d_in, d_out = Dev(L, sites.nbytes), Dev(L, sites.nbytes)
     d_in.put(sites)
@@ -410,7 +412,7 @@ def _fused_job(L, sites, clip=(-1, -1)):
     hip.check(L.tmh_corrector_create_device(smean.p, sstd.p, H, W, 1, ZERO_LOG10, None, C.byref(c)))
     hip.check(L.tmh_correct_u16_hist_device(c, h, d_in.p, d_out.p, n, clip[0], clip[1], None))
     L.tmh_synchronize(None)
-    acc = np.empty(100000)
+    acc = np.empty(Q)
     nn = C.c_int64()
     m_h = np.empty((H, W))
     s_h = np.empty((H, W))
@@ -461,3 +463,21 @@ def test_fused_correct_hist_pipeline(L, kind):
     for s, o in zip(sites, r["out"]):
         want = orc.correct_illumination(s, r["smean"], r["sstd"])
         assert dn_diff(o, want).max() <= 1
+
+
+@pytest.mark.parametrize("qkind", ["linspace", "custom"])
+def test_quantile_tables(L, qkind):
+    """Percentile sums stay bit-exact for the reference's linspace q
+    (stats.py:59-60, another Q) and for arbitrary non-uniform q tables."""
+    from tmlibrary_amd.synth import synth_sites_host
+    sites = np.stack(synth_sites_host(5, 120, 160, seed=12))
+    if qkind == "linspace":
+        q = np.linspace(0, 100, 10000)
+    else:
+        rng = np.random.default_rng(4)
+        q = np.concatenate([[0.0], np.sort(rng.uniform(0, 100, 997)), [99.99, 100.0]])
+    r = _fused_job(L, sites, q=q)
+    want = np.zeros(len(q))
+    for s in sites:
+        want += orc.percentile_linear(s, q)
+    assert np.array_equal(r["acc"], want)

@@ -130,8 +130,9 @@ struct tmh_stats {
   bool pct_sum_external = false;
   DBuf<double> mean, m2, lut_log, gamma, acc, tmp_mean, tmp_std, rn;
   DBuf<int32_t> q_lo, q_hi;
-  DBuf<unsigned long long> pooled;
+  DBuf<unsigned long long> pooled, pooled_parts;  // parts: kPooledParts zero-maintained copies
   DBuf<uint32_t> hist_hi, site_hist, hist_full;
+  QPos qp{};
   DBuf<uint16_t> vlo, vhi, stage;
   DBuf<int64_t> zeros;
 };
@@ -153,6 +154,8 @@ struct tmh_corrector {
 };
 
 static hipStream_t pick(hipStream_t own, void* s) { return s ? (hipStream_t)s : own; }
+
+constexpr int kPooledParts = 16;
 
 extern "C" {
 
@@ -264,6 +267,11 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
       TMH_HIP(hipMemcpy(h->q_hi.p, hi.data(), hi.size() * 4, hipMemcpyHostToDevice));
       TMH_HIP(hipMemcpy(h->gamma.p, q_gamma, (size_t)n_quantiles * 8, hipMemcpyHostToDevice));
       TMH_HIP(hipMemcpy(h->lut_log.p, lut_log10, (size_t)kBins * 8, hipMemcpyHostToDevice));
+      h->pooled_parts.alloc((size_t)kPooledParts * kBins, true);
+      h->qp.lo = h->q_lo.p;
+      h->qp.hi = h->q_hi.p;
+      h->qp.Q = n_quantiles;
+      h->qp.scale = h->scale;
     } catch (...) {
       tmh_stats_destroy(h);
       throw;
@@ -338,9 +346,8 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
       vlo = h->vlo.p;
       vhi = h->vhi.p;
     }
-    launch_hist_scatter(d + c0 * h->npx, h->npx, nc, h->hist_hi.p, h->q_lo.p, h->q_hi.p, h->Q,
-                        h->scale, vlo, vhi, h->pooled.p, h->zeros.p,
-                        (h->flags & 2u) ? h->site_hist.p : nullptr, hs);
+    launch_hist_scatter(d + c0 * h->npx, h->npx, nc, h->hist_hi.p, h->qp, vlo, vhi, h->pooled.p,
+                        h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr, hs);
     if (h->flags & TMH_STATS_DEFERRED_PCT)
       h->n_deferred += nc;
     else
@@ -769,15 +776,14 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       if (vec) {
         launch_correct_hist(din, dout, c->npx, nc, c->coef2.p, c->mconst2.p, c->log_transform,
                             clip_lo, clip_hi, h->hist_full.p, c->queues.p, c->n_wg, s);
-        launch_hist_finalize(h->hist_full.p, nc, h->q_lo.p, h->q_hi.p, h->Q, h->scale, vlo, vhi,
-                             h->pooled.p, h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr,
+        launch_hist_finalize(h->hist_full.p, nc, h->qp, vlo, vhi, h->pooled.p, h->pooled_parts.p,
+                             kPooledParts, h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr,
                              s);
       } else {  // odd shapes: correct and histogram in two passes
         stats_reserve_sites(h, nc);
         launch_correct_u16(din, dout, c->npx, nc, c->coef.p, c->lut.p, c->mconst.p,
                            c->log_transform, clip_lo, clip_hi, s);
-        launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->q_lo.p, h->q_hi.p, h->Q, h->scale,
-                            vlo, vhi, h->pooled.p, h->zeros.p,
+        launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->qp, vlo, vhi, h->pooled.p, h->zeros.p,
                             (h->flags & 2u) ? h->site_hist.p : nullptr, s);
       }
       if (h->flags & TMH_STATS_DEFERRED_PCT)

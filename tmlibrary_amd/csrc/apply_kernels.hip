@@ -39,6 +39,34 @@ __global__ __launch_bounds__(256) void k_smooth_axis0(const double* __restrict__
   out[(int64_t)y * W + x] = acc;
 }
 
+// axis 0 for a compile-time radius: each thread produces T consecutive rows
+// of one column from T + 2R loads (register accumulators, taps added in the
+// same order as k_smooth_axis0 -> bit-identical results), instead of 2R + 1
+// loads per output.
+template <int T, int R>
+__global__ __launch_bounds__(256) void k_smooth_axis0_strip(const double* __restrict__ in,
+                                                            double* __restrict__ out, int H, int W,
+                                                            const double* __restrict__ w) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  const int y0 = blockIdx.y * T;
+  if (x >= W) return;
+  double acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = 0.0;
+#pragma unroll
+  for (int u = 0; u < T + 2 * R; ++u) {
+    const double v = in[(int64_t)reflect_idx(y0 + u - R, H) * W + x];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int k = u - t;
+      if (k >= 0 && k <= 2 * R) acc[t] = fma(w[k], v, acc[t]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+    if (y0 + t < H) out[(int64_t)(y0 + t) * W + x] = acc[t];
+}
+
 // axis 1 (along a row), row segment + halo staged in LDS
 constexpr int kSmTile = 256;
 constexpr int kSmMaxR = 128;
@@ -74,7 +102,13 @@ void launch_smooth(const double* in, double* out, double* tmp, int H, int W, con
                    int radius, hipStream_t s) {
   ProfScope prof("smooth", s);
   const dim3 grid((unsigned)cdiv(W, 256), (unsigned)H);
-  hipLaunchKernelGGL(k_smooth_axis0, grid, dim3(256), 0, s, in, tmp, H, W, d_w, radius);
+  constexpr int kStrip = 32;
+  if (radius == 20)  // sigma = 5, the reference's default (image.py:1172)
+    hipLaunchKernelGGL((k_smooth_axis0_strip<kStrip, 20>),
+                       dim3((unsigned)cdiv(W, 256), (unsigned)cdiv(H, kStrip)), dim3(256), 0, s, in,
+                       tmp, H, W, d_w);
+  else
+    hipLaunchKernelGGL(k_smooth_axis0, grid, dim3(256), 0, s, in, tmp, H, W, d_w, radius);
   if (radius <= kSmMaxR)
     hipLaunchKernelGGL(k_smooth_axis1, dim3((unsigned)cdiv(W, kSmTile), (unsigned)H), dim3(256), 0,
                        s, tmp, out, H, W, d_w, radius);

@@ -52,18 +52,25 @@ constexpr int kBinsPerThread = kBins / kHistThreads;  // 64
 // log10 LUT entries staged in LDS by the per-pixel kernels (f64 / f32x2): 32 KB
 constexpr int kLutLds = 4096;
 
+// quantile positions (np.percentile 'linear' previous/next sorted positions)
+struct QPos {
+  const int32_t* lo;  // [Q] previous sorted positions (tables uploaded by the caller)
+  const int32_t* hi;  // [Q] next sorted positions
+  int Q;
+  double scale;  // (Q - 1) / (n - 1): the quantile at a sorted position, up to rounding
+};
+
 // launches (defined in the .hip files) -------------------------------------------
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
                     hipStream_t s);
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
-                         const int32_t* q_lo, const int32_t* q_hi, int Q, double scale,
-                         uint16_t* vlo, uint16_t* vhi, unsigned long long* pooled,
+                         const QPos& p, uint16_t* vlo, uint16_t* vhi, unsigned long long* pooled,
                          int64_t* zero_counts, uint32_t* site_hist, hipStream_t s);
-void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const int32_t* q_lo, const int32_t* q_hi,
-                          int Q, double scale, uint16_t* vlo, uint16_t* vhi,
-                          unsigned long long* pooled, int64_t* zero_counts, uint32_t* site_hist,
-                          hipStream_t s);
+void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const QPos& p, uint16_t* vlo,
+                          uint16_t* vhi, unsigned long long* pooled,
+                          unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
+                          uint32_t* site_hist, hipStream_t s);
 void launch_pct_accumulate(const uint16_t* vlo, const uint16_t* vhi, int64_t n_sites, int Q,
                            const double* gamma, double* acc, hipStream_t s);
 void launch_finalize(const double* mean, const double* m2, int64_t n, int64_t npx, double* out_mean,

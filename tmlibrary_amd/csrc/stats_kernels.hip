@@ -226,30 +226,6 @@ __device__ __forceinline__ void count8(const uint4 v, uint32_t* bins, uint32_t* 
   }
 }
 
-// smallest q in [0, Q] with tab[q] >= r (tab non-decreasing, ~linear in q)
-__device__ __forceinline__ int64_t first_q(const int32_t* __restrict__ tab, int Q, double scale,
-                                           int64_t r) {
-  int64_t q = (int64_t)((double)r * scale);
-  if (q > Q) q = Q;
-  if (q < 0) q = 0;
-  while (q > 0 && tab[q - 1] >= r) --q;
-  while (q < Q && tab[q] < r) ++q;
-  return q;
-}
-
-// Writes value b at every quantile whose previous (vlo) / next (vhi) sorted
-// position lies in [start, end).
-__device__ __forceinline__ void scatter_bin(uint32_t b, int64_t start, int64_t end,
-                                            const int32_t* __restrict__ q_lo,
-                                            const int32_t* __restrict__ q_hi, int Q, double scale,
-                                            uint16_t* __restrict__ vlo, uint16_t* __restrict__ vhi) {
-  const uint16_t v = (uint16_t)b;
-  const int64_t l0 = first_q(q_lo, Q, scale, start), l1 = first_q(q_lo, Q, scale, end);
-  const int64_t h0 = first_q(q_hi, Q, scale, start), h1 = first_q(q_hi, Q, scale, end);
-  for (int64_t q = l0; q < l1; ++q) vlo[q] = v;
-  for (int64_t q = h0; q < h1; ++q) vhi[q] = v;
-}
-
 // Exclusive scan of one value per thread over the 1024-thread workgroup.
 // `slots` holds 2 x 16 wave totals (double-buffered by the parity of the
 // caller's scan counter, so one barrier per scan suffices).  Returns the
@@ -278,31 +254,125 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, in
 }
 
 constexpr int kTailChunk = 8;  // rounds whose counts are loaded together
+// first index i with R[i] > x (R: 1024 non-decreasing inclusive prefix ranks in LDS)
+__device__ __forceinline__ int upper_rank(const int32_t* R, int32_t x) {
+  int pos = 0;
+#pragma unroll
+  for (int step = kHistThreads / 2; step > 0; step >>= 1)
+    if (R[pos + step - 1] <= x) pos += step;
+  return pos;
+}
+
+// One round's order statistics.  R[t] = inclusive prefix rank of the round's
+// bin t (value bin0 + t); the round owns the sorted positions [r0, r1).
+// Quantile-centric: each thread takes groups of 8 consecutive quantiles,
+// reads their previous/next positions from the (L2-resident) tables, keeps
+// the ones inside [r0, r1), finds each owning bin by a binary search over R
+// in LDS (reused while consecutive positions stay in one bin), and writes the
+// group with ONE 16-B store per stream (masked 2-B stores where a group
+// straddles the round's ends) -- whole lines leave instead of one 2-B store
+// per quantile.  The round's quantile range is [r0 * scale, r1 * scale] up
+// to rounding (and one position's worth of quantiles), so the groups scanned
+// carry a margin and the position test decides membership exactly.
+__device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_t r1,
+                                            uint32_t bin0, const QPos& p,
+                                            uint16_t* __restrict__ vlo, uint16_t* __restrict__ vhi,
+                                            bool vec16) {
+  const int64_t m = (int64_t)p.scale + 3;  // scale > 1 when Q exceeds the pixel count
+  int64_t qa = (int64_t)((double)r0 * p.scale) - m;
+  int64_t qb = (int64_t)((double)r1 * p.scale) + m;
+  qa = qa < 0 ? 0 : qa;
+  qb = qb > p.Q ? p.Q : qb;
+  if (qa >= qb) return;
+  const int64_t g1 = (qb - 1) >> 3;
+  const bool tab16 = vec16;  // tables are 16-B aligned rows when Q % 8 == 0 (hipMalloc base)
+  for (int64_t g = (qa >> 3) + threadIdx.x; g <= g1; g += kHistThreads) {
+    const int64_t q0 = g << 3;
+    int32_t pl[8], ph[8];
+    if (tab16 && q0 + 8 <= p.Q) {
+      const int4 a0 = reinterpret_cast<const int4*>(p.lo + q0)[0];
+      const int4 a1 = reinterpret_cast<const int4*>(p.lo + q0)[1];
+      const int4 b0 = reinterpret_cast<const int4*>(p.hi + q0)[0];
+      const int4 b1 = reinterpret_cast<const int4*>(p.hi + q0)[1];
+      pl[0] = a0.x; pl[1] = a0.y; pl[2] = a0.z; pl[3] = a0.w;
+      pl[4] = a1.x; pl[5] = a1.y; pl[6] = a1.z; pl[7] = a1.w;
+      ph[0] = b0.x; ph[1] = b0.y; ph[2] = b0.z; ph[3] = b0.w;
+      ph[4] = b1.x; ph[5] = b1.y; ph[6] = b1.z; ph[7] = b1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool in = q0 + j < p.Q;
+        pl[j] = in ? p.lo[q0 + j] : INT32_MAX;
+        ph[j] = in ? p.hi[q0 + j] : INT32_MAX;
+      }
+    }
+    uint32_t vl[8], vh[8];
+    uint32_t ml = 0, mh = 0;
+    int tl = -1, th = -1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (pl[j] >= r0 && pl[j] < r1) {
+        if (tl < 0 || R[tl] <= pl[j]) tl = upper_rank(R, pl[j]);
+        vl[j] = bin0 + (uint32_t)tl;
+        ml |= 1u << j;
+      } else {
+        vl[j] = 0u;
+      }
+      if (ph[j] >= r0 && ph[j] < r1) {
+        if (th < 0 || R[th] <= ph[j]) th = upper_rank(R, ph[j]);
+        vh[j] = bin0 + (uint32_t)th;
+        mh |= 1u << j;
+      } else {
+        vh[j] = 0u;
+      }
+    }
+    if (vec16 && ml == 0xFFu) {
+      *reinterpret_cast<uint4*>(vlo + q0) =
+          make_uint4(vl[0] | (vl[1] << 16), vl[2] | (vl[3] << 16), vl[4] | (vl[5] << 16),
+                     vl[6] | (vl[7] << 16));
+    } else if (ml) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if ((ml >> j) & 1u) vlo[q0 + j] = (uint16_t)vl[j];
+    }
+    if (vec16 && mh == 0xFFu) {
+      *reinterpret_cast<uint4*>(vhi + q0) =
+          make_uint4(vh[0] | (vh[1] << 16), vh[2] | (vh[3] << 16), vh[4] | (vh[5] << 16),
+                     vh[6] | (vh[7] << 16));
+    } else if (mh) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if ((mh >> j) & 1u) vhi[q0 + j] = (uint16_t)vh[j];
+    }
+  }
+}
 
 // Walk the 65,536 bins in 64 rounds of 1024 consecutive bins, thread t
 // owning bin 1024*j + t: reads are conflict-free/coalesced, and the dense part
 // of a microscopy histogram (a few thousand adjacent values) is spread over
-// every thread, so the percentile scatter is balanced.  count(b) returns the
-// site's count of value b.  Counts are fetched kTailChunk rounds at a time
-// (the next chunk's loads in flight while the current one is scanned) and
-// rounds that are empty for the whole workgroup are skipped, so a typical
-// microscopy site (values < ~10,000 plus saturation) scans ~12 rounds.
-// `cmask` is 3 words of LDS (chunk masks, triple-buffered).  done(b, c) is
-// called once per bin after its count has been used (e.g. to reset it).
-template <typename CountFn, typename DoneFn>
-__device__ __forceinline__ void hist_tail(CountFn count, DoneFn done, int64_t s,
-                                          const int32_t* __restrict__ q_lo,
-                                          const int32_t* __restrict__ q_hi, int Q, double scale,
+// every thread.  count(b) returns the site's count of value b.  Counts are
+// fetched kTailChunk rounds at a time (the next chunk's loads in flight while
+// the current one is scanned) and rounds that are empty for the whole
+// workgroup are skipped, so a typical microscopy site (values < ~10,000 plus
+// saturation) scans ~12 rounds.  `cmask` is 3 words of LDS (chunk masks,
+// triple-buffered), `starts` 2 x 1024 int32 of LDS (per-bin inclusive prefix
+// ranks, double-buffered by round).  done(b, c) is called once per bin
+// after its count has been used (e.g. to reset it).
+// ABL (development ablations, tools/mb; 0 in production): 1 = no order-
+// statistic output, 4 = no pooled histogram adds
+template <int ABL = 0, typename CountFn, typename DoneFn>
+__device__ __forceinline__ void hist_tail(CountFn count, DoneFn done, int64_t s, const QPos& p,
                                           uint16_t* __restrict__ vlo_all,
                                           uint16_t* __restrict__ vhi_all,
                                           unsigned long long* __restrict__ pooled,
                                           int64_t* __restrict__ zero_counts,
                                           uint32_t* __restrict__ site_hist, uint32_t* slots,
-                                          uint32_t* cmask) {
+                                          uint32_t* cmask, int32_t* starts) {
   const int tid = threadIdx.x;
-  uint16_t* vlo = vlo_all + s * (int64_t)Q;
-  uint16_t* vhi = vhi_all + s * (int64_t)Q;
-  int64_t base = 0;  // exclusive rank of the current round's first bin
+  uint16_t* vlo = vlo_all + s * (int64_t)p.Q;
+  uint16_t* vhi = vhi_all + s * (int64_t)p.Q;
+  const bool vec16 = (p.Q & 7) == 0;
+  int64_t base = 0;          // exclusive rank of the current round's first bin
   int nscan = 0;
   uint32_t cn[kTailChunk];
 #pragma unroll
@@ -334,26 +404,30 @@ __device__ __forceinline__ void hist_tail(CountFn count, DoneFn done, int64_t s,
       done(b, c[k]);
       if (!((mask >> k) & 1u)) continue;  // uniform: no counts in this round
       uint32_t total;
-      const int64_t r = base + block_exscan(c[k], slots, nscan++, &total);
+      const int64_t r = base + block_exscan(c[k], slots, nscan, &total);
+      int32_t* R = starts + (nscan & 1) * kHistThreads;
+      ++nscan;
+      const int64_t r0 = base;
       base += total;
-      if (c[k]) {
-        atomicAdd(&pooled[b], (unsigned long long)c[k]);
-        scatter_bin(b, r, r + c[k], q_lo, q_hi, Q, scale, vlo, vhi);
-      }
+      if (c[k] && !(ABL & 4)) atomicAdd(&pooled[b], (unsigned long long)c[k]);
+      if (ABL & 1) continue;
+      R[tid] = (int32_t)(r + c[k]);
+      __syncthreads();  // R visible; the other R buffer is rewritten only after the next scan
+      fill_groups(R, r0, base, (uint32_t)(jc + k) * kHistThreads, p, vlo, vhi, vec16);
     }
   }
 }
 
 __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
     const uint16_t* __restrict__ sites, int64_t npx, int vec, uint32_t* __restrict__ hist_hi,
-    const int32_t* __restrict__ q_lo, const int32_t* __restrict__ q_hi, int Q, double scale,
-    uint16_t* __restrict__ vlo_all, uint16_t* __restrict__ vhi_all,
+    const QPos p, uint16_t* __restrict__ vlo_all, uint16_t* __restrict__ vhi_all,
     unsigned long long* __restrict__ pooled, int64_t* __restrict__ zero_counts,
     uint32_t* __restrict__ site_hist) {
   __shared__ __attribute__((aligned(16))) uint32_t bins[kLdsBins];
   __shared__ uint32_t himask[16];
   __shared__ uint32_t slots[32];
   __shared__ uint32_t cmask[3];
+  __shared__ int32_t starts[2 * kHistThreads];
   const int tid = threadIdx.x;
   const int64_t s = blockIdx.x;
 
@@ -397,51 +471,69 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
         return ((himask[h >> 11] >> ((h >> 6) & 31u)) & 1u) ? atomicExch(&hhi[h], 0u) : 0u;
       },
       [](uint32_t, uint32_t) {},
-      s, q_lo, q_hi, Q, scale, vlo_all, vhi_all, pooled, zero_counts, site_hist, slots, cmask);
+      s, p, vlo_all, vhi_all, pooled, zero_counts, site_hist, slots, cmask, starts);
 }
 
 // Per-site histogram (65,536 counts, exact) -> order statistics, written from
 // a complete histogram held in global memory (zero-maintained: every count is
 // read and reset), e.g. accumulated by the fused correct+histogram pass.
+template <int ABL = 0>  // ABL 8: counts are not reset (re-runnable)
 __global__ __launch_bounds__(kHistThreads) void k_hist_finalize(
-    uint32_t* __restrict__ hist, const int32_t* __restrict__ q_lo,
-    const int32_t* __restrict__ q_hi, int Q, double scale, uint16_t* __restrict__ vlo_all,
-    uint16_t* __restrict__ vhi_all, unsigned long long* __restrict__ pooled,
+    uint32_t* __restrict__ hist, const QPos p, uint16_t* __restrict__ vlo_all,
+    uint16_t* __restrict__ vhi_all, unsigned long long* __restrict__ pooled, int n_pooled,
     int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist) {
   __shared__ uint32_t slots[32];
   __shared__ uint32_t cmask[3];
+  __shared__ int32_t starts[2 * kHistThreads];
   const int64_t s = blockIdx.x;
   if (threadIdx.x < 3) cmask[threadIdx.x] = 0u;
   __syncthreads();
   uint32_t* h = hist + s * (int64_t)kBins;
-  hist_tail(
+  // sites spread their pooled-histogram adds over n_pooled copies (fewer
+  // same-address atomic collisions); k_pooled_fold sums the copies
+  unsigned long long* pl = pooled + (int64_t)(blockIdx.x % n_pooled) * kBins;
+  hist_tail<ABL & 7>(
       [&](uint32_t b) -> uint32_t { return h[b]; },
       [&](uint32_t b, uint32_t c) {
-        if (c) h[b] = 0u;
+        if (!(ABL & 8) && c) h[b] = 0u;
       },
-      s, q_lo, q_hi, Q, scale, vlo_all, vhi_all, pooled, zero_counts, site_hist, slots, cmask);
+      s, p, vlo_all, vhi_all, pl, zero_counts, site_hist, slots, cmask, starts);
 }
 
-void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const int32_t* q_lo, const int32_t* q_hi,
-                          int Q, double scale, uint16_t* vlo, uint16_t* vhi,
-                          unsigned long long* pooled, int64_t* zero_counts, uint32_t* site_hist,
-                          hipStream_t s) {
+// pooled[b] += sum of the copies; copies reset to zero (zero-maintained)
+__global__ void k_pooled_fold(unsigned long long* __restrict__ pooled,
+                              unsigned long long* __restrict__ parts, int n_parts) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= kBins) return;
+  unsigned long long t = 0;
+  for (int i = 0; i < n_parts; ++i) {
+    t += parts[(int64_t)i * kBins + b];
+    parts[(int64_t)i * kBins + b] = 0ull;
+  }
+  pooled[b] += t;
+}
+
+void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const QPos& p, uint16_t* vlo,
+                          uint16_t* vhi, unsigned long long* pooled,
+                          unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
+                          uint32_t* site_hist, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("hist_finalize", s);
-  hipLaunchKernelGGL(k_hist_finalize, dim3((unsigned)n_sites), dim3(kHistThreads), 0, s, hist, q_lo,
-                     q_hi, Q, scale, vlo, vhi, pooled, zero_counts, site_hist);
+  hipLaunchKernelGGL(k_hist_finalize<0>, dim3((unsigned)n_sites), dim3(kHistThreads), 0, s, hist,
+                     p, vlo, vhi, pooled_parts, n_parts, zero_counts, site_hist);
+  hipLaunchKernelGGL(k_pooled_fold, dim3(kBins / 256), dim3(256), 0, s, pooled, pooled_parts,
+                     n_parts);
   TMH_HIP(hipGetLastError());
 }
 
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
-                         const int32_t* q_lo, const int32_t* q_hi, int Q, double scale,
-                         uint16_t* vlo, uint16_t* vhi, unsigned long long* pooled,
+                         const QPos& p, uint16_t* vlo, uint16_t* vhi, unsigned long long* pooled,
                          int64_t* zero_counts, uint32_t* site_hist, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("hist", s);
   const int vec = ((npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0) ? 1 : 0;
   hipLaunchKernelGGL(k_hist_scatter, dim3((unsigned)n_sites), dim3(kHistThreads), 0, s, sites, npx,
-                     vec, hist_hi, q_lo, q_hi, Q, scale, vlo, vhi, pooled, zero_counts, site_hist);
+                     vec, hist_hi, p, vlo, vhi, pooled, zero_counts, site_hist);
   TMH_HIP(hipGetLastError());
 }
 

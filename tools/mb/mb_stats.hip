@@ -15,6 +15,7 @@
 
 #include "../../tmlibrary_amd/csrc/common.h"
 #include "../../tmlibrary_amd/csrc/fused_kernels.hip"
+#include "../../tmlibrary_amd/csrc/stats_kernels.hip"
 
 #define CK(x)                                                                  \
   do {                                                                         \
@@ -528,8 +529,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&zeros, S * 8));
   for (int r = 0; r < reps; ++r) {
     t.start();
-    launch_hist_scatter(sites, npx, S, hist_hi, qlo, qhi, Q, (double)(Q - 1) / (npx - 1), vlo, vhi,
-                        pooled, zeros, nullptr, 0);
+    QPos qp{qlo, qhi, Q, (double)(Q - 1) / (npx - 1)};
+    launch_hist_scatter(sites, npx, S, hist_hi, qp, vlo, vhi, pooled, zeros, nullptr, 0);
     report("hist (prod)", t.stop(), S * site_gb);
   }
   // correct (production) with dummy stats
@@ -584,6 +585,27 @@ int main(int argc, char** argv) {
     run(k_correct_hist<true, 4, 3, 1024, 32768>, 1024, "fused spu4 t1024: math only");
     run(k_correct_hist<true, 4, 3, 512, 16384>, 512, "fused spu4 t512: math only");
     run(k_correct_hist<true, 2, 3, 512, 16384>, 512, "fused spu2 t512: math only");
+    // one clean fused pass -> exact per-site histograms in `hist`
+    CK(hipMemset(hist, 0, S * kBins * 4));
+    CK(hipMemset(queues, 0, 64));
+    hipLaunchKernelGGL((k_correct_hist<true, 4, 0, 512, 16384>), dim3(n_cu * 2), dim3(512), 0, 0,
+                       sites, out, npx, S, coef2, mconst2, -1, -1, hist, queues, bpx);
+    QPos qa{qlo, qhi, Q, (double)(Q - 1) / (npx - 1)};
+    unsigned long long* parts;
+    CK(hipMalloc(&parts, 16 * 65536 * 8));
+    CK(hipMemset(parts, 0, 16 * 65536 * 8));
+    auto runf = [&](auto kern, const char* name) {
+      for (int r = 0; r < reps; ++r) {
+        t.start();
+        hipLaunchKernelGGL(kern, dim3((unsigned)S), dim3(1024), 0, 0, hist, qa, vlo, vhi, parts, 16,
+                           zeros, (uint32_t*)nullptr);
+        report(name, t.stop(), 0.0);
+      }
+    };
+    runf(k_hist_finalize<8>, "hfin: full (no reset)");
+    runf(k_hist_finalize<9>, "hfin: no output");
+    runf(k_hist_finalize<13>, "hfin: scan only");
+    runf(k_hist_finalize<12>, "hfin: no pooled");
   }
   CK(hipDeviceSynchronize());
   printf("done\n");
