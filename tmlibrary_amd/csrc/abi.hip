@@ -272,6 +272,10 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
       h->qp.hi = h->q_hi.p;
       h->qp.Q = n_quantiles;
       h->qp.scale = h->scale;
+      h->qp.last = (int32_t)(npx - 1);
+      h->qp.hi_next = 1;
+      for (int i = 0; i < n_quantiles; ++i)
+        if (hi[i] != std::min<int32_t>(lo[i] + 1, (int32_t)(npx - 1))) h->qp.hi_next = 0;
     } catch (...) {
       tmh_stats_destroy(h);
       throw;
@@ -744,7 +748,9 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
     check_clip(clip_lo, clip_hi, 65535);
     hipStream_t s = pick(c->stream, stream);
     const bool vec = (h->npx & 7) == 0 && (reinterpret_cast<uintptr_t>(dev_in) & 15) == 0 &&
-                     (reinterpret_cast<uintptr_t>(dev_out) & 15) == 0;
+                     (reinterpret_cast<uintptr_t>(dev_out) & 15) == 0 &&
+                     // the fused pass floors zero pixels at 10**zero_log10 in f32
+                     (!c->log_transform || (c->zero_log10 >= -37.0 && c->zero_log10 <= 0.0));
     const int64_t chunk = 4096;
     for (int64_t c0 = 0; c0 < n_sites; c0 += chunk) {
       const int64_t nc = std::min(chunk, n_sites - c0);

@@ -58,6 +58,8 @@ struct QPos {
   const int32_t* hi;  // [Q] next sorted positions
   int Q;
   double scale;  // (Q - 1) / (n - 1): the quantile at a sorted position, up to rounding
+  int32_t last;  // n - 1
+  int hi_next;   // hi[q] == min(lo[q] + 1, n - 1) for every q: hi is not read
 };
 
 // launches (defined in the .hip files) -------------------------------------------

@@ -43,23 +43,68 @@ __device__ __forceinline__ int xcc_id() {
   return x & 7;
 }
 
-template <bool LOG>
-__device__ __forceinline__ uint32_t fcorrect(uint32_t px, float mu, float a, float mh, float ml,
-                                             float zero_l, int clip_lo, int clip_hi) {
-  float L;
-  if (LOG)
-    L = px ? __builtin_amdgcn_logf((float)px) : zero_l;  // v_log_f32
-  else
-    L = (float)px;
-  const float t = fmaf(L - mu, a, mh) + ml;
-  const float o = LOG ? __builtin_amdgcn_exp2f(t) : t;  // v_exp_f32
-  const int32_t iv = (o >= -2147483648.0f && o < 2147483648.0f) ? (int32_t)o : INT32_MIN;
-  uint32_t r = (uint32_t)iv & 0xFFFFu;  // x86 astype(uint16)
-  if (clip_lo >= 0) {
-    r = r < (uint32_t)clip_lo ? (uint32_t)clip_lo : r;
-    r = r > (uint32_t)clip_hi ? (uint32_t)clip_hi : r;
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// Largest f32 below 2^31 whose low 16 bits are 0: min(o, kCastTop) then
+// v_cvt_i32_f32 reproduces the x86 astype(uint16) rule for every o the f32
+// path can resolve -- o >= 2^31, +inf and NaN (minNum drops it) give 0,
+// o < -2^31 saturates to INT32_MIN whose low half is 0.  Only the f32 values in
+// [2^31 - 2^16, 2^31), where f32 already carries 128-DN steps, differ.
+constexpr float kCastTop = 2147418112.0f;
+
+// Eight pixels (four packed u16 words) -> their corrected u16 values packed
+// the same way.  k[p] = (mu_lo, mu_hi, a_lo, a_hi) of word p's two pixels: the
+// subtract / fma / add run as v_pk_*_f32 on the pair, and each stage is issued
+// for all four pairs before the next so dependent packed ops do not stall on
+// their one-pass hazard.  A zero pixel takes log2(zf), zf = 10**zero_log10 as
+// f32 (1e-10f: v_log_f32 is within 1 ulp of the reference's log10(1e-10) =
+// -10, scaled): one v_max instead of a compare + select.  The caller keeps zf
+// in [FLT_MIN, 1].
+template <bool LOG, bool CLIP>
+__device__ __forceinline__ void fcorrect8(const uint32_t (&w)[4], const float4 (&k)[4], float mh,
+                                          float zf, uint32_t clip_lo2, uint32_t clip_hi2,
+                                          uint32_t (&r)[4]) {
+  f32x2_t t[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    t[p].x = (float)(w[p] & 0xFFFFu);
+    t[p].y = (float)(w[p] >> 16);
   }
-  return r;
+  if (LOG) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      t[p].x = __builtin_amdgcn_logf(__builtin_fmaxf(t[p].x, zf));  // v_log_f32
+      t[p].y = __builtin_amdgcn_logf(__builtin_fmaxf(t[p].y, zf));
+    }
+  }
+  const f32x2_t M = {mh, mh};
+#pragma unroll
+  for (int p = 0; p < 4; ++p) t[p] -= (f32x2_t){k[p].x, k[p].y};
+#pragma unroll
+  for (int p = 0; p < 4; ++p) t[p] = __builtin_elementwise_fma(t[p], (f32x2_t){k[p].z, k[p].w}, M);
+  float o[8];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    o[2 * p] = LOG ? __builtin_amdgcn_exp2f(t[p].x) : t[p].x;  // v_exp_f32
+    o[2 * p + 1] = LOG ? __builtin_amdgcn_exp2f(t[p].y) : t[p].y;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    o[j] = __builtin_fminf(o[j], kCastTop);
+    if (!LOG) o[j] = __builtin_fmaxf(o[j], -2147483648.0f);  // t may be negative: stay in range
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    r[p] = __builtin_amdgcn_perm((uint32_t)(int32_t)o[2 * p + 1], (uint32_t)(int32_t)o[2 * p],
+                                 0x05040100u);
+    if (CLIP) {  // np.clip on the wrapped uint16 values, both halves at once
+      typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+      u16x2_t v = __builtin_bit_cast(u16x2_t, r[p]);
+      v = __builtin_elementwise_min(__builtin_elementwise_max(v, __builtin_bit_cast(u16x2_t, clip_lo2)),
+                                    __builtin_bit_cast(u16x2_t, clip_hi2));
+      r[p] = __builtin_bit_cast(uint32_t, v);
+    }
+  }
 }
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -85,36 +130,41 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 
 // ABL: development ablations (tools/mb), 0 in production: 1 = no histogram,
 // 2 = constant coefficients, 8 = no flush.
-// NT threads per workgroup, LB LDS bins per workgroup (split into SPU slices).
+// NT threads per workgroup, LB LDS bins per workgroup (split into SPU slices
+// of BINS counters plus one overflow counter each: a pixel >= BINS adds to the
+// overflow counter -- never read -- and to its global bin, so the common path
+// is one v_min + one ds_add per pixel).
 // Each workgroup reserves its NEXT unit while it streams the current one, and
 // issues the next unit's first loads before it flushes the current unit's
 // histogram slices, so the flush (LDS scan + global atomics + barriers) runs
 // with the next unit's pixels already in flight.
-template <bool LOG, int SPU, int ABL, int NT, int LB>
+template <bool LOG, bool CLIP, int SPU, int ABL, int NT, int LB>
 __global__ __launch_bounds__(NT, 4) void k_correct_hist(
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
-    const float2* __restrict__ coef2, const float4* __restrict__ mconst2, int clip_lo,
+    const float4* __restrict__ coef, const float4* __restrict__ mconst2, int clip_lo,
     int clip_hi, uint32_t* __restrict__ hist, int* __restrict__ queues, int bands_per_xcd) {
   constexpr int BINS = LB / SPU;
-  __shared__ __attribute__((aligned(16))) uint32_t bins[LB];
+  constexpr int SLICE = BINS + 1;
+  constexpr uint32_t HIMASK = (0xFFFFu & ~(uint32_t)(BINS - 1)) * 0x00010001u;
+  static_assert((BINS & (BINS - 1)) == 0, "slice size must be a power of two");
+  __shared__ __attribute__((aligned(16))) uint32_t bins[SPU * SLICE];
   __shared__ int unit_sh;
-  __shared__ uint32_t top_sh[SPU];
   const int tid = threadIdx.x;
-  for (int i = tid; i < LB / 4; i += NT)
-    reinterpret_cast<uint4*>(bins)[i] = make_uint4(0u, 0u, 0u, 0u);
-  if (tid < SPU) top_sh[tid] = 0u;
+  for (int i = tid; i < SPU * SLICE; i += NT) bins[i] = 0u;
 
   const float4 m = mconst2[0];
+  const uint32_t clo2 = (uint32_t)clip_lo * 0x00010001u, chi2 = (uint32_t)clip_hi * 0x00010001u;
   const int ngroups = (int)(npx >> 3);
   const int site_bytes = (int)(npx * 2);
   const int n_bands = 8 * bands_per_xcd;
   const int n_groups_s = (int)((n_sites + SPU - 1) / SPU);
   const int upq = bands_per_xcd * n_groups_s;  // units per queue
-  // coefficient planes: plane k holds pixels 8g+2k, 8g+2k+1 of group g, so each
-  // of a lane's four coefficient loads is one contiguous 1 KiB per wave
+  // coefficient planes: plane k holds (mu, mu, a, a) of pixels 8g+2k, 8g+2k+1
+  // of group g, so each of a lane's four coefficient loads is one contiguous
+  // 1 KiB per wave
   const __amdgpu_buffer_rsrc_t rcf =
-      __builtin_amdgcn_make_buffer_rsrc((void*)coef2, 0, (int)(npx * 8), 0x00020000);
-  const float4 cc = make_float4(2.5f, 1.1f, 2.4f, 0.9f);
+      __builtin_amdgcn_make_buffer_rsrc((void*)coef, 0, (int)(npx * 8), 0x00020000);
+  const float4 cc = make_float4(2.5f, 2.4f, 1.1f, 0.9f);
 
   // unit = (queue q, index u) -> band q + 8 * (u / n_groups_s), sites from s0
   int q = xcc_id(), exhausted = 0;
@@ -152,8 +202,7 @@ __global__ __launch_bounds__(NT, 4) void k_correct_hist(
                                                0x00020000);
     return r;
   };
-  auto load = [&](const Unit& un, int g, uint4 (&v)[SPU], float4& c0, float4& c1, float4& c2,
-                  float4& c3) {
+  auto load = [&](const Unit& un, int g, uint4 (&v)[SPU], float4 (&c)[4]) {
     const int off = g * 16;
 #pragma unroll
     for (int k = 0; k < SPU; ++k) {
@@ -161,15 +210,15 @@ __global__ __launch_bounds__(NT, 4) void k_correct_hist(
       v[k] = make_uint4(w.x, w.y, w.z, w.w);
     }
     if (!(ABL & 2)) {
-      c0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rcf, off, 0, 0));
-      c1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rcf, off, ngroups * 16, 0));
-      c2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rcf, off, ngroups * 32, 0));
-      c3 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rcf, off, ngroups * 48, 0));
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        c[p] = __builtin_bit_cast(float4,
+                                  __builtin_amdgcn_raw_buffer_load_b128(rcf, off, p * ngroups * 16, 0));
     }
   };
 
   uint4 v[SPU];
-  float4 c0 = cc, c1 = cc, c2 = cc, c3 = cc;
+  float4 c[4] = {cc, cc, cc, cc};
 #pragma unroll
   for (int k = 0; k < SPU; ++k) v[k] = make_uint4(0, 0, 0, 0);
   bool pre = false;  // v/c already hold this unit's first group (loaded by the previous unit)
@@ -180,91 +229,80 @@ __global__ __launch_bounds__(NT, 4) void k_correct_hist(
     Unit nu = un;
     if (nxt >= 0) nu = decode(nxt);
     uint32_t* hs = hist + un.s0 * (int64_t)kBins;
-    uint32_t top[SPU];
-#pragma unroll
-    for (int k = 0; k < SPU; ++k) top[k] = 0u;
 
-    auto process = [&](const uint4 w, const int k, const float4 k0, const float4 k1,
-                       const float4 k2, const float4 k3) -> u32x4_t {
-      const uint32_t px[8] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16,
-                              w.z & 0xFFFFu, w.z >> 16, w.w & 0xFFFFu, w.w >> 16};
-      const float mu[8] = {k0.x, k0.z, k1.x, k1.z, k2.x, k2.z, k3.x, k3.z};
-      const float a[8] = {k0.y, k0.w, k1.y, k1.w, k2.y, k2.w, k3.y, k3.w};
-      uint32_t mx = 0;
+    auto process = [&](const uint4 w, const int k, const float4 (&cf)[4]) -> u32x4_t {
+      const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+      if (!(ABL & 1)) {
+        uint32_t* sl = bins + k * SLICE;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        mx = px[j] > mx ? px[j] : mx;
-        if (!(ABL & 1)) atomicAdd(&bins[k * BINS + (px[j] & (BINS - 1))], px[j] < (uint32_t)BINS);
+        for (int p = 0; p < 4; ++p) {
+          const uint32_t lo = wd[p] & 0xFFFFu, hi = wd[p] >> 16;
+          atomicAdd(&sl[lo < (uint32_t)BINS ? lo : (uint32_t)BINS], 1u);
+          atomicAdd(&sl[hi < (uint32_t)BINS ? hi : (uint32_t)BINS], 1u);
+        }
+        if ((w.x | w.y | w.z | w.w) & HIMASK) {  // rare: beyond this site's LDS slice
+          uint32_t* h = hs + k * (int64_t)kBins;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const uint32_t lo = wd[p] & 0xFFFFu, hi = wd[p] >> 16;
+            if (lo >= (uint32_t)BINS) atomicAdd(&h[lo], 1u);
+            if (hi >= (uint32_t)BINS) atomicAdd(&h[hi], 1u);
+          }
+        }
       }
-      top[k] = mx > top[k] ? mx : top[k];
-      if (!(ABL & 1) && mx >= (uint32_t)BINS) {  // rare: beyond this site's LDS slice
-        uint32_t* h = hs + k * (int64_t)kBins;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (px[j] >= (uint32_t)BINS) atomicAdd(&h[px[j]], 1u);
-      }
-      uint32_t o[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        o[j] = fcorrect<LOG>(px[j], mu[j], a[j], m.x, m.y, m.z, clip_lo, clip_hi);
-      const u32x4_t r = {o[0] | (o[1] << 16), o[2] | (o[3] << 16), o[4] | (o[5] << 16),
-                         o[6] | (o[7] << 16)};
+      uint32_t o[4];
+      fcorrect8<LOG, CLIP>(wd, cf, m.x, m.z, clo2, chi2, o);
+      const u32x4_t r = {o[0], o[1], o[2], o[3]};
       return r;
     };
 
     int g = un.g0 + tid;
-    if (!pre && g < un.g1) load(un, g, v, c0, c1, c2, c3);
+    if (!pre && g < un.g1) load(un, g, v, c);
     pre = false;
     // two-stage pipeline over the unit's pixel groups; the last stage loads
     // the next unit's first group
     while (g < un.g1) {
       const int gn = g + NT;
       uint4 vn[SPU];
-      float4 n0 = cc, n1 = cc, n2 = cc, n3 = cc;
+      float4 cn[4] = {cc, cc, cc, cc};
 #pragma unroll
       for (int k = 0; k < SPU; ++k) vn[k] = make_uint4(0, 0, 0, 0);
       if (gn < un.g1) {
-        load(un, gn, vn, n0, n1, n2, n3);
+        load(un, gn, vn, cn);
       } else if (nxt >= 0 && nu.g0 + tid < nu.g1) {
-        load(nu, nu.g0 + tid, vn, n0, n1, n2, n3);
+        load(nu, nu.g0 + tid, vn, cn);
         pre = true;
       }
 #pragma unroll
       for (int k = 0; k < SPU; ++k)
         if (k < un.ns)
-          __builtin_amdgcn_raw_buffer_store_b128(process(v[k], k, c0, c1, c2, c3), un.rout,
-                                                 g * 16, k * site_bytes, 2);
+          __builtin_amdgcn_raw_buffer_store_b128(process(v[k], k, c), un.rout, g * 16,
+                                                 k * site_bytes, 2);
 #pragma unroll
       for (int k = 0; k < SPU; ++k) v[k] = vn[k];
-      c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) c[p] = cn[p];
       g = gn;
     }
     cur = nxt;
     if (ABL & 9) continue;
-    // largest value per site in this unit bounds the bins worth flushing
-#pragma unroll
-    for (int k = 0; k < SPU; ++k) {
-      const uint32_t t = wave_max(top[k]);
-      if ((tid & 63) == 0 && t) atomicMax(&top_sh[k], t);
-    }
     __syncthreads();
-    // fold this unit's slices into the sites' histograms (contiguous lanes -> bins)
+    // fold this unit's slices into the sites' histograms (contiguous lanes ->
+    // bins); the overflow counters are left to wrap, they are never read
 #pragma unroll
     for (int k = 0; k < SPU; ++k) {
       if (k >= un.ns) break;
-      const uint32_t t = top_sh[k];
-      const int lim = (int)(t < (uint32_t)BINS ? t : (uint32_t)BINS - 1);
       uint32_t* h = hs + k * (int64_t)kBins;
-      for (int b = tid; b <= lim; b += NT) {
-        const uint32_t c = bins[k * BINS + b];
-        if (c) {
-          atomicAdd(&h[b], c);
-          bins[k * BINS + b] = 0u;
+#pragma unroll 4
+      for (int b = tid; b < BINS; b += NT) {
+        const uint32_t cnt = bins[k * SLICE + b];
+        if (cnt) {
+          atomicAdd(&h[b], cnt);
+          bins[k * SLICE + b] = 0u;
         }
       }
     }
     __syncthreads();
-    if (tid < SPU) top_sh[tid] = 0u;  // next write is after grab()'s barriers
   }
 }
 
@@ -290,10 +328,16 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
     return v >= 1 && v <= 16 ? v : kBandsPerXcd;
   }();
   TMH_HIP(hipMemsetAsync(queues, 0, 8 * sizeof(int), s));
-#define TMH_LAUNCH_CH(L_, S_, T_, B_)                                                     \
-  hipLaunchKernelGGL((k_correct_hist<L_, S_, 0, T_, B_>), dim3(n_wg * (1024 / T_)), dim3(T_), \
-                     0, s, in, out, npx, n_sites, coef2, mconst2, clip_lo, clip_hi, hist,     \
-                     queues, bpx)
+  const float4* cf4 = reinterpret_cast<const float4*>(coef2);
+#define TMH_LAUNCH_CH(L_, S_, T_, B_)                                                        \
+  if (clip_lo >= 0)                                                                              \
+    hipLaunchKernelGGL((k_correct_hist<L_, true, S_, 0, T_, B_>), dim3(n_wg * (1024 / T_)),      \
+                       dim3(T_), 0, s, in, out, npx, n_sites, cf4, mconst2, clip_lo, clip_hi,   \
+                       hist, queues, bpx);                                                       \
+  else                                                                                           \
+    hipLaunchKernelGGL((k_correct_hist<L_, false, S_, 0, T_, B_>), dim3(n_wg * (1024 / T_)),     \
+                       dim3(T_), 0, s, in, out, npx, n_sites, cf4, mconst2, clip_lo, clip_hi,   \
+                       hist, queues, bpx)
 #define TMH_LAUNCH_CFG(L_)                                 \
   switch (fused_cfg()) {                                   \
     case 0: TMH_LAUNCH_CH(L_, 2, 1024, 32768); break;      \
@@ -311,37 +355,42 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
   TMH_HIP(hipGetLastError());
 }
 
-// coef2 = (f32 mean [*log2(10) when log], f32 mean(std)/std) per pixel: the
+// coef2 = per pixel (f32 mean [*log2(10) when log], f32 mean(std)/std): the
 // compact form the fused pass keeps L2-resident.  For npx % 8 == 0 (the only
-// case the fused pass runs) pixel 8g+j is stored in plane j/2 at float2 index
-// (j/2)*2*ngroups + 2g + j%2.  mconst2 = (M' hi, M' lo, zero pixel value, 0)
-// with M' = mean(mean) [*log2(10)].
+// case the fused pass runs) pixel 8g+j is stored in plane p = j/2 as the
+// float4 (mu_2p, mu_2p+1, a_2p, a_2p+1) at index g, so one 16-B load gives a
+// pixel pair its operands for the packed f32 ops.  mconst2 = (M' hi, M' lo,
+// 10**zero_log10 (the value a zero pixel takes before the log), 0) with
+// M' = mean(mean) [*log2(10)].
 __global__ void k_coeffs2(const double* __restrict__ mean, const double* __restrict__ std,
                           const double* __restrict__ sums, int64_t npx, int log_transform,
-                          double zero_log10, float2* __restrict__ coef2,
+                          double zero_log10, float* __restrict__ coef2,
                           float4* __restrict__ mconst2) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const double K = log_transform ? kLog2_10 : 1.0;
   if (i == 0) {
     const double M = sums[1] / (double)npx * K;
     const float mh = (float)M;
-    mconst2[0] = make_float4(mh, (float)(M - (double)mh), (float)(zero_log10 * kLog2_10), 0.f);
+    mconst2[0] = make_float4(mh, (float)(M - (double)mh), (float)exp10(zero_log10), 0.f);
   }
   if (i >= npx) return;
   const double S = sums[0] / (double)npx;
-  int64_t o = i;
+  int64_t om = 2 * i, oa = 2 * i + 1;
   if ((npx & 7) == 0) {
     const int64_t g = i >> 3, j = i & 7;
-    o = (j >> 1) * (npx >> 2) + 2 * g + (j & 1);
+    const int64_t base = (j >> 1) * (npx >> 1) + 4 * g + (j & 1);
+    om = base;
+    oa = base + 2;
   }
-  coef2[o] = make_float2((float)(mean[i] * K), (float)(S / std[i]));
+  coef2[om] = (float)(mean[i] * K);
+  coef2[oa] = (float)(S / std[i]);
 }
 
 void launch_coeffs2(const double* mean, const double* std, const double* sums, int64_t npx,
                     int log_transform, double zero_log10, float2* coef2, float4* mconst2,
                     hipStream_t s) {
   hipLaunchKernelGGL(k_coeffs2, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, mean, std, sums,
-                     npx, log_transform, zero_log10, coef2, mconst2);
+                     npx, log_transform, zero_log10, reinterpret_cast<float*>(coef2), mconst2);
   TMH_HIP(hipGetLastError());
 }
 

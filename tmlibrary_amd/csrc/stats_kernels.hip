@@ -64,16 +64,22 @@ __device__ __forceinline__ void welford1(double x, double rn, double& mu, double
   m2 = fma(d, x - mu, m2);      // M2 + delta * (x - mean_new)
 }
 
-// One branch per 8 pixels (not per pixel): gather all 8 from the LDS LUT
-// (index clamped with one v_min), then patch the rare values beyond it one
-// lane-slot at a time, so a single inlined log10 serves all eight slots
-// (eight unrolled copies cost ~30 VGPRs and a wave per SIMD).
+constexpr int kWfThreads = 256;
+constexpr int kWfGroup = 4;  // sites per pipeline stage (two stages in flight)
+
+// 1/n for the sites of one launch (uniform per site: read with scalar loads)
+__global__ void k_rn_table(double* __restrict__ rn, int64_t n0, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) rn[i] = 1.0 / (double)(n0 + i + 1);
+}
+
+// Stats transform of eight pixels: LDS LUT gather (index clamped with one
+// v_min), then the rare values beyond it patched one lane-slot at a time, so a
+// single inlined log10 serves all eight slots.
 template <bool LOG>
-__device__ __forceinline__ void welford8(const uint4 v, double rn, double (&mu)[8],
-                                         double (&m2)[8], const double* slut) {
+__device__ __forceinline__ void xform8(const uint4 v, const double* slut, double (&x)[8]) {
   const uint32_t u[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
                          v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
-  double x[8];
   if (LOG) {
     constexpr uint32_t kTop = kWfLut - 1;
     uint32_t mx = 0;
@@ -91,24 +97,28 @@ __device__ __forceinline__ void welford8(const uint4 v, double rn, double (&mu)[
 #pragma unroll
     for (int k = 0; k < 8; ++k) x[k] = (double)u[k];
   }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) welford1(x[k], rn, mu[k], m2[k]);
 }
 
-constexpr int kWfThreads = 256;
-constexpr int kWfGroup = 4;  // sites per pipeline stage (two stages in flight)
+// Launch-level constants of the shifted-sum pass (host-computed f64)
+struct WfMerge {
+  double inv_nl;  // 1 / sites of this launch
+  double w_new;   // nl / (n0 + nl)
+  double w_cross; // n0 * nl / (n0 + nl)
+  int first;      // n0 == 0: no previous state to merge
+};
 
-// 1/n for the sites of one launch (uniform per site: read with scalar loads)
-__global__ void k_rn_table(double* __restrict__ rn, int64_t n0, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) rn[i] = 1.0 / (double)(n0 + i + 1);
-}
-
+// Welford over the launch's sites as shifted sums (stats.py:86-92 restated):
+// per pixel K = x of the launch's first site, S1 = sum(x - K), S2 = sum((x - K)^2)
+// -- three f64 ops per pixel-site instead of Welford's four, no 1/n per site.
+// At the end (mean_l, M2_l) = (K + S1/nl, S2 - S1^2/nl) is merged into the
+// running (mean, M2) with Chan's pairwise formula.  K is one of the samples,
+// so (mean_l - K)^2 <= (nl - 1) var and the cancellation in S2 - S1^2/nl
+// costs at most a factor nl of f64 precision (~1e-12 relative at 3456 sites,
+// against the 1e-6 bar); a constant pixel gives exactly 0.
 template <bool LOG>
 __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
-    const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites,
-    const double* __restrict__ rn, double* __restrict__ mean, double* __restrict__ m2,
-    const double* __restrict__ lut) {
+    const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites, const WfMerge mg,
+    double* __restrict__ mean, double* __restrict__ m2, const double* __restrict__ lut) {
   __shared__ double slut[kWfLut];
   if (LOG)
     for (int i = threadIdx.x; i < kWfLut; i += kWfThreads) slut[i] = lut[i];
@@ -117,15 +127,6 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
   const int64_t g = (int64_t)blockIdx.x * kWfThreads + threadIdx.x;
   if (g >= ngroups) return;
 
-  double mu[8], q[8];
-  const double2* pm = reinterpret_cast<const double2*>(mean) + g * 4;
-  const double2* pq = reinterpret_cast<const double2*>(m2) + g * 4;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const double2 a = pm[k], b = pq[k];
-    mu[2 * k] = a.x; mu[2 * k + 1] = a.y;
-    q[2 * k] = b.x; q[2 * k + 1] = b.y;
-  }
   const uint4* src = reinterpret_cast<const uint4*>(sites) + g;
   const int64_t last = n_sites - 1;
   // two-stage pipeline: the next group's loads are in flight while the
@@ -133,6 +134,10 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
   uint4 cur[kWfGroup], nxt[kWfGroup];
 #pragma unroll
   for (int k = 0; k < kWfGroup; ++k) cur[k] = src[(k < last ? k : last) * ngroups];
+  double K[8], s1[8], s2[8];
+  xform8<LOG>(cur[0], slut, K);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.0;
   for (int64_t s = 0; s < n_sites; s += kWfGroup) {
 #pragma unroll
     for (int k = 0; k < kWfGroup; ++k) {
@@ -140,14 +145,46 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
       nxt[k] = src[(t < last ? t : last) * ngroups];
     }
 #pragma unroll
-    for (int k = 0; k < kWfGroup; ++k)
-      if (s + k < n_sites) welford8<LOG>(cur[k], rn[s + k], mu, q, slut);
+    for (int k = 0; k < kWfGroup; ++k) {
+      if (s + k < n_sites) {
+        double x[8];
+        xform8<LOG>(cur[k], slut, x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const double d = x[j] - K[j];
+          s1[j] += d;
+          s2[j] = fma(d, d, s2[j]);
+        }
+      }
+    }
 #pragma unroll
     for (int k = 0; k < kWfGroup; ++k) cur[k] = nxt[k];
   }
 
   double2* om = reinterpret_cast<double2*>(mean) + g * 4;
   double2* oq = reinterpret_cast<double2*>(m2) + g * 4;
+  double mu[8], q[8];
+  if (!mg.first) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double2 a = om[k], b = oq[k];
+      mu[2 * k] = a.x; mu[2 * k + 1] = a.y;
+      q[2 * k] = b.x; q[2 * k + 1] = b.y;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const double ml = K[j] + s1[j] * mg.inv_nl;
+    const double m2l = fmax(s2[j] - s1[j] * (s1[j] * mg.inv_nl), 0.0);
+    if (mg.first) {
+      mu[j] = ml;
+      q[j] = m2l;
+    } else {
+      const double d = ml - mu[j];
+      mu[j] = fma(d, mg.w_new, mu[j]);
+      q[j] = q[j] + m2l + d * d * mg.w_cross;
+    }
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     om[k] = make_double2(mu[2 * k], mu[2 * k + 1]);
@@ -179,15 +216,18 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
                     hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("welford", s);
-  hipLaunchKernelGGL(k_rn_table, dim3((unsigned)cdiv(n_sites, 256)), dim3(256), 0, s, rn, n0,
-                     n_sites);
   const bool vec = (npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0;
   const dim3 grid((unsigned)(vec ? cdiv(npx >> 3, kWfThreads) : cdiv(npx, kWfThreads)));
+  if (!vec)  // the per-pixel Welford of odd shapes reads 1/n per site
+    hipLaunchKernelGGL(k_rn_table, dim3((unsigned)cdiv(n_sites, 256)), dim3(256), 0, s, rn, n0,
+                       n_sites);
+  const double nl = (double)n_sites, n = (double)(n0 + n_sites);
+  const WfMerge mg{1.0 / nl, nl / n, (double)n0 * nl / n, n0 == 0};
   if (vec && log_transform)
-    hipLaunchKernelGGL(k_welford_vec8<true>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites, rn,
+    hipLaunchKernelGGL(k_welford_vec8<true>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites, mg,
                        mean, m2, lut);
   else if (vec)
-    hipLaunchKernelGGL(k_welford_vec8<false>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites, rn,
+    hipLaunchKernelGGL(k_welford_vec8<false>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites, mg,
                        mean, m2, lut);
   else if (log_transform)
     hipLaunchKernelGGL(k_welford_scalar<true>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
@@ -254,25 +294,35 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, in
 }
 
 constexpr int kTailChunk = 8;  // rounds whose counts are loaded together
-// first index i with R[i] > x (R: 1024 non-decreasing inclusive prefix ranks in LDS)
-__device__ __forceinline__ int upper_rank(const int32_t* R, int32_t x) {
-  int pos = 0;
-#pragma unroll
-  for (int step = kHistThreads / 2; step > 0; step >>= 1)
-    if (R[pos + step - 1] <= x) pos += step;
-  return pos;
+// first index i >= t with R[i] > x (R: 1024 non-decreasing inclusive prefix
+// ranks in LDS; the caller guarantees R[1023] > x).  Consecutive quantile
+// positions mostly stay in one bin or step to the next, so two probes settle
+// most calls; the rest finish with a binary search over (t+1, 1023].
+__device__ __forceinline__ int advance_rank(const int32_t* R, int t, int32_t x) {
+  if (R[t] > x) return t;
+  if (R[t + 1] > x) return t + 1;
+  int lo = t + 1, hi = kHistThreads - 1;  // R[lo] <= x < R[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (R[mid] > x)
+      hi = mid;
+    else
+      lo = mid;
+  }
+  return hi;
 }
 
 // One round's order statistics.  R[t] = inclusive prefix rank of the round's
 // bin t (value bin0 + t); the round owns the sorted positions [r0, r1).
 // Quantile-centric: each thread takes groups of 8 consecutive quantiles,
-// reads their previous/next positions from the (L2-resident) tables, keeps
-// the ones inside [r0, r1), finds each owning bin by a binary search over R
-// in LDS (reused while consecutive positions stay in one bin), and writes the
-// group with ONE 16-B store per stream (masked 2-B stores where a group
-// straddles the round's ends) -- whole lines leave instead of one 2-B store
-// per quantile.  The round's quantile range is [r0 * scale, r1 * scale] up
-// to rounding (and one position's worth of quantiles), so the groups scanned
+// reads their previous positions from the (L2-resident) table (the next
+// position is min(prev + 1, n - 1) for every q in [0, 100], np.percentile
+// 'linear'; a general next table is read only if the caller's differs), keeps
+// the ones inside [r0, r1), finds each owning bin by advancing through R in
+// LDS from the previous quantile's bin, and writes the group with ONE 16-B
+// store per stream (masked 2-B stores where a group straddles the round's
+// ends).  The round's quantile range is [r0 * scale, r1 * scale] up to
+// rounding (and one position's worth of quantiles), so the groups scanned
 // carry a margin and the position test decides membership exactly.
 __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_t r1,
                                             uint32_t bin0, const QPos& p,
@@ -286,44 +336,44 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
   if (qa >= qb) return;
   const int64_t g1 = (qb - 1) >> 3;
   const bool tab16 = vec16;  // tables are 16-B aligned rows when Q % 8 == 0 (hipMalloc base)
+  const int32_t a = (int32_t)r0, b = (int32_t)r1;
   for (int64_t g = (qa >> 3) + threadIdx.x; g <= g1; g += kHistThreads) {
     const int64_t q0 = g << 3;
     int32_t pl[8], ph[8];
     if (tab16 && q0 + 8 <= p.Q) {
       const int4 a0 = reinterpret_cast<const int4*>(p.lo + q0)[0];
       const int4 a1 = reinterpret_cast<const int4*>(p.lo + q0)[1];
-      const int4 b0 = reinterpret_cast<const int4*>(p.hi + q0)[0];
-      const int4 b1 = reinterpret_cast<const int4*>(p.hi + q0)[1];
       pl[0] = a0.x; pl[1] = a0.y; pl[2] = a0.z; pl[3] = a0.w;
       pl[4] = a1.x; pl[5] = a1.y; pl[6] = a1.z; pl[7] = a1.w;
-      ph[0] = b0.x; ph[1] = b0.y; ph[2] = b0.z; ph[3] = b0.w;
-      ph[4] = b1.x; ph[5] = b1.y; ph[6] = b1.z; ph[7] = b1.w;
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const bool in = q0 + j < p.Q;
-        pl[j] = in ? p.lo[q0 + j] : INT32_MAX;
-        ph[j] = in ? p.hi[q0 + j] : INT32_MAX;
-      }
+      for (int j = 0; j < 8; ++j) pl[j] = q0 + j < p.Q ? p.lo[q0 + j] : INT32_MAX;
     }
+    if (p.hi_next) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ph[j] = pl[j] < p.last ? pl[j] + 1 : pl[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ph[j] = q0 + j < p.Q ? p.hi[q0 + j] : INT32_MAX;
+    }
+    // positions are non-decreasing in q: the first one inside the round
+    // starts the scan at bin 0, every later one continues from its
+    // predecessor's bin
     uint32_t vl[8], vh[8];
     uint32_t ml = 0, mh = 0;
-    int tl = -1, th = -1;
+    int tl = 0, th = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (pl[j] >= r0 && pl[j] < r1) {
-        if (tl < 0 || R[tl] <= pl[j]) tl = upper_rank(R, pl[j]);
+      vl[j] = vh[j] = 0u;
+      if (pl[j] >= a && pl[j] < b) {
+        tl = advance_rank(R, tl, pl[j]);
         vl[j] = bin0 + (uint32_t)tl;
         ml |= 1u << j;
-      } else {
-        vl[j] = 0u;
       }
-      if (ph[j] >= r0 && ph[j] < r1) {
-        if (th < 0 || R[th] <= ph[j]) th = upper_rank(R, ph[j]);
+      if (ph[j] >= a && ph[j] < b) {
+        th = advance_rank(R, th > tl ? th : tl, ph[j]);
         vh[j] = bin0 + (uint32_t)th;
         mh |= 1u << j;
-      } else {
-        vh[j] = 0u;
       }
     }
     if (vec16 && ml == 0xFFu) {

@@ -529,7 +529,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&zeros, S * 8));
   for (int r = 0; r < reps; ++r) {
     t.start();
-    QPos qp{qlo, qhi, Q, (double)(Q - 1) / (npx - 1)};
+    QPos qp{qlo, qhi, Q, (double)(Q - 1) / (npx - 1), (int32_t)(npx - 1), 1};
     launch_hist_scatter(sites, npx, S, hist_hi, qp, vlo, vhi, pooled, zeros, nullptr, 0);
     report("hist (prod)", t.stop(), S * site_gb);
   }
@@ -570,27 +570,27 @@ int main(int argc, char** argv) {
       for (int r = 0; r < reps; ++r) {
         CK(hipMemset(queues, 0, 64));
         t.start();
-        hipLaunchKernelGGL(kern, dim3(n_cu * (1024 / nt)), dim3(nt), 0, 0, sites, out, npx, S, coef2,
+        hipLaunchKernelGGL(kern, dim3(n_cu * (1024 / nt)), dim3(nt), 0, 0, sites, out, npx, S, (const float4*)coef2,
                            mconst2, -1, -1, hist, queues, bpx);
         report(name, t.stop(), 2 * S * site_gb);
       }
     };
-    run(k_correct_hist<true, 2, 0, 1024, 32768>, 1024, "fused spu2 t1024: full");
-    run(k_correct_hist<true, 4, 0, 1024, 32768>, 1024, "fused spu4 t1024: full");
-    run(k_correct_hist<true, 2, 0, 512, 16384>, 512, "fused spu2 t512: full");
-    run(k_correct_hist<true, 4, 0, 512, 16384>, 512, "fused spu4 t512: full");
-    run(k_correct_hist<true, 4, 8, 1024, 32768>, 1024, "fused spu4 t1024: no flush");
-    run(k_correct_hist<true, 4, 1, 1024, 32768>, 1024, "fused spu4 t1024: no hist");
-    run(k_correct_hist<true, 4, 2, 1024, 32768>, 1024, "fused spu4 t1024: const coef");
-    run(k_correct_hist<true, 4, 3, 1024, 32768>, 1024, "fused spu4 t1024: math only");
-    run(k_correct_hist<true, 4, 3, 512, 16384>, 512, "fused spu4 t512: math only");
-    run(k_correct_hist<true, 2, 3, 512, 16384>, 512, "fused spu2 t512: math only");
+    run(k_correct_hist<true, false, 2, 0, 1024, 32768>, 1024, "fused spu2 t1024: full");
+    run(k_correct_hist<true, false, 4, 0, 1024, 32768>, 1024, "fused spu4 t1024: full");
+    run(k_correct_hist<true, false, 2, 0, 512, 16384>, 512, "fused spu2 t512: full");
+    run(k_correct_hist<true, false, 4, 0, 512, 16384>, 512, "fused spu4 t512: full");
+    run(k_correct_hist<true, false, 4, 8, 1024, 32768>, 1024, "fused spu4 t1024: no flush");
+    run(k_correct_hist<true, false, 4, 1, 1024, 32768>, 1024, "fused spu4 t1024: no hist");
+    run(k_correct_hist<true, false, 4, 2, 1024, 32768>, 1024, "fused spu4 t1024: const coef");
+    run(k_correct_hist<true, false, 4, 3, 1024, 32768>, 1024, "fused spu4 t1024: math only");
+    run(k_correct_hist<true, false, 4, 3, 512, 16384>, 512, "fused spu4 t512: math only");
+    run(k_correct_hist<true, false, 2, 3, 512, 16384>, 512, "fused spu2 t512: math only");
     // one clean fused pass -> exact per-site histograms in `hist`
     CK(hipMemset(hist, 0, S * kBins * 4));
     CK(hipMemset(queues, 0, 64));
-    hipLaunchKernelGGL((k_correct_hist<true, 4, 0, 512, 16384>), dim3(n_cu * 2), dim3(512), 0, 0,
-                       sites, out, npx, S, coef2, mconst2, -1, -1, hist, queues, bpx);
-    QPos qa{qlo, qhi, Q, (double)(Q - 1) / (npx - 1)};
+    hipLaunchKernelGGL((k_correct_hist<true, false, 4, 0, 512, 16384>), dim3(n_cu * 2), dim3(512), 0, 0,
+                       sites, out, npx, S, (const float4*)coef2, mconst2, -1, -1, hist, queues, bpx);
+    QPos qa{qlo, qhi, Q, (double)(Q - 1) / (npx - 1), (int32_t)(npx - 1), 1};
     unsigned long long* parts;
     CK(hipMalloc(&parts, 16 * 65536 * 8));
     CK(hipMemset(parts, 0, 16 * 65536 * 8));
