@@ -328,8 +328,9 @@ def test_deferred_chain_and_merge_single_gpu(L):
         hip.check(L.tmh_stats_merge_stage3(h, n, sum_dev.p, None))
     acc = Dev(L, 100000 * 8)
     acc.put(np.zeros(100000))
-    for h in hs:  # rank order
+    for h in hs:  # rank order; each handle has its own stream, so wait in between
         hip.check(L.tmh_stats_pct_accumulate(h, acc.p, None))
+        L.tmh_synchronize(None)
     for h in hs:
         hip.check(L.tmh_stats_set_pct_sum(h, acc.p, None))
     L.tmh_synchronize(None)
@@ -488,3 +489,41 @@ def test_quantile_tables(L, qkind):
     for s in sites:
         want += orc.percentile_linear(s, q)
     assert np.array_equal(r["acc"], want)
+
+
+_SPLIT_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path.insert(0, {repo!r})
+from oracle import corilla_oracle as orc
+from tmlibrary_amd.image import ChannelImage
+from tmlibrary_amd.synth import synth_sites_host
+from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
+sites = synth_sites_host(400, 48, 64, seed=31)
+st = OnlineStatistics((48, 64), batch_size=200)
+for s in sites:
+    st.update(ChannelImage(s))
+ref = orc.run_illumstats(sites)
+assert st.n == ref.n == 400
+for got, want in ((st.mean.array, ref.mean), (st.std.array, ref.std)):
+    err = np.abs(got - want) / np.maximum(np.abs(want), 1e-3)
+    assert err.max() <= 1e-6, err.max()
+assert np.array_equal(st.percentile_sums, ref.percentile_sums)
+print("split ok", float(np.abs(st.std.array - ref.std).max()))
+"""
+
+
+@pytest.mark.parametrize("parts", ["2", "3", "4"])
+def test_welford_site_parts(L, parts):
+    """Site-split Welford launches (TMH_WF_PARTS forces the split the launch
+    policy picks at 2160x2560): parts merged in order, then into the state of
+    the previous launch -- mean/std still within the 1e-6 bar."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TMH_WF_PARTS=parts)
+    r = subprocess.run([sys.executable, "-c", _SPLIT_SCRIPT.format(repo=repo)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "split ok" in r.stdout

@@ -129,6 +129,7 @@ struct tmh_stats {
   int64_t pending = 0;        // Welford-updated sites whose histograms are still to come
   bool pct_sum_external = false;
   DBuf<double> mean, m2, lut_log, gamma, acc, tmp_mean, tmp_std, rn;
+  DBuf<double> wf_part;  // partial (mean, M2) planes of site-split Welford launches
   DBuf<int32_t> q_lo, q_hi;
   DBuf<unsigned long long> pooled, pooled_parts;  // parts: kPooledParts zero-maintained copies
   DBuf<uint32_t> hist_hi, site_hist, hist_full;
@@ -248,6 +249,7 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
       h->stream = h->own_stream;
       h->mean.alloc(npx, true);
       h->m2.alloc(npx, true);
+      h->wf_part.alloc((size_t)8 * npx);
       h->acc.alloc(n_quantiles, true);
       h->pooled.alloc(kBins, true);
       h->lut_log.alloc(kBins);
@@ -338,7 +340,7 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
     TMH_HIP(hipStreamWaitEvent(hs, h->ev_fork, 0));
   }
   launch_welford(d, h->npx, ns, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
-                 log_transform, s);
+                 log_transform, h->wf_part.p, h->wf_part.n, s);
   // order statistics, in chunks so the per-site slabs stay bounded
   for (int64_t c0 = 0; c0 < ns; c0 += chunk) {
     const int64_t nc = std::min(chunk, ns - c0);
@@ -375,7 +377,7 @@ int tmh_stats_update_welford_device(tmh_stats* h, const uint16_t* dev_sites, int
       h->rn.alloc((size_t)n_sites);
     }
     launch_welford(dev_sites, h->npx, n_sites, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
-                   log_transform, s);
+                   log_transform, h->wf_part.p, h->wf_part.n, s);
     h->n += n_sites;
     h->pending += n_sites;
   });

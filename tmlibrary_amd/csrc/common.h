@@ -63,9 +63,10 @@ struct QPos {
 };
 
 // launches (defined in the .hip files) -------------------------------------------
+// part: optional scratch of part_cap doubles for site-split launches (null: one part)
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
-                    hipStream_t s);
+                    double* part, size_t part_cap, hipStream_t s);
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
                          const QPos& p, uint16_t* vlo, uint16_t* vhi, unsigned long long* pooled,
                          int64_t* zero_counts, uint32_t* site_hist, hipStream_t s);

@@ -19,6 +19,9 @@
 //                    percentile into the f64 accumulator in SITE ORDER, without
 //                    FMA, so the sum is bit-identical to the reference's
 //                    sequential `_percentiles +=`.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace tmh {
@@ -66,6 +69,7 @@ __device__ __forceinline__ void welford1(double x, double rn, double& mu, double
 
 constexpr int kWfThreads = 256;
 constexpr int kWfGroup = 4;  // sites per pipeline stage (two stages in flight)
+constexpr int kWfMaxParts = 4;
 
 // 1/n for the sites of one launch (uniform per site: read with scalar loads)
 __global__ void k_rn_table(double* __restrict__ rn, int64_t n0, int64_t n) {
@@ -115,10 +119,14 @@ struct WfMerge {
 // so (mean_l - K)^2 <= (nl - 1) var and the cancellation in S2 - S1^2/nl
 // costs at most a factor nl of f64 precision (~1e-12 relative at 3456 sites,
 // against the 1e-6 bar); a constant pixel gives exactly 0.
+// blockIdx.y = site part: part p covers sites [p * per, min((p + 1) * per, n));
+// with more than one part each writes its (mean_l, M2_l) to `part` planes and
+// k_wf_merge_parts folds them in part order.
 template <bool LOG>
 __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
-    const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites, const WfMerge mg,
-    double* __restrict__ mean, double* __restrict__ m2, const double* __restrict__ lut) {
+    const uint16_t* __restrict__ sites, int64_t npx, int64_t n_total, int64_t per,
+    const WfMerge mg, double* __restrict__ mean, double* __restrict__ m2,
+    const double* __restrict__ lut, double* __restrict__ part) {
   __shared__ double slut[kWfLut];
   if (LOG)
     for (int i = threadIdx.x; i < kWfLut; i += kWfThreads) slut[i] = lut[i];
@@ -127,7 +135,9 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
   const int64_t g = (int64_t)blockIdx.x * kWfThreads + threadIdx.x;
   if (g >= ngroups) return;
 
-  const uint4* src = reinterpret_cast<const uint4*>(sites) + g;
+  const int64_t s_begin = (int64_t)blockIdx.y * per;
+  const int64_t n_sites = n_total - s_begin < per ? n_total - s_begin : per;
+  const uint4* src = reinterpret_cast<const uint4*>(sites) + s_begin * ngroups + g;
   const int64_t last = n_sites - 1;
   // two-stage pipeline: the next group's loads are in flight while the
   // current group is folded in (tail loads clamp to the last site: harmless)
@@ -161,6 +171,24 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
     for (int k = 0; k < kWfGroup; ++k) cur[k] = nxt[k];
   }
 
+  if (gridDim.y > 1) {  // partial (mean_l, M2_l) of this part
+    const double inv = 1.0 / (double)n_sites;
+    double2* pm = reinterpret_cast<double2*>(part + (2 * blockIdx.y) * npx) + g * 4;
+    double2* pq = reinterpret_cast<double2*>(part + (2 * blockIdx.y + 1) * npx) + g * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      double a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int j = 2 * k + i;
+        a[i] = K[j] + s1[j] * inv;
+        b[i] = fmax(s2[j] - s1[j] * (s1[j] * inv), 0.0);
+      }
+      pm[k] = make_double2(a[0], a[1]);
+      pq[k] = make_double2(b[0], b[1]);
+    }
+    return;
+  }
   double2* om = reinterpret_cast<double2*>(mean) + g * 4;
   double2* oq = reinterpret_cast<double2*>(m2) + g * 4;
   double mu[8], q[8];
@@ -192,6 +220,35 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
   }
 }
 
+struct WfParts {
+  double cnt[kWfMaxParts];  // sites per part
+  int n;                    // parts
+};
+
+// Fold the parts' (mean_l, M2_l) in part order (Chan's pairwise combine),
+// then into the running state (n0 sites before this launch).
+__global__ void k_wf_merge_parts(const double* __restrict__ part, int64_t npx, const WfParts pc,
+                                 double n0, double* __restrict__ mean, double* __restrict__ m2) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npx) return;
+  double na = pc.cnt[0], ma = part[i], qa = part[npx + i];
+  for (int p = 1; p < pc.n; ++p) {
+    const double nb = pc.cnt[p], mb = part[(2 * p) * npx + i], qb = part[(2 * p + 1) * npx + i];
+    const double n = na + nb, d = mb - ma;
+    ma = fma(d, nb / n, ma);
+    qa = qa + qb + d * d * (na * nb / n);
+    na = n;
+  }
+  if (n0 > 0) {
+    const double n = n0 + na, d = ma - mean[i];
+    mean[i] = fma(d, na / n, mean[i]);
+    m2[i] = m2[i] + qa + d * d * (n0 * na / n);
+  } else {
+    mean[i] = ma;
+    m2[i] = qa;
+  }
+}
+
 // Any shape (npx % 8 != 0 leaves sites unaligned for 16-B loads): 1 px/thread.
 template <bool LOG>
 __global__ __launch_bounds__(kWfThreads) void k_welford_scalar(
@@ -211,30 +268,83 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_scalar(
   m2[p] = q;
 }
 
+// Site parts for one launch.  Each thread streams every site of its part, so
+// a launch is a few long "rounds" of resident workgroups; when the pixel
+// groups leave the last round mostly empty (2160x2560: 2,700 workgroups over
+// 1,024 resident -> 2.64 rounds), splitting the sites into f parts evens it
+// out (f = 3: 7.9 rounds of 1/3 the work) for one extra pass over 16*f B/px
+// of partial state.  TMH_WF_PARTS overrides (experiments).
+static int welford_parts(int64_t n_wg, int64_t n_sites, int64_t npx, size_t part_cap) {
+  static const int forced = [] {
+    const char* e = getenv("TMH_WF_PARTS");
+    return e ? atoi(e) : 0;
+  }();
+  static const int64_t slots = [] {
+    int dev = 0, cu = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_welford_vec8<true>, kWfThreads, 0) !=
+            hipSuccess)
+      return (int64_t)0;
+    return (int64_t)cu * per_cu;
+  }();
+  auto fits = [&](int f) {
+    return f >= 1 && f <= kWfMaxParts && (f == 1 || ((size_t)2 * f * npx <= part_cap &&
+                                                    n_sites >= (int64_t)f * 32));
+  };
+  if (forced) return fits(forced) ? forced : 1;
+  if (slots <= 0) return 1;
+  int best = 1;
+  double best_t = (double)((n_wg + slots - 1) / slots);
+  for (int f = 2; f <= kWfMaxParts; ++f) {
+    if (!fits(f)) continue;
+    const double t = (double)((n_wg * f + slots - 1) / slots) / f + 0.02 * f;  // + merge pass
+    if (t < best_t - 1e-9) {
+      best_t = t;
+      best = f;
+    }
+  }
+  return best;
+}
+
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
-                    hipStream_t s) {
+                    double* part, size_t part_cap, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("welford", s);
   const bool vec = (npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0;
-  const dim3 grid((unsigned)(vec ? cdiv(npx >> 3, kWfThreads) : cdiv(npx, kWfThreads)));
-  if (!vec)  // the per-pixel Welford of odd shapes reads 1/n per site
+  if (vec) {
+    const int64_t n_wg = cdiv(npx >> 3, kWfThreads);
+    const int f = part ? welford_parts(n_wg, n_sites, npx, part_cap) : 1;
+    const int64_t per = cdiv(n_sites, f);
+    const double nl = (double)n_sites, n = (double)(n0 + n_sites);
+    const WfMerge mg{1.0 / nl, nl / n, (double)n0 * nl / n, n0 == 0};
+    const dim3 grid((unsigned)n_wg, (unsigned)f);
+    if (log_transform)
+      hipLaunchKernelGGL(k_welford_vec8<true>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
+                         per, mg, mean, m2, lut, part);
+    else
+      hipLaunchKernelGGL(k_welford_vec8<false>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
+                         per, mg, mean, m2, lut, part);
+    if (f > 1) {
+      WfParts pc{};
+      pc.n = f;
+      for (int p = 0; p < f; ++p)
+        pc.cnt[p] = (double)std::min<int64_t>(per, n_sites - (int64_t)p * per);
+      hipLaunchKernelGGL(k_wf_merge_parts, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, part,
+                         npx, pc, (double)n0, mean, m2);
+    }
+  } else {  // the per-pixel Welford of odd shapes reads 1/n per site
+    const dim3 grid((unsigned)cdiv(npx, kWfThreads));
     hipLaunchKernelGGL(k_rn_table, dim3((unsigned)cdiv(n_sites, 256)), dim3(256), 0, s, rn, n0,
                        n_sites);
-  const double nl = (double)n_sites, n = (double)(n0 + n_sites);
-  const WfMerge mg{1.0 / nl, nl / n, (double)n0 * nl / n, n0 == 0};
-  if (vec && log_transform)
-    hipLaunchKernelGGL(k_welford_vec8<true>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites, mg,
-                       mean, m2, lut);
-  else if (vec)
-    hipLaunchKernelGGL(k_welford_vec8<false>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites, mg,
-                       mean, m2, lut);
-  else if (log_transform)
-    hipLaunchKernelGGL(k_welford_scalar<true>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
-                       rn, mean, m2, lut);
-  else
-    hipLaunchKernelGGL(k_welford_scalar<false>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
-                       rn, mean, m2, lut);
+    if (log_transform)
+      hipLaunchKernelGGL(k_welford_scalar<true>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
+                         rn, mean, m2, lut);
+    else
+      hipLaunchKernelGGL(k_welford_scalar<false>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
+                         rn, mean, m2, lut);
+  }
   TMH_HIP(hipGetLastError());
 }
 
@@ -293,7 +403,7 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, in
   return woff + incl - c;
 }
 
-constexpr int kTailChunk = 8;  // rounds whose counts are loaded together
+constexpr int kTailChunkDefault = 8;  // rounds whose counts are loaded together
 // first index i >= t with R[i] > x (R: 1024 non-decreasing inclusive prefix
 // ranks in LDS; the caller guarantees R[1023] > x).  Consecutive quantile
 // positions mostly stay in one bin or step to the next, so two probes settle
@@ -339,7 +449,7 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
   const int32_t a = (int32_t)r0, b = (int32_t)r1;
   for (int64_t g = (qa >> 3) + threadIdx.x; g <= g1; g += kHistThreads) {
     const int64_t q0 = g << 3;
-    int32_t pl[8], ph[8];
+    int32_t pl[8];
     if (tab16 && q0 + 8 <= p.Q) {
       const int4 a0 = reinterpret_cast<const int4*>(p.lo + q0)[0];
       const int4 a1 = reinterpret_cast<const int4*>(p.lo + q0)[1];
@@ -349,50 +459,41 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
 #pragma unroll
       for (int j = 0; j < 8; ++j) pl[j] = q0 + j < p.Q ? p.lo[q0 + j] : INT32_MAX;
     }
-    if (p.hi_next) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ph[j] = pl[j] < p.last ? pl[j] + 1 : pl[j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ph[j] = q0 + j < p.Q ? p.hi[q0 + j] : INT32_MAX;
-    }
     // positions are non-decreasing in q: the first one inside the round
     // starts the scan at bin 0, every later one continues from its
-    // predecessor's bin
-    uint32_t vl[8], vh[8];
+    // predecessor's bin.  Results are packed as they come (u16 pairs).
+    uint32_t ol[4] = {0u, 0u, 0u, 0u}, oh[4] = {0u, 0u, 0u, 0u};
     uint32_t ml = 0, mh = 0;
     int tl = 0, th = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      vl[j] = vh[j] = 0u;
-      if (pl[j] >= a && pl[j] < b) {
-        tl = advance_rank(R, tl, pl[j]);
-        vl[j] = bin0 + (uint32_t)tl;
+      const int32_t pj = pl[j];
+      if (pj >= a && pj < b) {
+        tl = advance_rank(R, tl, pj);
+        ol[j >> 1] |= (bin0 + (uint32_t)tl) << (16 * (j & 1));
         ml |= 1u << j;
       }
-      if (ph[j] >= a && ph[j] < b) {
-        th = advance_rank(R, th > tl ? th : tl, ph[j]);
-        vh[j] = bin0 + (uint32_t)th;
+      const int32_t hj = p.hi_next ? (pj < p.last ? pj + 1 : pj)
+                                   : (q0 + j < p.Q ? p.hi[q0 + j] : INT32_MAX);
+      if (hj >= a && hj < b) {
+        th = advance_rank(R, th > tl ? th : tl, hj);
+        oh[j >> 1] |= (bin0 + (uint32_t)th) << (16 * (j & 1));
         mh |= 1u << j;
       }
     }
     if (vec16 && ml == 0xFFu) {
-      *reinterpret_cast<uint4*>(vlo + q0) =
-          make_uint4(vl[0] | (vl[1] << 16), vl[2] | (vl[3] << 16), vl[4] | (vl[5] << 16),
-                     vl[6] | (vl[7] << 16));
+      *reinterpret_cast<uint4*>(vlo + q0) = make_uint4(ol[0], ol[1], ol[2], ol[3]);
     } else if (ml) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if ((ml >> j) & 1u) vlo[q0 + j] = (uint16_t)vl[j];
+        if ((ml >> j) & 1u) vlo[q0 + j] = (uint16_t)(ol[j >> 1] >> (16 * (j & 1)));
     }
     if (vec16 && mh == 0xFFu) {
-      *reinterpret_cast<uint4*>(vhi + q0) =
-          make_uint4(vh[0] | (vh[1] << 16), vh[2] | (vh[3] << 16), vh[4] | (vh[5] << 16),
-                     vh[6] | (vh[7] << 16));
+      *reinterpret_cast<uint4*>(vhi + q0) = make_uint4(oh[0], oh[1], oh[2], oh[3]);
     } else if (mh) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if ((mh >> j) & 1u) vhi[q0 + j] = (uint16_t)vh[j];
+        if ((mh >> j) & 1u) vhi[q0 + j] = (uint16_t)(oh[j >> 1] >> (16 * (j & 1)));
     }
   }
 }
@@ -410,7 +511,7 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
 // after its count has been used (e.g. to reset it).
 // ABL (development ablations, tools/mb; 0 in production): 1 = no order-
 // statistic output, 4 = no pooled histogram adds
-template <int ABL = 0, typename CountFn, typename DoneFn>
+template <int ABL = 0, int kTailChunk = kTailChunkDefault, typename CountFn, typename DoneFn>
 __device__ __forceinline__ void hist_tail(CountFn count, DoneFn done, int64_t s, const QPos& p,
                                           uint16_t* __restrict__ vlo_all,
                                           uint16_t* __restrict__ vhi_all,
@@ -528,7 +629,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
 // a complete histogram held in global memory (zero-maintained: every count is
 // read and reset), e.g. accumulated by the fused correct+histogram pass.
 template <int ABL = 0>  // ABL 8: counts are not reset (re-runnable)
-__global__ __launch_bounds__(kHistThreads) void k_hist_finalize(
+__global__ __launch_bounds__(kHistThreads, 8) void k_hist_finalize(
     uint32_t* __restrict__ hist, const QPos p, uint16_t* __restrict__ vlo_all,
     uint16_t* __restrict__ vhi_all, unsigned long long* __restrict__ pooled, int n_pooled,
     int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist) {
@@ -542,7 +643,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_finalize(
   // sites spread their pooled-histogram adds over n_pooled copies (fewer
   // same-address atomic collisions); k_pooled_fold sums the copies
   unsigned long long* pl = pooled + (int64_t)(blockIdx.x % n_pooled) * kBins;
-  hist_tail<ABL & 7>(
+  hist_tail<ABL & 7, 4>(
       [&](uint32_t b) -> uint32_t { return h[b]; },
       [&](uint32_t b, uint32_t c) {
         if (!(ABL & 8) && c) h[b] = 0u;
@@ -608,7 +709,7 @@ __device__ __forceinline__ double add_nc(double x, double y) {
 }
 
 constexpr int kPctThreads = 256;
-constexpr int kPctUnroll = 8;
+constexpr int kPctUnroll = 16;
 
 // each thread: two consecutive quantiles (one u32 load of each u16 array)
 __global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint16_t* __restrict__ vlo,
@@ -624,24 +725,36 @@ __global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint16_t* __restr
   const int64_t stride = Q / 2;  // u32 per site (Q even on this path)
   const uint32_t* pl = reinterpret_cast<const uint32_t*>(vlo) + q0 / 2;
   const uint32_t* ph = reinterpret_cast<const uint32_t*>(vhi) + q0 / 2;
-  int64_t s = 0;
-  for (; s + kPctUnroll <= n_sites; s += kPctUnroll) {
-    uint32_t l[kPctUnroll], h[kPctUnroll];
+  // software pipeline: the next kPctUnroll sites' loads are in flight while
+  // the current ones are folded in (tail loads clamp to the last site)
+  const int64_t last = n_sites - 1;
+  uint32_t l[kPctUnroll], h[kPctUnroll];
 #pragma unroll
-    for (int k = 0; k < kPctUnroll; ++k) {
-      l[k] = pl[(s + k) * stride];
-      h[k] = ph[(s + k) * stride];
-    }
-#pragma unroll
-    for (int k = 0; k < kPctUnroll; ++k) {
-      a0 = add_nc(a0, lerp_np(l[k] & 0xFFFFu, h[k] & 0xFFFFu, g0));
-      a1 = add_nc(a1, lerp_np(l[k] >> 16, h[k] >> 16, g1));
-    }
+  for (int k = 0; k < kPctUnroll; ++k) {
+    const int64_t t = k < last ? k : last;
+    l[k] = pl[t * stride];
+    h[k] = ph[t * stride];
   }
-  for (; s < n_sites; ++s) {
-    const uint32_t l = pl[s * stride], h = ph[s * stride];
-    a0 = add_nc(a0, lerp_np(l & 0xFFFFu, h & 0xFFFFu, g0));
-    a1 = add_nc(a1, lerp_np(l >> 16, h >> 16, g1));
+  for (int64_t s = 0; s < n_sites; s += kPctUnroll) {
+    uint32_t ln[kPctUnroll], hn[kPctUnroll];
+#pragma unroll
+    for (int k = 0; k < kPctUnroll; ++k) {
+      const int64_t t = s + kPctUnroll + k < last ? s + kPctUnroll + k : last;
+      ln[k] = pl[t * stride];
+      hn[k] = ph[t * stride];
+    }
+#pragma unroll
+    for (int k = 0; k < kPctUnroll; ++k) {
+      if (s + k < n_sites) {
+        a0 = add_nc(a0, lerp_np(l[k] & 0xFFFFu, h[k] & 0xFFFFu, g0));
+        a1 = add_nc(a1, lerp_np(l[k] >> 16, h[k] >> 16, g1));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kPctUnroll; ++k) {
+      l[k] = ln[k];
+      h[k] = hn[k];
+    }
   }
   acc[q0] = a0;
   if (two) acc[q0 + 1] = a1;

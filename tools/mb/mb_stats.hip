@@ -453,12 +453,17 @@ int main(int argc, char** argv) {
   std::vector<double> hl(65536);
   for (int v = 0; v < 65536; ++v) hl[v] = v ? log10((double)v) : 0.0;
   CK(hipMemcpy(lut, hl.data(), 65536 * 8, hipMemcpyHostToDevice));
-  for (int r = 0; r < reps; ++r) {
-    CK(hipMemset(mean, 0, npx * 8));
-    CK(hipMemset(m2, 0, npx * 8));
-    t.start();
-    launch_welford(sites, npx, S, 0, rn, mean, m2, lut, 1, 0);
-    report("welford (prod)", t.stop(), S * site_gb);
+  double* wpart;
+  CK(hipMalloc(&wpart, 8 * npx * 8));
+  for (int split = 0; split < 2; ++split) {
+    for (int r = 0; r < reps; ++r) {
+      CK(hipMemset(mean, 0, npx * 8));
+      CK(hipMemset(m2, 0, npx * 8));
+      t.start();
+      launch_welford(sites, npx, S, 0, rn, mean, m2, lut, 1, split ? wpart : nullptr,
+                     split ? (size_t)8 * npx : 0, 0);
+      report(split ? "welford (prod, site parts)" : "welford (one part)", t.stop(), S * site_gb);
+    }
   }
 
   if (getenv("MB_WF")) {
