@@ -129,6 +129,12 @@ int tmh_stats_merge_stage3(tmh_stats* h, int64_t n_total, const double* dev_sum_
  * in local site order (deferred mode).  Rank r runs this on the accumulator
  * received from rank r-1, keeping the reference's sequential summation. */
 int tmh_stats_pct_accumulate(tmh_stats* h, double* dev_acc, void* stream);
+/* Same for quantiles [q_begin, q_begin + q_count) only; dev_acc_range points at
+ * the range's first element.  Lets the rank chain run as a pipeline over
+ * quantile chunks (rank r adds chunk c while rank r-1 adds chunk c+1); each
+ * quantile still sees every rank's sites in order (bit-exact). */
+int tmh_stats_pct_accumulate_range(tmh_stats* h, double* dev_acc_range, int q_begin, int q_count,
+                                   void* stream);
 int tmh_stats_set_pct_sum(tmh_stats* h, const double* dev_acc, void* stream);
 
 /* ---- smoothing -----------------------------------------------------------

@@ -527,3 +527,39 @@ def test_welford_site_parts(L, parts):
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "split ok" in r.stdout
+
+
+def test_pipelined_chain_ranges_bit_exact(L):
+    """tmh_stats_pct_accumulate_range over quantile chunks, chunk-major across
+    two 'ranks' (the pipelined chain's order), equals the sequential sum."""
+    from tmlibrary_amd import hip
+    from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
+    from tmlibrary_amd.workflow.corilla.sharded import chain_chunks
+    sites = np.stack(load_golden("stats_medium")["sites"])
+    n, H, W = sites.shape
+    Q = 100000
+    lo, hi, gamma = quantile_table(H * W, np.linspace(0, 100, Q))
+    lut = stats_log10_lut()
+    parts = [sites[:2], sites[2:]]
+    hs = []
+    for p in parts:
+        h = C.c_void_p()
+        hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
+                                     hip.ptr(lut), 4, hip.TMH_STATS_DEFERRED_PCT, C.byref(h)))
+        hip.check(L.tmh_stats_update(h, hip.ptr(np.ascontiguousarray(p)), len(p), 1, None))
+        hs.append(h)
+    L.tmh_synchronize(None)
+    acc = Dev(L, Q * 8)
+    acc.put(np.zeros(Q))
+    for q0, qn in chain_chunks(Q, 2, chunks=7) + [(Q, 0)]:
+        for h in hs:
+            hip.check(L.tmh_stats_pct_accumulate_range(h, C.c_void_p(acc.p.value + 8 * q0), q0, qn,
+                                                       None))
+            L.tmh_synchronize(None)
+    got = acc.get(np.float64, Q)
+    ref = orc.run_illumstats(list(sites))
+    assert np.array_equal(got, ref.percentile_sums)
+    assert hip.lib().tmh_stats_pct_accumulate_range(hs[0], acc.p, Q - 2, 4, None) != 0
+    for h in hs:
+        L.tmh_stats_destroy(h)
+    acc.free()

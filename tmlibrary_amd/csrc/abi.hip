@@ -514,6 +514,19 @@ int tmh_stats_pct_accumulate(tmh_stats* h, double* dev_acc, void* stream) {
   });
 }
 
+int tmh_stats_pct_accumulate_range(tmh_stats* h, double* dev_acc_range, int q_begin, int q_count,
+                                   void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && dev_acc_range, TMH_EINVAL, "bad arguments");
+    TMH_CHECK(h->flags & TMH_STATS_DEFERRED_PCT, TMH_ESTATE,
+              "percentile chain needs a TMH_STATS_DEFERRED_PCT handle");
+    TMH_CHECK(q_begin >= 0 && q_count >= 0 && (int64_t)q_begin + q_count <= h->Q, TMH_EINVAL,
+              "quantile range out of bounds");
+    launch_pct_accumulate_range(h->vlo.p, h->vhi.p, h->n_deferred, h->Q, q_begin, q_count,
+                                h->gamma.p, dev_acc_range, pick(h->stream, stream));
+  });
+}
+
 int tmh_stats_set_pct_sum(tmh_stats* h, const double* dev_acc, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_acc, TMH_EINVAL, "bad arguments");

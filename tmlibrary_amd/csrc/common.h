@@ -76,6 +76,10 @@ void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const QPos& p, uint16
                           uint32_t* site_hist, hipStream_t s);
 void launch_pct_accumulate(const uint16_t* vlo, const uint16_t* vhi, int64_t n_sites, int Q,
                            const double* gamma, double* acc, hipStream_t s);
+// quantiles [q_begin, q_begin + q_count) of rows of ld; acc points at the range
+void launch_pct_accumulate_range(const uint16_t* vlo, const uint16_t* vhi, int64_t n_sites,
+                                 int64_t ld, int q_begin, int q_count, const double* gamma,
+                                 double* acc, hipStream_t s);
 void launch_finalize(const double* mean, const double* m2, int64_t n, int64_t npx, double* out_mean,
                      double* out_std, hipStream_t s);
 void launch_merge1(const double* mean, int64_t n, int64_t npx, double* nmean, hipStream_t s);

@@ -709,12 +709,15 @@ __device__ __forceinline__ double add_nc(double x, double y) {
 }
 
 constexpr int kPctThreads = 256;
-constexpr int kPctUnroll = 16;
+constexpr int kPctUnroll = 32;
 
 // each thread: two consecutive quantiles (one u32 load of each u16 array)
+// Quantiles [0, Q) of rows of `ld` u16 (vlo/vhi/gamma/acc point at the range's
+// first quantile: a sub-range of the full table is one launch of the
+// pipelined rank chain).
 __global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint16_t* __restrict__ vlo,
                                                           const uint16_t* __restrict__ vhi,
-                                                          int64_t n_sites, int Q,
+                                                          int64_t n_sites, int Q, int64_t ld,
                                                           const double* __restrict__ gamma,
                                                           double* __restrict__ acc) {
   const int q0 = ((int)blockIdx.x * kPctThreads + threadIdx.x) * 2;
@@ -722,7 +725,7 @@ __global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint16_t* __restr
   const bool two = q0 + 1 < Q;
   const double g0 = gamma[q0], g1 = two ? gamma[q0 + 1] : 0.0;
   double a0 = acc[q0], a1 = two ? acc[q0 + 1] : 0.0;
-  const int64_t stride = Q / 2;  // u32 per site (Q even on this path)
+  const int64_t stride = ld / 2;  // u32 per site (ld, Q and the offset even on this path)
   const uint32_t* pl = reinterpret_cast<const uint32_t*>(vlo) + q0 / 2;
   const uint32_t* ph = reinterpret_cast<const uint32_t*>(vhi) + q0 / 2;
   // software pipeline: the next kPctUnroll sites' loads are in flight while
@@ -762,29 +765,38 @@ __global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint16_t* __restr
 
 __global__ __launch_bounds__(kPctThreads) void k_pct_acc_odd(const uint16_t* __restrict__ vlo,
                                                               const uint16_t* __restrict__ vhi,
-                                                              int64_t n_sites, int Q,
+                                                              int64_t n_sites, int Q, int64_t ld,
                                                               const double* __restrict__ gamma,
                                                               double* __restrict__ acc) {
   const int q = (int)blockIdx.x * kPctThreads + threadIdx.x;
   if (q >= Q) return;
   const double g = gamma[q];
   double a = acc[q];
-  for (int64_t s = 0; s < n_sites; ++s) a = add_nc(a, lerp_np(vlo[s * Q + q], vhi[s * Q + q], g));
+  for (int64_t s = 0; s < n_sites; ++s) a = add_nc(a, lerp_np(vlo[s * ld + q], vhi[s * ld + q], g));
   acc[q] = a;
 }
 
 void launch_pct_accumulate(const uint16_t* vlo, const uint16_t* vhi, int64_t n_sites, int Q,
                            const double* gamma, double* acc, hipStream_t s) {
-  if (n_sites <= 0) return;
+  launch_pct_accumulate_range(vlo, vhi, n_sites, Q, 0, Q, gamma, acc, s);
+}
+
+void launch_pct_accumulate_range(const uint16_t* vlo, const uint16_t* vhi, int64_t n_sites,
+                                 int64_t ld, int q_begin, int q_count, const double* gamma,
+                                 double* acc, hipStream_t s) {
+  if (n_sites <= 0 || q_count <= 0) return;
   ProfScope prof("pct_acc", s);
-  if ((Q & 1) == 0) {
-    const int grid = (int)cdiv(Q / 2, kPctThreads);
-    hipLaunchKernelGGL(k_pct_acc, dim3(grid), dim3(kPctThreads), 0, s, vlo, vhi, n_sites, Q, gamma,
-                       acc);
+  vlo += q_begin;
+  vhi += q_begin;
+  gamma += q_begin;
+  if ((ld & 1) == 0 && (q_begin & 1) == 0 && (q_count & 1) == 0) {
+    const int grid = (int)cdiv(q_count / 2, kPctThreads);
+    hipLaunchKernelGGL(k_pct_acc, dim3(grid), dim3(kPctThreads), 0, s, vlo, vhi, n_sites, q_count,
+                       ld, gamma, acc);
   } else {
-    const int grid = (int)cdiv(Q, kPctThreads);
-    hipLaunchKernelGGL(k_pct_acc_odd, dim3(grid), dim3(kPctThreads), 0, s, vlo, vhi, n_sites, Q,
-                       gamma, acc);
+    const int grid = (int)cdiv(q_count, kPctThreads);
+    hipLaunchKernelGGL(k_pct_acc_odd, dim3(grid), dim3(kPctThreads), 0, s, vlo, vhi, n_sites,
+                       q_count, ld, gamma, acc);
   }
   TMH_HIP(hipGetLastError());
 }

@@ -52,6 +52,7 @@ SIGNATURES = {
     "tmh_stats_merge_stage2": (_I, [_P, _P, _I64, _P, _P]),
     "tmh_stats_merge_stage3": (_I, [_P, _I64, _P, _P]),
     "tmh_stats_pct_accumulate": (_I, [_P, _P, _P]),
+    "tmh_stats_pct_accumulate_range": (_I, [_P, _P, _I, _I, _P]),
     "tmh_stats_set_pct_sum": (_I, [_P, _P, _P]),
     "tmh_smooth_f64": (_I, [_P, _P, _I, _I, _D]),
     "tmh_smooth_f64_device": (_I, [_P, _P, _P, _I, _I, _D, _P]),

@@ -75,6 +75,10 @@ class StatsOps(object):
         self._chk(self.L.tmh_stats_pct_accumulate(self.h, C.c_void_p(acc.data_ptr()),
                                                   self._stream()))
 
+    def pct_accumulate_range(self, acc_range, q_begin, q_count):
+        self._chk(self.L.tmh_stats_pct_accumulate_range(
+            self.h, C.c_void_p(acc_range.data_ptr()), int(q_begin), int(q_count), self._stream()))
+
     def set_pct_sum(self, acc):
         self._chk(self.L.tmh_stats_set_pct_sum(self.h, C.c_void_p(acc.data_ptr()), self._stream()))
 
@@ -98,18 +102,39 @@ def merge_welford(ops, dist, group=None, int_device=None):
     return n_total
 
 
-def merge_percentiles(ops, dist, group=None):
+def chain_chunks(n_quantiles, world, chunks=None):
+    """Even-aligned quantile ranges for the pipelined rank chain: with C
+    chunks the chain takes (N + C - 1) chunk-steps instead of N full steps."""
+    Q = int(n_quantiles)
+    if chunks is None:
+        chunks = 1 if world <= 1 else min(2 * world, 16)
+    chunks = max(1, min(int(chunks), max(1, Q // 2)))
+    edges = [((Q * i // chunks) // 2) * 2 for i in range(chunks)] + [Q]
+    return [(a, b - a) for a, b in zip(edges[:-1], edges[1:]) if b > a]
+
+
+def merge_percentiles(ops, dist, group=None, chunks=None):
     """Ordered percentile chain: the f64 accumulator travels rank 0 -> N-1,
     each rank adding its own sites in order (bit-exact sequential sum), and
-    the last rank broadcasts it."""
+    the last rank broadcasts it.  The accumulator is split into quantile
+    chunks that flow down the chain as a pipeline (rank r adds chunk c while
+    rank r-1 adds chunk c+1); every quantile still sees the ranks' sites in
+    global site order."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     acc = ops.empty_acc()
-    if rank > 0:
-        dist.recv(acc, src=rank - 1, group=group)
-    ops.pct_accumulate(acc)
-    if rank < world - 1:
-        dist.send(acc, dst=rank + 1, group=group)
+    ranged = getattr(ops, "pct_accumulate_range", None) is not None
+    spans = chain_chunks(acc.numel(), world, chunks) if ranged else [(0, acc.numel())]
+    for q0, qn in spans:
+        part = acc[q0:q0 + qn]
+        if rank > 0:
+            dist.recv(part, src=rank - 1, group=group)
+        if ranged:
+            ops.pct_accumulate_range(part, q0, qn)
+        else:
+            ops.pct_accumulate(acc)
+        if rank < world - 1:
+            dist.send(part, dst=rank + 1, group=group)
     dist.broadcast(acc, src=world - 1, group=group)
     ops.set_pct_sum(acc)
 
