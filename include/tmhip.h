@@ -155,6 +155,14 @@ int tmh_smooth_f64_device(const double* dev_in, double* dev_out, double* dev_tmp
  * lut_zero_log10 = np.log10(1e-10) from the host numpy.  The float result is
  * cast with the x86 astype rule (trunc to int32, low bits) and optionally
  * clipped to [clip_lo, clip_hi] (clip_lo < 0: no clip). */
+/* One site's alignment window (Image.align, tmlib/image.py:345-454): output
+ * pixel (r, c) with 0 <= r - dst_r0 < rows and 0 <= c - dst_c0 < cols takes
+ * input pixel (r - dst_r0 + src_r0, c - dst_c0 + src_c0); every other output
+ * pixel is 0.  The host evaluates the reference's numpy slicing into it. */
+typedef struct tmh_window {
+  int32_t src_r0, src_c0, dst_r0, dst_c0, rows, cols;
+} tmh_window;
+
 typedef struct tmh_corrector tmh_corrector;
 
 int tmh_corrector_create(const double* host_mean, const double* host_std, int height, int width,
@@ -180,6 +188,27 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
                                 void* stream);
 int tmh_correct_u8(tmh_corrector* c, const uint8_t* host_in, uint8_t* host_out, int64_t n_sites,
                    int clip_lo, int clip_hi);
+/* ---- illuminati chain ------------------------------
+ * Image.align (tmlib/image.py:412-454) of n_sites images [n][height][width] of
+ * elem_bytes 1 (uint8) or 2 (uint16) into [n][out_height][out_width]: crop=True
+ * gives out = window extent, crop=False out = input size, zero padded. */
+int tmh_align(const void* host_in, void* host_out, int elem_bytes, int64_t n_sites, int height,
+              int width, const tmh_window* windows, int out_height, int out_width);
+/* ChannelImage._map_to_uint8 (tmlib/image.py:493-531) with explicit bounds
+ * (0 <= lower < upper <= 65535): the reference's numpy LUT, bit-exact. */
+int tmh_map_u16_to_u8(const uint16_t* host_in, uint8_t* host_out, int64_t n, int lower,
+                      int upper);
+/* illuminati/api.py:396-405 in one pass: correct (this corrector's statistics)
+ * -> align(crop=False) with each site's window -> clip(clip_lo, clip_hi) ->
+ * scale(clip_lo, clip_hi) to uint8.  Corrected values within +-1 DN of the
+ * reference before the clip/scale (the +-1 DN bar of the correction). */
+int tmh_correct_chain_u8_device(tmh_corrector* c, const uint16_t* dev_in, uint8_t* dev_out,
+                                int64_t n_sites, const tmh_window* host_windows, int clip_lo,
+                                int clip_hi, void* stream);
+int tmh_correct_chain_u8(tmh_corrector* c, const uint16_t* host_in, uint8_t* host_out,
+                         int64_t n_sites, const tmh_window* host_windows, int clip_lo,
+                         int clip_hi);
+
 /* ChannelImage.clip alone (image.py:589), u16. */
 int tmh_clip_u16(const uint16_t* host_in, uint16_t* host_out, int64_t n, int lo, int hi);
 

@@ -11,6 +11,7 @@ source is copied; the fixtures are data only.  Bytecode writing is disabled
 so nothing is written under /root/reference.
 
     python tests/golden/make_goldens.py            # (re)write all fixtures
+    python tests/golden/make_goldens.py chain align   # only the named ones
 """
 from __future__ import annotations
 
@@ -139,10 +140,14 @@ def main():
 
     index = {}
 
+    only = set(sys.argv[1:])  # fixture names to (re)write; empty: all
+
     def save(name, **arrays):
+        index[name] = sorted(arrays.keys())
+        if only and name not in only:
+            return
         path = os.path.join(HERE, name + ".npz")
         np.savez_compressed(path, **arrays)
-        index[name] = sorted(arrays.keys())
         print("wrote", path, os.path.getsize(path), "bytes")
 
     # --- stats cases ------------------------------------------------------
@@ -212,6 +217,63 @@ def main():
                          np.inf, -np.inf, np.nan, 1e300, 255.5, 256.0, 300.0], dtype=np.float64)
     save("cast_rule", values=specials, as_u16=specials.astype(np.uint16),
          as_u8=specials.astype(np.uint8))
+
+    # --- illuminati chain (§8(f) rank 3): align, map_to_uint8, full chain --
+    rng = np.random.default_rng(5151)
+    al_img = rng.integers(0, 65536, size=(40, 56), dtype=np.uint16)
+    al_cases = [(0, 0, 0, 0, 0, 0), (2, -3, 1, 2, 3, 4), (-2, 3, 2, 0, 0, 3), (3, 4, 0, 3, 4, 0),
+                (-3, -4, 3, 0, 0, 4), (1, 1, 3, 3, 4, 4), (0, 2, 0, 0, 0, 2), (-1, 0, 1, 1, 0, 0)]
+    al_out_pad, al_out_crop = [], []
+    for (y, x, bottom, top, right, left) in al_cases:
+        for crop in (False, True):
+            md = metadata.ChannelImageMetadata(channel_id=1, site_id=1, cycle_id=1, tpoint=0,
+                                               zplane=0)
+            md.y_shift, md.x_shift = y, x
+            md.bottom_residue, md.top_residue = bottom, top
+            md.right_residue, md.left_residue = right, left
+            got = image.ChannelImage(al_img.copy(), md).align(crop=crop).array
+            o = orc.shift_and_crop(al_img, y, x, bottom, top, right, left, crop=crop)
+            assert np.array_equal(o, got), ("align", y, x, crop)
+            (al_out_crop if crop else al_out_pad).append(got)
+    save("align", image=al_img, cases=np.array(al_cases, dtype=np.int64),
+         padded=np.stack(al_out_pad),
+         **{"cropped_%d" % i: a for i, a in enumerate(al_out_crop)})
+
+    full_range = np.arange(65536, dtype=np.uint16).reshape(256, 256)
+    bounds = [(0, 1), (0, 65535), (700, 701), (100, 4000), (3, 700), (65534, 65535), (12, 13000)]
+    luts = np.stack([image.ChannelImage._map_to_uint8(full_range, lo, hi).ravel()
+                     for lo, hi in bounds])
+    for (lo, hi), lut in zip(bounds, luts):
+        assert np.array_equal(orc.map_to_uint8(full_range, lo, hi).ravel(), lut)
+    save("map_uint8", bounds=np.array(bounds, dtype=np.int64), luts=luts)
+
+    apply = dict(np.load(os.path.join(HERE, "apply_log.npz")))
+    sm_mean, sm_std = apply["smooth_mean"], apply["smooth_std"]
+    md_s = metadata.IllumstatsImageMetadata(channel_id=1)
+    stats_c = image.IllumstatsContainer(image.IllumstatsImage(sm_mean.copy(), md_s),
+                                        image.IllumstatsImage(sm_std.copy(), md_s), {})
+    chain_imgs = synth(4, 96, 128, seed=6161)
+    chain_imgs[0][0, :8] = 0
+    shifts = np.array([[0, 0], [2, -3], [-3, 4], [1, 1]], dtype=np.int64)
+    residues = np.array([3, 3, 4, 4], dtype=np.int64)  # bottom, top, right, left
+    clip_lo, clip_hi = int(apply["clip_lo"]), int(apply["clip_hi"])
+    chained = []
+    for img, (y, x) in zip(chain_imgs, shifts):
+        md = metadata.ChannelImageMetadata(channel_id=1, site_id=1, cycle_id=1, tpoint=0, zplane=0)
+        md.y_shift, md.x_shift = int(y), int(x)
+        md.bottom_residue, md.top_residue, md.right_residue, md.left_residue = map(int, residues)
+        im = image.ChannelImage(img.copy(), md)
+        im = im.correct(stats_c)
+        im = im.align(crop=False)
+        im = im.clip(clip_lo, clip_hi)
+        im = im.scale(clip_lo, clip_hi)
+        chained.append(im.array)
+        o = orc.illuminati_chain(img, sm_mean, sm_std, (int(y), int(x)), tuple(residues), clip_lo,
+                                 clip_hi)
+        assert np.array_equal(o, im.array), "oracle chain != reference"
+    save("chain", images=np.stack(chain_imgs), smooth_mean=sm_mean, smooth_std=sm_std,
+         shifts=shifts, residues=residues, clip_lo=np.int64(clip_lo), clip_hi=np.int64(clip_hi),
+         scaled=np.stack(chained))
 
     # --- full-size sites (2160 x 2560): seeds + digests + samples ---------
     H, W = 2160, 2560

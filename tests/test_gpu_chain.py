@@ -1,0 +1,166 @@
+"""GPU parity of the illuminati post-correct chain:
+Image.align, ChannelImage._map_to_uint8 / scale, and the fused
+correct -> align(crop=False) -> clip -> scale pass, against fixtures generated
+from the reference (tests/golden/make_goldens.py: align, map_uint8, chain).
+
+Bars: align and the uint16 -> uint8 LUT bit-exact; the fused chain within the
+correction's +-1 DN carried through clip/scale (<= 1 uint8 step)."""
+import numpy as np
+import pytest
+
+from util import load_golden
+from oracle import corilla_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    from tmlibrary_amd import hip
+    return hip.lib()
+
+
+def _md(y=0, x=0, residues=(0, 0, 0, 0)):
+    from tmlibrary_amd.metadata import ChannelImageMetadata
+    md = ChannelImageMetadata(channel_id=1, site_id=1, cycle_id=1, tpoint=0, zplane=0)
+    md.y_shift, md.x_shift = int(y), int(x)
+    md.bottom_residue, md.top_residue, md.right_residue, md.left_residue = map(int, residues)
+    return md
+
+
+@pytest.mark.parametrize("dtype", [np.uint16, np.uint8])
+def test_align_vs_reference(L, dtype):
+    from tmlibrary_amd.image import ChannelImage
+    g = load_golden("align")
+    img = g["image"]
+    if dtype == np.uint8:
+        img = (img >> 8).astype(np.uint8)
+    for i, (y, x, b, t, r, l) in enumerate(g["cases"]):
+        for crop in (False, True):
+            got = ChannelImage(img.copy(), _md(y, x, (b, t, r, l))).align(crop=crop).array
+            want = g["cropped_%d" % i] if crop else g["padded"][i]
+            if dtype == np.uint8:
+                want = orc.shift_and_crop(img, y, x, b, t, r, l, crop=crop)
+            assert got.dtype == dtype
+            assert np.array_equal(got, want), (i, crop)
+
+
+def test_align_needs_metadata(L):
+    from tmlibrary_amd.image import ChannelImage
+    with pytest.raises(AttributeError):
+        ChannelImage(np.zeros((4, 4), np.uint16)).align()
+
+
+def test_map_to_uint8_lut_exhaustive(L):
+    """Every uint16 value through the GPU scale == the reference's numpy LUT."""
+    from tmlibrary_amd.image import ChannelImage
+    g = load_golden("map_uint8")
+    full = np.arange(65536, dtype=np.uint16).reshape(256, 256)
+    for (lo, hi), lut in zip(g["bounds"], g["luts"]):
+        got = ChannelImage._map_to_uint8(full, int(lo), int(hi))
+        assert np.array_equal(got.ravel(), lut), (lo, hi)
+
+
+def test_map_to_uint8_errors_and_defaults(L):
+    from tmlibrary_amd.image import ChannelImage
+    a = np.array([[5, 9], [300, 7]], dtype=np.uint16)
+    with pytest.raises(TypeError):
+        ChannelImage._map_to_uint8(a.astype(np.uint8), 0, 10)
+    with pytest.raises(ValueError):
+        ChannelImage._map_to_uint8(a, 10, 10)
+    with pytest.raises(ValueError):
+        ChannelImage._map_to_uint8(a, 0, 70000)
+    assert np.array_equal(ChannelImage._map_to_uint8(a), orc.map_to_uint8(a))
+    im = ChannelImage(a.copy(), _md()).scale(5, 300)
+    assert im.array.dtype == np.uint8 and im.metadata.is_rescaled
+    u8 = ChannelImage(np.ones((2, 2), np.uint8), _md())
+    assert u8.scale(0, 10) is u8
+
+
+def _chain_inputs():
+    from tmlibrary_amd.image import align_window
+    g = load_golden("chain")
+    wins = [align_window(g["images"].shape[1:], y, x, *g["residues"], crop=False)[0]
+            for y, x in g["shifts"]]
+    return g, np.stack(wins)
+
+
+def test_chain_fused_vs_reference(L):
+    from tmlibrary_amd.image import Corrector
+    g, wins = _chain_inputs()
+    corr = Corrector(g["smooth_mean"], g["smooth_std"])
+    got = corr.chain_u8(g["images"], wins, int(g["clip_lo"]), int(g["clip_hi"]))
+    corr.close()
+    d = np.abs(got.astype(np.int32) - g["scaled"].astype(np.int32))
+    assert d.max() <= 1
+    assert (d == 0).mean() > 0.99
+
+
+def test_chain_by_steps_vs_reference(L):
+    """The same chain through the drop-in API, one method at a time."""
+    from tmlibrary_amd.image import ChannelImage, IllumstatsContainer, IllumstatsImage
+    from tmlibrary_amd.metadata import IllumstatsImageMetadata
+    g, _ = _chain_inputs()
+    md_s = IllumstatsImageMetadata(channel_id=1)
+    stats = IllumstatsContainer(IllumstatsImage(g["smooth_mean"].copy(), md_s),
+                                IllumstatsImage(g["smooth_std"].copy(), md_s), {})
+    lo, hi = int(g["clip_lo"]), int(g["clip_hi"])
+    for img, (y, x), want in zip(g["images"], g["shifts"], g["scaled"]):
+        im = ChannelImage(img.copy(), _md(y, x, g["residues"]))
+        im = im.correct(stats).align(crop=False).clip(lo, hi).scale(lo, hi)
+        d = np.abs(im.array.astype(np.int32) - want.astype(np.int32))
+        assert d.max() <= 1
+
+
+@pytest.mark.parametrize("shape", [(256, 320), (70, 90)])
+def test_chain_device_random_windows(L, shape):
+    """Device-resident batch with per-site shifts (incl. odd column shifts and
+    an empty window) vs the oracle chain; odd widths take the scalar path."""
+    import ctypes as C
+    from tmlibrary_amd import hip
+    from tmlibrary_amd.image import Corrector, align_window
+    from tmlibrary_amd.synth import synth_sites_host
+    H, W = shape
+    base = synth_sites_host(5, H, W, seed=41)
+    st = orc.run_illumstats(base)
+    sm, ss = orc.smooth_reflect(st.mean), orc.smooth_reflect(st.std)
+    sites = np.stack(synth_sites_host(6, H, W, seed=42))
+    sites[0, 3, :9] = 0
+    shifts = [(0, 0), (3, -5), (-4, 7), (1, 1), (-2, -3), (0, 6)]
+    res = (4, 4, 7, 7)
+    wins = np.stack([align_window((H, W), y, x, *res, crop=False)[0] for y, x in shifts])
+    wins[5]["rows"] = 0  # all padding
+    lo, hi = 100, 3000
+    corr = Corrector(sm, ss)
+    d_in = C.c_void_p()
+    d_out = C.c_void_p()
+    assert L.tmh_malloc_device(C.byref(d_in), sites.nbytes) == 0
+    assert L.tmh_malloc_device(C.byref(d_out), sites.size) == 0
+    assert L.tmh_memcpy(d_in, sites.ctypes.data, sites.nbytes, 0, None) == 0
+    hip.check(L.tmh_correct_chain_u8_device(corr._h, d_in, d_out, len(sites), hip.ptr(wins), lo,
+                                            hi, None))
+    got = np.empty(sites.shape, np.uint8)
+    assert L.tmh_memcpy(got.ctypes.data, d_out, got.nbytes, 1, None) == 0
+    L.tmh_free_device(d_in)
+    L.tmh_free_device(d_out)
+    corr.close()
+    for i, ((y, x), s) in enumerate(zip(shifts, sites)):
+        if i == 5:
+            assert not got[i].any()
+            continue
+        want = orc.illuminati_chain(s, sm, ss, (y, x), res, lo, hi)
+        d = np.abs(got[i].astype(np.int32) - want.astype(np.int32))
+        assert d.max() <= 1, i
+
+
+def test_chain_rejects_bad_windows(L):
+    from tmlibrary_amd.image import Corrector, align_window
+    g, wins = _chain_inputs()
+    corr = Corrector(g["smooth_mean"], g["smooth_std"])
+    bad = wins.copy()
+    bad[0]["rows"] = 10 ** 6
+    with pytest.raises(ValueError):
+        corr.chain_u8(g["images"], bad, 10, 20)
+    with pytest.raises(ValueError):
+        corr.chain_u8(g["images"], wins, 20, 20)
+    corr.close()

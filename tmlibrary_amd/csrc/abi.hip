@@ -146,7 +146,8 @@ struct tmh_corrector {
   double zero_log10 = -10.0;
   hipStream_t stream = nullptr;
   DBuf<float4> coef, mconst2;
-  DBuf<float2> lut, mconst, coef2;
+  DBuf<float2> lut, mconst, coef2, coef_lin;
+  DBuf<tmh_window> win;  // per-site alignment windows of the chain pass
   DBuf<int> queues;
   int n_wg = 256;
   DBuf<double> sums, partial;
@@ -612,7 +613,7 @@ static void corrector_coeffs(tmh_corrector* c, const double* d_mean, const doubl
   launch_reduce_sum(d_mean, c->npx, c->partial.p, np, c->sums.p + 1, s);
   launch_coeffs(d_mean, d_std, c->sums.p, c->npx, c->coef.p, c->mconst.p, s);
   launch_coeffs2(d_mean, d_std, c->sums.p, c->npx, c->log_transform, c->zero_log10, c->coef2.p,
-                 c->mconst2.p, s);
+                 c->mconst2.p, c->coef_lin.p, s);
 }
 
 static void corrector_init(tmh_corrector* c, const double* d_mean, const double* d_std) {
@@ -620,6 +621,7 @@ static void corrector_init(tmh_corrector* c, const double* d_mean, const double*
   c->partial.alloc(512);
   c->coef.alloc(c->npx);
   c->coef2.alloc(c->npx);
+  c->coef_lin.alloc(c->npx);
   c->mconst.alloc(1);
   c->mconst2.alloc(1);
   c->queues.alloc(8, true);
@@ -814,6 +816,114 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       h->last_batch = nc;
       h->pending -= nc;
     }
+  });
+}
+
+// ---------------------------------------------------------------------------
+// illuminati chain: align / scale / fused correct->align->clip->scale
+// ---------------------------------------------------------------------------
+
+static void check_windows(const tmh_window* w, int64_t n, int H, int W, int oh, int ow) {
+  for (int64_t i = 0; i < n; ++i) {
+    const tmh_window& x = w[i];
+    TMH_CHECK(x.rows >= 0 && x.cols >= 0, TMH_EINVAL, "alignment window has negative extent");
+    if (x.rows == 0 || x.cols == 0) continue;
+    TMH_CHECK(x.src_r0 >= 0 && x.src_c0 >= 0 && x.src_r0 + x.rows <= H && x.src_c0 + x.cols <= W,
+              TMH_EINVAL, "alignment window leaves the source image");
+    TMH_CHECK(x.dst_r0 >= 0 && x.dst_c0 >= 0 && x.dst_r0 + x.rows <= oh && x.dst_c0 + x.cols <= ow,
+              TMH_EINVAL, "alignment window leaves the output image");
+  }
+}
+
+static void check_scale(int lo, int hi) {
+  TMH_CHECK(lo >= 0 && lo < 65536 && hi >= 0 && hi < 65536, TMH_EINVAL,
+            "scale bounds must be in the range [0, 65535]");
+  TMH_CHECK(lo < hi, TMH_EINVAL, "\"lower_bound\" must be smaller than \"upper_bound\"");
+}
+
+int tmh_align(const void* host_in, void* host_out, int elem_bytes, int64_t n_sites, int height,
+              int width, const tmh_window* windows, int out_height, int out_width) {
+  return guard([&] {
+    TMH_CHECK((elem_bytes == 1 || elem_bytes == 2) && n_sites >= 0 && height > 0 && width > 0 &&
+                  out_height >= 0 && out_width >= 0 && (windows || n_sites == 0) &&
+                  ((host_in && host_out) || n_sites == 0),
+              TMH_EINVAL, "bad arguments");
+    check_windows(windows, n_sites, height, width, out_height, out_width);
+    if (n_sites == 0) return;
+    const size_t in_b = (size_t)n_sites * height * width * elem_bytes;
+    const size_t out_b = (size_t)n_sites * out_height * out_width * elem_bytes;
+    DBuf<uint8_t> a, b;
+    DBuf<tmh_window> w;
+    a.alloc(in_b);
+    b.alloc(std::max<size_t>(out_b, 1));
+    w.alloc((size_t)n_sites);
+    TMH_HIP(hipMemcpy(a.p, host_in, in_b, hipMemcpyHostToDevice));
+    TMH_HIP(hipMemcpy(w.p, windows, (size_t)n_sites * sizeof(tmh_window), hipMemcpyHostToDevice));
+    launch_align(a.p, b.p, elem_bytes, n_sites, height, width, out_height, out_width, w.p, nullptr);
+    TMH_HIP(hipDeviceSynchronize());
+    if (out_b) TMH_HIP(hipMemcpy(host_out, b.p, out_b, hipMemcpyDeviceToHost));
+  });
+}
+
+int tmh_map_u16_to_u8(const uint16_t* host_in, uint8_t* host_out, int64_t n, int lower,
+                      int upper) {
+  return guard([&] {
+    TMH_CHECK(n >= 0 && ((host_in && host_out) || n == 0), TMH_EINVAL, "bad arguments");
+    check_scale(lower, upper);
+    if (n == 0) return;
+    DBuf<uint16_t> a;
+    DBuf<uint8_t> b;
+    a.alloc((size_t)n);
+    b.alloc((size_t)n);
+    TMH_HIP(hipMemcpy(a.p, host_in, (size_t)n * 2, hipMemcpyHostToDevice));
+    launch_map_u8(a.p, b.p, n, lower, upper, nullptr);
+    TMH_HIP(hipDeviceSynchronize());
+    TMH_HIP(hipMemcpy(host_out, b.p, (size_t)n, hipMemcpyDeviceToHost));
+  });
+}
+
+int tmh_correct_chain_u8_device(tmh_corrector* c, const uint16_t* dev_in, uint8_t* dev_out,
+                                int64_t n_sites, const tmh_window* host_windows, int clip_lo,
+                                int clip_hi, void* stream) {
+  return guard([&] {
+    TMH_CHECK(c && n_sites >= 0 && ((dev_in && dev_out && host_windows) || n_sites == 0),
+              TMH_EINVAL, "bad arguments");
+    check_scale(clip_lo, clip_hi);
+    check_windows(host_windows, n_sites, c->H, c->W, c->H, c->W);
+    TMH_CHECK(!c->log_transform || (c->zero_log10 >= -37.0 && c->zero_log10 <= 0.0), TMH_EINVAL,
+              "the chain pass needs zero_log10 in [-37, 0]");
+    if (n_sites == 0) return;
+    hipStream_t s = pick(c->stream, stream);
+    if ((size_t)n_sites > c->win.n) {
+      TMH_HIP(hipStreamSynchronize(s));
+      c->win.alloc((size_t)n_sites);
+    }
+    TMH_HIP(hipMemcpyAsync(c->win.p, host_windows, (size_t)n_sites * sizeof(tmh_window),
+                           hipMemcpyHostToDevice, s));
+    launch_chain_u8(dev_in, dev_out, c->H, c->W, n_sites, c->coef_lin.p, c->mconst2.p,
+                    c->log_transform, c->win.p, clip_lo, clip_hi, s);
+    TMH_HIP(hipStreamSynchronize(s));  // the window buffer is reused by the next call
+  });
+}
+
+int tmh_correct_chain_u8(tmh_corrector* c, const uint16_t* host_in, uint8_t* host_out,
+                         int64_t n_sites, const tmh_window* host_windows, int clip_lo,
+                         int clip_hi) {
+  return guard([&] {
+    TMH_CHECK(c && n_sites >= 0 && ((host_in && host_out && host_windows) || n_sites == 0),
+              TMH_EINVAL, "bad arguments");
+    if (n_sites == 0) return;
+    const size_t npx = (size_t)c->npx;
+    DBuf<uint16_t> a;
+    DBuf<uint8_t> b;
+    a.alloc((size_t)n_sites * npx);
+    b.alloc((size_t)n_sites * npx);
+    TMH_HIP(hipMemcpyAsync(a.p, host_in, (size_t)n_sites * npx * 2, hipMemcpyHostToDevice,
+                           c->stream));
+    int rc = tmh_correct_chain_u8_device(c, a.p, b.p, n_sites, host_windows, clip_lo, clip_hi,
+                                         nullptr);
+    if (rc) throw Error{rc, g_last_error};
+    TMH_HIP(hipMemcpy(host_out, b.p, (size_t)n_sites * npx, hipMemcpyDeviceToHost));
   });
 }
 

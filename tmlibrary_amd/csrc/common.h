@@ -106,7 +106,14 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
                          hipStream_t s);
 void launch_coeffs2(const double* mean, const double* std, const double* sums, int64_t npx,
                     int log_transform, double zero_log10, float2* coef2, float4* mconst2,
-                    hipStream_t s);
+                    float2* coef_lin, hipStream_t s);
+// illuminati chain (chain_kernels.hip)
+void launch_align(const void* in, void* out, int elem_bytes, int64_t n_sites, int H, int W, int oh,
+                  int ow, const tmh_window* d_win, hipStream_t s);
+void launch_map_u8(const uint16_t* in, uint8_t* out, int64_t n, int lo, int hi, hipStream_t s);
+void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_sites,
+                     const float2* coef_lin, const float4* mconst2, int log_transform,
+                     const tmh_window* d_win, int lo, int hi, hipStream_t s);
 void launch_clip_u16(const uint16_t* in, uint16_t* out, int64_t n, int lo, int hi, hipStream_t s);
 void launch_synth(uint16_t* out, int64_t n_sites, int H, int W, uint64_t seed, int channel,
                   int64_t first_site, hipStream_t s);

@@ -361,11 +361,12 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
 // float4 (mu_2p, mu_2p+1, a_2p, a_2p+1) at index g, so one 16-B load gives a
 // pixel pair its operands for the packed f32 ops.  mconst2 = (M' hi, M' lo,
 // 10**zero_log10 (the value a zero pixel takes before the log), 0) with
-// M' = mean(mean) [*log2(10)].
+// M' = mean(mean) [*log2(10)].  coef_lin (optional) holds the same pairs in
+// pixel order for the chain pass's shifted gathers.
 __global__ void k_coeffs2(const double* __restrict__ mean, const double* __restrict__ std,
                           const double* __restrict__ sums, int64_t npx, int log_transform,
                           double zero_log10, float* __restrict__ coef2,
-                          float4* __restrict__ mconst2) {
+                          float4* __restrict__ mconst2, float2* __restrict__ coef_lin) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const double K = log_transform ? kLog2_10 : 1.0;
   if (i == 0) {
@@ -382,15 +383,18 @@ __global__ void k_coeffs2(const double* __restrict__ mean, const double* __restr
     om = base;
     oa = base + 2;
   }
-  coef2[om] = (float)(mean[i] * K);
-  coef2[oa] = (float)(S / std[i]);
+  const float mu = (float)(mean[i] * K), a = (float)(S / std[i]);
+  coef2[om] = mu;
+  coef2[oa] = a;
+  if (coef_lin) coef_lin[i] = make_float2(mu, a);  // pixel order (shifted gathers)
 }
 
 void launch_coeffs2(const double* mean, const double* std, const double* sums, int64_t npx,
                     int log_transform, double zero_log10, float2* coef2, float4* mconst2,
-                    hipStream_t s) {
+                    float2* coef_lin, hipStream_t s) {
   hipLaunchKernelGGL(k_coeffs2, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, mean, std, sums,
-                     npx, log_transform, zero_log10, reinterpret_cast<float*>(coef2), mconst2);
+                     npx, log_transform, zero_log10, reinterpret_cast<float*>(coef2), mconst2,
+                     coef_lin);
   TMH_HIP(hipGetLastError());
 }
 

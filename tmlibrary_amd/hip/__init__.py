@@ -66,6 +66,10 @@ SIGNATURES = {
     "tmh_correct_u16_hist_device": (_I, [_P, _P, _P, _P, _I64, _I, _I, _P]),
     "tmh_correct_u8": (_I, [_P, _P, _P, _I64, _I, _I]),
     "tmh_clip_u16": (_I, [_P, _P, _I64, _I, _I]),
+    "tmh_align": (_I, [_P, _P, _I, _I64, _I, _I, _P, _I, _I]),
+    "tmh_map_u16_to_u8": (_I, [_P, _P, _I64, _I, _I]),
+    "tmh_correct_chain_u8_device": (_I, [_P, _P, _P, _I64, _P, _I, _I, _P]),
+    "tmh_correct_chain_u8": (_I, [_P, _P, _P, _I64, _P, _I, _I]),
     "tmh_synth_sites_device": (_I, [_P, _I64, _I, _I, C.c_uint64, _I, _I64, _P]),
     "tmh_malloc_device": (_I, [C.POINTER(_P), C.c_size_t]),
     "tmh_free_device": (_I, [_P]),
@@ -74,6 +78,11 @@ SIGNATURES = {
     "tmh_profile_read": (_I, [C.c_char_p, C.POINTER(_D), C.POINTER(_I64)]),
     "tmh_profile_reset": (_I, []),
 }
+
+
+#: struct tmh_window (include/tmhip.h) as a numpy record: one alignment window per site
+WINDOW_DTYPE = np.dtype([("src_r0", np.int32), ("src_c0", np.int32), ("dst_r0", np.int32),
+                         ("dst_c0", np.int32), ("rows", np.int32), ("cols", np.int32)])
 
 
 class HipUnavailableError(RuntimeError):

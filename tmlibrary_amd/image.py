@@ -1,14 +1,21 @@
 """Image classes of the illumination-correction path, computed on MI355X.
 
 Mirrors the hot-path subset of tmlib/image.py:
-  ``Image``                (:35-311; array/metadata checks, ``smooth`` :287-311)
-  ``ChannelImage``         (:455-670; ``clip`` :570-597,
-                            ``_correct_illumination`` :599-631, ``correct`` :633-670)
+  ``Image``                (:35-454; array/metadata checks, ``smooth`` :287-311,
+                            ``_shift_and_crop`` / ``align`` :345-454)
+  ``ChannelImage``         (:455-670; ``_map_to_uint8`` / ``scale`` :493-568,
+                            ``clip`` :570-597, ``_correct_illumination`` :599-631,
+                            ``correct`` :633-670)
   ``IllumstatsImage``      (:1097-1136)
   ``IllumstatsContainer``  (:1139-1213; ``smooth`` :1172-1193,
                             ``get_closest_percentile`` :1195-1213)
 
-Smoothing, correction and clipping run in libtmhip.so (no CPU fallback).
+plus the illuminati post-correct chain (illuminati/api.py:396-405) as one
+fused pass, ``Corrector.chain_u8``.
+
+Smoothing, correction, clipping, alignment and scaling run in libtmhip.so
+(no CPU fallback); the host only evaluates numpy slice bounds and LUT
+parameters.
 """
 from __future__ import annotations
 
@@ -83,6 +90,23 @@ class Image(object):
     def is_uint16(self):
         return self.array.dtype == np.uint16
 
+    def align(self, crop=True, inplace=True):
+        """Image.align (tmlib/image.py:412-454): shift by the metadata's
+        (y_shift, x_shift) and crop, or zero-pad with crop=False (on the GPU)."""
+        if self.metadata is None:
+            raise AttributeError('Image requires attribute "metadata" for alignment.')
+        md = self.metadata
+        w, shape = align_window(self.array.shape, md.y_shift, md.x_shift, md.bottom_residue,
+                                md.top_residue, md.right_residue, md.left_residue, crop=crop)
+        array = align_array(self.array, w, shape)
+        if inplace:
+            self.metadata.is_aligned = True
+            self.array = array
+            return self
+        new_object = self.__class__(array, self.metadata)
+        new_object.metadata.is_aligned = True
+        return new_object
+
     def smooth(self, sigma, inplace=True):
         """Gaussian smoothing (image.py:287-311 -> mahotas.gaussian_filter),
         'reflect' border, radius int(4*sigma+0.5), float64, on the GPU."""
@@ -94,6 +118,51 @@ class Image(object):
         new_img = self.__class__(array, self.metadata)
         new_img.metadata.is_smoothed = True
         return new_img
+
+
+def align_window(shape, y, x, bottom, top, right, left, crop=True):
+    """The numpy slicing of tmlib/image.py:345-410 as a tmh_window: the source
+    slice ``[top-y : -(bottom+y) or H, left-x : -(right+x) or W]`` and, for
+    crop=False, its destination at (top, left).  Returns (window, out_shape);
+    raises like the reference when the pasted window does not fit."""
+    H, W = int(shape[0]), int(shape[1])
+    row_start, row_end = top - y, bottom + y
+    row_end = H if row_end == 0 else -row_end
+    col_start, col_end = left - x, right + x
+    col_end = W if col_end == 0 else -col_end
+    rs, re_, _ = slice(row_start, row_end).indices(H)
+    cs, ce, _ = slice(col_start, col_end).indices(W)
+    rows, cols = max(0, re_ - rs), max(0, ce - cs)
+    w = np.zeros((), dtype=hip.WINDOW_DTYPE)
+    w["src_r0"], w["src_c0"], w["rows"], w["cols"] = rs, cs, rows, cols
+    if crop:
+        return w, (rows, cols)
+    # aligned_im[top:top+rows, left:left+cols] = extracted (numpy assignment,
+    # negative starts included)
+    dr = range(H)[top:top + rows]
+    dc = range(W)[left:left + cols]
+    # numpy broadcasting: equal extents, or a 1-extent source into an empty slice
+    ok = all(n == len(t) or (n == 1 and len(t) == 0) for n, t in ((rows, dr), (cols, dc)))
+    if not ok:
+        raise Exception("Shifting and cropping of the image failed!\n"
+                        "Reason: could not broadcast input array from shape (%d,%d) into "
+                        "shape (%d,%d)" % (rows, cols, len(dr), len(dc)))
+    if len(dr) == 0 or len(dc) == 0:
+        w["rows"] = w["cols"] = 0  # nothing pasted
+        return w, (H, W)
+    w["dst_r0"], w["dst_c0"] = dr.start, dc.start
+    return w, (H, W)
+
+
+def align_array(array: np.ndarray, window, out_shape) -> np.ndarray:
+    a = np.ascontiguousarray(array)
+    if a.dtype not in (np.uint8, np.uint16):
+        raise TypeError("only uint8/uint16 images are aligned on the device")
+    out = np.empty(out_shape, dtype=a.dtype)
+    win = np.ascontiguousarray(np.asarray(window, dtype=hip.WINDOW_DTYPE).reshape(1))
+    hip.check(hip.lib().tmh_align(hip.ptr(a), hip.ptr(out), a.itemsize, 1, a.shape[0],
+                                  a.shape[1], hip.ptr(win), out_shape[0], out_shape[1]))
+    return out
 
 
 def smooth_f64(array: np.ndarray, sigma) -> np.ndarray:
@@ -108,6 +177,44 @@ def smooth_f64(array: np.ndarray, sigma) -> np.ndarray:
 
 class ChannelImage(Image):
     """Grayscale uint8/uint16 site image (tmlib/image.py:455-670)."""
+
+    @staticmethod
+    def _map_to_uint8(img, lower_bound=None, upper_bound=None):
+        """tmlib/image.py:493-531: uint16 -> uint8 through the reference's numpy
+        LUT (evaluated bit-exactly per pixel on the GPU).  Bounds default to the
+        image's min / max (the reference's intent; its py3 range check would
+        raise on None)."""
+        if img.dtype != np.uint16:
+            raise TypeError('"img" must have 16-bit unsigned integer type.')
+        if lower_bound is not None and not (0 <= lower_bound < 2 ** 16):
+            raise ValueError('"lower_bound" must be in the range [0, 65535]')
+        if upper_bound is not None and not (0 <= upper_bound < 2 ** 16):
+            raise ValueError('"upper_bound" must be in the range [0, 65535]')
+        if lower_bound is None:
+            lower_bound = np.min(img)
+        if upper_bound is None:
+            upper_bound = np.max(img)
+        if lower_bound >= upper_bound:
+            raise ValueError('"lower_bound" must be smaller than "upper_bound"')
+        a = np.ascontiguousarray(img)
+        out = np.empty(a.shape, dtype=np.uint8)
+        hip.check(hip.lib().tmh_map_u16_to_u8(hip.ptr(a), hip.ptr(out), a.size, int(lower_bound),
+                                               int(upper_bound)))
+        return out
+
+    def scale(self, lower, upper, inplace=True):
+        """tmlib/image.py:533-568: map [lower, upper] to [0, 255] (uint16 only;
+        uint8 images are returned unchanged)."""
+        if self.is_uint16:
+            array = self._map_to_uint8(self.array, lower, upper)
+            if inplace:
+                self.array = array
+                self.metadata.is_rescaled = True
+                return self
+            new_image = self.__class__(array, self.metadata)
+            new_image.metadata.is_rescaled = True
+            return new_image
+        return self
 
     def __init__(self, array, metadata=None):
         super(ChannelImage, self).__init__(array, metadata)
@@ -226,6 +333,26 @@ class Corrector(object):
             hip.check(L.tmh_correct_u8(self._h, hip.ptr(a), hip.ptr(out), n, lo, hi))
         else:
             raise TypeError("only uint8/uint16 images can be corrected")
+        return out
+
+    def chain_u8(self, sites: np.ndarray, windows, clip_lo: int, clip_hi: int) -> np.ndarray:
+        """illuminati/api.py:396-405 for a stack of uint16 sites [n,H,W] in one
+        pass: correct -> align(crop=False) with each site's window (see
+        ``align_window``) -> clip(clip_lo, clip_hi) -> scale -> uint8."""
+        a = np.ascontiguousarray(sites)
+        if a.dtype != np.uint16:
+            raise TypeError("the chain takes uint16 sites")
+        if a.ndim == 2:
+            a = a[None]
+        if a.shape[-2:] != self.shape:
+            raise ValueError("site shape %s does not match the statistics %s"
+                             % (a.shape[-2:], self.shape))
+        win = np.ascontiguousarray(np.asarray(windows, dtype=hip.WINDOW_DTYPE).reshape(-1))
+        if win.size != a.shape[0]:
+            raise ValueError("one alignment window per site is required")
+        out = np.empty(a.shape, dtype=np.uint8)
+        hip.check(hip.lib().tmh_correct_chain_u8(self._h, hip.ptr(a), hip.ptr(out), a.shape[0],
+                                                  hip.ptr(win), int(clip_lo), int(clip_hi)))
         return out
 
     def close(self):

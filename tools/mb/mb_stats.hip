@@ -569,7 +569,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&hist, S * kBins * 4));
     CK(hipMalloc(&queues, 64));
     CK(hipMemset(hist, 0, S * kBins * 4));
-    launch_coeffs2(mean, m2, sums, npx, 1, -10.0, coef2, mconst2, 0);
+    launch_coeffs2(mean, m2, sums, npx, 1, -10.0, coef2, mconst2, nullptr, 0);
     const int bpx = getenv("MB_BANDS") ? atoi(getenv("MB_BANDS")) : 2;
     auto run = [&](auto kern, int nt, const char* name) {
       for (int r = 0; r < reps; ++r) {
