@@ -53,6 +53,8 @@ def parse():
                         "separate: Welford || histogram pass, then correct (8 B/px)")
     p.add_argument("--serial-stats", action="store_true",
                    help="run the histogram pass after Welford instead of concurrently")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the extra (non-headline) measurements: the illuminati chain pass")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     return p.parse_args()
@@ -89,6 +91,43 @@ def cpu_baseline(n_sites, H, W, total_sites):
                   % (n_sites, H, W, n_sites, n_sites, total_sites,
                      1e3 * (t1 - t0) / n_sites, 1e3 * (t3 - t2) / n_sites),
     }
+
+
+def bench_chain(L, corr, S_ptr, S, H, W, dev, sp, reps=3):
+    """§8(f) rank 3, measured beside the headline: the illuminati chain
+    (correct -> align(crop=False) -> clip -> scale to uint8, illuminati/api.py:
+    396-405) over the same resident sites with per-site shifts; 3 B/px
+    algorithmic (uint16 in, uint8 out)."""
+    import torch
+
+    from tmlibrary_amd import hip
+    from tmlibrary_amd.image import align_window
+    wins = np.stack([align_window((H, W), s % 7 - 3, s % 9 - 4, 3, 3, 4, 4, crop=False)[0]
+                     for s in range(S)])
+    out8 = torch.empty((S, H, W), dtype=torch.uint8, device=dev)
+    O8 = C.c_void_p(out8.data_ptr())
+    lo, hi = 110, 4000
+    hip.check(L.tmh_correct_chain_u8_device(corr, S_ptr, O8, S, hip.ptr(wins), lo, hi, sp))
+    L.tmh_profile_enable(1)
+    L.tmh_profile_reset()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        hip.check(L.tmh_correct_chain_u8_device(corr, S_ptr, O8, S, hip.ptr(wins), lo, hi, sp))
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / reps
+    ms, k = C.c_double(), C.c_int64()
+    hip.check(L.tmh_profile_read(b"chain", C.byref(ms), C.byref(k)))
+    L.tmh_profile_enable(0)
+    kern_ms = ms.value / max(k.value, 1)
+    alg = S * H * W * 3
+    del out8
+    return {"workload": "illumination correct + align(crop=False, per-site shifts) + clip + "
+                        "scale to uint8, %d sites of %dx%d" % (S, H, W),
+            "value": round(S / el, 1), "unit": "sites/s", "kernel_avg_ms": round(kern_ms, 4),
+            "alg_bytes_per_launch": alg,
+            "achieved_GBs": round(alg / (kern_ms * 1e-3) / 1e9, 1),
+            "frac_of_8TBs": round(alg / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def main():
@@ -204,6 +243,10 @@ def main():
                 kern[name] = (ms.value / k.value, k.value)
         L.tmh_profile_enable(0)
 
+    extras = {}
+    if not a.no_extras and world == 1:
+        extras["chain_u8"] = bench_chain(L, corr, S_ptr, S, H, W, dev, sp)
+
     if rank == 0:
         site_bytes = npx * 2
         alg = {  # algorithmic HBM bytes per launch (per-site figure x sites)
@@ -267,6 +310,8 @@ def main():
             "roofline": roofline,
             "kernels": kdetail,
         }
+        if extras:
+            res["extras"] = extras
         if world == 1 and a.cpu_sample > 0:
             res["cpu_baseline"] = cpu_baseline(a.cpu_sample, H, W, S)
         else:

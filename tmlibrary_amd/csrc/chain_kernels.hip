@@ -53,104 +53,247 @@ __global__ void k_align(const T* __restrict__ in, T* __restrict__ out, int H, in
 }
 
 __global__ void k_map_u8(const uint16_t* __restrict__ in, uint8_t* __restrict__ out, int64_t n,
-                         int lo, int hi, double step) {
+                         int lo, int hi, double step) {  // no clip: the LUT's zeros / 255 tails
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) out[i] = (uint8_t)scale8(in[i], lo, hi, step);
 }
 
-// u16 words K..K+7 of the 16 packed in d[8]
-template <int K>
-__device__ __forceinline__ void words8(const uint32_t (&d)[8], uint32_t (&px)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int q = K + j;
-    px[j] = (q & 1) ? (d[q >> 1] >> 16) : (d[q >> 1] & 0xFFFFu);
-  }
+// Clip to [lo, hi] then the reference LUT, branch-free: T = n - 1 for
+// n = hi - lo > 1 (linspace's end point and v = hi give 255), T = 1 for n = 1.
+__device__ __forceinline__ uint32_t clip_scale8(uint32_t v16, int lo, int hi, int T, double step) {
+  const uint32_t v = min(max(v16, (uint32_t)lo), (uint32_t)hi);
+  const uint32_t i = v - (uint32_t)lo;
+  return i >= (uint32_t)T ? 255u : (uint32_t)((double)i * step);
 }
 
-// correct one pixel (log2 domain, as the fused correct pass; image.py:599-631)
-// -> x86 uint16 cast -> clip -> scale
 template <bool LOG>
-__device__ __forceinline__ uint32_t chain1(uint32_t px, float2 k, float mh, float zf, int lo,
-                                           int hi, double step) {
+__device__ __forceinline__ uint32_t correct16(uint32_t px, float mu, float a, float mh, float zf) {
   float L = (float)px;
   if (LOG) L = __builtin_amdgcn_logf(__builtin_fmaxf(L, zf));
-  const float t = fmaf(L - k.x, k.y, mh);
+  const float t = fmaf(L - mu, a, mh);
   float o = LOG ? __builtin_amdgcn_exp2f(t) : t;
   o = __builtin_fminf(o, 2147418112.0f);  // >= 2^31, inf, NaN -> low half 0 (x86 astype)
   if (!LOG) o = __builtin_fmaxf(o, -2147483648.0f);
-  uint32_t v = (uint32_t)(int32_t)o & 0xFFFFu;
-  v = v < (uint32_t)lo ? (uint32_t)lo : (v > (uint32_t)hi ? (uint32_t)hi : v);
-  return scale8(v, lo, hi, step);
+  return (uint32_t)(int32_t)o & 0xFFFFu;
 }
 
-// Fused chain, one thread = 8 consecutive output pixels of a row (W % 8 == 0),
-// walking the sites of the launch.  Per site the source of the 8 pixels is a
-// uniformly shifted run: two aligned 16-B buffer loads (out-of-range reads
-// return 0) cover it and a uniform funnel shift picks the 8 values; the
-// per-pixel (mean*log2(10), mean(std)/std) coefficients at the source
-// positions are 8-B loads from the linear plane (L2-resident neighbourhood).
-template <bool LOG>
+// Source-driven fused chain (W % 8 == 0): one thread = 8 consecutive SOURCE
+// pixels, their coefficients loaded once and reused for every site of its
+// part (blockIdx.y = site part).  align is a flat shift per site, off =
+// (dst_r0 - src_r0) * W + (dst_c0 - src_c0): source pixel p lands at p + off,
+// a bijection onto [off, npx + off), and source pixels outside the window land
+// outside the destination window (they write the padding value, 0 scaled).
+// The 8 result bytes of thread i go to [8i + off, 8i + off + 8); unless off
+// is a multiple of the 128-B line they are staged in LDS per workgroup and
+// stored as line-aligned 16-B chunks.  k_chain_fill pads [0, off) / [npx + off,
+// npx), the only destinations no source pixel reaches.
+// n < 8 bytes of v (low first) at the 8-aligned address p: dword, short, byte
+// pieces, each naturally aligned
+__device__ __forceinline__ void store_head(uint8_t* p, uint64_t v, int n) {
+  if (n & 4) {
+    *reinterpret_cast<uint32_t*>(p) = (uint32_t)v;
+    p += 4;
+    v >>= 32;
+  }
+  if (n & 2) {
+    *reinterpret_cast<uint16_t*>(p) = (uint16_t)v;
+    p += 2;
+    v >>= 16;
+  }
+  if (n & 1) *p = (uint8_t)v;
+}
+
+// the low n < 8 bytes of v ending just below the 8-aligned address end
+__device__ __forceinline__ void store_tail(uint8_t* end, uint64_t v, int n) {
+  uint8_t* p = end - n;
+  if (n & 1) {
+    *p = (uint8_t)v;
+    p += 1;
+    v >>= 8;
+  }
+  if (n & 2) {
+    *reinterpret_cast<uint16_t*>(p) = (uint16_t)v;
+    p += 2;
+    v >>= 16;
+  }
+  if (n & 4) *reinterpret_cast<uint32_t*>(p) = (uint32_t)v;
+}
+
+// blockIdx -> tile with XCD x (= blockIdx % 8, the dispatch round-robin)
+// owning tiles [x*q + min(x, r), ...) of n = 8q + r: a bijection on [0, n)
+__device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t n) {
+  const int64_t q = n / 8, r = n % 8, x = b % 8, k = b / 8;
+  return x * q + (x < r ? x : r) + k;
+}
+
+typedef float f32x2c_t __attribute__((ext_vector_type(2)));
+constexpr int kChainDepth = 4;
+
+template <bool LOG, bool LUT>
 __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ in,
                                                    uint8_t* __restrict__ out, int H, int W,
-                                                   int64_t n_sites,
+                                                   int64_t n_sites, int64_t per,
                                                    const float2* __restrict__ coef_lin,
                                                    const float4* __restrict__ mconst2,
                                                    const tmh_window* __restrict__ win, int lo,
-                                                   int hi, double step) {
+                                                   int hi, int T, double step) {
+  // LUT: the reference's uint8 table for the clipped range [lo, hi] staged in
+  // LDS (hi - lo + 1 bytes), one ds_read_u8 per pixel instead of three f64 ops
+  extern __shared__ uint8_t slut[];
+  if (LUT) {
+    for (int i = threadIdx.x; i <= hi - lo; i += 256)
+      slut[i] = (uint8_t)(i >= T ? 255u : (uint32_t)((double)i * step));
+    __syncthreads();
+  }
   const int64_t npx = (int64_t)H * W;
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (g >= (npx >> 3)) return;
-  const int r = (int)((g * 8) / W), c0 = (int)((g * 8) % W);
+  const int64_t ngroups = npx >> 3;
+  // XCD-aware tile order: workgroups go round-robin over the 8 XCDs, so give
+  // XCD x a contiguous run of tiles -- neighbouring tiles' shifted outputs
+  // share a 128-B line at their seam, and a seam inside one XCD's L2 merges
+  // instead of leaving two partial lines to write back.
+  const int64_t tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t g = tile * 256 + threadIdx.x;
+  const bool live = g < ngroups;
+  const int lane = threadIdx.x & 63;
+  const bool top_lane = threadIdx.x == 255 || g + 1 >= ngroups;  // no upper neighbour run
+  __shared__ uint64_t edge[256 / 64];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[2048 + 256];
+  const int64_t p0 = (live ? g : 0) * 8;
+  const int r = (int)(p0 / W), c0 = (int)(p0 % W);
   const float4 m = mconst2[0];
-  const uint32_t pad = scale8((uint32_t)lo, lo, hi, step);  // clip(0) = lo
-  for (int64_t s = 0; s < n_sites; ++s) {
+  const f32x2c_t M = {m.x, m.x};
+  f32x2c_t mu[4], a[4];
+  {
+    const float4* cf = reinterpret_cast<const float4*>(coef_lin + p0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 v0 = live ? cf[k] : make_float4(0.f, 1.f, 0.f, 1.f);
+      mu[k] = (f32x2c_t){v0.x, v0.z};
+      a[k] = (f32x2c_t){v0.y, v0.w};
+    }
+  }
+  const int64_t s0 = (int64_t)blockIdx.y * per;
+  const int64_t s1 = s0 + per < n_sites ? s0 + per : n_sites;
+  const uint4* src = reinterpret_cast<const uint4*>(in) + (live ? g : 0);
+  // kChainDepth sites' loads in flight ahead of the one being processed
+  uint4 q[kChainDepth];
+#pragma unroll
+  for (int k = 0; k < kChainDepth; ++k)
+    q[k] = live && s0 + k < s1 ? src[(s0 + k) * ngroups] : make_uint4(0, 0, 0, 0);
+  for (int64_t s = s0; s < s1; ++s) {
+    const uint4 cur = q[0];
+#pragma unroll
+    for (int k = 0; k + 1 < kChainDepth; ++k) q[k] = q[k + 1];
+    q[kChainDepth - 1] = live && s + kChainDepth < s1 ? src[(s + kChainDepth) * ngroups]
+                                                      : make_uint4(0, 0, 0, 0);
     const tmh_window w = win[s];  // uniform: scalar loads
-    uint32_t o[8];
-    const bool row_in = (unsigned)(r - w.dst_r0) < (unsigned)w.rows;
-    const int dc = w.src_c0 - w.dst_c0;
-    if (row_in && c0 - w.dst_c0 >= 0 && c0 + 7 - w.dst_c0 < w.cols) {
-      // whole run inside the window
-      const int sr = r - w.dst_r0 + w.src_r0;
-      const int64_t p = (int64_t)sr * W + c0 + dc;  // first source pixel
-      const int64_t a = p & ~(int64_t)7;
-      const int k = (int)(p - a);  // uniform per site
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(in + s * npx), 0, (int)(npx * 2), 0x00020000);
-      typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-      const u32x4_t v0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(a * 2), 0, 0);
-      const u32x4_t v1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(a * 2) + 16, 0, 0);
-      const uint32_t d[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      uint32_t px[8];
-      switch (k) {  // uniform: one scalar branch per site
-        case 0: words8<0>(d, px); break;
-        case 1: words8<1>(d, px); break;
-        case 2: words8<2>(d, px); break;
-        case 3: words8<3>(d, px); break;
-        case 4: words8<4>(d, px); break;
-        case 5: words8<5>(d, px); break;
-        case 6: words8<6>(d, px); break;
-        default: words8<7>(d, px); break;
-      }
-      const float2* cf = coef_lin + p;
+    const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+    f32x2c_t t[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = chain1<LOG>(px[j], cf[j], m.x, m.z, lo, hi, step);
-    } else {
+    for (int k = 0; k < 4; ++k) {
+      t[k].x = (float)(wd[k] & 0xFFFFu);
+      t[k].y = (float)(wd[k] >> 16);
+    }
+    if (LOG) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = c0 + j;
-        if (row_in && in_window(r, c, w)) {
-          const int64_t p = (int64_t)(r - w.dst_r0 + w.src_r0) * W + (c + dc);
-          o[j] = chain1<LOG>(in[s * npx + p], coef_lin[p], m.x, m.z, lo, hi, step);
-        } else {
-          o[j] = pad;
-        }
+      for (int k = 0; k < 4; ++k) {
+        t[k].x = __builtin_amdgcn_logf(__builtin_fmaxf(t[k].x, m.z));
+        t[k].y = __builtin_amdgcn_logf(__builtin_fmaxf(t[k].y, m.z));
       }
     }
-    uint2 packed = make_uint2(o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24),
-                              o[4] | (o[5] << 8) | (o[6] << 16) | (o[7] << 24));
-    reinterpret_cast<uint2*>(out + s * npx)[g] = packed;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] = __builtin_elementwise_fma(t[k] - mu[k], a[k], M);
+    uint32_t o[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float x = LOG ? __builtin_amdgcn_exp2f(t[k][h]) : t[k][h];
+        x = __builtin_fminf(x, 2147418112.0f);  // >= 2^31, inf, NaN -> low half 0 (x86)
+        if (!LOG) x = __builtin_fmaxf(x, -2147483648.0f);
+        const uint32_t v16 = (uint32_t)(int32_t)x & 0xFFFFu;
+        const uint32_t v = min(max(v16, (uint32_t)lo), (uint32_t)hi);  // np.clip
+        o[2 * k + h] = LUT ? (uint32_t)slut[v - (uint32_t)lo]
+                           : (v - (uint32_t)lo >= (uint32_t)T ? 255u
+                                                              : (uint32_t)((double)(v - lo) * step));
+      }
+    }
+    // pixels outside the source window write the padding value: 0 after
+    // clip/scale (clip(0) = lo, the table's first entry is 0)
+    const int cs = c0 - w.src_c0;
+    int jlo = -cs < 0 ? 0 : (-cs > 8 ? 8 : -cs);
+    int jhi = w.cols - cs < 0 ? 0 : (w.cols - cs > 8 ? 8 : w.cols - cs);
+    if ((unsigned)(r - w.src_r0) >= (unsigned)w.rows) jhi = 0;
+    const uint64_t keep = jhi > jlo ? ((~0ull >> (8 * (8 - (jhi - jlo)))) << (8 * jlo)) : 0ull;
+    const uint32_t lo4 = (o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24)) & (uint32_t)keep;
+    const uint32_t hi4 = (o[4] | (o[5] << 8) | (o[6] << 16) | (o[7] << 24)) & (uint32_t)(keep >> 32);
+    const uint64_t v8 = ((uint64_t)hi4 << 32) | lo4;
+    const int64_t off = (int64_t)(w.dst_r0 - w.src_r0) * W + (w.dst_c0 - w.src_c0);
+    const int64_t D = p0 + off;  // destination of byte 0
+    const int rr = (int)(off & 7);  // uniform
+    uint8_t* o8 = out + s * npx;
+    if ((off & 127) == 0) {  // line-aligned destination: direct stores
+      if (live && D >= 0 && D < npx) *reinterpret_cast<uint64_t*>(o8 + D) = v8;
+      continue;
+    }
+    // Otherwise the workgroup's 2,048 output bytes [o0, o0 + 2048) are staged
+    // in LDS and leave as whole 16-B chunks of 128-B lines: a shifted run
+    // written lane by lane would split every wave's store across one more,
+    // partial line on each side.  Runs are first made 8-byte aligned with the
+    // upper neighbour's bytes (wave shuffle, LDS slot across waves).
+    const int wv = threadIdx.x >> 6;
+    if (lane == 0) edge[wv] = v8;
+    const uint32_t nlo = (uint32_t)__shfl_down((int)lo4, 1, 64);
+    const uint32_t nhi = (uint32_t)__shfl_down((int)hi4, 1, 64);
+    __syncthreads();  // (1) edge slots written; the previous site's stage is drained
+    uint64_t n8 = ((uint64_t)nhi << 32) | nlo;
+    if (lane == 63 && wv < 256 / 64 - 1) n8 = edge[wv + 1];
+    const int64_t o0 = tile * 2048 + off;  // destination of thread 0's byte 0
+    const int64_t L0 = o0 >= 0 ? (o0 & ~(int64_t)127) : -((-o0 + 127) & ~(int64_t)127);
+    if (!live) {
+      // no run (past the last group): nothing to stage
+    } else if (rr == 0) {
+      *reinterpret_cast<uint64_t*>(stage + (D - L0)) = v8;
+    } else {
+      const int64_t A = D - rr + 8;  // aligned word holding our bytes [8 - rr, 8)
+      if (!top_lane) {
+        *reinterpret_cast<uint64_t*>(stage + (A - L0)) = (v8 >> (8 * (8 - rr))) | (n8 << (8 * rr));
+      } else {
+        for (int b = 8 - rr; b < 8; ++b) stage[D + b - L0] = (uint8_t)(v8 >> (8 * b));
+      }
+      if (threadIdx.x == 0)
+        for (int b = 0; b < 8 - rr; ++b) stage[D + b - L0] = (uint8_t)(v8 >> (8 * b));
+    }
+    __syncthreads();  // (2) stage complete
+    // valid destination bytes of this workgroup: [o0, o0 + 2048) within the
+    // site (the last workgroup may own fewer groups)
+    const int64_t wg_bytes = (ngroups - tile * 256 < 256 ? ngroups - tile * 256 : 256) * 8;
+    const int64_t v0 = o0 > 0 ? o0 : 0;
+    const int64_t v1 = o0 + wg_bytes < npx ? o0 + wg_bytes : npx;
+    const int64_t c = L0 + 16 * (int64_t)threadIdx.x;  // this thread's 16-B chunk
+    if (c + 16 <= v1 && c >= v0) {
+      *reinterpret_cast<uint4*>(o8 + c) = *reinterpret_cast<const uint4*>(stage + (c - L0));
+    } else if (c < v1 && c + 16 > v0) {
+      for (int b = 0; b < 16; ++b)
+        if (c + b >= v0 && c + b < v1) o8[c + b] = stage[c + b - L0];
+    }
   }
+}
+
+// The destinations no source pixel reaches: [0, off) for off > 0, [npx + off,
+// npx) for off < 0 (all outside the destination window).
+__global__ void k_chain_fill(uint8_t* __restrict__ out, int H, int W,
+                             const tmh_window* __restrict__ win, int lo, int hi, int T,
+                             double step) {
+  const int64_t npx = (int64_t)H * W;
+  const int64_t s = blockIdx.y;
+  const tmh_window w = win[s];
+  const int64_t off = (int64_t)(w.dst_r0 - w.src_r0) * W + (w.dst_c0 - w.src_c0);
+  const int64_t b0 = off > 0 ? 0 : npx + off, b1 = off > 0 ? off : npx;
+  const uint8_t pad = (uint8_t)clip_scale8(0u, lo, hi, T, step);
+  for (int64_t i = b0 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < b1;
+       i += (int64_t)gridDim.x * 256)
+    out[s * npx + i] = pad;
 }
 
 // Any width: one thread per output pixel.
@@ -161,7 +304,7 @@ __global__ __launch_bounds__(256) void k_chain_u8_scalar(const uint16_t* __restr
                                                           const float2* __restrict__ coef_lin,
                                                           const float4* __restrict__ mconst2,
                                                           const tmh_window* __restrict__ win,
-                                                          int lo, int hi, double step) {
+                                                          int lo, int hi, int T, double step) {
   const int64_t npx = (int64_t)H * W;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= npx) return;
@@ -169,10 +312,11 @@ __global__ __launch_bounds__(256) void k_chain_u8_scalar(const uint16_t* __restr
   const float4 m = mconst2[0];
   for (int64_t s = 0; s < n_sites; ++s) {
     const tmh_window w = win[s];
-    uint32_t v = scale8((uint32_t)lo, lo, hi, step);
+    uint32_t v = clip_scale8(0u, lo, hi, T, step);
     if (in_window(r, c, w)) {
       const int64_t p = (int64_t)(r - w.dst_r0 + w.src_r0) * W + (c - w.dst_c0 + w.src_c0);
-      v = chain1<LOG>(in[s * npx + p], coef_lin[p], m.x, m.z, lo, hi, step);
+      const float2 k = coef_lin[p];
+      v = clip_scale8(correct16<LOG>(in[s * npx + p], k.x, k.y, m.x, m.z), lo, hi, T, step);
     }
     out[s * npx + i] = (uint8_t)v;
   }
@@ -207,24 +351,36 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
   ProfScope prof("chain", s);
   const int64_t npx = (int64_t)H * W;
   const double step = scale_step(lo, hi);
+  const int T = hi - lo > 1 ? hi - lo - 1 : 1;
   const bool vec = (W & 7) == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
-                   (reinterpret_cast<uintptr_t>(out) & 7) == 0 && npx * 2 < (int64_t)1 << 31;
+                   (reinterpret_cast<uintptr_t>(out) & 7) == 0;
   if (vec) {
-    const dim3 grid((unsigned)cdiv(npx >> 3, 256));
-    if (log_transform)
-      hipLaunchKernelGGL(k_chain_u8<true>, grid, dim3(256), 0, s, in, out, H, W, n_sites, coef_lin,
-                         mconst2, d_win, lo, hi, step);
-    else
-      hipLaunchKernelGGL(k_chain_u8<false>, grid, dim3(256), 0, s, in, out, H, W, n_sites,
-                         coef_lin, mconst2, d_win, lo, hi, step);
+    // site parts even out the dispatch rounds (each thread streams its part)
+    const int64_t parts = n_sites >= 64 ? 8 : 1;
+    const int64_t per = cdiv(n_sites, parts);
+    const dim3 grid((unsigned)cdiv(npx >> 3, 256), (unsigned)cdiv(n_sites, per));
+    const int lut_bytes = hi - lo + 1;
+    const bool lut = lut_bytes <= 16384;  // else three f64 ops per pixel
+    const size_t shm = lut ? (size_t)((lut_bytes + 15) & ~15) : 0;
+#define TMH_CHAIN(L_, U_)                                                                     \
+  hipLaunchKernelGGL((k_chain_u8<L_, U_>), grid, dim3(256), shm, s, in, out, H, W, n_sites, per, \
+                     coef_lin, mconst2, d_win, lo, hi, T, step)
+    if (log_transform) {
+      if (lut) TMH_CHAIN(true, true); else TMH_CHAIN(true, false);
+    } else {
+      if (lut) TMH_CHAIN(false, true); else TMH_CHAIN(false, false);
+    }
+#undef TMH_CHAIN
+    hipLaunchKernelGGL(k_chain_fill, dim3(64, (unsigned)n_sites), dim3(256), 0, s, out, H, W,
+                       d_win, lo, hi, T, step);
   } else {
     const dim3 grid((unsigned)cdiv(npx, 256));
     if (log_transform)
       hipLaunchKernelGGL(k_chain_u8_scalar<true>, grid, dim3(256), 0, s, in, out, H, W, n_sites,
-                         coef_lin, mconst2, d_win, lo, hi, step);
+                         coef_lin, mconst2, d_win, lo, hi, T, step);
     else
       hipLaunchKernelGGL(k_chain_u8_scalar<false>, grid, dim3(256), 0, s, in, out, H, W, n_sites,
-                         coef_lin, mconst2, d_win, lo, hi, step);
+                         coef_lin, mconst2, d_win, lo, hi, T, step);
   }
   TMH_HIP(hipGetLastError());
 }

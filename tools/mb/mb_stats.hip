@@ -556,6 +556,43 @@ int main(int argc, char** argv) {
     launch_correct_u16(sites, out, npx, S, coef, clut, mconst, 1, -1, -1, 0);
     report("correct (prod)", t.stop(), 2 * S * site_gb);
   }
+  // illuminati chain (correct -> align -> clip -> scale u8), 3 B/px
+  if (!getenv("MB_NO_CHAIN")) {
+    float2* clin;
+    float4* mc2;
+    float2* c2;
+    uint8_t* o8;
+    tmh_window* dw;
+    CK(hipMalloc(&clin, npx * 8));
+    CK(hipMalloc(&c2, npx * 8));
+    CK(hipMalloc(&mc2, 16));
+    CK(hipMalloc(&o8, S * npx));
+    CK(hipMalloc(&dw, S * sizeof(tmh_window)));
+    launch_coeffs2(mean, m2, sums, npx, 1, -10.0, c2, mc2, clin, 0);
+    auto run_chain = [&](int shift_mode, int lo, int hi, const char* name) {
+      std::vector<tmh_window> w(S);
+      for (int64_t i = 0; i < S; ++i) {
+        int dy = shift_mode ? (int)(i % 7) - 3 : 0, dx = shift_mode ? (int)(i % 9) - 4 : 0;
+        if (shift_mode == 2) dx = 0;             // row shifts only: aligned destinations
+        if (shift_mode == 3) dy = 0;             // column shifts only
+        // residues 3,3,4,4 (bottom, top, right, left) as align_window computes them
+        w[i].src_r0 = 3 - dy; w[i].src_c0 = 4 - dx; w[i].dst_r0 = 3; w[i].dst_c0 = 4;
+        w[i].rows = H - 6; w[i].cols = W - 8;
+      }
+      CK(hipMemcpy(dw, w.data(), S * sizeof(tmh_window), hipMemcpyHostToDevice));
+      for (int r = 0; r < reps; ++r) {
+        t.start();
+        launch_chain_u8(sites, o8, H, W, S, clin, mc2, 1, dw, lo, hi, 0);
+        report(name, t.stop(), 1.5 * S * site_gb);
+      }
+    };
+    run_chain(1, 110, 4000, "chain: shifts, LUT");
+    run_chain(0, 110, 4000, "chain: no shift, LUT");
+    run_chain(1, 110, 40000, "chain: shifts, f64 scale");
+    run_chain(2, 110, 4000, "chain: row shifts only");
+    run_chain(3, 110, 4000, "chain: col shifts only");
+    CK(hipFree(clin)); CK(hipFree(c2)); CK(hipFree(mc2)); CK(hipFree(o8)); CK(hipFree(dw));
+  }
   // fused correct+hist ablations (persistent, 1 WG per CU)
   {
     int n_cu = 0;
