@@ -34,6 +34,8 @@ SHORT = {
     "k_correct_hist": "correct_hist",
     "k_correct_u16_vec8": "correct",
     "k_pct_acc": "pct_acc",
+    "k_wf_merge_parts": "welford_merge",
+    "k_chain_u8": "chain",
 }
 
 
@@ -76,7 +78,8 @@ def main():
     site_bytes = 2 * npx
     alg = {"welford": a.sites * site_bytes + 32 * npx, "hist": a.sites * site_bytes,
            "correct": 2 * a.sites * site_bytes + 16 * npx,
-           "correct_hist": 2 * a.sites * site_bytes + 8 * npx}
+           "correct_hist": 2 * a.sites * site_bytes + 8 * npx,
+           "chain": 3 * a.sites * npx}
     res = {"config": {"sites": a.sites, "height": a.height, "width": a.width},
            "method": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch (separate --pmc passes; "
                      "gfx950 FETCH_SIZE halving corrected); median over launches",
