@@ -145,7 +145,10 @@ def main():
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    # TMH_BENCH_FORCE_DIST=1 runs the multi-GPU code path (RCCL merge,
+    # deferred percentiles, pipelined chain) even with one rank
+    dist_on = world > 1 or os.environ.get("TMH_BENCH_FORCE_DIST") == "1"
+    if dist_on:
         dist.init_process_group("nccl", device_id=dev)
     L = hip.lib()
     hip.check(L.tmh_set_device(local_rank))
@@ -170,7 +173,7 @@ def main():
 
     lo, hi, gamma = quantile_table(npx, np.linspace(0, 100, Q))
     lut = stats_log10_lut()
-    flags = hip.TMH_STATS_DEFERRED_PCT if world > 1 else 0
+    flags = hip.TMH_STATS_DEFERRED_PCT if dist_on else 0
     if a.serial_stats:
         flags |= hip.TMH_STATS_SERIAL
     h = C.c_void_p()
@@ -192,7 +195,7 @@ def main():
             hip.check(L.tmh_stats_update_welford_device(h, S_ptr, S, 1, sp))
         else:
             hip.check(L.tmh_stats_update_device(h, S_ptr, S, 1, sp))
-        if world > 1:
+        if dist_on:
             merge_welford(ops, dist)
         hip.check(L.tmh_stats_finalize_device(h, C.c_void_p(mean.data_ptr()),
                                               C.c_void_p(std.data_ptr()), sp))
@@ -206,7 +209,7 @@ def main():
             hip.check(L.tmh_correct_u16_hist_device(corr, h, S_ptr, O_ptr, S, -1, -1, sp))
         else:
             hip.check(L.tmh_correct_u16_device(corr, S_ptr, O_ptr, S, -1, -1, sp))
-        if world > 1:
+        if dist_on:
             merge_percentiles(ops, dist)
 
     for _ in range(a.warmup):
@@ -217,17 +220,17 @@ def main():
     if prof:
         L.tmh_profile_enable(1)
         L.tmh_profile_reset()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -242,6 +245,17 @@ def main():
             if k.value:
                 kern[name] = (ms.value / k.value, k.value)
         L.tmh_profile_enable(0)
+
+    # result fingerprint of the last step (identical on every rank and for
+    # any N: merged mean/std and the bit-exact percentile sums)
+    nn = C.c_int64()
+    m_h = np.empty(npx)
+    s_h = np.empty(npx)
+    acc_h = np.empty(Q)
+    hip.check(L.tmh_stats_finalize(h, C.byref(nn), hip.ptr(m_h), hip.ptr(s_h), hip.ptr(acc_h), None))
+    import hashlib
+    check = {"n": int(nn.value), "mean_sum": float(m_h.sum()), "std_sum": float(s_h.sum()),
+             "pct_sums_sha256": hashlib.sha256(acc_h.tobytes()).hexdigest()[:16]}
 
     extras = {}
     if not a.no_extras and world == 1:
@@ -310,6 +324,7 @@ def main():
             "roofline": roofline,
             "kernels": kdetail,
         }
+        res["check"] = check
         if extras:
             res["extras"] = extras
         if world == 1 and a.cpu_sample > 0:
@@ -320,7 +335,7 @@ def main():
 
     L.tmh_corrector_destroy(corr)
     L.tmh_stats_destroy(h)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

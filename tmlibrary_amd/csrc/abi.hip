@@ -134,7 +134,8 @@ struct tmh_stats {
   DBuf<unsigned long long> pooled, pooled_parts;  // parts: kPooledParts zero-maintained copies
   DBuf<uint32_t> hist_hi, site_hist, hist_full;
   QPos qp{};
-  DBuf<uint16_t> vlo, vhi, stage;
+  DBuf<uint16_t> stage;
+  DBuf<uint32_t> vlh;  // per site Q x (previous | next << 16) order statistics
   DBuf<int64_t> zeros;
 };
 
@@ -190,7 +191,7 @@ static void stats_reserve_sites(tmh_stats* h, int64_t n_sites) {
   // growing frees buffers earlier launches may still be using
   const bool grow = (size_t)n_sites * kHiBins > h->hist_hi.n || (size_t)n_sites > h->zeros.n ||
                     ((h->flags & 2u) && (size_t)n_sites * kBins > h->site_hist.n) ||
-                    (!(h->flags & TMH_STATS_DEFERRED_PCT) && (size_t)n_sites * h->Q > h->vlo.n);
+                    (!(h->flags & TMH_STATS_DEFERRED_PCT) && (size_t)n_sites * h->Q > h->vlh.n);
   if (grow) {
     TMH_HIP(hipStreamSynchronize(h->stream));
     TMH_HIP(hipStreamSynchronize(h->side));
@@ -201,26 +202,23 @@ static void stats_reserve_sites(tmh_stats* h, int64_t n_sites) {
   h->zeros.ensure((size_t)n_sites);
   if (h->flags & 2u) h->site_hist.ensure((size_t)n_sites * kBins);
   if (!(h->flags & TMH_STATS_DEFERRED_PCT)) {
-    h->vlo.ensure((size_t)n_sites * h->Q);
-    h->vhi.ensure((size_t)n_sites * h->Q);
+    h->vlh.ensure((size_t)n_sites * h->Q);
   }
 }
 
 static void stats_grow_deferred(tmh_stats* h, int64_t extra) {
   const size_t need = (size_t)(h->n_deferred + extra) * h->Q;
-  if (need <= h->vlo.n) return;
-  size_t cap = std::max(need, h->vlo.n * 2);
-  for (auto* b : {&h->vlo, &h->vhi}) {
-    DBuf<uint16_t> nb;
-    nb.alloc(cap);
-    if (h->n_deferred)
-      TMH_HIP(hipMemcpyAsync(nb.p, b->p, (size_t)h->n_deferred * h->Q * sizeof(uint16_t),
-                             hipMemcpyDeviceToDevice, h->stream));
-    TMH_HIP(hipStreamSynchronize(h->stream));
-    TMH_HIP(hipStreamSynchronize(h->side));
-    std::swap(b->p, nb.p);
-    std::swap(b->n, nb.n);
-  }
+  if (need <= h->vlh.n) return;
+  const size_t cap = std::max(need, h->vlh.n * 2);
+  DBuf<uint32_t> nb;
+  nb.alloc(cap);
+  if (h->n_deferred)
+    TMH_HIP(hipMemcpyAsync(nb.p, h->vlh.p, (size_t)h->n_deferred * h->Q * sizeof(uint32_t),
+                           hipMemcpyDeviceToDevice, h->stream));
+  TMH_HIP(hipStreamSynchronize(h->stream));
+  TMH_HIP(hipStreamSynchronize(h->side));
+  std::swap(h->vlh.p, nb.p);
+  std::swap(h->vlh.n, nb.n);
 }
 
 int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo,
@@ -345,20 +343,14 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
   // order statistics, in chunks so the per-site slabs stay bounded
   for (int64_t c0 = 0; c0 < ns; c0 += chunk) {
     const int64_t nc = std::min(chunk, ns - c0);
-    uint16_t *vlo, *vhi;
-    if (h->flags & TMH_STATS_DEFERRED_PCT) {
-      vlo = h->vlo.p + (size_t)h->n_deferred * h->Q;
-      vhi = h->vhi.p + (size_t)h->n_deferred * h->Q;
-    } else {
-      vlo = h->vlo.p;
-      vhi = h->vhi.p;
-    }
-    launch_hist_scatter(d + c0 * h->npx, h->npx, nc, h->hist_hi.p, h->qp, vlo, vhi, h->pooled.p,
+    uint32_t* vlh = h->vlh.p;
+    if (h->flags & TMH_STATS_DEFERRED_PCT) vlh += (size_t)h->n_deferred * h->Q;
+    launch_hist_scatter(d + c0 * h->npx, h->npx, nc, h->hist_hi.p, h->qp, vlh, h->pooled.p,
                         h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr, hs);
     if (h->flags & TMH_STATS_DEFERRED_PCT)
       h->n_deferred += nc;
     else
-      launch_pct_accumulate(vlo, vhi, nc, h->Q, h->gamma.p, h->acc.p, hs);
+      launch_pct_accumulate(vlh, nc, h->Q, h->gamma.p, h->acc.p, hs);
     h->last_batch = nc;
   }
   if (!serial) {
@@ -416,7 +408,7 @@ int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites, 
 static void stats_pct_sum_device(tmh_stats* h) {
   if ((h->flags & TMH_STATS_DEFERRED_PCT) && !h->pct_sum_external) {
     TMH_HIP(hipMemsetAsync(h->acc.p, 0, (size_t)h->Q * 8, h->stream));
-    launch_pct_accumulate(h->vlo.p, h->vhi.p, h->n_deferred, h->Q, h->gamma.p, h->acc.p, h->stream);
+    launch_pct_accumulate(h->vlh.p, h->n_deferred, h->Q, h->gamma.p, h->acc.p, h->stream);
   }
 }
 
@@ -468,8 +460,14 @@ int tmh_stats_site_order_stats(tmh_stats* h, int64_t site, uint16_t* host_vlo, u
     const int64_t avail = deferred ? h->n_deferred : h->last_batch;
     TMH_CHECK(site >= 0 && site < avail, TMH_EINVAL, "site not available");
     const size_t off = (size_t)site * h->Q;
-    TMH_HIP(hipMemcpyAsync(host_vlo, h->vlo.p + off, (size_t)h->Q * 2, hipMemcpyDeviceToHost, h->stream));
-    TMH_HIP(hipMemcpyAsync(host_vhi, h->vhi.p + off, (size_t)h->Q * 2, hipMemcpyDeviceToHost, h->stream));
+    std::vector<uint32_t> w((size_t)h->Q);
+    TMH_HIP(hipMemcpyAsync(w.data(), h->vlh.p + off, (size_t)h->Q * 4, hipMemcpyDeviceToHost,
+                           h->stream));
+    TMH_HIP(hipStreamSynchronize(h->stream));
+    for (int64_t q = 0; q < h->Q; ++q) {
+      host_vlo[q] = (uint16_t)(w[q] & 0xFFFFu);
+      host_vhi[q] = (uint16_t)(w[q] >> 16);
+    }
     TMH_HIP(hipStreamSynchronize(h->stream));
   });
 }
@@ -510,7 +508,7 @@ int tmh_stats_pct_accumulate(tmh_stats* h, double* dev_acc, void* stream) {
     TMH_CHECK(h && dev_acc, TMH_EINVAL, "bad arguments");
     TMH_CHECK(h->flags & TMH_STATS_DEFERRED_PCT, TMH_ESTATE,
               "percentile chain needs a TMH_STATS_DEFERRED_PCT handle");
-    launch_pct_accumulate(h->vlo.p, h->vhi.p, h->n_deferred, h->Q, h->gamma.p, dev_acc,
+    launch_pct_accumulate(h->vlh.p, h->n_deferred, h->Q, h->gamma.p, dev_acc,
                           pick(h->stream, stream));
   });
 }
@@ -523,8 +521,8 @@ int tmh_stats_pct_accumulate_range(tmh_stats* h, double* dev_acc_range, int q_be
               "percentile chain needs a TMH_STATS_DEFERRED_PCT handle");
     TMH_CHECK(q_begin >= 0 && q_count >= 0 && (int64_t)q_begin + q_count <= h->Q, TMH_EINVAL,
               "quantile range out of bounds");
-    launch_pct_accumulate_range(h->vlo.p, h->vhi.p, h->n_deferred, h->Q, q_begin, q_count,
-                                h->gamma.p, dev_acc_range, pick(h->stream, stream));
+    launch_pct_accumulate_range(h->vlh.p, h->n_deferred, h->Q, q_begin, q_count, h->gamma.p,
+                                dev_acc_range, pick(h->stream, stream));
   });
 }
 
@@ -776,7 +774,7 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       // per-site buffers (growing frees memory earlier launches may still use)
       const bool grow = (size_t)nc * kBins > h->hist_full.n || (size_t)nc > h->zeros.n ||
                         ((h->flags & 2u) && (size_t)nc * kBins > h->site_hist.n) ||
-                        (!(h->flags & TMH_STATS_DEFERRED_PCT) && (size_t)nc * h->Q > h->vlo.n);
+                        (!(h->flags & TMH_STATS_DEFERRED_PCT) && (size_t)nc * h->Q > h->vlh.n);
       if (grow) {
         TMH_HIP(hipStreamSynchronize(s));
         TMH_HIP(hipStreamSynchronize(h->stream));
@@ -785,34 +783,31 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       if ((size_t)nc * kBins > h->hist_full.n) h->hist_full.alloc((size_t)nc * kBins, true);
       h->zeros.ensure((size_t)nc);
       if (h->flags & 2u) h->site_hist.ensure((size_t)nc * kBins);
-      uint16_t *vlo, *vhi;
+      uint32_t* vlh;
       if (h->flags & TMH_STATS_DEFERRED_PCT) {
         stats_grow_deferred(h, nc);
-        vlo = h->vlo.p + (size_t)h->n_deferred * h->Q;
-        vhi = h->vhi.p + (size_t)h->n_deferred * h->Q;
+        vlh = h->vlh.p + (size_t)h->n_deferred * h->Q;
       } else {
-        h->vlo.ensure((size_t)nc * h->Q);
-        h->vhi.ensure((size_t)nc * h->Q);
-        vlo = h->vlo.p;
-        vhi = h->vhi.p;
+        h->vlh.ensure((size_t)nc * h->Q);
+        vlh = h->vlh.p;
       }
       if (vec) {
         launch_correct_hist(din, dout, c->npx, nc, c->coef2.p, c->mconst2.p, c->log_transform,
                             clip_lo, clip_hi, h->hist_full.p, c->queues.p, c->n_wg, s);
-        launch_hist_finalize(h->hist_full.p, nc, h->qp, vlo, vhi, h->pooled.p, h->pooled_parts.p,
+        launch_hist_finalize(h->hist_full.p, nc, h->qp, vlh, h->pooled.p, h->pooled_parts.p,
                              kPooledParts, h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr,
                              s);
       } else {  // odd shapes: correct and histogram in two passes
         stats_reserve_sites(h, nc);
         launch_correct_u16(din, dout, c->npx, nc, c->coef.p, c->lut.p, c->mconst.p,
                            c->log_transform, clip_lo, clip_hi, s);
-        launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->qp, vlo, vhi, h->pooled.p, h->zeros.p,
+        launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->qp, vlh, h->pooled.p, h->zeros.p,
                             (h->flags & 2u) ? h->site_hist.p : nullptr, s);
       }
       if (h->flags & TMH_STATS_DEFERRED_PCT)
         h->n_deferred += nc;
       else
-        launch_pct_accumulate(vlo, vhi, nc, h->Q, h->gamma.p, h->acc.p, s);
+        launch_pct_accumulate(vlh, nc, h->Q, h->gamma.p, h->acc.p, s);
       h->last_batch = nc;
       h->pending -= nc;
     }

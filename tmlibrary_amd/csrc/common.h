@@ -68,18 +68,18 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
                     double* mean, double* m2, const double* lut, int log_transform,
                     double* part, size_t part_cap, hipStream_t s);
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
-                         const QPos& p, uint16_t* vlo, uint16_t* vhi, unsigned long long* pooled,
+                         const QPos& p, uint32_t* vlh, unsigned long long* pooled,
                          int64_t* zero_counts, uint32_t* site_hist, hipStream_t s);
-void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const QPos& p, uint16_t* vlo,
-                          uint16_t* vhi, unsigned long long* pooled,
+void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const QPos& p, uint32_t* vlh,
+                          unsigned long long* pooled,
                           unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
                           uint32_t* site_hist, hipStream_t s);
-void launch_pct_accumulate(const uint16_t* vlo, const uint16_t* vhi, int64_t n_sites, int Q,
-                           const double* gamma, double* acc, hipStream_t s);
+// order statistics: per site Q u32 words (previous | next << 16)
+void launch_pct_accumulate(const uint32_t* vlh, int64_t n_sites, int Q, const double* gamma,
+                           double* acc, hipStream_t s);
 // quantiles [q_begin, q_begin + q_count) of rows of ld; acc points at the range
-void launch_pct_accumulate_range(const uint16_t* vlo, const uint16_t* vhi, int64_t n_sites,
-                                 int64_t ld, int q_begin, int q_count, const double* gamma,
-                                 double* acc, hipStream_t s);
+void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t ld, int q_begin,
+                                 int q_count, const double* gamma, double* acc, hipStream_t s);
 void launch_finalize(const double* mean, const double* m2, int64_t n, int64_t npx, double* out_mean,
                      double* out_std, hipStream_t s);
 void launch_merge1(const double* mean, int64_t n, int64_t npx, double* nmean, hipStream_t s);

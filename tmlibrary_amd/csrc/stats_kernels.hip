@@ -436,8 +436,7 @@ __device__ __forceinline__ int advance_rank(const int32_t* R, int t, int32_t x) 
 // carry a margin and the position test decides membership exactly.
 __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_t r1,
                                             uint32_t bin0, const QPos& p,
-                                            uint16_t* __restrict__ vlo, uint16_t* __restrict__ vhi,
-                                            bool vec16) {
+                                            uint32_t* __restrict__ vlh, bool vec16) {
   const int64_t m = (int64_t)p.scale + 3;  // scale > 1 when Q exceeds the pixel count
   int64_t qa = (int64_t)((double)r0 * p.scale) - m;
   int64_t qb = (int64_t)((double)r1 * p.scale) + m;
@@ -481,19 +480,24 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
         mh |= 1u << j;
       }
     }
-    if (vec16 && ml == 0xFFu) {
-      *reinterpret_cast<uint4*>(vlo + q0) = make_uint4(ol[0], ol[1], ol[2], ol[3]);
-    } else if (ml) {
+    // interleaved (previous, next) order statistics: one u32 per quantile
+    if (vec16 && ml == 0xFFu && mh == 0xFFu) {
+      uint4* dst = reinterpret_cast<uint4*>(vlh + q0);
+      dst[0] = make_uint4(__builtin_amdgcn_perm(oh[0], ol[0], 0x05040100u),
+                          __builtin_amdgcn_perm(oh[0], ol[0], 0x07060302u),
+                          __builtin_amdgcn_perm(oh[1], ol[1], 0x05040100u),
+                          __builtin_amdgcn_perm(oh[1], ol[1], 0x07060302u));
+      dst[1] = make_uint4(__builtin_amdgcn_perm(oh[2], ol[2], 0x05040100u),
+                          __builtin_amdgcn_perm(oh[2], ol[2], 0x07060302u),
+                          __builtin_amdgcn_perm(oh[3], ol[3], 0x05040100u),
+                          __builtin_amdgcn_perm(oh[3], ol[3], 0x07060302u));
+    } else if (ml | mh) {  // a round edge: write the halves this round owns
+      uint16_t* h16 = reinterpret_cast<uint16_t*>(vlh + q0);
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if ((ml >> j) & 1u) vlo[q0 + j] = (uint16_t)(ol[j >> 1] >> (16 * (j & 1)));
-    }
-    if (vec16 && mh == 0xFFu) {
-      *reinterpret_cast<uint4*>(vhi + q0) = make_uint4(oh[0], oh[1], oh[2], oh[3]);
-    } else if (mh) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if ((mh >> j) & 1u) vhi[q0 + j] = (uint16_t)(oh[j >> 1] >> (16 * (j & 1)));
+      for (int j = 0; j < 8; ++j) {
+        if ((ml >> j) & 1u) h16[2 * j] = (uint16_t)(ol[j >> 1] >> (16 * (j & 1)));
+        if ((mh >> j) & 1u) h16[2 * j + 1] = (uint16_t)(oh[j >> 1] >> (16 * (j & 1)));
+      }
     }
   }
 }
@@ -513,15 +517,13 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
 // statistic output, 4 = no pooled histogram adds
 template <int ABL = 0, int kTailChunk = kTailChunkDefault, typename CountFn, typename DoneFn>
 __device__ __forceinline__ void hist_tail(CountFn count, DoneFn done, int64_t s, const QPos& p,
-                                          uint16_t* __restrict__ vlo_all,
-                                          uint16_t* __restrict__ vhi_all,
+                                          uint32_t* __restrict__ vlh_all,
                                           unsigned long long* __restrict__ pooled,
                                           int64_t* __restrict__ zero_counts,
                                           uint32_t* __restrict__ site_hist, uint32_t* slots,
                                           uint32_t* cmask, int32_t* starts) {
   const int tid = threadIdx.x;
-  uint16_t* vlo = vlo_all + s * (int64_t)p.Q;
-  uint16_t* vhi = vhi_all + s * (int64_t)p.Q;
+  uint32_t* vlh = vlh_all + s * (int64_t)p.Q;
   const bool vec16 = (p.Q & 7) == 0;
   int64_t base = 0;          // exclusive rank of the current round's first bin
   int nscan = 0;
@@ -564,14 +566,14 @@ __device__ __forceinline__ void hist_tail(CountFn count, DoneFn done, int64_t s,
       if (ABL & 1) continue;
       R[tid] = (int32_t)(r + c[k]);
       __syncthreads();  // R visible; the other R buffer is rewritten only after the next scan
-      fill_groups(R, r0, base, (uint32_t)(jc + k) * kHistThreads, p, vlo, vhi, vec16);
+      fill_groups(R, r0, base, (uint32_t)(jc + k) * kHistThreads, p, vlh, vec16);
     }
   }
 }
 
 __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
     const uint16_t* __restrict__ sites, int64_t npx, int vec, uint32_t* __restrict__ hist_hi,
-    const QPos p, uint16_t* __restrict__ vlo_all, uint16_t* __restrict__ vhi_all,
+    const QPos p, uint32_t* __restrict__ vlh_all,
     unsigned long long* __restrict__ pooled, int64_t* __restrict__ zero_counts,
     uint32_t* __restrict__ site_hist) {
   __shared__ __attribute__((aligned(16))) uint32_t bins[kLdsBins];
@@ -622,7 +624,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
         return ((himask[h >> 11] >> ((h >> 6) & 31u)) & 1u) ? atomicExch(&hhi[h], 0u) : 0u;
       },
       [](uint32_t, uint32_t) {},
-      s, p, vlo_all, vhi_all, pooled, zero_counts, site_hist, slots, cmask, starts);
+      s, p, vlh_all, pooled, zero_counts, site_hist, slots, cmask, starts);
 }
 
 // Per-site histogram (65,536 counts, exact) -> order statistics, written from
@@ -630,8 +632,8 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
 // read and reset), e.g. accumulated by the fused correct+histogram pass.
 template <int ABL = 0>  // ABL 8: counts are not reset (re-runnable)
 __global__ __launch_bounds__(kHistThreads, 8) void k_hist_finalize(
-    uint32_t* __restrict__ hist, const QPos p, uint16_t* __restrict__ vlo_all,
-    uint16_t* __restrict__ vhi_all, unsigned long long* __restrict__ pooled, int n_pooled,
+    uint32_t* __restrict__ hist, const QPos p, uint32_t* __restrict__ vlh_all,
+    unsigned long long* __restrict__ pooled, int n_pooled,
     int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist) {
   __shared__ uint32_t slots[32];
   __shared__ uint32_t cmask[3];
@@ -648,7 +650,7 @@ __global__ __launch_bounds__(kHistThreads, 8) void k_hist_finalize(
       [&](uint32_t b, uint32_t c) {
         if (!(ABL & 8) && c) h[b] = 0u;
       },
-      s, p, vlo_all, vhi_all, pl, zero_counts, site_hist, slots, cmask, starts);
+      s, p, vlh_all, pl, zero_counts, site_hist, slots, cmask, starts);
 }
 
 // pooled[b] += sum of the copies; copies reset to zero (zero-maintained)
@@ -664,27 +666,27 @@ __global__ void k_pooled_fold(unsigned long long* __restrict__ pooled,
   pooled[b] += t;
 }
 
-void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const QPos& p, uint16_t* vlo,
-                          uint16_t* vhi, unsigned long long* pooled,
+void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const QPos& p, uint32_t* vlh,
+                          unsigned long long* pooled,
                           unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
                           uint32_t* site_hist, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("hist_finalize", s);
   hipLaunchKernelGGL(k_hist_finalize<0>, dim3((unsigned)n_sites), dim3(kHistThreads), 0, s, hist,
-                     p, vlo, vhi, pooled_parts, n_parts, zero_counts, site_hist);
+                     p, vlh, pooled_parts, n_parts, zero_counts, site_hist);
   hipLaunchKernelGGL(k_pooled_fold, dim3(kBins / 256), dim3(256), 0, s, pooled, pooled_parts,
                      n_parts);
   TMH_HIP(hipGetLastError());
 }
 
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
-                         const QPos& p, uint16_t* vlo, uint16_t* vhi, unsigned long long* pooled,
+                         const QPos& p, uint32_t* vlh, unsigned long long* pooled,
                          int64_t* zero_counts, uint32_t* site_hist, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("hist", s);
   const int vec = ((npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0) ? 1 : 0;
   hipLaunchKernelGGL(k_hist_scatter, dim3((unsigned)n_sites), dim3(kHistThreads), 0, s, sites, npx,
-                     vec, hist_hi, p, vlo, vhi, pooled, zero_counts, site_hist);
+                     vec, hist_hi, p, vlh, pooled, zero_counts, site_hist);
   TMH_HIP(hipGetLastError());
 }
 
@@ -709,95 +711,56 @@ __device__ __forceinline__ double add_nc(double x, double y) {
 }
 
 constexpr int kPctThreads = 256;
-constexpr int kPctUnroll = 32;
+constexpr int kPctUnroll = 16;
 
 // each thread: two consecutive quantiles (one u32 load of each u16 array)
-// Quantiles [0, Q) of rows of `ld` u16 (vlo/vhi/gamma/acc point at the range's
-// first quantile: a sub-range of the full table is one launch of the
-// pipelined rank chain).
-__global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint16_t* __restrict__ vlo,
-                                                          const uint16_t* __restrict__ vhi,
+// Quantiles [0, Q) of rows of `ld` interleaved (previous, next) order
+// statistics (vlh/gamma/acc point at the range's first quantile: a sub-range
+// of the table is one launch of the pipelined rank chain).  Thread =
+// quantile: one u32 load per site, the lerp off the critical path, and only
+// the f64 add (no contraction) on the in-order dependency chain.
+__global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint32_t* __restrict__ vlh,
                                                           int64_t n_sites, int Q, int64_t ld,
                                                           const double* __restrict__ gamma,
                                                           double* __restrict__ acc) {
-  const int q0 = ((int)blockIdx.x * kPctThreads + threadIdx.x) * 2;
-  if (q0 >= Q) return;
-  const bool two = q0 + 1 < Q;
-  const double g0 = gamma[q0], g1 = two ? gamma[q0 + 1] : 0.0;
-  double a0 = acc[q0], a1 = two ? acc[q0 + 1] : 0.0;
-  const int64_t stride = ld / 2;  // u32 per site (ld, Q and the offset even on this path)
-  const uint32_t* pl = reinterpret_cast<const uint32_t*>(vlo) + q0 / 2;
-  const uint32_t* ph = reinterpret_cast<const uint32_t*>(vhi) + q0 / 2;
-  // software pipeline: the next kPctUnroll sites' loads are in flight while
-  // the current ones are folded in (tail loads clamp to the last site)
-  const int64_t last = n_sites - 1;
-  uint32_t l[kPctUnroll], h[kPctUnroll];
-#pragma unroll
-  for (int k = 0; k < kPctUnroll; ++k) {
-    const int64_t t = k < last ? k : last;
-    l[k] = pl[t * stride];
-    h[k] = ph[t * stride];
-  }
-  for (int64_t s = 0; s < n_sites; s += kPctUnroll) {
-    uint32_t ln[kPctUnroll], hn[kPctUnroll];
-#pragma unroll
-    for (int k = 0; k < kPctUnroll; ++k) {
-      const int64_t t = s + kPctUnroll + k < last ? s + kPctUnroll + k : last;
-      ln[k] = pl[t * stride];
-      hn[k] = ph[t * stride];
-    }
-#pragma unroll
-    for (int k = 0; k < kPctUnroll; ++k) {
-      if (s + k < n_sites) {
-        a0 = add_nc(a0, lerp_np(l[k] & 0xFFFFu, h[k] & 0xFFFFu, g0));
-        a1 = add_nc(a1, lerp_np(l[k] >> 16, h[k] >> 16, g1));
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kPctUnroll; ++k) {
-      l[k] = ln[k];
-      h[k] = hn[k];
-    }
-  }
-  acc[q0] = a0;
-  if (two) acc[q0 + 1] = a1;
-}
-
-__global__ __launch_bounds__(kPctThreads) void k_pct_acc_odd(const uint16_t* __restrict__ vlo,
-                                                              const uint16_t* __restrict__ vhi,
-                                                              int64_t n_sites, int Q, int64_t ld,
-                                                              const double* __restrict__ gamma,
-                                                              double* __restrict__ acc) {
   const int q = (int)blockIdx.x * kPctThreads + threadIdx.x;
   if (q >= Q) return;
   const double g = gamma[q];
   double a = acc[q];
-  for (int64_t s = 0; s < n_sites; ++s) a = add_nc(a, lerp_np(vlo[s * ld + q], vhi[s * ld + q], g));
+  const uint32_t* p = vlh + q;
+  // software pipeline: the next kPctUnroll sites' loads are in flight while
+  // the current ones are folded in (tail loads clamp to the last site)
+  const int64_t last = n_sites - 1;
+  uint32_t v[kPctUnroll];
+#pragma unroll
+  for (int k = 0; k < kPctUnroll; ++k) v[k] = p[(k < last ? k : last) * ld];
+  for (int64_t s = 0; s < n_sites; s += kPctUnroll) {
+    uint32_t vn[kPctUnroll];
+#pragma unroll
+    for (int k = 0; k < kPctUnroll; ++k) {
+      const int64_t t = s + kPctUnroll + k < last ? s + kPctUnroll + k : last;
+      vn[k] = p[t * ld];
+    }
+#pragma unroll
+    for (int k = 0; k < kPctUnroll; ++k)
+      if (s + k < n_sites) a = add_nc(a, lerp_np(v[k] & 0xFFFFu, v[k] >> 16, g));
+#pragma unroll
+    for (int k = 0; k < kPctUnroll; ++k) v[k] = vn[k];
+  }
   acc[q] = a;
 }
 
-void launch_pct_accumulate(const uint16_t* vlo, const uint16_t* vhi, int64_t n_sites, int Q,
-                           const double* gamma, double* acc, hipStream_t s) {
-  launch_pct_accumulate_range(vlo, vhi, n_sites, Q, 0, Q, gamma, acc, s);
+void launch_pct_accumulate(const uint32_t* vlh, int64_t n_sites, int Q, const double* gamma,
+                           double* acc, hipStream_t s) {
+  launch_pct_accumulate_range(vlh, n_sites, Q, 0, Q, gamma, acc, s);
 }
 
-void launch_pct_accumulate_range(const uint16_t* vlo, const uint16_t* vhi, int64_t n_sites,
-                                 int64_t ld, int q_begin, int q_count, const double* gamma,
-                                 double* acc, hipStream_t s) {
+void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t ld, int q_begin,
+                                 int q_count, const double* gamma, double* acc, hipStream_t s) {
   if (n_sites <= 0 || q_count <= 0) return;
   ProfScope prof("pct_acc", s);
-  vlo += q_begin;
-  vhi += q_begin;
-  gamma += q_begin;
-  if ((ld & 1) == 0 && (q_begin & 1) == 0 && (q_count & 1) == 0) {
-    const int grid = (int)cdiv(q_count / 2, kPctThreads);
-    hipLaunchKernelGGL(k_pct_acc, dim3(grid), dim3(kPctThreads), 0, s, vlo, vhi, n_sites, q_count,
-                       ld, gamma, acc);
-  } else {
-    const int grid = (int)cdiv(q_count, kPctThreads);
-    hipLaunchKernelGGL(k_pct_acc_odd, dim3(grid), dim3(kPctThreads), 0, s, vlo, vhi, n_sites,
-                       q_count, ld, gamma, acc);
-  }
+  hipLaunchKernelGGL(k_pct_acc, dim3((unsigned)cdiv(q_count, kPctThreads)), dim3(kPctThreads), 0,
+                     s, vlh + q_begin, n_sites, q_count, ld, gamma + q_begin, acc);
   TMH_HIP(hipGetLastError());
 }
 

@@ -107,7 +107,10 @@ def chain_chunks(n_quantiles, world, chunks=None):
     chunks the chain takes (N + C - 1) chunk-steps instead of N full steps."""
     Q = int(n_quantiles)
     if chunks is None:
-        chunks = 1 if world <= 1 else min(2 * world, 16)
+        # a chunk's pass is bounded below by the in-order f64 chain over the
+        # rank's sites (~0.06 ms at 3,456 sites), so more chunks than ranks
+        # only lengthen the pipeline's fill
+        chunks = 1 if world <= 1 else min(max(2, world), 16)
     chunks = max(1, min(int(chunks), max(1, Q // 2)))
     edges = [((Q * i // chunks) // 2) * 2 for i in range(chunks)] + [Q]
     return [(a, b - a) for a, b in zip(edges[:-1], edges[1:]) if b > a]

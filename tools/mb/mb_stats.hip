@@ -525,9 +525,8 @@ int main(int argc, char** argv) {
   }
   CK(hipMemcpy(qlo, lo.data(), Q * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(qhi, hi.data(), Q * 4, hipMemcpyHostToDevice));
-  uint16_t *vlo, *vhi;
-  CK(hipMalloc(&vlo, S * Q * 2));
-  CK(hipMalloc(&vhi, S * Q * 2));
+  uint32_t* vlh;
+  CK(hipMalloc(&vlh, S * Q * 4));
   unsigned long long* pooled;
   CK(hipMalloc(&pooled, 65536 * 8));
   int64_t* zeros;
@@ -535,7 +534,7 @@ int main(int argc, char** argv) {
   for (int r = 0; r < reps; ++r) {
     t.start();
     QPos qp{qlo, qhi, Q, (double)(Q - 1) / (npx - 1), (int32_t)(npx - 1), 1};
-    launch_hist_scatter(sites, npx, S, hist_hi, qp, vlo, vhi, pooled, zeros, nullptr, 0);
+    launch_hist_scatter(sites, npx, S, hist_hi, qp, vlh, pooled, zeros, nullptr, 0);
     report("hist (prod)", t.stop(), S * site_gb);
   }
   // correct (production) with dummy stats
@@ -639,7 +638,7 @@ int main(int argc, char** argv) {
     auto runf = [&](auto kern, const char* name) {
       for (int r = 0; r < reps; ++r) {
         t.start();
-        hipLaunchKernelGGL(kern, dim3((unsigned)S), dim3(1024), 0, 0, hist, qa, vlo, vhi, parts, 16,
+        hipLaunchKernelGGL(kern, dim3((unsigned)S), dim3(1024), 0, 0, hist, qa, vlh, parts, 16,
                            zeros, (uint32_t*)nullptr);
         report(name, t.stop(), 0.0);
       }
