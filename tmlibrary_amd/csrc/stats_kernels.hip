@@ -404,13 +404,19 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, in
 }
 
 constexpr int kTailChunkDefault = 8;  // rounds whose counts are loaded together
-// first index i >= t with R[i] > x (R: 1024 non-decreasing inclusive prefix
-// ranks in LDS; the caller guarantees R[1023] > x).  Consecutive quantile
-// positions mostly stay in one bin or step to the next, so two probes settle
-// most calls; the rest finish with a binary search over (t+1, 1023].
-__device__ __forceinline__ int advance_rank(const int32_t* R, int t, int32_t x) {
-  if (R[t] > x) return t;
-  if (R[t + 1] > x) return t + 1;
+// Advance (t, Rt = R[t]) to the first index >= t with R[index] > x (R: 1024
+// non-decreasing inclusive prefix ranks in LDS; the caller guarantees
+// R[t - 1] <= x < R[1023]).  Consecutive quantile positions mostly stay in
+// one bin (no LDS read: Rt is cached) or step to the next (one read); the
+// rest finish with a binary search over (t+1, 1023].
+__device__ __forceinline__ void advance_rank(const int32_t* R, int& t, int32_t& Rt, int32_t x) {
+  if (Rt > x) return;
+  const int32_t r1 = R[t + 1];
+  if (r1 > x) {
+    ++t;
+    Rt = r1;
+    return;
+  }
   int lo = t + 1, hi = kHistThreads - 1;  // R[lo] <= x < R[hi]
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
@@ -419,18 +425,22 @@ __device__ __forceinline__ int advance_rank(const int32_t* R, int t, int32_t x) 
     else
       lo = mid;
   }
-  return hi;
+  t = hi;
+  Rt = R[hi];
 }
+
+constexpr int kFillGroups = 1;  // groups of 8 quantiles a thread walks in a row
 
 // One round's order statistics.  R[t] = inclusive prefix rank of the round's
 // bin t (value bin0 + t); the round owns the sorted positions [r0, r1).
-// Quantile-centric: each thread takes groups of 8 consecutive quantiles,
-// reads their previous positions from the (L2-resident) table (the next
-// position is min(prev + 1, n - 1) for every q in [0, 100], np.percentile
-// 'linear'; a general next table is read only if the caller's differs), keeps
-// the ones inside [r0, r1), finds each owning bin by advancing through R in
-// LDS from the previous quantile's bin, and writes the group with ONE 16-B
-// store per stream (masked 2-B stores where a group straddles the round's
+// Quantile-centric: each thread walks kFillGroups consecutive groups of 8
+// quantiles, reads their previous positions from the (L2-resident) table (the
+// next position is min(prev + 1, n - 1) for every q in [0, 100],
+// np.percentile 'linear'; a general next table is read only if the caller's
+// differs), keeps the ones inside [r0, r1), and finds each owning bin by
+// advancing through R from the previous quantile's bin (one binary search
+// per 32 quantiles), writing each group as one 32-B store of interleaved
+// (previous, next) values (2-B stores where a group straddles the round's
 // ends).  The round's quantile range is [r0 * scale, r1 * scale] up to
 // rounding (and one position's worth of quantiles), so the groups scanned
 // carry a margin and the position test decides membership exactly.
@@ -443,60 +453,65 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
   qa = qa < 0 ? 0 : qa;
   qb = qb > p.Q ? p.Q : qb;
   if (qa >= qb) return;
-  const int64_t g1 = (qb - 1) >> 3;
+  const int64_t g0 = qa >> 3, g1 = (qb - 1) >> 3;
   const bool tab16 = vec16;  // tables are 16-B aligned rows when Q % 8 == 0 (hipMalloc base)
   const int32_t a = (int32_t)r0, b = (int32_t)r1;
-  for (int64_t g = (qa >> 3) + threadIdx.x; g <= g1; g += kHistThreads) {
-    const int64_t q0 = g << 3;
-    int32_t pl[8];
-    if (tab16 && q0 + 8 <= p.Q) {
-      const int4 a0 = reinterpret_cast<const int4*>(p.lo + q0)[0];
-      const int4 a1 = reinterpret_cast<const int4*>(p.lo + q0)[1];
-      pl[0] = a0.x; pl[1] = a0.y; pl[2] = a0.z; pl[3] = a0.w;
-      pl[4] = a1.x; pl[5] = a1.y; pl[6] = a1.z; pl[7] = a1.w;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pl[j] = q0 + j < p.Q ? p.lo[q0 + j] : INT32_MAX;
-    }
-    // positions are non-decreasing in q: the first one inside the round
-    // starts the scan at bin 0, every later one continues from its
-    // predecessor's bin.  Results are packed as they come (u16 pairs).
-    uint32_t ol[4] = {0u, 0u, 0u, 0u}, oh[4] = {0u, 0u, 0u, 0u};
-    uint32_t ml = 0, mh = 0;
+  for (int64_t sg = g0 + (int64_t)threadIdx.x * kFillGroups; sg <= g1;
+       sg += (int64_t)kHistThreads * kFillGroups) {
     int tl = 0, th = 0;
+    int32_t Rl = R[0], Rh = Rl;
+    for (int64_t g = sg; g < sg + kFillGroups && g <= g1; ++g) {
+      const int64_t q0 = g << 3;
+      int32_t pl[8];
+      if (tab16 && q0 + 8 <= p.Q) {
+        const int4 a0 = reinterpret_cast<const int4*>(p.lo + q0)[0];
+        const int4 a1 = reinterpret_cast<const int4*>(p.lo + q0)[1];
+        pl[0] = a0.x; pl[1] = a0.y; pl[2] = a0.z; pl[3] = a0.w;
+        pl[4] = a1.x; pl[5] = a1.y; pl[6] = a1.z; pl[7] = a1.w;
+      } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int32_t pj = pl[j];
-      if (pj >= a && pj < b) {
-        tl = advance_rank(R, tl, pj);
-        ol[j >> 1] |= (bin0 + (uint32_t)tl) << (16 * (j & 1));
-        ml |= 1u << j;
+        for (int j = 0; j < 8; ++j) pl[j] = q0 + j < p.Q ? p.lo[q0 + j] : INT32_MAX;
       }
-      const int32_t hj = p.hi_next ? (pj < p.last ? pj + 1 : pj)
-                                   : (q0 + j < p.Q ? p.hi[q0 + j] : INT32_MAX);
-      if (hj >= a && hj < b) {
-        th = advance_rank(R, th > tl ? th : tl, hj);
-        oh[j >> 1] |= (bin0 + (uint32_t)th) << (16 * (j & 1));
-        mh |= 1u << j;
-      }
-    }
-    // interleaved (previous, next) order statistics: one u32 per quantile
-    if (vec16 && ml == 0xFFu && mh == 0xFFu) {
-      uint4* dst = reinterpret_cast<uint4*>(vlh + q0);
-      dst[0] = make_uint4(__builtin_amdgcn_perm(oh[0], ol[0], 0x05040100u),
-                          __builtin_amdgcn_perm(oh[0], ol[0], 0x07060302u),
-                          __builtin_amdgcn_perm(oh[1], ol[1], 0x05040100u),
-                          __builtin_amdgcn_perm(oh[1], ol[1], 0x07060302u));
-      dst[1] = make_uint4(__builtin_amdgcn_perm(oh[2], ol[2], 0x05040100u),
-                          __builtin_amdgcn_perm(oh[2], ol[2], 0x07060302u),
-                          __builtin_amdgcn_perm(oh[3], ol[3], 0x05040100u),
-                          __builtin_amdgcn_perm(oh[3], ol[3], 0x07060302u));
-    } else if (ml | mh) {  // a round edge: write the halves this round owns
-      uint16_t* h16 = reinterpret_cast<uint16_t*>(vlh + q0);
+      uint32_t ol[4] = {0u, 0u, 0u, 0u}, oh[4] = {0u, 0u, 0u, 0u};
+      uint32_t ml = 0, mh = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if ((ml >> j) & 1u) h16[2 * j] = (uint16_t)(ol[j >> 1] >> (16 * (j & 1)));
-        if ((mh >> j) & 1u) h16[2 * j + 1] = (uint16_t)(oh[j >> 1] >> (16 * (j & 1)));
+        const int32_t pj = pl[j];
+        if (pj >= a && pj < b) {
+          advance_rank(R, tl, Rl, pj);
+          ol[j >> 1] |= (bin0 + (uint32_t)tl) << (16 * (j & 1));
+          ml |= 1u << j;
+        }
+        const int32_t hj = p.hi_next ? (pj < p.last ? pj + 1 : pj)
+                                     : (q0 + j < p.Q ? p.hi[q0 + j] : INT32_MAX);
+        if (hj >= a && hj < b) {
+          if (th < tl) {
+            th = tl;
+            Rh = Rl;
+          }
+          advance_rank(R, th, Rh, hj);
+          oh[j >> 1] |= (bin0 + (uint32_t)th) << (16 * (j & 1));
+          mh |= 1u << j;
+        }
+      }
+      // interleaved (previous, next) order statistics: one u32 per quantile
+      if (vec16 && ml == 0xFFu && mh == 0xFFu) {
+        uint4* dst = reinterpret_cast<uint4*>(vlh + q0);
+        dst[0] = make_uint4(__builtin_amdgcn_perm(oh[0], ol[0], 0x05040100u),
+                            __builtin_amdgcn_perm(oh[0], ol[0], 0x07060302u),
+                            __builtin_amdgcn_perm(oh[1], ol[1], 0x05040100u),
+                            __builtin_amdgcn_perm(oh[1], ol[1], 0x07060302u));
+        dst[1] = make_uint4(__builtin_amdgcn_perm(oh[2], ol[2], 0x05040100u),
+                            __builtin_amdgcn_perm(oh[2], ol[2], 0x07060302u),
+                            __builtin_amdgcn_perm(oh[3], ol[3], 0x05040100u),
+                            __builtin_amdgcn_perm(oh[3], ol[3], 0x07060302u));
+      } else if (ml | mh) {  // a round edge: write the halves this round owns
+        uint16_t* h16 = reinterpret_cast<uint16_t*>(vlh + q0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if ((ml >> j) & 1u) h16[2 * j] = (uint16_t)(ol[j >> 1] >> (16 * (j & 1)));
+          if ((mh >> j) & 1u) h16[2 * j + 1] = (uint16_t)(oh[j >> 1] >> (16 * (j & 1)));
+        }
       }
     }
   }
