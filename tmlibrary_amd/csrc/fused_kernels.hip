@@ -139,7 +139,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // histogram slices, so the flush (LDS scan + global atomics + barriers) runs
 // with the next unit's pixels already in flight.
 template <bool LOG, bool CLIP, int SPU, int ABL, int NT, int LB>
-__global__ __launch_bounds__(NT, 4) void k_correct_hist(
+__global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void k_correct_hist(
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
     const float4* __restrict__ coef, const float4* __restrict__ mconst2, int clip_lo,
     int clip_hi, uint32_t* __restrict__ hist, int* __restrict__ queues, int bands_per_xcd) {

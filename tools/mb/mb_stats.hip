@@ -620,6 +620,11 @@ int main(int argc, char** argv) {
     run(k_correct_hist<true, false, 4, 0, 1024, 32768>, 1024, "fused spu4 t1024: full");
     run(k_correct_hist<true, false, 2, 0, 512, 16384>, 512, "fused spu2 t512: full");
     run(k_correct_hist<true, false, 4, 0, 512, 16384>, 512, "fused spu4 t512: full");
+    run(k_correct_hist<true, false, 8, 0, 1024, 32768>, 1024, "fused spu8 t1024: full");
+    run(k_correct_hist<true, false, 8, 3, 1024, 32768>, 1024, "fused spu8 t1024: math only");
+    run(k_correct_hist<true, false, 4, 0, 256, 8192>, 256, "fused spu4 t256: full");
+    run(k_correct_hist<true, false, 8, 0, 512, 32768>, 512, "fused spu8 t512 lds128k: full");
+    run(k_correct_hist<true, false, 8, 3, 512, 32768>, 512, "fused spu8 t512 lds128k: math only");
     run(k_correct_hist<true, false, 4, 8, 1024, 32768>, 1024, "fused spu4 t1024: no flush");
     run(k_correct_hist<true, false, 4, 1, 1024, 32768>, 1024, "fused spu4 t1024: no hist");
     run(k_correct_hist<true, false, 4, 2, 1024, 32768>, 1024, "fused spu4 t1024: const coef");
