@@ -766,13 +766,74 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
                      (reinterpret_cast<uintptr_t>(dev_out) & 15) == 0 &&
                      // the fused pass floors zero pixels at 10**zero_log10 in f32
                      (!c->log_transform || (c->zero_log10 >= -37.0 && c->zero_log10 <= 0.0));
-    const int64_t chunk = 4096;
+    if (vec && n_sites > 0) {
+      // Optional site chunks (TMH_CH_CHUNKS, default 1): chunk k's order
+      // statistics (hist finalize, ordered percentile sum) go to the side
+      // stream behind chunk k's correct+histogram pass, in chunk order (the
+      // percentile sums stay in site order).  Measured: no gain -- the
+      // persistent pass keeps every CU's slots until its queues drain, so the
+      // side-stream finalize only runs in the next chunk's tail.
+      static const int env_chunks = [] {
+        const char* e = getenv("TMH_CH_CHUNKS");
+        return e ? atoi(e) : 0;
+      }();
+      int nch = env_chunks > 0 ? env_chunks : 1;
+      nch = (int)std::min<int64_t>(nch, n_sites);
+      const bool grow = (size_t)n_sites * kBins > h->hist_full.n || (size_t)n_sites > h->zeros.n ||
+                        ((h->flags & 2u) && (size_t)n_sites * kBins > h->site_hist.n) ||
+                        (!(h->flags & TMH_STATS_DEFERRED_PCT) &&
+                         (size_t)n_sites * h->Q > h->vlh.n);
+      if (grow) {
+        TMH_HIP(hipStreamSynchronize(s));
+        TMH_HIP(hipStreamSynchronize(h->stream));
+        TMH_HIP(hipStreamSynchronize(h->side));
+      }
+      if ((size_t)n_sites * kBins > h->hist_full.n)
+        h->hist_full.alloc((size_t)n_sites * kBins, true);
+      h->zeros.ensure((size_t)n_sites);
+      if (h->flags & 2u) h->site_hist.ensure((size_t)n_sites * kBins);
+      uint32_t* vlh;
+      if (h->flags & TMH_STATS_DEFERRED_PCT) {
+        stats_grow_deferred(h, n_sites);
+        vlh = h->vlh.p + (size_t)h->n_deferred * h->Q;
+      } else {
+        h->vlh.ensure((size_t)n_sites * h->Q);
+        vlh = h->vlh.p;
+      }
+      hipStream_t side = nch > 1 ? h->side : s;
+      for (int k = 0; k < nch; ++k) {
+        const int64_t c0 = n_sites * k / nch, nc = n_sites * (k + 1) / nch - c0;
+        launch_correct_hist(dev_in + c0 * h->npx, dev_out + c0 * h->npx, c->npx, nc, c->coef2.p,
+                            c->mconst2.p, c->log_transform, clip_lo, clip_hi,
+                            h->hist_full.p + (size_t)c0 * kBins, c->queues.p, c->n_wg, s);
+        if (side != s) {
+          TMH_HIP(hipEventRecord(h->ev_fork, s));
+          TMH_HIP(hipStreamWaitEvent(side, h->ev_fork, 0));
+        }
+        launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, nc, h->qp,
+                             vlh + (size_t)c0 * h->Q, h->pooled.p, h->pooled_parts.p,
+                             kPooledParts, h->zeros.p + c0,
+                             (h->flags & 2u) ? h->site_hist.p + (size_t)c0 * kBins : nullptr,
+                             side);
+        if (!(h->flags & TMH_STATS_DEFERRED_PCT))
+          launch_pct_accumulate(vlh + (size_t)c0 * h->Q, nc, h->Q, h->gamma.p, h->acc.p, side);
+      }
+      if (side != s) {
+        TMH_HIP(hipEventRecord(h->ev_join, side));
+        TMH_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
+      }
+      if (h->flags & TMH_STATS_DEFERRED_PCT) h->n_deferred += n_sites;
+      h->last_batch = n_sites;
+      h->pending -= n_sites;
+      return;
+    }
+    const int64_t chunk = 4096;  // odd shapes: correct and histogram in two passes
     for (int64_t c0 = 0; c0 < n_sites; c0 += chunk) {
       const int64_t nc = std::min(chunk, n_sites - c0);
       const uint16_t* din = dev_in + c0 * h->npx;
       uint16_t* dout = dev_out + c0 * h->npx;
       // per-site buffers (growing frees memory earlier launches may still use)
-      const bool grow = (size_t)nc * kBins > h->hist_full.n || (size_t)nc > h->zeros.n ||
+      const bool grow = (size_t)nc > h->zeros.n ||
                         ((h->flags & 2u) && (size_t)nc * kBins > h->site_hist.n) ||
                         (!(h->flags & TMH_STATS_DEFERRED_PCT) && (size_t)nc * h->Q > h->vlh.n);
       if (grow) {
@@ -780,7 +841,6 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         TMH_HIP(hipStreamSynchronize(h->stream));
         TMH_HIP(hipStreamSynchronize(h->side));
       }
-      if ((size_t)nc * kBins > h->hist_full.n) h->hist_full.alloc((size_t)nc * kBins, true);
       h->zeros.ensure((size_t)nc);
       if (h->flags & 2u) h->site_hist.ensure((size_t)nc * kBins);
       uint32_t* vlh;
@@ -791,19 +851,11 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         h->vlh.ensure((size_t)nc * h->Q);
         vlh = h->vlh.p;
       }
-      if (vec) {
-        launch_correct_hist(din, dout, c->npx, nc, c->coef2.p, c->mconst2.p, c->log_transform,
-                            clip_lo, clip_hi, h->hist_full.p, c->queues.p, c->n_wg, s);
-        launch_hist_finalize(h->hist_full.p, nc, h->qp, vlh, h->pooled.p, h->pooled_parts.p,
-                             kPooledParts, h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr,
-                             s);
-      } else {  // odd shapes: correct and histogram in two passes
-        stats_reserve_sites(h, nc);
-        launch_correct_u16(din, dout, c->npx, nc, c->coef.p, c->lut.p, c->mconst.p,
-                           c->log_transform, clip_lo, clip_hi, s);
-        launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->qp, vlh, h->pooled.p, h->zeros.p,
-                            (h->flags & 2u) ? h->site_hist.p : nullptr, s);
-      }
+      stats_reserve_sites(h, nc);
+      launch_correct_u16(din, dout, c->npx, nc, c->coef.p, c->lut.p, c->mconst.p, c->log_transform,
+                         clip_lo, clip_hi, s);
+      launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->qp, vlh, h->pooled.p, h->zeros.p,
+                          (h->flags & 2u) ? h->site_hist.p : nullptr, s);
       if (h->flags & TMH_STATS_DEFERRED_PCT)
         h->n_deferred += nc;
       else
