@@ -34,8 +34,17 @@ int tmh5_read_illumstats(const char* path, double* mean, double* std_, double* k
 /* bits: 8 or 16; gzip_level < 0 writes an uncompressed contiguous dataset */
 int tmh5_write_channel_image(const char* path, int height, int width, int bits, const void* data,
                              int gzip_level);
+/* same with explicit chunk extents (0: the default whole-row ~256 KiB chunks),
+ * e.g. to reproduce h5py's automatic 2-D chunking of the reference's files */
+int tmh5_write_channel_image_chunked(const char* path, int height, int width, int bits,
+                                     const void* data, int gzip_level, int chunk_rows,
+                                     int chunk_cols);
 int tmh5_channel_image_shape(const char* path, int* height, int* width, int* bits);
 int tmh5_read_channel_image(const char* path, void* out);
+/* n_files channel images (same shape and dtype) into out[n][H][W], decoded by
+ * n_threads workers: raw deflate chunks from HDF5, zlib inflate in parallel
+ * (the input path of run_job / configs[4]). */
+int tmh5_read_channel_images(const char* const* paths, int64_t n_files, void* out, int n_threads);
 
 #ifdef __cplusplus
 }

@@ -62,3 +62,45 @@ def test_missing_dataset_is_keyerror(tmp_path):
     h5.write_channel_image(p, np.zeros((4, 4), np.uint16))
     with pytest.raises((KeyError, IOError)):
         h5.read_illumstats(p)
+
+
+@pytest.mark.parametrize("dtype,chunks,gzip", [
+    (np.uint16, None, 4),          # whole-row chunks (our default)
+    (np.uint16, (37, 50), 4),      # 2-D chunks with partial edge chunks (h5py-style)
+    (np.uint16, (64, 64), 1),
+    (np.uint8, (30, 41), 6),
+    (np.uint16, None, -1),         # contiguous, uncompressed: H5Dread fallback
+])
+def test_read_channel_images_parallel(tmp_path, dtype, chunks, gzip):
+    """Parallel chunk inflate == the serial H5Dread path."""
+    rng = np.random.default_rng(17)
+    H, W = 101, 157
+    hi = 256 if dtype == np.uint8 else 65536
+    imgs = [rng.integers(0, hi, size=(H, W), dtype=dtype) for _ in range(9)]
+    imgs[2][:] = 7  # highly compressible
+    paths = []
+    for i, a in enumerate(imgs):
+        p = str(tmp_path / ("channel_image_file_%d.h5" % i))
+        h5.write_channel_image(p, a, gzip_level=gzip, chunks=chunks)
+        paths.append(p)
+    for nt in (1, 3, 16):
+        got = h5.read_channel_images(paths, n_threads=nt)
+        assert got.dtype == dtype and got.shape == (9, H, W)
+        assert np.array_equal(got, np.stack(imgs))
+    for p, a in zip(paths, imgs):
+        assert np.array_equal(h5.read_channel_image(p), a)
+
+
+def test_read_channel_images_errors(tmp_path):
+    a = np.zeros((10, 12), np.uint16)
+    p0, p1, p2 = (str(tmp_path / ("f%d.h5" % i)) for i in range(3))
+    h5.write_channel_image(p0, a)
+    h5.write_channel_image(p1, np.zeros((10, 13), np.uint16))
+    h5.write_channel_image(p2, a.astype(np.uint8))
+    with pytest.raises(Exception, match="differs"):
+        h5.read_channel_images([p0, p1], n_threads=2)
+    with pytest.raises(Exception, match="differs"):
+        h5.read_channel_images([p0, p2], n_threads=2)
+    with pytest.raises(Exception):
+        h5.read_channel_images([p0, str(tmp_path / "missing.h5")], n_threads=2)
+    assert h5.read_channel_images([], n_threads=2).shape[0] == 0

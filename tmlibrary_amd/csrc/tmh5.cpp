@@ -14,10 +14,16 @@
 // Error convention as libtmhip: 0 ok, negative errno-style code on failure,
 // message in tmh5_last_error().
 #include <hdf5.h>
+#include <zlib.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 #include "../../include/tmh5.h"
 
@@ -139,19 +145,28 @@ int tmh5_read_illumstats(const char* path, double* mean, double* std_, double* k
 
 int tmh5_write_channel_image(const char* path, int height, int width, int bits, const void* data,
                              int gzip_level) {
+  return tmh5_write_channel_image_chunked(path, height, width, bits, data, gzip_level, 0, 0);
+}
+
+int tmh5_write_channel_image_chunked(const char* path, int height, int width, int bits,
+                                     const void* data, int gzip_level, int chunk_rows,
+                                     int chunk_cols) {
   return guard([&] {
     silence();
-    if (!path || !data || height <= 0 || width <= 0 || (bits != 8 && bits != 16))
+    if (!path || !data || height <= 0 || width <= 0 || (bits != 8 && bits != 16) ||
+        chunk_rows < 0 || chunk_cols < 0)
       throw H5Err{-22, "bad arguments"};
     Hid f(H5Fcreate(path, H5F_ACC_TRUNC, H5P_DEFAULT, H5P_DEFAULT), H5Fclose);
     const hsize_t d2[2] = {(hsize_t)height, (hsize_t)width};
     Hid dcpl(H5Pcreate(H5P_DATASET_CREATE), H5Pclose);
     if (gzip_level >= 0) {
-      // chunk of whole rows, ~256 KiB, like h5py's automatic chunking scale
+      // default: chunks of whole rows, ~256 KiB, like h5py's automatic chunking scale
       const hsize_t row_bytes = (hsize_t)width * (bits / 8);
       hsize_t rows = row_bytes ? (262144 + row_bytes - 1) / row_bytes : 1;
       if (rows > (hsize_t)height) rows = height;
-      const hsize_t chunk[2] = {rows, (hsize_t)width};
+      hsize_t chunk[2] = {rows, (hsize_t)width};
+      if (chunk_rows > 0) chunk[0] = std::min<hsize_t>(chunk_rows, height);
+      if (chunk_cols > 0) chunk[1] = std::min<hsize_t>(chunk_cols, width);
       H5Pset_chunk(dcpl, 2, chunk);
       H5Pset_deflate(dcpl, (unsigned)(gzip_level > 9 ? 9 : gzip_level));
     }
@@ -188,6 +203,138 @@ int tmh5_read_channel_image(const char* path, void* out) {
     const hid_t mtype = H5Tget_size(t) == 1 ? H5T_NATIVE_UINT8 : H5T_NATIVE_UINT16;
     if (H5Dread(ds, mtype, H5S_ALL, H5S_ALL, H5P_DEFAULT, out) < 0)
       throw H5Err{-5, "reading /array failed"};
+  });
+}
+
+// Many channel images at once (the input path is
+// bound by gzip inflate, not by the GPU).  libhdf5 serialises every call
+// behind its global lock -- including the deflate filter inside H5Dread -- so
+// the workers take only the raw compressed chunks from HDF5
+// (H5Dget_chunk_info + H5Dread_chunk) and inflate them with zlib in
+// parallel, straight into the caller's [n][H][W] buffer.  Datasets that are
+// not chunked+deflate-only (contiguous, shuffle, other filters) are read
+// with H5Dread instead.  All files must share one shape and dtype.
+namespace {
+
+void read_one_parallel(const char* path, uint8_t* out, int height, int width, int esize) {
+  std::vector<std::vector<uint8_t>> raw;
+  std::vector<std::pair<hsize_t, hsize_t>> offs;
+  std::vector<char> stored;  // filter mask: deflate skipped for this chunk
+  hsize_t ch[2] = {0, 0};
+  {
+    Hid f(H5Fopen(path, H5F_ACC_RDONLY, H5P_DEFAULT), H5Fclose);
+    Hid ds(H5Dopen2(f, "array", H5P_DEFAULT), H5Dclose);
+    Hid t(H5Dget_type(ds), H5Tclose);
+    Hid sp(H5Dget_space(ds), H5Sclose);
+    hsize_t d[2] = {0, 0};
+    if (H5Sget_simple_extent_ndims(sp) != 2) throw H5Err{-22, std::string(path) + ": /array is not 2-D"};
+    H5Sget_simple_extent_dims(sp, d, nullptr);
+    if ((int)d[0] != height || (int)d[1] != width || (int)H5Tget_size(t) != esize ||
+        H5Tget_class(t) != H5T_INTEGER || H5Tget_sign(t) != H5T_SGN_NONE)
+      throw H5Err{-22, std::string(path) + ": shape or dtype differs from the first image"};
+    Hid dcpl(H5Dget_create_plist(ds), H5Pclose);
+    bool direct = H5Pget_layout(dcpl) == H5D_CHUNKED && H5Pget_nfilters(dcpl) == 1 &&
+                  H5Tget_order(t) == H5T_ORDER_LE;
+    if (direct) {
+      unsigned flags = 0, cd[8];
+      size_t ncd = 8;
+      direct = H5Pget_filter2(dcpl, 0, &flags, &ncd, cd, 0, nullptr, nullptr) == H5Z_FILTER_DEFLATE &&
+               H5Pget_chunk(dcpl, 2, ch) == 2;
+    }
+    if (!direct) {
+      const hid_t mtype = esize == 1 ? H5T_NATIVE_UINT8 : H5T_NATIVE_UINT16;
+      if (H5Dread(ds, mtype, H5S_ALL, H5S_ALL, H5P_DEFAULT, out) < 0)
+        throw H5Err{-5, std::string(path) + ": reading /array failed"};
+      return;
+    }
+    hsize_t nchunks = 0;
+    if (H5Dget_num_chunks(ds, sp, &nchunks) < 0) throw H5Err{-5, "H5Dget_num_chunks failed"};
+    if (nchunks < (hsize_t)(((d[0] + ch[0] - 1) / ch[0]) * ((d[1] + ch[1] - 1) / ch[1])))
+      memset(out, 0, (size_t)height * width * esize);  // unwritten chunks read as fill (0)
+    raw.resize(nchunks);
+    offs.resize(nchunks);
+    stored.resize(nchunks);
+    for (hsize_t i = 0; i < nchunks; ++i) {
+      hsize_t coord[2];
+      unsigned fmask = 0;
+      haddr_t addr;
+      hsize_t size = 0;
+      if (H5Dget_chunk_info(ds, sp, i, coord, &fmask, &addr, &size) < 0)
+        throw H5Err{-5, "H5Dget_chunk_info failed"};
+      raw[i].resize(size);
+      uint32_t fm = 0;
+      if (H5Dread_chunk(ds, H5P_DEFAULT, coord, &fm, raw[i].data()) < 0)
+        throw H5Err{-5, "H5Dread_chunk failed"};
+      stored[i] = (fm & 1u) ? 1 : 0;
+      offs[i] = {coord[0], coord[1]};
+    }
+  }
+  // inflate outside the HDF5 lock
+  const size_t full = (size_t)(ch[0] * ch[1]) * esize;
+  std::vector<uint8_t> buf(full);
+  for (size_t i = 0; i < raw.size(); ++i) {
+    uLongf len = (uLongf)full;
+    const uint8_t* src = buf.data();
+    if (stored[i]) {
+      if (raw[i].size() != full) throw H5Err{-5, std::string(path) + ": bad unfiltered chunk"};
+      src = raw[i].data();
+    } else if (uncompress(buf.data(), &len, raw[i].data(), (uLong)raw[i].size()) != Z_OK ||
+               len != (uLongf)full) {
+      throw H5Err{-5, std::string(path) + ": corrupt deflate chunk"};
+    }
+    const hsize_t r0 = offs[i].first, c0 = offs[i].second;
+    const hsize_t rows = std::min<hsize_t>(ch[0], (hsize_t)height - r0);
+    const hsize_t cols = std::min<hsize_t>(ch[1], (hsize_t)width - c0);
+    for (hsize_t r = 0; r < rows; ++r)
+      memcpy(out + ((r0 + r) * (hsize_t)width + c0) * esize, src + r * ch[1] * esize,
+             (size_t)cols * esize);
+  }
+}
+
+}  // namespace
+
+int tmh5_read_channel_images(const char* const* paths, int64_t n_files, void* out, int n_threads) {
+  return guard([&] {
+    silence();
+    if (n_files < 0 || ((!paths || !out) && n_files > 0)) throw H5Err{-22, "bad arguments"};
+    if (n_files == 0) return;
+    int h = 0, w = 0, bits = 0;
+    int rc = tmh5_channel_image_shape(paths[0], &h, &w, &bits);
+    if (rc) throw H5Err{rc, g_err};
+    const int esize = bits / 8;
+    const size_t img = (size_t)h * w * esize;
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(n_threads > 0 ? n_threads : 1, n_files));
+    std::atomic<int64_t> next{0};
+    std::atomic<bool> failed{false};
+    std::string first_err;
+    int first_code = 0;
+    std::mutex m;
+    auto work = [&] {
+      for (;;) {
+        const int64_t i = next.fetch_add(1);
+        if (i >= n_files || failed.load()) return;
+        try {
+          read_one_parallel(paths[i], static_cast<uint8_t*>(out) + (size_t)i * img, h, w, esize);
+        } catch (const H5Err& e) {
+          std::lock_guard<std::mutex> lk(m);
+          if (!failed.exchange(true)) {
+            first_err = e.msg;
+            first_code = e.code;
+          }
+        } catch (...) {
+          std::lock_guard<std::mutex> lk(m);
+          if (!failed.exchange(true)) {
+            first_err = std::string(paths[i]) + ": read failed";
+            first_code = -5;
+          }
+        }
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    if (failed) throw H5Err{first_code, first_err};
   });
 }
 

@@ -42,6 +42,10 @@ _SIGS = {
     "tmh5_channel_image_shape": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                            C.POINTER(C.c_int)]),
     "tmh5_read_channel_image": (C.c_int, [C.c_char_p, C.c_void_p]),
+    "tmh5_write_channel_image_chunked": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int,
+                                                   C.c_void_p, C.c_int, C.c_int, C.c_int]),
+    "tmh5_read_channel_images": (C.c_int, [C.POINTER(C.c_char_p), C.c_int64, C.c_void_p,
+                                           C.c_int]),
 }
 
 
@@ -101,13 +105,16 @@ def read_illumstats(path):
     return mean, std, keys, vals
 
 
-def write_channel_image(path, array, gzip_level=4):
+def write_channel_image(path, array, gzip_level=4, chunks=None):
+    """``/array`` gzip-compressed (gzip_level < 0: contiguous, uncompressed);
+    ``chunks`` = (rows, cols) or None for whole-row ~256 KiB chunks."""
     L = h5lib()
     a = np.ascontiguousarray(array)
     if a.dtype not in (np.uint8, np.uint16) or a.ndim != 2:
         raise ValueError("channel images are 2-D uint8/uint16")
-    _check(L.tmh5_write_channel_image(_b(path), a.shape[0], a.shape[1], 8 * a.itemsize,
-                                      a.ctypes.data, int(gzip_level)), path)
+    cr, cc = (0, 0) if chunks is None else (int(chunks[0]), int(chunks[1]))
+    _check(L.tmh5_write_channel_image_chunked(_b(path), a.shape[0], a.shape[1], 8 * a.itemsize,
+                                              a.ctypes.data, int(gzip_level), cr, cc), path)
 
 
 def read_channel_image(path):
@@ -116,6 +123,29 @@ def read_channel_image(path):
     _check(L.tmh5_channel_image_shape(_b(path), C.byref(h), C.byref(w), C.byref(bits)), path)
     out = np.empty((h.value, w.value), np.uint8 if bits.value == 8 else np.uint16)
     _check(L.tmh5_read_channel_image(_b(path), out.ctypes.data), path)
+    return out
+
+
+def default_decode_threads():
+    n = os.cpu_count() or 1
+    return max(1, min(16, n))  # the GPU boxes grant 16 cores per GPU
+
+
+def read_channel_images(paths, n_threads=None):
+    """Decode many channel image files (same shape/dtype) into one [n, H, W]
+    array with ``n_threads`` parallel inflate workers (libtmh5; the HDF5
+    layout of tmlib/models/file.py:322-363)."""
+    paths = list(paths)
+    L = h5lib()
+    if not paths:
+        return np.empty((0, 0, 0), np.uint16)
+    h, w, bits = C.c_int(), C.c_int(), C.c_int()
+    _check(L.tmh5_channel_image_shape(_b(paths[0]), C.byref(h), C.byref(w), C.byref(bits)),
+           paths[0])
+    out = np.empty((len(paths), h.value, w.value), np.uint8 if bits.value == 8 else np.uint16)
+    arr = (C.c_char_p * len(paths))(*[_b(p) for p in paths])
+    nt = default_decode_threads() if n_threads is None else int(n_threads)
+    _check(L.tmh5_read_channel_images(arr, len(paths), out.ctypes.data, nt), paths[0])
     return out
 
 

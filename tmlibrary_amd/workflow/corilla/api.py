@@ -18,7 +18,7 @@ import queue
 import threading
 
 from tmlibrary_amd.image import IllumstatsContainer
-from tmlibrary_amd.models.file import ExperimentStore
+from tmlibrary_amd.models.file import ExperimentStore, read_channel_images
 from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
 
 logger = logging.getLogger(__name__)
@@ -37,7 +37,7 @@ def _file_id(fid):
 class IllumstatsCalculator(object):
     """Calculation of illumination statistics (corilla/api.py:31-146)."""
 
-    def __init__(self, experiment_id, store=None, batch_size=32, prefetch=8):
+    def __init__(self, experiment_id, store=None, batch_size=32, prefetch=2, decode_threads=None):
         self.experiment_id = experiment_id
         if store is None:
             raise ValueError("an ExperimentStore is required (no database in this build)")
@@ -46,6 +46,7 @@ class IllumstatsCalculator(object):
         self.store = store
         self.batch_size = batch_size
         self.prefetch = prefetch
+        self.decode_threads = decode_threads  # None: min(16, cpu count)
 
     def create_run_batches(self, args=None, channel_files=None, channel_names=None, seed=None):
         """One job per channel (corilla/api.py:45-105).
@@ -81,29 +82,36 @@ class IllumstatsCalculator(object):
             yield {"id": count, "channel_image_files_ids": [[f] for f in file_ids],
                    "channel_id": ch_id}
 
-    def _images(self, file_ids):
-        """Yield (file_id, ChannelImage) in order, decoded one thread ahead."""
+    def _blocks(self, file_ids):
+        """Yield (file ids, [n, H, W] sites) in order, ``batch_size`` files at a
+        time, decoded by ``decode_threads`` parallel inflate workers one block
+        ahead of the GPU update."""
         q = queue.Queue(maxsize=max(1, self.prefetch))
         stop = object()
+        step = max(1, self.batch_size)
 
         def reader():
             try:
-                for fid in file_ids:
-                    q.put((fid, self.store.channel_image_file(fid).get()))
+                for i in range(0, len(file_ids), step):
+                    ids = file_ids[i:i + step]
+                    paths = [self.store.channel_image_file(f).location for f in ids]
+                    q.put((ids, read_channel_images(paths, self.decode_threads)))
             except BaseException as e:  # surface I/O errors in the caller
                 q.put(e)
             q.put(stop)
 
         t = threading.Thread(target=reader, daemon=True)
         t.start()
-        while True:
-            item = q.get()
-            if item is stop:
-                break
-            if isinstance(item, BaseException):
-                raise item
-            yield item
-        t.join()
+        try:
+            while True:
+                item = q.get()
+                if item is stop:
+                    break
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
+        finally:
+            t.join()
 
     def run_job(self, batch, assume_clean_state=False):
         """corilla/api.py:115-146."""
@@ -113,9 +121,10 @@ class IllumstatsCalculator(object):
         stats = OnlineStatistics(image_dimensions=first.dimensions[0:2],
                                  batch_size=self.batch_size)
         try:
-            for fid, img in self._images(file_ids):
-                logger.info("update statistics for image: %d", fid)
-                stats.update(img)
+            for ids, sites in self._blocks(file_ids):
+                for fid in ids:
+                    logger.info("update statistics for image: %d", fid)
+                stats.update_batch(sites)
             stats_file = self.store.illumstats_file(batch["channel_id"])
             logger.info("write calculated statistics to file")
             illumstats = IllumstatsContainer(stats.mean, stats.std, stats.percentiles)

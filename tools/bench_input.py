@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Input path: sites/s of gzip-HDF5 channel images
+decoded by the parallel inflate reader, and of IllumstatsCalculator.run_job
+(decode -> GPU statistics -> illumstats HDF5) end to end.
+
+Files are written first (synthetic 2160x2560 uint16, gzip level 4, h5py-style
+2-D chunks of 270x320 like the reference's DatasetWriter.write(compression=
+True) output).  Prints one JSON line.
+
+    python tools/bench_input.py --sites 64 --threads 16
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sites", type=int, default=64)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--width", type=int, default=2560)
+    ap.add_argument("--no-gpu", action="store_true")
+    a = ap.parse_args()
+    from tmlibrary_amd.models import file as h5
+    from tmlibrary_amd.synth import synth_sites_host
+    root = tempfile.mkdtemp(prefix="tmh_input_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        d = os.path.join(root, "channel_image_files")
+        os.makedirs(d)
+        sites = synth_sites_host(a.sites, a.height, a.width, seed=99)
+        paths = []
+        for i, s in enumerate(sites):
+            p = os.path.join(d, "channel_image_file_%d.h5" % i)
+            h5.write_channel_image(p, s, gzip_level=4, chunks=(270, 320))
+            paths.append(p)
+        res = {"sites": a.sites, "shape": [a.height, a.width],
+               "file_mb": round(os.path.getsize(paths[0]) / 1e6, 2)}
+        t0 = time.perf_counter()
+        for p in paths[:8]:
+            h5.read_channel_image(p)
+        res["serial_h5dread_sites_per_s"] = round(8 / (time.perf_counter() - t0), 1)
+        for nt in sorted({1, 4, a.threads}):
+            t0 = time.perf_counter()
+            out = h5.read_channel_images(paths, nt)
+            res["parallel_decode_%dt_sites_per_s" % nt] = round(a.sites / (time.perf_counter() - t0), 1)
+        assert np.array_equal(out, np.stack(sites))
+        if not a.no_gpu:
+            from tmlibrary_amd.models.file import ExperimentStore
+            from tmlibrary_amd.workflow.corilla.api import IllumstatsCalculator
+            store = ExperimentStore(root)
+            batch = {"id": 1, "channel_id": 1,
+                     "channel_image_files_ids": [[i] for i in range(a.sites)]}
+            calc = IllumstatsCalculator(1, store=store, batch_size=32, decode_threads=a.threads)
+            calc.run_job(batch)  # warm-up (library load, GPU init)
+            t0 = time.perf_counter()
+            calc.run_job(batch)
+            res["run_job_sites_per_s"] = round(a.sites / (time.perf_counter() - t0), 1)
+        res["cpus_visible"] = os.cpu_count()
+        res["threads"] = a.threads
+        print(json.dumps(res), flush=True)
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
