@@ -42,7 +42,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--sites", type=int, default=3456, help="sites per GPU (configs[1])")
+    p.add_argument("--sites", type=int, default=3456,
+                   help="sites per channel per GPU (configs[1]: 384 wells x 9 sites)")
+    p.add_argument("--channels", type=int, default=1,
+                   help="channels per GPU, each its own job on its own stream (configs[2]/[3]: 4)")
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--width", type=int, default=2560)
     p.add_argument("--cpu-sample", type=int, default=24,
@@ -160,57 +163,90 @@ def main():
     torch.cuda.set_stream(stream)
     sp = C.c_void_p(stream.cuda_stream)
 
-    # resident inputs / outputs (int16 tensors = raw uint16 bytes)
-    sites = torch.empty((S, H, W), dtype=torch.int16, device=dev)
+    # resident inputs / outputs (int16 tensors = raw uint16 bytes); channel c
+    # owns sites [c*S, (c+1)*S)
+    CH = a.channels
+    sites = torch.empty((CH * S, H, W), dtype=torch.int16, device=dev)
     out = torch.empty_like(sites)
-    hip.check(L.tmh_synth_sites_device(C.c_void_p(sites.data_ptr()), S, H, W, 12345, 0,
-                                       rank * S, sp))
-    mean = torch.empty(npx, dtype=torch.float64, device=dev)
-    std = torch.empty_like(mean)
-    smean = torch.empty_like(mean)
-    sstd = torch.empty_like(mean)
-    tmp = torch.empty_like(mean)
-
+    for c in range(CH):
+        hip.check(L.tmh_synth_sites_device(C.c_void_p(sites[c * S].data_ptr()), S, H, W, 12345, c,
+                                           rank * S, sp))
     lo, hi, gamma = quantile_table(npx, np.linspace(0, 100, Q))
     lut = stats_log10_lut()
     flags = hip.TMH_STATS_DEFERRED_PCT if dist_on else 0
     if a.serial_stats:
         flags |= hip.TMH_STATS_SERIAL
-    h = C.c_void_p()
-    hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma), hip.ptr(lut),
-                                 1, flags, C.byref(h)))
-    hip.check(L.tmh_stats_set_stream(h, sp))
-    corr = C.c_void_p()
-    torch.cuda.synchronize(dev)
-    hip.check(L.tmh_corrector_create_device(C.c_void_p(mean.data_ptr()), C.c_void_p(std.data_ptr()),
-                                            H, W, 1, ZERO_LOG10, sp, C.byref(corr)))
-    ops = StatsOps(L, h, npx, Q, dev)
-
     fused = a.pipeline == "fused"
-    S_ptr, O_ptr = C.c_void_p(sites.data_ptr()), C.c_void_p(out.data_ptr())
+
+    class Channel(object):
+        """One channel's job: its sites, statistics handle, corrector and
+        stream (channel 0 runs on the main stream; with several channels the
+        others overlap on their own streams, configs[2]/[3])."""
+
+        def __init__(self, c):
+            self.stream = stream if c == 0 else torch.cuda.Stream(dev)
+            self.sp = C.c_void_p(self.stream.cuda_stream)
+            self.S_ptr = C.c_void_p(sites[c * S].data_ptr())
+            self.O_ptr = C.c_void_p(out[c * S].data_ptr())
+            self.mean = torch.empty(npx, dtype=torch.float64, device=dev)
+            self.std = torch.empty_like(self.mean)
+            self.smean = torch.empty_like(self.mean)
+            self.sstd = torch.empty_like(self.mean)
+            self.tmp = torch.empty_like(self.mean)
+            self.h = C.c_void_p()
+            hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
+                                         hip.ptr(lut), 1, flags, C.byref(self.h)))
+            hip.check(L.tmh_stats_set_stream(self.h, self.sp))
+            self.corr = C.c_void_p()
+            torch.cuda.synchronize(dev)
+            hip.check(L.tmh_corrector_create_device(C.c_void_p(self.mean.data_ptr()),
+                                                    C.c_void_p(self.std.data_ptr()), H, W, 1,
+                                                    ZERO_LOG10, self.sp, C.byref(self.corr)))
+            self.ops = StatsOps(L, self.h, npx, Q, dev)
+
+        def stats(self):
+            hip.check(L.tmh_stats_reset(self.h))
+            if fused:  # Welford pass; histograms come from the correction's read
+                hip.check(L.tmh_stats_update_welford_device(self.h, self.S_ptr, S, 1, self.sp))
+            else:
+                hip.check(L.tmh_stats_update_device(self.h, self.S_ptr, S, 1, self.sp))
+
+        def apply(self):
+            p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+            hip.check(L.tmh_stats_finalize_device(self.h, p(self.mean), p(self.std), self.sp))
+            hip.check(L.tmh_smooth_f64_device(p(self.mean), p(self.smean), p(self.tmp), H, W, 5.0,
+                                              self.sp))
+            hip.check(L.tmh_smooth_f64_device(p(self.std), p(self.sstd), p(self.tmp), H, W, 5.0,
+                                              self.sp))
+            hip.check(L.tmh_corrector_update_device(self.corr, p(self.smean), p(self.sstd),
+                                                    self.sp))
+            if fused:
+                hip.check(L.tmh_correct_u16_hist_device(self.corr, self.h, self.S_ptr, self.O_ptr,
+                                                        S, -1, -1, self.sp))
+            else:
+                hip.check(L.tmh_correct_u16_device(self.corr, self.S_ptr, self.O_ptr, S, -1, -1,
+                                                   self.sp))
+
+        def close(self):
+            L.tmh_corrector_destroy(self.corr)
+            L.tmh_stats_destroy(self.h)
+
+    chans = [Channel(c) for c in range(CH)]
+    h, corr, S_ptr = chans[0].h, chans[0].corr, chans[0].S_ptr  # single-channel extras / check
 
     def step():
-        hip.check(L.tmh_stats_reset(h))
-        if fused:  # Welford pass; histograms come from the correction's read
-            hip.check(L.tmh_stats_update_welford_device(h, S_ptr, S, 1, sp))
-        else:
-            hip.check(L.tmh_stats_update_device(h, S_ptr, S, 1, sp))
+        for ch in chans:
+            ch.stats()
         if dist_on:
-            merge_welford(ops, dist)
-        hip.check(L.tmh_stats_finalize_device(h, C.c_void_p(mean.data_ptr()),
-                                              C.c_void_p(std.data_ptr()), sp))
-        hip.check(L.tmh_smooth_f64_device(C.c_void_p(mean.data_ptr()), C.c_void_p(smean.data_ptr()),
-                                          C.c_void_p(tmp.data_ptr()), H, W, 5.0, sp))
-        hip.check(L.tmh_smooth_f64_device(C.c_void_p(std.data_ptr()), C.c_void_p(sstd.data_ptr()),
-                                          C.c_void_p(tmp.data_ptr()), H, W, 5.0, sp))
-        hip.check(L.tmh_corrector_update_device(corr, C.c_void_p(smean.data_ptr()),
-                                                C.c_void_p(sstd.data_ptr()), sp))
-        if fused:
-            hip.check(L.tmh_correct_u16_hist_device(corr, h, S_ptr, O_ptr, S, -1, -1, sp))
-        else:
-            hip.check(L.tmh_correct_u16_device(corr, S_ptr, O_ptr, S, -1, -1, sp))
+            for ch in chans:
+                with torch.cuda.stream(ch.stream):
+                    merge_welford(ch.ops, dist)
+        for ch in chans:
+            ch.apply()
         if dist_on:
-            merge_percentiles(ops, dist)
+            for ch in chans:
+                with torch.cuda.stream(ch.stream):
+                    merge_percentiles(ch.ops, dist)
 
     for _ in range(a.warmup):
         step()
@@ -295,9 +331,9 @@ def main():
             roofline = {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                         "traffic": traffic, "alg_bytes_per_launch": alg[dominant]}
-        total_sites = world * S * a.steps
+        total_sites = world * CH * S * a.steps
         value = total_sites / elapsed
-        job_bytes = world * S * 6 * npx  # 6 B/px algorithmic per site-image
+        job_bytes = world * CH * S * 6 * npx  # 6 B/px algorithmic per site-image
         res = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -312,9 +348,12 @@ def main():
             "dtype": "f64",
             "data": "synthetic (device counter-hash generator, SURVEY.md §8(d) distribution), "
                     "resident in HBM",
-            "config": {"workload": "illumstats+correct, 1 channel, %d sites/GPU of %dx%d uint16 "
-                                   "(configs[1]: 384 wells x 9 sites)" % (S, H, W),
-                       "sites_per_gpu": S, "height": H, "width": W, "decimals": 3,
+            "config": {"workload": ("illumstats+correct, 1 channel, %d sites/GPU of %dx%d uint16 "
+                                    "(configs[1]: 384 wells x 9 sites)" % (S, H, W)) if CH == 1
+                       else ("illumstats+correct, %d channels x %d sites/GPU of %dx%d uint16, "
+                             "one job per channel on its own stream" % (CH, S, H, W)),
+                       "sites_per_gpu": CH * S, "channels": CH, "height": H, "width": W,
+                       "decimals": 3,
                        "smoothing_sigma": 5, "clip": None,
                        "parallelism": "sites sharded (contiguous); RCCL all-reduce Welford "
                                       "merge + ordered percentile chain" if world > 1
@@ -333,8 +372,8 @@ def main():
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
 
-    L.tmh_corrector_destroy(corr)
-    L.tmh_stats_destroy(h)
+    for ch in chans:
+        ch.close()
     if dist_on:
         dist.destroy_process_group()
 
