@@ -129,6 +129,13 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t n) {
 typedef float f32x2c_t __attribute__((ext_vector_type(2)));
 constexpr int kChainDepth = 4;
 
+// streamed-once site loads: non-temporal
+__device__ __forceinline__ uint4 ld_nt16(const uint4* p) {
+  typedef unsigned int u32x4n_t __attribute__((ext_vector_type(4)));
+  const u32x4n_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4n_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 template <bool LOG, bool LUT>
 __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ in,
                                                    uint8_t* __restrict__ out, int H, int W,
@@ -179,12 +186,12 @@ __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ i
   uint4 q[kChainDepth];
 #pragma unroll
   for (int k = 0; k < kChainDepth; ++k)
-    q[k] = live && s0 + k < s1 ? src[(s0 + k) * ngroups] : make_uint4(0, 0, 0, 0);
+    q[k] = live && s0 + k < s1 ? ld_nt16(src + (s0 + k) * ngroups) : make_uint4(0, 0, 0, 0);
   for (int64_t s = s0; s < s1; ++s) {
     const uint4 cur = q[0];
 #pragma unroll
     for (int k = 0; k + 1 < kChainDepth; ++k) q[k] = q[k + 1];
-    q[kChainDepth - 1] = live && s + kChainDepth < s1 ? src[(s + kChainDepth) * ngroups]
+    q[kChainDepth - 1] = live && s + kChainDepth < s1 ? ld_nt16(src + (s + kChainDepth) * ngroups)
                                                       : make_uint4(0, 0, 0, 0);
     const tmh_window w = win[s];  // uniform: scalar loads
     const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};

@@ -122,7 +122,16 @@ struct WfMerge {
 // blockIdx.y = site part: part p covers sites [p * per, min((p + 1) * per, n));
 // with more than one part each writes its (mean_l, M2_l) to `part` planes and
 // k_wf_merge_parts folds them in part order.
-template <bool LOG>
+// site loads: NTL = non-temporal (streamed once, kept out of L2's way)
+template <bool NTL>
+__device__ __forceinline__ uint4 ld_site(const uint4* p) {
+  if (!NTL) return *p;
+  typedef unsigned int u32x4w_t __attribute__((ext_vector_type(4)));
+  const u32x4w_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4w_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <bool LOG, bool NTL = true>
 __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
     const uint16_t* __restrict__ sites, int64_t npx, int64_t n_total, int64_t per,
     const WfMerge mg, double* __restrict__ mean, double* __restrict__ m2,
@@ -143,7 +152,7 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
   // current group is folded in (tail loads clamp to the last site: harmless)
   uint4 cur[kWfGroup], nxt[kWfGroup];
 #pragma unroll
-  for (int k = 0; k < kWfGroup; ++k) cur[k] = src[(k < last ? k : last) * ngroups];
+  for (int k = 0; k < kWfGroup; ++k) cur[k] = ld_site<NTL>(src + (k < last ? k : last) * ngroups);
   double K[8], s1[8], s2[8];
   xform8<LOG>(cur[0], slut, K);
 #pragma unroll
@@ -152,7 +161,7 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
 #pragma unroll
     for (int k = 0; k < kWfGroup; ++k) {
       const int64_t t = s + kWfGroup + k;
-      nxt[k] = src[(t < last ? t : last) * ngroups];
+      nxt[k] = ld_site<NTL>(src + (t < last ? t : last) * ngroups);
     }
 #pragma unroll
     for (int k = 0; k < kWfGroup; ++k) {
@@ -748,13 +757,13 @@ __global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint32_t* __restr
   const int64_t last = n_sites - 1;
   uint32_t v[kPctUnroll];
 #pragma unroll
-  for (int k = 0; k < kPctUnroll; ++k) v[k] = p[(k < last ? k : last) * ld];
+  for (int k = 0; k < kPctUnroll; ++k) v[k] = __builtin_nontemporal_load(p + (k < last ? k : last) * ld);
   for (int64_t s = 0; s < n_sites; s += kPctUnroll) {
     uint32_t vn[kPctUnroll];
 #pragma unroll
     for (int k = 0; k < kPctUnroll; ++k) {
       const int64_t t = s + kPctUnroll + k < last ? s + kPctUnroll + k : last;
-      vn[k] = p[t * ld];
+      vn[k] = __builtin_nontemporal_load(p + t * ld);
     }
 #pragma unroll
     for (int k = 0; k < kPctUnroll; ++k)

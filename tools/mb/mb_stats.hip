@@ -466,6 +466,24 @@ int main(int argc, char** argv) {
     }
   }
 
+  {  // non-temporal site loads A/B (one part, same grid as production's parts)
+    const int64_t ng = npx >> 3;
+    const int64_t per = cdiv(S, 3);
+    const dim3 grid((unsigned)cdiv(ng, 256), 3);
+    WfMerge mg{1.0 / S, 1.0, 0.0, 1};
+    for (int v = 0; v < 2; ++v)
+      for (int r = 0; r < reps; ++r) {
+        t.start();
+        if (v)
+          hipLaunchKernelGGL((k_welford_vec8<true, true>), grid, dim3(256), 0, 0, sites, npx, S, per,
+                             mg, mean, m2, lut, wpart);
+        else
+          hipLaunchKernelGGL((k_welford_vec8<true, false>), grid, dim3(256), 0, 0, sites, npx, S,
+                             per, mg, mean, m2, lut, wpart);
+        report(v ? "welford kernel 3 parts, nt loads" : "welford kernel 3 parts, plain loads",
+               t.stop(), S * site_gb);
+      }
+  }
   if (getenv("MB_WF")) {
     const dim3 gr((unsigned)cdiv(npx / 8, 256));
     auto runw = [&](auto kern, const char* name) {
