@@ -250,6 +250,17 @@ __device__ __forceinline__ uint32_t correct1(uint32_t u, const float4 c, const f
   return correct_l<LOG, BITS>(l.x, l.y, c, mh, ml, clip_lo, clip_hi);
 }
 
+// streamed-once site data: non-temporal loads / stores
+typedef unsigned int u32x4a_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt_u4(const uint4* p) {
+  const u32x4a_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4a_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt_u4(uint4* p, uint4 v) {
+  const u32x4a_t w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4a_t*>(p));
+}
+
 constexpr int kCorrThreads = 256;
 constexpr int kCorrGroup = 4;  // sites per pipeline stage (two stages in flight)
 
@@ -301,16 +312,16 @@ __global__ __launch_bounds__(kCorrThreads) void k_correct_u16_vec8(
   const int64_t last = n_sites - 1;
   uint4 cur[kCorrGroup], nxt[kCorrGroup];
 #pragma unroll
-  for (int k = 0; k < kCorrGroup; ++k) cur[k] = src[(k < last ? k : last) * ngroups];
+  for (int k = 0; k < kCorrGroup; ++k) cur[k] = ld_nt_u4(src + (k < last ? k : last) * ngroups);
   for (int64_t s = 0; s < n_sites; s += kCorrGroup) {
 #pragma unroll
     for (int k = 0; k < kCorrGroup; ++k) {
       const int64_t t = s + kCorrGroup + k;
-      nxt[k] = src[(t < last ? t : last) * ngroups];
+      nxt[k] = ld_nt_u4(src + (t < last ? t : last) * ngroups);
     }
 #pragma unroll
     for (int k = 0; k < kCorrGroup; ++k)
-      if (s + k < n_sites) dst[(s + k) * ngroups] = one(cur[k]);
+      if (s + k < n_sites) st_nt_u4(dst + (s + k) * ngroups, one(cur[k]));
 #pragma unroll
     for (int k = 0; k < kCorrGroup; ++k) cur[k] = nxt[k];
   }

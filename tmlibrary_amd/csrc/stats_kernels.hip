@@ -621,14 +621,15 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
     const int64_t n16 = npx >> 3;
     int64_t i = tid;
     for (; i + 3 * kHistThreads < n16; i += 4 * kHistThreads) {
-      const uint4 v0 = src[i], v1 = src[i + kHistThreads], v2 = src[i + 2 * kHistThreads],
-                  v3 = src[i + 3 * kHistThreads];
+      const uint4 v0 = ld_site<true>(src + i), v1 = ld_site<true>(src + i + kHistThreads),
+                  v2 = ld_site<true>(src + i + 2 * kHistThreads),
+                  v3 = ld_site<true>(src + i + 3 * kHistThreads);
       count8(v0, bins, himask, hhi);
       count8(v1, bins, himask, hhi);
       count8(v2, bins, himask, hhi);
       count8(v3, bins, himask, hhi);
     }
-    for (; i < n16; i += kHistThreads) count8(src[i], bins, himask, hhi);
+    for (; i < n16; i += kHistThreads) count8(ld_site<true>(src + i), bins, himask, hhi);
   } else {
     for (int64_t i = tid; i < npx; i += kHistThreads) {
       const uint32_t u = site[i];
