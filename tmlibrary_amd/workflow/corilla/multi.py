@@ -1,0 +1,113 @@
+"""corilla as ONE multi-GPU job over all channels.
+
+The reference schedules one single-process GC3Pie job per channel
+(tmlib/workflow/corilla/api.py:45-105 ``create_run_batches``, :115-146
+``run_job``) and the site order inside a channel is whatever the database
+query returns.  Here every rank of one ``torchrun`` job walks the same list of
+channel batches (``IllumstatsCalculator.create_run_batches`` order) and, per
+channel:
+
+1. takes the contiguous block ``shard_bounds(n, world, rank)`` of the batch's
+   file list -- the list itself is the recorded site order, so the merged
+   result is the reference's sequential result over that order;
+2. decodes its block with the parallel inflate reader and accumulates it
+   (``update_batch``);
+3. merges the partial statistics (Welford all-reduce + ordered percentile
+   chain, ``sharded.merge_shards``), so every rank holds identical results;
+4. rank 0 writes the ``IllumstatsFile`` (4-dataset HDF5 layout).
+
+The per-channel statistics object is pluggable (``stats_factory``): the
+default runs on the GPU through libtmhip; tests plug a CPU double in to check
+the orchestration (tests/test_multi_job.py).
+"""
+from __future__ import annotations
+
+import logging
+
+import numpy as np
+
+from tmlibrary_amd.image import IllumstatsContainer
+from tmlibrary_amd.models.file import read_channel_images
+from tmlibrary_amd.workflow.corilla.sharded import merge_shards, shard_bounds
+
+logger = logging.getLogger(__name__)
+
+
+class GpuChannelStats(object):
+    """One rank's share of one channel on the GPU: ``OnlineStatistics`` in
+    deferred-percentile mode + ``StatsOps`` for the merge."""
+
+    def __init__(self, image_dimensions, world, device=None, batch_size=32, merge_single=False):
+        from tmlibrary_amd import hip
+        from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
+        # merge_single: run the deferred-percentile merge path even with one
+        # rank (exercises the multi-GPU code on a one-GPU box)
+        self.merging = world > 1 or merge_single
+        flags = hip.TMH_STATS_DEFERRED_PCT if self.merging else 0
+        self.st = OnlineStatistics(image_dimensions, batch_size=batch_size, flags=flags)
+        self.world = world
+        self.device = device
+
+    def update_batch(self, sites):
+        self.st.update_batch(sites)
+
+    def merge(self, dist, group=None):
+        if not self.merging or dist is None:
+            return self.st.n
+        import torch
+        from tmlibrary_amd import hip
+        from tmlibrary_amd.workflow.corilla.sharded import StatsOps
+        st = self.st
+        st._flush()
+        h, w = st.image_dimensions
+        dev = self.device if self.device is not None else torch.device("cuda",
+                                                                         torch.cuda.current_device())
+        ops = StatsOps(hip.lib(), st._h, h * w, len(st._q), dev)
+        n_total = merge_shards(ops, dist, group, int_device=dev)
+        torch.cuda.current_stream(dev).synchronize()
+        st._n_flushed = n_total  # the merged state is the whole channel's
+        st._cache = None
+        return n_total
+
+    def container(self):
+        return IllumstatsContainer(self.st.mean, self.st.std, self.st.percentiles)
+
+    def close(self):
+        self.st.close()
+
+
+def run_channels_sharded(store, batches, dist=None, group=None, stats_factory=None,
+                         block=32, decode_threads=None, device=None):
+    """Run every channel batch as one sharded job; returns {channel_id:
+    IllumstatsContainer} (identical on every rank).  ``dist`` is
+    torch.distributed (or None for one process)."""
+    world = dist.get_world_size(group) if dist is not None else 1
+    rank = dist.get_rank(group) if dist is not None else 0
+    if stats_factory is None:
+        def stats_factory(dims):
+            return GpuChannelStats(dims, world, device=device, batch_size=block)
+    results = {}
+    for batch in batches:
+        ids = [f[0] if isinstance(f, (list, tuple)) else f
+               for f in batch["channel_image_files_ids"]]
+        paths = [store.channel_image_file(i).location for i in ids]
+        first = read_channel_images(paths[:1], 1)
+        dims = first.shape[1:]
+        a, b = shard_bounds(len(paths), world, rank)
+        logger.info("channel %s: rank %d of %d takes sites [%d, %d) of %d",
+                    batch["channel_id"], rank, world, a, b, len(paths))
+        stats = stats_factory(dims)
+        try:
+            for i in range(a, b, block):
+                sites = read_channel_images(paths[i:min(b, i + block)], decode_threads)
+                if sites.dtype == np.uint8:
+                    sites = sites.astype(np.uint16)
+                stats.update_batch(sites)
+            stats.merge(dist, group)
+            cont = stats.container()
+        finally:
+            stats.close()
+        if rank == 0:
+            store.illumstats_file(batch["channel_id"]).put(cont)
+        results[batch["channel_id"]] = cont
+    return results
