@@ -11,6 +11,8 @@
 // hi/lo LUT (|err| ~1e-14) staged in LDS, the affine step runs in f32
 // keeping (L - mean) exact to ~1e-7, and 10**t is one v_exp_f32: |rel err|
 // < 1e-6, i.e. < 0.07 DN at 65535 (tolerance +-1 DN).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace tmh {
@@ -102,13 +104,22 @@ void launch_smooth(const double* in, double* out, double* tmp, int H, int W, con
                    int radius, hipStream_t s) {
   ProfScope prof("smooth", s);
   const dim3 grid((unsigned)cdiv(W, 256), (unsigned)H);
-  constexpr int kStrip = 32;
-  if (radius == 20)  // sigma = 5, the reference's default (image.py:1172)
-    hipLaunchKernelGGL((k_smooth_axis0_strip<kStrip, 20>),
-                       dim3((unsigned)cdiv(W, 256), (unsigned)cdiv(H, kStrip)), dim3(256), 0, s, in,
-                       tmp, H, W, d_w);
-  else
+  static const int strip = [] {  // rows per thread of the axis-0 pass (TMH_SMOOTH_STRIP)
+    const char* e = getenv("TMH_SMOOTH_STRIP");
+    const int v = e ? atoi(e) : 16;  // 16: 1,350 workgroups at 2160x2560 (measured best)
+    return (v == 8 || v == 16 || v == 32) ? v : 16;
+  }();
+  if (radius == 20) {  // sigma = 5, the reference's default (image.py:1172)
+    const dim3 g2((unsigned)cdiv(W, 256), (unsigned)cdiv(H, strip));
+    if (strip == 8)
+      hipLaunchKernelGGL((k_smooth_axis0_strip<8, 20>), g2, dim3(256), 0, s, in, tmp, H, W, d_w);
+    else if (strip == 16)
+      hipLaunchKernelGGL((k_smooth_axis0_strip<16, 20>), g2, dim3(256), 0, s, in, tmp, H, W, d_w);
+    else
+      hipLaunchKernelGGL((k_smooth_axis0_strip<32, 20>), g2, dim3(256), 0, s, in, tmp, H, W, d_w);
+  } else {
     hipLaunchKernelGGL(k_smooth_axis0, grid, dim3(256), 0, s, in, tmp, H, W, d_w, radius);
+  }
   if (radius <= kSmMaxR)
     hipLaunchKernelGGL(k_smooth_axis1, dim3((unsigned)cdiv(W, kSmTile), (unsigned)H), dim3(256), 0,
                        s, tmp, out, H, W, d_w, radius);
