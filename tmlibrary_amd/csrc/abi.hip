@@ -606,9 +606,8 @@ int tmh_smooth_f64(const double* host_in, double* host_out, int height, int widt
 static void corrector_coeffs(tmh_corrector* c, const double* d_mean, const double* d_std,
                              hipStream_t s) {
   ProfScope prof("coeffs", s);
-  const int np = 512;
-  launch_reduce_sum(d_std, c->npx, c->partial.p, np, c->sums.p, s);
-  launch_reduce_sum(d_mean, c->npx, c->partial.p, np, c->sums.p + 1, s);
+  const int np = 1024;
+  launch_reduce_sum2(d_std, d_mean, c->npx, c->partial.p, np, c->sums.p, s);
   launch_coeffs(d_mean, d_std, c->sums.p, c->npx, c->coef.p, c->mconst.p, s);
   launch_coeffs2(d_mean, d_std, c->sums.p, c->npx, c->log_transform, c->zero_log10, c->coef2.p,
                  c->mconst2.p, c->coef_lin.p, s);
@@ -616,7 +615,7 @@ static void corrector_coeffs(tmh_corrector* c, const double* d_mean, const doubl
 
 static void corrector_init(tmh_corrector* c, const double* d_mean, const double* d_std) {
   c->sums.alloc(2);
-  c->partial.alloc(512);
+  c->partial.alloc(2 * 1024);
   c->coef.alloc(c->npx);
   c->coef2.alloc(c->npx);
   c->coef_lin.alloc(c->npx);

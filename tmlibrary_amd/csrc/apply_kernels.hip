@@ -163,6 +163,39 @@ __global__ __launch_bounds__(256) void k_reduce_final(const double* __restrict__
   if (threadIdx.x == 0) *out = t;
 }
 
+// sums of two planes at once (np.mean(std), np.mean(mean) of image.py:627):
+// blockIdx.y selects the plane, fixed partition -> deterministic
+__global__ __launch_bounds__(256) void k_reduce_partial2(const double* __restrict__ x0,
+                                                         const double* __restrict__ x1, int64_t n,
+                                                         double* __restrict__ partial) {
+  __shared__ double red[256];
+  const double* x = blockIdx.y ? x1 : x0;
+  const int64_t chunk = cdiv(n, gridDim.x);
+  const int64_t b = (int64_t)blockIdx.x * chunk;
+  const int64_t e = (b + chunk < n) ? b + chunk : n;
+  double acc = 0.0;
+  for (int64_t i = b + threadIdx.x; i < e; i += 256) acc += x[i];
+  const double t = block_sum256(acc, red);
+  if (threadIdx.x == 0) partial[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void k_reduce_final2(const double* __restrict__ partial, int n,
+                                                       double* __restrict__ out) {
+  __shared__ double red[256];
+  const double* p = partial + (int64_t)blockIdx.x * n;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) acc += p[i];
+  const double t = block_sum256(acc, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = t;
+}
+
+void launch_reduce_sum2(const double* x0, const double* x1, int64_t n, double* partial,
+                        int n_partial, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_partial2, dim3(n_partial, 2), dim3(256), 0, s, x0, x1, n, partial);
+  hipLaunchKernelGGL(k_reduce_final2, dim3(2), dim3(256), 0, s, partial, n_partial, out);
+  TMH_HIP(hipGetLastError());
+}
+
 void launch_reduce_sum(const double* x, int64_t n, double* partial, int n_partial, double* out,
                        hipStream_t s) {
   hipLaunchKernelGGL(k_reduce_partial, dim3(n_partial), dim3(256), 0, s, x, n, partial);

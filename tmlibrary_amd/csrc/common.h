@@ -89,6 +89,9 @@ void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s);
 
 void launch_smooth(const double* in, double* out, double* tmp, int H, int W, const double* d_w,
                    int radius, hipStream_t s);
+// out[0] = sum(x0), out[1] = sum(x1); partial holds 2 * n_partial
+void launch_reduce_sum2(const double* x0, const double* x1, int64_t n, double* partial,
+                        int n_partial, double* out, hipStream_t s);
 void launch_reduce_sum(const double* x, int64_t n, double* partial, int n_partial, double* out,
                        hipStream_t s);
 void launch_build_corr_lut(float2* lut, int log_transform, double zero_log10, hipStream_t s);
