@@ -133,6 +133,39 @@ def bench_chain(L, corr, S_ptr, S, H, W, dev, sp, reps=3):
             "frac_of_8TBs": round(alg / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def bench_host_path(H, W, n_sites=64, reps=3):
+    """PCIe-inclusive rate of the drop-in host-buffer path (SURVEY §8(d) C5
+    note; never the headline): numpy sites in host memory through
+    OnlineStatistics.update_batch (tmh_stats_update) and Corrector.apply
+    (tmh_correct_u16), double-buffered device slots on copy streams."""
+    from tmlibrary_amd.image import Corrector
+    from tmlibrary_amd.synth import synth_sites_host
+    from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
+    sites = np.ascontiguousarray(np.stack(synth_sites_host(n_sites, H, W, seed=7)))
+    st = OnlineStatistics((H, W), batch_size=32)
+    st.update_batch(sites)  # warm-up: both pinned and device slots allocated
+    corr = Corrector(st.mean.array, st.std.array)
+    corr.apply(sites)
+    t_stats = t_corr = 1e30
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        st.update_batch(sites)
+        t_stats = min(t_stats, time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        corr.apply(sites)
+        t_corr = min(t_corr, time.perf_counter() - t0)
+    st.close()
+    corr.close()
+    site_b = H * W * 2
+    return {"workload": "%d host (numpy, pageable) sites of %dx%d: stats update (H2D 2 B/px) then "
+                        "correct (H2D + D2H 4 B/px), PCIe-inclusive" % (n_sites, H, W),
+            "stats_sites_per_s": round(n_sites / t_stats, 1),
+            "stats_h2d_GBs": round(n_sites * site_b / t_stats / 1e9, 1),
+            "correct_sites_per_s": round(n_sites / t_corr, 1),
+            "correct_pcie_GBs": round(2 * n_sites * site_b / t_corr / 1e9, 1),
+            "job_sites_per_s": round(n_sites / (t_stats + t_corr), 1)}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -296,6 +329,7 @@ def main():
     extras = {}
     if not a.no_extras and world == 1:
         extras["chain_u8"] = bench_chain(L, corr, S_ptr, S, H, W, dev, sp)
+        extras["host_path"] = bench_host_path(H, W)
 
     if rank == 0:
         site_bytes = npx * 2
