@@ -137,10 +137,16 @@ struct PinBuf {
 };
 
 // memcpy between pageable and pinned host memory, split over a few threads
-// (one thread moves ~10 GB/s, well below a PCIe 5 x16 link).
+// (TMH_COPY_THREADS, default 8): one thread moves <= 30 GB/s and much less
+// into a fresh (unfaulted) numpy output, below a PCIe 5 x16 link.
 static void par_copy(void* dst, const void* src, size_t bytes) {
   const size_t min_part = (size_t)4 << 20;
-  size_t nt = std::min<size_t>(8, std::max<size_t>(1, bytes / min_part));
+  static const size_t max_t = [] {
+    const char* e = std::getenv("TMH_COPY_THREADS");
+    const long v = e ? std::strtol(e, nullptr, 10) : 8;
+    return (size_t)std::min(64L, std::max(1L, v));
+  }();
+  size_t nt = std::min<size_t>(max_t, std::max<size_t>(1, bytes / min_part));
   nt = std::min<size_t>(nt, std::max(1u, std::thread::hardware_concurrency()));
   if (nt <= 1) {
     std::memcpy(dst, src, bytes);
