@@ -72,3 +72,19 @@ def test_correct_u16_pipelined(n):
     clipped = corr.apply(sites, clip=(120, 3000))
     assert np.array_equal(clipped, np.clip(got, 120, 3000))
     corr.close()
+
+
+def test_correct_into_out_buffer():
+    from tmlibrary_amd.image import Corrector
+    sites = _sites(20, seed=13)
+    rng = np.random.default_rng(6)
+    corr = Corrector(2.0 + rng.random(sites.shape[1:]), 0.1 + 0.05 * rng.random(sites.shape[1:]))
+    want = corr.apply(sites)
+    out = np.full_like(sites, 7)
+    assert corr.apply(sites, out=out) is out
+    assert np.array_equal(out, want)
+    with pytest.raises(ValueError):
+        corr.apply(sites, out=np.empty((20, 40, 55), np.uint16))
+    with pytest.raises(ValueError):
+        corr.apply(sites, out=sites)
+    corr.close()

@@ -316,14 +316,25 @@ class Corrector(object):
         hip.check(hip.lib().tmh_corrector_means(self._h, C.byref(a), C.byref(b)))
         return a.value, b.value
 
-    def apply(self, img: np.ndarray, clip=None) -> np.ndarray:
-        """Correct one image [H,W] or a stack [n,H,W] (uint8/uint16)."""
+    def apply(self, img: np.ndarray, clip=None, out=None) -> np.ndarray:
+        """Correct one image [H,W] or a stack [n,H,W] (uint8/uint16).
+
+        ``out``: optional C-contiguous array of the same shape and dtype to
+        write into (a reused buffer skips the first-touch page faults of a
+        fresh result, which bound the host path's rate)."""
         img = np.asarray(img)
         if img.shape[-2:] != self.shape:
             raise ValueError("operands could not be broadcast together with shapes %s %s"
                              % (img.shape, self.shape))
         a = np.ascontiguousarray(img)
-        out = np.empty_like(a)
+        if out is None:
+            out = np.empty_like(a)
+        elif (not isinstance(out, np.ndarray) or out.shape != a.shape or out.dtype != a.dtype
+              or not out.flags.c_contiguous or not out.flags.writeable):
+            raise ValueError("out must be a writeable C-contiguous %s array of shape %s"
+                             % (a.dtype, a.shape))
+        elif np.shares_memory(out, a):
+            raise ValueError("out must not overlap the input")
         n = 1 if a.ndim == 2 else int(np.prod(a.shape[:-2]))
         lo, hi = (-1, -1) if clip is None else (int(clip[0]), int(clip[1]))
         L = hip.lib()
