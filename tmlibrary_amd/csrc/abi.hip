@@ -195,6 +195,14 @@ struct HostPipe {
       TMH_HIP(hipEventCreateWithFlags(&ev_done[i], hipEventDisableTiming));
     }
   }
+  // after an error mid-call: let queued work finish, forget the chunks (their
+  // host destinations belong to the failed call)
+  void abandon(hipStream_t compute) {
+    if (h2d) (void)hipStreamSynchronize(h2d);
+    if (d2h) (void)hipStreamSynchronize(d2h);
+    if (compute) (void)hipStreamSynchronize(compute);
+    busy[0] = busy[1] = false;
+  }
   ~HostPipe() {
     if (!h2d) return;
     (void)hipStreamSynchronize(h2d);
@@ -511,33 +519,38 @@ int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites, 
       p.busy[slot] = false;
     };
     int64_t k = 0;
-    for (int64_t s0 = 0; s0 < n_sites; s0 += per, ++k) {
-      const int slot = (int)(k & 1);
-      const int64_t ns = std::min<int64_t>(per, n_sites - s0);
-      const size_t bytes = (size_t)ns * h->npx * 2;
-      retire(slot);
-      p.out[slot].ensure((size_t)per * 8);
-      const void* src = host_sites + s0 * h->npx;
-      if (pinned) {
-        p.in[slot].ensure(slot_px * 2);
-        par_copy(p.in[slot].p, src, bytes);
-        src = p.in[slot].p;
+    try {
+      for (int64_t s0 = 0; s0 < n_sites; s0 += per, ++k) {
+        const int slot = (int)(k & 1);
+        const int64_t ns = std::min<int64_t>(per, n_sites - s0);
+        const size_t bytes = (size_t)ns * h->npx * 2;
+        retire(slot);
+        p.out[slot].ensure((size_t)per * 8);
+        const void* src = host_sites + s0 * h->npx;
+        if (pinned) {
+          p.in[slot].ensure(slot_px * 2);
+          par_copy(p.in[slot].p, src, bytes);
+          src = p.in[slot].p;
+        }
+        uint16_t* dev = h->stage.p + (size_t)slot * slot_px;
+        TMH_HIP(hipMemcpyAsync(dev, src, bytes, hipMemcpyHostToDevice, p.h2d));
+        TMH_HIP(hipEventRecord(p.ev_in[slot], p.h2d));
+        TMH_HIP(hipStreamWaitEvent(h->stream, p.ev_in[slot], 0));
+        stats_update_dev(h, dev, ns, log_transform, h->stream);
+        if (zero_counts_out)
+          TMH_HIP(hipMemcpyAsync(p.out[slot].p, h->zeros.p, (size_t)ns * 8, hipMemcpyDeviceToHost,
+                                 h->stream));
+        TMH_HIP(hipEventRecord(p.ev_done[slot], h->stream));
+        p.busy[slot] = true;
+        p.s0[slot] = s0;
+        p.ns[slot] = ns;
       }
-      uint16_t* dev = h->stage.p + (size_t)slot * slot_px;
-      TMH_HIP(hipMemcpyAsync(dev, src, bytes, hipMemcpyHostToDevice, p.h2d));
-      TMH_HIP(hipEventRecord(p.ev_in[slot], p.h2d));
-      TMH_HIP(hipStreamWaitEvent(h->stream, p.ev_in[slot], 0));
-      stats_update_dev(h, dev, ns, log_transform, h->stream);
-      if (zero_counts_out)
-        TMH_HIP(hipMemcpyAsync(p.out[slot].p, h->zeros.p, (size_t)ns * 8, hipMemcpyDeviceToHost,
-                               h->stream));
-      TMH_HIP(hipEventRecord(p.ev_done[slot], h->stream));
-      p.busy[slot] = true;
-      p.s0[slot] = s0;
-      p.ns[slot] = ns;
+      retire((int)(k & 1));
+      retire((int)((k + 1) & 1));
+    } catch (...) {
+      p.abandon(h->stream);
+      throw;
     }
-    retire((int)(k & 1));
-    retire((int)((k + 1) & 1));
   });
 }
 
@@ -871,39 +884,44 @@ int tmh_correct_u16(tmh_corrector* c, const uint16_t* host_in, uint16_t* host_ou
       p.busy[slot] = false;
     };
     int64_t k = 0;
-    for (int64_t s0 = 0; s0 < n_sites; s0 += step, ++k) {
-      const int slot = (int)(k & 1);
-      const int64_t ns = std::min(step, n_sites - s0);
-      const size_t bytes = (size_t)ns * c->npx * 2;
-      retire(slot);  // chunk k-2: output copied out, both slot buffers free
-      const void* src = host_in + s0 * c->npx;
-      void* dst = host_out + s0 * c->npx;
-      if (pinned_in) {
-        p.in[slot].ensure(slot_px * 2);
-        par_copy(p.in[slot].p, src, bytes);
-        src = p.in[slot].p;
+    try {
+      for (int64_t s0 = 0; s0 < n_sites; s0 += step, ++k) {
+        const int slot = (int)(k & 1);
+        const int64_t ns = std::min(step, n_sites - s0);
+        const size_t bytes = (size_t)ns * c->npx * 2;
+        retire(slot);  // chunk k-2: output copied out, both slot buffers free
+        const void* src = host_in + s0 * c->npx;
+        void* dst = host_out + s0 * c->npx;
+        if (pinned_in) {
+          p.in[slot].ensure(slot_px * 2);
+          par_copy(p.in[slot].p, src, bytes);
+          src = p.in[slot].p;
+        }
+        if (pinned_out) {
+          p.out[slot].ensure(slot_px * 2);
+          dst = p.out[slot].p;
+        }
+        uint16_t* din = c->stage_in.p + (size_t)slot * slot_px;
+        uint16_t* dout = c->stage_out.p + (size_t)slot * slot_px;
+        TMH_HIP(hipMemcpyAsync(din, src, bytes, hipMemcpyHostToDevice, p.h2d));
+        TMH_HIP(hipEventRecord(p.ev_in[slot], p.h2d));
+        TMH_HIP(hipStreamWaitEvent(c->stream, p.ev_in[slot], 0));
+        launch_correct_u16(din, dout, c->npx, ns, c->coef.p, c->lut.p, c->mconst.p, c->log_transform,
+                           clip_lo, clip_hi, c->stream);
+        TMH_HIP(hipEventRecord(p.ev_kern[slot], c->stream));
+        TMH_HIP(hipStreamWaitEvent(p.d2h, p.ev_kern[slot], 0));
+        TMH_HIP(hipMemcpyAsync(dst, dout, bytes, hipMemcpyDeviceToHost, p.d2h));
+        TMH_HIP(hipEventRecord(p.ev_done[slot], p.d2h));
+        p.busy[slot] = true;
+        p.s0[slot] = s0;
+        p.ns[slot] = ns;
       }
-      if (pinned_out) {
-        p.out[slot].ensure(slot_px * 2);
-        dst = p.out[slot].p;
-      }
-      uint16_t* din = c->stage_in.p + (size_t)slot * slot_px;
-      uint16_t* dout = c->stage_out.p + (size_t)slot * slot_px;
-      TMH_HIP(hipMemcpyAsync(din, src, bytes, hipMemcpyHostToDevice, p.h2d));
-      TMH_HIP(hipEventRecord(p.ev_in[slot], p.h2d));
-      TMH_HIP(hipStreamWaitEvent(c->stream, p.ev_in[slot], 0));
-      launch_correct_u16(din, dout, c->npx, ns, c->coef.p, c->lut.p, c->mconst.p, c->log_transform,
-                         clip_lo, clip_hi, c->stream);
-      TMH_HIP(hipEventRecord(p.ev_kern[slot], c->stream));
-      TMH_HIP(hipStreamWaitEvent(p.d2h, p.ev_kern[slot], 0));
-      TMH_HIP(hipMemcpyAsync(dst, dout, bytes, hipMemcpyDeviceToHost, p.d2h));
-      TMH_HIP(hipEventRecord(p.ev_done[slot], p.d2h));
-      p.busy[slot] = true;
-      p.s0[slot] = s0;
-      p.ns[slot] = ns;
+      retire((int)(k & 1));
+      retire((int)((k + 1) & 1));
+    } catch (...) {
+      p.abandon(c->stream);
+      throw;
     }
-    retire((int)(k & 1));
-    retire((int)((k + 1) & 1));
   });
 }
 
