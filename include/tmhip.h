@@ -80,7 +80,9 @@ int tmh_stats_reset(tmh_stats* h);
 
 /* update(image) for a run of sites.  zero_counts_out (host, n_sites, may be
  * NULL): per-site number of zero pixels, for the 'image contains zero
- * values' warning (stats.py:81-82); non-NULL forces a synchronisation. */
+ * values' warning (stats.py:81-82).  Host sites move in chunks of the
+ * handle's batch capacity through two device slots on a copy stream, so
+ * chunk k's H2D overlaps chunk k-1's kernels; returns when all are done. */
 int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites,
                      int log_transform, int64_t* zero_counts_out);
 int tmh_stats_update_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
@@ -177,6 +179,10 @@ int tmh_corrector_update_device(tmh_corrector* c, const double* dev_mean, const 
                                 void* stream);
 /* The two global means (np.mean(std), np.mean(mean), image.py:627). */
 int tmh_corrector_means(tmh_corrector* c, double* mean_of_std, double* mean_of_mean);
+/* Host buffers: chunks of <= 16 sites, H2D / kernel / D2H on three streams
+ * with two device and two pinned output slots (TMH_HOST_STAGING=0: all
+ * direct, =1: inputs through pinned slots too).  Returns when host_out is
+ * complete; host_out must not overlap host_in. */
 int tmh_correct_u16(tmh_corrector* c, const uint16_t* host_in, uint16_t* host_out,
                     int64_t n_sites, int clip_lo, int clip_hi);
 int tmh_correct_u16_device(tmh_corrector* c, const uint16_t* dev_in, uint16_t* dev_out,
