@@ -243,6 +243,7 @@ struct tmh_stats {
   DBuf<int32_t> q_lo, q_hi;
   DBuf<unsigned long long> pooled, pooled_parts;  // parts: kPooledParts zero-maintained copies
   DBuf<uint32_t> hist_hi, site_hist, hist_full;
+  DBuf<unsigned long long> hist_rmask;  // per site: touched high rounds of hist_full
   QPos qp{};
   DBuf<uint16_t> stage;  // two device slots of batch_cap sites
   HostPipe pipe;
@@ -972,6 +973,7 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       int nch = env_chunks > 0 ? env_chunks : 1;
       nch = (int)std::min<int64_t>(nch, n_sites);
       const bool grow = (size_t)n_sites * kBins > h->hist_full.n || (size_t)n_sites > h->zeros.n ||
+                        (size_t)n_sites > h->hist_rmask.n ||
                         ((h->flags & 2u) && (size_t)n_sites * kBins > h->site_hist.n) ||
                         (!(h->flags & TMH_STATS_DEFERRED_PCT) &&
                          (size_t)n_sites * h->Q > h->vlh.n);
@@ -982,6 +984,7 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       }
       if ((size_t)n_sites * kBins > h->hist_full.n)
         h->hist_full.alloc((size_t)n_sites * kBins, true);
+      if ((size_t)n_sites > h->hist_rmask.n) h->hist_rmask.alloc((size_t)n_sites, true);
       h->zeros.ensure((size_t)n_sites);
       if (h->flags & 2u) h->site_hist.ensure((size_t)n_sites * kBins);
       uint32_t* vlh;
@@ -997,12 +1000,14 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         const int64_t c0 = n_sites * k / nch, nc = n_sites * (k + 1) / nch - c0;
         launch_correct_hist(dev_in + c0 * h->npx, dev_out + c0 * h->npx, c->npx, nc, c->coef2.p,
                             c->mconst2.p, c->log_transform, clip_lo, clip_hi,
-                            h->hist_full.p + (size_t)c0 * kBins, c->queues.p, c->n_wg, s);
+                            h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0,
+                            c->queues.p, c->n_wg, s);
         if (side != s) {
           TMH_HIP(hipEventRecord(h->ev_fork, s));
           TMH_HIP(hipStreamWaitEvent(side, h->ev_fork, 0));
         }
-        launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, nc, h->qp,
+        launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0,
+                             correct_hist_dense_rounds(), nc, h->qp,
                              vlh + (size_t)c0 * h->Q, h->pooled.p, h->pooled_parts.p,
                              kPooledParts, h->zeros.p + c0,
                              (h->flags & 2u) ? h->site_hist.p + (size_t)c0 * kBins : nullptr,

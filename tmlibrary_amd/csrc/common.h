@@ -70,7 +70,8 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
                          const QPos& p, uint32_t* vlh, unsigned long long* pooled,
                          int64_t* zero_counts, uint32_t* site_hist, hipStream_t s);
-void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const QPos& p, uint32_t* vlh,
+void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_rounds,
+                          int64_t n_sites, const QPos& p, uint32_t* vlh,
                           unsigned long long* pooled,
                           unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
                           uint32_t* site_hist, hipStream_t s);
@@ -105,8 +106,9 @@ void launch_correct_u8(const uint8_t* in, uint8_t* out, int64_t npx, int64_t n_s
                        int log_transform, int clip_lo, int clip_hi, hipStream_t s);
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, int log_transform,
-                         int clip_lo, int clip_hi, uint32_t* hist, int* queues, int n_wg,
-                         hipStream_t s);
+                         int clip_lo, int clip_hi, uint32_t* hist, unsigned long long* rmask,
+                         int* queues, int n_wg, hipStream_t s);
+int correct_hist_dense_rounds();
 void launch_coeffs2(const double* mean, const double* std, const double* sums, int64_t npx,
                     int log_transform, double zero_log10, float2* coef2, float4* mconst2,
                     float2* coef_lin, hipStream_t s);

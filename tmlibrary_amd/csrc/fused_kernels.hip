@@ -142,7 +142,8 @@ template <bool LOG, bool CLIP, int SPU, int ABL, int NT, int LB>
 __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void k_correct_hist(
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
     const float4* __restrict__ coef, const float4* __restrict__ mconst2, int clip_lo,
-    int clip_hi, uint32_t* __restrict__ hist, int* __restrict__ queues, int bands_per_xcd) {
+    int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
+    int* __restrict__ queues, int bands_per_xcd) {
   constexpr int BINS = LB / SPU;
   constexpr int SLICE = BINS + 1;
   constexpr uint32_t HIMASK = (0xFFFFu & ~(uint32_t)(BINS - 1)) * 0x00010001u;
@@ -242,12 +243,20 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
         }
         if ((w.x | w.y | w.z | w.w) & HIMASK) {  // rare: beyond this site's LDS slice
           uint32_t* h = hs + k * (int64_t)kBins;
+          unsigned long long rounds = 0ull;  // 1,024-bin rounds this site touches
 #pragma unroll
           for (int p = 0; p < 4; ++p) {
             const uint32_t lo = wd[p] & 0xFFFFu, hi = wd[p] >> 16;
-            if (lo >= (uint32_t)BINS) atomicAdd(&h[lo], 1u);
-            if (hi >= (uint32_t)BINS) atomicAdd(&h[hi], 1u);
+            if (lo >= (uint32_t)BINS) {
+              atomicAdd(&h[lo], 1u);
+              rounds |= 1ull << (lo >> 10);
+            }
+            if (hi >= (uint32_t)BINS) {
+              atomicAdd(&h[hi], 1u);
+              rounds |= 1ull << (hi >> 10);
+            }
           }
+          atomicOr(&rmask[un.s0 + k], rounds);
         }
       }
       uint32_t o[4];
@@ -316,10 +325,21 @@ static int fused_cfg() {
   return v;
 }
 
+// 1,024-bin rounds of every site's histogram that the current configuration
+// fills from its LDS slices (the rounds above are flagged in rmask per site)
+int correct_hist_dense_rounds() {
+  switch (fused_cfg()) {
+    case 0: return 32768 / 2 / 1024;
+    case 1: return 32768 / 4 / 1024;
+    case 2: return 16384 / 2 / 1024;
+    default: return 16384 / 4 / 1024;
+  }
+}
+
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, int log_transform,
-                         int clip_lo, int clip_hi, uint32_t* hist, int* queues, int n_wg,
-                         hipStream_t s) {
+                         int clip_lo, int clip_hi, uint32_t* hist, unsigned long long* rmask,
+                         int* queues, int n_wg, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("correct_hist", s);
   static const int bpx = [] {
@@ -333,11 +353,11 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
   if (clip_lo >= 0)                                                                              \
     hipLaunchKernelGGL((k_correct_hist<L_, true, S_, 0, T_, B_>), dim3(n_wg * (1024 / T_)),      \
                        dim3(T_), 0, s, in, out, npx, n_sites, cf4, mconst2, clip_lo, clip_hi,   \
-                       hist, queues, bpx);                                                       \
+                       hist, rmask, queues, bpx);                                                \
   else                                                                                           \
     hipLaunchKernelGGL((k_correct_hist<L_, false, S_, 0, T_, B_>), dim3(n_wg * (1024 / T_)),     \
                        dim3(T_), 0, s, in, out, npx, n_sites, cf4, mconst2, clip_lo, clip_hi,   \
-                       hist, queues, bpx)
+                       hist, rmask, queues, bpx)
 #define TMH_LAUNCH_CFG(L_)                                 \
   switch (fused_cfg()) {                                   \
     case 0: TMH_LAUNCH_CH(L_, 2, 1024, 32768); break;      \

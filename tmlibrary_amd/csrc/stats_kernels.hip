@@ -656,22 +656,32 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
 // a complete histogram held in global memory (zero-maintained: every count is
 // read and reset), e.g. accumulated by the fused correct+histogram pass.
 template <int ABL = 0>  // ABL 8: counts are not reset (re-runnable)
+// rmask (may be NULL: every round is read): per site, the 1,024-bin rounds
+// at or above dense_rounds that hold counts; the others are known empty and
+// are not read (a microscopy site touches a handful of the 64).  The mask is
+// zero-maintained like the counts.
 __global__ __launch_bounds__(kHistThreads, 8) void k_hist_finalize(
-    uint32_t* __restrict__ hist, const QPos p, uint32_t* __restrict__ vlh_all,
+    uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask, int dense_rounds,
+    const QPos p, uint32_t* __restrict__ vlh_all,
     unsigned long long* __restrict__ pooled, int n_pooled,
     int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist) {
   __shared__ uint32_t slots[32];
   __shared__ uint32_t cmask[3];
   __shared__ int32_t starts[2 * kHistThreads];
   const int64_t s = blockIdx.x;
+  const unsigned long long rm = rmask ? rmask[s] : ~0ull;
   if (threadIdx.x < 3) cmask[threadIdx.x] = 0u;
   __syncthreads();
+  if (rmask && !(ABL & 8) && threadIdx.x == 0) rmask[s] = 0ull;  // every thread has read it
   uint32_t* h = hist + s * (int64_t)kBins;
   // sites spread their pooled-histogram adds over n_pooled copies (fewer
   // same-address atomic collisions); k_pooled_fold sums the copies
   unsigned long long* pl = pooled + (int64_t)(blockIdx.x % n_pooled) * kBins;
   hist_tail<ABL & 7, 4>(
-      [&](uint32_t b) -> uint32_t { return h[b]; },
+      [&](uint32_t b) -> uint32_t {
+        const uint32_t j = b >> 10;
+        return ((int)j < dense_rounds || ((rm >> j) & 1ull)) ? h[b] : 0u;
+      },
       [&](uint32_t b, uint32_t c) {
         if (!(ABL & 8) && c) h[b] = 0u;
       },
@@ -691,14 +701,15 @@ __global__ void k_pooled_fold(unsigned long long* __restrict__ pooled,
   pooled[b] += t;
 }
 
-void launch_hist_finalize(uint32_t* hist, int64_t n_sites, const QPos& p, uint32_t* vlh,
+void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_rounds,
+                          int64_t n_sites, const QPos& p, uint32_t* vlh,
                           unsigned long long* pooled,
                           unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
                           uint32_t* site_hist, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("hist_finalize", s);
   hipLaunchKernelGGL(k_hist_finalize<0>, dim3((unsigned)n_sites), dim3(kHistThreads), 0, s, hist,
-                     p, vlh, pooled_parts, n_parts, zero_counts, site_hist);
+                     rmask, dense_rounds, p, vlh, pooled_parts, n_parts, zero_counts, site_hist);
   hipLaunchKernelGGL(k_pooled_fold, dim3(kBins / 256), dim3(256), 0, s, pooled, pooled_parts,
                      n_parts);
   TMH_HIP(hipGetLastError());

@@ -618,6 +618,9 @@ int main(int argc, char** argv) {
     float4* mconst2;
     uint32_t* hist;
     int* queues;
+    unsigned long long* rmask;
+    CK(hipMalloc(&rmask, S * 8));
+    CK(hipMemset(rmask, 0, S * 8));
     CK(hipMalloc(&coef2, npx * 8));
     CK(hipMalloc(&mconst2, 16));
     CK(hipMalloc(&hist, S * kBins * 4));
@@ -630,7 +633,7 @@ int main(int argc, char** argv) {
         CK(hipMemset(queues, 0, 64));
         t.start();
         hipLaunchKernelGGL(kern, dim3(n_cu * (1024 / nt)), dim3(nt), 0, 0, sites, out, npx, S, (const float4*)coef2,
-                           mconst2, -1, -1, hist, queues, bpx);
+                           mconst2, -1, -1, hist, rmask, queues, bpx);
         report(name, t.stop(), 2 * S * site_gb);
       }
     };
@@ -653,7 +656,7 @@ int main(int argc, char** argv) {
     CK(hipMemset(hist, 0, S * kBins * 4));
     CK(hipMemset(queues, 0, 64));
     hipLaunchKernelGGL((k_correct_hist<true, false, 4, 0, 512, 16384>), dim3(n_cu * 2), dim3(512), 0, 0,
-                       sites, out, npx, S, (const float4*)coef2, mconst2, -1, -1, hist, queues, bpx);
+                       sites, out, npx, S, (const float4*)coef2, mconst2, -1, -1, hist, rmask, queues, bpx);
     QPos qa{qlo, qhi, Q, (double)(Q - 1) / (npx - 1), (int32_t)(npx - 1), 1};
     unsigned long long* parts;
     CK(hipMalloc(&parts, 16 * 65536 * 8));
@@ -661,7 +664,7 @@ int main(int argc, char** argv) {
     auto runf = [&](auto kern, const char* name) {
       for (int r = 0; r < reps; ++r) {
         t.start();
-        hipLaunchKernelGGL(kern, dim3((unsigned)S), dim3(1024), 0, 0, hist, qa, vlh, parts, 16,
+        hipLaunchKernelGGL(kern, dim3((unsigned)S), dim3(1024), 0, 0, hist, rmask, 4, qa, vlh, parts, 16,
                            zeros, (uint32_t*)nullptr);
         report(name, t.stop(), 0.0);
       }
