@@ -329,12 +329,22 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
     const double nl = (double)n_sites, n = (double)(n0 + n_sites);
     const WfMerge mg{1.0 / nl, nl / n, (double)n0 * nl / n, n0 == 0};
     const dim3 grid((unsigned)n_wg, (unsigned)f);
-    if (log_transform)
-      hipLaunchKernelGGL(k_welford_vec8<true>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
-                         per, mg, mean, m2, lut, part);
+    static const bool ntl = [] {  // TMH_WF_NTL=0: regular site loads (A/B)
+      const char* e = getenv("TMH_WF_NTL");
+      return !(e && e[0] == '0');
+    }();
+    if (log_transform && ntl)
+      hipLaunchKernelGGL((k_welford_vec8<true, true>), grid, dim3(kWfThreads), 0, s, sites, npx,
+                         n_sites, per, mg, mean, m2, lut, part);
+    else if (log_transform)
+      hipLaunchKernelGGL((k_welford_vec8<true, false>), grid, dim3(kWfThreads), 0, s, sites, npx,
+                         n_sites, per, mg, mean, m2, lut, part);
+    else if (ntl)
+      hipLaunchKernelGGL((k_welford_vec8<false, true>), grid, dim3(kWfThreads), 0, s, sites, npx,
+                         n_sites, per, mg, mean, m2, lut, part);
     else
-      hipLaunchKernelGGL(k_welford_vec8<false>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
-                         per, mg, mean, m2, lut, part);
+      hipLaunchKernelGGL((k_welford_vec8<false, false>), grid, dim3(kWfThreads), 0, s, sites, npx,
+                         n_sites, per, mg, mean, m2, lut, part);
     if (f > 1) {
       WfParts pc{};
       pc.n = f;
