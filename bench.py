@@ -3,18 +3,29 @@
 
 Metric (BASELINE.json): sites/sec for 2160x2560 uint16 site images through
 corilla illumination statistics AND ChannelImage.correct.  One *step* is the
-whole job over one channel's resident batch of sites (configs[1]: 384 wells x
-9 sites = 3,456 sites per GPU):
+whole job over every channel's resident batch of sites:
 
-    reset stats -> Welford + per-site histogram/percentiles over every site
-    (tmh_stats_update_device) -> [N>1: RCCL Welford all-reduce merge + ordered
-    percentile chain] -> finalize mean/std -> smooth both planes (sigma 5)
-    -> correction coefficients -> correct every site (tmh_correct_u16_device)
+    reset stats -> Welford (tmh_stats_update_welford_device)
+    -> [N>1: RCCL Welford all-reduce merge] -> finalize mean/std -> smooth both
+    planes (sigma 5) -> correction coefficients -> fused correct + per-site
+    histogram pass -> order statistics -> ordered percentile sum
+    (tmh_correct_u16_hist_device) -> [N>1: ordered percentile chain +
+    histogram all-reduce]
 
-Inputs are synthetic (counter-hash generator, SURVEY.md §8(d) distribution)
-and resident in HBM before timing starts.  With N GPUs each rank owns its own
-3,456 sites (weak scaling) and the merged statistics are identical on every
-rank.  Prints ONE JSON line on rank 0.
+Workloads:
+  N = 1   configs[1]: one channel, 3,456 sites (384 wells x 9 sites) on one GPU.
+  N > 1   configs[2]: 4 channels x 3,456 sites, each channel's sites sharded
+          contiguously over the ranks (432 per channel per GPU at N = 8); one
+          job per channel on its own stream, so a channel's merge overlaps the
+          next channel's kernels.  Total work is fixed: "scaling": "strong".
+  --layout per-gpu gives every rank its own 3,456 sites per channel instead
+  (weak scaling).
+
+Inputs come from the device generator (tmh_synth_sites_device), resident in
+HBM before timing starts.  Its host twin (tmlibrary_amd/synth.py) regenerates
+the same pixels, so the last step's results are compared against an oracle
+fingerprint committed under tests/golden/ (make_bench_fingerprint.py):
+``check_vs_oracle``.  Prints ONE JSON line on rank 0.
 
     python bench.py                      # N=1, default steps
     torchrun --nproc-per-node N bench.py --gpus N
@@ -23,6 +34,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes as C
+import hashlib
 import json
 import os
 import sys
@@ -35,6 +47,12 @@ import numpy as np  # noqa: E402
 
 METRIC = "sites/sec (2160×2560 uint16) illumstats+correct; % of HBM roofline at 1–8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+SEED = 12345
+
+
+def log(msg):
+    """Progress on stderr (a long silent run looks hung to the GPU harness)."""
+    print("[bench %s] %s" % (time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
 
 
 def parse():
@@ -43,13 +61,23 @@ def parse():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--sites", type=int, default=3456,
-                   help="sites per channel per GPU (configs[1]: 384 wells x 9 sites)")
-    p.add_argument("--channels", type=int, default=1,
-                   help="channels per GPU, each its own job on its own stream (configs[2]/[3]: 4)")
+                   help="sites per channel (384 wells x 9 sites); per GPU with --layout per-gpu")
+    p.add_argument("--channels", type=int, default=None,
+                   help="channels, each its own job on its own stream (default 1 at N=1, "
+                        "4 when sharded: configs[2])")
+    p.add_argument("--layout", choices=["auto", "per-gpu", "sharded"], default="auto",
+                   help="sharded: each channel's sites split over the ranks (default for N>1); "
+                        "per-gpu: every rank has its own --sites per channel")
+    p.add_argument("--distribution", choices=["synthetic", "bright", "uniform"],
+                   default="synthetic",
+                   help="pixel distribution of the generated sites (tmlibrary_amd/synth.py)")
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--width", type=int, default=2560)
-    p.add_argument("--cpu-sample", type=int, default=24,
-                   help="sites in the bounded CPU-baseline sample (0 disables)")
+    p.add_argument("--cpu-sample", type=int, default=96,
+                   help="sites of the CPU-baseline job (configs[0]: 96; 0 disables)")
+    p.add_argument("--cpu-procs", type=int, default=4,
+                   help="P of the P-process CPU variant (one channel job per process; "
+                        "P = min(this, cores))")
     p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
     p.add_argument("--pipeline", choices=["fused", "separate"], default="fused",
                    help="fused: histograms built from the correction's read (6 B/px); "
@@ -57,44 +85,103 @@ def parse():
     p.add_argument("--serial-stats", action="store_true",
                    help="run the histogram pass after Welford instead of concurrently")
     p.add_argument("--no-extras", action="store_true",
-                   help="skip the extra (non-headline) measurements: the illuminati chain pass")
+                   help="skip the extra (non-headline) measurements: chain pass, host path")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     return p.parse_args()
 
 
-def cpu_baseline(n_sites, H, W, total_sites):
-    """Bounded sample of the CPU oracle (numpy, 1 process, single-threaded
-    elementwise ops) over the same op sequence: per-site stats update +
-    correct, plus the one-time smoothing amortised over the full job."""
+# ---------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1 only; the oracle is the timed thing here, never
+# the GPU path's checker)
+# ---------------------------------------------------------------------------
+
+def _cpu_job(args):
+    """One channel job of the numpy oracle on a process's own core: per-site
+    OnlineStatistics.update (np.percentile with 100,000 q as stats.py:76,
+    log10, Welford), smoothing of both planes once, per-site correct."""
+    n_sites, H, W, seed, distinct = args
+    sys.path.insert(0, REPO)
     from oracle import corilla_oracle as orc
-    from tmlibrary_amd.synth import synth_sites_host
-    sites = synth_sites_host(n_sites, H, W, seed=2024)
+    from tmlibrary_amd.synth import synth_exact_host
+    base = [synth_exact_host(H, W, seed, 0, i) for i in range(min(distinct, n_sites))]
     st = orc.OracleOnlineStatistics((H, W), percentile="numpy")  # stats.py:76 as written
     t0 = time.perf_counter()
-    for s in sites:
-        st.update(s)
+    for i in range(n_sites):
+        st.update(base[i % len(base)])
     t1 = time.perf_counter()
     sm_mean = orc.smooth_reflect(st.mean, 5)
     sm_std = orc.smooth_reflect(st.std, 5)
     t2 = time.perf_counter()
-    for s in sites:
-        orc.correct_illumination(s, sm_mean, sm_std)
+    for i in range(n_sites):
+        orc.correct_illumination(base[i % len(base)], sm_mean, sm_std)
     t3 = time.perf_counter()
-    per_site = ((t1 - t0) + (t3 - t2)) / n_sites + (t2 - t1) / total_sites
+    return t1 - t0, t2 - t1, t3 - t2
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(n_sites, H, W, procs):
+    """configs[0] on the host: one process (the reference's cores=1 job,
+    workflow/args.py:538-545) over n_sites, plus P processes each running
+    its own channel job (the reference's one-job-per-channel parallelism,
+    corilla/api.py:64-105).  Both in fresh spawned interpreters."""
+    import multiprocessing as mp
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    distinct = 8  # the timing does not depend on which sites repeat
+    env_keep = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS")}
+    os.environ["OMP_NUM_THREADS"] = os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    try:
+        ctx = mp.get_context("spawn")
+        with ctx.Pool(1) as pool:
+            ts, tsm, tc = pool.apply(_cpu_job, ((n_sites, H, W, SEED, distinct),))
+        P = max(1, min(procs, cores))
+        per = max(1, n_sites // 4)
+        with ctx.Pool(P) as pool:
+            # concurrent jobs; each times its own job (site generation excluded)
+            times = pool.map(_cpu_job, [(per, H, W, SEED + k, distinct) for k in range(P)])
+        rate_p = sum(per / sum(t) for t in times)
+    finally:
+        for k, v in env_keep.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    job = ts + tsm + tc
     return {
-        "value": round(1.0 / per_site, 4),
+        "value": round(n_sites / job, 4),
         "unit": "sites/s",
         "cores": 1,
         "kind": "port",
-        "sample": "%d synthetic %dx%d sites: oracle OnlineStatistics.update (np.percentile "
-                  "with 100,000 q, log10, Welford) x%d + "
-                  "correct_illumination x%d (numpy, 1 process) + smoothing of 2 planes "
-                  "amortised over %d sites; stats %.1f ms/site, correct %.1f ms/site"
-                  % (n_sites, H, W, n_sites, n_sites, total_sites,
-                     1e3 * (t1 - t0) / n_sites, 1e3 * (t3 - t2) / n_sites),
+        "cpu": cpu_model(),
+        "nproc": cores,
+        "sample": "configs[0]: one channel job of %d synthetic %dx%d sites (%d distinct, cycled) "
+                  "in the numpy oracle, 1 process: OnlineStatistics.update (np.percentile with "
+                  "100,000 q, log10, Welford) %.1f ms/site + smoothing of both planes once "
+                  "%.2f s + correct_illumination %.1f ms/site"
+                  % (n_sites, H, W, distinct, 1e3 * ts / n_sites, tsm, 1e3 * tc / n_sites),
+        "multi_process": {"processes": P, "sites_per_process": per,
+                          "value": round(rate_p, 4), "unit": "sites/s",
+                          "note": "P = min(%d channels, %d cores) processes, one channel job "
+                                  "each (the reference's job-level parallelism)" % (procs, cores)},
     }
 
+
+# ---------------------------------------------------------------------------
+# extras beside the headline (N = 1)
+# ---------------------------------------------------------------------------
 
 def bench_chain(L, corr, S_ptr, S, H, W, dev, sp, reps=3):
     """§8(f) rank 3, measured beside the headline: the illuminati chain
@@ -139,9 +226,10 @@ def bench_host_path(H, W, n_sites=64, reps=3):
     OnlineStatistics.update_batch (tmh_stats_update) and Corrector.apply
     (tmh_correct_u16), double-buffered device slots on copy streams."""
     from tmlibrary_amd.image import Corrector
-    from tmlibrary_amd.synth import synth_sites_host
+    from tmlibrary_amd.synth import synth_exact_host
     from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
-    sites = np.ascontiguousarray(np.stack(synth_sites_host(n_sites, H, W, seed=7)))
+    base = [synth_exact_host(H, W, 7, 0, i) for i in range(8)]
+    sites = np.ascontiguousarray(np.stack([base[i % 8] for i in range(n_sites)]))
     st = OnlineStatistics((H, W), batch_size=32)
     st.update_batch(sites)  # warm-up: both pinned and device slots allocated
     corr = Corrector(st.mean.array, st.std.array)
@@ -175,50 +263,122 @@ def bench_host_path(H, W, n_sites=64, reps=3):
             "job_sites_per_s": round(n_sites / (t_stats + t_corr), 1)}
 
 
+# ---------------------------------------------------------------------------
+# oracle fingerprint check
+# ---------------------------------------------------------------------------
+
+def fingerprint_name(H, W, S, seed, channel, distribution):
+    """File (under tests/golden/) of the oracle fingerprint for one channel
+    job; written by tests/golden/make_bench_fingerprint.py."""
+    return "bench_fp_%dx%d_s%d_seed%d_c%d_%s.npz" % (H, W, S, seed, channel, distribution)
+
+
+def load_fingerprint(H, W, S_total, distribution):
+    path = os.path.join(REPO, "tests", "golden",
+                        fingerprint_name(H, W, S_total, SEED, 0, distribution))
+    if not os.path.exists(path):
+        return None, path
+    with np.load(path, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}, path
+
+
+def _close(got, want, rtol=1e-6, atol=1e-9):
+    return bool(np.all(np.abs(got - want) <= atol + rtol * np.abs(want)))
+
+
+def check_against_fingerprint(fp, res, smean, sstd, corr_sites):
+    """This rank's view of the channel-0 job vs the oracle fingerprint.
+    corr_sites: {global site index: corrected uint16 plane} for the
+    fingerprint's sampled sites that this rank holds."""
+    sp = fp["stat_px"]
+    out = {
+        "n": int(res["n"]) == int(fp["n"]),
+        "pct_sums_bit_exact": hashlib.sha256(res["acc"].tobytes()).hexdigest() ==
+        str(fp["pct_sums_sha256"]),
+        "hist_bit_exact": hashlib.sha256(res["hist"].tobytes()).hexdigest() ==
+        str(fp["hist_sha256"]),
+        "mean_1e-6": _close(res["mean"].ravel()[sp], fp["mean_samples"]),
+        "std_1e-6": _close(res["std"].ravel()[sp], fp["std_samples"]),
+        "smoothed_1e-6": _close(smean[sp], fp["smean_samples"]) and
+        _close(sstd[sp], fp["sstd_samples"]),
+    }
+    cnt = np.zeros(5, dtype=np.int64)  # equal, +1, -1, |d| > 1, wrap flips
+    for k, s in enumerate(fp["corr_sites"].tolist()):
+        if s not in corr_sites:
+            continue
+        got = corr_sites[s].ravel()[fp["corr_px"]].astype(np.int64)
+        d = got - fp["corr_samples"][k].astype(np.int64)
+        flips = np.abs(d) == 65535
+        cnt += [np.count_nonzero(d == 0), np.count_nonzero(d == 1), np.count_nonzero(d == -1),
+                np.count_nonzero((np.abs(d) > 1) & ~flips), np.count_nonzero(flips)]
+    return out, cnt
+
+
+# ---------------------------------------------------------------------------
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    H, W = a.height, a.width
+    npx = H * W
+    Q = 100000
+
+    cpu = None
+    if world == 1 and a.cpu_sample > 0:  # before the GPU is touched: nothing competes
+        log("CPU baseline: %d sites, 1 process + %d processes" % (a.cpu_sample, a.cpu_procs))
+        cpu = cpu_baseline(a.cpu_sample, H, W, a.cpu_procs)
+        log("CPU baseline: %.3f sites/s" % cpu["value"])
+
     import torch
     import torch.distributed as dist
 
     from tmlibrary_amd import hip
     from tmlibrary_amd.image import ZERO_LOG10
+    from tmlibrary_amd.synth import DISTRIBUTIONS
     from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
-    from tmlibrary_amd.workflow.corilla.sharded import StatsOps, merge_percentiles, merge_welford
+    from tmlibrary_amd.workflow.corilla.sharded import (StatsOps, merge_counts, merge_welford,
+                                                         shard_bounds)
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    # TMH_BENCH_FORCE_DIST=1 runs the multi-GPU code path (RCCL merge,
+    # TMH_BENCH_FORCE_DIST=1 runs the multi-GPU code path (RCCL merges,
     # deferred percentiles, pipelined chain) even with one rank
     dist_on = world > 1 or os.environ.get("TMH_BENCH_FORCE_DIST") == "1"
     if dist_on:
         dist.init_process_group("nccl", device_id=dev)
+    sharded = a.layout == "sharded" or (a.layout == "auto" and world > 1)
+    CH = a.channels if a.channels else (4 if sharded else 1)
+    S_total = a.sites
+    if sharded:
+        s_begin, s_end = shard_bounds(S_total, world, rank)
+    else:
+        s_begin, s_end = rank * S_total, (rank + 1) * S_total
+    S = s_end - s_begin  # this rank's sites per channel
+    n_channel = S_total if sharded else world * S_total  # sites per channel job
     L = hip.lib()
     hip.check(L.tmh_set_device(local_rank))
-    H, W, S = a.height, a.width, a.sites
-    npx = H * W
-    Q = 100000
     # one non-null stream for our launches AND torch/RCCL work, so they order
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sp = C.c_void_p(stream.cuda_stream)
 
     # resident inputs / outputs (int16 tensors = raw uint16 bytes); channel c
-    # owns sites [c*S, (c+1)*S)
-    CH = a.channels
+    # owns local rows [c*S, (c+1)*S) = its global sites [s_begin, s_end)
+    dist_id = DISTRIBUTIONS[a.distribution]
     sites = torch.empty((CH * S, H, W), dtype=torch.int16, device=dev)
     out = torch.empty_like(sites)
     for c in range(CH):
-        hip.check(L.tmh_synth_sites_device(C.c_void_p(sites[c * S].data_ptr()), S, H, W, 12345, c,
-                                           rank * S, sp))
+        hip.check(L.tmh_synth_sites_device(C.c_void_p(sites[c * S].data_ptr()), S, H, W, SEED, c,
+                                           s_begin, dist_id, sp))
     lo, hi, gamma = quantile_table(npx, np.linspace(0, 100, Q))
     lut = stats_log10_lut()
     flags = hip.TMH_STATS_DEFERRED_PCT if dist_on else 0
     if a.serial_stats:
         flags |= hip.TMH_STATS_SERIAL
     fused = a.pipeline == "fused"
+    prof = not a.no_profile
 
     class Channel(object):
         """One channel's job: its sites, statistics handle, corrector and
@@ -245,6 +405,7 @@ def main():
                                                     C.c_void_p(self.std.data_ptr()), H, W, 1,
                                                     ZERO_LOG10, self.sp, C.byref(self.corr)))
             self.ops = StatsOps(L, self.h, npx, Q, dev)
+            self.merge_ev = []  # (welford start, end, counts start, end) per timed step
 
         def stats(self):
             hip.check(L.tmh_stats_reset(self.h))
@@ -269,35 +430,49 @@ def main():
                 hip.check(L.tmh_correct_u16_device(self.corr, self.S_ptr, self.O_ptr, S, -1, -1,
                                                    self.sp))
 
+        def event(self):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(self.stream)
+            return e
+
         def close(self):
             L.tmh_corrector_destroy(self.corr)
             L.tmh_stats_destroy(self.h)
 
     chans = [Channel(c) for c in range(CH)]
-    h, corr, S_ptr = chans[0].h, chans[0].corr, chans[0].S_ptr  # single-channel extras / check
+    log("%d channel(s) x %d sites resident; warm-up" % (CH, S))
+
+    timing = {"on": False}
 
     def step():
         for ch in chans:
             ch.stats()
+        evs = {}
         if dist_on:
             for ch in chans:
                 with torch.cuda.stream(ch.stream):
-                    merge_welford(ch.ops, dist)
+                    e0 = ch.event() if timing["on"] else None
+                    merge_welford(ch.ops, dist, n_total=n_channel)
+                    evs[id(ch)] = [e0, ch.event() if timing["on"] else None]
         for ch in chans:
             ch.apply()
         if dist_on:
             for ch in chans:
                 with torch.cuda.stream(ch.stream):
-                    merge_percentiles(ch.ops, dist)
+                    e2 = ch.event() if timing["on"] else None
+                    merge_counts(ch.ops, dist)
+                    if timing["on"]:
+                        ch.merge_ev.append(evs[id(ch)] + [e2, ch.event()])
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
 
-    prof = not a.no_profile
+    log("timing %d steps" % a.steps)
     if prof:
         L.tmh_profile_enable(1)
         L.tmh_profile_reset()
+        timing["on"] = dist_on
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -323,21 +498,55 @@ def main():
             if k.value:
                 kern[name] = (ms.value / k.value, k.value)
         L.tmh_profile_enable(0)
+    merge_ms = None
+    if dist_on and prof:
+        merge_ms = []
+        for ch in chans:
+            w = [e[0].elapsed_time(e[1]) for e in ch.merge_ev]
+            m = [e[2].elapsed_time(e[3]) for e in ch.merge_ev]
+            merge_ms.append({"welford_allreduce_ms": round(float(np.mean(w)), 4),
+                             "pct_chain_hist_allreduce_ms": round(float(np.mean(m)), 4)})
 
-    # result fingerprint of the last step (identical on every rank and for
-    # any N: merged mean/std and the bit-exact percentile sums)
+    # channel 0's results after the last step (identical on every rank)
+    ch0 = chans[0]
     nn = C.c_int64()
-    m_h = np.empty(npx)
-    s_h = np.empty(npx)
-    acc_h = np.empty(Q)
-    hip.check(L.tmh_stats_finalize(h, C.byref(nn), hip.ptr(m_h), hip.ptr(s_h), hip.ptr(acc_h), None))
-    import hashlib
-    check = {"n": int(nn.value), "mean_sum": float(m_h.sum()), "std_sum": float(s_h.sum()),
-             "pct_sums_sha256": hashlib.sha256(acc_h.tobytes()).hexdigest()[:16]}
+    res = {"mean": np.empty(npx), "std": np.empty(npx), "acc": np.empty(Q),
+           "hist": np.empty(65536, np.uint64)}
+    hip.check(L.tmh_stats_finalize(ch0.h, C.byref(nn), hip.ptr(res["mean"]), hip.ptr(res["std"]),
+                                   hip.ptr(res["acc"]), hip.ptr(res["hist"])))
+    res["n"] = nn.value
+    check = {"n": int(nn.value), "mean_sum": float(res["mean"].sum()),
+             "std_sum": float(res["std"].sum()),
+             "pct_sums_sha256": hashlib.sha256(res["acc"].tobytes()).hexdigest()[:16],
+             "hist_sha256": hashlib.sha256(res["hist"].tobytes()).hexdigest()[:16]}
+    fp, fp_path = load_fingerprint(H, W, S_total, a.distribution)
+    check_ok = None
+    if fp is not None and n_channel == S_total and fused:
+        held = {s: out[s - s_begin].cpu().numpy().view(np.uint16)
+                for s in fp["corr_sites"].tolist() if s_begin <= s < s_end}
+        oks, cnt = check_against_fingerprint(fp, res, ch0.smean.cpu().numpy(),
+                                             ch0.sstd.cpu().numpy(), held)
+        if dist_on:
+            flags_t = torch.tensor([int(v) for v in oks.values()], dtype=torch.int64, device=dev)
+            dist.all_reduce(flags_t, op=dist.ReduceOp.MIN)
+            oks = dict(zip(oks, (bool(v) for v in flags_t.tolist())))
+            cnt_t = torch.tensor(cnt, dtype=torch.int64, device=dev)
+            dist.all_reduce(cnt_t)
+            cnt = cnt_t.cpu().numpy()
+        tot = max(int(cnt.sum()), 1)
+        oks["corrected_within_1DN"] = bool(cnt[3] == 0 and cnt[4] == 0)
+        check["vs_oracle"] = dict(oks, fingerprint=os.path.relpath(fp_path, REPO))
+        check["corrected_vs_oracle"] = {
+            "sampled_pixels": tot, "sites": fp["corr_sites"].tolist(),
+            "frac_equal": round(cnt[0] / tot, 6), "frac_plus1": round(cnt[1] / tot, 6),
+            "frac_minus1": round(cnt[2] / tot, 6), "beyond_1DN": int(cnt[3]),
+            "wrap_flips": int(cnt[4])}
+        check_ok = all(oks.values())
 
+    log("%.1f ms/step; check_vs_oracle %s" % (1e3 * elapsed / a.steps, check_ok))
     extras = {}
     if not a.no_extras and world == 1:
-        extras["chain_u8"] = bench_chain(L, corr, S_ptr, S, H, W, dev, sp)
+        extras["chain_u8"] = bench_chain(L, ch0.corr, ch0.S_ptr, S, H, W, dev, sp)
         extras["host_path"] = bench_host_path(H, W)
 
     if rank == 0:
@@ -367,17 +576,29 @@ def main():
                 with open(a.traffic_json) as f:
                     tj = json.load(f)
                 cfg = tj.get("config", {})
-                if cfg.get("sites") == S and cfg.get("height") == H and cfg.get("width") == W:
+                if cfg.get("sites") == S and cfg.get("height") == H and cfg.get("width") == W \
+                        and cfg.get("distribution", "synthetic") == a.distribution:
                     traffic = tj.get("kernels", {}).get(dominant, {}).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 pass
             roofline = {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                         "traffic": traffic, "alg_bytes_per_launch": alg[dominant]}
-        total_sites = world * CH * S * a.steps
+        total_sites = world * CH * S * a.steps if not sharded else CH * S_total * a.steps
         value = total_sites / elapsed
-        job_bytes = world * CH * S * 6 * npx  # 6 B/px algorithmic per site-image
-        res = {
+        job_bytes = total_sites // a.steps * 6 * npx  # 6 B/px algorithmic per site-image
+        if sharded:
+            workload = ("illumstats+correct, %d channels x %d sites of %dx%d uint16, each channel's "
+                        "sites sharded over %d GPU(s) (%d per GPU), one job per channel on its own "
+                        "stream (configs[2]: full plate 384 wells x 9 sites x 4 channels)"
+                        % (CH, S_total, H, W, world, S, ))
+        elif CH == 1:
+            workload = ("illumstats+correct, 1 channel, %d sites/GPU of %dx%d uint16 "
+                        "(configs[1]: 384 wells x 9 sites)" % (S, H, W))
+        else:
+            workload = ("illumstats+correct, %d channels x %d sites/GPU of %dx%d uint16, "
+                        "one job per channel on its own stream" % (CH, S, H, W))
+        resd = {
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "sites/s",
@@ -386,34 +607,32 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(1e3 * elapsed / a.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (device counter-hash generator, SURVEY.md §8(d) distribution), "
-                    "resident in HBM",
-            "config": {"workload": ("illumstats+correct, 1 channel, %d sites/GPU of %dx%d uint16 "
-                                    "(configs[1]: 384 wells x 9 sites)" % (S, H, W)) if CH == 1
-                       else ("illumstats+correct, %d channels x %d sites/GPU of %dx%d uint16, "
-                             "one job per channel on its own stream" % (CH, S, H, W)),
-                       "sites_per_gpu": CH * S, "channels": CH, "height": H, "width": W,
-                       "decimals": 3,
-                       "smoothing_sigma": 5, "clip": None,
-                       "parallelism": "sites sharded (contiguous); RCCL all-reduce Welford "
-                                      "merge + ordered percentile chain" if world > 1
-                                      else "single GPU",
+            "dtype": "f64 stats / f32 correct (±1 DN)",
+            "data": "synthetic '%s' (integer-exact device generator, tmlibrary_amd/synth.py; "
+                    "SURVEY.md §8(d) distribution), resident in HBM" % a.distribution,
+            "config": {"workload": workload,
+                       "sites_per_gpu": CH * S, "channels": CH, "sites_per_channel": n_channel,
+                       "height": H, "width": W, "decimals": 3,
+                       "smoothing_sigma": 5, "clip": None, "distribution": a.distribution,
+                       "parallelism": ("sites sharded (contiguous); RCCL all-reduce Welford "
+                                       "merge, ordered percentile chain, histogram all-reduce")
+                       if dist_on else "single GPU",
                        "pipeline": a.pipeline},
-            "job_hbm_roofline_frac": round(job_bytes * a.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world), 4),
+            "job_hbm_roofline_frac": round(job_bytes * a.steps / elapsed / 1e9 /
+                                           (HBM_PEAK_GBS * world), 4),
             "roofline": roofline,
             "kernels": kdetail,
         }
-        res["check"] = check
+        if merge_ms is not None:
+            resd["merge_per_channel"] = merge_ms
+        resd["check"] = check
+        resd["check_vs_oracle"] = check_ok
         if extras:
-            res["extras"] = extras
-        if world == 1 and a.cpu_sample > 0:
-            res["cpu_baseline"] = cpu_baseline(a.cpu_sample, H, W, S)
-        else:
-            res["cpu_baseline"] = None
-        print(json.dumps(res), flush=True)
+            resd["extras"] = extras
+        resd["cpu_baseline"] = cpu
+        print(json.dumps(resd), flush=True)
 
     for ch in chans:
         ch.close()

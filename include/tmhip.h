@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define TMH_ABI_VERSION 1
+#define TMH_ABI_VERSION 2
 
 #define TMH_OK 0
 #define TMH_EINVAL (-22)  /* bad argument: maps to ValueError / TypeError */
@@ -76,7 +76,21 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
                      int batch_capacity, unsigned flags, tmh_stats** out);
 void tmh_stats_destroy(tmh_stats* h);
 int tmh_stats_set_stream(tmh_stats* h, void* stream);
+/* Start a new job on the handle (stats.py:53-62 state).  Also restores the
+ * handle's zero-maintained histogram slabs if a fused pass was interrupted. */
 int tmh_stats_reset(tmh_stats* h);
+
+/* Launch-shape options of a handle (results never depend on them):
+ *   TMH_OPT_FUSED_CONFIG   0..3: (sites per unit, threads, LDS bins) of the
+ *                          fused correct+histogram pass = (2, 1024, 32768),
+ *                          (4, 1024, 32768), (2, 512, 16384), (4, 512, 16384);
+ *                          default 3
+ *   TMH_OPT_WELFORD_PARTS  0: split a Welford launch's sites into parts when it
+ *                          fills the GPU better (default); 1..4: force that
+ *                          many parts where the launch has >= 32 sites a part */
+#define TMH_OPT_FUSED_CONFIG 1
+#define TMH_OPT_WELFORD_PARTS 2
+int tmh_stats_set_option(tmh_stats* h, int option, int value);
 
 /* update(image) for a run of sites.  zero_counts_out (host, n_sites, may be
  * NULL): per-site number of zero pixels, for the 'image contains zero
@@ -109,6 +123,8 @@ int tmh_stats_finalize(tmh_stats* h, int64_t* n, double* mean, double* std, doub
                        uint64_t* hist);
 /* Device form: writes mean/std planes into caller device buffers. */
 int tmh_stats_finalize_device(tmh_stats* h, double* dev_mean, double* dev_std, void* stream);
+/* var = M2 / (n - 1), NaN everywhere when n < 2 (stats.py:94-102), host copy. */
+int tmh_stats_variance(tmh_stats* h, double* host_var);
 /* Per-site histogram of the most recent update batch (debug/parity). */
 int tmh_stats_site_histogram(tmh_stats* h, int64_t site_in_last_batch, uint32_t* host_hist);
 /* Order statistics at every quantile's previous/next sorted position for one
@@ -138,6 +154,11 @@ int tmh_stats_pct_accumulate(tmh_stats* h, double* dev_acc, void* stream);
 int tmh_stats_pct_accumulate_range(tmh_stats* h, double* dev_acc_range, int q_begin, int q_count,
                                    void* stream);
 int tmh_stats_set_pct_sum(tmh_stats* h, const double* dev_acc, void* stream);
+/* Pooled 65,536-bin u64 histogram out of / into the handle (device buffers):
+ * the histogram merge is get -> all_reduce(sum) -> set.  Sums of counts are
+ * exact, so any reduction order gives the same bins. */
+int tmh_stats_get_hist_device(tmh_stats* h, uint64_t* dev_hist, void* stream);
+int tmh_stats_set_hist_device(tmh_stats* h, const uint64_t* dev_hist, void* stream);
 
 /* ---- smoothing -----------------------------------------------------------
  * Replaces tmlib/image.py:287-311 Image.smooth -> mahotas.gaussian_filter
@@ -188,7 +209,10 @@ int tmh_correct_u16(tmh_corrector* c, const uint16_t* host_in, uint16_t* host_ou
 int tmh_correct_u16_device(tmh_corrector* c, const uint16_t* dev_in, uint16_t* dev_out,
                            int64_t n_sites, int clip_lo, int clip_hi, void* stream);
 /* Correct n_sites pending sites of h and fold their histograms/percentiles
- * into h (see tmh_stats_update_welford_device). */
+ * into h (see tmh_stats_update_welford_device).  Stream contract: the work
+ * runs on `stream` (NULL: the corrector's stream), ordered after everything
+ * already queued on h's stream, and h's stream waits for it before any later
+ * work on h -- the two handles may live on different streams. */
 int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* dev_in,
                                 uint16_t* dev_out, int64_t n_sites, int clip_lo, int clip_hi,
                                 void* stream);
@@ -218,9 +242,26 @@ int tmh_correct_chain_u8(tmh_corrector* c, const uint16_t* host_in, uint8_t* hos
 /* ChannelImage.clip alone (image.py:589), u16. */
 int tmh_clip_u16(const uint16_t* host_in, uint16_t* host_out, int64_t n, int lo, int hi);
 
-/* ---- synthetic input (imextract stand-in for benchmarks) ----------------- */
+/* ---- synthetic input (imextract stand-in for benchmarks) -----------------
+ * Sites [first_site, first_site + n_sites) of (seed, channel), generated in
+ * HBM with integer arithmetic only, so tmlibrary_amd/synth.py
+ * (synth_exact_host) reproduces every pixel bit for bit on the host and the
+ * bench's full-size results can be checked against the CPU oracle.
+ * distribution: TMH_SYNTH_STANDARD  100 + vignetting * LogNormal(6, 0.6) + N(0, 5)
+ *               TMH_SYNTH_BRIGHT    the same with LogNormal(8.5, 0.6) (median ~5,000)
+ *               TMH_SYNTH_UNIFORM   uniform 0..65535
+ * (STANDARD / BRIGHT also carry 0.01 % zeros and 0.01 % saturated pixels.) */
+#define TMH_SYNTH_STANDARD 0
+#define TMH_SYNTH_BRIGHT 1
+#define TMH_SYNTH_UNIFORM 2
 int tmh_synth_sites_device(uint16_t* dev_out, int64_t n_sites, int height, int width,
-                           uint64_t seed, int channel, int64_t first_site, void* stream);
+                           uint64_t seed, int channel, int64_t first_site, int distribution,
+                           void* stream);
+/* The generator's integer tables (host only, no GPU needed): ln16/nz16
+ * [4096] (lognormal and noise quantiles in 1/16 DN), ey[height], ex[width]
+ * (vignetting factors, 2^15 = 1). */
+int tmh_synth_tables(int distribution, int height, int width, int32_t* ln16, int32_t* nz16,
+                     int32_t* ey, int32_t* ex);
 
 /* ---- device memory helpers for callers without another allocator -------- */
 int tmh_malloc_device(void** dev_ptr, size_t bytes);

@@ -31,7 +31,7 @@ def test_library_exports_every_symbol():
     lib = hip.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.tmh_abi_version() == 1
+    assert lib.tmh_abi_version() == hip.ABI_VERSION
 
 
 def test_errors_without_gpu_are_loud():

@@ -15,13 +15,15 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from util import REPO, load_golden
+from oracle import corilla_oracle as orc
 
 
 class HostOps(object):
     """Test double of sharded.StatsOps on numpy/torch CPU state."""
 
-    def __init__(self, n, mean, m2, site_pcts):
+    def __init__(self, n, mean, m2, site_pcts, hist):
         self.n = int(n)
+        self.hist = torch.tensor(np.asarray(hist, dtype=np.uint64).astype(np.int64))
         self.mean = torch.tensor(np.asarray(mean, dtype=np.float64).ravel())
         self.m2 = torch.tensor(np.asarray(m2, dtype=np.float64).ravel())
         self.site_pcts = [np.asarray(p, dtype=np.float64) for p in site_pcts]
@@ -66,6 +68,15 @@ class HostOps(object):
     def set_pct_sum(self, acc):
         self.acc = acc.clone()
 
+    def empty_hist(self):
+        return torch.empty(65536, dtype=torch.int64)
+
+    def get_hist(self, buf):
+        buf.copy_(self.hist)
+
+    def set_hist(self, buf):
+        self.hist = buf.clone()
+
 
 class WholeOps(HostOps):
     """Ops without the ranged accumulate: the chain falls back to one step."""
@@ -97,10 +108,11 @@ def _worker(rank, world, port, name, out_dir):
     for s in mine:
         st.update(s)
     cls = WholeOps if name == "stats_small" and world == 2 else HostOps
-    ops = cls(st.n, st.mean, st._M2, [orc.percentile_linear(s, q) for s in mine])
+    local_hist = sum((orc.histogram_u16(s) for s in mine), np.zeros(65536, np.uint64))
+    ops = cls(st.n, st.mean, st._M2, [orc.percentile_linear(s, q) for s in mine], local_hist)
     n_total = merge_shards(ops, dist)
     np.savez(os.path.join(out_dir, "r%d.npz" % rank), n=n_total, mean=ops.mean.numpy(),
-             m2=ops.m2.numpy(), acc=ops.acc.numpy())
+             m2=ops.m2.numpy(), acc=ops.acc.numpy(), hist=ops.hist.numpy().astype(np.uint64))
     dist.destroy_process_group()
 
 
@@ -119,6 +131,8 @@ def test_merge_shards_gloo(tmp_path, world, name):
         var = z["m2"].reshape(g["mean"].shape) / (int(z["n"]) - 1)
         assert np.allclose(var, want_var, rtol=1e-6, atol=1e-12)
         assert np.array_equal(z["acc"], g["pct_sums"]), "chained percentile sum not bit-exact"
+        want_hist = sum((orc.histogram_u16(s) for s in g["sites"]), np.zeros(65536, np.uint64))
+        assert np.array_equal(z["hist"], want_hist), "merged histogram differs from the oracle's"
 
 
 def test_chain_chunks_even_cover():

@@ -62,11 +62,13 @@ class OracleChannelStats(object):
         for s in sites:
             self.st.update(s)
             self.site_pcts.append(orc.percentile_linear(s, self.q))
+            self.local_hist = getattr(self, "local_hist", 0) + orc.histogram_u16(s)
 
     def merge(self, d, group=None):
         from test_distributed_gloo import HostOps
         from tmlibrary_amd.workflow.corilla.sharded import merge_shards
-        ops = HostOps(self.st.n, self.st.mean, self.st._M2, self.site_pcts or [np.zeros(len(self.q))])
+        ops = HostOps(self.st.n, self.st.mean, self.st._M2, self.site_pcts or [np.zeros(len(self.q))],
+                      getattr(self, "local_hist", np.zeros(65536, np.uint64)))
         if not self.site_pcts:
             ops.site_pcts = []
         if d is not None:
@@ -80,6 +82,7 @@ class OracleChannelStats(object):
         self.mean = ops.mean.numpy().reshape(self.st.mean.shape)
         self.std = np.sqrt(ops.m2.numpy().reshape(self.st.mean.shape) / (self.n - 1))
         self.acc = acc
+        self.histogram = ops.hist.numpy().astype(np.uint64)
         return self.n
 
     def container(self):
@@ -91,6 +94,26 @@ class OracleChannelStats(object):
 
     def close(self):
         pass
+
+
+class Recorder(object):
+    """stats_factory wrapper keeping every channel's statistics object, so
+    the merged pooled histogram can be checked after the job."""
+
+    def __init__(self, factory):
+        self.factory = factory
+        self.made = []
+
+    def __call__(self, dims):
+        st = self.factory(dims)
+        self.made.append(st)
+        return st
+
+
+def _check_hist(made, sites):
+    for st, ids in zip(made, CHANNELS.values()):
+        want = sum((orc.histogram_u16(sites[i]) for i in ids), np.zeros(65536, np.uint64))
+        assert np.array_equal(np.asarray(st.histogram, np.uint64), want), "pooled histogram"
 
 
 def _check(results, sites, rtol=1e-6):
@@ -114,11 +137,13 @@ def _worker(rank, world, port, root):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     store = ExperimentStore(root)
-    res = run_channels_sharded(store, _batches(), dist=dist, stats_factory=OracleChannelStats,
+    rec = Recorder(OracleChannelStats)
+    res = run_channels_sharded(store, _batches(), dist=dist, stats_factory=rec,
                                block=2, decode_threads=2)
     np.savez(os.path.join(root, "r%d.npz" % rank),
              **{"mean%d" % ch: c.mean.array for ch, c in res.items()},
-             **{"std%d" % ch: c.std.array for ch, c in res.items()})
+             **{"std%d" % ch: c.std.array for ch, c in res.items()},
+             **{"hist%d" % ch: st.histogram for ch, st in zip(CHANNELS, rec.made)})
     dist.destroy_process_group()
 
 
@@ -134,6 +159,8 @@ def test_sharded_job_gloo(tmp_path, world):
             z = np.load(tmp_path / ("r%d.npz" % r))
             assert np.allclose(z["mean%d" % ch], ref.mean, rtol=1e-6, atol=1e-12)
             assert np.allclose(z["std%d" % ch], ref.std, rtol=1e-6, atol=1e-12)
+            want = sum((orc.histogram_u16(sites[i]) for i in ids), np.zeros(65536, np.uint64))
+            assert np.array_equal(z["hist%d" % ch], want), "merged pooled histogram"
         # rank 0 wrote the channel's illumstats file (4 datasets, unsmoothed)
         mean, std, keys, vals = h5.read_illumstats(store.illumstats_file(ch).location)
         assert np.allclose(mean, ref.mean, rtol=1e-6, atol=1e-12)
@@ -144,34 +171,38 @@ def test_sharded_job_gloo(tmp_path, world):
 def test_single_process_cpu_double(tmp_path):
     from tmlibrary_amd.workflow.corilla.multi import run_channels_sharded
     store, sites = _make_store(str(tmp_path))
-    res = run_channels_sharded(store, _batches(), dist=None, stats_factory=OracleChannelStats,
-                               block=3)
+    rec = Recorder(OracleChannelStats)
+    res = run_channels_sharded(store, _batches(), dist=None, stats_factory=rec, block=3)
     _check(res, sites)
+    _check_hist(rec.made, sites)
 
 
 @pytest.mark.gpu
 def test_single_process_gpu(tmp_path):
     from tmlibrary_amd.workflow.corilla.multi import run_channels_sharded
+    from tmlibrary_amd.workflow.corilla.multi import GpuChannelStats
     store, sites = _make_store(str(tmp_path))
-    res = run_channels_sharded(store, _batches(), dist=None, block=3)
+    rec = Recorder(lambda d: GpuChannelStats(d, 1, batch_size=3))
+    res = run_channels_sharded(store, _batches(), dist=None, stats_factory=rec, block=3)
     _check(res, sites)
+    _check_hist(rec.made, sites)
 
 
 _RCCL_SCRIPT = r"""
 import os, sys
 sys.path.insert(0, {repo!r}); sys.path.insert(0, os.path.join({repo!r}, "tests"))
 import torch, torch.distributed as dist
-from test_multi_job import _make_store, _batches, _check
+from test_multi_job import _make_store, _batches, _check, _check_hist, Recorder
 from tmlibrary_amd.workflow.corilla.multi import GpuChannelStats, run_channels_sharded
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 dist.init_process_group("nccl", rank=0, world_size=1, init_method="tcp://127.0.0.1:{port}",
                         device_id=dev)
 store, sites = _make_store({root!r})
-res = run_channels_sharded(store, _batches(), dist=dist, block=3, device=dev,
-                           stats_factory=lambda d: GpuChannelStats(d, 1, device=dev,
-                                                                   merge_single=True))
+rec = Recorder(lambda d: GpuChannelStats(d, 1, device=dev, merge_single=True))
+res = run_channels_sharded(store, _batches(), dist=dist, block=3, device=dev, stats_factory=rec)
 _check(res, sites)
+_check_hist(rec.made, sites)  # through get -> RCCL all_reduce -> set
 dist.destroy_process_group()
 print("rccl merge ok")
 """

@@ -233,6 +233,10 @@ struct tmh_stats {
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;   // histogram pass runs here, concurrent with Welford
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;  // ordering against a caller's stream
+  int fused_cfg = kFusedDefault;  // TMH_OPT_FUSED_CONFIG
+  int wf_parts = 0;               // TMH_OPT_WELFORD_PARTS (0: automatic)
+  bool hist_dirty = false;        // a fused launch may have left counts / round masks behind
   int64_t n = 0;              // sites accumulated (Welford count)
   int64_t n_deferred = 0;     // sites whose order statistics are stored
   int64_t last_batch = 0;
@@ -358,6 +362,8 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
       TMH_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
       TMH_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
       TMH_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+      TMH_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
+      TMH_HIP(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
       h->stream = h->own_stream;
       h->mean.alloc(npx, true);
       h->m2.alloc(npx, true);
@@ -406,6 +412,8 @@ void tmh_stats_destroy(tmh_stats* h) {
   if (side) (void)hipStreamSynchronize(side);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->ev_in) (void)hipEventDestroy(h->ev_in);
+  if (h->ev_out) (void)hipEventDestroy(h->ev_out);
   delete h;
   if (s) (void)hipStreamDestroy(s);
   if (side) (void)hipStreamDestroy(side);
@@ -418,9 +426,36 @@ int tmh_stats_set_stream(tmh_stats* h, void* stream) {
   });
 }
 
+int tmh_stats_set_option(tmh_stats* h, int option, int value) {
+  return guard([&] {
+    TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
+    switch (option) {
+      case TMH_OPT_FUSED_CONFIG:
+        TMH_CHECK(value >= 0 && value < kFusedConfigs, TMH_EINVAL, "fused configuration out of range");
+        h->fused_cfg = value;
+        break;
+      case TMH_OPT_WELFORD_PARTS:
+        TMH_CHECK(value >= 0 && value <= 4, TMH_EINVAL, "Welford parts must be 0..4");
+        h->wf_parts = value;
+        break;
+      default:
+        throw Error{TMH_EINVAL, "unknown option"};
+    }
+  });
+}
+
 int tmh_stats_reset(tmh_stats* h) {
   return guard([&] {
     TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
+    if (h->hist_dirty) {  // an interrupted fused launch: restore the zero-maintained slabs
+      TMH_HIP(hipDeviceSynchronize());  // it may have been queued on any stream
+      if (h->hist_full.n)
+        TMH_HIP(hipMemsetAsync(h->hist_full.p, 0, h->hist_full.n * 4, h->stream));
+      if (h->hist_rmask.n)
+        TMH_HIP(hipMemsetAsync(h->hist_rmask.p, 0, h->hist_rmask.n * 8, h->stream));
+      TMH_HIP(hipMemsetAsync(h->pooled_parts.p, 0, h->pooled_parts.n * 8, h->stream));
+      h->hist_dirty = false;
+    }
     TMH_HIP(hipMemsetAsync(h->mean.p, 0, h->npx * 8, h->stream));
     TMH_HIP(hipMemsetAsync(h->m2.p, 0, h->npx * 8, h->stream));
     TMH_HIP(hipMemsetAsync(h->acc.p, 0, (size_t)h->Q * 8, h->stream));
@@ -452,7 +487,7 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
     TMH_HIP(hipStreamWaitEvent(hs, h->ev_fork, 0));
   }
   launch_welford(d, h->npx, ns, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
-                 log_transform, h->wf_part.p, h->wf_part.n, s);
+                 log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, s);
   // order statistics, in chunks so the per-site slabs stay bounded
   for (int64_t c0 = 0; c0 < ns; c0 += chunk) {
     const int64_t nc = std::min(chunk, ns - c0);
@@ -483,7 +518,7 @@ int tmh_stats_update_welford_device(tmh_stats* h, const uint16_t* dev_sites, int
       h->rn.alloc((size_t)n_sites);
     }
     launch_welford(dev_sites, h->npx, n_sites, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
-                   log_transform, h->wf_part.p, h->wf_part.n, s);
+                   log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, s);
     h->n += n_sites;
     h->pending += n_sites;
   });
@@ -589,6 +624,32 @@ int tmh_stats_finalize_device(tmh_stats* h, double* dev_mean, double* dev_std, v
   return guard([&] {
     TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
     launch_finalize(h->mean.p, h->m2.p, h->n, h->npx, dev_mean, dev_std, pick(h->stream, stream));
+  });
+}
+
+int tmh_stats_variance(tmh_stats* h, double* host_var) {
+  return guard([&] {
+    TMH_CHECK(h && host_var, TMH_EINVAL, "bad arguments");
+    h->tmp_std.ensure(h->npx);
+    launch_variance(h->m2.p, h->n, h->npx, h->tmp_std.p, h->stream);
+    TMH_HIP(hipMemcpyAsync(host_var, h->tmp_std.p, h->npx * 8, hipMemcpyDeviceToHost, h->stream));
+    TMH_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int tmh_stats_get_hist_device(tmh_stats* h, uint64_t* dev_hist, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && dev_hist, TMH_EINVAL, "bad arguments");
+    TMH_HIP(hipMemcpyAsync(dev_hist, h->pooled.p, (size_t)kBins * 8, hipMemcpyDeviceToDevice,
+                           pick(h->stream, stream)));
+  });
+}
+
+int tmh_stats_set_hist_device(tmh_stats* h, const uint64_t* dev_hist, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && dev_hist, TMH_EINVAL, "bad arguments");
+    TMH_HIP(hipMemcpyAsync(h->pooled.p, dev_hist, (size_t)kBins * 8, hipMemcpyDeviceToDevice,
+                           pick(h->stream, stream)));
   });
 }
 
@@ -954,24 +1015,21 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
     TMH_CHECK(n_sites <= h->pending, TMH_ESTATE,
               "more sites than were passed to tmh_stats_update_welford_device");
     check_clip(clip_lo, clip_hi, 65535);
+    if (n_sites == 0) return;
     hipStream_t s = pick(c->stream, stream);
+    // Stream contract (include/tmhip.h): the launches below run on s, after
+    // everything already queued on the statistics handle's stream, and the
+    // handle's stream waits for them before any later work on the handle.
+    const bool cross = s != h->stream;
+    if (cross) {
+      TMH_HIP(hipEventRecord(h->ev_in, h->stream));
+      TMH_HIP(hipStreamWaitEvent(s, h->ev_in, 0));
+    }
     const bool vec = (h->npx & 7) == 0 && (reinterpret_cast<uintptr_t>(dev_in) & 15) == 0 &&
                      (reinterpret_cast<uintptr_t>(dev_out) & 15) == 0 &&
                      // the fused pass floors zero pixels at 10**zero_log10 in f32
                      (!c->log_transform || (c->zero_log10 >= -37.0 && c->zero_log10 <= 0.0));
-    if (vec && n_sites > 0) {
-      // Optional site chunks (TMH_CH_CHUNKS, default 1): chunk k's order
-      // statistics (hist finalize, ordered percentile sum) go to the side
-      // stream behind chunk k's correct+histogram pass, in chunk order (the
-      // percentile sums stay in site order).  Measured: no gain -- the
-      // persistent pass keeps every CU's slots until its queues drain, so the
-      // side-stream finalize only runs in the next chunk's tail.
-      static const int env_chunks = [] {
-        const char* e = getenv("TMH_CH_CHUNKS");
-        return e ? atoi(e) : 0;
-      }();
-      int nch = env_chunks > 0 ? env_chunks : 1;
-      nch = (int)std::min<int64_t>(nch, n_sites);
+    if (vec) {
       const bool grow = (size_t)n_sites * kBins > h->hist_full.n || (size_t)n_sites > h->zeros.n ||
                         (size_t)n_sites > h->hist_rmask.n ||
                         ((h->flags & 2u) && (size_t)n_sites * kBins > h->site_hist.n) ||
@@ -995,33 +1053,26 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         h->vlh.ensure((size_t)n_sites * h->Q);
         vlh = h->vlh.p;
       }
-      hipStream_t side = nch > 1 ? h->side : s;
-      for (int k = 0; k < nch; ++k) {
-        const int64_t c0 = n_sites * k / nch, nc = n_sites * (k + 1) / nch - c0;
-        launch_correct_hist(dev_in + c0 * h->npx, dev_out + c0 * h->npx, c->npx, nc, c->coef2.p,
-                            c->mconst2.p, c->log_transform, clip_lo, clip_hi,
-                            h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0,
-                            c->queues.p, c->n_wg, s);
-        if (side != s) {
-          TMH_HIP(hipEventRecord(h->ev_fork, s));
-          TMH_HIP(hipStreamWaitEvent(side, h->ev_fork, 0));
-        }
-        launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0,
-                             correct_hist_dense_rounds(), nc, h->qp,
-                             vlh + (size_t)c0 * h->Q, h->pooled.p, h->pooled_parts.p,
-                             kPooledParts, h->zeros.p + c0,
-                             (h->flags & 2u) ? h->site_hist.p + (size_t)c0 * kBins : nullptr,
-                             side);
-        if (!(h->flags & TMH_STATS_DEFERRED_PCT))
-          launch_pct_accumulate(vlh + (size_t)c0 * h->Q, nc, h->Q, h->gamma.p, h->acc.p, side);
-      }
-      if (side != s) {
-        TMH_HIP(hipEventRecord(h->ev_join, side));
-        TMH_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
-      }
+      // the histogram slab and round masks are zero-maintained: the fused pass
+      // fills them and k_hist_finalize resets what it read; if anything fails
+      // in between, tmh_stats_reset clears them (hist_dirty)
+      h->hist_dirty = true;
+      launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p,
+                          c->log_transform, clip_lo, clip_hi, h->hist_full.p, h->hist_rmask.p,
+                          c->queues.p, c->n_wg, h->fused_cfg, s);
+      launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, correct_hist_dense_rounds(h->fused_cfg),
+                           n_sites, h->qp, vlh, h->pooled.p, h->pooled_parts.p, kPooledParts,
+                           h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr, s);
+      if (!(h->flags & TMH_STATS_DEFERRED_PCT))
+        launch_pct_accumulate(vlh, n_sites, h->Q, h->gamma.p, h->acc.p, s);
+      h->hist_dirty = false;
       if (h->flags & TMH_STATS_DEFERRED_PCT) h->n_deferred += n_sites;
       h->last_batch = n_sites;
       h->pending -= n_sites;
+      if (cross) {
+        TMH_HIP(hipEventRecord(h->ev_out, s));
+        TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
+      }
       return;
     }
     const int64_t chunk = 4096;  // odd shapes: correct and histogram in two passes
@@ -1059,6 +1110,10 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         launch_pct_accumulate(vlh, nc, h->Q, h->gamma.p, h->acc.p, s);
       h->last_batch = nc;
       h->pending -= nc;
+    }
+    if (cross) {
+      TMH_HIP(hipEventRecord(h->ev_out, s));
+      TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
     }
   });
 }
@@ -1190,10 +1245,25 @@ int tmh_clip_u16(const uint16_t* host_in, uint16_t* host_out, int64_t n, int lo,
 // ---------------------------------------------------------------------------
 
 int tmh_synth_sites_device(uint16_t* dev_out, int64_t n_sites, int height, int width, uint64_t seed,
-                           int channel, int64_t first_site, void* stream) {
+                           int channel, int64_t first_site, int distribution, void* stream) {
   return guard([&] {
-    TMH_CHECK(dev_out && n_sites >= 0 && height > 0 && width > 0, TMH_EINVAL, "bad arguments");
-    launch_synth(dev_out, n_sites, height, width, seed, channel, first_site, (hipStream_t)stream);
+    TMH_CHECK(dev_out && n_sites >= 0 && height > 0 && width > 0 && first_site >= 0, TMH_EINVAL,
+              "bad arguments");
+    TMH_CHECK(distribution >= TMH_SYNTH_STANDARD && distribution <= TMH_SYNTH_UNIFORM, TMH_EINVAL,
+              "unknown distribution");
+    if (n_sites == 0) return;
+    launch_synth(dev_out, n_sites, height, width, seed, channel, first_site, distribution,
+                 (hipStream_t)stream);
+  });
+}
+
+int tmh_synth_tables(int distribution, int height, int width, int32_t* ln16, int32_t* nz16,
+                     int32_t* ey, int32_t* ex) {
+  return guard([&] {
+    TMH_CHECK(ln16 && nz16 && ey && ex && height > 0 && width > 0, TMH_EINVAL, "bad arguments");
+    TMH_CHECK(distribution >= TMH_SYNTH_STANDARD && distribution <= TMH_SYNTH_UNIFORM, TMH_EINVAL,
+              "unknown distribution");
+    synth_tables_host(distribution, height, width, ln16, nz16, ey, ex);
   });
 }
 

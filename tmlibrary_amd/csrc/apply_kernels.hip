@@ -104,19 +104,10 @@ void launch_smooth(const double* in, double* out, double* tmp, int H, int W, con
                    int radius, hipStream_t s) {
   ProfScope prof("smooth", s);
   const dim3 grid((unsigned)cdiv(W, 256), (unsigned)H);
-  static const int strip = [] {  // rows per thread of the axis-0 pass (TMH_SMOOTH_STRIP)
-    const char* e = getenv("TMH_SMOOTH_STRIP");
-    const int v = e ? atoi(e) : 16;  // 16: 1,350 workgroups at 2160x2560 (measured best)
-    return (v == 8 || v == 16 || v == 32) ? v : 16;
-  }();
   if (radius == 20) {  // sigma = 5, the reference's default (image.py:1172)
-    const dim3 g2((unsigned)cdiv(W, 256), (unsigned)cdiv(H, strip));
-    if (strip == 8)
-      hipLaunchKernelGGL((k_smooth_axis0_strip<8, 20>), g2, dim3(256), 0, s, in, tmp, H, W, d_w);
-    else if (strip == 16)
-      hipLaunchKernelGGL((k_smooth_axis0_strip<16, 20>), g2, dim3(256), 0, s, in, tmp, H, W, d_w);
-    else
-      hipLaunchKernelGGL((k_smooth_axis0_strip<32, 20>), g2, dim3(256), 0, s, in, tmp, H, W, d_w);
+    // 16 rows per thread: 1,350 workgroups at 2160x2560 (8 / 32 measured slower)
+    const dim3 g2((unsigned)cdiv(W, 256), (unsigned)cdiv(H, 16));
+    hipLaunchKernelGGL((k_smooth_axis0_strip<16, 20>), g2, dim3(256), 0, s, in, tmp, H, W, d_w);
   } else {
     hipLaunchKernelGGL(k_smooth_axis0, grid, dim3(256), 0, s, in, tmp, H, W, d_w, radius);
   }
@@ -442,53 +433,6 @@ __global__ void k_clip_u16(const uint16_t* __restrict__ in, uint16_t* __restrict
 
 void launch_clip_u16(const uint16_t* in, uint16_t* out, int64_t n, int lo, int hi, hipStream_t s) {
   hipLaunchKernelGGL(k_clip_u16, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, in, out, n, lo, hi);
-  TMH_HIP(hipGetLastError());
-}
-
-// ---------------------------------------------------------------------------
-// synthetic sites on device (SURVEY.md §8(d) distribution; counter-based)
-// ---------------------------------------------------------------------------
-
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-
-__global__ __launch_bounds__(256) void k_synth(uint16_t* __restrict__ out, int H, int W,
-                                               uint64_t key, int64_t first_site) {
-  const int64_t npx = (int64_t)H * W;
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t s = blockIdx.y;
-  if (p >= npx) return;
-  const uint64_t z1 = splitmix64(key ^ splitmix64((uint64_t)(first_site + s)) ^ (uint64_t)p);
-  const uint64_t z2 = splitmix64(z1);
-  const float u1 = ((float)(z1 >> 40) + 0.5f) * (1.0f / 16777216.0f);
-  const float u2 = (float)((z1 >> 16) & 0xFFFFFFu) * (1.0f / 16777216.0f);
-  const float u3 = (float)(z2 >> 40) * (1.0f / 16777216.0f);
-  const float rr = sqrtf(-2.0f * logf(u1));
-  const float n1 = rr * cospif(2.0f * u2), n2 = rr * sinpif(2.0f * u2);
-  const int y = (int)(p / W), x = (int)(p % W);
-  const float fy = (y - (H - 1) * 0.5f) / fmaxf(H * 0.5f, 1.0f);
-  const float fx = (x - (W - 1) * 0.5f) / fmaxf(W * 0.5f, 1.0f);
-  const float illum = expf(-1.5f * 0.5f * (fy * fy + fx * fx));
-  float v = 100.0f + illum * expf(6.0f + 0.6f * n1) + 5.0f * n2;
-  v = fminf(fmaxf(rintf(v), 0.0f), 65535.0f);
-  if (u3 < 1e-4f) v = 0.0f;
-  if (u3 > 1.0f - 1e-4f) v = 65535.0f;
-  out[s * npx + p] = (uint16_t)v;
-}
-
-void launch_synth(uint16_t* out, int64_t n_sites, int H, int W, uint64_t seed, int channel,
-                  int64_t first_site, hipStream_t s) {
-  const int64_t npx = (int64_t)H * W;
-  const uint64_t key = seed * 0x100000001B3ull ^ ((uint64_t)channel << 56);
-  for (int64_t s0 = 0; s0 < n_sites; s0 += 65535) {
-    const int64_t ns = (n_sites - s0 < 65535) ? n_sites - s0 : 65535;
-    hipLaunchKernelGGL(k_synth, dim3((unsigned)cdiv(npx, 256), (unsigned)ns), dim3(256), 0, s,
-                       out + s0 * npx, H, W, key, first_site + s0);
-  }
   TMH_HIP(hipGetLastError());
 }
 

@@ -64,9 +64,10 @@ struct QPos {
 
 // launches (defined in the .hip files) -------------------------------------------
 // part: optional scratch of part_cap doubles for site-split launches (null: one part)
+// forced_parts: 0 = pick the site split automatically, 1..4 = that many parts
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
-                    double* part, size_t part_cap, hipStream_t s);
+                    double* part, size_t part_cap, int forced_parts, hipStream_t s);
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
                          const QPos& p, uint32_t* vlh, unsigned long long* pooled,
                          int64_t* zero_counts, uint32_t* site_hist, hipStream_t s);
@@ -83,6 +84,8 @@ void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t l
                                  int q_count, const double* gamma, double* acc, hipStream_t s);
 void launch_finalize(const double* mean, const double* m2, int64_t n, int64_t npx, double* out_mean,
                      double* out_std, hipStream_t s);
+// var = M2 / (n - 1), NaN where n < 2 (stats.py:94-102)
+void launch_variance(const double* m2, int64_t n, int64_t npx, double* out_var, hipStream_t s);
 void launch_merge1(const double* mean, int64_t n, int64_t npx, double* nmean, hipStream_t s);
 void launch_merge2(double* mean, const double* m2, int64_t n_r, const double* sum_nmean,
                    int64_t n_total, int64_t npx, double* m2c, hipStream_t s);
@@ -104,11 +107,14 @@ void launch_correct_u16(const uint16_t* in, uint16_t* out, int64_t npx, int64_t 
 void launch_correct_u8(const uint8_t* in, uint8_t* out, int64_t npx, int64_t n_sites,
                        const float4* coef, const float2* lut, const float2* mconst,
                        int log_transform, int clip_lo, int clip_hi, hipStream_t s);
+// fused pass configurations (fused_kernels.hip kFusedCfgs); default kFusedDefault
+constexpr int kFusedConfigs = 4;
+constexpr int kFusedDefault = 3;
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, int log_transform,
                          int clip_lo, int clip_hi, uint32_t* hist, unsigned long long* rmask,
-                         int* queues, int n_wg, hipStream_t s);
-int correct_hist_dense_rounds();
+                         int* queues, int n_wg, int cfg, hipStream_t s);
+int correct_hist_dense_rounds(int cfg);
 void launch_coeffs2(const double* mean, const double* std, const double* sums, int64_t npx,
                     int log_transform, double zero_log10, float2* coef2, float4* mconst2,
                     float2* coef_lin, hipStream_t s);
@@ -121,7 +127,8 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
                      const tmh_window* d_win, int lo, int hi, hipStream_t s);
 void launch_clip_u16(const uint16_t* in, uint16_t* out, int64_t n, int lo, int hi, hipStream_t s);
 void launch_synth(uint16_t* out, int64_t n_sites, int H, int W, uint64_t seed, int channel,
-                  int64_t first_site, hipStream_t s);
+                  int64_t first_site, int dist, hipStream_t s);
+void synth_tables_host(int dist, int H, int W, int32_t* ln, int32_t* nz, int32_t* ey, int32_t* ex);
 
 __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

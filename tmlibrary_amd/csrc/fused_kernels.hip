@@ -28,13 +28,11 @@
 // log2 is v_log_f32 (<= 1 ulp: <= 0.1 DN at 65535); mean*log2(10) and
 // mean(std)/std are f32 (mean's rounding adds <= 0.05*a DN at 65535); zero
 // pixels take the reference's log10(1e-10) = -10.  Parity bar: +-1 DN.
-#include <cstdlib>
-
 #include "common.h"
 
 namespace tmh {
 
-constexpr int kBandsPerXcd = 2;  // default; TMH_FUSED_BANDS overrides (experiments)
+constexpr int kBandsPerXcd = 2;  // pixel bands per XCD queue
 constexpr double kLog2_10 = 3.32192809488736234787;
 
 __device__ __forceinline__ int xcc_id() {
@@ -315,55 +313,55 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   }
 }
 
-// (SPU, threads, LDS bins) configurations; TMH_FUSED_CFG selects (experiments)
-static int fused_cfg() {
-  static const int v = [] {
-    const char* e = getenv("TMH_FUSED_CFG");
-    const int x = e ? atoi(e) : 3;
-    return (x >= 0 && x <= 3) ? x : 3;
-  }();
-  return v;
-}
+// (sites per unit, threads, LDS bins) of the fused pass: ONE table drives both
+// the launch and the rounds k_hist_finalize treats as dense, so the two cannot
+// drift apart.  Selected per handle (tmh_stats_set_option, TMH_OPT_FUSED_CONFIG).
+struct FusedCfg {
+  int spu, threads, lds_bins;
+};
+constexpr FusedCfg kFusedCfgs[kFusedConfigs] = {
+    {2, 1024, 32768}, {4, 1024, 32768}, {2, 512, 16384}, {4, 512, 16384}};
+template <int K>
+struct FusedCfgCheck {
+  static_assert((kFusedCfgs[K].lds_bins / kFusedCfgs[K].spu) % 1024 == 0,
+                "LDS slices must cover whole 1,024-bin rounds");
+  static constexpr bool ok = true;
+};
+static_assert(FusedCfgCheck<0>::ok && FusedCfgCheck<1>::ok && FusedCfgCheck<2>::ok &&
+              FusedCfgCheck<3>::ok, "");
 
-// 1,024-bin rounds of every site's histogram that the current configuration
-// fills from its LDS slices (the rounds above are flagged in rmask per site)
-int correct_hist_dense_rounds() {
-  switch (fused_cfg()) {
-    case 0: return 32768 / 2 / 1024;
-    case 1: return 32768 / 4 / 1024;
-    case 2: return 16384 / 2 / 1024;
-    default: return 16384 / 4 / 1024;
-  }
+int correct_hist_dense_rounds(int cfg) {
+  const FusedCfg& c = kFusedCfgs[cfg];
+  return c.lds_bins / c.spu / 1024;
 }
 
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, int log_transform,
                          int clip_lo, int clip_hi, uint32_t* hist, unsigned long long* rmask,
-                         int* queues, int n_wg, hipStream_t s) {
+                         int* queues, int n_wg, int cfg, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("correct_hist", s);
-  static const int bpx = [] {
-    const char* e = getenv("TMH_FUSED_BANDS");
-    const int v = e ? atoi(e) : kBandsPerXcd;
-    return v >= 1 && v <= 16 ? v : kBandsPerXcd;
-  }();
   TMH_HIP(hipMemsetAsync(queues, 0, 8 * sizeof(int), s));
   const float4* cf4 = reinterpret_cast<const float4*>(coef2);
-#define TMH_LAUNCH_CH(L_, S_, T_, B_)                                                        \
-  if (clip_lo >= 0)                                                                              \
-    hipLaunchKernelGGL((k_correct_hist<L_, true, S_, 0, T_, B_>), dim3(n_wg * (1024 / T_)),      \
-                       dim3(T_), 0, s, in, out, npx, n_sites, cf4, mconst2, clip_lo, clip_hi,   \
-                       hist, rmask, queues, bpx);                                                \
-  else                                                                                           \
-    hipLaunchKernelGGL((k_correct_hist<L_, false, S_, 0, T_, B_>), dim3(n_wg * (1024 / T_)),     \
-                       dim3(T_), 0, s, in, out, npx, n_sites, cf4, mconst2, clip_lo, clip_hi,   \
-                       hist, rmask, queues, bpx)
-#define TMH_LAUNCH_CFG(L_)                                 \
-  switch (fused_cfg()) {                                   \
-    case 0: TMH_LAUNCH_CH(L_, 2, 1024, 32768); break;      \
-    case 1: TMH_LAUNCH_CH(L_, 4, 1024, 32768); break;      \
-    case 2: TMH_LAUNCH_CH(L_, 2, 512, 16384); break;       \
-    default: TMH_LAUNCH_CH(L_, 4, 512, 16384); break;      \
+#define TMH_LAUNCH_CH(L_, K_)                                                                    \
+  {                                                                                              \
+    constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
+    const dim3 grid(n_wg * (1024 / c.threads));                                                  \
+    if (clip_lo >= 0)                                                                            \
+      hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, 0, c.threads, c.lds_bins>), grid,     \
+                         dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, clip_lo,   \
+                         clip_hi, hist, rmask, queues, kBandsPerXcd);                            \
+    else                                                                                         \
+      hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, 0, c.threads, c.lds_bins>), grid,    \
+                         dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, clip_lo,   \
+                         clip_hi, hist, rmask, queues, kBandsPerXcd);                            \
+  }
+#define TMH_LAUNCH_CFG(L_)            \
+  switch (cfg) {                      \
+    case 0: TMH_LAUNCH_CH(L_, 0) break; \
+    case 1: TMH_LAUNCH_CH(L_, 1) break; \
+    case 2: TMH_LAUNCH_CH(L_, 2) break; \
+    default: TMH_LAUNCH_CH(L_, 3) break; \
   }
   if (log_transform) {
     TMH_LAUNCH_CFG(true);

@@ -20,7 +20,6 @@
 //                    FMA, so the sum is bit-identical to the reference's
 //                    sequential `_percentiles +=`.
 #include <algorithm>
-#include <cstdlib>
 
 #include "common.h"
 
@@ -282,12 +281,9 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_scalar(
 // groups leave the last round mostly empty (2160x2560: 2,700 workgroups over
 // 1,024 resident -> 2.64 rounds), splitting the sites into f parts evens it
 // out (f = 3: 7.9 rounds of 1/3 the work) for one extra pass over 16*f B/px
-// of partial state.  TMH_WF_PARTS overrides (experiments).
-static int welford_parts(int64_t n_wg, int64_t n_sites, int64_t npx, size_t part_cap) {
-  static const int forced = [] {
-    const char* e = getenv("TMH_WF_PARTS");
-    return e ? atoi(e) : 0;
-  }();
+// of partial state.  forced (tmh_stats_set_option TMH_OPT_WELFORD_PARTS, for
+// tests) overrides the choice where the split is possible.
+static int welford_parts(int64_t n_wg, int64_t n_sites, int64_t npx, size_t part_cap, int forced) {
   static const int64_t slots = [] {
     int dev = 0, cu = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -318,32 +314,24 @@ static int welford_parts(int64_t n_wg, int64_t n_sites, int64_t npx, size_t part
 
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
-                    double* part, size_t part_cap, hipStream_t s) {
+                    double* part, size_t part_cap, int forced_parts, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("welford", s);
   const bool vec = (npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0;
   if (vec) {
     const int64_t n_wg = cdiv(npx >> 3, kWfThreads);
-    const int f = part ? welford_parts(n_wg, n_sites, npx, part_cap) : 1;
+    const int f = part ? welford_parts(n_wg, n_sites, npx, part_cap, forced_parts) : 1;
     const int64_t per = cdiv(n_sites, f);
     const double nl = (double)n_sites, n = (double)(n0 + n_sites);
     const WfMerge mg{1.0 / nl, nl / n, (double)n0 * nl / n, n0 == 0};
     const dim3 grid((unsigned)n_wg, (unsigned)f);
-    static const bool ntl = [] {  // TMH_WF_NTL=0: regular site loads (A/B)
-      const char* e = getenv("TMH_WF_NTL");
-      return !(e && e[0] == '0');
-    }();
-    if (log_transform && ntl)
+    // site loads are non-temporal (streamed once; regular loads measured
+    // 6.60-6.75 vs 6.19-6.34 ms at job level, profiles/r1/ab_welford_ntl.txt)
+    if (log_transform)
       hipLaunchKernelGGL((k_welford_vec8<true, true>), grid, dim3(kWfThreads), 0, s, sites, npx,
                          n_sites, per, mg, mean, m2, lut, part);
-    else if (log_transform)
-      hipLaunchKernelGGL((k_welford_vec8<true, false>), grid, dim3(kWfThreads), 0, s, sites, npx,
-                         n_sites, per, mg, mean, m2, lut, part);
-    else if (ntl)
-      hipLaunchKernelGGL((k_welford_vec8<false, true>), grid, dim3(kWfThreads), 0, s, sites, npx,
-                         n_sites, per, mg, mean, m2, lut, part);
     else
-      hipLaunchKernelGGL((k_welford_vec8<false, false>), grid, dim3(kWfThreads), 0, s, sites, npx,
+      hipLaunchKernelGGL((k_welford_vec8<false, true>), grid, dim3(kWfThreads), 0, s, sites, npx,
                          n_sites, per, mg, mean, m2, lut, part);
     if (f > 1) {
       WfParts pc{};
@@ -806,21 +794,13 @@ void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t l
                                  int q_count, const double* gamma, double* acc, hipStream_t s) {
   if (n_sites <= 0 || q_count <= 0) return;
   ProfScope prof("pct_acc", s);
-  // regular (not non-temporal) loads of the order statistics: the kernel
-  // itself is 5% slower, but the next job's Welford and fused passes ran
-  // 0.35 ms faster in steady state (A/B x3 on one box); TMH_PCT_NTL=1 restores
-  static const bool ntl = [] {
-    const char* e = getenv("TMH_PCT_NTL");
-    return e && e[0] == '1';
-  }();
-  if (ntl)
-    hipLaunchKernelGGL(k_pct_acc<true>, dim3((unsigned)cdiv(q_count, kPctThreads)),
-                       dim3(kPctThreads), 0, s, vlh + q_begin, n_sites, q_count, ld,
-                       gamma + q_begin, acc);
-  else
-    hipLaunchKernelGGL(k_pct_acc<false>, dim3((unsigned)cdiv(q_count, kPctThreads)),
-                       dim3(kPctThreads), 0, s, vlh + q_begin, n_sites, q_count, ld,
-                       gamma + q_begin, acc);
+  // Regular (not non-temporal) loads of the order statistics.  PROVISIONAL:
+  // the kernel itself runs 5% slower with them, and the +1.7% job throughput
+  // measured for this choice (profiles/r1/ab_pct_ntl.txt) is within the
+  // run-to-run spread of one build (profiles/r1/noise_same_build.txt).
+  hipLaunchKernelGGL(k_pct_acc<false>, dim3((unsigned)cdiv(q_count, kPctThreads)),
+                     dim3(kPctThreads), 0, s, vlh + q_begin, n_sites, q_count, ld,
+                     gamma + q_begin, acc);
   TMH_HIP(hipGetLastError());
 }
 
@@ -834,6 +814,19 @@ __global__ void k_finalize(const double* __restrict__ mean, const double* __rest
   if (i >= npx) return;
   if (out_mean) out_mean[i] = mean[i];
   if (out_std) out_std[i] = (n < 2) ? __builtin_nan("") : sqrt(m2[i] / (double)(n - 1));
+}
+
+__global__ void k_variance(const double* __restrict__ m2, int64_t n, int64_t npx,
+                           double* __restrict__ out_var) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npx) return;
+  out_var[i] = (n < 2) ? __builtin_nan("") : m2[i] / (double)(n - 1);
+}
+
+void launch_variance(const double* m2, int64_t n, int64_t npx, double* out_var, hipStream_t s) {
+  hipLaunchKernelGGL(k_variance, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, m2, n, npx,
+                     out_var);
+  TMH_HIP(hipGetLastError());
 }
 
 void launch_finalize(const double* mean, const double* m2, int64_t n, int64_t npx, double* out_mean,

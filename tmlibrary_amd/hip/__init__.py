@@ -23,6 +23,12 @@ TMH_ESTATE = -71
 TMH_STATS_DEFERRED_PCT = 1
 TMH_STATS_KEEP_SITE_HIST = 2
 TMH_STATS_SERIAL = 4
+TMH_OPT_FUSED_CONFIG = 1
+TMH_OPT_WELFORD_PARTS = 2
+TMH_SYNTH_STANDARD = 0
+TMH_SYNTH_BRIGHT = 1
+TMH_SYNTH_UNIFORM = 2
+ABI_VERSION = 2
 
 _P = C.c_void_p
 _I64 = C.c_int64
@@ -40,6 +46,10 @@ SIGNATURES = {
     "tmh_stats_destroy": (None, [_P]),
     "tmh_stats_set_stream": (_I, [_P, _P]),
     "tmh_stats_reset": (_I, [_P]),
+    "tmh_stats_set_option": (_I, [_P, _I, _I]),
+    "tmh_stats_variance": (_I, [_P, _P]),
+    "tmh_stats_get_hist_device": (_I, [_P, _P, _P]),
+    "tmh_stats_set_hist_device": (_I, [_P, _P, _P]),
     "tmh_stats_update": (_I, [_P, _P, _I64, _I, _P]),
     "tmh_stats_update_device": (_I, [_P, _P, _I64, _I, _P]),
     "tmh_stats_update_welford_device": (_I, [_P, _P, _I64, _I, _P]),
@@ -70,7 +80,8 @@ SIGNATURES = {
     "tmh_map_u16_to_u8": (_I, [_P, _P, _I64, _I, _I]),
     "tmh_correct_chain_u8_device": (_I, [_P, _P, _P, _I64, _P, _I, _I, _P]),
     "tmh_correct_chain_u8": (_I, [_P, _P, _P, _I64, _P, _I, _I]),
-    "tmh_synth_sites_device": (_I, [_P, _I64, _I, _I, C.c_uint64, _I, _I64, _P]),
+    "tmh_synth_sites_device": (_I, [_P, _I64, _I, _I, C.c_uint64, _I, _I64, _I, _P]),
+    "tmh_synth_tables": (_I, [_I, _I, _I, _P, _P, _P, _P]),
     "tmh_malloc_device": (_I, [C.POINTER(_P), C.c_size_t]),
     "tmh_free_device": (_I, [_P]),
     "tmh_memcpy": (_I, [_P, _P, C.c_size_t, _I, _P]),
@@ -119,7 +130,7 @@ def lib() -> C.CDLL:
     with _lock:
         if _lib is None:
             L = load_library()
-            if L.tmh_abi_version() != 1:
+            if L.tmh_abi_version() != ABI_VERSION:
                 raise HipUnavailableError("libtmhip ABI version mismatch")
             n = C.c_int(0)
             rc = L.tmh_device_count(C.byref(n))

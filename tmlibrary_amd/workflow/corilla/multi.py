@@ -12,8 +12,9 @@ channel:
    result is the reference's sequential result over that order;
 2. decodes its block with the parallel inflate reader and accumulates it
    (``update_batch``);
-3. merges the partial statistics (Welford all-reduce + ordered percentile
-   chain, ``sharded.merge_shards``), so every rank holds identical results;
+3. merges the partial statistics (Welford all-reduce, ordered percentile
+   chain, histogram all-reduce: ``sharded.merge_shards``), so every rank
+   holds identical results (``stats.histogram``: the channel's pooled counts);
 4. rank 0 writes the ``IllumstatsFile`` (4-dataset HDF5 layout).
 
 The per-channel statistics object is pluggable (``stats_factory``): the
@@ -53,6 +54,7 @@ class GpuChannelStats(object):
 
     def merge(self, dist, group=None):
         if not self.merging or dist is None:
+            self.histogram = self.st.histogram
             return self.st.n
         import torch
         from tmlibrary_amd import hip
@@ -67,6 +69,7 @@ class GpuChannelStats(object):
         torch.cuda.current_stream(dev).synchronize()
         st._n_flushed = n_total  # the merged state is the whole channel's
         st._cache = None
+        self.histogram = st.histogram  # pooled over every rank's sites
         return n_total
 
     def container(self):

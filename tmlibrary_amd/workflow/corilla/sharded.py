@@ -14,7 +14,9 @@ kernels as a single GPU, then the partial states are merged:
             rank adds its own sites in order, reproducing the reference's
             sequential ``_percentiles +=`` bit for bit (a plain all-reduce sum
             would reassociate it); the last rank broadcasts the result.
-  histogram all-reduce of the pooled u64 counts (exact).
+  histogram  all-reduce(sum) of the pooled 65,536-bin counts (integer sums:
+            exact in any order), so every rank's ``OnlineStatistics.histogram``
+            is the whole channel's.
 
 Collectives use ``torch.distributed`` (backend "nccl" = RCCL over xGMI on
 MI355X) on device buffers; the arithmetic runs in libtmhip kernels through
@@ -82,15 +84,32 @@ class StatsOps(object):
     def set_pct_sum(self, acc):
         self._chk(self.L.tmh_stats_set_pct_sum(self.h, C.c_void_p(acc.data_ptr()), self._stream()))
 
+    def empty_hist(self):
+        # int64 on the wire (counts < 2**63; RCCL/gloo sum int64 exactly)
+        return self.torch.empty(65536, dtype=self.torch.int64, device=self.device)
 
-def merge_welford(ops, dist, group=None, int_device=None):
+    def get_hist(self, buf):
+        self._chk(self.L.tmh_stats_get_hist_device(self.h, C.c_void_p(buf.data_ptr()),
+                                                   self._stream()))
+
+    def set_hist(self, buf):
+        self._chk(self.L.tmh_stats_set_hist_device(self.h, C.c_void_p(buf.data_ptr()),
+                                                   self._stream()))
+
+
+def merge_welford(ops, dist, group=None, int_device=None, n_total=None):
     """All-reduce merge of every rank's Welford state (identical on all ranks).
-    Returns the global site count."""
+    Returns the global site count.  ``n_total`` (optional) is the global site
+    count when the caller already knows it (e.g. from the shard bounds): it
+    saves the count all-reduce, whose host read would block the issuing
+    thread until this rank's statistics pass has finished."""
     import torch
-    dev = int_device if int_device is not None else getattr(ops, "device", "cpu")
-    n_t = torch.tensor([ops.n_local()], dtype=torch.int64, device=dev)
-    dist.all_reduce(n_t, group=group)
-    n_total = int(n_t.item())
+    if n_total is None:
+        dev = int_device if int_device is not None else getattr(ops, "device", "cpu")
+        n_t = torch.tensor([ops.n_local()], dtype=torch.int64, device=dev)
+        dist.all_reduce(n_t, group=group)
+        n_total = int(n_t.item())
+    n_total = int(n_total)
     if n_total > 0:
         buf = ops.empty_plane()
         ops.stage1(buf)
@@ -142,16 +161,33 @@ def merge_percentiles(ops, dist, group=None, chunks=None):
     ops.set_pct_sum(acc)
 
 
+def merge_histogram(ops, dist, group=None):
+    """All-reduce of the pooled per-site histograms (exact integer sums)."""
+    buf = ops.empty_hist()
+    ops.get_hist(buf)
+    dist.all_reduce(buf, group=group)
+    ops.set_hist(buf)
+
+
+def merge_counts(ops, dist, group=None, chunks=None):
+    """The merges that need every site's histogram: the ordered percentile
+    chain and the pooled-histogram all-reduce (after the fused correct pass
+    in the split pipeline)."""
+    merge_percentiles(ops, dist, group, chunks)
+    merge_histogram(ops, dist, group)
+
+
 def merge_shards(ops, dist, group=None, int_device=None):
     """Merge every rank's partial statistics into identical global state
-    (Welford all-reduce merge, then the ordered percentile chain).
+    (Welford all-reduce merge, the ordered percentile chain and the
+    histogram all-reduce).
 
     ``ops`` provides n_local/empty_plane/empty_acc/stage1-3/pct_accumulate/
-    set_pct_sum on this rank's state; ``dist`` is torch.distributed.
-    Returns the global site count.
+    set_pct_sum/empty_hist/get_hist/set_hist on this rank's state; ``dist``
+    is torch.distributed.  Returns the global site count.
     """
     n_total = merge_welford(ops, dist, group, int_device)
-    merge_percentiles(ops, dist, group)
+    merge_counts(ops, dist, group)
     return n_total
 
 

@@ -36,7 +36,8 @@ DEFAULT_BATCH = 32
 class OnlineStatistics(object):
     """Welford mean/variance + percentile accumulator (stats.py:35-121)."""
 
-    def __init__(self, image_dimensions, decimals=3, batch_size=DEFAULT_BATCH, flags=0):
+    def __init__(self, image_dimensions, decimals=3, batch_size=DEFAULT_BATCH, flags=0,
+                 options=None):
         self.image_dimensions = tuple(int(d) for d in image_dimensions)
         if len(self.image_dimensions) != 2:
             raise ValueError("image_dimensions must be (height, width)")
@@ -62,6 +63,8 @@ class OnlineStatistics(object):
                                      hip.ptr(self._lut), self._batch_size, int(flags),
                                      C.byref(handle)))
         self._h = handle
+        for opt, val in (options or {}).items():  # launch shapes only (tmh_stats_set_option)
+            hip.check(L.tmh_stats_set_option(handle, int(opt), int(val)))
 
     # -- reference attributes ---------------------------------------------------
     @property
@@ -135,12 +138,13 @@ class OnlineStatistics(object):
     # -- results (stats.py:94-121) ----------------------------------------------
     @property
     def var(self):
+        """M2 / (n - 1), NaN where n < 2 (stats.py:94-102)."""
         c = self._finalize()
-        if c["n"] < 2:
-            v = np.zeros(self.image_dimensions, dtype=float)
-            v[:] = np.nan
-            return v
-        return c["std"] * c["std"]
+        if c.get("var") is None:
+            v = np.empty(self.image_dimensions, dtype=np.float64)
+            hip.check(hip.lib().tmh_stats_variance(self._h, hip.ptr(v)))
+            c["var"] = v
+        return c["var"].copy()
 
     @property
     def mean(self):

@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out
 TAG=${1:-run}
-timeout -k 10 900 python -m pytest tests -m gpu -q -ra --timeout=300 > gpurun_out/gpu_tests_$TAG.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v -ra --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/gpu_tests_$TAG.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
