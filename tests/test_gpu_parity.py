@@ -445,11 +445,15 @@ def _fused_job(L, sites, clip=(-1, -1), q=None):
     return res
 
 
-@pytest.mark.parametrize("kind", ["synth", "extremes", "uniform", "tiny", "many"])
+@pytest.mark.parametrize("kind", ["synth", "extremes", "uniform", "tiny", "many", "saturated"])
 def test_fused_correct_hist_pipeline(L, kind):
-    from tmlibrary_amd.synth import synth_sites_host
+    from tmlibrary_amd.synth import synth_exact_sites_host, synth_sites_host
     rng = np.random.default_rng(97)
-    if kind == "synth":
+    if kind == "saturated":  # corrected values far above 2**16 (f64 refinement, common.h)
+        sites = synth_exact_sites_host(6, 240, 320, 5, 0)
+        sites[:, ::7, ::5] = 65535
+        sites[1:, 3::11, 1::13] = 0
+    elif kind == "synth":
         sites = np.stack(synth_sites_host(7, 240, 320, seed=31))
         sites[2, :4, :4] = 65535
         sites[3, 5, :9] = 40000  # beyond the LDS bins and the LDS LUT

@@ -262,8 +262,11 @@ struct tmh_corrector {
   int log_transform = 1;
   double zero_log10 = -10.0;
   hipStream_t stream = nullptr;
-  DBuf<float4> coef, mconst2;
-  DBuf<float2> lut, mconst, coef2, coef_lin;
+  DBuf<float4> coef, mconst, mconst2;
+  DBuf<float2> lut, coef2, coef_lin;
+  DBuf<double2> coef64;              // f64 (mean, std): the refinement's operands
+  DBuf<RefineConst> rc;
+  DBuf<unsigned long long> amax;     // scratch: largest finite mean(std)/std
   DBuf<tmh_window> win;  // per-site alignment windows of the chain pass
   DBuf<int> queues;
   int n_wg = 256;
@@ -819,9 +822,9 @@ static void corrector_coeffs(tmh_corrector* c, const double* d_mean, const doubl
   ProfScope prof("coeffs", s);
   const int np = 1024;
   launch_reduce_sum2(d_std, d_mean, c->npx, c->partial.p, np, c->sums.p, s);
-  launch_coeffs(d_mean, d_std, c->sums.p, c->npx, c->coef.p, c->mconst.p, s);
-  launch_coeffs2(d_mean, d_std, c->sums.p, c->npx, c->log_transform, c->zero_log10, c->coef2.p,
-                 c->mconst2.p, c->coef_lin.p, s);
+  launch_coeffs_all(d_mean, d_std, c->sums.p, c->npx, c->log_transform, c->zero_log10, c->coef.p,
+                    c->mconst.p, c->coef2.p, c->mconst2.p, c->coef_lin.p, c->coef64.p, c->rc.p,
+                    c->amax.p, s);
 }
 
 static void corrector_init(tmh_corrector* c, const double* d_mean, const double* d_std) {
@@ -830,8 +833,11 @@ static void corrector_init(tmh_corrector* c, const double* d_mean, const double*
   c->coef.alloc(c->npx);
   c->coef2.alloc(c->npx);
   c->coef_lin.alloc(c->npx);
+  c->coef64.alloc(c->npx);
   c->mconst.alloc(1);
   c->mconst2.alloc(1);
+  c->rc.alloc(1);
+  c->amax.alloc(1);
   c->queues.alloc(8, true);
   TMH_HIP(hipDeviceGetAttribute(&c->n_wg, hipDeviceAttributeMultiprocessorCount, c->device));
   corrector_coeffs(c, d_mean, d_std, c->stream);
@@ -915,7 +921,8 @@ int tmh_correct_u16_device(tmh_corrector* c, const uint16_t* dev_in, uint16_t* d
     TMH_CHECK(c && (dev_in && dev_out || n_sites == 0) && n_sites >= 0, TMH_EINVAL, "bad arguments");
     check_clip(clip_lo, clip_hi, 65535);
     launch_correct_u16(dev_in, dev_out, c->npx, n_sites, c->coef.p, c->lut.p, c->mconst.p,
-                       c->log_transform, clip_lo, clip_hi, pick(c->stream, stream));
+                       c->coef64.p, c->rc.p, c->log_transform, clip_lo, clip_hi,
+                       pick(c->stream, stream));
   });
 }
 
@@ -968,8 +975,8 @@ int tmh_correct_u16(tmh_corrector* c, const uint16_t* host_in, uint16_t* host_ou
         TMH_HIP(hipMemcpyAsync(din, src, bytes, hipMemcpyHostToDevice, p.h2d));
         TMH_HIP(hipEventRecord(p.ev_in[slot], p.h2d));
         TMH_HIP(hipStreamWaitEvent(c->stream, p.ev_in[slot], 0));
-        launch_correct_u16(din, dout, c->npx, ns, c->coef.p, c->lut.p, c->mconst.p, c->log_transform,
-                           clip_lo, clip_hi, c->stream);
+        launch_correct_u16(din, dout, c->npx, ns, c->coef.p, c->lut.p, c->mconst.p, c->coef64.p,
+                           c->rc.p, c->log_transform, clip_lo, clip_hi, c->stream);
         TMH_HIP(hipEventRecord(p.ev_kern[slot], c->stream));
         TMH_HIP(hipStreamWaitEvent(p.d2h, p.ev_kern[slot], 0));
         TMH_HIP(hipMemcpyAsync(dst, dout, bytes, hipMemcpyDeviceToHost, p.d2h));
@@ -999,7 +1006,8 @@ int tmh_correct_u8(tmh_corrector* c, const uint8_t* host_in, uint8_t* host_out, 
     c->stage8_out.ensure(bytes);
     TMH_HIP(hipMemcpyAsync(c->stage8_in.p, host_in, bytes, hipMemcpyHostToDevice, c->stream));
     launch_correct_u8(c->stage8_in.p, c->stage8_out.p, c->npx, n_sites, c->coef.p, c->lut.p,
-                      c->mconst.p, c->log_transform, clip_lo, clip_hi, c->stream);
+                      c->mconst.p, c->coef64.p, c->rc.p, c->log_transform, clip_lo, clip_hi,
+                      c->stream);
     TMH_HIP(hipMemcpyAsync(host_out, c->stage8_out.p, bytes, hipMemcpyDeviceToHost, c->stream));
     TMH_HIP(hipStreamSynchronize(c->stream));
   });
@@ -1057,9 +1065,9 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       // fills them and k_hist_finalize resets what it read; if anything fails
       // in between, tmh_stats_reset clears them (hist_dirty)
       h->hist_dirty = true;
-      launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p,
-                          c->log_transform, clip_lo, clip_hi, h->hist_full.p, h->hist_rmask.p,
-                          c->queues.p, c->n_wg, h->fused_cfg, s);
+      launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p, c->coef64.p,
+                          c->rc.p, c->log_transform, clip_lo, clip_hi, h->hist_full.p,
+                          h->hist_rmask.p, c->queues.p, c->n_wg, h->fused_cfg, s);
       launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, correct_hist_dense_rounds(h->fused_cfg),
                            n_sites, h->qp, vlh, h->pooled.p, h->pooled_parts.p, kPooledParts,
                            h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr, s);
@@ -1100,8 +1108,8 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         vlh = h->vlh.p;
       }
       stats_reserve_sites(h, nc);
-      launch_correct_u16(din, dout, c->npx, nc, c->coef.p, c->lut.p, c->mconst.p, c->log_transform,
-                         clip_lo, clip_hi, s);
+      launch_correct_u16(din, dout, c->npx, nc, c->coef.p, c->lut.p, c->mconst.p, c->coef64.p,
+                         c->rc.p, c->log_transform, clip_lo, clip_hi, s);
       launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->qp, vlh, h->pooled.p, h->zeros.p,
                           (h->flags & 2u) ? h->site_hist.p : nullptr, s);
       if (h->flags & TMH_STATS_DEFERRED_PCT)
@@ -1199,8 +1207,8 @@ int tmh_correct_chain_u8_device(tmh_corrector* c, const uint16_t* dev_in, uint8_
     }
     TMH_HIP(hipMemcpyAsync(c->win.p, host_windows, (size_t)n_sites * sizeof(tmh_window),
                            hipMemcpyHostToDevice, s));
-    launch_chain_u8(dev_in, dev_out, c->H, c->W, n_sites, c->coef_lin.p, c->mconst2.p,
-                    c->log_transform, c->win.p, clip_lo, clip_hi, s);
+    launch_chain_u8(dev_in, dev_out, c->H, c->W, n_sites, c->coef_lin.p, c->mconst2.p, c->coef64.p,
+                    c->rc.p, c->log_transform, c->win.p, clip_lo, clip_hi, s);
     TMH_HIP(hipStreamSynchronize(s));  // the window buffer is reused by the next call
   });
 }

@@ -215,27 +215,81 @@ void launch_build_corr_lut(float2* lut, int log_transform, double zero_log10, hi
   TMH_HIP(hipGetLastError());
 }
 
-// coef[i] = (mean_hi, mean_lo, a = mean(std)/std, 0);  mconst = mean(mean) hi/lo
-__global__ void k_coeffs(const double* __restrict__ mean, const double* __restrict__ std,
-                         const double* __restrict__ sums, int64_t npx, float4* __restrict__ coef,
-                         float2* __restrict__ mconst) {
+constexpr double kLog2_10d = 3.32192809488736234787;
+
+// Every coefficient form of one (mean, std) pair, one thread per pixel i:
+//   coef[i]    = (mean hi, mean lo, a = mean(std)/std, 0)      LUT path
+//   coef2      = (mean [* log2 10], a) as f32, for npx % 8 == 0 pixel 8g+j in
+//                plane j/2 as float4 (mu_2p, mu_2p+1, a_2p, a_2p+1) at g: one
+//                16-B load gives a pixel pair its packed-f32 operands (fused pass)
+//   coef_lin[i] = the same pair in pixel order (the chain's shifted gathers)
+//   coef64[i]  = (mean, std) in f64 (the refinement, common.h)
+// and the largest finite a into *amax (u64 bits of a non-negative double).
+__global__ void k_coeffs_all(const double* __restrict__ mean, const double* __restrict__ std,
+                             const double* __restrict__ sums, int64_t npx, int log_transform,
+                             float4* __restrict__ coef, float* __restrict__ coef2,
+                             float2* __restrict__ coef_lin, double2* __restrict__ coef64,
+                             unsigned long long* __restrict__ amax) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const double S = sums[0] / (double)npx;  // np.mean(std)
-  const double M = sums[1] / (double)npx;  // np.mean(mean)
-  if (i == 0) {
-    const float mh = (float)M;
-    mconst[0] = make_float2(mh, (float)(M - (double)mh));
+  double am = 0.0;
+  if (i < npx) {
+    const double S = sums[0] / (double)npx;  // np.mean(std)
+    const double mu = mean[i], sd = std[i];
+    const double a = S / sd;
+    const float mh = (float)mu;
+    coef[i] = make_float4(mh, (float)(mu - (double)mh), (float)a, 0.0f);
+    const double K = log_transform ? kLog2_10d : 1.0;
+    int64_t om = 2 * i, oa = 2 * i + 1;
+    if ((npx & 7) == 0) {
+      const int64_t g = i >> 3, j = i & 7;
+      const int64_t base = (j >> 1) * (npx >> 1) + 4 * g + (j & 1);
+      om = base;
+      oa = base + 2;
+    }
+    const float mu2 = (float)(mu * K), af = (float)a;
+    coef2[om] = mu2;
+    coef2[oa] = af;
+    coef_lin[i] = make_float2(mu2, af);
+    coef64[i] = make_double2(mu, sd);
+    const double aa = fabs(a);
+    if (aa <= 1.7976931348623157e308) am = aa;  // finite (NaN fails the compare)
   }
-  if (i >= npx) return;
-  const double mu = mean[i];
-  const float mh = (float)mu;
-  coef[i] = make_float4(mh, (float)(mu - (double)mh), (float)(S / std[i]), 0.0f);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) am = fmax(am, __shfl_xor(am, off, 64));
+  if ((threadIdx.x & 63) == 0 && am > 0.0)
+    atomicMax(amax, (unsigned long long)__double_as_longlong(am));
 }
 
-void launch_coeffs(const double* mean, const double* std, const double* sums, int64_t npx,
-                   float4* coef, float2* mconst, hipStream_t s) {
-  hipLaunchKernelGGL(k_coeffs, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, mean, std, sums,
-                     npx, coef, mconst);
+// Launch constants: mconst = (M hi, M lo, T, 0) (LUT path), mconst2 = (M' hi,
+// M' lo, 10**zero_log10 as f32 (a zero pixel's floor), T) with M' = M [* log2
+// 10], and the refinement constants; T rounded down to f32.
+__global__ void k_refine_const(const double* __restrict__ sums, int64_t npx, int log_transform,
+                               double zero_log10, const unsigned long long* __restrict__ amax,
+                               float4* __restrict__ mconst, float4* __restrict__ mconst2,
+                               RefineConst* __restrict__ rc) {
+  const double S = sums[0] / (double)npx, M = sums[1] / (double)npx;
+  const double am = __longlong_as_double((long long)*amax);
+  const double T = 1.0 / (kRefineK1 * am + kRefineK2);
+  float Tf = (float)T;
+  if ((double)Tf > T) Tf = __uint_as_float(__float_as_uint(Tf) - 1u);  // T > 0: one f32 step down
+  const float mh = (float)M;
+  mconst[0] = make_float4(mh, (float)(M - (double)mh), Tf, 0.0f);
+  const double M2 = M * (log_transform ? kLog2_10d : 1.0);
+  const float m2h = (float)M2;
+  mconst2[0] = make_float4(m2h, (float)(M2 - (double)m2h), (float)exp10(zero_log10), Tf);
+  rc[0] = RefineConst{S, M, zero_log10, (double)Tf};
+}
+
+void launch_coeffs_all(const double* mean, const double* std, const double* sums, int64_t npx,
+                       int log_transform, double zero_log10, float4* coef, float4* mconst,
+                       float2* coef2, float4* mconst2, float2* coef_lin, double2* coef64,
+                       RefineConst* rc, unsigned long long* amax, hipStream_t s) {
+  TMH_HIP(hipMemsetAsync(amax, 0, sizeof(unsigned long long), s));
+  hipLaunchKernelGGL(k_coeffs_all, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, mean, std, sums,
+                     npx, log_transform, coef, reinterpret_cast<float*>(coef2), coef_lin, coef64,
+                     amax);
+  hipLaunchKernelGGL(k_refine_const, dim3(1), dim3(1), 0, s, sums, npx, log_transform, zero_log10,
+                     amax, mconst, mconst2, rc);
   TMH_HIP(hipGetLastError());
 }
 
@@ -254,16 +308,24 @@ __device__ __noinline__ float2 corr_log_slow(uint32_t u) {
   return make_float2(hi, (float)(L - (double)hi));
 }
 
-// the correction of one pixel given its log10 (hi, lo) (or value) L
+// the correction of one pixel u (pixel index p) given its log10 (hi, lo) (or
+// value) L; m = mconst (M hi, M lo, T, 0)
 template <bool LOG, int BITS>
-__device__ __forceinline__ uint32_t correct_l(float Lh, float Ll, const float4 c, float mh, float ml,
-                                              int clip_lo, int clip_hi) {
-  const float d = (Lh - c.x) + (Ll - c.y);       // (img - mean)
-  const float t = fmaf(d, c.z, mh) + ml;          // * mean(std)/std + mean(mean)
-  const float o = LOG ? exp2f(t * kLog2_10) : t;  // 10 ** t
+__device__ __forceinline__ uint32_t correct_l(float Lh, float Ll, const float4 c, const float4 m,
+                                              uint32_t u, int64_t p,
+                                              const double2* __restrict__ c64,
+                                              const RefineConst* __restrict__ rc, int clip_lo,
+                                              int clip_hi) {
+  const float d = (Lh - c.x) + (Ll - c.y);        // (img - mean)
+  const float t = fmaf(d, c.z, m.x) + m.y;         // * mean(std)/std + mean(mean)
+  const float o = LOG ? exp2f(t * kLog2_10) : t;   // 10 ** t
   // numpy float64 -> uint astype on x86: trunc to int32 (out of range/NaN ->
   // INT32_MIN), keep the low bits (image.py:631)
-  const int32_t iv = (o >= -2147483648.0f && o < 2147483648.0f) ? (int32_t)o : INT32_MIN;
+  int32_t iv = (o >= -2147483648.0f && o < 2147483648.0f) ? (int32_t)o : INT32_MIN;
+  if (__builtin_fabsf(o) >= m.z) {  // beyond the f32 error bound: f64 as the reference
+    const double2 q = c64[p];
+    iv = correct_ref_f64<LOG>(u, q.x, q.y, rc->S, rc->M, rc->zero_log10);
+  }
   uint32_t r = (uint32_t)iv & ((1u << BITS) - 1u);
   if (clip_lo >= 0) {
     r = r < (uint32_t)clip_lo ? (uint32_t)clip_lo : r;
@@ -274,7 +336,10 @@ __device__ __forceinline__ uint32_t correct_l(float Lh, float Ll, const float4 c
 
 template <bool LOG, int BITS>
 __device__ __forceinline__ uint32_t correct1(uint32_t u, const float4 c, const float2* slut,
-                                             float mh, float ml, int clip_lo, int clip_hi) {
+                                             const float4 m, int64_t p,
+                                             const double2* __restrict__ c64,
+                                             const RefineConst* __restrict__ rc, int clip_lo,
+                                             int clip_hi) {
   float2 l;
   if (LOG) {
     l = slut[u < (uint32_t)kLutLds ? u : 0u];
@@ -282,7 +347,7 @@ __device__ __forceinline__ uint32_t correct1(uint32_t u, const float4 c, const f
   } else {
     l = make_float2((float)u, 0.0f);
   }
-  return correct_l<LOG, BITS>(l.x, l.y, c, mh, ml, clip_lo, clip_hi);
+  return correct_l<LOG, BITS>(l.x, l.y, c, m, u, p, c64, rc, clip_lo, clip_hi);
 }
 
 // streamed-once site data: non-temporal loads / stores
@@ -303,7 +368,8 @@ template <bool LOG>
 __global__ __launch_bounds__(kCorrThreads) void k_correct_u16_vec8(
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
     const float4* __restrict__ coef, const float2* __restrict__ lut,
-    const float2* __restrict__ mconst, int clip_lo, int clip_hi) {
+    const float4* __restrict__ mconst, const double2* __restrict__ c64,
+    const RefineConst* __restrict__ rc, int clip_lo, int clip_hi) {
   __shared__ float2 slut[kLutLds];
   if (LOG)
     for (int i = threadIdx.x; i < kLutLds; i += kCorrThreads) slut[i] = lut[i];
@@ -311,7 +377,7 @@ __global__ __launch_bounds__(kCorrThreads) void k_correct_u16_vec8(
   const int64_t ngroups = npx >> 3;
   const int64_t g = (int64_t)blockIdx.x * kCorrThreads + threadIdx.x;
   if (g >= ngroups) return;
-  const float2 m = mconst[0];
+  const float4 m = mconst[0];
   float4 c[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) c[k] = coef[g * 8 + k];
@@ -340,7 +406,9 @@ __global__ __launch_bounds__(kCorrThreads) void k_correct_u16_vec8(
     }
     uint32_t o[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = correct_l<LOG, 16>(l[k].x, l[k].y, c[k], m.x, m.y, clip_lo, clip_hi);
+    for (int k = 0; k < 8; ++k)
+      o[k] = correct_l<LOG, 16>(l[k].x, l[k].y, c[k], m, u[k], g * 8 + k, c64, rc, clip_lo,
+                                clip_hi);
     return make_uint4(o[0] | (o[1] << 16), o[2] | (o[3] << 16), o[4] | (o[5] << 16),
                       o[6] | (o[7] << 16));
   };
@@ -366,22 +434,25 @@ template <bool LOG, typename T, int BITS>
 __global__ __launch_bounds__(kCorrThreads) void k_correct_scalar(
     const T* __restrict__ in, T* __restrict__ out, int64_t npx, int64_t n_sites,
     const float4* __restrict__ coef, const float2* __restrict__ lut,
-    const float2* __restrict__ mconst, int clip_lo, int clip_hi) {
+    const float4* __restrict__ mconst, const double2* __restrict__ c64,
+    const RefineConst* __restrict__ rc, int clip_lo, int clip_hi) {
   __shared__ float2 slut[kLutLds];
   if (LOG)
     for (int i = threadIdx.x; i < kLutLds; i += kCorrThreads) slut[i] = lut[i];
   __syncthreads();
   const int64_t p = (int64_t)blockIdx.x * kCorrThreads + threadIdx.x;
   if (p >= npx) return;
-  const float2 m = mconst[0];
+  const float4 m = mconst[0];
   const float4 c = coef[p];
   for (int64_t s = 0; s < n_sites; ++s)
-    out[s * npx + p] = (T)correct1<LOG, BITS>(in[s * npx + p], c, slut, m.x, m.y, clip_lo, clip_hi);
+    out[s * npx + p] =
+        (T)correct1<LOG, BITS>(in[s * npx + p], c, slut, m, p, c64, rc, clip_lo, clip_hi);
 }
 
 void launch_correct_u16(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
-                        const float4* coef, const float2* lut, const float2* mconst,
-                        int log_transform, int clip_lo, int clip_hi, hipStream_t s) {
+                        const float4* coef, const float2* lut, const float4* mconst,
+                        const double2* coef64, const RefineConst* rc, int log_transform,
+                        int clip_lo, int clip_hi, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("correct", s);
   const bool vec = (npx & 7) == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
@@ -390,34 +461,35 @@ void launch_correct_u16(const uint16_t* in, uint16_t* out, int64_t npx, int64_t 
     const dim3 grid((unsigned)cdiv(npx >> 3, kCorrThreads));
     if (log_transform)
       hipLaunchKernelGGL(k_correct_u16_vec8<true>, grid, dim3(kCorrThreads), 0, s, in, out, npx,
-                         n_sites, coef, lut, mconst, clip_lo, clip_hi);
+                         n_sites, coef, lut, mconst, coef64, rc, clip_lo, clip_hi);
     else
       hipLaunchKernelGGL(k_correct_u16_vec8<false>, grid, dim3(kCorrThreads), 0, s, in, out, npx,
-                         n_sites, coef, lut, mconst, clip_lo, clip_hi);
+                         n_sites, coef, lut, mconst, coef64, rc, clip_lo, clip_hi);
   } else {
     const dim3 grid((unsigned)cdiv(npx, kCorrThreads));
     if (log_transform)
       hipLaunchKernelGGL((k_correct_scalar<true, uint16_t, 16>), grid, dim3(kCorrThreads), 0, s, in,
-                         out, npx, n_sites, coef, lut, mconst, clip_lo, clip_hi);
+                         out, npx, n_sites, coef, lut, mconst, coef64, rc, clip_lo, clip_hi);
     else
       hipLaunchKernelGGL((k_correct_scalar<false, uint16_t, 16>), grid, dim3(kCorrThreads), 0, s,
-                         in, out, npx, n_sites, coef, lut, mconst, clip_lo, clip_hi);
+                         in, out, npx, n_sites, coef, lut, mconst, coef64, rc, clip_lo, clip_hi);
   }
   TMH_HIP(hipGetLastError());
 }
 
 void launch_correct_u8(const uint8_t* in, uint8_t* out, int64_t npx, int64_t n_sites,
-                       const float4* coef, const float2* lut, const float2* mconst,
-                       int log_transform, int clip_lo, int clip_hi, hipStream_t s) {
+                       const float4* coef, const float2* lut, const float4* mconst,
+                       const double2* coef64, const RefineConst* rc, int log_transform,
+                       int clip_lo, int clip_hi, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("correct_u8", s);
   const dim3 grid((unsigned)cdiv(npx, kCorrThreads));
   if (log_transform)
     hipLaunchKernelGGL((k_correct_scalar<true, uint8_t, 8>), grid, dim3(kCorrThreads), 0, s, in,
-                       out, npx, n_sites, coef, lut, mconst, clip_lo, clip_hi);
+                       out, npx, n_sites, coef, lut, mconst, coef64, rc, clip_lo, clip_hi);
   else
     hipLaunchKernelGGL((k_correct_scalar<false, uint8_t, 8>), grid, dim3(kCorrThreads), 0, s, in,
-                       out, npx, n_sites, coef, lut, mconst, clip_lo, clip_hi);
+                       out, npx, n_sites, coef, lut, mconst, coef64, rc, clip_lo, clip_hi);
   TMH_HIP(hipGetLastError());
 }
 

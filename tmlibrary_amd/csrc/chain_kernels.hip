@@ -66,12 +66,20 @@ __device__ __forceinline__ uint32_t clip_scale8(uint32_t v16, int lo, int hi, in
   return i >= (uint32_t)T ? 255u : (uint32_t)((double)i * step);
 }
 
+// one pixel px (index p) of the packed-f32 correction; m = mconst2 (M' hi,
+// M' lo, zf, T): beyond T the f64 refinement (common.h)
 template <bool LOG>
-__device__ __forceinline__ uint32_t correct16(uint32_t px, float mu, float a, float mh, float zf) {
+__device__ __forceinline__ uint32_t correct16(uint32_t px, float mu, float a, const float4 m,
+                                              int64_t p, const double2* __restrict__ c64,
+                                              const RefineConst* __restrict__ rc) {
   float L = (float)px;
-  if (LOG) L = __builtin_amdgcn_logf(__builtin_fmaxf(L, zf));
-  const float t = fmaf(L - mu, a, mh);
+  if (LOG) L = __builtin_amdgcn_logf(__builtin_fmaxf(L, m.z));
+  const float t = fmaf(L - mu, a, m.x);
   float o = LOG ? __builtin_amdgcn_exp2f(t) : t;
+  if (__builtin_fabsf(o) >= m.w) {
+    const double2 q = c64[p];
+    return (uint32_t)correct_ref_f64<LOG>(px, q.x, q.y, rc->S, rc->M, rc->zero_log10) & 0xFFFFu;
+  }
   o = __builtin_fminf(o, 2147418112.0f);  // >= 2^31, inf, NaN -> low half 0 (x86 astype)
   if (!LOG) o = __builtin_fmaxf(o, -2147483648.0f);
   return (uint32_t)(int32_t)o & 0xFFFFu;
@@ -142,6 +150,8 @@ __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ i
                                                    int64_t n_sites, int64_t per,
                                                    const float2* __restrict__ coef_lin,
                                                    const float4* __restrict__ mconst2,
+                                                   const double2* __restrict__ c64,
+                                                   const RefineConst* __restrict__ rc,
                                                    const tmh_window* __restrict__ win, int lo,
                                                    int hi, int T, double step) {
   // LUT: the reference's uint8 table for the clipped range [lo, hi] staged in
@@ -211,14 +221,38 @@ __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ i
 #pragma unroll
     for (int k = 0; k < 4; ++k) t[k] = __builtin_elementwise_fma(t[k] - mu[k], a[k], M);
     uint32_t o[8];
+    float ox[8];
+    uint32_t far = 0;  // pixels beyond the f32 bound: f64 refinement (common.h)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        float x = LOG ? __builtin_amdgcn_exp2f(t[k][h]) : t[k][h];
-        x = __builtin_fminf(x, 2147418112.0f);  // >= 2^31, inf, NaN -> low half 0 (x86)
-        if (!LOG) x = __builtin_fmaxf(x, -2147483648.0f);
-        const uint32_t v16 = (uint32_t)(int32_t)x & 0xFFFFu;
+        const float x = LOG ? __builtin_amdgcn_exp2f(t[k][h]) : t[k][h];
+        far |= (__builtin_fabsf(x) >= m.w ? 1u : 0u) << (2 * k + h);
+        ox[2 * k + h] = x;
+      }
+    }
+    int32_t iv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float x = __builtin_fminf(ox[j], 2147418112.0f);  // >= 2^31, inf, NaN -> low half 0 (x86)
+      if (!LOG) x = __builtin_fmaxf(x, -2147483648.0f);
+      iv[j] = (int32_t)x;
+    }
+    if (far) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if ((far >> j) & 1u) {
+          const double2 q = c64[p0 + j];
+          iv[j] = correct_ref_f64<LOG>((wd[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, q.x, q.y, rc->S,
+                                       rc->M, rc->zero_log10);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t v16 = (uint32_t)iv[2 * k + h] & 0xFFFFu;
         const uint32_t v = min(max(v16, (uint32_t)lo), (uint32_t)hi);  // np.clip
         o[2 * k + h] = LUT ? (uint32_t)slut[v - (uint32_t)lo]
                            : (v - (uint32_t)lo >= (uint32_t)T ? 255u
@@ -310,6 +344,8 @@ __global__ __launch_bounds__(256) void k_chain_u8_scalar(const uint16_t* __restr
                                                           int64_t n_sites,
                                                           const float2* __restrict__ coef_lin,
                                                           const float4* __restrict__ mconst2,
+                                                          const double2* __restrict__ c64,
+                                                          const RefineConst* __restrict__ rc,
                                                           const tmh_window* __restrict__ win,
                                                           int lo, int hi, int T, double step) {
   const int64_t npx = (int64_t)H * W;
@@ -323,7 +359,7 @@ __global__ __launch_bounds__(256) void k_chain_u8_scalar(const uint16_t* __restr
     if (in_window(r, c, w)) {
       const int64_t p = (int64_t)(r - w.dst_r0 + w.src_r0) * W + (c - w.dst_c0 + w.src_c0);
       const float2 k = coef_lin[p];
-      v = clip_scale8(correct16<LOG>(in[s * npx + p], k.x, k.y, m.x, m.z), lo, hi, T, step);
+      v = clip_scale8(correct16<LOG>(in[s * npx + p], k.x, k.y, m, p, c64, rc), lo, hi, T, step);
     }
     out[s * npx + i] = (uint8_t)v;
   }
@@ -352,8 +388,9 @@ void launch_map_u8(const uint16_t* in, uint8_t* out, int64_t n, int lo, int hi, 
 }
 
 void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_sites,
-                     const float2* coef_lin, const float4* mconst2, int log_transform,
-                     const tmh_window* d_win, int lo, int hi, hipStream_t s) {
+                     const float2* coef_lin, const float4* mconst2, const double2* coef64,
+                     const RefineConst* rc, int log_transform, const tmh_window* d_win, int lo,
+                     int hi, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("chain", s);
   const int64_t npx = (int64_t)H * W;
@@ -371,7 +408,7 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
     const size_t shm = lut ? (size_t)((lut_bytes + 15) & ~15) : 0;
 #define TMH_CHAIN(L_, U_)                                                                     \
   hipLaunchKernelGGL((k_chain_u8<L_, U_>), grid, dim3(256), shm, s, in, out, H, W, n_sites, per, \
-                     coef_lin, mconst2, d_win, lo, hi, T, step)
+                     coef_lin, mconst2, coef64, rc, d_win, lo, hi, T, step)
     if (log_transform) {
       if (lut) TMH_CHAIN(true, true); else TMH_CHAIN(true, false);
     } else {
@@ -384,10 +421,10 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
     const dim3 grid((unsigned)cdiv(npx, 256));
     if (log_transform)
       hipLaunchKernelGGL(k_chain_u8_scalar<true>, grid, dim3(256), 0, s, in, out, H, W, n_sites,
-                         coef_lin, mconst2, d_win, lo, hi, T, step);
+                         coef_lin, mconst2, coef64, rc, d_win, lo, hi, T, step);
     else
       hipLaunchKernelGGL(k_chain_u8_scalar<false>, grid, dim3(256), 0, s, in, out, H, W, n_sites,
-                         coef_lin, mconst2, d_win, lo, hi, T, step);
+                         coef_lin, mconst2, coef64, rc, d_win, lo, hi, T, step);
   }
   TMH_HIP(hipGetLastError());
 }

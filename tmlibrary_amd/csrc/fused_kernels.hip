@@ -33,7 +33,6 @@
 namespace tmh {
 
 constexpr int kBandsPerXcd = 2;  // pixel bands per XCD queue
-constexpr double kLog2_10 = 3.32192809488736234787;
 
 __device__ __forceinline__ int xcc_id() {
   int x;
@@ -57,11 +56,15 @@ constexpr float kCastTop = 2147418112.0f;
 // their one-pass hazard.  A zero pixel takes log2(zf), zf = 10**zero_log10 as
 // f32 (1e-10f: v_log_f32 is within 1 ulp of the reference's log10(1e-10) =
 // -10, scaled): one v_max instead of a compare + select.  The caller keeps zf
-// in [FLT_MIN, 1].
+// in [FLT_MIN, 1].  Pixels whose f32 result reaches T (mconst2.w, the f32
+// error bound's limit, common.h) are recomputed in f64 from c64 (their
+// (mean, std)), exactly as the reference: rare (saturated pixels in dim
+// corners), one wave-uniform test per 8 pixels otherwise.
 template <bool LOG, bool CLIP>
 __device__ __forceinline__ void fcorrect8(const uint32_t (&w)[4], const float4 (&k)[4], float mh,
-                                          float zf, uint32_t clip_lo2, uint32_t clip_hi2,
-                                          uint32_t (&r)[4]) {
+                                          float zf, float T, uint32_t clip_lo2, uint32_t clip_hi2,
+                                          const double2* __restrict__ c64g,
+                                          const RefineConst* __restrict__ rc, uint32_t (&r)[4]) {
   f32x2_t t[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -86,15 +89,29 @@ __device__ __forceinline__ void fcorrect8(const uint32_t (&w)[4], const float4 (
     o[2 * p] = LOG ? __builtin_amdgcn_exp2f(t[p].x) : t[p].x;  // v_exp_f32
     o[2 * p + 1] = LOG ? __builtin_amdgcn_exp2f(t[p].y) : t[p].y;
   }
+  uint32_t far = 0;  // pixels beyond the f32 bound
+#pragma unroll
+  for (int j = 0; j < 8; ++j) far |= (__builtin_fabsf(o[j]) >= T ? 1u : 0u) << j;
+  int32_t iv[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     o[j] = __builtin_fminf(o[j], kCastTop);
     if (!LOG) o[j] = __builtin_fmaxf(o[j], -2147483648.0f);  // t may be negative: stay in range
+    iv[j] = (int32_t)o[j];
+  }
+  if (far) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if ((far >> j) & 1u) {
+        const double2 q = c64g[j];
+        const uint32_t u = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+        iv[j] = correct_ref_f64<LOG>(u, q.x, q.y, rc->S, rc->M, rc->zero_log10);
+      }
+    }
   }
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    r[p] = __builtin_amdgcn_perm((uint32_t)(int32_t)o[2 * p + 1], (uint32_t)(int32_t)o[2 * p],
-                                 0x05040100u);
+    r[p] = __builtin_amdgcn_perm((uint32_t)iv[2 * p + 1], (uint32_t)iv[2 * p], 0x05040100u);
     if (CLIP) {  // np.clip on the wrapped uint16 values, both halves at once
       typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
       u16x2_t v = __builtin_bit_cast(u16x2_t, r[p]);
@@ -139,7 +156,8 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 template <bool LOG, bool CLIP, int SPU, int ABL, int NT, int LB>
 __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void k_correct_hist(
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
-    const float4* __restrict__ coef, const float4* __restrict__ mconst2, int clip_lo,
+    const float4* __restrict__ coef, const float4* __restrict__ mconst2,
+    const double2* __restrict__ coef64, const RefineConst* __restrict__ rc, int clip_lo,
     int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
     int* __restrict__ queues, int bands_per_xcd) {
   constexpr int BINS = LB / SPU;
@@ -229,7 +247,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     if (nxt >= 0) nu = decode(nxt);
     uint32_t* hs = hist + un.s0 * (int64_t)kBins;
 
-    auto process = [&](const uint4 w, const int k, const float4 (&cf)[4]) -> u32x4_t {
+    auto process = [&](const uint4 w, const int k, const float4 (&cf)[4], const int g) -> u32x4_t {
       const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
       if (!(ABL & 1)) {
         uint32_t* sl = bins + k * SLICE;
@@ -258,7 +276,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
         }
       }
       uint32_t o[4];
-      fcorrect8<LOG, CLIP>(wd, cf, m.x, m.z, clo2, chi2, o);
+      fcorrect8<LOG, CLIP>(wd, cf, m.x, m.z, m.w, clo2, chi2, coef64 + (int64_t)g * 8, rc, o);
       const u32x4_t r = {o[0], o[1], o[2], o[3]};
       return r;
     };
@@ -283,7 +301,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
 #pragma unroll
       for (int k = 0; k < SPU; ++k)
         if (k < un.ns)
-          __builtin_amdgcn_raw_buffer_store_b128(process(v[k], k, c), un.rout, g * 16,
+          __builtin_amdgcn_raw_buffer_store_b128(process(v[k], k, c, g), un.rout, g * 16,
                                                  k * site_bytes, 2);
 #pragma unroll
       for (int k = 0; k < SPU; ++k) v[k] = vn[k];
@@ -336,9 +354,10 @@ int correct_hist_dense_rounds(int cfg) {
 }
 
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
-                         const float2* coef2, const float4* mconst2, int log_transform,
-                         int clip_lo, int clip_hi, uint32_t* hist, unsigned long long* rmask,
-                         int* queues, int n_wg, int cfg, hipStream_t s) {
+                         const float2* coef2, const float4* mconst2, const double2* coef64,
+                         const RefineConst* rc, int log_transform, int clip_lo, int clip_hi,
+                         uint32_t* hist, unsigned long long* rmask, int* queues, int n_wg, int cfg,
+                         hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("correct_hist", s);
   TMH_HIP(hipMemsetAsync(queues, 0, 8 * sizeof(int), s));
@@ -349,12 +368,12 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
     const dim3 grid(n_wg * (1024 / c.threads));                                                  \
     if (clip_lo >= 0)                                                                            \
       hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, 0, c.threads, c.lds_bins>), grid,     \
-                         dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, clip_lo,   \
-                         clip_hi, hist, rmask, queues, kBandsPerXcd);                            \
+                         dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, coef64, rc,   \
+                         clip_lo, clip_hi, hist, rmask, queues, kBandsPerXcd);                   \
     else                                                                                         \
       hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, 0, c.threads, c.lds_bins>), grid,    \
-                         dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, clip_lo,   \
-                         clip_hi, hist, rmask, queues, kBandsPerXcd);                            \
+                         dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, coef64, rc,   \
+                         clip_lo, clip_hi, hist, rmask, queues, kBandsPerXcd);                   \
   }
 #define TMH_LAUNCH_CFG(L_)            \
   switch (cfg) {                      \
@@ -370,49 +389,6 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
   }
 #undef TMH_LAUNCH_CFG
 #undef TMH_LAUNCH_CH
-  TMH_HIP(hipGetLastError());
-}
-
-// coef2 = per pixel (f32 mean [*log2(10) when log], f32 mean(std)/std): the
-// compact form the fused pass keeps L2-resident.  For npx % 8 == 0 (the only
-// case the fused pass runs) pixel 8g+j is stored in plane p = j/2 as the
-// float4 (mu_2p, mu_2p+1, a_2p, a_2p+1) at index g, so one 16-B load gives a
-// pixel pair its operands for the packed f32 ops.  mconst2 = (M' hi, M' lo,
-// 10**zero_log10 (the value a zero pixel takes before the log), 0) with
-// M' = mean(mean) [*log2(10)].  coef_lin (optional) holds the same pairs in
-// pixel order for the chain pass's shifted gathers.
-__global__ void k_coeffs2(const double* __restrict__ mean, const double* __restrict__ std,
-                          const double* __restrict__ sums, int64_t npx, int log_transform,
-                          double zero_log10, float* __restrict__ coef2,
-                          float4* __restrict__ mconst2, float2* __restrict__ coef_lin) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const double K = log_transform ? kLog2_10 : 1.0;
-  if (i == 0) {
-    const double M = sums[1] / (double)npx * K;
-    const float mh = (float)M;
-    mconst2[0] = make_float4(mh, (float)(M - (double)mh), (float)exp10(zero_log10), 0.f);
-  }
-  if (i >= npx) return;
-  const double S = sums[0] / (double)npx;
-  int64_t om = 2 * i, oa = 2 * i + 1;
-  if ((npx & 7) == 0) {
-    const int64_t g = i >> 3, j = i & 7;
-    const int64_t base = (j >> 1) * (npx >> 1) + 4 * g + (j & 1);
-    om = base;
-    oa = base + 2;
-  }
-  const float mu = (float)(mean[i] * K), a = (float)(S / std[i]);
-  coef2[om] = mu;
-  coef2[oa] = a;
-  if (coef_lin) coef_lin[i] = make_float2(mu, a);  // pixel order (shifted gathers)
-}
-
-void launch_coeffs2(const double* mean, const double* std, const double* sums, int64_t npx,
-                    int log_transform, double zero_log10, float2* coef2, float4* mconst2,
-                    float2* coef_lin, hipStream_t s) {
-  hipLaunchKernelGGL(k_coeffs2, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, mean, std, sums,
-                     npx, log_transform, zero_log10, reinterpret_cast<float*>(coef2), mconst2,
-                     coef_lin);
   TMH_HIP(hipGetLastError());
 }
 
