@@ -266,7 +266,8 @@ struct tmh_corrector {
   DBuf<float2> lut, coef2, coef_lin;
   DBuf<double2> coef64;              // f64 (mean, std): the refinement's operands
   DBuf<RefineConst> rc;
-  DBuf<unsigned long long> amax;     // scratch: largest finite mean(std)/std
+  DBuf<unsigned long long> fix_e;    // pixels flagged for the f64 refinement (common.h)
+  DBuf<unsigned int> fix_n;
   DBuf<tmh_window> win;  // per-site alignment windows of the chain pass
   DBuf<int> queues;
   int n_wg = 256;
@@ -823,13 +824,12 @@ static void corrector_coeffs(tmh_corrector* c, const double* d_mean, const doubl
   const int np = 1024;
   launch_reduce_sum2(d_std, d_mean, c->npx, c->partial.p, np, c->sums.p, s);
   launch_coeffs_all(d_mean, d_std, c->sums.p, c->npx, c->log_transform, c->zero_log10, c->coef.p,
-                    c->mconst.p, c->coef2.p, c->mconst2.p, c->coef_lin.p, c->coef64.p, c->rc.p,
-                    c->amax.p, s);
+                    c->mconst.p, c->coef2.p, c->mconst2.p, c->coef_lin.p, c->coef64.p, c->rc.p, s);
 }
 
 static void corrector_init(tmh_corrector* c, const double* d_mean, const double* d_std) {
-  c->sums.alloc(2);
-  c->partial.alloc(2 * 1024);
+  c->sums.alloc(3);
+  c->partial.alloc(3 * 1024);
   c->coef.alloc(c->npx);
   c->coef2.alloc(c->npx);
   c->coef_lin.alloc(c->npx);
@@ -837,10 +837,25 @@ static void corrector_init(tmh_corrector* c, const double* d_mean, const double*
   c->mconst.alloc(1);
   c->mconst2.alloc(1);
   c->rc.alloc(1);
-  c->amax.alloc(1);
+  c->fix_n.alloc(1, true);
   c->queues.alloc(8, true);
   TMH_HIP(hipDeviceGetAttribute(&c->n_wg, hipDeviceAttributeMultiprocessorCount, c->device));
   corrector_coeffs(c, d_mean, d_std, c->stream);
+}
+
+// The refinement list of one correct launch over n_sites sites on stream s:
+// capacity for 1/1024 of the launch's pixels (an overflow makes the fixup
+// recompute every pixel in f64: slow but exact), count reset on s.  One
+// launch at a time per corrector (the list is reused).
+static FixList corrector_fixlist(tmh_corrector* c, int64_t n_sites, hipStream_t s) {
+  const int64_t want = std::min<int64_t>(std::max<int64_t>((int64_t)1 << 20, n_sites * c->npx / 1024),
+                                         (int64_t)1 << 30);
+  if ((size_t)want > c->fix_e.n) {
+    TMH_HIP(hipDeviceSynchronize());  // the list may be in use on any stream
+    c->fix_e.alloc((size_t)want);
+  }
+  TMH_HIP(hipMemsetAsync(c->fix_n.p, 0, sizeof(unsigned int), s));
+  return FixList{c->fix_e.p, c->fix_n.p, (unsigned int)c->fix_e.n};
 }
 
 int tmh_corrector_create_device(const double* dev_mean, const double* dev_std, int height,
@@ -920,9 +935,12 @@ int tmh_correct_u16_device(tmh_corrector* c, const uint16_t* dev_in, uint16_t* d
   return guard([&] {
     TMH_CHECK(c && (dev_in && dev_out || n_sites == 0) && n_sites >= 0, TMH_EINVAL, "bad arguments");
     check_clip(clip_lo, clip_hi, 65535);
-    launch_correct_u16(dev_in, dev_out, c->npx, n_sites, c->coef.p, c->lut.p, c->mconst.p,
-                       c->coef64.p, c->rc.p, c->log_transform, clip_lo, clip_hi,
-                       pick(c->stream, stream));
+    hipStream_t s = pick(c->stream, stream);
+    const FixList fl = corrector_fixlist(c, n_sites, s);
+    launch_correct_u16(dev_in, dev_out, c->npx, n_sites, c->coef.p, c->lut.p, c->mconst.p, fl,
+                       c->log_transform, clip_lo, clip_hi, s);
+    launch_fix_correct(dev_in, dev_out, 2, c->npx, n_sites, fl, c->coef64.p, c->rc.p,
+                       c->log_transform, clip_lo, clip_hi, s);
   });
 }
 
@@ -975,8 +993,11 @@ int tmh_correct_u16(tmh_corrector* c, const uint16_t* host_in, uint16_t* host_ou
         TMH_HIP(hipMemcpyAsync(din, src, bytes, hipMemcpyHostToDevice, p.h2d));
         TMH_HIP(hipEventRecord(p.ev_in[slot], p.h2d));
         TMH_HIP(hipStreamWaitEvent(c->stream, p.ev_in[slot], 0));
-        launch_correct_u16(din, dout, c->npx, ns, c->coef.p, c->lut.p, c->mconst.p, c->coef64.p,
-                           c->rc.p, c->log_transform, clip_lo, clip_hi, c->stream);
+        const FixList fl = corrector_fixlist(c, ns, c->stream);
+        launch_correct_u16(din, dout, c->npx, ns, c->coef.p, c->lut.p, c->mconst.p, fl,
+                           c->log_transform, clip_lo, clip_hi, c->stream);
+        launch_fix_correct(din, dout, 2, c->npx, ns, fl, c->coef64.p, c->rc.p, c->log_transform,
+                           clip_lo, clip_hi, c->stream);
         TMH_HIP(hipEventRecord(p.ev_kern[slot], c->stream));
         TMH_HIP(hipStreamWaitEvent(p.d2h, p.ev_kern[slot], 0));
         TMH_HIP(hipMemcpyAsync(dst, dout, bytes, hipMemcpyDeviceToHost, p.d2h));
@@ -1005,9 +1026,11 @@ int tmh_correct_u8(tmh_corrector* c, const uint8_t* host_in, uint8_t* host_out, 
     c->stage8_in.ensure(bytes);
     c->stage8_out.ensure(bytes);
     TMH_HIP(hipMemcpyAsync(c->stage8_in.p, host_in, bytes, hipMemcpyHostToDevice, c->stream));
+    const FixList fl = corrector_fixlist(c, n_sites, c->stream);
     launch_correct_u8(c->stage8_in.p, c->stage8_out.p, c->npx, n_sites, c->coef.p, c->lut.p,
-                      c->mconst.p, c->coef64.p, c->rc.p, c->log_transform, clip_lo, clip_hi,
-                      c->stream);
+                      c->mconst.p, fl, c->log_transform, clip_lo, clip_hi, c->stream);
+    launch_fix_correct(c->stage8_in.p, c->stage8_out.p, 1, c->npx, n_sites, fl, c->coef64.p,
+                       c->rc.p, c->log_transform, clip_lo, clip_hi, c->stream);
     TMH_HIP(hipMemcpyAsync(host_out, c->stage8_out.p, bytes, hipMemcpyDeviceToHost, c->stream));
     TMH_HIP(hipStreamSynchronize(c->stream));
   });
@@ -1065,9 +1088,12 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       // fills them and k_hist_finalize resets what it read; if anything fails
       // in between, tmh_stats_reset clears them (hist_dirty)
       h->hist_dirty = true;
-      launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p, c->coef64.p,
-                          c->rc.p, c->log_transform, clip_lo, clip_hi, h->hist_full.p,
-                          h->hist_rmask.p, c->queues.p, c->n_wg, h->fused_cfg, s);
+      const FixList fl = corrector_fixlist(c, n_sites, s);
+      launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p, fl,
+                          c->log_transform, clip_lo, clip_hi, h->hist_full.p, h->hist_rmask.p,
+                          c->queues.p, c->n_wg, h->fused_cfg, s);
+      launch_fix_correct(dev_in, dev_out, 2, c->npx, n_sites, fl, c->coef64.p, c->rc.p,
+                         c->log_transform, clip_lo, clip_hi, s);
       launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, correct_hist_dense_rounds(h->fused_cfg),
                            n_sites, h->qp, vlh, h->pooled.p, h->pooled_parts.p, kPooledParts,
                            h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr, s);
@@ -1108,8 +1134,11 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         vlh = h->vlh.p;
       }
       stats_reserve_sites(h, nc);
-      launch_correct_u16(din, dout, c->npx, nc, c->coef.p, c->lut.p, c->mconst.p, c->coef64.p,
-                         c->rc.p, c->log_transform, clip_lo, clip_hi, s);
+      const FixList fl = corrector_fixlist(c, nc, s);
+      launch_correct_u16(din, dout, c->npx, nc, c->coef.p, c->lut.p, c->mconst.p, fl,
+                         c->log_transform, clip_lo, clip_hi, s);
+      launch_fix_correct(din, dout, 2, c->npx, nc, fl, c->coef64.p, c->rc.p, c->log_transform,
+                         clip_lo, clip_hi, s);
       launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->qp, vlh, h->pooled.p, h->zeros.p,
                           (h->flags & 2u) ? h->site_hist.p : nullptr, s);
       if (h->flags & TMH_STATS_DEFERRED_PCT)
@@ -1207,8 +1236,9 @@ int tmh_correct_chain_u8_device(tmh_corrector* c, const uint16_t* dev_in, uint8_
     }
     TMH_HIP(hipMemcpyAsync(c->win.p, host_windows, (size_t)n_sites * sizeof(tmh_window),
                            hipMemcpyHostToDevice, s));
-    launch_chain_u8(dev_in, dev_out, c->H, c->W, n_sites, c->coef_lin.p, c->mconst2.p, c->coef64.p,
-                    c->rc.p, c->log_transform, c->win.p, clip_lo, clip_hi, s);
+    const FixList fl = corrector_fixlist(c, n_sites, s);
+    launch_chain_u8(dev_in, dev_out, c->H, c->W, n_sites, c->coef_lin.p, c->mconst2.p, fl,
+                    c->coef64.p, c->rc.p, c->log_transform, c->win.p, clip_lo, clip_hi, s);
     TMH_HIP(hipStreamSynchronize(s));  // the window buffer is reused by the next call
   });
 }

@@ -154,8 +154,20 @@ __global__ __launch_bounds__(256) void k_reduce_final(const double* __restrict__
   if (threadIdx.x == 0) *out = t;
 }
 
+__device__ __forceinline__ double block_min256(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = fmin(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  return red[0];
+}
+
 // sums of two planes at once (np.mean(std), np.mean(mean) of image.py:627):
-// blockIdx.y selects the plane, fixed partition -> deterministic
+// blockIdx.y selects the plane, fixed partition -> deterministic.  The std
+// plane's blocks also take the smallest positive finite value (the largest
+// mean(std)/std, which sets the refinement threshold, common.h).
 __global__ __launch_bounds__(256) void k_reduce_partial2(const double* __restrict__ x0,
                                                          const double* __restrict__ x1, int64_t n,
                                                          double* __restrict__ partial) {
@@ -164,16 +176,32 @@ __global__ __launch_bounds__(256) void k_reduce_partial2(const double* __restric
   const int64_t chunk = cdiv(n, gridDim.x);
   const int64_t b = (int64_t)blockIdx.x * chunk;
   const int64_t e = (b + chunk < n) ? b + chunk : n;
-  double acc = 0.0;
-  for (int64_t i = b + threadIdx.x; i < e; i += 256) acc += x[i];
+  double acc = 0.0, mn = __builtin_inf();
+  for (int64_t i = b + threadIdx.x; i < e; i += 256) {
+    const double v = x[i];
+    acc += v;
+    if (v > 0.0 && v < mn) mn = v;  // NaN fails both; +inf never below mn
+  }
   const double t = block_sum256(acc, red);
   if (threadIdx.x == 0) partial[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = t;
+  if (blockIdx.y == 0) {
+    __syncthreads();
+    const double m = block_min256(mn, red);
+    if (threadIdx.x == 0) partial[(int64_t)2 * gridDim.x + blockIdx.x] = m;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_reduce_final2(const double* __restrict__ partial, int n,
                                                        double* __restrict__ out) {
   __shared__ double red[256];
   const double* p = partial + (int64_t)blockIdx.x * n;
+  if (blockIdx.x == 2) {
+    double mn = __builtin_inf();
+    for (int i = threadIdx.x; i < n; i += 256) mn = fmin(mn, p[i]);
+    const double m = block_min256(mn, red);
+    if (threadIdx.x == 0) out[2] = m;
+    return;
+  }
   double acc = 0.0;
   for (int i = threadIdx.x; i < n; i += 256) acc += p[i];
   const double t = block_sum256(acc, red);
@@ -183,7 +211,7 @@ __global__ __launch_bounds__(256) void k_reduce_final2(const double* __restrict_
 void launch_reduce_sum2(const double* x0, const double* x1, int64_t n, double* partial,
                         int n_partial, double* out, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce_partial2, dim3(n_partial, 2), dim3(256), 0, s, x0, x1, n, partial);
-  hipLaunchKernelGGL(k_reduce_final2, dim3(2), dim3(256), 0, s, partial, n_partial, out);
+  hipLaunchKernelGGL(k_reduce_final2, dim3(3), dim3(256), 0, s, partial, n_partial, out);
   TMH_HIP(hipGetLastError());
 }
 
@@ -224,51 +252,42 @@ constexpr double kLog2_10d = 3.32192809488736234787;
 //                16-B load gives a pixel pair its packed-f32 operands (fused pass)
 //   coef_lin[i] = the same pair in pixel order (the chain's shifted gathers)
 //   coef64[i]  = (mean, std) in f64 (the refinement, common.h)
-// and the largest finite a into *amax (u64 bits of a non-negative double).
 __global__ void k_coeffs_all(const double* __restrict__ mean, const double* __restrict__ std,
                              const double* __restrict__ sums, int64_t npx, int log_transform,
                              float4* __restrict__ coef, float* __restrict__ coef2,
-                             float2* __restrict__ coef_lin, double2* __restrict__ coef64,
-                             unsigned long long* __restrict__ amax) {
+                             float2* __restrict__ coef_lin, double2* __restrict__ coef64) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  double am = 0.0;
-  if (i < npx) {
-    const double S = sums[0] / (double)npx;  // np.mean(std)
-    const double mu = mean[i], sd = std[i];
-    const double a = S / sd;
-    const float mh = (float)mu;
-    coef[i] = make_float4(mh, (float)(mu - (double)mh), (float)a, 0.0f);
-    const double K = log_transform ? kLog2_10d : 1.0;
-    int64_t om = 2 * i, oa = 2 * i + 1;
-    if ((npx & 7) == 0) {
-      const int64_t g = i >> 3, j = i & 7;
-      const int64_t base = (j >> 1) * (npx >> 1) + 4 * g + (j & 1);
-      om = base;
-      oa = base + 2;
-    }
-    const float mu2 = (float)(mu * K), af = (float)a;
-    coef2[om] = mu2;
-    coef2[oa] = af;
-    coef_lin[i] = make_float2(mu2, af);
-    coef64[i] = make_double2(mu, sd);
-    const double aa = fabs(a);
-    if (aa <= 1.7976931348623157e308) am = aa;  // finite (NaN fails the compare)
+  if (i >= npx) return;
+  const double S = sums[0] / (double)npx;  // np.mean(std)
+  const double mu = mean[i], sd = std[i];
+  const double a = S / sd;
+  const float mh = (float)mu;
+  coef[i] = make_float4(mh, (float)(mu - (double)mh), (float)a, 0.0f);
+  const double K = log_transform ? kLog2_10d : 1.0;
+  int64_t om = 2 * i, oa = 2 * i + 1;
+  if ((npx & 7) == 0) {
+    const int64_t g = i >> 3, j = i & 7;
+    const int64_t base = (j >> 1) * (npx >> 1) + 4 * g + (j & 1);
+    om = base;
+    oa = base + 2;
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) am = fmax(am, __shfl_xor(am, off, 64));
-  if ((threadIdx.x & 63) == 0 && am > 0.0)
-    atomicMax(amax, (unsigned long long)__double_as_longlong(am));
+  const float mu2 = (float)(mu * K), af = (float)a;
+  coef2[om] = mu2;
+  coef2[oa] = af;
+  coef_lin[i] = make_float2(mu2, af);
+  coef64[i] = make_double2(mu, sd);
 }
 
 // Launch constants: mconst = (M hi, M lo, T, 0) (LUT path), mconst2 = (M' hi,
 // M' lo, 10**zero_log10 as f32 (a zero pixel's floor), T) with M' = M [* log2
-// 10], and the refinement constants; T rounded down to f32.
+// 10], and the refinement constants; a_max = S / (smallest positive std), T
+// rounded down to f32.
 __global__ void k_refine_const(const double* __restrict__ sums, int64_t npx, int log_transform,
-                               double zero_log10, const unsigned long long* __restrict__ amax,
-                               float4* __restrict__ mconst, float4* __restrict__ mconst2,
-                               RefineConst* __restrict__ rc) {
+                               double zero_log10, float4* __restrict__ mconst,
+                               float4* __restrict__ mconst2, RefineConst* __restrict__ rc) {
   const double S = sums[0] / (double)npx, M = sums[1] / (double)npx;
-  const double am = __longlong_as_double((long long)*amax);
+  double am = fabs(S / sums[2]);  // sums[2] = +inf (no positive std): 0
+  if (!(am <= 1.7976931348623157e308)) am = 0.0;  // S inf/NaN: every pixel is inf/NaN anyway
   const double T = 1.0 / (kRefineK1 * am + kRefineK2);
   float Tf = (float)T;
   if ((double)Tf > T) Tf = __uint_as_float(__float_as_uint(Tf) - 1u);  // T > 0: one f32 step down
@@ -283,13 +302,74 @@ __global__ void k_refine_const(const double* __restrict__ sums, int64_t npx, int
 void launch_coeffs_all(const double* mean, const double* std, const double* sums, int64_t npx,
                        int log_transform, double zero_log10, float4* coef, float4* mconst,
                        float2* coef2, float4* mconst2, float2* coef_lin, double2* coef64,
-                       RefineConst* rc, unsigned long long* amax, hipStream_t s) {
-  TMH_HIP(hipMemsetAsync(amax, 0, sizeof(unsigned long long), s));
+                       RefineConst* rc, hipStream_t s) {
   hipLaunchKernelGGL(k_coeffs_all, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, mean, std, sums,
-                     npx, log_transform, coef, reinterpret_cast<float*>(coef2), coef_lin, coef64,
-                     amax);
+                     npx, log_transform, coef, reinterpret_cast<float*>(coef2), coef_lin, coef64);
   hipLaunchKernelGGL(k_refine_const, dim3(1), dim3(1), 0, s, sums, npx, log_transform, zero_log10,
-                     amax, mconst, mconst2, rc);
+                     mconst, mconst2, rc);
+  TMH_HIP(hipGetLastError());
+}
+
+// The f64 refinement of the pixels a correct launch flagged: e = site << 32 |
+// pixel, written as the launch would (low BITS bits, clip).  If the list
+// overflowed, every pixel of the launch is recomputed in f64.
+template <bool LOG, typename T, int BITS>
+__global__ __launch_bounds__(256) void k_fix_correct(const T* __restrict__ in, T* __restrict__ out,
+                                                     int64_t npx, int64_t n_sites, FixList fl,
+                                                     const double2* __restrict__ c64,
+                                                     const RefineConst* __restrict__ rc,
+                                                     int clip_lo, int clip_hi) {
+  const unsigned int n = *fl.n;
+  const bool all = n > fl.cap;
+  const int64_t total = all ? n_sites * npx : (int64_t)n;
+  if (total == 0) return;
+  const RefineConst k = *rc;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * 256) {
+    int64_t s, p;
+    if (all) {
+      s = i / npx;
+      p = i - s * npx;
+    } else {
+      const unsigned long long e = fl.e[i];
+      s = (int64_t)(e >> 32);
+      p = (int64_t)(e & 0xFFFFFFFFull);
+    }
+    const double2 q = c64[p];
+    uint32_t r = (uint32_t)correct_ref_f64<LOG>(in[s * npx + p], q.x, q.y, k.S, k.M, k.zero_log10) &
+                 ((1u << BITS) - 1u);
+    if (clip_lo >= 0) {
+      r = r < (uint32_t)clip_lo ? (uint32_t)clip_lo : r;
+      r = r > (uint32_t)clip_hi ? (uint32_t)clip_hi : r;
+    }
+    out[s * npx + p] = (T)r;
+  }
+}
+
+void launch_fix_correct(const void* in, void* out, int elem_bytes, int64_t npx, int64_t n_sites,
+                        const FixList& fl, const double2* coef64, const RefineConst* rc,
+                        int log_transform, int clip_lo, int clip_hi, hipStream_t s) {
+  if (n_sites <= 0) return;
+  const dim3 grid(512), block(256);
+  if (elem_bytes == 2) {
+    auto i16 = static_cast<const uint16_t*>(in);
+    auto o16 = static_cast<uint16_t*>(out);
+    if (log_transform)
+      hipLaunchKernelGGL((k_fix_correct<true, uint16_t, 16>), grid, block, 0, s, i16, o16, npx,
+                         n_sites, fl, coef64, rc, clip_lo, clip_hi);
+    else
+      hipLaunchKernelGGL((k_fix_correct<false, uint16_t, 16>), grid, block, 0, s, i16, o16, npx,
+                         n_sites, fl, coef64, rc, clip_lo, clip_hi);
+  } else {
+    auto i8 = static_cast<const uint8_t*>(in);
+    auto o8 = static_cast<uint8_t*>(out);
+    if (log_transform)
+      hipLaunchKernelGGL((k_fix_correct<true, uint8_t, 8>), grid, block, 0, s, i8, o8, npx, n_sites,
+                         fl, coef64, rc, clip_lo, clip_hi);
+    else
+      hipLaunchKernelGGL((k_fix_correct<false, uint8_t, 8>), grid, block, 0, s, i8, o8, npx,
+                         n_sites, fl, coef64, rc, clip_lo, clip_hi);
+  }
   TMH_HIP(hipGetLastError());
 }
 
@@ -310,22 +390,19 @@ __device__ __noinline__ float2 corr_log_slow(uint32_t u) {
 
 // the correction of one pixel u (pixel index p) given its log10 (hi, lo) (or
 // value) L; m = mconst (M hi, M lo, T, 0)
+// (site s): a result beyond the f32 error bound T = m.z is flagged for the
+// f64 refinement (common.h)
 template <bool LOG, int BITS>
 __device__ __forceinline__ uint32_t correct_l(float Lh, float Ll, const float4 c, const float4 m,
-                                              uint32_t u, int64_t p,
-                                              const double2* __restrict__ c64,
-                                              const RefineConst* __restrict__ rc, int clip_lo,
-                                              int clip_hi) {
+                                              int64_t s, int64_t p, const FixList& fl,
+                                              int clip_lo, int clip_hi) {
   const float d = (Lh - c.x) + (Ll - c.y);        // (img - mean)
   const float t = fmaf(d, c.z, m.x) + m.y;         // * mean(std)/std + mean(mean)
   const float o = LOG ? exp2f(t * kLog2_10) : t;   // 10 ** t
+  if (__builtin_fabsf(o) >= m.z) fix_push(fl, s, p);
   // numpy float64 -> uint astype on x86: trunc to int32 (out of range/NaN ->
   // INT32_MIN), keep the low bits (image.py:631)
-  int32_t iv = (o >= -2147483648.0f && o < 2147483648.0f) ? (int32_t)o : INT32_MIN;
-  if (__builtin_fabsf(o) >= m.z) {  // beyond the f32 error bound: f64 as the reference
-    const double2 q = c64[p];
-    iv = correct_ref_f64<LOG>(u, q.x, q.y, rc->S, rc->M, rc->zero_log10);
-  }
+  const int32_t iv = (o >= -2147483648.0f && o < 2147483648.0f) ? (int32_t)o : INT32_MIN;
   uint32_t r = (uint32_t)iv & ((1u << BITS) - 1u);
   if (clip_lo >= 0) {
     r = r < (uint32_t)clip_lo ? (uint32_t)clip_lo : r;
@@ -336,10 +413,8 @@ __device__ __forceinline__ uint32_t correct_l(float Lh, float Ll, const float4 c
 
 template <bool LOG, int BITS>
 __device__ __forceinline__ uint32_t correct1(uint32_t u, const float4 c, const float2* slut,
-                                             const float4 m, int64_t p,
-                                             const double2* __restrict__ c64,
-                                             const RefineConst* __restrict__ rc, int clip_lo,
-                                             int clip_hi) {
+                                             const float4 m, int64_t s, int64_t p,
+                                             const FixList& fl, int clip_lo, int clip_hi) {
   float2 l;
   if (LOG) {
     l = slut[u < (uint32_t)kLutLds ? u : 0u];
@@ -347,7 +422,7 @@ __device__ __forceinline__ uint32_t correct1(uint32_t u, const float4 c, const f
   } else {
     l = make_float2((float)u, 0.0f);
   }
-  return correct_l<LOG, BITS>(l.x, l.y, c, m, u, p, c64, rc, clip_lo, clip_hi);
+  return correct_l<LOG, BITS>(l.x, l.y, c, m, s, p, fl, clip_lo, clip_hi);
 }
 
 // streamed-once site data: non-temporal loads / stores
@@ -368,8 +443,7 @@ template <bool LOG>
 __global__ __launch_bounds__(kCorrThreads) void k_correct_u16_vec8(
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
     const float4* __restrict__ coef, const float2* __restrict__ lut,
-    const float4* __restrict__ mconst, const double2* __restrict__ c64,
-    const RefineConst* __restrict__ rc, int clip_lo, int clip_hi) {
+    const float4* __restrict__ mconst, FixList fl, int clip_lo, int clip_hi) {
   __shared__ float2 slut[kLutLds];
   if (LOG)
     for (int i = threadIdx.x; i < kLutLds; i += kCorrThreads) slut[i] = lut[i];
@@ -383,7 +457,7 @@ __global__ __launch_bounds__(kCorrThreads) void k_correct_u16_vec8(
   for (int k = 0; k < 8; ++k) c[k] = coef[g * 8 + k];
   const uint4* src = reinterpret_cast<const uint4*>(in) + g;
   uint4* dst = reinterpret_cast<uint4*>(out) + g;
-  auto one = [&](const uint4 v) -> uint4 {
+  auto one = [&](const uint4 v, const int64_t site) -> uint4 {
     const uint32_t u[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
                            v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
     float2 l[8];
@@ -407,8 +481,7 @@ __global__ __launch_bounds__(kCorrThreads) void k_correct_u16_vec8(
     uint32_t o[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-      o[k] = correct_l<LOG, 16>(l[k].x, l[k].y, c[k], m, u[k], g * 8 + k, c64, rc, clip_lo,
-                                clip_hi);
+      o[k] = correct_l<LOG, 16>(l[k].x, l[k].y, c[k], m, site, g * 8 + k, fl, clip_lo, clip_hi);
     return make_uint4(o[0] | (o[1] << 16), o[2] | (o[3] << 16), o[4] | (o[5] << 16),
                       o[6] | (o[7] << 16));
   };
@@ -424,7 +497,7 @@ __global__ __launch_bounds__(kCorrThreads) void k_correct_u16_vec8(
     }
 #pragma unroll
     for (int k = 0; k < kCorrGroup; ++k)
-      if (s + k < n_sites) st_nt_u4(dst + (s + k) * ngroups, one(cur[k]));
+      if (s + k < n_sites) st_nt_u4(dst + (s + k) * ngroups, one(cur[k], s + k));
 #pragma unroll
     for (int k = 0; k < kCorrGroup; ++k) cur[k] = nxt[k];
   }
@@ -434,8 +507,7 @@ template <bool LOG, typename T, int BITS>
 __global__ __launch_bounds__(kCorrThreads) void k_correct_scalar(
     const T* __restrict__ in, T* __restrict__ out, int64_t npx, int64_t n_sites,
     const float4* __restrict__ coef, const float2* __restrict__ lut,
-    const float4* __restrict__ mconst, const double2* __restrict__ c64,
-    const RefineConst* __restrict__ rc, int clip_lo, int clip_hi) {
+    const float4* __restrict__ mconst, FixList fl, int clip_lo, int clip_hi) {
   __shared__ float2 slut[kLutLds];
   if (LOG)
     for (int i = threadIdx.x; i < kLutLds; i += kCorrThreads) slut[i] = lut[i];
@@ -446,13 +518,13 @@ __global__ __launch_bounds__(kCorrThreads) void k_correct_scalar(
   const float4 c = coef[p];
   for (int64_t s = 0; s < n_sites; ++s)
     out[s * npx + p] =
-        (T)correct1<LOG, BITS>(in[s * npx + p], c, slut, m, p, c64, rc, clip_lo, clip_hi);
+        (T)correct1<LOG, BITS>(in[s * npx + p], c, slut, m, s, p, fl, clip_lo, clip_hi);
 }
 
 void launch_correct_u16(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                         const float4* coef, const float2* lut, const float4* mconst,
-                        const double2* coef64, const RefineConst* rc, int log_transform,
-                        int clip_lo, int clip_hi, hipStream_t s) {
+                        const FixList& fl, int log_transform, int clip_lo, int clip_hi,
+                        hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("correct", s);
   const bool vec = (npx & 7) == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
@@ -461,35 +533,35 @@ void launch_correct_u16(const uint16_t* in, uint16_t* out, int64_t npx, int64_t 
     const dim3 grid((unsigned)cdiv(npx >> 3, kCorrThreads));
     if (log_transform)
       hipLaunchKernelGGL(k_correct_u16_vec8<true>, grid, dim3(kCorrThreads), 0, s, in, out, npx,
-                         n_sites, coef, lut, mconst, coef64, rc, clip_lo, clip_hi);
+                         n_sites, coef, lut, mconst, fl, clip_lo, clip_hi);
     else
       hipLaunchKernelGGL(k_correct_u16_vec8<false>, grid, dim3(kCorrThreads), 0, s, in, out, npx,
-                         n_sites, coef, lut, mconst, coef64, rc, clip_lo, clip_hi);
+                         n_sites, coef, lut, mconst, fl, clip_lo, clip_hi);
   } else {
     const dim3 grid((unsigned)cdiv(npx, kCorrThreads));
     if (log_transform)
       hipLaunchKernelGGL((k_correct_scalar<true, uint16_t, 16>), grid, dim3(kCorrThreads), 0, s, in,
-                         out, npx, n_sites, coef, lut, mconst, coef64, rc, clip_lo, clip_hi);
+                         out, npx, n_sites, coef, lut, mconst, fl, clip_lo, clip_hi);
     else
       hipLaunchKernelGGL((k_correct_scalar<false, uint16_t, 16>), grid, dim3(kCorrThreads), 0, s,
-                         in, out, npx, n_sites, coef, lut, mconst, coef64, rc, clip_lo, clip_hi);
+                         in, out, npx, n_sites, coef, lut, mconst, fl, clip_lo, clip_hi);
   }
   TMH_HIP(hipGetLastError());
 }
 
 void launch_correct_u8(const uint8_t* in, uint8_t* out, int64_t npx, int64_t n_sites,
                        const float4* coef, const float2* lut, const float4* mconst,
-                       const double2* coef64, const RefineConst* rc, int log_transform,
-                       int clip_lo, int clip_hi, hipStream_t s) {
+                       const FixList& fl, int log_transform, int clip_lo, int clip_hi,
+                       hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("correct_u8", s);
   const dim3 grid((unsigned)cdiv(npx, kCorrThreads));
   if (log_transform)
     hipLaunchKernelGGL((k_correct_scalar<true, uint8_t, 8>), grid, dim3(kCorrThreads), 0, s, in,
-                       out, npx, n_sites, coef, lut, mconst, coef64, rc, clip_lo, clip_hi);
+                       out, npx, n_sites, coef, lut, mconst, fl, clip_lo, clip_hi);
   else
     hipLaunchKernelGGL((k_correct_scalar<false, uint8_t, 8>), grid, dim3(kCorrThreads), 0, s, in,
-                       out, npx, n_sites, coef, lut, mconst, coef64, rc, clip_lo, clip_hi);
+                       out, npx, n_sites, coef, lut, mconst, fl, clip_lo, clip_hi);
   TMH_HIP(hipGetLastError());
 }
 

@@ -66,20 +66,17 @@ __device__ __forceinline__ uint32_t clip_scale8(uint32_t v16, int lo, int hi, in
   return i >= (uint32_t)T ? 255u : (uint32_t)((double)i * step);
 }
 
-// one pixel px (index p) of the packed-f32 correction; m = mconst2 (M' hi,
-// M' lo, zf, T): beyond T the f64 refinement (common.h)
+// one pixel px (site s, source index p) of the packed-f32 correction; m =
+// mconst2 (M' hi, M' lo, zf, T): beyond T the pixel is flagged for the f64
+// refinement (common.h, k_fix_chain)
 template <bool LOG>
 __device__ __forceinline__ uint32_t correct16(uint32_t px, float mu, float a, const float4 m,
-                                              int64_t p, const double2* __restrict__ c64,
-                                              const RefineConst* __restrict__ rc) {
+                                              int64_t s, int64_t p, const FixList& fl) {
   float L = (float)px;
   if (LOG) L = __builtin_amdgcn_logf(__builtin_fmaxf(L, m.z));
   const float t = fmaf(L - mu, a, m.x);
   float o = LOG ? __builtin_amdgcn_exp2f(t) : t;
-  if (__builtin_fabsf(o) >= m.w) {
-    const double2 q = c64[p];
-    return (uint32_t)correct_ref_f64<LOG>(px, q.x, q.y, rc->S, rc->M, rc->zero_log10) & 0xFFFFu;
-  }
+  if (__builtin_fabsf(o) >= m.w) fix_push(fl, s, p);
   o = __builtin_fminf(o, 2147418112.0f);  // >= 2^31, inf, NaN -> low half 0 (x86 astype)
   if (!LOG) o = __builtin_fmaxf(o, -2147483648.0f);
   return (uint32_t)(int32_t)o & 0xFFFFu;
@@ -150,8 +147,7 @@ __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ i
                                                    int64_t n_sites, int64_t per,
                                                    const float2* __restrict__ coef_lin,
                                                    const float4* __restrict__ mconst2,
-                                                   const double2* __restrict__ c64,
-                                                   const RefineConst* __restrict__ rc,
+                                                   FixList fl,
                                                    const tmh_window* __restrict__ win, int lo,
                                                    int hi, int T, double step) {
   // LUT: the reference's uint8 table for the clipped range [lo, hi] staged in
@@ -239,14 +235,10 @@ __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ i
       if (!LOG) x = __builtin_fmaxf(x, -2147483648.0f);
       iv[j] = (int32_t)x;
     }
-    if (far) {
+    if (far && live) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if ((far >> j) & 1u) {
-          const double2 q = c64[p0 + j];
-          iv[j] = correct_ref_f64<LOG>((wd[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, q.x, q.y, rc->S,
-                                       rc->M, rc->zero_log10);
-        }
+        if ((far >> j) & 1u) fix_push(fl, s, p0 + j);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -344,8 +336,7 @@ __global__ __launch_bounds__(256) void k_chain_u8_scalar(const uint16_t* __restr
                                                           int64_t n_sites,
                                                           const float2* __restrict__ coef_lin,
                                                           const float4* __restrict__ mconst2,
-                                                          const double2* __restrict__ c64,
-                                                          const RefineConst* __restrict__ rc,
+                                                          FixList fl,
                                                           const tmh_window* __restrict__ win,
                                                           int lo, int hi, int T, double step) {
   const int64_t npx = (int64_t)H * W;
@@ -359,9 +350,50 @@ __global__ __launch_bounds__(256) void k_chain_u8_scalar(const uint16_t* __restr
     if (in_window(r, c, w)) {
       const int64_t p = (int64_t)(r - w.dst_r0 + w.src_r0) * W + (c - w.dst_c0 + w.src_c0);
       const float2 k = coef_lin[p];
-      v = clip_scale8(correct16<LOG>(in[s * npx + p], k.x, k.y, m, p, c64, rc), lo, hi, T, step);
+      v = clip_scale8(correct16<LOG>(in[s * npx + p], k.x, k.y, m, s, p, fl), lo, hi, T, step);
     }
     out[s * npx + i] = (uint8_t)v;
+  }
+}
+
+// f64 refinement of the chain pixels the pass flagged (e = site << 32 |
+// source pixel): the source pixel's corrected value -> clip -> scale, written
+// at its aligned destination; pixels outside the source window were written
+// as padding and are left alone.  Overflowed list: every source pixel.
+template <bool LOG>
+__global__ __launch_bounds__(256) void k_fix_chain(const uint16_t* __restrict__ in,
+                                                   uint8_t* __restrict__ out, int H, int W,
+                                                   int64_t n_sites, FixList fl,
+                                                   const double2* __restrict__ c64,
+                                                   const RefineConst* __restrict__ rc,
+                                                   const tmh_window* __restrict__ win, int lo,
+                                                   int hi, int T, double step) {
+  const int64_t npx = (int64_t)H * W;
+  const unsigned int n = *fl.n;
+  const bool all = n > fl.cap;
+  const int64_t total = all ? n_sites * npx : (int64_t)n;
+  if (total == 0) return;
+  const RefineConst k = *rc;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * 256) {
+    int64_t s, p;
+    if (all) {
+      s = i / npx;
+      p = i - s * npx;
+    } else {
+      const unsigned long long e = fl.e[i];
+      s = (int64_t)(e >> 32);
+      p = (int64_t)(e & 0xFFFFFFFFull);
+    }
+    const tmh_window w = win[s];
+    const int r = (int)(p / W), c = (int)(p % W);
+    if ((unsigned)(r - w.src_r0) >= (unsigned)w.rows || (unsigned)(c - w.src_c0) >= (unsigned)w.cols)
+      continue;
+    const double2 q = c64[p];
+    const uint32_t v16 =
+        (uint32_t)correct_ref_f64<LOG>(in[s * npx + p], q.x, q.y, k.S, k.M, k.zero_log10) & 0xFFFFu;
+    const int64_t d = (int64_t)(r - w.src_r0 + w.dst_r0) * W + (c - w.src_c0 + w.dst_c0);
+    out[s * npx + d] = (uint8_t)clip_scale8(v16, lo, hi, T, step);
   }
 }
 
@@ -388,9 +420,9 @@ void launch_map_u8(const uint16_t* in, uint8_t* out, int64_t n, int lo, int hi, 
 }
 
 void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_sites,
-                     const float2* coef_lin, const float4* mconst2, const double2* coef64,
-                     const RefineConst* rc, int log_transform, const tmh_window* d_win, int lo,
-                     int hi, hipStream_t s) {
+                     const float2* coef_lin, const float4* mconst2, const FixList& fl,
+                     const double2* coef64, const RefineConst* rc, int log_transform,
+                     const tmh_window* d_win, int lo, int hi, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("chain", s);
   const int64_t npx = (int64_t)H * W;
@@ -408,7 +440,7 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
     const size_t shm = lut ? (size_t)((lut_bytes + 15) & ~15) : 0;
 #define TMH_CHAIN(L_, U_)                                                                     \
   hipLaunchKernelGGL((k_chain_u8<L_, U_>), grid, dim3(256), shm, s, in, out, H, W, n_sites, per, \
-                     coef_lin, mconst2, coef64, rc, d_win, lo, hi, T, step)
+                     coef_lin, mconst2, fl, d_win, lo, hi, T, step)
     if (log_transform) {
       if (lut) TMH_CHAIN(true, true); else TMH_CHAIN(true, false);
     } else {
@@ -421,11 +453,17 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
     const dim3 grid((unsigned)cdiv(npx, 256));
     if (log_transform)
       hipLaunchKernelGGL(k_chain_u8_scalar<true>, grid, dim3(256), 0, s, in, out, H, W, n_sites,
-                         coef_lin, mconst2, coef64, rc, d_win, lo, hi, T, step);
+                         coef_lin, mconst2, fl, d_win, lo, hi, T, step);
     else
       hipLaunchKernelGGL(k_chain_u8_scalar<false>, grid, dim3(256), 0, s, in, out, H, W, n_sites,
-                         coef_lin, mconst2, coef64, rc, d_win, lo, hi, T, step);
+                         coef_lin, mconst2, fl, d_win, lo, hi, T, step);
   }
+  if (log_transform)
+    hipLaunchKernelGGL(k_fix_chain<true>, dim3(512), dim3(256), 0, s, in, out, H, W, n_sites, fl,
+                       coef64, rc, d_win, lo, hi, T, step);
+  else
+    hipLaunchKernelGGL(k_fix_chain<false>, dim3(512), dim3(256), 0, s, in, out, H, W, n_sites, fl,
+                       coef64, rc, d_win, lo, hi, T, step);
   TMH_HIP(hipGetLastError());
 }
 

@@ -72,7 +72,10 @@ struct QPos {
 // within 1 DN of the reference -- wherever |o| < T = 1 / (K1 * a_max + K2),
 // a_max the image's largest finite a.  Pixels with |o| >= T (saturated pixels
 // in dim corners: corrected values up to ~1e6 that numpy wraps modulo 2^16)
-// are recomputed in f64, op for op as the reference does.
+// are appended to a fixup list by the streaming kernel, and a small kernel
+// after it recomputes them in f64, op for op as the reference does.  (Doing
+// the f64 work inline would make every streaming kernel reserve its
+// registers: the chain pass fell from 8 to 5 waves per SIMD.)
 constexpr double kRefineK1 = 6.7e-6;
 constexpr double kRefineK2 = 4.2e-6;
 
@@ -82,12 +85,25 @@ struct RefineConst {
   double S, M, zero_log10, T;
 };
 
+// pixels to refine: e[i] = site << 32 | pixel for i < min(*n, cap); *n > cap
+// means the list overflowed and the fixup recomputes every pixel in f64
+struct FixList {
+  unsigned long long* e;
+  unsigned int* n;
+  unsigned int cap;
+};
+
+__device__ __forceinline__ void fix_push(const FixList& fl, int64_t site, int64_t px) {
+  const unsigned int i = atomicAdd(fl.n, 1u);
+  if (i < fl.cap) fl.e[i] = ((unsigned long long)site << 32) | (unsigned long long)(uint32_t)px;
+}
+
 // ChannelImage._correct_illumination (tmlib/image.py:619-631) of one pixel in
 // f64, one rounding per numpy operation; returns the int32 numpy's x86
 // astype truncates to (NaN, +-inf, out of range -> INT32_MIN).
 template <bool LOG>
-__device__ __noinline__ int32_t correct_ref_f64(uint32_t x, double mean, double std, double S,
-                                                double M, double zero_log10) {
+__device__ __forceinline__ int32_t correct_ref_f64(uint32_t x, double mean, double std, double S,
+                                                   double M, double zero_log10) {
 #pragma clang fp contract(off)
   double v = (double)x;
   if (LOG) v = (x == 0u) ? zero_log10 : log10(v);  // img[img == 0] = 1e-10; log10
@@ -97,7 +113,6 @@ __device__ __noinline__ int32_t correct_ref_f64(uint32_t x, double mean, double 
   if (LOG) t = exp10(t);  // 10 ** img
   return (t > -2147483649.0 && t < 2147483648.0) ? (int32_t)t : INT32_MIN;
 }
-
 
 // launches (defined in the .hip files) -------------------------------------------
 // part: optional scratch of part_cap doubles for site-split launches (null: one part)
@@ -130,7 +145,8 @@ void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s);
 
 void launch_smooth(const double* in, double* out, double* tmp, int H, int W, const double* d_w,
                    int radius, hipStream_t s);
-// out[0] = sum(x0), out[1] = sum(x1); partial holds 2 * n_partial
+// out[0] = sum(x0), out[1] = sum(x1), out[2] = smallest positive finite x0
+// (+inf if none); partial holds 3 * n_partial
 void launch_reduce_sum2(const double* x0, const double* x1, int64_t n, double* partial,
                         int n_partial, double* out, hipStream_t s);
 void launch_reduce_sum(const double* x, int64_t n, double* partial, int n_partial, double* out,
@@ -139,36 +155,41 @@ void launch_build_corr_lut(float2* lut, int log_transform, double zero_log10, hi
 // Every coefficient form of one (mean, std) pair in one pass: coef (LUT path,
 // mconst = (M hi, M lo, T, 0)), coef2 / coef_lin / mconst2 (packed log2-domain
 // path, fused_kernels.hip), coef64 (f64 (mean, std) for the refinement) and
-// rc (RefineConst); amax = scratch u64.  sums = (sum(std), sum(mean)).
+// rc (RefineConst).  sums = (sum(std), sum(mean), min positive std).
 void launch_coeffs_all(const double* mean, const double* std, const double* sums, int64_t npx,
                        int log_transform, double zero_log10, float4* coef, float4* mconst,
                        float2* coef2, float4* mconst2, float2* coef_lin, double2* coef64,
-                       RefineConst* rc, unsigned long long* amax, hipStream_t s);
+                       RefineConst* rc, hipStream_t s);
+// Refinement of the pixels a correct launch flagged (fl), written into out
+// (u16 or u8 of in's type; clip as the launch); launched on the same stream.
+void launch_fix_correct(const void* in, void* out, int elem_bytes, int64_t npx, int64_t n_sites,
+                        const FixList& fl, const double2* coef64, const RefineConst* rc,
+                        int log_transform, int clip_lo, int clip_hi, hipStream_t s);
 void launch_correct_u16(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                         const float4* coef, const float2* lut, const float4* mconst,
-                        const double2* coef64, const RefineConst* rc, int log_transform,
-                        int clip_lo, int clip_hi, hipStream_t s);
+                        const FixList& fl, int log_transform, int clip_lo, int clip_hi,
+                        hipStream_t s);
 void launch_correct_u8(const uint8_t* in, uint8_t* out, int64_t npx, int64_t n_sites,
                        const float4* coef, const float2* lut, const float4* mconst,
-                       const double2* coef64, const RefineConst* rc, int log_transform,
-                       int clip_lo, int clip_hi, hipStream_t s);
+                       const FixList& fl, int log_transform, int clip_lo, int clip_hi,
+                       hipStream_t s);
 // fused pass configurations (fused_kernels.hip kFusedCfgs); default kFusedDefault
 constexpr int kFusedConfigs = 4;
 constexpr int kFusedDefault = 3;
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
-                         const float2* coef2, const float4* mconst2, const double2* coef64,
-                         const RefineConst* rc, int log_transform, int clip_lo, int clip_hi,
-                         uint32_t* hist, unsigned long long* rmask, int* queues, int n_wg, int cfg,
-                         hipStream_t s);
+                         const float2* coef2, const float4* mconst2, const FixList& fl,
+                         int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
+                         unsigned long long* rmask, int* queues, int n_wg, int cfg, hipStream_t s);
 int correct_hist_dense_rounds(int cfg);
 // illuminati chain (chain_kernels.hip)
 void launch_align(const void* in, void* out, int elem_bytes, int64_t n_sites, int H, int W, int oh,
                   int ow, const tmh_window* d_win, hipStream_t s);
 void launch_map_u8(const uint16_t* in, uint8_t* out, int64_t n, int lo, int hi, hipStream_t s);
+// (launches its own fixup kernel after the chain pass)
 void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_sites,
-                     const float2* coef_lin, const float4* mconst2, const double2* coef64,
-                     const RefineConst* rc, int log_transform, const tmh_window* d_win, int lo,
-                     int hi, hipStream_t s);
+                     const float2* coef_lin, const float4* mconst2, const FixList& fl,
+                     const double2* coef64, const RefineConst* rc, int log_transform,
+                     const tmh_window* d_win, int lo, int hi, hipStream_t s);
 void launch_clip_u16(const uint16_t* in, uint16_t* out, int64_t n, int lo, int hi, hipStream_t s);
 void launch_synth(uint16_t* out, int64_t n_sites, int H, int W, uint64_t seed, int channel,
                   int64_t first_site, int dist, hipStream_t s);

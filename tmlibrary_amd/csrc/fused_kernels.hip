@@ -56,15 +56,13 @@ constexpr float kCastTop = 2147418112.0f;
 // their one-pass hazard.  A zero pixel takes log2(zf), zf = 10**zero_log10 as
 // f32 (1e-10f: v_log_f32 is within 1 ulp of the reference's log10(1e-10) =
 // -10, scaled): one v_max instead of a compare + select.  The caller keeps zf
-// in [FLT_MIN, 1].  Pixels whose f32 result reaches T (mconst2.w, the f32
-// error bound's limit, common.h) are recomputed in f64 from c64 (their
-// (mean, std)), exactly as the reference: rare (saturated pixels in dim
-// corners), one wave-uniform test per 8 pixels otherwise.
+// in [FLT_MIN, 1].  Returns the mask of the pixels whose f32 result reaches
+// T (mconst2.w, the f32 error bound's limit): the caller flags them for the
+// f64 refinement (common.h) -- rare, saturated pixels in dim corners.
 template <bool LOG, bool CLIP>
-__device__ __forceinline__ void fcorrect8(const uint32_t (&w)[4], const float4 (&k)[4], float mh,
-                                          float zf, float T, uint32_t clip_lo2, uint32_t clip_hi2,
-                                          const double2* __restrict__ c64g,
-                                          const RefineConst* __restrict__ rc, uint32_t (&r)[4]) {
+__device__ __forceinline__ uint32_t fcorrect8(const uint32_t (&w)[4], const float4 (&k)[4],
+                                              float mh, float zf, float T, uint32_t clip_lo2,
+                                              uint32_t clip_hi2, uint32_t (&r)[4]) {
   f32x2_t t[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -99,16 +97,6 @@ __device__ __forceinline__ void fcorrect8(const uint32_t (&w)[4], const float4 (
     if (!LOG) o[j] = __builtin_fmaxf(o[j], -2147483648.0f);  // t may be negative: stay in range
     iv[j] = (int32_t)o[j];
   }
-  if (far) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if ((far >> j) & 1u) {
-        const double2 q = c64g[j];
-        const uint32_t u = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-        iv[j] = correct_ref_f64<LOG>(u, q.x, q.y, rc->S, rc->M, rc->zero_log10);
-      }
-    }
-  }
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     r[p] = __builtin_amdgcn_perm((uint32_t)iv[2 * p + 1], (uint32_t)iv[2 * p], 0x05040100u);
@@ -120,6 +108,7 @@ __device__ __forceinline__ void fcorrect8(const uint32_t (&w)[4], const float4 (
       r[p] = __builtin_bit_cast(uint32_t, v);
     }
   }
+  return far;
 }
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -156,9 +145,8 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 template <bool LOG, bool CLIP, int SPU, int ABL, int NT, int LB>
 __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void k_correct_hist(
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
-    const float4* __restrict__ coef, const float4* __restrict__ mconst2,
-    const double2* __restrict__ coef64, const RefineConst* __restrict__ rc, int clip_lo,
-    int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
+    const float4* __restrict__ coef, const float4* __restrict__ mconst2, FixList fl,
+    int clip_lo, int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
     int* __restrict__ queues, int bands_per_xcd) {
   constexpr int BINS = LB / SPU;
   constexpr int SLICE = BINS + 1;
@@ -276,7 +264,12 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
         }
       }
       uint32_t o[4];
-      fcorrect8<LOG, CLIP>(wd, cf, m.x, m.z, m.w, clo2, chi2, coef64 + (int64_t)g * 8, rc, o);
+      const uint32_t far = fcorrect8<LOG, CLIP>(wd, cf, m.x, m.z, m.w, clo2, chi2, o);
+      if (far) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if ((far >> j) & 1u) fix_push(fl, un.s0 + k, (int64_t)g * 8 + j);
+      }
       const u32x4_t r = {o[0], o[1], o[2], o[3]};
       return r;
     };
@@ -354,10 +347,9 @@ int correct_hist_dense_rounds(int cfg) {
 }
 
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
-                         const float2* coef2, const float4* mconst2, const double2* coef64,
-                         const RefineConst* rc, int log_transform, int clip_lo, int clip_hi,
-                         uint32_t* hist, unsigned long long* rmask, int* queues, int n_wg, int cfg,
-                         hipStream_t s) {
+                         const float2* coef2, const float4* mconst2, const FixList& fl,
+                         int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
+                         unsigned long long* rmask, int* queues, int n_wg, int cfg, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("correct_hist", s);
   TMH_HIP(hipMemsetAsync(queues, 0, 8 * sizeof(int), s));
@@ -368,11 +360,11 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
     const dim3 grid(n_wg * (1024 / c.threads));                                                  \
     if (clip_lo >= 0)                                                                            \
       hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, 0, c.threads, c.lds_bins>), grid,     \
-                         dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, coef64, rc,   \
+                         dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
                          clip_lo, clip_hi, hist, rmask, queues, kBandsPerXcd);                   \
     else                                                                                         \
       hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, 0, c.threads, c.lds_bins>), grid,    \
-                         dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, coef64, rc,   \
+                         dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
                          clip_lo, clip_hi, hist, rmask, queues, kBandsPerXcd);                   \
   }
 #define TMH_LAUNCH_CFG(L_)            \
