@@ -848,6 +848,7 @@ static void corrector_init(tmh_corrector* c, const double* d_mean, const double*
 // recompute every pixel in f64: slow but exact), count reset on s.  One
 // launch at a time per corrector (the list is reused).
 static FixList corrector_fixlist(tmh_corrector* c, int64_t n_sites, hipStream_t s) {
+  TMH_CHECK(n_sites < ((int64_t)1 << 24), TMH_EINVAL, "at most 2^24 - 1 sites per correct call");
   const int64_t want = std::min<int64_t>(std::max<int64_t>((int64_t)1 << 20, n_sites * c->npx / 1024),
                                          (int64_t)1 << 30);
   if ((size_t)want > c->fix_e.n) {

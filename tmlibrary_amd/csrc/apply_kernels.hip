@@ -310,8 +310,8 @@ void launch_coeffs_all(const double* mean, const double* std, const double* sums
   TMH_HIP(hipGetLastError());
 }
 
-// The f64 refinement of the pixels a correct launch flagged: e = site << 32 |
-// pixel, written as the launch would (low BITS bits, clip).  If the list
+// The f64 refinement of the pixels a correct launch flagged (FixList,
+// common.h), written as the launch would (low BITS bits, clip).  If the list
 // overflowed, every pixel of the launch is recomputed in f64.
 template <bool LOG, typename T, int BITS>
 __global__ __launch_bounds__(256) void k_fix_correct(const T* __restrict__ in, T* __restrict__ out,
@@ -321,28 +321,27 @@ __global__ __launch_bounds__(256) void k_fix_correct(const T* __restrict__ in, T
                                                      int clip_lo, int clip_hi) {
   const unsigned int n = *fl.n;
   const bool all = n > fl.cap;
-  const int64_t total = all ? n_sites * npx : (int64_t)n;
+  const int64_t total = all ? n_sites * ((npx + 7) / 8) : (int64_t)n;
   if (total == 0) return;
   const RefineConst k = *rc;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * 256) {
-    int64_t s, p;
-    if (all) {
-      s = i / npx;
-      p = i - s * npx;
-    } else {
-      const unsigned long long e = fl.e[i];
-      s = (int64_t)(e >> 32);
-      p = (int64_t)(e & 0xFFFFFFFFull);
+    int64_t s, p0;
+    uint32_t mask;
+    fix_entry(fl, all, i, npx, s, p0, mask);
+    for (int j = 0; j < 8; ++j) {
+      const int64_t p = p0 + j;
+      if (!((mask >> j) & 1u) || p >= npx) continue;
+      const double2 q = c64[p];
+      uint32_t r =
+          (uint32_t)correct_ref_f64<LOG>(in[s * npx + p], q.x, q.y, k.S, k.M, k.zero_log10) &
+          ((1u << BITS) - 1u);
+      if (clip_lo >= 0) {
+        r = r < (uint32_t)clip_lo ? (uint32_t)clip_lo : r;
+        r = r > (uint32_t)clip_hi ? (uint32_t)clip_hi : r;
+      }
+      out[s * npx + p] = (T)r;
     }
-    const double2 q = c64[p];
-    uint32_t r = (uint32_t)correct_ref_f64<LOG>(in[s * npx + p], q.x, q.y, k.S, k.M, k.zero_log10) &
-                 ((1u << BITS) - 1u);
-    if (clip_lo >= 0) {
-      r = r < (uint32_t)clip_lo ? (uint32_t)clip_lo : r;
-      r = r > (uint32_t)clip_hi ? (uint32_t)clip_hi : r;
-    }
-    out[s * npx + p] = (T)r;
   }
 }
 

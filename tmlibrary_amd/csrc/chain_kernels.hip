@@ -217,40 +217,25 @@ __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ i
 #pragma unroll
     for (int k = 0; k < 4; ++k) t[k] = __builtin_elementwise_fma(t[k] - mu[k], a[k], M);
     uint32_t o[8];
-    float ox[8];
-    uint32_t far = 0;  // pixels beyond the f32 bound: f64 refinement (common.h)
+    float mx = 0.0f;  // largest |result| of the 8 pixels: one compare against T per 8
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const float x = LOG ? __builtin_amdgcn_exp2f(t[k][h]) : t[k][h];
-        far |= (__builtin_fabsf(x) >= m.w ? 1u : 0u) << (2 * k + h);
-        ox[2 * k + h] = x;
-      }
-    }
-    int32_t iv[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float x = __builtin_fminf(ox[j], 2147418112.0f);  // >= 2^31, inf, NaN -> low half 0 (x86)
-      if (!LOG) x = __builtin_fmaxf(x, -2147483648.0f);
-      iv[j] = (int32_t)x;
-    }
-    if (far && live) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if ((far >> j) & 1u) fix_push(fl, s, p0 + j);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t v16 = (uint32_t)iv[2 * k + h] & 0xFFFFu;
+        float x = LOG ? __builtin_amdgcn_exp2f(t[k][h]) : t[k][h];
+        mx = __builtin_fmaxf(mx, __builtin_fabsf(x));
+        x = __builtin_fminf(x, 2147418112.0f);  // >= 2^31, inf, NaN -> low half 0 (x86)
+        if (!LOG) x = __builtin_fmaxf(x, -2147483648.0f);
+        const uint32_t v16 = (uint32_t)(int32_t)x & 0xFFFFu;
         const uint32_t v = min(max(v16, (uint32_t)lo), (uint32_t)hi);  // np.clip
         o[2 * k + h] = LUT ? (uint32_t)slut[v - (uint32_t)lo]
                            : (v - (uint32_t)lo >= (uint32_t)T ? 255u
                                                               : (uint32_t)((double)(v - lo) * step));
       }
     }
+    // rare: a pixel beyond the f32 bound flags its group of 8 for the f64
+    // refinement (common.h; f64 is the reference value for all 8)
+    if (mx >= m.w && live) fix_push8(fl, 0xFFu, s, p0);
     // pixels outside the source window write the padding value: 0 after
     // clip/scale (clip(0) = lo, the table's first entry is 0)
     const int cs = c0 - w.src_c0;
@@ -356,10 +341,10 @@ __global__ __launch_bounds__(256) void k_chain_u8_scalar(const uint16_t* __restr
   }
 }
 
-// f64 refinement of the chain pixels the pass flagged (e = site << 32 |
-// source pixel): the source pixel's corrected value -> clip -> scale, written
-// at its aligned destination; pixels outside the source window were written
-// as padding and are left alone.  Overflowed list: every source pixel.
+// f64 refinement of the chain pixels the pass flagged (FixList, common.h;
+// source pixels): the corrected value -> clip -> scale, written at the pixel's
+// aligned destination; pixels outside the source window were written as
+// padding and are left alone.  Overflowed list: every source pixel.
 template <bool LOG>
 __global__ __launch_bounds__(256) void k_fix_chain(const uint16_t* __restrict__ in,
                                                    uint8_t* __restrict__ out, int H, int W,
@@ -371,29 +356,29 @@ __global__ __launch_bounds__(256) void k_fix_chain(const uint16_t* __restrict__ 
   const int64_t npx = (int64_t)H * W;
   const unsigned int n = *fl.n;
   const bool all = n > fl.cap;
-  const int64_t total = all ? n_sites * npx : (int64_t)n;
+  const int64_t total = all ? n_sites * ((npx + 7) / 8) : (int64_t)n;
   if (total == 0) return;
   const RefineConst k = *rc;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * 256) {
-    int64_t s, p;
-    if (all) {
-      s = i / npx;
-      p = i - s * npx;
-    } else {
-      const unsigned long long e = fl.e[i];
-      s = (int64_t)(e >> 32);
-      p = (int64_t)(e & 0xFFFFFFFFull);
-    }
+    int64_t s, p0;
+    uint32_t mask;
+    fix_entry(fl, all, i, npx, s, p0, mask);
     const tmh_window w = win[s];
-    const int r = (int)(p / W), c = (int)(p % W);
-    if ((unsigned)(r - w.src_r0) >= (unsigned)w.rows || (unsigned)(c - w.src_c0) >= (unsigned)w.cols)
-      continue;
-    const double2 q = c64[p];
-    const uint32_t v16 =
-        (uint32_t)correct_ref_f64<LOG>(in[s * npx + p], q.x, q.y, k.S, k.M, k.zero_log10) & 0xFFFFu;
-    const int64_t d = (int64_t)(r - w.src_r0 + w.dst_r0) * W + (c - w.src_c0 + w.dst_c0);
-    out[s * npx + d] = (uint8_t)clip_scale8(v16, lo, hi, T, step);
+    for (int j = 0; j < 8; ++j) {
+      const int64_t p = p0 + j;
+      if (!((mask >> j) & 1u) || p >= npx) continue;
+      const int r = (int)(p / W), c = (int)(p % W);
+      if ((unsigned)(r - w.src_r0) >= (unsigned)w.rows ||
+          (unsigned)(c - w.src_c0) >= (unsigned)w.cols)
+        continue;
+      const double2 q = c64[p];
+      const uint32_t v16 =
+          (uint32_t)correct_ref_f64<LOG>(in[s * npx + p], q.x, q.y, k.S, k.M, k.zero_log10) &
+          0xFFFFu;
+      const int64_t d = (int64_t)(r - w.src_r0 + w.dst_r0) * W + (c - w.src_c0 + w.dst_c0);
+      out[s * npx + d] = (uint8_t)clip_scale8(v16, lo, hi, T, step);
+    }
   }
 }
 

@@ -85,17 +85,41 @@ struct RefineConst {
   double S, M, zero_log10, T;
 };
 
-// pixels to refine: e[i] = site << 32 | pixel for i < min(*n, cap); *n > cap
-// means the list overflowed and the fixup recomputes every pixel in f64
+// pixels to refine, one entry per group of up to 8 consecutive pixels:
+// e[i] = site << 40 | mask << 32 | p0 (bit j of mask: pixel p0 + j), for
+// i < min(*n, cap); *n > cap means the list overflowed and the fixup
+// recomputes every pixel in f64.  (A launch covers < 2^24 sites.)
 struct FixList {
   unsigned long long* e;
   unsigned int* n;
   unsigned int cap;
 };
 
-__device__ __forceinline__ void fix_push(const FixList& fl, int64_t site, int64_t px) {
+__device__ __forceinline__ void fix_push8(const FixList& fl, uint32_t mask, int64_t site, int64_t p0) {
   const unsigned int i = atomicAdd(fl.n, 1u);
-  if (i < fl.cap) fl.e[i] = ((unsigned long long)site << 32) | (unsigned long long)(uint32_t)px;
+  if (i < fl.cap)
+    fl.e[i] = ((unsigned long long)site << 40) | ((unsigned long long)(mask & 0xFFu) << 32) |
+              (unsigned long long)(uint32_t)p0;
+}
+
+__device__ __forceinline__ void fix_push(const FixList& fl, int64_t site, int64_t px) {
+  fix_push8(fl, 1u, site, px);
+}
+
+// entry i of the list (or, overflowed, the i-th group of 8 pixels)
+__device__ __forceinline__ void fix_entry(const FixList& fl, bool all, int64_t i, int64_t npx,
+                                          int64_t& site, int64_t& p0, uint32_t& mask) {
+  if (all) {
+    const int64_t gps = (npx + 7) / 8;  // groups per site
+    site = i / gps;
+    p0 = (i - site * gps) * 8;
+    mask = 0xFFu;
+  } else {
+    const unsigned long long e = fl.e[i];
+    site = (int64_t)(e >> 40);
+    mask = (uint32_t)(e >> 32) & 0xFFu;
+    p0 = (int64_t)(e & 0xFFFFFFFFull);
+  }
 }
 
 // ChannelImage._correct_illumination (tmlib/image.py:619-631) of one pixel in

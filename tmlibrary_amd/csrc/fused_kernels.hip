@@ -87,9 +87,14 @@ __device__ __forceinline__ uint32_t fcorrect8(const uint32_t (&w)[4], const floa
     o[2 * p] = LOG ? __builtin_amdgcn_exp2f(t[p].x) : t[p].x;  // v_exp_f32
     o[2 * p + 1] = LOG ? __builtin_amdgcn_exp2f(t[p].y) : t[p].y;
   }
-  uint32_t far = 0;  // pixels beyond the f32 bound
+  float mx = __builtin_fabsf(o[0]);  // one compare per 8 pixels; the mask only if needed
 #pragma unroll
-  for (int j = 0; j < 8; ++j) far |= (__builtin_fabsf(o[j]) >= T ? 1u : 0u) << j;
+  for (int j = 1; j < 8; ++j) mx = __builtin_fmaxf(mx, __builtin_fabsf(o[j]));
+  uint32_t far = 0;  // pixels beyond the f32 bound
+  if (mx >= T) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) far |= (__builtin_fabsf(o[j]) >= T ? 1u : 0u) << j;
+  }
   int32_t iv[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -265,11 +270,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
       }
       uint32_t o[4];
       const uint32_t far = fcorrect8<LOG, CLIP>(wd, cf, m.x, m.z, m.w, clo2, chi2, o);
-      if (far) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if ((far >> j) & 1u) fix_push(fl, un.s0 + k, (int64_t)g * 8 + j);
-      }
+      if (far) fix_push8(fl, far, un.s0 + k, (int64_t)g * 8);
       const u32x4_t r = {o[0], o[1], o[2], o[3]};
       return r;
     };
