@@ -7,8 +7,10 @@ bench.py's step (one channel job, configs[1]) is, on one stream:
        correct + per-site histogram pass, then order statistics and the
        ordered percentile sum)
 Here the same calls run on 128 device-resident 2160x2560 sites from the
-bench's own generator (so welford_parts may split the launch: >= 32 sites a
-part), and everything is compared with the CPU oracle on the same pixels
+bench's own generator -- once with the production launch shapes (one Welford
+site part) and once with the launch split into 4 site parts (32 full-size
+sites each, merged) -- and everything is compared with the CPU oracle on the
+same pixels
 (reference: tmlib/workflow/corilla/stats.py:64-121, tmlib/image.py:599-631,
 :1172-1193): mean/std within 1e-6, pooled and per-site histograms and the
 percentile sums bit-exact, corrected pixels within +-1 DN (non-modular) with
@@ -98,9 +100,12 @@ def test_headline_pipeline_fullsize(L):
         hip.check(L.tmh_correct_u16_hist_device(c, h, d_in.p, d_out.p, N, -1, -1, sp))
         return _results(L, h, H, W, N)
 
-    r1 = job()
+    r1 = job()  # the production launch shapes (one Welford site part)
     out1 = d_out.get(np.uint16, (N, npx))[::37].copy()
-    r = job()  # steady state: the second job on the same handle (bench warm-up -> timed)
+    # the second job on the same handle (bench warm-up -> timed) with the
+    # Welford launch split into 4 site parts (32 full-size sites each) + merge
+    hip.check(L.tmh_stats_set_option(h, hip.TMH_OPT_WELFORD_PARTS, 4))
+    r = job()
     assert np.array_equal(r["acc"], r1["acc"]) and np.array_equal(r["hist"], r1["hist"])
     site_hist = {}
     for i in (0, 63, N - 1):
@@ -127,9 +132,10 @@ def test_headline_pipeline_fullsize(L):
         pooled += hs
         if i in site_hist:
             assert np.array_equal(site_hist[i].astype(np.uint64), hs), "site %d histogram" % i
-    assert r["n"] == ref.n == N
-    assert_close_rel(r["mean"], ref.mean)
-    assert_close_rel(r["std"], ref.std)
+    assert r["n"] == r1["n"] == ref.n == N
+    for res in (r1, r):  # one part, four parts
+        assert_close_rel(res["mean"], ref.mean)
+        assert_close_rel(res["std"], ref.std)
     assert np.array_equal(r["hist"], pooled), "pooled histogram not bit-exact"
     assert np.array_equal(r["acc"], ref.percentile_sums), "percentile sums not bit-exact"
     sm_ref, ss_ref = orc.smooth_reflect(ref.mean, 5), orc.smooth_reflect(ref.std, 5)

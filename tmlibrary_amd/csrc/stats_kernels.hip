@@ -37,7 +37,7 @@ namespace tmh {
 // with a 3-term series (truncation < 7e-15 absolute): no transcendental and
 // few registers, so the rare branch does not cost the streaming loop waves.
 __device__ __forceinline__ double log10_slow(uint32_t u, const double* slut) {
-  const int k = u < 64496u ? 4 : 5;  // a <= 4030 < kWfLut - 1
+  const int k = u < 64496u ? 4 : 5;  // a <= 4030 < 4096 (LDS LUT)
   const uint32_t a = u >> k;
   const double den = (double)(a << k);
   const double t = (double)(u - (a << k)) / den;
@@ -47,16 +47,16 @@ __device__ __forceinline__ double log10_slow(uint32_t u, const double* slut) {
   return slut[a] + (double)k * kLog10_2 + series;
 }
 
-// LUT entries staged in LDS: 4032 x 8 B leaves room for one Welford
-// workgroup beside a histogram workgroup (131,264 B) in a CU's 160 KiB, so
-// the two passes can run concurrently
-constexpr int kWfLut = 4032;
+// LUT entries staged in LDS: the 4,096 values below 2^12 (32 KB), so a site's
+// 8 pixels need the rare path exactly when one of their 16-bit words has a
+// bit >= 12 set (one OR/AND over the four packed words)
+constexpr int kWfLut = 4096;
 
 template <bool LOG>
 __device__ __forceinline__ double xform(uint32_t u, const double* slut) {
   if (!LOG) return (double)u;
-  double x = slut[u < (uint32_t)kWfLut - 1 ? u : 0u];
-  if (u >= (uint32_t)kWfLut - 1) x = log10_slow(u, slut);
+  double x = slut[u & (uint32_t)(kWfLut - 1)];
+  if (u >= (uint32_t)kWfLut) x = log10_slow(u, slut);
   return x;
 }
 
@@ -67,7 +67,7 @@ __device__ __forceinline__ void welford1(double x, double rn, double& mu, double
 }
 
 constexpr int kWfThreads = 256;
-constexpr int kWfGroup = 4;  // sites per pipeline stage (two stages in flight)
+constexpr int kWfGroup = 2;  // sites per pipeline stage (two stages in flight)
 constexpr int kWfMaxParts = 4;
 
 // 1/n for the sites of one launch (uniform per site: read with scalar loads)
@@ -76,25 +76,24 @@ __global__ void k_rn_table(double* __restrict__ rn, int64_t n0, int64_t n) {
   if (i < n) rn[i] = 1.0 / (double)(n0 + i + 1);
 }
 
-// Stats transform of eight pixels: LDS LUT gather (index clamped with one
-// v_min), then the rare values beyond it patched one lane-slot at a time, so a
-// single inlined log10 serves all eight slots.
+// Stats transform of eight pixels: LDS LUT gather of each value's low 12
+// bits (no clamp: the index stays in the table), then -- only when a word has
+// a value >= 4,096 -- those slots patched one at a time, so a single inlined
+// log10 serves all eight.  The inner loop is VALU-issue bound (3 f64 ops per
+// pixel at half rate), so the integer work per pixel is kept to the gather
+// address.
 template <bool LOG>
 __device__ __forceinline__ void xform8(const uint4 v, const double* slut, double (&x)[8]) {
   const uint32_t u[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
                          v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
   if (LOG) {
-    constexpr uint32_t kTop = kWfLut - 1;
-    uint32_t mx = 0;
+    constexpr uint32_t kIdx = kWfLut - 1;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      mx = u[k] > mx ? u[k] : mx;
-      x[k] = slut[u[k] < kTop ? u[k] : kTop];
-    }
-    if (mx > kTop) {
+    for (int k = 0; k < 8; ++k) x[k] = slut[u[k] & kIdx];
+    if ((v.x | v.y | v.z | v.w) & 0xF000F000u) {
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        if (u[k] > kTop) x[k] = log10_slow(u[k], slut);
+        if (u[k] > kIdx) x[k] = log10_slow(u[k], slut);
     }
   } else {
 #pragma unroll
@@ -156,15 +155,19 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
   xform8<LOG>(cur[0], slut, K);
 #pragma unroll
   for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.0;
-  for (int64_t s = 0; s < n_sites; s += kWfGroup) {
+  // 32-bit site counters: the per-site bounds test is then one scalar compare
+  // (gfx9 has no 64-bit scalar less-than; an int64 test costs two VALU ops
+  // per site in a VALU-issue-bound loop)
+  const int ns = (int)n_sites;
+  for (int s = 0; s < ns; s += kWfGroup) {
 #pragma unroll
     for (int k = 0; k < kWfGroup; ++k) {
-      const int64_t t = s + kWfGroup + k;
-      nxt[k] = ld_site<NTL>(src + (t < last ? t : last) * ngroups);
+      const int t = s + kWfGroup + k;
+      nxt[k] = ld_site<NTL>(src + (int64_t)(t < (int)last ? t : (int)last) * ngroups);
     }
 #pragma unroll
     for (int k = 0; k < kWfGroup; ++k) {
-      if (s + k < n_sites) {
+      if (s + k < ns) {
         double x[8];
         xform8<LOG>(cur[k], slut, x);
 #pragma unroll
@@ -276,40 +279,20 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_scalar(
   m2[p] = q;
 }
 
-// Site parts for one launch.  Each thread streams every site of its part, so
-// a launch is a few long "rounds" of resident workgroups; when the pixel
-// groups leave the last round mostly empty (2160x2560: 2,700 workgroups over
-// 1,024 resident -> 2.64 rounds), splitting the sites into f parts evens it
-// out (f = 3: 7.9 rounds of 1/3 the work) for one extra pass over 16*f B/px
-// of partial state.  forced (tmh_stats_set_option TMH_OPT_WELFORD_PARTS, for
-// tests) overrides the choice where the split is possible.
-static int welford_parts(int64_t n_wg, int64_t n_sites, int64_t npx, size_t part_cap, int forced) {
-  static const int64_t slots = [] {
-    int dev = 0, cu = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_welford_vec8<true>, kWfThreads, 0) !=
-            hipSuccess)
-      return (int64_t)0;
-    return (int64_t)cu * per_cu;
-  }();
+// Site parts for one launch.  Each thread streams every site of its part;
+// splitting the sites into f parts gives f times the workgroups (shorter
+// dispatch tail) for one extra pass over 16*f B/px of partial state plus a
+// merge.  Measured at 2160x2560 x 3,456 sites with the issue-trimmed loop
+// (tools/mb/mb_welford.hip, profiles/r2/mb_welford_r2f.txt): 1 part 5.85 ms,
+// 2 parts 5.98, 3 parts 6.00, 4 parts 6.18 -- so a launch is one part unless
+// forced (tmh_stats_set_option TMH_OPT_WELFORD_PARTS, for tests), where the
+// split is possible.
+static int welford_parts(int64_t n_sites, int64_t npx, size_t part_cap, int forced) {
   auto fits = [&](int f) {
     return f >= 1 && f <= kWfMaxParts && (f == 1 || ((size_t)2 * f * npx <= part_cap &&
                                                     n_sites >= (int64_t)f * 32));
   };
-  if (forced) return fits(forced) ? forced : 1;
-  if (slots <= 0) return 1;
-  int best = 1;
-  double best_t = (double)((n_wg + slots - 1) / slots);
-  for (int f = 2; f <= kWfMaxParts; ++f) {
-    if (!fits(f)) continue;
-    const double t = (double)((n_wg * f + slots - 1) / slots) / f + 0.02 * f;  // + merge pass
-    if (t < best_t - 1e-9) {
-      best_t = t;
-      best = f;
-    }
-  }
-  return best;
+  return forced && fits(forced) ? forced : 1;
 }
 
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
@@ -320,7 +303,7 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
   const bool vec = (npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0;
   if (vec) {
     const int64_t n_wg = cdiv(npx >> 3, kWfThreads);
-    const int f = part ? welford_parts(n_wg, n_sites, npx, part_cap, forced_parts) : 1;
+    const int f = part ? welford_parts(n_sites, npx, part_cap, forced_parts) : 1;
     const int64_t per = cdiv(n_sites, f);
     const double nl = (double)n_sites, n = (double)(n0 + n_sites);
     const WfMerge mg{1.0 / nl, nl / n, (double)n0 * nl / n, n0 == 0};

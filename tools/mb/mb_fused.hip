@@ -1,0 +1,173 @@
+// Microbenchmark (development tool, not shipped): where the fused correct +
+// histogram pass stands against plain copies of the same bytes on this box.
+//   copy_*     4 B/px copies of the bench's sites (grid-stride, 4 loads in flight)
+//   fused ABL  the production kernel with ablations: 0 = production,
+//              1 = no histogram, 3 = no histogram + constant coefficients,
+//              8 = no LDS flush
+// Usage: mb_fused [n_sites=3456] [reps=3] [H=2160] [W=2560]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../tmlibrary_amd/csrc/common.h"
+#include "../../tmlibrary_amd/csrc/fused_kernels.hip"
+
+#define CK(x)                                                                                  \
+  do {                                                                                         \
+    hipError_t e = (x);                                                                        \
+    if (e != hipSuccess) {                                                                     \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e));        \
+      exit(1);                                                                                 \
+    }                                                                                          \
+  } while (0)
+
+namespace tmh {  // no per-kernel event timing in this tool
+ProfScope::ProfScope(const char* n, hipStream_t s) : name_(n), s_(s), slot_(nullptr) {}
+ProfScope::~ProfScope() {}
+}  // namespace tmh
+
+using namespace tmh;
+typedef unsigned int u32x4m __attribute__((ext_vector_type(4)));
+
+template <int U, int MODE>  // MODE 0 plain, 1 nontemporal loads + stores, 2 nt loads only
+__global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ p, uint4* __restrict__ q,
+                                              int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += U * stride) {
+    u32x4m v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t j = i + k * stride;
+      if (j < n)
+        v[k] = MODE ? __builtin_nontemporal_load(reinterpret_cast<const u32x4m*>(p + j))
+                    : *reinterpret_cast<const u32x4m*>(p + j);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t j = i + k * stride;
+      if (j < n) {
+        if (MODE == 1)
+          __builtin_nontemporal_store(v[k], reinterpret_cast<u32x4m*>(q + j));
+        else
+          *reinterpret_cast<u32x4m*>(q + j) = v[k];
+      }
+    }
+  }
+}
+
+// sink for the read-only stream
+template <int U>
+__global__ __launch_bounds__(256) void k_read(const uint4* __restrict__ p, int64_t n,
+                                              uint32_t* __restrict__ sink) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  uint32_t acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += U * stride) {
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t j = i + k * stride;
+      if (j < n) {
+        const u32x4m v = __builtin_nontemporal_load(reinterpret_cast<const u32x4m*>(p + j));
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+      }
+    }
+  }
+  if (acc == 0x9u) sink[0] = acc;
+}
+
+int main(int argc, char** argv) {
+  const int64_t S = argc > 1 ? atoll(argv[1]) : 3456;
+  const int reps = argc > 2 ? atoi(argv[2]) : 3;
+  const int H = argc > 3 ? atoi(argv[3]) : 2160, W = argc > 4 ? atoi(argv[4]) : 2560;
+  const int64_t npx = (int64_t)H * W;
+  const int64_t bytes = S * npx * 2;
+  uint16_t *in, *out;
+  CK(hipMalloc(&in, bytes));
+  CK(hipMalloc(&out, bytes));
+  CK(hipMemset(in, 0, bytes));
+  // a synthetic-looking site: values ~ 100..3000 (the LDS slice), a few above
+  {
+    std::vector<uint16_t> site(npx);
+    uint64_t z = 88172645463325252ull;
+    for (int64_t i = 0; i < npx; ++i) {
+      z ^= z << 13; z ^= z >> 7; z ^= z << 17;
+      const uint32_t r = (uint32_t)(z >> 40);
+      site[i] = (uint16_t)(100 + (r % 2900) * ((r >> 12) % 3 == 0 ? 1 : 0) + (r & 255));
+      if ((r & 0xFFFF) == 7) site[i] = 65535;
+    }
+    for (int64_t s = 0; s < S; ++s) CK(hipMemcpy(in + s * npx, site.data(), npx * 2, hipMemcpyHostToDevice));
+  }
+  float4 *coef, *mconst2;
+  uint32_t* hist;
+  unsigned long long *rmask, *fe;
+  unsigned int* fn;
+  int* queues;
+  uint32_t* sink;
+  CK(hipMalloc(&coef, npx * 8));
+  CK(hipMalloc(&mconst2, 16));
+  CK(hipMalloc(&hist, (size_t)S * 65536 * 4));
+  CK(hipMalloc(&rmask, S * 8));
+  CK(hipMalloc(&fe, (size_t)1 << 23));
+  CK(hipMalloc(&fn, 4));
+  CK(hipMalloc(&queues, 64));
+  CK(hipMalloc(&sink, 64));
+  {
+    std::vector<float> c(npx * 2);
+    for (int64_t i = 0; i < npx * 2; ++i) c[i] = (i & 2) ? 1.02f : 8.3f;  // (mu, mu, a, a) planes
+    CK(hipMemcpy(coef, c.data(), npx * 8, hipMemcpyHostToDevice));
+    const float m[4] = {8.2f, 0.0f, 1e-10f, 3.0e38f};  // T huge: nothing flagged
+    CK(hipMemcpy(mconst2, m, 16, hipMemcpyHostToDevice));
+  }
+  CK(hipMemset(hist, 0, (size_t)S * 65536 * 4));
+  CK(hipMemset(rmask, 0, S * 8));
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const FixList fl{fe, fn, (unsigned)(((size_t)1 << 23) / 8)};
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  auto time = [&](const char* name, double alg_bytes, auto&& launch) {
+    launch();
+    CK(hipDeviceSynchronize());
+    float best = 1e30f, tot = 0.f;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(a, 0));
+      launch();
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      best = ms < best ? ms : best;
+      tot += ms;
+    }
+    printf("%-34s %9.3f ms (best %8.3f)  %7.1f GB/s  %5.1f%% of 8 TB/s\n", name, tot / reps, best,
+           alg_bytes / (tot / reps * 1e-3) / 1e9, 100.0 * alg_bytes / (tot / reps * 1e-3) / 8e12);
+  };
+  const int64_t n16 = bytes / 16;
+  const double cb = 2.0 * bytes;
+  for (int g : {1024, 2048, 4096}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "copy plain u4 grid%d", g);
+    time(nm, cb, [&] { hipLaunchKernelGGL((k_copy<4, 0>), dim3(g), dim3(256), 0, 0, (const uint4*)in, (uint4*)out, n16); });
+    snprintf(nm, sizeof nm, "copy nt u4 grid%d", g);
+    time(nm, cb, [&] { hipLaunchKernelGGL((k_copy<4, 1>), dim3(g), dim3(256), 0, 0, (const uint4*)in, (uint4*)out, n16); });
+    snprintf(nm, sizeof nm, "copy ntload u4 grid%d", g);
+    time(nm, cb, [&] { hipLaunchKernelGGL((k_copy<4, 2>), dim3(g), dim3(256), 0, 0, (const uint4*)in, (uint4*)out, n16); });
+  }
+  time("read nt u4 grid2048 (2 B/px)", (double)bytes, [&] { hipLaunchKernelGGL((k_read<4>), dim3(2048), dim3(256), 0, 0, (const uint4*)in, n16, sink); });
+  const dim3 fg(cus * 2), fb(512);
+  auto fused = [&](auto abl_tag) {
+    constexpr int ABL = decltype(abl_tag)::value;
+    CK(hipMemsetAsync(queues, 0, 32, 0));
+    CK(hipMemsetAsync(fn, 0, 4, 0));
+    hipLaunchKernelGGL((k_correct_hist<true, false, 4, ABL, 512, 16384>), fg, fb, 0, 0, in, out,
+                       npx, S, coef, mconst2, fl, -1, -1, hist, rmask, queues, kBandsPerXcd);
+  };
+  time("fused prod (ABL 0)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 0>()); });
+  time("fused no hist (ABL 1)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 1>()); });
+  time("fused no hist, const coef (ABL 3)", cb, [&] { fused(std::integral_constant<int, 3>()); });
+  time("fused no flush (ABL 8)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 8>()); });
+  time("fused prod (ABL 0) again", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 0>()); });
+  return 0;
+}
