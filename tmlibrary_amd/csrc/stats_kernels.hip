@@ -576,6 +576,55 @@ __device__ __forceinline__ void hist_tail(CountFn count, DoneFn done, int64_t s,
   }
 }
 
+// hist_tail for a histogram whose possibly non-empty 1,024-bin rounds are
+// known up front (need: bit j = round j): only those rounds are loaded and
+// scanned -- one count load per thread and one or two barriers per round, the
+// next round's counts in flight while the current one is scanned -- instead
+// of walking all 64 rounds.  Same outputs as hist_tail (site_hist rows are
+// zero-filled for the rounds not visited).
+template <int ABL = 0, typename CountFn, typename DoneFn>
+__device__ __forceinline__ void hist_tail_rounds(unsigned long long need, CountFn count,
+                                                 DoneFn done, int64_t s, const QPos& p,
+                                                 uint32_t* __restrict__ vlh_all,
+                                                 unsigned long long* __restrict__ pooled,
+                                                 int64_t* __restrict__ zero_counts,
+                                                 uint32_t* __restrict__ site_hist,
+                                                 uint32_t* slots, int32_t* starts) {
+  const int tid = threadIdx.x;
+  uint32_t* vlh = vlh_all + s * (int64_t)p.Q;
+  const bool vec16 = (p.Q & 7) == 0;
+  if (site_hist) {  // debug/parity copy: the rounds not visited are empty
+    for (int j = 0; j < kBins / kHistThreads; ++j)
+      if (!((need >> j) & 1ull)) site_hist[s * kBins + (uint32_t)j * kHistThreads + tid] = 0u;
+  }
+  int64_t base = 0;  // exclusive rank of the current round's first bin
+  int nscan = 0;
+  uint32_t cn = need ? count((uint32_t)__builtin_ctzll(need) * kHistThreads + tid) : 0u;
+  while (need) {
+    const int j = __builtin_ctzll(need);
+    need &= need - 1ull;
+    const uint32_t c = cn;
+    if (need) cn = count((uint32_t)__builtin_ctzll(need) * kHistThreads + tid);
+    const uint32_t b = (uint32_t)j * kHistThreads + tid;
+    if (site_hist) site_hist[s * kBins + b] = c;
+    if (b == 0 && zero_counts) zero_counts[s] = c;
+    done(b, c);
+    uint32_t total;
+    // slots and R are double-buffered by scan parity: every scan flips it
+    const int64_t r = base + block_exscan(c, slots, nscan, &total);
+    int32_t* R = starts + (nscan & 1) * kHistThreads;
+    ++nscan;
+    if (total == 0) continue;  // uniform: an empty round
+    const int64_t r0 = base;
+    base += total;
+    if (c && !(ABL & 4)) atomicAdd(&pooled[b], (unsigned long long)c);
+    if (ABL & 1) continue;
+    R[tid] = (int32_t)(r + c);
+    __syncthreads();  // R visible; the other R buffer is rewritten only after the next scan
+    fill_groups(R, r0, base, (uint32_t)j * kHistThreads, p, vlh, vec16);
+  }
+}
+
 __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
     const uint16_t* __restrict__ sites, int64_t npx, int vec, uint32_t* __restrict__ hist_hi,
     const QPos p, uint32_t* __restrict__ vlh_all,
@@ -651,22 +700,20 @@ __global__ __launch_bounds__(kHistThreads, 8) void k_hist_finalize(
   __shared__ int32_t starts[2 * kHistThreads];
   const int64_t s = blockIdx.x;
   const unsigned long long rm = rmask ? rmask[s] : ~0ull;
-  if (threadIdx.x < 3) cmask[threadIdx.x] = 0u;
+  (void)cmask;
   __syncthreads();
   if (rmask && !(ABL & 8) && threadIdx.x == 0) rmask[s] = 0ull;  // every thread has read it
   uint32_t* h = hist + s * (int64_t)kBins;
   // sites spread their pooled-histogram adds over n_pooled copies (fewer
   // same-address atomic collisions); k_pooled_fold sums the copies
   unsigned long long* pl = pooled + (int64_t)(blockIdx.x % n_pooled) * kBins;
-  hist_tail<ABL & 7, 4>(
-      [&](uint32_t b) -> uint32_t {
-        const uint32_t j = b >> 10;
-        return ((int)j < dense_rounds || ((rm >> j) & 1ull)) ? h[b] : 0u;
-      },
+  const unsigned long long dense = dense_rounds >= 64 ? ~0ull : ((1ull << dense_rounds) - 1ull);
+  hist_tail_rounds<ABL & 7>(
+      dense | rm, [&](uint32_t b) -> uint32_t { return h[b]; },
       [&](uint32_t b, uint32_t c) {
         if (!(ABL & 8) && c) h[b] = 0u;
       },
-      s, p, vlh_all, pl, zero_counts, site_hist, slots, cmask, starts);
+      s, p, vlh_all, pl, zero_counts, site_hist, slots, starts);
 }
 
 // pooled[b] += sum of the copies; copies reset to zero (zero-maintained)
