@@ -251,7 +251,9 @@ struct tmh_stats {
   QPos qp{};
   DBuf<uint16_t> stage;  // two device slots of batch_cap sites
   HostPipe pipe;
-  DBuf<uint32_t> vlh;  // per site Q x (previous | next << 16) order statistics
+  DBuf<uint32_t> vlh;  // order statistics (previous | next << 16), quantile-tiled (common.h)
+  int64_t vlh_cap = 0;   // deferred mode: sites the tiles have room for
+  int64_t vlh_ld = 0;    // tile stride in sites of the current contents
   DBuf<int64_t> zeros;
 };
 
@@ -308,11 +310,16 @@ int tmh_synchronize(void* stream) {
 // stats
 // ---------------------------------------------------------------------------
 
+// words of order statistics for n sites (quantile tiles of kOsTile)
+static size_t os_words(const tmh_stats* h, int64_t n_sites) {
+  return (size_t)n_sites * (size_t)os_tiles(h->Q) * kOsTile;
+}
+
 static void stats_reserve_sites(tmh_stats* h, int64_t n_sites) {
   // growing frees buffers earlier launches may still be using
   const bool grow = (size_t)n_sites * kHiBins > h->hist_hi.n || (size_t)n_sites > h->zeros.n ||
                     ((h->flags & 2u) && (size_t)n_sites * kBins > h->site_hist.n) ||
-                    (!(h->flags & TMH_STATS_DEFERRED_PCT) && (size_t)n_sites * h->Q > h->vlh.n);
+                    (!(h->flags & TMH_STATS_DEFERRED_PCT) && os_words(h, n_sites) > h->vlh.n);
   if (grow) {
     TMH_HIP(hipStreamSynchronize(h->stream));
     TMH_HIP(hipStreamSynchronize(h->side));
@@ -323,23 +330,34 @@ static void stats_reserve_sites(tmh_stats* h, int64_t n_sites) {
   h->zeros.ensure((size_t)n_sites);
   if (h->flags & 2u) h->site_hist.ensure((size_t)n_sites * kBins);
   if (!(h->flags & TMH_STATS_DEFERRED_PCT)) {
-    h->vlh.ensure((size_t)n_sites * h->Q);
+    h->vlh.ensure(os_words(h, n_sites));
   }
 }
 
+// Deferred mode keeps every site's order statistics: room for n_deferred +
+// extra sites, growing geometrically; the tiles' stride is the capacity, so a
+// growth re-lays the stored sites out (one 2-D copy: a row per tile).
 static void stats_grow_deferred(tmh_stats* h, int64_t extra) {
-  const size_t need = (size_t)(h->n_deferred + extra) * h->Q;
-  if (need <= h->vlh.n) return;
-  const size_t cap = std::max(need, h->vlh.n * 2);
+  const int64_t need = h->n_deferred + extra;
+  if (need <= h->vlh_cap) {
+    h->vlh_ld = h->vlh_cap;
+    return;
+  }
+  const int64_t cap = std::max(need, 2 * h->vlh_cap);
   DBuf<uint32_t> nb;
-  nb.alloc(cap);
-  if (h->n_deferred)
-    TMH_HIP(hipMemcpyAsync(nb.p, h->vlh.p, (size_t)h->n_deferred * h->Q * sizeof(uint32_t),
-                           hipMemcpyDeviceToDevice, h->stream));
+  nb.alloc(os_words(h, cap));
+  if (h->n_deferred) {
+    const size_t row = (size_t)kOsTile * 4;
+    TMH_HIP(hipMemcpy2DAsync(nb.p, (size_t)cap * row, h->vlh.p, (size_t)h->vlh_cap * row,
+                             (size_t)h->n_deferred * row, (size_t)os_tiles(h->Q),
+                             hipMemcpyDeviceToDevice, h->stream));
+  }
   TMH_HIP(hipStreamSynchronize(h->stream));
   TMH_HIP(hipStreamSynchronize(h->side));
   std::swap(h->vlh.p, nb.p);
   std::swap(h->vlh.n, nb.n);
+  h->vlh_cap = cap;
+  h->vlh_ld = cap;
 }
 
 int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo,
@@ -495,14 +513,16 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
   // order statistics, in chunks so the per-site slabs stay bounded
   for (int64_t c0 = 0; c0 < ns; c0 += chunk) {
     const int64_t nc = std::min(chunk, ns - c0);
-    uint32_t* vlh = h->vlh.p;
-    if (h->flags & TMH_STATS_DEFERRED_PCT) vlh += (size_t)h->n_deferred * h->Q;
-    launch_hist_scatter(d + c0 * h->npx, h->npx, nc, h->hist_hi.p, h->qp, vlh, h->pooled.p,
+    const bool deferred = (h->flags & TMH_STATS_DEFERRED_PCT) != 0;
+    uint32_t* vlh = h->vlh.p + (deferred ? (size_t)h->n_deferred * kOsTile : 0);
+    const int64_t ld = deferred ? h->vlh_cap : nc;
+    launch_hist_scatter(d + c0 * h->npx, h->npx, nc, h->hist_hi.p, h->qp, vlh, ld, h->pooled.p,
                         h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr, hs);
-    if (h->flags & TMH_STATS_DEFERRED_PCT)
+    if (deferred)
       h->n_deferred += nc;
     else
-      launch_pct_accumulate(vlh, nc, h->Q, h->gamma.p, h->acc.p, hs);
+      launch_pct_accumulate(vlh, nc, ld, h->Q, h->gamma.p, h->acc.p, hs);
+    h->vlh_ld = ld;
     h->last_batch = nc;
   }
   if (!serial) {
@@ -597,7 +617,8 @@ int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites, 
 static void stats_pct_sum_device(tmh_stats* h) {
   if ((h->flags & TMH_STATS_DEFERRED_PCT) && !h->pct_sum_external) {
     TMH_HIP(hipMemsetAsync(h->acc.p, 0, (size_t)h->Q * 8, h->stream));
-    launch_pct_accumulate(h->vlh.p, h->n_deferred, h->Q, h->gamma.p, h->acc.p, h->stream);
+    launch_pct_accumulate(h->vlh.p, h->n_deferred, h->vlh_cap, h->Q, h->gamma.p, h->acc.p,
+                          h->stream);
   }
 }
 
@@ -674,10 +695,12 @@ int tmh_stats_site_order_stats(tmh_stats* h, int64_t site, uint16_t* host_vlo, u
     const bool deferred = h->flags & TMH_STATS_DEFERRED_PCT;
     const int64_t avail = deferred ? h->n_deferred : h->last_batch;
     TMH_CHECK(site >= 0 && site < avail, TMH_EINVAL, "site not available");
-    const size_t off = (size_t)site * h->Q;
-    std::vector<uint32_t> w((size_t)h->Q);
-    TMH_HIP(hipMemcpyAsync(w.data(), h->vlh.p + off, (size_t)h->Q * 4, hipMemcpyDeviceToHost,
-                           h->stream));
+    // one site's column of every quantile tile
+    const size_t row = (size_t)kOsTile * 4;
+    std::vector<uint32_t> w((size_t)os_tiles(h->Q) * kOsTile);
+    TMH_HIP(hipMemcpy2DAsync(w.data(), row, h->vlh.p + (size_t)site * kOsTile,
+                             (size_t)h->vlh_ld * row, row, (size_t)os_tiles(h->Q),
+                             hipMemcpyDeviceToHost, h->stream));
     TMH_HIP(hipStreamSynchronize(h->stream));
     for (int64_t q = 0; q < h->Q; ++q) {
       host_vlo[q] = (uint16_t)(w[q] & 0xFFFFu);
@@ -723,7 +746,7 @@ int tmh_stats_pct_accumulate(tmh_stats* h, double* dev_acc, void* stream) {
     TMH_CHECK(h && dev_acc, TMH_EINVAL, "bad arguments");
     TMH_CHECK(h->flags & TMH_STATS_DEFERRED_PCT, TMH_ESTATE,
               "percentile chain needs a TMH_STATS_DEFERRED_PCT handle");
-    launch_pct_accumulate(h->vlh.p, h->n_deferred, h->Q, h->gamma.p, dev_acc,
+    launch_pct_accumulate(h->vlh.p, h->n_deferred, h->vlh_cap, h->Q, h->gamma.p, dev_acc,
                           pick(h->stream, stream));
   });
 }
@@ -736,7 +759,7 @@ int tmh_stats_pct_accumulate_range(tmh_stats* h, double* dev_acc_range, int q_be
               "percentile chain needs a TMH_STATS_DEFERRED_PCT handle");
     TMH_CHECK(q_begin >= 0 && q_count >= 0 && (int64_t)q_begin + q_count <= h->Q, TMH_EINVAL,
               "quantile range out of bounds");
-    launch_pct_accumulate_range(h->vlh.p, h->n_deferred, h->Q, q_begin, q_count, h->gamma.p,
+    launch_pct_accumulate_range(h->vlh.p, h->n_deferred, h->vlh_cap, q_begin, q_count, h->gamma.p,
                                 dev_acc_range, pick(h->stream, stream));
   });
 }
@@ -1065,8 +1088,7 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       const bool grow = (size_t)n_sites * kBins > h->hist_full.n || (size_t)n_sites > h->zeros.n ||
                         (size_t)n_sites > h->hist_rmask.n ||
                         ((h->flags & 2u) && (size_t)n_sites * kBins > h->site_hist.n) ||
-                        (!(h->flags & TMH_STATS_DEFERRED_PCT) &&
-                         (size_t)n_sites * h->Q > h->vlh.n);
+                        (!(h->flags & TMH_STATS_DEFERRED_PCT) && os_words(h, n_sites) > h->vlh.n);
       if (grow) {
         TMH_HIP(hipStreamSynchronize(s));
         TMH_HIP(hipStreamSynchronize(h->stream));
@@ -1078,13 +1100,17 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       h->zeros.ensure((size_t)n_sites);
       if (h->flags & 2u) h->site_hist.ensure((size_t)n_sites * kBins);
       uint32_t* vlh;
+      int64_t ld;
       if (h->flags & TMH_STATS_DEFERRED_PCT) {
         stats_grow_deferred(h, n_sites);
-        vlh = h->vlh.p + (size_t)h->n_deferred * h->Q;
+        vlh = h->vlh.p + (size_t)h->n_deferred * kOsTile;
+        ld = h->vlh_cap;
       } else {
-        h->vlh.ensure((size_t)n_sites * h->Q);
+        h->vlh.ensure(os_words(h, n_sites));
         vlh = h->vlh.p;
+        ld = n_sites;
       }
+      h->vlh_ld = ld;
       // the histogram slab and round masks are zero-maintained: the fused pass
       // fills them and k_hist_finalize resets what it read; if anything fails
       // in between, tmh_stats_reset clears them (hist_dirty)
@@ -1096,10 +1122,10 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       launch_fix_correct(dev_in, dev_out, 2, c->npx, n_sites, fl, c->coef64.p, c->rc.p,
                          c->log_transform, clip_lo, clip_hi, s);
       launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, correct_hist_dense_rounds(h->fused_cfg),
-                           n_sites, h->qp, vlh, h->pooled.p, h->pooled_parts.p, kPooledParts,
+                           n_sites, h->qp, vlh, ld, h->pooled.p, h->pooled_parts.p, kPooledParts,
                            h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr, s);
       if (!(h->flags & TMH_STATS_DEFERRED_PCT))
-        launch_pct_accumulate(vlh, n_sites, h->Q, h->gamma.p, h->acc.p, s);
+        launch_pct_accumulate(vlh, n_sites, ld, h->Q, h->gamma.p, h->acc.p, s);
       h->hist_dirty = false;
       if (h->flags & TMH_STATS_DEFERRED_PCT) h->n_deferred += n_sites;
       h->last_batch = n_sites;
@@ -1118,7 +1144,7 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       // per-site buffers (growing frees memory earlier launches may still use)
       const bool grow = (size_t)nc > h->zeros.n ||
                         ((h->flags & 2u) && (size_t)nc * kBins > h->site_hist.n) ||
-                        (!(h->flags & TMH_STATS_DEFERRED_PCT) && (size_t)nc * h->Q > h->vlh.n);
+                        (!(h->flags & TMH_STATS_DEFERRED_PCT) && os_words(h, nc) > h->vlh.n);
       if (grow) {
         TMH_HIP(hipStreamSynchronize(s));
         TMH_HIP(hipStreamSynchronize(h->stream));
@@ -1127,25 +1153,29 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       h->zeros.ensure((size_t)nc);
       if (h->flags & 2u) h->site_hist.ensure((size_t)nc * kBins);
       uint32_t* vlh;
+      int64_t ld;
       if (h->flags & TMH_STATS_DEFERRED_PCT) {
         stats_grow_deferred(h, nc);
-        vlh = h->vlh.p + (size_t)h->n_deferred * h->Q;
+        vlh = h->vlh.p + (size_t)h->n_deferred * kOsTile;
+        ld = h->vlh_cap;
       } else {
-        h->vlh.ensure((size_t)nc * h->Q);
+        h->vlh.ensure(os_words(h, nc));
         vlh = h->vlh.p;
+        ld = nc;
       }
+      h->vlh_ld = ld;
       stats_reserve_sites(h, nc);
       const FixList fl = corrector_fixlist(c, nc, s);
       launch_correct_u16(din, dout, c->npx, nc, c->coef.p, c->lut.p, c->mconst.p, fl,
                          c->log_transform, clip_lo, clip_hi, s);
       launch_fix_correct(din, dout, 2, c->npx, nc, fl, c->coef64.p, c->rc.p, c->log_transform,
                          clip_lo, clip_hi, s);
-      launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->qp, vlh, h->pooled.p, h->zeros.p,
+      launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->qp, vlh, ld, h->pooled.p, h->zeros.p,
                           (h->flags & 2u) ? h->site_hist.p : nullptr, s);
       if (h->flags & TMH_STATS_DEFERRED_PCT)
         h->n_deferred += nc;
       else
-        launch_pct_accumulate(vlh, nc, h->Q, h->gamma.p, h->acc.p, s);
+        launch_pct_accumulate(vlh, nc, ld, h->Q, h->gamma.p, h->acc.p, s);
       h->last_batch = nc;
       h->pending -= nc;
     }

@@ -60,7 +60,16 @@ struct QPos {
   double scale;  // (Q - 1) / (n - 1): the quantile at a sorted position, up to rounding
   int32_t last;  // n - 1
   int hi_next;   // hi[q] == min(lo[q] + 1, n - 1) for every q: hi is not read
+  int64_t tstride;  // order statistics: words between quantile tiles (sites x kOsTile)
 };
+
+// Order statistics (per site and quantile, u32 previous | next << 16) are
+// stored quantile-tiled, [Q / kOsTile][site][kOsTile]: the ordered percentile
+// sum (one thread per quantile, sites in order) then reads a contiguous 1 KB
+// run per site per workgroup instead of 1 KB every Q words.  A buffer with
+// room for C sites has tile stride C * kOsTile words.
+constexpr int kOsTile = 256;
+__host__ __device__ inline int64_t os_tiles(int64_t Q) { return (Q + kOsTile - 1) / kOsTile; }
 
 // ---------------------------------------------------------------------------
 // f64 refinement of the f32 correction
@@ -144,19 +153,20 @@ __device__ __forceinline__ int32_t correct_ref_f64(uint32_t x, double mean, doub
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
                     double* part, size_t part_cap, int forced_parts, hipStream_t s);
+// vlh: the order statistics of the launch's first site (buffer + site *
+// kOsTile) in a buffer with room for vlh_ld sites (kOsTile layout above)
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
-                         const QPos& p, uint32_t* vlh, unsigned long long* pooled,
+                         const QPos& p, uint32_t* vlh, int64_t vlh_ld, unsigned long long* pooled,
                          int64_t* zero_counts, uint32_t* site_hist, hipStream_t s);
 void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_rounds,
-                          int64_t n_sites, const QPos& p, uint32_t* vlh,
+                          int64_t n_sites, const QPos& p, uint32_t* vlh, int64_t vlh_ld,
                           unsigned long long* pooled,
                           unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
                           uint32_t* site_hist, hipStream_t s);
-// order statistics: per site Q u32 words (previous | next << 16)
-void launch_pct_accumulate(const uint32_t* vlh, int64_t n_sites, int Q, const double* gamma,
-                           double* acc, hipStream_t s);
-// quantiles [q_begin, q_begin + q_count) of rows of ld; acc points at the range
-void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t ld, int q_begin,
+void launch_pct_accumulate(const uint32_t* vlh, int64_t n_sites, int64_t vlh_ld, int Q,
+                           const double* gamma, double* acc, hipStream_t s);
+// quantiles [q_begin, q_begin + q_count) only; acc points at the range
+void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t vlh_ld, int q_begin,
                                  int q_count, const double* gamma, double* acc, hipStream_t s);
 void launch_finalize(const double* mean, const double* m2, int64_t n, int64_t npx, double* out_mean,
                      double* out_std, hipStream_t s);

@@ -484,9 +484,11 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
           mh |= 1u << j;
         }
       }
-      // interleaved (previous, next) order statistics: one u32 per quantile
+      // interleaved (previous, next) order statistics: one u32 per quantile,
+      // a group of 8 is contiguous inside one quantile tile
+      uint32_t* og = vlh + (q0 / kOsTile) * p.tstride + (q0 % kOsTile);
       if (vec16 && ml == 0xFFu && mh == 0xFFu) {
-        uint4* dst = reinterpret_cast<uint4*>(vlh + q0);
+        uint4* dst = reinterpret_cast<uint4*>(og);
         dst[0] = make_uint4(__builtin_amdgcn_perm(oh[0], ol[0], 0x05040100u),
                             __builtin_amdgcn_perm(oh[0], ol[0], 0x07060302u),
                             __builtin_amdgcn_perm(oh[1], ol[1], 0x05040100u),
@@ -496,7 +498,7 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
                             __builtin_amdgcn_perm(oh[3], ol[3], 0x05040100u),
                             __builtin_amdgcn_perm(oh[3], ol[3], 0x07060302u));
       } else if (ml | mh) {  // a round edge: write the halves this round owns
-        uint16_t* h16 = reinterpret_cast<uint16_t*>(vlh + q0);
+        uint16_t* h16 = reinterpret_cast<uint16_t*>(og);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           if ((ml >> j) & 1u) h16[2 * j] = (uint16_t)(ol[j >> 1] >> (16 * (j & 1)));
@@ -528,7 +530,7 @@ __device__ __forceinline__ void hist_tail(CountFn count, DoneFn done, int64_t s,
                                           uint32_t* __restrict__ site_hist, uint32_t* slots,
                                           uint32_t* cmask, int32_t* starts) {
   const int tid = threadIdx.x;
-  uint32_t* vlh = vlh_all + s * (int64_t)p.Q;
+  uint32_t* vlh = vlh_all + s * (int64_t)kOsTile;  // this site's column of the tiles
   const bool vec16 = (p.Q & 7) == 0;
   int64_t base = 0;          // exclusive rank of the current round's first bin
   int nscan = 0;
@@ -591,7 +593,7 @@ __device__ __forceinline__ void hist_tail_rounds(unsigned long long need, CountF
                                                  uint32_t* __restrict__ site_hist,
                                                  uint32_t* slots, int32_t* starts) {
   const int tid = threadIdx.x;
-  uint32_t* vlh = vlh_all + s * (int64_t)p.Q;
+  uint32_t* vlh = vlh_all + s * (int64_t)kOsTile;  // this site's column of the tiles
   const bool vec16 = (p.Q & 7) == 0;
   if (site_hist) {  // debug/parity copy: the rounds not visited are empty
     for (int j = 0; j < kBins / kHistThreads; ++j)
@@ -730,27 +732,31 @@ __global__ void k_pooled_fold(unsigned long long* __restrict__ pooled,
 }
 
 void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_rounds,
-                          int64_t n_sites, const QPos& p, uint32_t* vlh,
+                          int64_t n_sites, const QPos& p, uint32_t* vlh, int64_t vlh_ld,
                           unsigned long long* pooled,
                           unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
                           uint32_t* site_hist, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("hist_finalize", s);
+  QPos pp = p;
+  pp.tstride = vlh_ld * kOsTile;
   hipLaunchKernelGGL(k_hist_finalize<0>, dim3((unsigned)n_sites), dim3(kHistThreads), 0, s, hist,
-                     rmask, dense_rounds, p, vlh, pooled_parts, n_parts, zero_counts, site_hist);
+                     rmask, dense_rounds, pp, vlh, pooled_parts, n_parts, zero_counts, site_hist);
   hipLaunchKernelGGL(k_pooled_fold, dim3(kBins / 256), dim3(256), 0, s, pooled, pooled_parts,
                      n_parts);
   TMH_HIP(hipGetLastError());
 }
 
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
-                         const QPos& p, uint32_t* vlh, unsigned long long* pooled,
+                         const QPos& p, uint32_t* vlh, int64_t vlh_ld, unsigned long long* pooled,
                          int64_t* zero_counts, uint32_t* site_hist, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("hist", s);
   const int vec = ((npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0) ? 1 : 0;
+  QPos pp = p;
+  pp.tstride = vlh_ld * kOsTile;
   hipLaunchKernelGGL(k_hist_scatter, dim3((unsigned)n_sites), dim3(kHistThreads), 0, s, sites, npx,
-                     vec, hist_hi, p, vlh, pooled, zero_counts, site_hist);
+                     vec, hist_hi, pp, vlh, pooled, zero_counts, site_hist);
   TMH_HIP(hipGetLastError());
 }
 
@@ -777,22 +783,26 @@ __device__ __forceinline__ double add_nc(double x, double y) {
 constexpr int kPctThreads = 256;
 constexpr int kPctUnroll = 16;
 
-// each thread: two consecutive quantiles (one u32 load of each u16 array)
-// Quantiles [0, Q) of rows of `ld` interleaved (previous, next) order
-// statistics (vlh/gamma/acc point at the range's first quantile: a sub-range
-// of the table is one launch of the pipelined rank chain).  Thread =
-// quantile: one u32 load per site, the lerp off the critical path, and only
-// the f64 add (no contraction) on the in-order dependency chain.
+// Quantiles [q_begin, q_begin + Q) of the quantile-tiled order statistics of
+// n_sites sites (vlh: the first site's column, tstride words between tiles;
+// acc points at the range's first quantile: a sub-range is one launch of the
+// pipelined rank chain).  Thread = quantile: one u32 load per site -- a
+// workgroup's 256 quantiles are one tile, so it streams contiguous 1 KB runs,
+// site after site -- the lerp off the critical path, and only the f64 add (no
+// contraction) on the in-order dependency chain.
 template <bool NTL>
 __global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint32_t* __restrict__ vlh,
-                                                          int64_t n_sites, int Q, int64_t ld,
+                                                          int64_t n_sites, int64_t tstride,
+                                                          int q_begin, int Q,
                                                           const double* __restrict__ gamma,
                                                           double* __restrict__ acc) {
-  const int q = (int)blockIdx.x * kPctThreads + threadIdx.x;
-  if (q >= Q) return;
+  const int t = (int)blockIdx.x * kPctThreads + threadIdx.x;
+  if (t >= Q) return;
+  const int q = q_begin + t;
   const double g = gamma[q];
-  double a = acc[q];
-  const uint32_t* p = vlh + q;
+  double a = acc[t];
+  const uint32_t* p = vlh + (int64_t)(q / kOsTile) * tstride + (q % kOsTile);
+  constexpr int64_t ld = kOsTile;
   // software pipeline: the next kPctUnroll sites' loads are in flight while
   // the current ones are folded in (tail loads clamp to the last site)
   const int64_t last = n_sites - 1;
@@ -803,8 +813,8 @@ __global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint32_t* __restr
     uint32_t vn[kPctUnroll];
 #pragma unroll
     for (int k = 0; k < kPctUnroll; ++k) {
-      const int64_t t = s + kPctUnroll + k < last ? s + kPctUnroll + k : last;
-      vn[k] = NTL ? __builtin_nontemporal_load(p + t * ld) : p[t * ld];
+      const int64_t u = s + kPctUnroll + k < last ? s + kPctUnroll + k : last;
+      vn[k] = NTL ? __builtin_nontemporal_load(p + u * ld) : p[u * ld];
     }
 #pragma unroll
     for (int k = 0; k < kPctUnroll; ++k)
@@ -812,15 +822,15 @@ __global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint32_t* __restr
 #pragma unroll
     for (int k = 0; k < kPctUnroll; ++k) v[k] = vn[k];
   }
-  acc[q] = a;
+  acc[t] = a;
 }
 
-void launch_pct_accumulate(const uint32_t* vlh, int64_t n_sites, int Q, const double* gamma,
-                           double* acc, hipStream_t s) {
-  launch_pct_accumulate_range(vlh, n_sites, Q, 0, Q, gamma, acc, s);
+void launch_pct_accumulate(const uint32_t* vlh, int64_t n_sites, int64_t vlh_ld, int Q,
+                           const double* gamma, double* acc, hipStream_t s) {
+  launch_pct_accumulate_range(vlh, n_sites, vlh_ld, 0, Q, gamma, acc, s);
 }
 
-void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t ld, int q_begin,
+void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t vlh_ld, int q_begin,
                                  int q_count, const double* gamma, double* acc, hipStream_t s) {
   if (n_sites <= 0 || q_count <= 0) return;
   ProfScope prof("pct_acc", s);
@@ -829,8 +839,8 @@ void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t l
   // measured for this choice (profiles/r1/ab_pct_ntl.txt) is within the
   // run-to-run spread of one build (profiles/r1/noise_same_build.txt).
   hipLaunchKernelGGL(k_pct_acc<false>, dim3((unsigned)cdiv(q_count, kPctThreads)),
-                     dim3(kPctThreads), 0, s, vlh + q_begin, n_sites, q_count, ld,
-                     gamma + q_begin, acc);
+                     dim3(kPctThreads), 0, s, vlh, n_sites, vlh_ld * kOsTile, q_begin, q_count,
+                     gamma, acc);
   TMH_HIP(hipGetLastError());
 }
 
