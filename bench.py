@@ -78,6 +78,9 @@ def parse():
     p.add_argument("--cpu-procs", type=int, default=4,
                    help="P of the P-process CPU variant (one channel job per process; "
                         "P = min(this, cores))")
+    p.add_argument("--tail-chunks", type=int, default=None,
+                   help="fused pass in this many site chunks, each chunk's histogram finalize "
+                        "overlapping the next chunk (TMH_OPT_TAIL_CHUNKS; default: the library's)")
     p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
     p.add_argument("--pipeline", choices=["fused", "separate"], default="fused",
                    help="fused: histograms built from the correction's read (6 B/px); "
@@ -399,6 +402,8 @@ def main():
             hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
                                          hip.ptr(lut), 1, flags, C.byref(self.h)))
             hip.check(L.tmh_stats_set_stream(self.h, self.sp))
+            if a.tail_chunks:
+                hip.check(L.tmh_stats_set_option(self.h, hip.TMH_OPT_TAIL_CHUNKS, a.tail_chunks))
             self.corr = C.c_void_p()
             torch.cuda.synchronize(dev)
             hip.check(L.tmh_corrector_create_device(C.c_void_p(self.mean.data_ptr()),

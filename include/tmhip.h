@@ -85,11 +85,15 @@ int tmh_stats_reset(tmh_stats* h);
  *                          fused correct+histogram pass = (2, 1024, 32768),
  *                          (4, 1024, 32768), (2, 512, 16384), (4, 512, 16384);
  *                          default 3
- *   TMH_OPT_WELFORD_PARTS  0: split a Welford launch's sites into parts when it
- *                          fills the GPU better (default); 1..4: force that
- *                          many parts where the launch has >= 32 sites a part */
+ *   TMH_OPT_WELFORD_PARTS  0: automatic (one part); 1..4: split a Welford
+ *                          launch's sites into that many parts, merged in
+ *                          order, where the launch has >= 32 sites a part
+ *   TMH_OPT_TAIL_CHUNKS    1..16: run the fused correct+histogram pass in that
+ *                          many site chunks, each chunk's histogram finalize
+ *                          overlapping the next chunk's streaming (1: off) */
 #define TMH_OPT_FUSED_CONFIG 1
 #define TMH_OPT_WELFORD_PARTS 2
+#define TMH_OPT_TAIL_CHUNKS 3
 int tmh_stats_set_option(tmh_stats* h, int option, int value);
 
 /* update(image) for a run of sites.  zero_counts_out (host, n_sites, may be

@@ -236,6 +236,7 @@ struct tmh_stats {
   hipEvent_t ev_in = nullptr, ev_out = nullptr;  // ordering against a caller's stream
   int fused_cfg = kFusedDefault;  // TMH_OPT_FUSED_CONFIG
   int wf_parts = 0;               // TMH_OPT_WELFORD_PARTS (0: automatic)
+  int tail_chunks = 1;            // TMH_OPT_TAIL_CHUNKS (1: no overlap)
   bool hist_dirty = false;        // a fused launch may have left counts / round masks behind
   int64_t n = 0;              // sites accumulated (Welford count)
   int64_t n_deferred = 0;     // sites whose order statistics are stored
@@ -459,6 +460,10 @@ int tmh_stats_set_option(tmh_stats* h, int option, int value) {
       case TMH_OPT_WELFORD_PARTS:
         TMH_CHECK(value >= 0 && value <= 4, TMH_EINVAL, "Welford parts must be 0..4");
         h->wf_parts = value;
+        break;
+      case TMH_OPT_TAIL_CHUNKS:
+        TMH_CHECK(value >= 1 && value <= 16, TMH_EINVAL, "tail chunks must be 1..16");
+        h->tail_chunks = value;
         break;
       default:
         throw Error{TMH_EINVAL, "unknown option"};
@@ -1115,15 +1120,41 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       // fills them and k_hist_finalize resets what it read; if anything fails
       // in between, tmh_stats_reset clears them (hist_dirty)
       h->hist_dirty = true;
-      const FixList fl = corrector_fixlist(c, n_sites, s);
-      launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p, fl,
-                          c->log_transform, clip_lo, clip_hi, h->hist_full.p, h->hist_rmask.p,
-                          c->queues.p, c->n_wg, h->fused_cfg, s);
-      launch_fix_correct(dev_in, dev_out, 2, c->npx, n_sites, fl, c->coef64.p, c->rc.p,
-                         c->log_transform, clip_lo, clip_hi, s);
-      launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, correct_hist_dense_rounds(h->fused_cfg),
-                           n_sites, h->qp, vlh, ld, h->pooled.p, h->pooled_parts.p, kPooledParts,
-                           h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr, s);
+      // Tail overlap (TMH_OPT_TAIL_CHUNKS = C > 1): the fused pass runs in C
+      // site chunks on s; chunk k's histogram finalize runs on the side
+      // stream in its narrow (256-thread) form, which fits beside the fused
+      // pass's workgroups on a CU, while chunk k+1 streams.  The last chunk's
+      // finalize runs on the whole GPU after both.  Chunks keep site order,
+      // so the ordered percentile sum at the end is unchanged.
+      const int nch = (int)std::min<int64_t>(h->tail_chunks, n_sites / 64 > 0 ? n_sites / 64 : 1);
+      const int dense = correct_hist_dense_rounds(h->fused_cfg);
+      uint32_t* sh = (h->flags & 2u) ? h->site_hist.p : nullptr;
+      if (nch > 1) {
+        TMH_HIP(hipEventRecord(h->ev_fork, s));
+        TMH_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+      }
+      for (int k = 0; k < nch; ++k) {
+        const int64_t c0 = n_sites * k / nch, nc = n_sites * (k + 1) / nch - c0;
+        const FixList fl = corrector_fixlist(c, nc, s);
+        launch_correct_hist(dev_in + c0 * h->npx, dev_out + c0 * h->npx, c->npx, nc, c->coef2.p,
+                            c->mconst2.p, fl, c->log_transform, clip_lo, clip_hi,
+                            h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0,
+                            c->queues.p, c->n_wg, h->fused_cfg, s);
+        launch_fix_correct(dev_in + c0 * h->npx, dev_out + c0 * h->npx, 2, c->npx, nc, fl,
+                           c->coef64.p, c->rc.p, c->log_transform, clip_lo, clip_hi, s);
+        const bool side = k < nch - 1;
+        if (side) {
+          TMH_HIP(hipEventRecord(h->ev_fork, s));
+          TMH_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+        } else if (nch > 1) {
+          TMH_HIP(hipEventRecord(h->ev_join, h->side));
+          TMH_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
+        }
+        launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0, dense, nc,
+                             h->qp, vlh + (size_t)c0 * kOsTile, ld, h->pooled.p, h->pooled_parts.p,
+                             kPooledParts, h->zeros.p + c0, sh ? sh + (size_t)c0 * kBins : nullptr,
+                             side ? h->side : s, side);
+      }
       if (!(h->flags & TMH_STATS_DEFERRED_PCT))
         launch_pct_accumulate(vlh, n_sites, ld, h->Q, h->gamma.p, h->acc.p, s);
       h->hist_dirty = false;

@@ -162,7 +162,7 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
                           int64_t n_sites, const QPos& p, uint32_t* vlh, int64_t vlh_ld,
                           unsigned long long* pooled,
                           unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
-                          uint32_t* site_hist, hipStream_t s);
+                          uint32_t* site_hist, hipStream_t s, bool narrow = false);
 void launch_pct_accumulate(const uint32_t* vlh, int64_t n_sites, int64_t vlh_ld, int Q,
                            const double* gamma, double* acc, hipStream_t s);
 // quantiles [q_begin, q_begin + q_count) only; acc points at the range

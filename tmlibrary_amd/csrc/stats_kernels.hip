@@ -366,12 +366,14 @@ __device__ __forceinline__ void count8(const uint4 v, uint32_t* bins, uint32_t* 
   }
 }
 
-// Exclusive scan of one value per thread over the 1024-thread workgroup.
+// Exclusive scan of one value per thread over an NT-thread workgroup.
 // `slots` holds 2 x 16 wave totals (double-buffered by the parity of the
 // caller's scan counter, so one barrier per scan suffices).  Returns the
 // exclusive prefix; *total = sum.
-__device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, int round,
-                                                 uint32_t* total) {
+template <int NT>
+__device__ __forceinline__ uint32_t block_exscan_t(uint32_t c, uint32_t* slots, int round,
+                                                   uint32_t* total) {
+  static_assert(NT % 64 == 0 && NT <= 1024, "whole waves, at most 16");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t incl = c;
 #pragma unroll
@@ -384,7 +386,7 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, in
   __syncthreads();
   uint32_t woff = 0, all = 0;
 #pragma unroll
-  for (int w = 0; w < 16; ++w) {
+  for (int w = 0; w < NT / 64; ++w) {
     const uint32_t t = ws[w];
     woff += (w < wid) ? t : 0u;
     all += t;
@@ -392,6 +394,13 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, in
   *total = all;
   return woff + incl - c;
 }
+
+__device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, int round,
+                                                 uint32_t* total) {
+  return block_exscan_t<kHistThreads>(c, slots, round, total);
+}
+
+constexpr int kRound = 1024;  // histogram bins per round of the scans
 
 constexpr int kTailChunkDefault = 8;  // rounds whose counts are loaded together
 // Advance (t, Rt = R[t]) to the first index >= t with R[index] > x (R: 1024
@@ -407,7 +416,7 @@ __device__ __forceinline__ void advance_rank(const int32_t* R, int& t, int32_t& 
     Rt = r1;
     return;
   }
-  int lo = t + 1, hi = kHistThreads - 1;  // R[lo] <= x < R[hi]
+  int lo = t + 1, hi = kRound - 1;  // R[lo] <= x < R[hi]
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
     if (R[mid] > x)
@@ -434,6 +443,7 @@ constexpr int kFillGroups = 1;  // groups of 8 quantiles a thread walks in a row
 // ends).  The round's quantile range is [r0 * scale, r1 * scale] up to
 // rounding (and one position's worth of quantiles), so the groups scanned
 // carry a margin and the position test decides membership exactly.
+template <int NT = kHistThreads>
 __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_t r1,
                                             uint32_t bin0, const QPos& p,
                                             uint32_t* __restrict__ vlh, bool vec16) {
@@ -447,7 +457,7 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
   const bool tab16 = vec16;  // tables are 16-B aligned rows when Q % 8 == 0 (hipMalloc base)
   const int32_t a = (int32_t)r0, b = (int32_t)r1;
   for (int64_t sg = g0 + (int64_t)threadIdx.x * kFillGroups; sg <= g1;
-       sg += (int64_t)kHistThreads * kFillGroups) {
+       sg += (int64_t)NT * kFillGroups) {
     int tl = 0, th = 0;
     int32_t Rl = R[0], Rh = Rl;
     for (int64_t g = sg; g < sg + kFillGroups && g <= g1; ++g) {
@@ -580,11 +590,12 @@ __device__ __forceinline__ void hist_tail(CountFn count, DoneFn done, int64_t s,
 
 // hist_tail for a histogram whose possibly non-empty 1,024-bin rounds are
 // known up front (need: bit j = round j): only those rounds are loaded and
-// scanned -- one count load per thread and one or two barriers per round, the
-// next round's counts in flight while the current one is scanned -- instead
-// of walking all 64 rounds.  Same outputs as hist_tail (site_hist rows are
-// zero-filled for the rounds not visited).
-template <int ABL = 0, typename CountFn, typename DoneFn>
+// scanned -- BPT = 1024 / NT consecutive bins per thread, one or two barriers
+// per round, the next round's counts in flight while the current one is
+// scanned -- instead of walking all 64 rounds.  Same outputs as hist_tail
+// (site_hist rows are zero-filled for the rounds not visited).  NT = 256 is
+// the narrow form that fits beside the fused pass's workgroups on a CU.
+template <int ABL, int NT, typename CountFn, typename DoneFn>
 __device__ __forceinline__ void hist_tail_rounds(unsigned long long need, CountFn count,
                                                  DoneFn done, int64_t s, const QPos& p,
                                                  uint32_t* __restrict__ vlh_all,
@@ -592,38 +603,62 @@ __device__ __forceinline__ void hist_tail_rounds(unsigned long long need, CountF
                                                  int64_t* __restrict__ zero_counts,
                                                  uint32_t* __restrict__ site_hist,
                                                  uint32_t* slots, int32_t* starts) {
+  constexpr int BPT = kRound / NT;
   const int tid = threadIdx.x;
   uint32_t* vlh = vlh_all + s * (int64_t)kOsTile;  // this site's column of the tiles
   const bool vec16 = (p.Q & 7) == 0;
   if (site_hist) {  // debug/parity copy: the rounds not visited are empty
-    for (int j = 0; j < kBins / kHistThreads; ++j)
-      if (!((need >> j) & 1ull)) site_hist[s * kBins + (uint32_t)j * kHistThreads + tid] = 0u;
+    for (int j = 0; j < kBins / kRound; ++j)
+      if (!((need >> j) & 1ull))
+#pragma unroll
+        for (int i = 0; i < BPT; ++i) site_hist[s * kBins + (uint32_t)(j * kRound + tid * BPT + i)] = 0u;
   }
   int64_t base = 0;  // exclusive rank of the current round's first bin
   int nscan = 0;
-  uint32_t cn = need ? count((uint32_t)__builtin_ctzll(need) * kHistThreads + tid) : 0u;
+  uint32_t cn[BPT];
+  if (need) {
+    const uint32_t b0 = (uint32_t)__builtin_ctzll(need) * kRound + tid * BPT;
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) cn[i] = count(b0 + i);
+  }
   while (need) {
     const int j = __builtin_ctzll(need);
     need &= need - 1ull;
-    const uint32_t c = cn;
-    if (need) cn = count((uint32_t)__builtin_ctzll(need) * kHistThreads + tid);
-    const uint32_t b = (uint32_t)j * kHistThreads + tid;
-    if (site_hist) site_hist[s * kBins + b] = c;
-    if (b == 0 && zero_counts) zero_counts[s] = c;
-    done(b, c);
+    uint32_t c[BPT], inc[BPT];
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) c[i] = cn[i];
+    if (need) {
+      const uint32_t b0 = (uint32_t)__builtin_ctzll(need) * kRound + tid * BPT;
+#pragma unroll
+      for (int i = 0; i < BPT; ++i) cn[i] = count(b0 + i);
+    }
+    const uint32_t b0 = (uint32_t)j * kRound + tid * BPT;
+    uint32_t run = 0;
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      run += c[i];
+      inc[i] = run;  // inclusive prefix inside the thread's bins
+      const uint32_t b = b0 + i;
+      if (site_hist) site_hist[s * kBins + b] = c[i];
+      if (b == 0 && zero_counts) zero_counts[s] = c[i];
+      done(b, c[i]);
+    }
     uint32_t total;
     // slots and R are double-buffered by scan parity: every scan flips it
-    const int64_t r = base + block_exscan(c, slots, nscan, &total);
-    int32_t* R = starts + (nscan & 1) * kHistThreads;
+    const int64_t r = base + block_exscan_t<NT>(run, slots, nscan, &total);
+    int32_t* R = starts + (nscan & 1) * kRound;
     ++nscan;
     if (total == 0) continue;  // uniform: an empty round
     const int64_t r0 = base;
     base += total;
-    if (c && !(ABL & 4)) atomicAdd(&pooled[b], (unsigned long long)c);
+#pragma unroll
+    for (int i = 0; i < BPT; ++i)
+      if (c[i] && !(ABL & 4)) atomicAdd(&pooled[b0 + i], (unsigned long long)c[i]);
     if (ABL & 1) continue;
-    R[tid] = (int32_t)(r + c);
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) R[tid * BPT + i] = (int32_t)(r + inc[i]);
     __syncthreads();  // R visible; the other R buffer is rewritten only after the next scan
-    fill_groups(R, r0, base, (uint32_t)j * kHistThreads, p, vlh, vec16);
+    fill_groups<NT>(R, r0, base, (uint32_t)j * kRound, p, vlh, vec16);
   }
 }
 
@@ -687,22 +722,22 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
 // Per-site histogram (65,536 counts, exact) -> order statistics, written from
 // a complete histogram held in global memory (zero-maintained: every count is
 // read and reset), e.g. accumulated by the fused correct+histogram pass.
-template <int ABL = 0>  // ABL 8: counts are not reset (re-runnable)
+// ABL 8: counts are not reset (re-runnable).  NT threads per site (1024, or
+// 256: one workgroup fits beside the fused pass's two on a CU -- VGPRs <= 64).
 // rmask (may be NULL: every round is read): per site, the 1,024-bin rounds
 // at or above dense_rounds that hold counts; the others are known empty and
 // are not read (a microscopy site touches a handful of the 64).  The mask is
 // zero-maintained like the counts.
-__global__ __launch_bounds__(kHistThreads, 8) void k_hist_finalize(
+template <int ABL = 0, int NT = kHistThreads>
+__global__ __launch_bounds__(NT, 8) void k_hist_finalize(
     uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask, int dense_rounds,
     const QPos p, uint32_t* __restrict__ vlh_all,
     unsigned long long* __restrict__ pooled, int n_pooled,
     int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist) {
   __shared__ uint32_t slots[32];
-  __shared__ uint32_t cmask[3];
-  __shared__ int32_t starts[2 * kHistThreads];
+  __shared__ int32_t starts[2 * kRound];
   const int64_t s = blockIdx.x;
   const unsigned long long rm = rmask ? rmask[s] : ~0ull;
-  (void)cmask;
   __syncthreads();
   if (rmask && !(ABL & 8) && threadIdx.x == 0) rmask[s] = 0ull;  // every thread has read it
   uint32_t* h = hist + s * (int64_t)kBins;
@@ -710,7 +745,7 @@ __global__ __launch_bounds__(kHistThreads, 8) void k_hist_finalize(
   // same-address atomic collisions); k_pooled_fold sums the copies
   unsigned long long* pl = pooled + (int64_t)(blockIdx.x % n_pooled) * kBins;
   const unsigned long long dense = dense_rounds >= 64 ? ~0ull : ((1ull << dense_rounds) - 1ull);
-  hist_tail_rounds<ABL & 7>(
+  hist_tail_rounds<ABL & 7, NT>(
       dense | rm, [&](uint32_t b) -> uint32_t { return h[b]; },
       [&](uint32_t b, uint32_t c) {
         if (!(ABL & 8) && c) h[b] = 0u;
@@ -735,13 +770,18 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
                           int64_t n_sites, const QPos& p, uint32_t* vlh, int64_t vlh_ld,
                           unsigned long long* pooled,
                           unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
-                          uint32_t* site_hist, hipStream_t s) {
+                          uint32_t* site_hist, hipStream_t s, bool narrow) {
   if (n_sites <= 0) return;
-  ProfScope prof("hist_finalize", s);
+  ProfScope prof(narrow ? "hist_finalize_side" : "hist_finalize", s);
   QPos pp = p;
   pp.tstride = vlh_ld * kOsTile;
-  hipLaunchKernelGGL(k_hist_finalize<0>, dim3((unsigned)n_sites), dim3(kHistThreads), 0, s, hist,
-                     rmask, dense_rounds, pp, vlh, pooled_parts, n_parts, zero_counts, site_hist);
+  if (narrow)
+    hipLaunchKernelGGL((k_hist_finalize<0, 256>), dim3((unsigned)n_sites), dim3(256), 0, s, hist,
+                       rmask, dense_rounds, pp, vlh, pooled_parts, n_parts, zero_counts, site_hist);
+  else
+    hipLaunchKernelGGL((k_hist_finalize<0, kHistThreads>), dim3((unsigned)n_sites),
+                       dim3(kHistThreads), 0, s, hist, rmask, dense_rounds, pp, vlh, pooled_parts,
+                       n_parts, zero_counts, site_hist);
   hipLaunchKernelGGL(k_pooled_fold, dim3(kBins / 256), dim3(256), 0, s, pooled, pooled_parts,
                      n_parts);
   TMH_HIP(hipGetLastError());

@@ -25,6 +25,7 @@ TMH_STATS_KEEP_SITE_HIST = 2
 TMH_STATS_SERIAL = 4
 TMH_OPT_FUSED_CONFIG = 1
 TMH_OPT_WELFORD_PARTS = 2
+TMH_OPT_TAIL_CHUNKS = 3
 TMH_SYNTH_STANDARD = 0
 TMH_SYNTH_BRIGHT = 1
 TMH_SYNTH_UNIFORM = 2
