@@ -81,6 +81,9 @@ def parse():
     p.add_argument("--tail-chunks", type=int, default=None,
                    help="fused pass in this many site chunks, each chunk's histogram finalize "
                         "overlapping the next chunk (TMH_OPT_TAIL_CHUNKS; default: the library's)")
+    p.add_argument("--fused-config", type=int, default=None,
+                   help="fused pass (sites per unit, threads, LDS bins) configuration 0..3 "
+                        "(TMH_OPT_FUSED_CONFIG; default: the library's)")
     p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
     p.add_argument("--pipeline", choices=["fused", "separate"], default="fused",
                    help="fused: histograms built from the correction's read (6 B/px); "
@@ -402,6 +405,8 @@ def main():
             hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
                                          hip.ptr(lut), 1, flags, C.byref(self.h)))
             hip.check(L.tmh_stats_set_stream(self.h, self.sp))
+            if a.fused_config is not None:
+                hip.check(L.tmh_stats_set_option(self.h, hip.TMH_OPT_FUSED_CONFIG, a.fused_config))
             if a.tail_chunks:
                 hip.check(L.tmh_stats_set_option(self.h, hip.TMH_OPT_TAIL_CHUNKS, a.tail_chunks))
             self.corr = C.c_void_p()

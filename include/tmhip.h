@@ -81,10 +81,13 @@ int tmh_stats_set_stream(tmh_stats* h, void* stream);
 int tmh_stats_reset(tmh_stats* h);
 
 /* Launch-shape options of a handle (results never depend on them):
- *   TMH_OPT_FUSED_CONFIG   0..3: (sites per unit, threads, LDS bins) of the
+ *   TMH_OPT_FUSED_CONFIG   0..4: (sites per unit, threads, LDS bins) of the
  *                          fused correct+histogram pass = (2, 1024, 32768),
- *                          (4, 1024, 32768), (2, 512, 16384), (4, 512, 16384);
- *                          default 3
+ *                          (4, 1024, 32768), (2, 512, 16384), (4, 512, 16384),
+ *                          (1, 1024, 32768); -1 (default): per launch, on the
+ *                          device, 3 unless the Welford pass over the pending
+ *                          sites saw >= 2% of 8-pixel groups holding a value
+ *                          >= 4,096, then 0.  Results are identical for all.
  *   TMH_OPT_WELFORD_PARTS  0: automatic (one part); 1..4: split a Welford
  *                          launch's sites into that many parts, merged in
  *                          order, where the launch has >= 32 sites a part
@@ -129,6 +132,11 @@ int tmh_stats_finalize(tmh_stats* h, int64_t* n, double* mean, double* std, doub
 int tmh_stats_finalize_device(tmh_stats* h, double* dev_mean, double* dev_std, void* stream);
 /* var = M2 / (n - 1), NaN everywhere when n < 2 (stats.py:94-102), host copy. */
 int tmh_stats_variance(tmh_stats* h, double* host_var);
+/* Pixel groups (8 consecutive pixels of one site) holding a value >= 4,096
+ * in the sites passed to tmh_stats_update_welford_device since the last fused
+ * pass consumed them (synchronous; diagnostics: the automatic fused
+ * configuration compares it with 2% of the groups).  sites_out may be NULL. */
+int tmh_stats_wide_groups(tmh_stats* h, uint64_t* groups_out, int64_t* sites_out);
 /* Per-site histogram of the most recent update batch (debug/parity). */
 int tmh_stats_site_histogram(tmh_stats* h, int64_t site_in_last_batch, uint32_t* host_hist);
 /* Order statistics at every quantile's previous/next sorted position for one

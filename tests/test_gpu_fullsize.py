@@ -16,6 +16,9 @@ same pixels
 percentile sums bit-exact, corrected pixels within +-1 DN (non-modular) with
 zero wrap flips.
 
+test_bright_fullsize covers bright data (the wide log10 path and the
+automatic wide fused configuration) at full size.
+
 test_fused_multi_job_configs covers ADVICE r1: several jobs on one handle
 (tmh_stats_reset between), high values in different 1,024-bin rounds per
 job, every fused configuration, and the corrector on a different stream from
@@ -161,11 +164,93 @@ def test_headline_pipeline_fullsize(L):
           % (N, 100.0 * pm1 / tot))
 
 
-def _job_sites(k, n, H, W):
+@pytest.mark.timeout(600)
+def test_bright_fullsize(L):
+    """bright 16-bit data (lognormal(8.5, 0.6), about a third
+    of the pixels >= 4,096) at full size.  The Welford pass takes its wide
+    log10 path for most pixel groups and counts them; the automatic fused
+    configuration then runs the one-site, 32,768-bin slice (kFusedWide).  The
+    same job with the narrow slices forced (global adds for every pixel
+    >= 4,096) must give identical results, and both match the oracle."""
+    import torch
+
+    from tmlibrary_amd import hip
+    from tmlibrary_amd.image import ZERO_LOG10
+    from tmlibrary_amd.synth import BRIGHT, synth_exact_host
+    H, W, N = 2160, 2560, 64
+    seed, channel, first = 4242, 2, 0
+    npx = H * W
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    sp = C.c_void_p(stream.cuda_stream)
+    d_in, d_out = Dev(L, N * npx * 2), Dev(L, N * npx * 2)
+    planes = [Dev(L, npx * 8) for _ in range(5)]
+    mean, std, smean, sstd, tmp = planes
+    hip.check(L.tmh_synth_sites_device(d_in.p, N, H, W, seed, channel, first, hip.TMH_SYNTH_BRIGHT, sp))
+    h = _stats_handle(L, H, W, hip.TMH_STATS_KEEP_SITE_HIST)
+    hip.check(L.tmh_stats_set_stream(h, sp))
+    c = C.c_void_p()
+    L.tmh_synchronize(None)
+    hip.check(L.tmh_corrector_create_device(mean.p, std.p, H, W, 1, ZERO_LOG10, sp, C.byref(c)))
+    wide = []
+
+    def job():
+        hip.check(L.tmh_stats_reset(h))
+        hip.check(L.tmh_stats_update_welford_device(h, d_in.p, N, 1, sp))
+        wg = C.c_uint64()
+        hip.check(L.tmh_stats_wide_groups(h, C.byref(wg), None))
+        wide.append(wg.value)
+        hip.check(L.tmh_stats_finalize_device(h, mean.p, std.p, sp))
+        hip.check(L.tmh_smooth_f64_device(mean.p, smean.p, tmp.p, H, W, 5.0, sp))
+        hip.check(L.tmh_smooth_f64_device(std.p, sstd.p, tmp.p, H, W, 5.0, sp))
+        hip.check(L.tmh_corrector_update_device(c, smean.p, sstd.p, sp))
+        hip.check(L.tmh_correct_u16_hist_device(c, h, d_in.p, d_out.p, N, -1, -1, sp))
+        return _results(L, h, H, W, N)
+
+    r = job()  # automatic: wide
+    out_auto = d_out.get(np.uint16, (N, npx))
+    hist0 = np.empty(65536, np.uint32)
+    hip.check(L.tmh_stats_site_histogram(h, 0, hip.ptr(hist0)))
+    hip.check(L.tmh_stats_set_option(h, hip.TMH_OPT_FUSED_CONFIG, 3))  # narrow, forced
+    rn = job()
+    assert np.array_equal(d_out.get(np.uint16, (N, npx)), out_auto)
+    assert np.array_equal(rn["acc"], r["acc"]) and np.array_equal(rn["hist"], r["hist"])
+    assert np.array_equal(rn["mean"], r["mean"]) and np.array_equal(rn["std"], r["std"])
+    sites = d_in.get(np.uint16, (N, H, W))
+    gm, gs = smean.get(np.float64, (H, W)), sstd.get(np.float64, (H, W))
+    L.tmh_corrector_destroy(c)
+    L.tmh_stats_destroy(h)
+    for b in planes + [d_in, d_out]:
+        b.free()
+
+    for i in (0, N - 1):
+        assert np.array_equal(sites[i], synth_exact_host(H, W, seed, channel, first + i, BRIGHT))
+    assert wide[0] == wide[1] == _wide_groups(sites)
+    assert wide[0] >= 0.02 * N * npx // 8, wide[0] / (N * npx // 8)
+    ref = orc.OracleOnlineStatistics((H, W))
+    pooled = np.zeros(65536, np.uint64)
+    for s in sites:
+        ref.update(s)
+        pooled += orc.histogram_u16(s)
+    assert np.array_equal(hist0.astype(np.uint64), orc.histogram_u16(sites[0]))
+    assert_close_rel(r["mean"], ref.mean)
+    assert_close_rel(r["std"], ref.std)
+    assert np.array_equal(r["hist"], pooled)
+    assert np.array_equal(r["acc"], ref.percentile_sums)
+    sm_ref, ss_ref = orc.smooth_reflect(ref.mean, 5), orc.smooth_reflect(ref.std, 5)
+    assert_close_rel(gm, sm_ref)
+    assert_close_rel(gs, ss_ref)
+    for i in (0, N // 2, N - 1):
+        want = orc.correct_illumination(sites[i], sm_ref, ss_ref)
+        worst, flips, _ = dn_report(out_auto.reshape(N, H, W)[i], want)
+        assert worst <= 1 and flips == 0, (i, worst, flips)
+
+
+def _job_sites(k, n, H, W, dist=0):
     """Job k's sites: synthetic plus high values in job-specific 1,024-bin
     rounds (beyond every configuration's LDS slice) and saturated pixels."""
     from tmlibrary_amd.synth import synth_exact_host
-    sites = np.stack([synth_exact_host(H, W, 77 + k, 0, i) for i in range(n)])
+    sites = np.stack([synth_exact_host(H, W, 77 + k, 0, i, dist) for i in range(n)])
     hi_vals = [(40000, 65535), (20000, 5000), (60000, 12345)][k % 3]
     sites[0, :3, :40] = hi_vals[0]
     sites[n // 2, 5, :17] = hi_vals[1]
@@ -173,11 +258,20 @@ def _job_sites(k, n, H, W):
     return sites
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def _wide_groups(sites):
+    """8-pixel groups (row-major, per site) holding a value >= 4,096."""
+    g = sites.reshape(sites.shape[0], -1, 8)
+    return int(np.count_nonzero((g >= 4096).any(axis=2)))
+
+
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4])
 def test_fused_multi_job_configs(L, cfg):
+    """cfg -1 is the automatic choice: job 1 is bright (lognormal(8.5, 0.6)),
+    so the Welford count must select the wide configuration for it, and the
+    synthetic jobs around it the narrow one."""
     import torch
 
-    from tmlibrary_amd import hip
+    from tmlibrary_amd import hip, synth
     from tmlibrary_amd.image import ZERO_LOG10
     H, W, n = 240, 320, 9
     npx = H * W
@@ -195,7 +289,8 @@ def test_fused_multi_job_configs(L, cfg):
     hip.check(L.tmh_corrector_create_device(mean.p, std.p, H, W, 1, ZERO_LOG10, sp2, C.byref(c)))
     L.tmh_synchronize(None)
     for k in range(3):
-        sites = _job_sites(k, n, H, W)
+        bright = cfg == -1 and k == 1
+        sites = _job_sites(k, n, H, W, synth.BRIGHT if bright else synth.STANDARD)
         d_in.put(sites)
         # one job, no host synchronisation: statistics on stream 1, the
         # fused pass on stream 2 (tmh_correct_u16_hist_device orders itself
@@ -206,8 +301,17 @@ def test_fused_multi_job_configs(L, cfg):
         hip.check(L.tmh_smooth_f64_device(mean.p, smean.p, tmp.p, H, W, 5.0, sp1))
         hip.check(L.tmh_smooth_f64_device(std.p, sstd.p, tmp.p, H, W, 5.0, sp1))
         hip.check(L.tmh_corrector_update_device(c, smean.p, sstd.p, sp1))
+        wg, ws = C.c_uint64(), C.c_int64()
+        hip.check(L.tmh_stats_wide_groups(h, C.byref(wg), C.byref(ws)))
+        groups = n * npx // 8
+        assert ws.value == n
+        assert wg.value == _wide_groups(sites), (cfg, k)
+        if cfg == -1:  # the automatic choice's threshold: 2 % of the groups
+            assert (wg.value >= 0.02 * groups) == bright, (k, wg.value / groups)
         hip.check(L.tmh_correct_u16_hist_device(c, h, d_in.p, d_out.p, n, -1, -1, None))
         r = _results(L, h, H, W, n)  # on stream 1: waits for stream 2's fused pass
+        hip.check(L.tmh_stats_wide_groups(h, C.byref(wg), C.byref(ws)))
+        assert wg.value == 0 and ws.value == 0  # consumed by the fused pass
         ref = orc.run_illumstats(list(sites))
         assert r["n"] == n
         assert_close_rel(r["mean"], ref.mean)

@@ -234,7 +234,7 @@ struct tmh_stats {
   hipStream_t side = nullptr;   // histogram pass runs here, concurrent with Welford
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;  // ordering against a caller's stream
-  int fused_cfg = kFusedDefault;  // TMH_OPT_FUSED_CONFIG
+  int fused_cfg = kFusedAuto;     // TMH_OPT_FUSED_CONFIG (-1: per launch, on the device)
   int wf_parts = 0;               // TMH_OPT_WELFORD_PARTS (0: automatic)
   int tail_chunks = 1;            // TMH_OPT_TAIL_CHUNKS (1: no overlap)
   bool hist_dirty = false;        // a fused launch may have left counts / round masks behind
@@ -242,6 +242,8 @@ struct tmh_stats {
   int64_t n_deferred = 0;     // sites whose order statistics are stored
   int64_t last_batch = 0;
   int64_t pending = 0;        // Welford-updated sites whose histograms are still to come
+  DBuf<unsigned long long> wide;  // pixel groups with a value >= 4,096 in the pending sites
+  int64_t wide_sites = 0;         // sites that count covers
   bool pct_sum_external = false;
   DBuf<double> mean, m2, lut_log, gamma, acc, tmp_mean, tmp_std, rn;
   DBuf<double> wf_part;  // partial (mean, M2) planes of site-split Welford launches
@@ -391,6 +393,7 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
       h->mean.alloc(npx, true);
       h->m2.alloc(npx, true);
       h->wf_part.alloc((size_t)8 * npx);
+      h->wide.alloc(1, true);
       h->acc.alloc(n_quantiles, true);
       h->pooled.alloc(kBins, true);
       h->lut_log.alloc(kBins);
@@ -454,7 +457,8 @@ int tmh_stats_set_option(tmh_stats* h, int option, int value) {
     TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
     switch (option) {
       case TMH_OPT_FUSED_CONFIG:
-        TMH_CHECK(value >= 0 && value < kFusedConfigs, TMH_EINVAL, "fused configuration out of range");
+        TMH_CHECK(value >= kFusedAuto && value < kFusedConfigs, TMH_EINVAL,
+                  "fused configuration out of range");
         h->fused_cfg = value;
         break;
       case TMH_OPT_WELFORD_PARTS:
@@ -487,6 +491,8 @@ int tmh_stats_reset(tmh_stats* h) {
     TMH_HIP(hipMemsetAsync(h->m2.p, 0, h->npx * 8, h->stream));
     TMH_HIP(hipMemsetAsync(h->acc.p, 0, (size_t)h->Q * 8, h->stream));
     TMH_HIP(hipMemsetAsync(h->pooled.p, 0, (size_t)kBins * 8, h->stream));
+    TMH_HIP(hipMemsetAsync(h->wide.p, 0, 8, h->stream));
+    h->wide_sites = 0;
     h->n = 0;
     h->n_deferred = 0;
     h->last_batch = 0;
@@ -514,7 +520,7 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
     TMH_HIP(hipStreamWaitEvent(hs, h->ev_fork, 0));
   }
   launch_welford(d, h->npx, ns, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
-                 log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, s);
+                 log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, nullptr, s);
   // order statistics, in chunks so the per-site slabs stay bounded
   for (int64_t c0 = 0; c0 < ns; c0 += chunk) {
     const int64_t nc = std::min(chunk, ns - c0);
@@ -547,7 +553,8 @@ int tmh_stats_update_welford_device(tmh_stats* h, const uint16_t* dev_sites, int
       h->rn.alloc((size_t)n_sites);
     }
     launch_welford(dev_sites, h->npx, n_sites, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
-                   log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, s);
+                   log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, h->wide.p, s);
+    if ((h->npx & 7) == 0) h->wide_sites += n_sites;
     h->n += n_sites;
     h->pending += n_sites;
   });
@@ -664,6 +671,17 @@ int tmh_stats_variance(tmh_stats* h, double* host_var) {
     launch_variance(h->m2.p, h->n, h->npx, h->tmp_std.p, h->stream);
     TMH_HIP(hipMemcpyAsync(host_var, h->tmp_std.p, h->npx * 8, hipMemcpyDeviceToHost, h->stream));
     TMH_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int tmh_stats_wide_groups(tmh_stats* h, uint64_t* groups_out, int64_t* sites_out) {
+  return guard([&] {
+    TMH_CHECK(h && groups_out, TMH_EINVAL, "bad arguments");
+    unsigned long long w = 0;
+    TMH_HIP(hipMemcpyAsync(&w, h->wide.p, 8, hipMemcpyDeviceToHost, h->stream));
+    TMH_HIP(hipStreamSynchronize(h->stream));
+    *groups_out = w;
+    if (sites_out) *sites_out = h->wide_sites;
   });
 }
 
@@ -1127,8 +1145,11 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       // finalize runs on the whole GPU after both.  Chunks keep site order,
       // so the ordered percentile sum at the end is unchanged.
       const int nch = (int)std::min<int64_t>(h->tail_chunks, n_sites / 64 > 0 ? n_sites / 64 : 1);
-      const int dense = correct_hist_dense_rounds(h->fused_cfg);
       uint32_t* sh = (h->flags & 2u) ? h->site_hist.p : nullptr;
+      // the wide configuration pays off once a few % of the pixel groups
+      // overflow the narrow slices (their values then take global atomics)
+      const unsigned long long wide_thresh = (unsigned long long)std::max<double>(
+          1.0, kWideFrac * (double)h->wide_sites * (double)(h->npx >> 3));
       if (nch > 1) {
         TMH_HIP(hipEventRecord(h->ev_fork, s));
         TMH_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
@@ -1139,7 +1160,7 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         launch_correct_hist(dev_in + c0 * h->npx, dev_out + c0 * h->npx, c->npx, nc, c->coef2.p,
                             c->mconst2.p, fl, c->log_transform, clip_lo, clip_hi,
                             h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0,
-                            c->queues.p, c->n_wg, h->fused_cfg, s);
+                            c->queues.p, c->n_wg, h->fused_cfg, h->wide.p, wide_thresh, s);
         launch_fix_correct(dev_in + c0 * h->npx, dev_out + c0 * h->npx, 2, c->npx, nc, fl,
                            c->coef64.p, c->rc.p, c->log_transform, clip_lo, clip_hi, s);
         const bool side = k < nch - 1;
@@ -1150,7 +1171,7 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
           TMH_HIP(hipEventRecord(h->ev_join, h->side));
           TMH_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
         }
-        launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0, dense, nc,
+        launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0, 0, nc,
                              h->qp, vlh + (size_t)c0 * kOsTile, ld, h->pooled.p, h->pooled_parts.p,
                              kPooledParts, h->zeros.p + c0, sh ? sh + (size_t)c0 * kBins : nullptr,
                              side ? h->side : s, side);
@@ -1161,6 +1182,10 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       if (h->flags & TMH_STATS_DEFERRED_PCT) h->n_deferred += n_sites;
       h->last_batch = n_sites;
       h->pending -= n_sites;
+      if (h->pending == 0) {  // the wide count restarts with the next Welford batch
+        TMH_HIP(hipMemsetAsync(h->wide.p, 0, 8, s));
+        h->wide_sites = 0;
+      }
       if (cross) {
         TMH_HIP(hipEventRecord(h->ev_out, s));
         TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
@@ -1209,6 +1234,10 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         launch_pct_accumulate(vlh, nc, ld, h->Q, h->gamma.p, h->acc.p, s);
       h->last_batch = nc;
       h->pending -= nc;
+    }
+    if (h->pending == 0 && h->wide_sites) {
+      TMH_HIP(hipMemsetAsync(h->wide.p, 0, 8, s));
+      h->wide_sites = 0;
     }
     if (cross) {
       TMH_HIP(hipEventRecord(h->ev_out, s));

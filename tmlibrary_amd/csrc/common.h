@@ -152,7 +152,8 @@ __device__ __forceinline__ int32_t correct_ref_f64(uint32_t x, double mean, doub
 // forced_parts: 0 = pick the site split automatically, 1..4 = that many parts
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
-                    double* part, size_t part_cap, int forced_parts, hipStream_t s);
+                    double* part, size_t part_cap, int forced_parts,
+                    unsigned long long* wide, hipStream_t s, int shape = -1);
 // vlh: the order statistics of the launch's first site (buffer + site *
 // kOsTile) in a buffer with room for vlh_ld sites (kOsTile layout above)
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
@@ -207,14 +208,24 @@ void launch_correct_u8(const uint8_t* in, uint8_t* out, int64_t npx, int64_t n_s
                        const float4* coef, const float2* lut, const float4* mconst,
                        const FixList& fl, int log_transform, int clip_lo, int clip_hi,
                        hipStream_t s);
-// fused pass configurations (fused_kernels.hip kFusedCfgs); default kFusedDefault
-constexpr int kFusedConfigs = 4;
-constexpr int kFusedDefault = 3;
+// fused pass configurations (fused_kernels.hip kFusedCfgs).  kFusedAuto picks
+// per launch, on the device: kFusedNarrow (four sites per unit, 4,096-bin
+// slices) unless the Welford pass counted at least kWideFrac of the pixel
+// groups with a value >= 4,096, then kFusedWide (two sites, 16,384 bins each;
+// on bright sites 18.6 ms against 22.4 ms for one site x 32,768 bins, whose
+// single site per unit keeps too few loads in flight, and 231 ms narrow:
+// profiles/r2/mb_fused_bright_r2f.txt).
+constexpr int kFusedConfigs = 5;
+constexpr int kFusedAuto = -1;
+constexpr int kFusedNarrow = 3;
+constexpr int kFusedWide = 0;
+constexpr double kWideFrac = 0.02;
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, const FixList& fl,
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
-                         unsigned long long* rmask, int* queues, int n_wg, int cfg, hipStream_t s);
-int correct_hist_dense_rounds(int cfg);
+                         unsigned long long* rmask, int* queues, int n_wg, int cfg,
+                         const unsigned long long* wide, unsigned long long wide_thresh,
+                         hipStream_t s);
 // illuminati chain (chain_kernels.hip)
 void launch_align(const void* in, void* out, int elem_bytes, int64_t n_sites, int H, int W, int oh,
                   int ow, const tmh_window* d_win, hipStream_t s);

@@ -152,15 +152,28 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
     const float4* __restrict__ coef, const float4* __restrict__ mconst2, FixList fl,
     int clip_lo, int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
-    int* __restrict__ queues, int bands_per_xcd) {
+    int* __restrict__ queues, int bands_per_xcd, const unsigned long long* __restrict__ wide,
+    unsigned long long wide_lo, unsigned long long wide_hi) {
+  // launch-time selection (launch_correct_hist): this configuration runs only
+  // when the Welford pass's count of wide pixel groups is in [wide_lo, wide_hi)
+  if (wide) {
+    const unsigned long long w = __builtin_nontemporal_load(wide);
+    if (w < wide_lo || w >= wide_hi) return;
+  }
   constexpr int BINS = LB / SPU;
   constexpr int SLICE = BINS + 1;
   constexpr uint32_t HIMASK = (0xFFFFu & ~(uint32_t)(BINS - 1)) * 0x00010001u;
   static_assert((BINS & (BINS - 1)) == 0, "slice size must be a power of two");
   __shared__ __attribute__((aligned(16))) uint32_t bins[SPU * SLICE];
   __shared__ int unit_sh;
+  // per site of the unit: the 1,024-bin rounds holding counts (the rare
+  // global adds and, at the flush, the slice's non-empty rounds); two sets,
+  // alternating by unit, so one is published while the next unit fills the
+  // other.  k_hist_finalize reads exactly these rounds.
+  __shared__ unsigned long long rm_sh[2][SPU];
   const int tid = threadIdx.x;
   for (int i = tid; i < SPU * SLICE; i += NT) bins[i] = 0u;
+  if (tid < 2 * SPU) rm_sh[tid / SPU][tid % SPU] = 0ull;
 
   const float4 m = mconst2[0];
   const uint32_t clo2 = (uint32_t)clip_lo * 0x00010001u, chi2 = (uint32_t)clip_hi * 0x00010001u;
@@ -232,8 +245,9 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
 #pragma unroll
   for (int k = 0; k < SPU; ++k) v[k] = make_uint4(0, 0, 0, 0);
   bool pre = false;  // v/c already hold this unit's first group (loaded by the previous unit)
-  int cur = grab();
+  int cur = grab(), par = 0;
   while (cur >= 0) {
+    unsigned long long* rm = rm_sh[par];
     const int nxt = grab();
     const Unit un = decode(cur);
     Unit nu = un;
@@ -265,7 +279,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
               rounds |= 1ull << (hi >> 10);
             }
           }
-          atomicOr(&rmask[un.s0 + k], rounds);
+          atomicOr(&rm[k], rounds);  // LDS: published once per unit
         }
       }
       uint32_t o[4];
@@ -312,27 +326,38 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     for (int k = 0; k < SPU; ++k) {
       if (k >= un.ns) break;
       uint32_t* h = hs + k * (int64_t)kBins;
+      unsigned long long lm = 0ull;  // this thread's non-empty rounds
 #pragma unroll 4
       for (int b = tid; b < BINS; b += NT) {
         const uint32_t cnt = bins[k * SLICE + b];
         if (cnt) {
           atomicAdd(&h[b], cnt);
           bins[k * SLICE + b] = 0u;
+          lm |= 1ull << (b >> 10);
         }
       }
+      if (lm) atomicOr(&rm[k], lm);
     }
     __syncthreads();
+    // publish the unit's round masks; the next unit fills the other set, and
+    // this one is not touched again before the next unit's first barrier
+    if (tid < un.ns) {
+      const unsigned long long r = rm[tid];
+      if (r) atomicOr(&rmask[un.s0 + tid], r);
+      rm[tid] = 0ull;
+    }
+    par ^= 1;
   }
 }
 
-// (sites per unit, threads, LDS bins) of the fused pass: ONE table drives both
-// the launch and the rounds k_hist_finalize treats as dense, so the two cannot
-// drift apart.  Selected per handle (tmh_stats_set_option, TMH_OPT_FUSED_CONFIG).
+// (sites per unit, threads, LDS bins) of the fused pass, selected per handle
+// (tmh_stats_set_option, TMH_OPT_FUSED_CONFIG) or automatically per launch
+// (kFusedAuto: kFusedNarrow, or kFusedWide when the sites are bright).
 struct FusedCfg {
   int spu, threads, lds_bins;
 };
 constexpr FusedCfg kFusedCfgs[kFusedConfigs] = {
-    {2, 1024, 32768}, {4, 1024, 32768}, {2, 512, 16384}, {4, 512, 16384}};
+    {2, 1024, 32768}, {4, 1024, 32768}, {2, 512, 16384}, {4, 512, 16384}, {1, 1024, 32768}};
 template <int K>
 struct FusedCfgCheck {
   static_assert((kFusedCfgs[K].lds_bins / kFusedCfgs[K].spu) % 1024 == 0,
@@ -340,21 +365,15 @@ struct FusedCfgCheck {
   static constexpr bool ok = true;
 };
 static_assert(FusedCfgCheck<0>::ok && FusedCfgCheck<1>::ok && FusedCfgCheck<2>::ok &&
-              FusedCfgCheck<3>::ok, "");
+              FusedCfgCheck<3>::ok && FusedCfgCheck<4>::ok, "");
 
-int correct_hist_dense_rounds(int cfg) {
-  const FusedCfg& c = kFusedCfgs[cfg];
-  return c.lds_bins / c.spu / 1024;
-}
-
-void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
-                         const float2* coef2, const float4* mconst2, const FixList& fl,
-                         int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
-                         unsigned long long* rmask, int* queues, int n_wg, int cfg, hipStream_t s) {
-  if (n_sites <= 0) return;
-  ProfScope prof("correct_hist", s);
+static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
+                                    const float4* cf4, const float4* mconst2, const FixList& fl,
+                                    int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
+                                    unsigned long long* rmask, int* queues, int n_wg, int cfg,
+                                    const unsigned long long* wide, unsigned long long wide_lo,
+                                    unsigned long long wide_hi, hipStream_t s) {
   TMH_HIP(hipMemsetAsync(queues, 0, 8 * sizeof(int), s));
-  const float4* cf4 = reinterpret_cast<const float4*>(coef2);
 #define TMH_LAUNCH_CH(L_, K_)                                                                    \
   {                                                                                              \
     constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
@@ -362,18 +381,21 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
     if (clip_lo >= 0)                                                                            \
       hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, 0, c.threads, c.lds_bins>), grid,     \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, queues, kBandsPerXcd);                   \
+                         clip_lo, clip_hi, hist, rmask, queues, kBandsPerXcd, wide, wide_lo,       \
+                         wide_hi);                                                               \
     else                                                                                         \
       hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, 0, c.threads, c.lds_bins>), grid,    \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, queues, kBandsPerXcd);                   \
+                         clip_lo, clip_hi, hist, rmask, queues, kBandsPerXcd, wide, wide_lo,       \
+                         wide_hi);                                                               \
   }
-#define TMH_LAUNCH_CFG(L_)            \
-  switch (cfg) {                      \
+#define TMH_LAUNCH_CFG(L_)              \
+  switch (cfg) {                        \
     case 0: TMH_LAUNCH_CH(L_, 0) break; \
     case 1: TMH_LAUNCH_CH(L_, 1) break; \
     case 2: TMH_LAUNCH_CH(L_, 2) break; \
-    default: TMH_LAUNCH_CH(L_, 3) break; \
+    case 3: TMH_LAUNCH_CH(L_, 3) break; \
+    default: TMH_LAUNCH_CH(L_, 4) break; \
   }
   if (log_transform) {
     TMH_LAUNCH_CFG(true);
@@ -383,6 +405,33 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
 #undef TMH_LAUNCH_CFG
 #undef TMH_LAUNCH_CH
   TMH_HIP(hipGetLastError());
+}
+
+// cfg >= 0: that configuration.  cfg == kFusedAuto: both kFusedNarrow and
+// kFusedWide are queued and each reads the Welford pass's wide-group count
+// (*wide) on the device, so exactly one of them runs -- the choice costs no
+// host round trip, and the idle launch ends in microseconds.  wide_thresh =
+// groups at which the wide configuration is preferred.  Either way the round
+// masks name every non-empty round, so the histogram finalize is the same.
+void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
+                         const float2* coef2, const float4* mconst2, const FixList& fl,
+                         int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
+                         unsigned long long* rmask, int* queues, int n_wg, int cfg,
+                         const unsigned long long* wide, unsigned long long wide_thresh,
+                         hipStream_t s) {
+  if (n_sites <= 0) return;
+  ProfScope prof("correct_hist", s);
+  const float4* cf4 = reinterpret_cast<const float4*>(coef2);
+  if (cfg >= 0 || !wide) {
+    launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo,
+                            clip_hi, hist, rmask, queues, n_wg, cfg >= 0 ? cfg : kFusedNarrow,
+                            nullptr, 0, 0, s);
+    return;
+  }
+  launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
+                          hist, rmask, queues, n_wg, kFusedNarrow, wide, 0, wide_thresh, s);
+  launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
+                          hist, rmask, queues, n_wg, kFusedWide, wide, wide_thresh, ~0ull, s);
 }
 
 }  // namespace tmh

@@ -30,33 +30,55 @@ namespace tmh {
 // ---------------------------------------------------------------------------
 
 // x = stats transform of one pixel value.  LOG: np.log10 with 0 -> 0 from the
-// host-numpy LUT for values < kWfLut - 1 (LDS, bit-identical to numpy); the
-// rare larger values use the same LUT on their top bits,
-//   log10(u) = log10(a) + k log10(2) + log1p(t) / ln 10,  a = u >> k,
-//   t = (u - (a << k)) / (a << k) < 1/2015,
-// with a 3-term series (truncation < 7e-15 absolute): no transcendental and
-// few registers, so the rare branch does not cost the streaming loop waves.
-__device__ __forceinline__ double log10_slow(uint32_t u, const double* slut) {
-  const int k = u < 64496u ? 4 : 5;  // a <= 4030 < 4096 (LDS LUT)
-  const uint32_t a = u >> k;
-  const double den = (double)(a << k);
-  const double t = (double)(u - (a << k)) / den;
-  constexpr double kInvLn10 = 0.43429448190325182765;
-  constexpr double kLog10_2 = 0.30102999566398119521;
-  const double series = t * (kInvLn10 + t * (-0.5 * kInvLn10 + t * (kInvLn10 / 3.0)));
-  return slut[a] + (double)k * kLog10_2 + series;
+// host-numpy LUT for values < kWfLut (LDS, bit-identical to numpy).  Larger
+// values (bright sites) use the same LUT on their top bits:
+//   u = 16 a + r,  a = u >> 4 in [256, 4096),
+//   log10(u) = log10(a) + log10(16) + log1p(t) / ln 10,  t = r * sinv[a] < 1/256,
+// where sinv[a] = 1/(16 a) is a second LDS table (f64, correctly rounded: t
+// carries <= 2 ulp) and the 5-term series truncates below 3e-16 absolute.  No
+// division and no per-pixel branch, so a bright group costs ~9 f64 ops per
+// pixel instead of the LUT path's 3 (the f64 division this replaces was ~17).
+constexpr double kInvLn10 = 0.43429448190325182765;
+constexpr double kLog10_16 = 1.2041199826559247809;
+// 1/(16 a): INV = 1 from the LDS table, INV = 0 by v_rcp_f32 plus one f64
+// Newton step (relative error ~1e-14: t then carries < 1e-17 absolute)
+template <int INV>
+__device__ __forceinline__ double recip16(uint32_t a, const double* sinv) {
+  if (INV) return sinv[a];
+  const double d = (double)(a << 4);
+  const double r0 = (double)__builtin_amdgcn_rcpf((float)(a << 4));
+  return fma(r0, fma(-d, r0, 1.0), r0);
+}
+template <int INV>
+__device__ __forceinline__ double log10_big(uint32_t u, const double* slut, const double* sinv) {
+  const uint32_t a = u >> 4;
+  const double t = (double)(u & 15u) * recip16<INV>(a, sinv);
+  const double series =
+      t * (kInvLn10 +
+           t * (-0.5 * kInvLn10 + t * (kInvLn10 / 3.0 + t * (-0.25 * kInvLn10 + t * (0.2 * kInvLn10)))));
+  return (slut[a] + kLog10_16) + series;
 }
 
-// LUT entries staged in LDS: the 4,096 values below 2^12 (32 KB), so a site's
-// 8 pixels need the rare path exactly when one of their 16-bit words has a
-// bit >= 12 set (one OR/AND over the four packed words)
+// LUT entries staged in LDS: the 4,096 values below 2^12 (32 KB) and, with
+// INV = 1, the 4,096 reciprocals 1/(16 a) (32 KB more), so a site's 8 pixels
+// need the rare path exactly when one of their 16-bit words has a bit >= 12
+// set (one OR/AND over the four packed words).
 constexpr int kWfLut = 4096;
+
+template <int INV>
+__device__ __forceinline__ void fill_wf_tables(const double* __restrict__ lut, double* slut,
+                                               double* sinv, int nt) {
+  for (int i = threadIdx.x; i < kWfLut; i += nt) {
+    slut[i] = lut[i];
+    if (INV) sinv[i] = i ? 1.0 / (16.0 * (double)i) : 0.0;
+  }
+}
 
 template <bool LOG>
 __device__ __forceinline__ double xform(uint32_t u, const double* slut) {
   if (!LOG) return (double)u;
   double x = slut[u & (uint32_t)(kWfLut - 1)];
-  if (u >= (uint32_t)kWfLut) x = log10_slow(u, slut);
+  if (u >= (uint32_t)kWfLut) x = log10_big<0>(u, slut, nullptr);
   return x;
 }
 
@@ -66,7 +88,12 @@ __device__ __forceinline__ void welford1(double x, double rn, double& mu, double
   m2 = fma(d, x - mu, m2);      // M2 + delta * (x - mean_new)
 }
 
+// Production shape of the vec8 pass: threads per workgroup and the
+// reciprocal source (tools/mb/mb_welford.hip compares the four shapes on
+// standard and bright sites; profiles/r2/mb_welford_shapes_*.txt).
 constexpr int kWfThreads = 256;
+constexpr int kWfInv = 0;
+constexpr int kWfScalarThreads = 256;
 constexpr int kWfGroup = 2;  // sites per pipeline stage (two stages in flight)
 constexpr int kWfMaxParts = 4;
 
@@ -78,24 +105,30 @@ __global__ void k_rn_table(double* __restrict__ rn, int64_t n0, int64_t n) {
 
 // Stats transform of eight pixels: LDS LUT gather of each value's low 12
 // bits (no clamp: the index stays in the table), then -- only when a word has
-// a value >= 4,096 -- those slots patched one at a time, so a single inlined
-// log10 serves all eight.  The inner loop is VALU-issue bound (3 f64 ops per
-// pixel at half rate), so the integer work per pixel is kept to the gather
-// address.
-template <bool LOG>
-__device__ __forceinline__ void xform8(const uint4 v, const double* slut, double (&x)[8]) {
+// a value >= 4,096 -- all eight recomputed branch-free with log10_big and the
+// large ones selected (wc counts such groups: the fused pass picks its LDS
+// slice width from it).  The inner loop is VALU-issue bound (3 f64 ops per
+// pixel), so the integer work per pixel is kept to the gather address.
+template <bool LOG, int INV>
+__device__ __forceinline__ void xform8(const uint4 v, const double* slut, const double* sinv,
+                                       double (&x)[8], uint32_t& wc) {
   const uint32_t u[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
                          v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
+  const bool wide = ((v.x | v.y | v.z | v.w) & 0xF000F000u) != 0;
   if (LOG) {
     constexpr uint32_t kIdx = kWfLut - 1;
 #pragma unroll
     for (int k = 0; k < 8; ++k) x[k] = slut[u[k] & kIdx];
-    if ((v.x | v.y | v.z | v.w) & 0xF000F000u) {
+    if (wide) {
+      ++wc;
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (u[k] > kIdx) x[k] = log10_slow(u[k], slut);
+      for (int k = 0; k < 8; ++k) {
+        const double xb = log10_big<INV>(u[k], slut, sinv);
+        x[k] = u[k] > kIdx ? xb : x[k];
+      }
     }
   } else {
+    wc += wide ? 1u : 0u;
 #pragma unroll
     for (int k = 0; k < 8; ++k) x[k] = (double)u[k];
   }
@@ -129,17 +162,19 @@ __device__ __forceinline__ uint4 ld_site(const uint4* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-template <bool LOG, bool NTL = true>
-__global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
+template <bool LOG, bool NTL, int NT, int INV>
+__global__ __launch_bounds__(NT) void k_welford_vec8(
     const uint16_t* __restrict__ sites, int64_t npx, int64_t n_total, int64_t per,
     const WfMerge mg, double* __restrict__ mean, double* __restrict__ m2,
-    const double* __restrict__ lut, double* __restrict__ part) {
-  __shared__ double slut[kWfLut];
-  if (LOG)
-    for (int i = threadIdx.x; i < kWfLut; i += kWfThreads) slut[i] = lut[i];
+    const double* __restrict__ lut, double* __restrict__ part,
+    unsigned long long* __restrict__ wide) {
+  __shared__ double slut[kWfLut], sinv[INV ? kWfLut : 1];
+  __shared__ uint32_t wide_sh;
+  if (LOG) fill_wf_tables<INV>(lut, slut, sinv, NT);
+  if (threadIdx.x == 0) wide_sh = 0u;
   __syncthreads();
   const int64_t ngroups = npx >> 3;
-  const int64_t g = (int64_t)blockIdx.x * kWfThreads + threadIdx.x;
+  const int64_t g = (int64_t)blockIdx.x * NT + threadIdx.x;
   if (g >= ngroups) return;
 
   const int64_t s_begin = (int64_t)blockIdx.y * per;
@@ -152,7 +187,9 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
 #pragma unroll
   for (int k = 0; k < kWfGroup; ++k) cur[k] = ld_site<NTL>(src + (k < last ? k : last) * ngroups);
   double K[8], s1[8], s2[8];
-  xform8<LOG>(cur[0], slut, K);
+  uint32_t wc = 0;  // this thread's wide groups (value >= 4,096) over its sites
+  xform8<LOG, INV>(cur[0], slut, sinv, K, wc);
+  wc = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.0;
   // 32-bit site counters: the per-site bounds test is then one scalar compare
@@ -169,7 +206,7 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
     for (int k = 0; k < kWfGroup; ++k) {
       if (s + k < ns) {
         double x[8];
-        xform8<LOG>(cur[k], slut, x);
+        xform8<LOG, INV>(cur[k], slut, sinv, x, wc);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const double d = x[j] - K[j];
@@ -180,6 +217,12 @@ __global__ __launch_bounds__(kWfThreads) void k_welford_vec8(
     }
 #pragma unroll
     for (int k = 0; k < kWfGroup; ++k) cur[k] = nxt[k];
+  }
+
+  if (wide) {  // one global add per workgroup (thread 0's group always exists)
+    if (wc) atomicAdd(&wide_sh, wc);
+    __syncthreads();
+    if (threadIdx.x == 0 && wide_sh) atomicAdd(wide, (unsigned long long)wide_sh);
   }
 
   if (gridDim.y > 1) {  // partial (mean_l, M2_l) of this part
@@ -262,15 +305,14 @@ __global__ void k_wf_merge_parts(const double* __restrict__ part, int64_t npx, c
 
 // Any shape (npx % 8 != 0 leaves sites unaligned for 16-B loads): 1 px/thread.
 template <bool LOG>
-__global__ __launch_bounds__(kWfThreads) void k_welford_scalar(
+__global__ __launch_bounds__(kWfScalarThreads) void k_welford_scalar(
     const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites,
     const double* __restrict__ rn, double* __restrict__ mean, double* __restrict__ m2,
     const double* __restrict__ lut) {
   __shared__ double slut[kWfLut];
-  if (LOG)
-    for (int i = threadIdx.x; i < kWfLut; i += kWfThreads) slut[i] = lut[i];
+  if (LOG) fill_wf_tables<0>(lut, slut, nullptr, kWfScalarThreads);
   __syncthreads();
-  const int64_t p = (int64_t)blockIdx.x * kWfThreads + threadIdx.x;
+  const int64_t p = (int64_t)blockIdx.x * kWfScalarThreads + threadIdx.x;
   if (p >= npx) return;
   double mu = mean[p], q = m2[p];
   for (int64_t s = 0; s < n_sites; ++s)
@@ -295,27 +337,43 @@ static int welford_parts(int64_t n_sites, int64_t npx, size_t part_cap, int forc
   return forced && fits(forced) ? forced : 1;
 }
 
+template <int NT, int INV>
+static void launch_welford_vec8(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t per,
+                                int f, const WfMerge& mg, double* mean, double* m2,
+                                const double* lut, int log_transform, double* part,
+                                unsigned long long* wide, hipStream_t s) {
+  const dim3 grid((unsigned)cdiv(npx >> 3, NT), (unsigned)f);
+  // site loads are non-temporal (streamed once; regular loads measured
+  // 6.60-6.75 vs 6.19-6.34 ms at job level, profiles/r1/ab_welford_ntl.txt)
+  if (log_transform)
+    hipLaunchKernelGGL((k_welford_vec8<true, true, NT, INV>), grid, dim3(NT), 0, s, sites, npx,
+                       n_sites, per, mg, mean, m2, lut, part, wide);
+  else
+    hipLaunchKernelGGL((k_welford_vec8<false, true, NT, INV>), grid, dim3(NT), 0, s, sites, npx,
+                       n_sites, per, mg, mean, m2, lut, part, wide);
+}
+
+// shape = -1: production (kWfThreads, kWfInv); 0..3: (256|512 threads) x
+// (Newton | LDS-table reciprocal) for the microbenchmark
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
-                    double* part, size_t part_cap, int forced_parts, hipStream_t s) {
+                    double* part, size_t part_cap, int forced_parts,
+                    unsigned long long* wide, hipStream_t s, int shape) {
   if (n_sites <= 0) return;
   ProfScope prof("welford", s);
   const bool vec = (npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0;
   if (vec) {
-    const int64_t n_wg = cdiv(npx >> 3, kWfThreads);
     const int f = part ? welford_parts(n_sites, npx, part_cap, forced_parts) : 1;
     const int64_t per = cdiv(n_sites, f);
     const double nl = (double)n_sites, n = (double)(n0 + n_sites);
     const WfMerge mg{1.0 / nl, nl / n, (double)n0 * nl / n, n0 == 0};
-    const dim3 grid((unsigned)n_wg, (unsigned)f);
-    // site loads are non-temporal (streamed once; regular loads measured
-    // 6.60-6.75 vs 6.19-6.34 ms at job level, profiles/r1/ab_welford_ntl.txt)
-    if (log_transform)
-      hipLaunchKernelGGL((k_welford_vec8<true, true>), grid, dim3(kWfThreads), 0, s, sites, npx,
-                         n_sites, per, mg, mean, m2, lut, part);
-    else
-      hipLaunchKernelGGL((k_welford_vec8<false, true>), grid, dim3(kWfThreads), 0, s, sites, npx,
-                         n_sites, per, mg, mean, m2, lut, part);
+    if (shape < 0) shape = (kWfThreads == 512 ? 2 : 0) + kWfInv;
+    switch (shape) {
+      case 0: launch_welford_vec8<256, 0>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
+      case 1: launch_welford_vec8<256, 1>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
+      case 2: launch_welford_vec8<512, 0>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
+      default: launch_welford_vec8<512, 1>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
+    }
     if (f > 1) {
       WfParts pc{};
       pc.n = f;
@@ -325,15 +383,15 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
                          npx, pc, (double)n0, mean, m2);
     }
   } else {  // the per-pixel Welford of odd shapes reads 1/n per site
-    const dim3 grid((unsigned)cdiv(npx, kWfThreads));
+    const dim3 grid((unsigned)cdiv(npx, kWfScalarThreads));
     hipLaunchKernelGGL(k_rn_table, dim3((unsigned)cdiv(n_sites, 256)), dim3(256), 0, s, rn, n0,
                        n_sites);
     if (log_transform)
-      hipLaunchKernelGGL(k_welford_scalar<true>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
-                         rn, mean, m2, lut);
+      hipLaunchKernelGGL(k_welford_scalar<true>, grid, dim3(kWfScalarThreads), 0, s, sites, npx,
+                         n_sites, rn, mean, m2, lut);
     else
-      hipLaunchKernelGGL(k_welford_scalar<false>, grid, dim3(kWfThreads), 0, s, sites, npx, n_sites,
-                         rn, mean, m2, lut);
+      hipLaunchKernelGGL(k_welford_scalar<false>, grid, dim3(kWfScalarThreads), 0, s, sites, npx,
+                         n_sites, rn, mean, m2, lut);
   }
   TMH_HIP(hipGetLastError());
 }

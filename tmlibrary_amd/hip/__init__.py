@@ -49,6 +49,7 @@ SIGNATURES = {
     "tmh_stats_reset": (_I, [_P]),
     "tmh_stats_set_option": (_I, [_P, _I, _I]),
     "tmh_stats_variance": (_I, [_P, _P]),
+    "tmh_stats_wide_groups": (_I, [_P, _P, _P]),
     "tmh_stats_get_hist_device": (_I, [_P, _P, _P]),
     "tmh_stats_set_hist_device": (_I, [_P, _P, _P]),
     "tmh_stats_update": (_I, [_P, _P, _I64, _I, _P]),

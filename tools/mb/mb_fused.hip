@@ -4,7 +4,9 @@
 //   fused ABL  the production kernel with ablations: 0 = production,
 //              1 = no histogram, 3 = no histogram + constant coefficients,
 //              8 = no LDS flush
-// Usage: mb_fused [n_sites=3456] [reps=3] [H=2160] [W=2560]
+//   cfg K      the production kernel in fused configuration K (kFusedCfgs)
+// Input: the bench's generator (dist 0 standard, 1 bright, 2 uniform).
+// Usage: mb_fused [n_sites=3456] [reps=3] [H=2160] [W=2560] [dist=0]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -13,6 +15,7 @@
 
 #include "../../tmlibrary_amd/csrc/common.h"
 #include "../../tmlibrary_amd/csrc/fused_kernels.hip"
+#include "../../tmlibrary_amd/csrc/synth_kernels.hip"
 
 #define CK(x)                                                                                  \
   do {                                                                                         \
@@ -85,19 +88,9 @@ int main(int argc, char** argv) {
   uint16_t *in, *out;
   CK(hipMalloc(&in, bytes));
   CK(hipMalloc(&out, bytes));
-  CK(hipMemset(in, 0, bytes));
-  // a synthetic-looking site: values ~ 100..3000 (the LDS slice), a few above
-  {
-    std::vector<uint16_t> site(npx);
-    uint64_t z = 88172645463325252ull;
-    for (int64_t i = 0; i < npx; ++i) {
-      z ^= z << 13; z ^= z >> 7; z ^= z << 17;
-      const uint32_t r = (uint32_t)(z >> 40);
-      site[i] = (uint16_t)(100 + (r % 2900) * ((r >> 12) % 3 == 0 ? 1 : 0) + (r & 255));
-      if ((r & 0xFFFF) == 7) site[i] = 65535;
-    }
-    for (int64_t s = 0; s < S; ++s) CK(hipMemcpy(in + s * npx, site.data(), npx * 2, hipMemcpyHostToDevice));
-  }
+  const int dist = argc > 5 ? atoi(argv[5]) : 0;
+  launch_synth(in, S, H, W, 12345, 0, 0, dist, 0);
+  CK(hipDeviceSynchronize());
   float4 *coef, *mconst2;
   uint32_t* hist;
   unsigned long long *rmask, *fe;
@@ -162,12 +155,24 @@ int main(int argc, char** argv) {
     CK(hipMemsetAsync(queues, 0, 32, 0));
     CK(hipMemsetAsync(fn, 0, 4, 0));
     hipLaunchKernelGGL((k_correct_hist<true, false, 4, ABL, 512, 16384>), fg, fb, 0, 0, in, out,
-                       npx, S, coef, mconst2, fl, -1, -1, hist, rmask, queues, kBandsPerXcd);
+                       npx, S, coef, mconst2, fl, -1, -1, hist, rmask, queues, kBandsPerXcd,
+                       nullptr, 0ull, 0ull);
   };
   time("fused prod (ABL 0)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 0>()); });
   time("fused no hist (ABL 1)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 1>()); });
   time("fused no hist, const coef (ABL 3)", cb, [&] { fused(std::integral_constant<int, 3>()); });
   time("fused no flush (ABL 8)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 8>()); });
   time("fused prod (ABL 0) again", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 0>()); });
+  for (int cfg = 0; cfg < kFusedConfigs; ++cfg) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "fused cfg %d (%d,%d,%d)", cfg, kFusedCfgs[cfg].spu,
+             kFusedCfgs[cfg].threads, kFusedCfgs[cfg].lds_bins);
+    time(nm, cb + 8.0 * npx, [&] {
+      CK(hipMemsetAsync(fn, 0, 4, 0));
+      launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist,
+                          rmask, queues, cus, cfg,
+                          nullptr, 0, 0);
+    });
+  }
   return 0;
 }

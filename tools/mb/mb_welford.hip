@@ -4,7 +4,7 @@
 // thread, the number of site parts (parts run one after another in dispatch
 // order) and the site depth in flight, against a contiguous grid-stride read
 // of the same bytes and the production launch.
-// Usage: mb_welford [n_sites=3456] [reps=3]
+// Usage: mb_welford [n_sites=3456] [reps=3] [dist=0 standard|1 bright|2 uniform]
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -83,9 +83,10 @@ template <int MODE>
 __global__ __launch_bounds__(256) void k_wf_abl(const uint16_t* __restrict__ sites, int64_t npx,
                                                 int64_t n_sites, const double* __restrict__ lut,
                                                 double* __restrict__ out) {
-  __shared__ double slut[kWfLut];
-  for (int i = threadIdx.x; i < kWfLut; i += 256) slut[i] = lut[i];
+  __shared__ double slut[kWfLut], sinv[kWfLut];
+  fill_wf_tables<1>(lut, slut, sinv, 256);
   __syncthreads();
+  uint32_t wc = 0;
   const int64_t ng = npx >> 3;
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= ng) return;
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(256) void k_wf_abl(const uint16_t* __restrict__ sit
   for (int k = 0; k < 4; ++k) cur[k] = ld_site<true>(src + (k < last ? k : last) * ng);
   double K[8], s1[8], s2[8];
   uint32_t isum = 0;
-  xform8<true>(cur[0], slut, K);
+  xform8<true, 1>(cur[0], slut, sinv, K, wc);
 #pragma unroll
   for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.0;
   for (int64_t s = 0; s < n_sites; s += 4) {
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(256) void k_wf_abl(const uint16_t* __restrict__ sit
 #pragma unroll
           for (int j = 0; j < 8; ++j) x[j] = (double)u[j];
         } else {
-          xform8<true>(v, slut, x);
+          xform8<true, 1>(v, slut, sinv, x, wc);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(256) void k_wf_abl(const uint16_t* __restrict__ sit
   double r = (double)isum;
 #pragma unroll
   for (int j = 0; j < 8; ++j) r += s1[j] + s2[j];
-  if (r == 1.2345) out[g] = r;
+  if (r == 1.2345 + wc) out[g] = r;
 }
 
 // full Welford math, variants: G sites per pipeline stage, KF (shift K kept in
@@ -150,9 +151,10 @@ template <int G, bool KF, int WPS>
 __global__ __launch_bounds__(256, WPS) void k_wf_var(const uint16_t* __restrict__ sites, int64_t npx,
                                                      int64_t n_sites, const double* __restrict__ lut,
                                                      double* __restrict__ out) {
-  __shared__ double slut[kWfLut];
-  for (int i = threadIdx.x; i < kWfLut; i += 256) slut[i] = lut[i];
+  __shared__ double slut[kWfLut], sinv[kWfLut];
+  fill_wf_tables<1>(lut, slut, sinv, 256);
   __syncthreads();
+  uint32_t wc = 0;
   const int64_t ng = npx >> 3;
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= ng) return;
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(256, WPS) void k_wf_var(const uint16_t* __restrict_
   for (int k = 0; k < G; ++k) cur[k] = ld_site<true>(src + (k < last ? k : last) * ng);
   double K[8], s1[8], s2[8];
   float Kf[8];
-  xform8<true>(cur[0], slut, K);
+  xform8<true, 1>(cur[0], slut, sinv, K, wc);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     s1[k] = s2[k] = 0.0;
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(256, WPS) void k_wf_var(const uint16_t* __restrict_
     for (int k = 0; k < G; ++k) {
       if (s + k < n_sites) {
         double x[8];
-        xform8<true>(cur[k], slut, x);
+        xform8<true, 1>(cur[k], slut, sinv, x, wc);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const double d = x[j] - (KF ? (double)Kf[j] : K[j]);
@@ -194,7 +196,7 @@ __global__ __launch_bounds__(256, WPS) void k_wf_var(const uint16_t* __restrict_
   double r = 0.0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) r += s1[j] + s2[j];
-  if (r == 1.2345) out[g] = r;
+  if (r == 1.2345 + wc) out[g] = r;
 }
 
 template <int U>
@@ -223,7 +225,8 @@ int main(int argc, char** argv) {
   const int64_t bytes = S * npx * 2;
   uint16_t* in;
   CK(hipMalloc(&in, bytes));
-  launch_synth(in, S, H, W, 12345, 0, 0, TMH_SYNTH_STANDARD, 0);  // the bench's sites
+  const int dist = argc > 3 ? atoi(argv[3]) : 0;
+  launch_synth(in, S, H, W, 12345, 0, 0, dist, 0);  // the bench's sites
   CK(hipDeviceSynchronize());
   uint32_t* sink;
   CK(hipMalloc(&sink, 64));
@@ -306,12 +309,18 @@ int main(int argc, char** argv) {
   var("wf var G2 Kf32 wps6", I2(), B1(), W6());
   var("wf var G4 Kf32 wps5", I4(), B1(), W5());
   var("wf var G1 Kf32 wps6", I1(), B1(), W6());
-  for (int f : {0, 1, 2, 3, 4}) {
-    char nm[64];
-    snprintf(nm, sizeof nm, "welford prod (parts %s%d)", f ? "" : "auto ", f);
-    time(nm, [&] {
-      launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, f, 0);
-    });
-  }
+  static const char* shapes[4] = {"256 thr, Newton rcp", "256 thr, LDS rcp", "512 thr, Newton rcp",
+                                  "512 thr, LDS rcp"};
+  for (int shape = 0; shape < 4; ++shape)
+    for (int f : {1, 3}) {
+      char nm[80];
+      snprintf(nm, sizeof nm, "welford shape %d (%s) parts %d", shape, shapes[shape], f);
+      time(nm, [&] {
+        launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, f, nullptr, 0, shape);
+      });
+    }
+  time("welford production (parts 1)", [&] {
+    launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 1, nullptr, 0);
+  });
   return 0;
 }
