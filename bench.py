@@ -92,6 +92,16 @@ def parse():
                    help="run the histogram pass after Welford instead of concurrently")
     p.add_argument("--no-extras", action="store_true",
                    help="skip the extra (non-headline) measurements: chain pass, host path")
+    p.add_argument("--stream-host", action="store_true",
+                   help="configs[4]: sites streamed from pinned host memory over PCIe (one JSON "
+                        "line of its own; never the HBM headline)")
+    p.add_argument("--stream-sites", type=int, default=24576,
+                   help="--stream-host: sites per channel (4 plates x 384 wells x 16 sites), "
+                        "sharded over the ranks")
+    p.add_argument("--stream-channels", type=int, default=5)
+    p.add_argument("--resident-gb", type=float, default=160.0,
+                   help="--stream-host: HBM for the two in-flight channels' resident sites; a "
+                        "channel share beyond half of it is streamed twice (stats, then correct)")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     return p.parse_args()
@@ -269,6 +279,265 @@ def bench_host_path(H, W, n_sites=64, reps=3):
             "job_sites_per_s": round(n_sites / (t_stats + t_corr), 1)}
 
 
+def link_rates(dev, nbytes=2 << 30):
+    """Pinned host <-> HBM copy rates on this box (GB/s): H2D alone, D2H alone,
+    both at once on two streams -- the PCIe roofline of --stream-host."""
+    import torch
+    h_in = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d_a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    d_b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def run(h2d, d2h):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        if h2d:
+            with torch.cuda.stream(s1):
+                d_a.copy_(h_in, non_blocking=True)
+        if d2h:
+            with torch.cuda.stream(s2):
+                h_out.copy_(d_b, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        return nbytes / (time.perf_counter() - t0) / 1e9
+
+    run(True, True)
+    r = {"h2d_GBs": round(max(run(True, False) for _ in range(2)), 1),
+         "d2h_GBs": round(max(run(False, True) for _ in range(2)), 1)}
+    both = max(run(True, True) for _ in range(2))
+    r["duplex_each_way_GBs"] = round(both, 1)
+    del h_in, h_out, d_a, d_b
+    return r
+
+
+def bench_stream_host(a, world, rank, local_rank, dist_on):
+    """configs[4]: a multi-plate batch (4 plates x 384 wells x 16 sites = 24,576
+    sites per channel, 5 channels) that does not live in HBM: the sites come
+    from pinned host memory over PCIe (corilla/api.py:69-83 reads them from
+    files one site at a time).  Each rank takes its contiguous share of every
+    channel.  A channel share that fits (--resident-gb) crosses the link once:
+    streamed in (H2D 2 B/px) chunk by chunk with the Welford pass chasing the
+    arrivals, kept resident for the fused correct + histogram pass, and the
+    corrected sites streamed out (D2H 2 B/px) while the NEXT channel streams in
+    on the other copy engine.  Sites beyond the resident budget are streamed
+    twice (stats, then correct).  The host side is a pinned ring of distinct
+    generated sites, cycled: the reference's file reads are not modelled."""
+    import torch
+    import torch.distributed as dist
+
+    from tmlibrary_amd import hip
+    from tmlibrary_amd.image import ZERO_LOG10
+    from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
+    from tmlibrary_amd.workflow.corilla.sharded import (StatsOps, merge_counts, merge_welford,
+                                                         shard_bounds)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if dist_on:
+        dist.init_process_group("nccl", device_id=dev)
+    H, W = a.height, a.width
+    npx = H * W
+    site_b = npx * 2
+    Q = 100000
+    CH = a.stream_channels
+    S_total = a.stream_sites
+    s_begin, s_end = shard_bounds(S_total, world, rank)
+    S = s_end - s_begin
+    CK = 32  # sites per copy / Welford launch
+    R = min(S, int(a.resident_gb * 1e9 / 2 / site_b) // CK * CK)  # resident sites per channel
+    RING = 64  # distinct host sites
+    L = hip.lib()
+    hip.check(L.tmh_set_device(local_rank))
+    log("stream-host: %d channels x %d sites/rank (%d resident, %d streamed twice); link test"
+        % (CH, S, R, S - R))
+    link = link_rates(dev)
+    log("link: %s" % link)
+
+    h_ring = torch.empty((RING, H, W), dtype=torch.int16, pin_memory=True)
+    tmp = torch.empty((RING, H, W), dtype=torch.int16, device=dev)
+    hip.check(L.tmh_synth_sites_device(C.c_void_p(tmp.data_ptr()), RING, H, W, SEED, 0, s_begin,
+                                       hip.TMH_SYNTH_STANDARD, None))
+    h_ring.copy_(tmp)
+    del tmp
+    h_out = torch.empty((4, CK, H, W), dtype=torch.int16, pin_memory=True)
+    resident = [torch.empty((max(R, 1), H, W), dtype=torch.int16, device=dev) for _ in range(2)]
+    stage = [torch.empty((CK, H, W), dtype=torch.int16, device=dev) for _ in range(2)]
+    d_out = [torch.empty((CK, H, W), dtype=torch.int16, device=dev) for _ in range(4)]
+    s_h2d, s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    comp = [torch.cuda.Stream(dev) for _ in range(2)]
+    lo, hi, gamma = quantile_table(npx, np.linspace(0, 100, Q))
+    lut = stats_log10_lut()
+    flags = hip.TMH_STATS_DEFERRED_PCT if dist_on else 0
+    handles = []
+    for b in range(2):
+        h, corr = C.c_void_p(), C.c_void_p()
+        hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
+                                     hip.ptr(lut), 1, flags, C.byref(h)))
+        sp = C.c_void_p(comp[b].cuda_stream)
+        hip.check(L.tmh_stats_set_stream(h, sp))
+        planes = [torch.empty(npx, dtype=torch.float64, device=dev) for _ in range(5)]
+        torch.cuda.synchronize(dev)
+        hip.check(L.tmh_corrector_create_device(C.c_void_p(planes[0].data_ptr()),
+                                                C.c_void_p(planes[1].data_ptr()), H, W, 1,
+                                                ZERO_LOG10, sp, C.byref(corr)))
+        handles.append((h, corr, sp, planes, StatsOps(L, h, npx, Q, dev)))
+    ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    state = {"buf_free": [None, None], "stage_free": [None, None], "out_free": [None] * 4,
+             "k_in": 0, "k_out": 0}
+    marks = []  # (channel, phase, timing event) of the timed run
+
+    def record(stream):
+        e = torch.cuda.Event()
+        e.record(stream)
+        return e
+
+    host_t = {}
+
+    def mark(c, phase, stream):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        marks.append((c, phase, e))
+        host_t.setdefault("c%d" % c, {})["enq_" + phase] = time.perf_counter()
+
+    def h2d(dst, j, c):
+        """chunk j of channel c from the host ring into dst (on the H2D engine)."""
+        src = h_ring[((j + c) * CK) % RING:((j + c) * CK) % RING + CK]
+        with torch.cuda.stream(s_h2d):
+            dst.copy_(src, non_blocking=True)
+        return record(s_h2d)
+
+    def channel(c):
+        b = c % 2
+        h, corr, sp, planes, ops = handles[b]
+        cs = comp[b]
+        mean, std, smean, sstd, ptmp = planes
+        buf = resident[b]
+        if state["buf_free"][b] is not None:
+            s_h2d.wait_event(state["buf_free"][b])
+        hip.check(L.tmh_stats_reset(h))
+        nch = (S + CK - 1) // CK
+        mark(c, "h2d_begin", s_h2d)
+        for j in range(nch):  # pass 1: arrivals -> Welford
+            n = min(CK, S - j * CK)
+            if j * CK < R:
+                dst = buf[j * CK:j * CK + n]
+            else:
+                k = state["k_in"] % 2
+                state["k_in"] += 1
+                if state["stage_free"][k] is not None:
+                    s_h2d.wait_event(state["stage_free"][k])
+                dst = stage[k][:n]
+            cs.wait_event(h2d(dst, j, c))
+            hip.check(L.tmh_stats_update_welford_device(h, ptr(dst), n, 1, sp))
+            if j * CK >= R:
+                state["stage_free"][k] = record(cs)
+        mark(c, "h2d_end", s_h2d)
+        with torch.cuda.stream(cs):
+            if dist_on:
+                merge_welford(ops, dist, n_total=S_total)
+            hip.check(L.tmh_stats_finalize_device(h, ptr(mean), ptr(std), sp))
+            hip.check(L.tmh_smooth_f64_device(ptr(mean), ptr(smean), ptr(ptmp), H, W, 5.0, sp))
+            hip.check(L.tmh_smooth_f64_device(ptr(std), ptr(sstd), ptr(ptmp), H, W, 5.0, sp))
+            hip.check(L.tmh_corrector_update_device(corr, ptr(smean), ptr(sstd), sp))
+        for j in range(nch):  # pass 2: correct + histogram -> out slots -> host
+            n = min(CK, S - j * CK)
+            if j * CK < R:
+                src = buf[j * CK:j * CK + n]
+            else:
+                k = state["k_in"] % 2
+                state["k_in"] += 1
+                if state["stage_free"][k] is not None:
+                    s_h2d.wait_event(state["stage_free"][k])
+                src = stage[k][:n]
+                cs.wait_event(h2d(src, j, c))
+            o = state["k_out"] % 4
+            state["k_out"] += 1
+            if state["out_free"][o] is not None:
+                cs.wait_event(state["out_free"][o])
+            hip.check(L.tmh_correct_u16_hist_device(corr, h, ptr(src), ptr(d_out[o]), n, -1, -1,
+                                                    sp))
+            e = record(cs)
+            if j * CK >= R:
+                state["stage_free"][k] = e
+            s_d2h.wait_event(e)
+            with torch.cuda.stream(s_d2h):
+                h_out[o][:n].copy_(d_out[o][:n], non_blocking=True)
+            state["out_free"][o] = record(s_d2h)
+        mark(c, "d2h_end", s_d2h)
+        if dist_on:
+            with torch.cuda.stream(cs):
+                merge_counts(ops, dist)
+        state["buf_free"][b] = record(cs)
+
+    log("stream-host: warm-up (both buffers)")
+    channel(0)
+    channel(1)
+    torch.cuda.synchronize(dev)
+    for k in list(state):
+        state[k] = [None] * len(state[k]) if isinstance(state[k], list) else 0
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    log("stream-host: timing %d channels" % CH)
+    marks.clear()
+    host_t.clear()
+    t0 = time.perf_counter()
+    for c in range(CH):
+        channel(c)
+    torch.cuda.synchronize(dev)
+    timeline = {}
+    if marks:
+        e0 = marks[0][2]
+        for c, phase, e in marks:
+            timeline.setdefault("c%d" % c, {})[phase] = round(e0.elapsed_time(e), 1)
+        for c, d in host_t.items():  # host enqueue times, same origin (approximately)
+            for k, v in d.items():
+                timeline[c][k] = round(1e3 * (v - t0), 1)
+    if dist_on:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # the last channel's statistics are complete: one sanity check of the job
+    h, corr, sp, planes, ops = handles[(CH - 1) % 2]
+    nn = C.c_int64()
+    mean = np.empty(npx)
+    hip.check(L.tmh_stats_finalize(h, C.byref(nn), hip.ptr(mean), None, None, None))
+    for h, corr, *_ in handles:
+        L.tmh_corrector_destroy(corr)
+        L.tmh_stats_destroy(h)
+    if dist_on:
+        dist.destroy_process_group()
+    if rank != 0:
+        return None
+    sites_done = CH * S_total
+    h2d_b = CH * (S_total * site_b + (S_total - min(S_total, R * world)) * site_b)
+    d2h_b = CH * S_total * site_b
+    per_link = elapsed * world
+    return {
+        "metric": "sites/sec (2160x2560 uint16) illumstats+correct streamed from host (PCIe-bound)",
+        "value": round(sites_done / elapsed, 1), "unit": "sites/s", "n_gpus": world,
+        "ms_total": round(1e3 * elapsed, 1), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64 stats / f32 correct (±1 DN)",
+        "data": "synthetic, %d distinct sites in a pinned host ring, cycled" % RING,
+        "config": {"workload": "configs[4]: %d channels x %d sites (4 plates x 384 wells x 16 "
+                               "sites) of %dx%d uint16 streamed from host, sharded over %d GPU(s)"
+                               % (CH, S_total, H, W, world),
+                   "resident_sites_per_channel_per_gpu": R, "sites_per_channel_per_gpu": S,
+                   "chunk_sites": CK},
+        "pcie": {"h2d_bytes": h2d_b, "d2h_bytes": d2h_b,
+                 "h2d_GBs_per_gpu": round(h2d_b / per_link / 1e9, 1),
+                 "d2h_GBs_per_gpu": round(d2h_b / per_link / 1e9, 1),
+                 "link": link,
+                 "frac_of_duplex_link": round(max(h2d_b, d2h_b) / per_link / 1e9 /
+                                              link["duplex_each_way_GBs"], 4)},
+        "timeline_ms": timeline,
+        "check": {"n_last_channel": int(nn.value), "expected": S_total,
+                  "mean_finite": bool(np.isfinite(mean).all())},
+    }
+
+
 # ---------------------------------------------------------------------------
 # oracle fingerprint check
 # ---------------------------------------------------------------------------
@@ -327,6 +596,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.stream_host:
+        r = bench_stream_host(a, world, rank, local_rank,
+                              world > 1 or os.environ.get("TMH_BENCH_FORCE_DIST") == "1")
+        if r is not None:
+            print(json.dumps(r), flush=True)
+        return
     H, W = a.height, a.width
     npx = H * W
     Q = 100000

@@ -78,3 +78,41 @@ def test_create_run_batches(tmp_path, caplog):
     assert [f[0] for f in batches[1]["channel_image_files_ids"]] == files[3]
     msgs = " ".join(r.message for r in caplog.records)
     assert "only 50 images" in msgs and 'no image files found for channel "2"' in msgs
+
+
+@pytest.mark.parametrize("prefetch,batch", [(1, 3), (2, 4), (4, 2), (3, 32)])
+def test_run_job_read_ahead_order(tmp_path, prefetch, batch):
+    """IllumstatsCalculator._blocks: several blocks decoded at once into a
+    bounded pool of reused buffers, yielded in file order (VERDICT r2 #8)."""
+    import os
+
+    from tmlibrary_amd.models import file as h5
+    from tmlibrary_amd.workflow.corilla.api import IllumstatsCalculator
+    store = h5.ExperimentStore(str(tmp_path))
+    os.makedirs(tmp_path / "channel_image_files")
+    rng = np.random.default_rng(prefetch * 10 + batch)
+    want = {}
+    for fid in range(13):
+        a = rng.integers(0, 65536, (24, 40), dtype=np.uint16)
+        h5.write_channel_image(store.channel_image_file(fid).location, a)
+        want[fid] = a
+    order = [7, 3, 12, 0, 1, 2, 11, 10, 4, 5, 6, 8, 9]
+    calc = IllumstatsCalculator(1, store=store, batch_size=batch, prefetch=prefetch,
+                                decode_threads=3)
+    for rep in range(2):  # the second job reuses the buffers
+        got_ids = []
+        for ids, sites in calc._blocks(order):
+            assert sites.shape == (len(ids), 24, 40)
+            for fid, s in zip(ids, sites):
+                assert np.array_equal(s, want[fid]), (rep, fid)
+            got_ids += list(ids)
+        assert got_ids == order
+    # abandoning the generator early does not hang
+    gen = calc._blocks(order)
+    next(gen)
+    gen.close()
+    # an unreadable file surfaces in the caller, and the workers stop
+    os.remove(store.channel_image_file(12).location)
+    with pytest.raises((IOError, OSError, KeyError, ValueError)):
+        for _ in calc._blocks(order):
+            pass

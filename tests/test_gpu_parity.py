@@ -195,6 +195,57 @@ def test_smooth_and_correct_vs_golden(L, name):
         assert np.array_equal(clipped.array, want_clip)
 
 
+@pytest.mark.parametrize("shape", [(1, 1), (1, 9), (3, 5), (20, 40), (40, 41), (41, 3), (7, 100)])
+def test_smooth_small_planes(L, shape):
+    """Planes smaller than the 41-tap kernel (sigma 5, radius 20): the
+    reflected border indices repeat (apply_kernels.hip reflect rule,
+    mahotas/scipy 'reflect' as restated by the oracle, itself pinned against
+    scipy in test_oracle_golden)."""
+    from tmlibrary_amd.image import smooth_f64
+    rng = np.random.default_rng(shape[0] * 131 + shape[1])
+    plane = rng.random(shape) * 4.0 + 1.0
+    got = smooth_f64(plane, 5)
+    want = orc.smooth_reflect(plane, 5)
+    assert np.allclose(got, want, rtol=1e-10, atol=1e-13), np.abs(got - want).max()
+    if plane.size > 1:
+        assert np.allclose(smooth_f64(plane, 2), orc.smooth_reflect(plane, 2), rtol=1e-10,
+                           atol=1e-13)
+
+
+def test_corrector_cache_sees_in_place_writes(L):
+    """the container's cached corrector is keyed on content.
+    Building it marks the planes read-only, so an in-place write raises; a
+    caller who re-enables writing gets a rebuilt corrector on the next call."""
+    from tmlibrary_amd.image import ChannelImage, IllumstatsContainer, IllumstatsImage
+    from tmlibrary_amd.metadata import ChannelImageMetadata, IllumstatsImageMetadata
+    rng = np.random.default_rng(9)
+    img = rng.integers(1, 5000, (48, 64), dtype=np.uint16)
+    mean = rng.random((48, 64)) * 0.2 + 2.5
+    std = rng.random((48, 64)) * 0.1 + 0.2
+    md = IllumstatsImageMetadata(channel_id=3)
+    cont = IllumstatsContainer(IllumstatsImage(mean.copy(), md), IllumstatsImage(std.copy(), md), {})
+
+    def corrected():
+        ci = ChannelImage(img.copy(), ChannelImageMetadata(3, 1, 1, 0, 0))
+        return ci.correct(cont).array
+
+    first = corrected()
+    assert_dn(first, orc.correct_illumination(img, mean, std))
+    with pytest.raises(ValueError):
+        cont.mean.array[0, 0] = 9.0  # read-only while a corrector is cached
+    c1 = cont.corrector()
+    assert cont.corrector() is c1  # unchanged planes: cached
+    cont.mean.array.flags.writeable = True
+    cont.mean.array[:, :32] += 0.05
+    second = corrected()
+    assert_dn(second, orc.correct_illumination(img, cont.mean.array, std))
+    assert not np.array_equal(first, second)
+    assert not cont.mean.array.flags.writeable  # protected again
+    cont.smooth()  # replaced planes: rebuilt
+    third = corrected()
+    assert_dn(third, orc.correct_illumination(img, cont.mean.array, cont.std.array))
+
+
 def test_correct_channel_mismatch(L):
     from tmlibrary_amd.image import ChannelImage, IllumstatsContainer, IllumstatsImage
     from tmlibrary_amd.metadata import ChannelImageMetadata, IllumstatsImageMetadata

@@ -33,11 +33,11 @@ namespace tmh {
 // host-numpy LUT for values < kWfLut (LDS, bit-identical to numpy).  Larger
 // values (bright sites) use the same LUT on their top bits:
 //   u = 16 a + r,  a = u >> 4 in [256, 4096),
-//   log10(u) = log10(a) + log10(16) + log1p(t) / ln 10,  t = r * sinv[a] < 1/256,
-// where sinv[a] = 1/(16 a) is a second LDS table (f64, correctly rounded: t
-// carries <= 2 ulp) and the 5-term series truncates below 3e-16 absolute.  No
-// division and no per-pixel branch, so a bright group costs ~9 f64 ops per
-// pixel instead of the LUT path's 3 (the f64 division this replaces was ~17).
+//   log10(u) = log10(a) + log10(16) + log1p(t) / ln 10,  t = r / (16 a) < 1/256,
+// with 1/(16 a) from recip16 (t carries < 1e-17 absolute) and a 5-term series
+// (truncation below 3e-16 absolute).  No
+// division: a large value costs ~12 f64 ops instead of the LUT path's 3 (the
+// f64 division this replaces took ~17).
 constexpr double kInvLn10 = 0.43429448190325182765;
 constexpr double kLog10_16 = 1.2041199826559247809;
 // 1/(16 a): INV = 1 from the LDS table, INV = 0 by v_rcp_f32 plus one f64
@@ -105,9 +105,8 @@ __global__ void k_rn_table(double* __restrict__ rn, int64_t n0, int64_t n) {
 
 // Stats transform of eight pixels: LDS LUT gather of each value's low 12
 // bits (no clamp: the index stays in the table), then -- only when a word has
-// a value >= 4,096 -- all eight recomputed branch-free with log10_big and the
-// large ones selected (wc counts such groups: the fused pass picks its LDS
-// slice width from it).  The inner loop is VALU-issue bound (3 f64 ops per
+// a value >= 4,096 -- those slots recomputed with log10_big (wc counts such
+// groups: the fused pass picks its LDS slice width from it).  The inner loop is VALU-issue bound (3 f64 ops per
 // pixel), so the integer work per pixel is kept to the gather address.
 template <bool LOG, int INV>
 __device__ __forceinline__ void xform8(const uint4 v, const double* slut, const double* sinv,
@@ -121,11 +120,11 @@ __device__ __forceinline__ void xform8(const uint4 v, const double* slut, const 
     for (int k = 0; k < 8; ++k) x[k] = slut[u[k] & kIdx];
     if (wide) {
       ++wc;
+      // per pixel: on standard data ~7 % of wave-steps have one lane with
+      // one such value, and a branch-free pass over all eight cost 0.2 ms
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const double xb = log10_big<INV>(u[k], slut, sinv);
-        x[k] = u[k] > kIdx ? xb : x[k];
-      }
+      for (int k = 0; k < 8; ++k)
+        if (u[k] > kIdx) x[k] = log10_big<INV>(u[k], slut, sinv);
     }
   } else {
     wc += wide ? 1u : 0u;

@@ -434,13 +434,23 @@ class IllumstatsContainer(object):
         return self.percentiles[keys[idx]]
 
     def corrector(self, log_transform=True) -> Corrector:
-        """Cached device corrector for the current mean/std arrays (rebuilt
-        when either array object is replaced, e.g. by ``smooth``)."""
-        key = (id(self.mean.array), id(self.std.array), bool(log_transform))
-        if self._corr is None or self._corr_key != key:
+        """Cached device corrector for the current mean/std planes.
+
+        The cache is keyed on the plane objects AND their contents: building
+        the corrector marks both arrays read-only, so an in-place write into
+        ``mean.array`` / ``std.array`` raises instead of leaving stale device
+        coefficients behind.  Replacing a plane (``smooth`` does) or making it
+        writeable again (``arr.flags.writeable = True``, then writing) makes
+        the next call rebuild the corrector from the current values."""
+        m, s = self.mean.array, self.std.array
+        key = (id(m), id(s), bool(log_transform))
+        if (self._corr is None or self._corr_key != key or m.flags.writeable or
+                s.flags.writeable):
             if self._corr is not None:
                 self._corr.close()
-            self._corr = Corrector(self.mean.array, self.std.array, log_transform)
+            self._corr = Corrector(m, s, log_transform)
             self._corr_key = key
-            self._corr_arrays = (self.mean.array, self.std.array)  # keep ids valid
+            self._corr_arrays = (m, s)  # keep the ids valid while cached
+            m.flags.writeable = False
+            s.flags.writeable = False
         return self._corr

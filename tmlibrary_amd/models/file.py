@@ -126,15 +126,54 @@ def read_channel_image(path):
     return out
 
 
+def granted_cores():
+    """CPUs this process may actually use: the affinity mask, capped by a
+    cgroup v2/v1 CPU quota when one is set (a GPU box shows every core of the
+    host but grants a share of them)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(period)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                period = int(f.read())
+            if q > 0:
+                quota = q / period
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = min(n, max(1, int(quota)))
+    return max(1, n)
+
+
 def default_decode_threads():
-    n = os.cpu_count() or 1
-    return max(1, min(16, n))  # the GPU boxes grant 16 cores per GPU
+    """Inflate workers: the cores granted, at most 64 (one file each)."""
+    return max(1, min(64, granted_cores()))
 
 
-def read_channel_images(paths, n_threads=None):
+def channel_image_shape(path):
+    """(height, width, numpy dtype) of a channel image file, from its header."""
+    L = h5lib()
+    h, w, bits = C.c_int(), C.c_int(), C.c_int()
+    _check(L.tmh5_channel_image_shape(_b(path), C.byref(h), C.byref(w), C.byref(bits)), path)
+    return h.value, w.value, (np.uint8 if bits.value == 8 else np.uint16)
+
+
+def read_channel_images(paths, n_threads=None, out=None):
     """Decode many channel image files (same shape/dtype) into one [n, H, W]
     array with ``n_threads`` parallel inflate workers (libtmh5; the HDF5
-    layout of tmlib/models/file.py:322-363)."""
+    layout of tmlib/models/file.py:322-363).  ``out``: a C-contiguous
+    [>= n, H, W] array of the files' dtype to decode into (reused buffers
+    skip the page faults of a fresh allocation); returns its first n planes."""
     paths = list(paths)
     L = h5lib()
     if not paths:
@@ -142,7 +181,15 @@ def read_channel_images(paths, n_threads=None):
     h, w, bits = C.c_int(), C.c_int(), C.c_int()
     _check(L.tmh5_channel_image_shape(_b(paths[0]), C.byref(h), C.byref(w), C.byref(bits)),
            paths[0])
-    out = np.empty((len(paths), h.value, w.value), np.uint8 if bits.value == 8 else np.uint16)
+    dt = np.uint8 if bits.value == 8 else np.uint16
+    if out is None:
+        out = np.empty((len(paths), h.value, w.value), dt)
+    else:
+        if (out.dtype != dt or out.ndim != 3 or out.shape[0] < len(paths) or
+                out.shape[1:] != (h.value, w.value) or not out.flags.c_contiguous):
+            raise ValueError("out must be a C-contiguous [>= %d, %d, %d] %s array"
+                             % (len(paths), h.value, w.value, np.dtype(dt).name))
+        out = out[:len(paths)]
     arr = (C.c_char_p * len(paths))(*[_b(p) for p in paths])
     nt = default_decode_threads() if n_threads is None else int(n_threads)
     _check(L.tmh5_read_channel_images(arr, len(paths), out.ctypes.data, nt), paths[0])

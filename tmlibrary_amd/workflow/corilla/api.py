@@ -17,14 +17,30 @@ import logging
 import queue
 import threading
 
+import numpy as np
+
 from tmlibrary_amd.image import IllumstatsContainer
-from tmlibrary_amd.models.file import ExperimentStore, read_channel_images
+from tmlibrary_amd.models.file import (ExperimentStore, channel_image_shape,
+                                       default_decode_threads, read_channel_images)
 from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
 
 logger = logging.getLogger(__name__)
 
 #: corilla/api.py:69 — sites per channel beyond which the reference subsamples
 SITE_LIMIT = 20000
+
+
+def _block_buffer(n, H, W, dtype):
+    """[n, H, W] host buffer for a decoded block: page-locked when torch can
+    pin memory (the H2D copy is then pure DMA, no CPU staging), else
+    pageable."""
+    try:
+        import torch
+        tdt = torch.int16 if np.dtype(dtype) == np.uint16 else torch.uint8
+        t = torch.empty((n, H, W), dtype=tdt, pin_memory=True)
+        return t.numpy().view(dtype)
+    except Exception:  # no torch, or no pinnable memory (no device)
+        return np.empty((n, H, W), dtype)
 
 
 def _file_id(fid):
@@ -38,6 +54,9 @@ class IllumstatsCalculator(object):
     """Calculation of illumination statistics (corilla/api.py:31-146)."""
 
     def __init__(self, experiment_id, store=None, batch_size=32, prefetch=2, decode_threads=None):
+        """prefetch: blocks of ``batch_size`` files decoded concurrently ahead of
+        the GPU update; decode_threads: inflate workers over all of them (None:
+        the cores granted, models/file.py:granted_cores)."""
         self.experiment_id = experiment_id
         if store is None:
             raise ValueError("an ExperimentStore is required (no database in this build)")
@@ -46,7 +65,8 @@ class IllumstatsCalculator(object):
         self.store = store
         self.batch_size = batch_size
         self.prefetch = prefetch
-        self.decode_threads = decode_threads  # None: min(16, cpu count)
+        self.decode_threads = decode_threads
+        self._buffers = {}  # (block, H, W, dtype) -> reused block buffers
 
     def create_run_batches(self, args=None, channel_files=None, channel_names=None, seed=None):
         """One job per channel (corilla/api.py:45-105).
@@ -84,34 +104,73 @@ class IllumstatsCalculator(object):
 
     def _blocks(self, file_ids):
         """Yield (file ids, [n, H, W] sites) in order, ``batch_size`` files at a
-        time, decoded by ``decode_threads`` parallel inflate workers one block
-        ahead of the GPU update."""
-        q = queue.Queue(maxsize=max(1, self.prefetch))
-        stop = object()
+        time.  ``prefetch`` blocks are decoded at once,
+        each by its share of ``decode_threads`` inflate workers, into a bounded
+        pool of reused (pinned when torch can pin) block buffers, so decode of
+        the next blocks overlaps the GPU update of the current one and no
+        block pays fresh-page faults.  A worker takes a free buffer BEFORE it
+        claims the next block index: buffers then go to blocks in order and a
+        run-ahead worker can never hold the buffer the next block needs."""
         step = max(1, self.batch_size)
+        blocks = [file_ids[i:i + step] for i in range(0, len(file_ids), step)]
+        if not blocks:
+            return
+        paths = [[self.store.channel_image_file(f).location for f in b] for b in blocks]
+        H, W, dt = channel_image_shape(paths[0][0])
+        total = self.decode_threads or default_decode_threads()
+        inflight = max(1, min(self.prefetch, len(blocks)))
+        per = max(1, total // inflight)
+        # the block buffers are kept on the calculator: pinning ~0.35 GB per
+        # buffer costs more than decoding a short job
+        key = (step, H, W, np.dtype(dt).str)
+        bufs = self._buffers.setdefault(key, [])
+        while len(bufs) < min(inflight + 1, len(blocks)):
+            bufs.append(_block_buffer(step, H, W, dt))
+        pool = queue.Queue()
+        for b in bufs[:min(inflight + 1, len(blocks))]:
+            pool.put(b)
+        lock = threading.Lock()
+        ready = threading.Condition(lock)
+        results = {}
+        state = {"next": 0, "stop": False}
 
-        def reader():
-            try:
-                for i in range(0, len(file_ids), step):
-                    ids = file_ids[i:i + step]
-                    paths = [self.store.channel_image_file(f).location for f in ids]
-                    q.put((ids, read_channel_images(paths, self.decode_threads)))
-            except BaseException as e:  # surface I/O errors in the caller
-                q.put(e)
-            q.put(stop)
-
-        t = threading.Thread(target=reader, daemon=True)
-        t.start()
-        try:
+        def worker():
             while True:
-                item = q.get()
-                if item is stop:
-                    break
+                buf = pool.get()
+                with lock:
+                    k = state["next"]
+                    if state["stop"] or k >= len(blocks):
+                        pool.put(buf)
+                        return
+                    state["next"] = k + 1
+                try:
+                    item = read_channel_images(paths[k], per, out=buf)
+                except BaseException as e:  # surface I/O errors in the caller
+                    item = e
+                with ready:
+                    results[k] = (buf, item)
+                    ready.notify_all()
+
+        threads = [threading.Thread(target=worker, daemon=True) for _ in range(inflight)]
+        for t in threads:
+            t.start()
+        try:
+            for k in range(len(blocks)):
+                with ready:
+                    while k not in results:
+                        ready.wait()
+                    buf, item = results.pop(k)
                 if isinstance(item, BaseException):
                     raise item
-                yield item
+                yield blocks[k], item
+                pool.put(buf)  # the consumer's update has returned: reuse
         finally:
-            t.join()
+            with lock:
+                state["stop"] = True
+            for _ in threads:
+                pool.put(None)  # wake workers waiting for a buffer
+            for t in threads:
+                t.join()
 
     def run_job(self, batch, assume_clean_state=False):
         """corilla/api.py:115-146."""

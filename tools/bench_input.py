@@ -56,7 +56,30 @@ def main():
             out = h5.read_channel_images(paths, nt)
             res["parallel_decode_%dt_sites_per_s" % nt] = round(a.sites / (time.perf_counter() - t0), 1)
         assert np.array_equal(out, np.stack(sites))
+        blk = min(32, a.sites)
+        buf = np.empty((blk, a.height, a.width), np.uint16)
+        h5.read_channel_images(paths[:blk], a.threads, out=buf)  # fault the pages in
+        t0 = time.perf_counter()
+        for i in range(0, a.sites - blk + 1, blk):
+            h5.read_channel_images(paths[i:i + blk], a.threads, out=buf)
+        res["parallel_decode_%dt_reused_out_sites_per_s" % a.threads] = round(
+            (a.sites // blk) * blk / (time.perf_counter() - t0), 1)
         if not a.no_gpu:
+            import torch
+
+            from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
+            stack = np.ascontiguousarray(np.stack(sites[:blk]))
+            pinned = torch.empty(stack.shape, dtype=torch.int16, pin_memory=True).numpy().view(
+                np.uint16)
+            pinned[...] = stack
+            for name, src in (("pageable", stack), ("pinned", pinned)):
+                st = OnlineStatistics((a.height, a.width), batch_size=32)
+                st.update_batch(src)  # warm-up
+                t0 = time.perf_counter()
+                for _ in range(4):
+                    st.update_batch(src)
+                res["update_batch_%s_sites_per_s" % name] = round(4 * blk / (time.perf_counter() - t0), 1)
+                st.close()
             from tmlibrary_amd.models.file import ExperimentStore
             from tmlibrary_amd.workflow.corilla.api import IllumstatsCalculator
             store = ExperimentStore(root)

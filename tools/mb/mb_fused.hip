@@ -163,6 +163,14 @@ int main(int argc, char** argv) {
   time("fused no hist, const coef (ABL 3)", cb, [&] { fused(std::integral_constant<int, 3>()); });
   time("fused no flush (ABL 8)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 8>()); });
   time("fused prod (ABL 0) again", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 0>()); });
+  unsigned long long* wide;
+  CK(hipMalloc(&wide, 8));
+  CK(hipMemset(wide, 0, 8));
+  time("fused auto (narrow runs, wide exits)", cb + 8.0 * npx, [&] {
+    CK(hipMemsetAsync(fn, 0, 4, 0));
+    launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
+                        queues, cus, kFusedAuto, wide, 1000ull, 0);
+  });
   for (int cfg = 0; cfg < kFusedConfigs; ++cfg) {
     char nm[64];
     snprintf(nm, sizeof nm, "fused cfg %d (%d,%d,%d)", cfg, kFusedCfgs[cfg].spu,
