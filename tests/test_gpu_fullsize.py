@@ -30,7 +30,7 @@ import numpy as np
 import pytest
 
 from oracle import corilla_oracle as orc
-from test_gpu_parity import Dev
+from test_gpu_parity import Dev, check_order_stats, site_order_stats
 from util import assert_close_rel, dn_report
 
 pytestmark = pytest.mark.gpu
@@ -123,6 +123,7 @@ def test_headline_pipeline_fullsize(L):
         sh = np.empty(65536, np.uint32)
         hip.check(L.tmh_stats_site_histogram(h, i, hip.ptr(sh)))
         site_hist[i] = sh
+    order_stats = site_order_stats(L, h, (0, 63, N - 1), 100000)
     sites = d_in.get(np.uint16, (N, H, W))
     out = d_out.get(np.uint16, (N, H, W))
     assert np.array_equal(out.reshape(N, npx)[::37], out1), "fused pass not repeatable"
@@ -147,6 +148,7 @@ def test_headline_pipeline_fullsize(L):
     for res in (r1, r):  # one part, four parts
         assert_close_rel(res["mean"], ref.mean)
         assert_close_rel(res["std"], ref.std)
+    check_order_stats([sites[i] for i in (0, 63, N - 1)], order_stats)
     assert np.array_equal(r["hist"], pooled), "pooled histogram not bit-exact"
     assert np.array_equal(r["acc"], ref.percentile_sums), "percentile sums not bit-exact"
     sm_ref, ss_ref = orc.smooth_reflect(ref.mean, 5), orc.smooth_reflect(ref.std, 5)

@@ -44,6 +44,29 @@ class Dev:
         self.L.tmh_free_device(self.p)
 
 
+def site_order_stats(L, h, sites, Q):
+    """(previous, next) order statistics of the given sites of the handle's
+    last batch, decoded from the device's (compact or dense) storage."""
+    from tmlibrary_amd import hip
+    res = []
+    for i in sites:
+        a, b = np.empty(Q, np.uint16), np.empty(Q, np.uint16)
+        hip.check(L.tmh_stats_site_order_stats(h, i, hip.ptr(a), hip.ptr(b)))
+        res.append((a, b))
+    return res
+
+
+def check_order_stats(sites, got, q=None):
+    """Every site's (previous, next) order statistics equal the oracle's
+    (numpy 'linear' positions read off the exact CDF)."""
+    q = np.linspace(0, 100, 100000) if q is None else q
+    lo, hi, _ = orc.quantile_table(sites[0].size, q)
+    for i, (s, (a, b)) in enumerate(zip(sites, got)):
+        hs = orc.histogram_u16(s)
+        assert np.array_equal(a, orc.order_statistics_from_hist(hs, lo)), "site %d previous" % i
+        assert np.array_equal(b, orc.order_statistics_from_hist(hs, hi)), "site %d next" % i
+
+
 def run_stats(sites, log=True, decimals=3, batch=3, flags=0):
     from tmlibrary_amd.image import ChannelImage
     from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
@@ -488,7 +511,8 @@ def _fused_job(L, sites, clip=(-1, -1), q=None):
         site_h.append(sh)
     out = d_out.get(np.uint16, sites.shape)
     res = dict(n=nn.value, mean=m_h, std=s_h, acc=acc, hist=hist, site_hist=site_h, out=out,
-               smean=smean.get(np.float64, (H, W)), sstd=sstd.get(np.float64, (H, W)))
+               smean=smean.get(np.float64, (H, W)), sstd=sstd.get(np.float64, (H, W)),
+               order_stats=site_order_stats(L, h, range(n), Q))
     L.tmh_corrector_destroy(c)
     L.tmh_stats_destroy(h)
     for b in planes + [d_in, d_out]:
@@ -529,6 +553,39 @@ def test_fused_correct_hist_pipeline(L, kind):
     for s, o in zip(sites, r["out"]):
         want = orc.correct_illumination(s, r["smean"], r["sstd"])
         assert_dn(o, want)
+    check_order_stats(sites, r["order_stats"])
+
+
+@pytest.mark.parametrize("kind", ["lognormal_tails", "uniform", "constant", "two_values",
+                                  "sparse", "tiny"])
+def test_order_statistics_scatter_path(L, kind):
+    """The per-site order statistics of the non-fused update path (one
+    histogram workgroup per site, all 64 rounds) decode to the oracle's for
+    every quantile: dense middles (compact tiles), sparse tails (dense
+    fallback tiles), one-bin sites, Q > pixel count (tiny)."""
+    from tmlibrary_amd.synth import synth_sites_host
+    rng = np.random.default_rng(5)
+    h, w = 240, 320
+    if kind == "lognormal_tails":
+        sites = [np.clip(rng.lognormal(7.0, 1.1, (h, w)), 0, 65535).astype(np.uint16)
+                 for _ in range(3)]
+    elif kind == "uniform":
+        sites = [rng.integers(0, 65536, (h, w), dtype=np.uint16) for _ in range(3)]
+    elif kind == "constant":
+        sites = [np.full((h, w), 777, np.uint16), np.full((h, w), 0, np.uint16),
+                 np.full((h, w), 65535, np.uint16)]
+    elif kind == "two_values":
+        sites = [np.where(rng.random((h, w)) < 0.3, 3, 60000).astype(np.uint16) for _ in range(3)]
+    elif kind == "sparse":  # few distinct values spread over the range
+        vals = np.sort(rng.choice(65536, 40, replace=False)).astype(np.uint16)
+        sites = [vals[rng.integers(0, 40, (h, w))] for _ in range(3)]
+    else:
+        sites = synth_sites_host(4, 20, 30, seed=3)
+    st = run_stats(sites, batch=len(sites))
+    st._finalize()
+    check_order_stats(sites, site_order_stats(L, st._h, range(len(sites)), 100000))
+    ref = orc.run_illumstats(sites)
+    assert np.array_equal(st.percentile_sums, ref.percentile_sums)
 
 
 @pytest.mark.parametrize("qkind", ["linspace", "custom"])
@@ -547,6 +604,7 @@ def test_quantile_tables(L, qkind):
     for s in sites:
         want += orc.percentile_linear(s, q)
     assert np.array_equal(r["acc"], want)
+    check_order_stats(sites, r["order_stats"], q)
 
 
 @pytest.mark.parametrize("parts", [2, 3, 4])
