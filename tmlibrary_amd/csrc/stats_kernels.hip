@@ -485,21 +485,22 @@ __device__ __forceinline__ void advance_rank(const int32_t* R, int& t, int32_t& 
   Rt = R[hi];
 }
 
-constexpr int kFillGroups = 1;  // groups of 8 quantiles a thread walks in a row
-
 // One round's order statistics.  R[t] = inclusive prefix rank of the round's
 // bin t (value bin0 + t); the round owns the sorted positions [r0, r1).
-// Quantile-centric: each thread walks kFillGroups consecutive groups of 8
-// quantiles, reads their previous positions from the (L2-resident) table (the
-// next position is min(prev + 1, n - 1) for every q in [0, 100],
-// np.percentile 'linear'; a general next table is read only if the caller's
-// differs), keeps the ones inside [r0, r1), and finds each owning bin by
-// advancing through R from the previous quantile's bin (one binary search
-// per 32 quantiles), writing each group as one 32-B store of interleaved
-// (previous, next) values (2-B stores where a group straddles the round's
-// ends).  The round's quantile range is [r0 * scale, r1 * scale] up to
-// rounding (and one position's worth of quantiles), so the groups scanned
-// carry a margin and the position test decides membership exactly.
+// Quantile-centric: each thread takes groups of 8 quantiles, reads their
+// previous positions from the (L2-resident) table -- the next group's
+// positions are loaded while the current group is resolved -- keeps the ones
+// inside [r0, r1), and finds each owning bin by advancing through R from the
+// previous quantile's bin (one binary search per group).  The next position
+// is min(prev + 1, n - 1) for every q in [0, 100] (np.percentile 'linear'):
+// when it is still inside the previous statistic's bin (R[bin] > prev + 1,
+// nearly always) the next statistic is the same value and needs no search; a
+// general next table is read only if the caller's differs.  Each group is
+// written as one 32-B store of interleaved (previous, next) values (2-B
+// stores where a group straddles the round's ends).  The round's quantile
+// range is [r0 * scale, r1 * scale] up to rounding (and one position's worth
+// of quantiles), so the groups scanned carry a margin and the position test
+// decides membership exactly.
 template <int NT = kHistThreads>
 __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_t r1,
                                             uint32_t bin0, const QPos& p,
@@ -513,64 +514,73 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
   const int64_t g0 = qa >> 3, g1 = (qb - 1) >> 3;
   const bool tab16 = vec16;  // tables are 16-B aligned rows when Q % 8 == 0 (hipMalloc base)
   const int32_t a = (int32_t)r0, b = (int32_t)r1;
-  for (int64_t sg = g0 + (int64_t)threadIdx.x * kFillGroups; sg <= g1;
-       sg += (int64_t)NT * kFillGroups) {
+  auto positions = [&](int64_t q0, int32_t (&pl)[8]) {
+    if (tab16 && q0 + 8 <= p.Q) {
+      const int4 a0 = reinterpret_cast<const int4*>(p.lo + q0)[0];
+      const int4 a1 = reinterpret_cast<const int4*>(p.lo + q0)[1];
+      pl[0] = a0.x; pl[1] = a0.y; pl[2] = a0.z; pl[3] = a0.w;
+      pl[4] = a1.x; pl[5] = a1.y; pl[6] = a1.z; pl[7] = a1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pl[j] = q0 + j < p.Q ? p.lo[q0 + j] : INT32_MAX;
+    }
+  };
+  int64_t g = g0 + (int64_t)threadIdx.x;
+  int32_t pn[8];
+  if (g <= g1) positions(g << 3, pn);
+  for (; g <= g1; g += NT) {
+    const int64_t q0 = g << 3;
+    int32_t pl[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pl[j] = pn[j];
+    if (g + NT <= g1) positions((g + NT) << 3, pn);  // in flight while this group resolves
     int tl = 0, th = 0;
     int32_t Rl = R[0], Rh = Rl;
-    for (int64_t g = sg; g < sg + kFillGroups && g <= g1; ++g) {
-      const int64_t q0 = g << 3;
-      int32_t pl[8];
-      if (tab16 && q0 + 8 <= p.Q) {
-        const int4 a0 = reinterpret_cast<const int4*>(p.lo + q0)[0];
-        const int4 a1 = reinterpret_cast<const int4*>(p.lo + q0)[1];
-        pl[0] = a0.x; pl[1] = a0.y; pl[2] = a0.z; pl[3] = a0.w;
-        pl[4] = a1.x; pl[5] = a1.y; pl[6] = a1.z; pl[7] = a1.w;
-      } else {
+    uint32_t ol[4] = {0u, 0u, 0u, 0u}, oh[4] = {0u, 0u, 0u, 0u};
+    uint32_t ml = 0, mh = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pl[j] = q0 + j < p.Q ? p.lo[q0 + j] : INT32_MAX;
+    for (int j = 0; j < 8; ++j) {
+      const int32_t pj = pl[j];
+      const bool mine = pj >= a && pj < b;
+      if (mine) {
+        advance_rank(R, tl, Rl, pj);
+        ol[j >> 1] |= (bin0 + (uint32_t)tl) << (16 * (j & 1));
+        ml |= 1u << j;
       }
-      uint32_t ol[4] = {0u, 0u, 0u, 0u}, oh[4] = {0u, 0u, 0u, 0u};
-      uint32_t ml = 0, mh = 0;
+      const int32_t hj = p.hi_next ? (pj < p.last ? pj + 1 : pj)
+                                   : (q0 + j < p.Q ? p.hi[q0 + j] : INT32_MAX);
+      if (p.hi_next && mine && hj < Rl) {  // next position in the same bin
+        oh[j >> 1] |= (bin0 + (uint32_t)tl) << (16 * (j & 1));
+        mh |= 1u << j;
+      } else if (hj >= a && hj < b) {
+        if (th < tl) {
+          th = tl;
+          Rh = Rl;
+        }
+        advance_rank(R, th, Rh, hj);
+        oh[j >> 1] |= (bin0 + (uint32_t)th) << (16 * (j & 1));
+        mh |= 1u << j;
+      }
+    }
+    // interleaved (previous, next) order statistics: one u32 per quantile,
+    // a group of 8 is contiguous inside one quantile tile
+    uint32_t* og = vlh + (q0 / kOsTile) * p.tstride + (q0 % kOsTile);
+    if (vec16 && ml == 0xFFu && mh == 0xFFu) {
+      uint4* dst = reinterpret_cast<uint4*>(og);
+      dst[0] = make_uint4(__builtin_amdgcn_perm(oh[0], ol[0], 0x05040100u),
+                          __builtin_amdgcn_perm(oh[0], ol[0], 0x07060302u),
+                          __builtin_amdgcn_perm(oh[1], ol[1], 0x05040100u),
+                          __builtin_amdgcn_perm(oh[1], ol[1], 0x07060302u));
+      dst[1] = make_uint4(__builtin_amdgcn_perm(oh[2], ol[2], 0x05040100u),
+                          __builtin_amdgcn_perm(oh[2], ol[2], 0x07060302u),
+                          __builtin_amdgcn_perm(oh[3], ol[3], 0x05040100u),
+                          __builtin_amdgcn_perm(oh[3], ol[3], 0x07060302u));
+    } else if (ml | mh) {  // a round edge: write the halves this round owns
+      uint16_t* h16 = reinterpret_cast<uint16_t*>(og);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int32_t pj = pl[j];
-        if (pj >= a && pj < b) {
-          advance_rank(R, tl, Rl, pj);
-          ol[j >> 1] |= (bin0 + (uint32_t)tl) << (16 * (j & 1));
-          ml |= 1u << j;
-        }
-        const int32_t hj = p.hi_next ? (pj < p.last ? pj + 1 : pj)
-                                     : (q0 + j < p.Q ? p.hi[q0 + j] : INT32_MAX);
-        if (hj >= a && hj < b) {
-          if (th < tl) {
-            th = tl;
-            Rh = Rl;
-          }
-          advance_rank(R, th, Rh, hj);
-          oh[j >> 1] |= (bin0 + (uint32_t)th) << (16 * (j & 1));
-          mh |= 1u << j;
-        }
-      }
-      // interleaved (previous, next) order statistics: one u32 per quantile,
-      // a group of 8 is contiguous inside one quantile tile
-      uint32_t* og = vlh + (q0 / kOsTile) * p.tstride + (q0 % kOsTile);
-      if (vec16 && ml == 0xFFu && mh == 0xFFu) {
-        uint4* dst = reinterpret_cast<uint4*>(og);
-        dst[0] = make_uint4(__builtin_amdgcn_perm(oh[0], ol[0], 0x05040100u),
-                            __builtin_amdgcn_perm(oh[0], ol[0], 0x07060302u),
-                            __builtin_amdgcn_perm(oh[1], ol[1], 0x05040100u),
-                            __builtin_amdgcn_perm(oh[1], ol[1], 0x07060302u));
-        dst[1] = make_uint4(__builtin_amdgcn_perm(oh[2], ol[2], 0x05040100u),
-                            __builtin_amdgcn_perm(oh[2], ol[2], 0x07060302u),
-                            __builtin_amdgcn_perm(oh[3], ol[3], 0x05040100u),
-                            __builtin_amdgcn_perm(oh[3], ol[3], 0x07060302u));
-      } else if (ml | mh) {  // a round edge: write the halves this round owns
-        uint16_t* h16 = reinterpret_cast<uint16_t*>(og);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if ((ml >> j) & 1u) h16[2 * j] = (uint16_t)(ol[j >> 1] >> (16 * (j & 1)));
-          if ((mh >> j) & 1u) h16[2 * j + 1] = (uint16_t)(oh[j >> 1] >> (16 * (j & 1)));
-        }
+        if ((ml >> j) & 1u) h16[2 * j] = (uint16_t)(ol[j >> 1] >> (16 * (j & 1)));
+        if ((mh >> j) & 1u) h16[2 * j + 1] = (uint16_t)(oh[j >> 1] >> (16 * (j & 1)));
       }
     }
   }
