@@ -836,7 +836,7 @@ def main():
 
     if rank == 0:
         site_bytes = npx * 2
-        alg = {  # algorithmic HBM bytes per launch (per-site figure x sites)
+        alg = {  # algorithmic HBM bytes per channel job (per-site figure x sites)
             "welford": S * site_bytes + 4 * 8 * npx,       # sites + mean/M2 read & write
             "hist": S * site_bytes,                        # sites
             "correct": S * site_bytes * 2 + 16 * npx,      # sites in + out, coefficients
@@ -845,9 +845,12 @@ def main():
         }
         kdetail = {}
         for name, (avg_ms, k) in kern.items():
-            d = {"avg_ms": round(avg_ms, 4), "launches": k}
+            # alg bytes are per channel job; a kernel may run in several launches
+            # per job (pct_acc / hist_finalize in pieces): rate over its job time
+            step_ms = avg_ms * k / (a.steps * CH)
+            d = {"avg_ms": round(avg_ms, 4), "launches": k, "ms_per_job": round(step_ms, 4)}
             if name in alg:
-                gbs = alg[name] / (avg_ms * 1e-3) / 1e9
+                gbs = alg[name] / (step_ms * 1e-3) / 1e9
                 d["alg_GBs"] = round(gbs, 1)
                 d["frac_of_8TBs"] = round(gbs / HBM_PEAK_GBS, 4)
             kdetail[name] = d

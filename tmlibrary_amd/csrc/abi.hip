@@ -274,7 +274,6 @@ struct tmh_corrector {
   DBuf<unsigned long long> fix_e;    // pixels flagged for the f64 refinement (common.h)
   DBuf<unsigned int> fix_n;
   DBuf<tmh_window> win;  // per-site alignment windows of the chain pass
-  DBuf<int> queues;
   int n_wg = 256;
   DBuf<double> sums, partial;
   DBuf<uint16_t> stage_in, stage_out;
@@ -884,7 +883,6 @@ static void corrector_init(tmh_corrector* c, const double* d_mean, const double*
   c->mconst2.alloc(1);
   c->rc.alloc(1);
   c->fix_n.alloc(1, true);
-  c->queues.alloc(8, true);
   TMH_HIP(hipDeviceGetAttribute(&c->n_wg, hipDeviceAttributeMultiprocessorCount, c->device));
   corrector_coeffs(c, d_mean, d_std, c->stream);
 }
@@ -1160,7 +1158,7 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         launch_correct_hist(dev_in + c0 * h->npx, dev_out + c0 * h->npx, c->npx, nc, c->coef2.p,
                             c->mconst2.p, fl, c->log_transform, clip_lo, clip_hi,
                             h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0,
-                            c->queues.p, c->n_wg, h->fused_cfg, h->wide.p, wide_thresh, s);
+                            c->n_wg, h->fused_cfg, h->wide.p, wide_thresh, s);
         launch_fix_correct(dev_in + c0 * h->npx, dev_out + c0 * h->npx, 2, c->npx, nc, fl,
                            c->coef64.p, c->rc.p, c->log_transform, clip_lo, clip_hi, s);
         const bool side = k < nch - 1;

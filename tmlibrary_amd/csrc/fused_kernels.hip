@@ -7,19 +7,22 @@
 // their histograms are built from the correction's read instead of a pass of
 // their own: HBM traffic is then the algorithmic 2 + 4 B/px per site.
 //
-// Layout of the work: the image is cut into 8 * bands_per_xcd pixel bands;
-// XCD x owns bands {x, x+8, ...} and walks (band, site-group) units
-// band-major from its own queue, so a band's correction coefficients (8 B/px:
-// 2.76 MB per band at 2160x2560 and 2 bands per XCD) stay resident in that
-// XCD's 4 MB L2 while the sites stream through.  A unit is SPU sites of one
-// band: each lane loads its 8 pixels' coefficients once and applies them to
-// the SPU sites, so the L2 coefficient traffic is 8/SPU B/px.  Each site of
-// the unit histograms its raw pixels into its own LDS slice (values below
+// Layout of the work: the image is cut into n_bands = 16 pixel bands, and a
+// unit is SPU sites of one band.  Units are dealt out statically (units are
+// equal in size, so there is nothing to balance): workgroup b takes units b,
+// b + G, b + 2G, ... in a band-major sweep, the 8 XCDs two bands apart -- each
+// XCD's L2 holds the coefficients of the band it is on (8 B/px: 2.76 MB per
+// band at 2160x2560) while the site groups stream through.  Measured against
+// the previous per-XCD band queues with work stealing, same-box A/B of the
+// whole job (profiles/r2/ab_fused_sched_r2pqr.jsonl): 13.8 vs 14.3 ms on one
+// box, 14.5 vs 14.7 ms (5 runs each) on another; a sweep with every XCD on
+// the SAME band ran 15.5 ms -- its site streams all sit at one offset.  Each
+// lane loads its 8 pixels' coefficients once per group and applies them to
+// the SPU sites (L2 coefficient traffic 8/SPU B/px).  Each site of the unit
+// histograms its raw pixels into its own LDS slice (values below
 // kLdsBins/SPU; larger values go straight to the global histogram), and at
 // the end of the unit the slices are added to the sites' global histograms
-// with contiguous-lane atomics, only up to the largest value the unit saw.
-// Idle XCDs steal from other queues (placement is a speed choice only; every
-// unit is processed exactly once).
+// with contiguous-lane atomics.
 //
 // Arithmetic (ChannelImage._correct_illumination, tmlib/image.py:599-631), in
 // the log2 domain so 10**t is one v_exp_f32:
@@ -32,13 +35,7 @@
 
 namespace tmh {
 
-constexpr int kBandsPerXcd = 2;  // pixel bands per XCD queue
-
-__device__ __forceinline__ int xcc_id() {
-  int x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-  return x & 7;
-}
+constexpr int kFusedBands = 16;  // pixel bands of the static schedule
 
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
@@ -138,21 +135,20 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 }
 
 // ABL: development ablations (tools/mb), 0 in production: 1 = no histogram,
-// 2 = constant coefficients, 8 = no flush.
+// 2 = constant coefficients, 8 = no flush, 32 = no arithmetic.
 // NT threads per workgroup, LB LDS bins per workgroup (split into SPU slices
 // of BINS counters plus one overflow counter each: a pixel >= BINS adds to the
 // overflow counter -- never read -- and to its global bin, so the common path
 // is one v_min + one ds_add per pixel).
-// Each workgroup reserves its NEXT unit while it streams the current one, and
-// issues the next unit's first loads before it flushes the current unit's
-// histogram slices, so the flush (LDS scan + global atomics + barriers) runs
-// with the next unit's pixels already in flight.
+// Each workgroup issues its next unit's first loads before it flushes the
+// current unit's histogram slices, so the flush (LDS scan + global atomics +
+// barriers) runs with the next unit's pixels already in flight.
 template <bool LOG, bool CLIP, int SPU, int ABL, int NT, int LB>
 __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void k_correct_hist(
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
     const float4* __restrict__ coef, const float4* __restrict__ mconst2, FixList fl,
     int clip_lo, int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
-    int* __restrict__ queues, int bands_per_xcd, const unsigned long long* __restrict__ wide,
+    int n_bands, const unsigned long long* __restrict__ wide,
     unsigned long long wide_lo, unsigned long long wide_hi) {
   // launch-time selection (launch_correct_hist): this configuration runs only
   // when the Welford pass's count of wide pixel groups is in [wide_lo, wide_hi)
@@ -165,7 +161,6 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   constexpr uint32_t HIMASK = (0xFFFFu & ~(uint32_t)(BINS - 1)) * 0x00010001u;
   static_assert((BINS & (BINS - 1)) == 0, "slice size must be a power of two");
   __shared__ __attribute__((aligned(16))) uint32_t bins[SPU * SLICE];
-  __shared__ int unit_sh;
   // per site of the unit: the 1,024-bin rounds holding counts (the rare
   // global adds and, at the flush, the slice's non-empty rounds); two sets,
   // alternating by unit, so one is published while the next unit fills the
@@ -174,14 +169,14 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   const int tid = threadIdx.x;
   for (int i = tid; i < SPU * SLICE; i += NT) bins[i] = 0u;
   if (tid < 2 * SPU) rm_sh[tid / SPU][tid % SPU] = 0ull;
+  __syncthreads();
 
   const float4 m = mconst2[0];
   const uint32_t clo2 = (uint32_t)clip_lo * 0x00010001u, chi2 = (uint32_t)clip_hi * 0x00010001u;
   const int ngroups = (int)(npx >> 3);
   const int site_bytes = (int)(npx * 2);
-  const int n_bands = 8 * bands_per_xcd;
   const int n_groups_s = (int)((n_sites + SPU - 1) / SPU);
-  const int upq = bands_per_xcd * n_groups_s;  // units per queue
+  const int n_units = n_bands * n_groups_s;
   // coefficient planes: plane k holds (mu, mu, a, a) of pixels 8g+2k, 8g+2k+1
   // of group g, so each of a lane's four coefficient loads is one contiguous
   // 1 KiB per wave
@@ -189,22 +184,17 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
       __builtin_amdgcn_make_buffer_rsrc((void*)coef, 0, (int)(npx * 8), 0x00020000);
   const float4 cc = make_float4(2.5f, 2.4f, 1.1f, 0.9f);
 
-  // unit = (queue q, index u) -> band q + 8 * (u / n_groups_s), sites from s0
-  int q = xcc_id(), exhausted = 0;
+  // Static deal: workgroup b takes units i = b, b + G, b + 2G, ... (G =
+  // gridDim.x, a multiple of 8, so i % 8 is b's XCD).  Unit i is site group
+  // i % n_groups_s of band (i / n_groups_s + 2 * (i % 8)) % n_bands: the
+  // sweep is band-major, with the 8 XCDs two bands apart.
+  int next_i = (int)blockIdx.x;
   auto grab = [&]() -> int {
-    while (exhausted < 8) {
-      if (tid == 0) unit_sh = atomicAdd(&queues[q], 1);
-      __syncthreads();
-      const int u = __builtin_amdgcn_readfirstlane(unit_sh);
-      __syncthreads();
-      if (u < upq) {
-        exhausted = 0;
-        return q * upq + u;
-      }
-      q = (q + 1) & 7;  // this queue is drained: steal from the next
-      ++exhausted;
-    }
-    return -1;
+    const int i = next_i;
+    next_i += (int)gridDim.x;
+    if (i >= n_units) return -1;
+    const int band = (i / n_groups_s + 2 * (i % 8)) % n_bands;
+    return band * n_groups_s + i % n_groups_s;
   };
   struct Unit {
     int g0, g1, ns;
@@ -212,10 +202,9 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     __amdgpu_buffer_rsrc_t rin, rout;  // the unit's SPU sites; loads past ns read 0
   };
   auto decode = [&](int code) -> Unit {
-    const int qq = code / upq, u = code % upq;
-    const int band = qq + 8 * (u / n_groups_s);
+    const int band = code / n_groups_s;
     Unit r;
-    r.s0 = (int64_t)(u % n_groups_s) * SPU;
+    r.s0 = (int64_t)(code % n_groups_s) * SPU;
     r.ns = (int)(n_sites - r.s0 < SPU ? n_sites - r.s0 : SPU);
     r.g0 = (int)((int64_t)band * ngroups / n_bands);
     r.g1 = (int)((int64_t)(band + 1) * ngroups / n_bands);
@@ -283,6 +272,11 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
         }
       }
       uint32_t o[4];
+      if (ABL & 32) {  // no arithmetic: the pixels pass through (coefficients kept live)
+        const u32x4_t r = {w.x ^ (__float_as_uint(cf[0].x) & 1u), w.y ^ (__float_as_uint(cf[1].y) & 1u),
+                           w.z ^ (__float_as_uint(cf[2].z) & 1u), w.w ^ (__float_as_uint(cf[3].w) & 1u)};
+        return r;
+      }
       const uint32_t far = fcorrect8<LOG, CLIP>(wd, cf, m.x, m.z, m.w, clo2, chi2, o);
       if (far) fix_push8(fl, far, un.s0 + k, (int64_t)g * 8);
       const u32x4_t r = {o[0], o[1], o[2], o[3]};
@@ -370,10 +364,9 @@ static_assert(FusedCfgCheck<0>::ok && FusedCfgCheck<1>::ok && FusedCfgCheck<2>::
 static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                                     const float4* cf4, const float4* mconst2, const FixList& fl,
                                     int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
-                                    unsigned long long* rmask, int* queues, int n_wg, int cfg,
+                                    unsigned long long* rmask, int n_wg, int cfg,
                                     const unsigned long long* wide, unsigned long long wide_lo,
                                     unsigned long long wide_hi, hipStream_t s) {
-  TMH_HIP(hipMemsetAsync(queues, 0, 8 * sizeof(int), s));
 #define TMH_LAUNCH_CH(L_, K_)                                                                    \
   {                                                                                              \
     constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
@@ -381,12 +374,12 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
     if (clip_lo >= 0)                                                                            \
       hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, 0, c.threads, c.lds_bins>), grid,     \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, queues, kBandsPerXcd, wide, wide_lo,       \
+                         clip_lo, clip_hi, hist, rmask, kFusedBands, wide, wide_lo,              \
                          wide_hi);                                                               \
     else                                                                                         \
       hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, 0, c.threads, c.lds_bins>), grid,    \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, queues, kBandsPerXcd, wide, wide_lo,       \
+                         clip_lo, clip_hi, hist, rmask, kFusedBands, wide, wide_lo,              \
                          wide_hi);                                                               \
   }
 #define TMH_LAUNCH_CFG(L_)              \
@@ -416,7 +409,7 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, const FixList& fl,
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
-                         unsigned long long* rmask, int* queues, int n_wg, int cfg,
+                         unsigned long long* rmask, int n_wg, int cfg,
                          const unsigned long long* wide, unsigned long long wide_thresh,
                          hipStream_t s) {
   if (n_sites <= 0) return;
@@ -424,14 +417,14 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
   const float4* cf4 = reinterpret_cast<const float4*>(coef2);
   if (cfg >= 0 || !wide) {
     launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo,
-                            clip_hi, hist, rmask, queues, n_wg, cfg >= 0 ? cfg : kFusedNarrow,
+                            clip_hi, hist, rmask, n_wg, cfg >= 0 ? cfg : kFusedNarrow,
                             nullptr, 0, 0, s);
     return;
   }
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedNarrow, wide, 0, wide_thresh, s);
+                          hist, rmask, n_wg, kFusedNarrow, wide, 0, wide_thresh, s);
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedWide, wide, wide_thresh, ~0ull, s);
+                          hist, rmask, n_wg, kFusedWide, wide, wide_thresh, ~0ull, s);
 }
 
 }  // namespace tmh

@@ -95,7 +95,6 @@ int main(int argc, char** argv) {
   uint32_t* hist;
   unsigned long long *rmask, *fe;
   unsigned int* fn;
-  int* queues;
   uint32_t* sink;
   CK(hipMalloc(&coef, npx * 8));
   CK(hipMalloc(&mconst2, 16));
@@ -103,7 +102,6 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&rmask, S * 8));
   CK(hipMalloc(&fe, (size_t)1 << 23));
   CK(hipMalloc(&fn, 4));
-  CK(hipMalloc(&queues, 64));
   CK(hipMalloc(&sink, 64));
   {
     std::vector<float> c(npx * 2);
@@ -152,10 +150,9 @@ int main(int argc, char** argv) {
   const dim3 fg(cus * 2), fb(512);
   auto fused = [&](auto abl_tag) {
     constexpr int ABL = decltype(abl_tag)::value;
-    CK(hipMemsetAsync(queues, 0, 32, 0));
     CK(hipMemsetAsync(fn, 0, 4, 0));
     hipLaunchKernelGGL((k_correct_hist<true, false, 4, ABL, 512, 16384>), fg, fb, 0, 0, in, out,
-                       npx, S, coef, mconst2, fl, -1, -1, hist, rmask, queues, kBandsPerXcd,
+                       npx, S, coef, mconst2, fl, -1, -1, hist, rmask, kFusedBands,
                        nullptr, 0ull, 0ull);
   };
   time("fused prod (ABL 0)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 0>()); });
@@ -169,7 +166,7 @@ int main(int argc, char** argv) {
   time("fused auto (narrow runs, wide exits)", cb + 8.0 * npx, [&] {
     CK(hipMemsetAsync(fn, 0, 4, 0));
     launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                        queues, cus, kFusedAuto, wide, 1000ull, 0);
+                        cus, kFusedAuto, wide, 1000ull, 0);
   });
   for (int cfg = 0; cfg < kFusedConfigs; ++cfg) {
     char nm[64];
@@ -178,7 +175,7 @@ int main(int argc, char** argv) {
     time(nm, cb + 8.0 * npx, [&] {
       CK(hipMemsetAsync(fn, 0, 4, 0));
       launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist,
-                          rmask, queues, cus, cfg,
+                          rmask, cus, cfg,
                           nullptr, 0, 0);
     });
   }

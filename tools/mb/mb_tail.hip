@@ -93,7 +93,6 @@ int main(int argc, char** argv) {
   uint32_t* hist;
   unsigned long long *rmask, *fe, *pooled, *parts;
   unsigned int* fn;
-  int* queues;
   uint32_t* sink;
   CK(hipMalloc(&coef, npx * 8));
   CK(hipMalloc(&mconst2, 16));
@@ -101,7 +100,6 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&rmask, S * 8));
   CK(hipMalloc(&fe, (size_t)1 << 23));
   CK(hipMalloc(&fn, 4));
-  CK(hipMalloc(&queues, 64));
   CK(hipMalloc(&sink, 64));
   CK(hipMalloc(&pooled, kBins * 8));
   CK(hipMalloc(&parts, 16 * kBins * 8));
@@ -120,7 +118,7 @@ int main(int argc, char** argv) {
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const FixList fl{fe, fn, (unsigned)(((size_t)1 << 23) / 8)};
   launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                      queues, cus, dist == 0 ? kFusedNarrow : kFusedWide, nullptr, 0, 0);
+                      cus, dist == 0 ? kFusedNarrow : kFusedWide, nullptr, 0, 0);
   CK(hipDeviceSynchronize());
   {
     std::vector<unsigned long long> rm(S);
