@@ -199,6 +199,89 @@ __global__ __launch_bounds__(256, WPS) void k_wf_var(const uint16_t* __restrict_
   if (r == 1.2345 + wc) out[g] = r;
 }
 
+// f32 packed arithmetic variant: LUT as (hi, lo) f32 pairs, d = (x_hi - K_hi) +
+// (x_lo - K_lo) in f32, 16-site f32 block sums folded into f64
+typedef float f2_t __attribute__((ext_vector_type(2)));
+template <int G, int BLK>
+__global__ __launch_bounds__(256) void k_wf_f32(const uint16_t* __restrict__ sites, int64_t npx,
+                                                int64_t n_sites, const double* __restrict__ lut,
+                                                double* __restrict__ out) {
+  __shared__ float2 slut2[kWfLut];
+  for (int i = threadIdx.x; i < kWfLut; i += 256) {
+    const double x = lut[i];
+    const float hi = (float)x;
+    slut2[i] = make_float2(hi, (float)(x - (double)hi));
+  }
+  __syncthreads();
+  const int64_t ng = npx >> 3;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= ng) return;
+  const uint4* src = reinterpret_cast<const uint4*>(sites) + g;
+  const int64_t last = n_sites - 1;
+  uint4 cur[G], nxt[G];
+#pragma unroll
+  for (int k = 0; k < G; ++k) cur[k] = ld_site<true>(src + (k < last ? k : last) * ng);
+  f2_t Kh[4], Kl[4];
+  {
+    const uint4 v = cur[0];
+    const uint32_t u[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
+                           v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const float2 a = slut2[u[2 * p] & 4095u], b = slut2[u[2 * p + 1] & 4095u];
+      Kh[p] = (f2_t){a.x, b.x};
+      Kl[p] = (f2_t){a.y, b.y};
+    }
+  }
+  double s1[8], s2[8];
+  f2_t f1[4], f2[4];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) f1[p] = f2[p] = (f2_t){0.f, 0.f};
+  int blk = 0;
+  for (int64_t s = 0; s < n_sites; s += G) {
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int64_t t = s + G + k;
+      nxt[k] = ld_site<true>(src + (t < last ? t : last) * ng);
+    }
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      if (s + k < n_sites) {
+        const uint4 v = cur[k];
+        const uint32_t u[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
+                               v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const float2 a = slut2[u[2 * p] & 4095u], b = slut2[u[2 * p + 1] & 4095u];
+          const f2_t d = ((f2_t){a.x, b.x} - Kh[p]) + ((f2_t){a.y, b.y} - Kl[p]);
+          f1[p] += d;
+          f2[p] = __builtin_elementwise_fma(d, d, f2[p]);
+        }
+      }
+    }
+    blk += G;
+    if (blk >= BLK) {
+      blk = 0;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        s1[2 * p] += f1[p].x; s1[2 * p + 1] += f1[p].y;
+        s2[2 * p] += f2[p].x; s2[2 * p + 1] += f2[p].y;
+        f1[p] = f2[p] = (f2_t){0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < G; ++k) cur[k] = nxt[k];
+  }
+  double r = 0.0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) r += f1[p].x + f2[p].y;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r += s1[j] + s2[j];
+  if (r == 1.2345) out[g] = r;
+}
+
 template <int U>
 __global__ __launch_bounds__(256) void k_read(const uint4* __restrict__ p, int64_t n,
                                               uint32_t* __restrict__ sink) {
@@ -319,6 +402,9 @@ int main(int argc, char** argv) {
         launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, f, nullptr, 0, shape);
       });
     }
+  time("wf f32 G2 blk16", [&] { hipLaunchKernelGGL((k_wf_f32<2, 16>), ag, dim3(256), 0, 0, in, npx, S, lut, mean); });
+  time("wf f32 G2 blk32", [&] { hipLaunchKernelGGL((k_wf_f32<2, 32>), ag, dim3(256), 0, 0, in, npx, S, lut, mean); });
+  time("wf f32 G4 blk16", [&] { hipLaunchKernelGGL((k_wf_f32<4, 16>), ag, dim3(256), 0, 0, in, npx, S, lut, mean); });
   time("welford production (parts 1)", [&] {
     launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 1, nullptr, 0);
   });
