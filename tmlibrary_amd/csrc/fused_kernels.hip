@@ -347,11 +347,17 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
 // (sites per unit, threads, LDS bins) of the fused pass, selected per handle
 // (tmh_stats_set_option, TMH_OPT_FUSED_CONFIG) or automatically per launch
 // (kFusedAuto: kFusedNarrow, or kFusedWide when the sites are bright).
+// bands: pixel bands of the static deal -- 8 for the wide configuration, whose
+// 16,384-bin slices flush more counts per unit (fewer, longer units: 17.3 vs
+// 17.95 ms on bright sites, profiles/r2/mb_shape_bright_r2x.txt), 16 otherwise.
 struct FusedCfg {
-  int spu, threads, lds_bins;
+  int spu, threads, lds_bins, bands;
 };
-constexpr FusedCfg kFusedCfgs[kFusedConfigs] = {
-    {2, 1024, 32768}, {4, 1024, 32768}, {2, 512, 16384}, {4, 512, 16384}, {1, 1024, 32768}};
+constexpr FusedCfg kFusedCfgs[kFusedConfigs] = {{2, 1024, 32768, 8},
+                                                {4, 1024, 32768, kFusedBands},
+                                                {2, 512, 16384, kFusedBands},
+                                                {4, 512, 16384, kFusedBands},
+                                                {1, 1024, 32768, kFusedBands}};
 template <int K>
 struct FusedCfgCheck {
   static_assert((kFusedCfgs[K].lds_bins / kFusedCfgs[K].spu) % 1024 == 0,
@@ -374,12 +380,12 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
     if (clip_lo >= 0)                                                                            \
       hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, 0, c.threads, c.lds_bins>), grid,     \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, kFusedBands, wide, wide_lo,              \
+                         clip_lo, clip_hi, hist, rmask, c.bands, wide, wide_lo,                  \
                          wide_hi);                                                               \
     else                                                                                         \
       hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, 0, c.threads, c.lds_bins>), grid,    \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, kFusedBands, wide, wide_lo,              \
+                         clip_lo, clip_hi, hist, rmask, c.bands, wide, wide_lo,                  \
                          wide_hi);                                                               \
   }
 #define TMH_LAUNCH_CFG(L_)              \

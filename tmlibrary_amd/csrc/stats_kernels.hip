@@ -33,18 +33,23 @@ namespace tmh {
 // host-numpy LUT for values < kWfLut (LDS, bit-identical to numpy).  Larger
 // values (bright sites) use the same LUT on their top bits:
 //   u = 16 a + r,  a = u >> 4 in [256, 4096),
-//   log10(u) = log10(a) + log10(16) + log1p(t) / ln 10,  t = r / (16 a) < 1/256,
-// with 1/(16 a) from recip16 (t carries < 1e-17 absolute) and a 5-term series
-// (truncation below 3e-16 absolute).  No
-// division: a large value costs ~12 f64 ops instead of the LUT path's 3 (the
-// f64 division this replaces took ~17).
+//   log10(u) = log10(a) + log10(16) + log1p(t) / ln 10,  t = r / (16 a) < 1/256.
+// INV 0 / 1: 1/(16 a) in f64 (Newton step / LDS table) and a 5-term f64 series
+// (truncation below 3e-16 absolute), ~12 f64 ops.  INV 2 (production): the
+// small term log1p(t) / ln 10 <= 1.6e-3 in f32 -- rcp, three-term series
+// (truncation <= t^4/4 / ln 10 < 5e-11), f32 rounding < 2e-10 absolute -- then
+// one f64 add: a value >= 4,096 is within 3e-10 of numpy's log10 (1e-10
+// relative, against the 1e-6 bar on mean and std), at a fraction of the
+// VALU cost -- bright sites (most values >= 4,096) made the f64 form's pass
+// VALU-bound (17.7 ms vs 6.0 on standard sites, profiles/r2/ab_finalize_sr_r2y.jsonl).
 constexpr double kInvLn10 = 0.43429448190325182765;
 constexpr double kLog10_16 = 1.2041199826559247809;
+constexpr int kWfInvScalar = 2;  // rare-value form of the odd-shape (per-pixel) pass
 // 1/(16 a): INV = 1 from the LDS table, INV = 0 by v_rcp_f32 plus one f64
 // Newton step (relative error ~1e-14: t then carries < 1e-17 absolute)
 template <int INV>
 __device__ __forceinline__ double recip16(uint32_t a, const double* sinv) {
-  if (INV) return sinv[a];
+  if (INV == 1) return sinv[a];
   const double d = (double)(a << 4);
   const double r0 = (double)__builtin_amdgcn_rcpf((float)(a << 4));
   return fma(r0, fma(-d, r0, 1.0), r0);
@@ -52,6 +57,13 @@ __device__ __forceinline__ double recip16(uint32_t a, const double* sinv) {
 template <int INV>
 __device__ __forceinline__ double log10_big(uint32_t u, const double* slut, const double* sinv) {
   const uint32_t a = u >> 4;
+  if (INV == 2) {
+    constexpr float c1 = (float)kInvLn10, c2 = (float)(-0.5 * kInvLn10),
+                    c3 = (float)(kInvLn10 / 3.0);
+    const float t = (float)(u & 15u) * __builtin_amdgcn_rcpf((float)(a << 4));
+    const float c = t * __builtin_fmaf(t, __builtin_fmaf(t, c3, c2), c1);
+    return slut[a] + (kLog10_16 + (double)c);
+  }
   const double t = (double)(u & 15u) * recip16<INV>(a, sinv);
   const double series =
       t * (kInvLn10 +
@@ -70,7 +82,7 @@ __device__ __forceinline__ void fill_wf_tables(const double* __restrict__ lut, d
                                                double* sinv, int nt) {
   for (int i = threadIdx.x; i < kWfLut; i += nt) {
     slut[i] = lut[i];
-    if (INV) sinv[i] = i ? 1.0 / (16.0 * (double)i) : 0.0;
+    if (INV == 1) sinv[i] = i ? 1.0 / (16.0 * (double)i) : 0.0;
   }
 }
 
@@ -78,7 +90,7 @@ template <bool LOG>
 __device__ __forceinline__ double xform(uint32_t u, const double* slut) {
   if (!LOG) return (double)u;
   double x = slut[u & (uint32_t)(kWfLut - 1)];
-  if (u >= (uint32_t)kWfLut) x = log10_big<0>(u, slut, nullptr);
+  if (u >= (uint32_t)kWfLut) x = log10_big<kWfInvScalar>(u, slut, nullptr);
   return x;
 }
 
@@ -92,7 +104,7 @@ __device__ __forceinline__ void welford1(double x, double rn, double& mu, double
 // reciprocal source (tools/mb/mb_welford.hip compares the four shapes on
 // standard and bright sites; profiles/r2/mb_welford_shapes_*.txt).
 constexpr int kWfThreads = 256;
-constexpr int kWfInv = 0;
+constexpr int kWfInv = 2;
 constexpr int kWfScalarThreads = 256;
 constexpr int kWfGroup = 2;  // sites per pipeline stage (two stages in flight)
 constexpr int kWfMaxParts = 4;
@@ -167,7 +179,7 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
     const WfMerge mg, double* __restrict__ mean, double* __restrict__ m2,
     const double* __restrict__ lut, double* __restrict__ part,
     unsigned long long* __restrict__ wide) {
-  __shared__ double slut[kWfLut], sinv[INV ? kWfLut : 1];
+  __shared__ double slut[kWfLut], sinv[INV == 1 ? kWfLut : 1];
   __shared__ uint32_t wide_sh;
   if (LOG) fill_wf_tables<INV>(lut, slut, sinv, NT);
   if (threadIdx.x == 0) wide_sh = 0u;
@@ -352,8 +364,8 @@ static void launch_welford_vec8(const uint16_t* sites, int64_t npx, int64_t n_si
                        n_sites, per, mg, mean, m2, lut, part, wide);
 }
 
-// shape = -1: production (kWfThreads, kWfInv); 0..3: (256|512 threads) x
-// (Newton | LDS-table reciprocal) for the microbenchmark
+// shape = -1: production (kWfThreads, kWfInv); 0..5: (256|512 threads) x
+// (f64 Newton | f64 LDS-table reciprocal | f32 small term) for the microbenchmark
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
                     double* part, size_t part_cap, int forced_parts,
@@ -366,12 +378,14 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
     const int64_t per = cdiv(n_sites, f);
     const double nl = (double)n_sites, n = (double)(n0 + n_sites);
     const WfMerge mg{1.0 / nl, nl / n, (double)n0 * nl / n, n0 == 0};
-    if (shape < 0) shape = (kWfThreads == 512 ? 2 : 0) + kWfInv;
     switch (shape) {
       case 0: launch_welford_vec8<256, 0>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       case 1: launch_welford_vec8<256, 1>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       case 2: launch_welford_vec8<512, 0>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
-      default: launch_welford_vec8<512, 1>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
+      case 3: launch_welford_vec8<512, 1>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
+      case 4: launch_welford_vec8<256, 2>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
+      case 5: launch_welford_vec8<512, 2>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
+      default: launch_welford_vec8<kWfThreads, kWfInv>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
     }
     if (f > 1) {
       WfParts pc{};
@@ -460,11 +474,12 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, in
 constexpr int kRound = 1024;  // histogram bins per round of the scans
 
 constexpr int kTailChunkDefault = 8;  // rounds whose counts are loaded together
-// Advance (t, Rt = R[t]) to the first index >= t with R[index] > x (R: 1024
+// Advance (t, Rt = R[t]) to the first index >= t with R[index] > x (R: LEN
 // non-decreasing inclusive prefix ranks in LDS; the caller guarantees
-// R[t - 1] <= x < R[1023]).  Consecutive quantile positions mostly stay in
+// R[t - 1] <= x < R[LEN - 1]).  Consecutive quantile positions mostly stay in
 // one bin (no LDS read: Rt is cached) or step to the next (one read); the
 // rest finish with a binary search over (t+1, 1023].
+template <int LEN = kRound>
 __device__ __forceinline__ void advance_rank(const int32_t* R, int& t, int32_t& Rt, int32_t x) {
   if (Rt > x) return;
   const int32_t r1 = R[t + 1];
@@ -473,7 +488,7 @@ __device__ __forceinline__ void advance_rank(const int32_t* R, int& t, int32_t& 
     Rt = r1;
     return;
   }
-  int lo = t + 1, hi = kRound - 1;  // R[lo] <= x < R[hi]
+  int lo = t + 1, hi = LEN - 1;  // R[lo] <= x < R[hi]
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
     if (R[mid] > x)
@@ -501,7 +516,7 @@ __device__ __forceinline__ void advance_rank(const int32_t* R, int& t, int32_t& 
 // range is [r0 * scale, r1 * scale] up to rounding (and one position's worth
 // of quantiles), so the groups scanned carry a margin and the position test
 // decides membership exactly.
-template <int NT = kHistThreads>
+template <int NT = kHistThreads, int LEN = kRound>
 __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_t r1,
                                             uint32_t bin0, const QPos& p,
                                             uint32_t* __restrict__ vlh, bool vec16) {
@@ -543,7 +558,7 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
       const int32_t pj = pl[j];
       const bool mine = pj >= a && pj < b;
       if (mine) {
-        advance_rank(R, tl, Rl, pj);
+        advance_rank<LEN>(R, tl, Rl, pj);
         ol[j >> 1] |= (bin0 + (uint32_t)tl) << (16 * (j & 1));
         ml |= 1u << j;
       }
@@ -557,7 +572,7 @@ __device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_
           th = tl;
           Rh = Rl;
         }
-        advance_rank(R, th, Rh, hj);
+        advance_rank<LEN>(R, th, Rh, hj);
         oh[j >> 1] |= (bin0 + (uint32_t)th) << (16 * (j & 1));
         mh |= 1u << j;
       }
@@ -656,13 +671,16 @@ __device__ __forceinline__ void hist_tail(CountFn count, DoneFn done, int64_t s,
 }
 
 // hist_tail for a histogram whose possibly non-empty 1,024-bin rounds are
-// known up front (need: bit j = round j): only those rounds are loaded and
-// scanned -- BPT = 1024 / NT consecutive bins per thread, one or two barriers
-// per round, the next round's counts in flight while the current one is
-// scanned -- instead of walking all 64 rounds.  Same outputs as hist_tail
-// (site_hist rows are zero-filled for the rounds not visited).  NT = 256 is
-// the narrow form that fits beside the fused pass's workgroups on a CU.
-template <int ABL, int NT, typename CountFn, typename DoneFn>
+// known up front (need: bit j = round j): only those rounds are loaded, and
+// they are scanned SR rounds at a time (a super-round of SR * 1,024 bins: one
+// block scan and one rank table per super-round that holds any needed round,
+// bins of the rounds not needed taken as 0 without a load) -- BPT = SR *
+// 1024 / NT consecutive bins per thread, the next super-round's counts in
+// flight while the current one is scanned -- instead of walking all 64
+// rounds.  Same outputs as hist_tail (site_hist rows are zero-filled for the
+// rounds not visited).  NT = 256, SR = 1 is the narrow form that fits beside
+// the fused pass's workgroups on a CU.  starts: 2 * SR * 1024 int32 of LDS.
+template <int ABL, int NT, int SR, typename CountFn, typename DoneFn>
 __device__ __forceinline__ void hist_tail_rounds(unsigned long long need, CountFn count,
                                                  DoneFn done, int64_t s, const QPos& p,
                                                  uint32_t* __restrict__ vlh_all,
@@ -670,62 +688,69 @@ __device__ __forceinline__ void hist_tail_rounds(unsigned long long need, CountF
                                                  int64_t* __restrict__ zero_counts,
                                                  uint32_t* __restrict__ site_hist,
                                                  uint32_t* slots, int32_t* starts) {
-  constexpr int BPT = kRound / NT;
+  constexpr int LEN = SR * kRound;
+  constexpr int BPT = LEN / NT;
+  static_assert(BPT >= 1 && kRound % BPT == 0, "a thread's bins lie inside one round");
   const int tid = threadIdx.x;
   uint32_t* vlh = vlh_all + s * (int64_t)kOsTile;  // this site's column of the tiles
   const bool vec16 = (p.Q & 7) == 0;
   if (site_hist) {  // debug/parity copy: the rounds not visited are empty
     for (int j = 0; j < kBins / kRound; ++j)
       if (!((need >> j) & 1ull))
-#pragma unroll
-        for (int i = 0; i < BPT; ++i) site_hist[s * kBins + (uint32_t)(j * kRound + tid * BPT + i)] = 0u;
+        for (int i = tid; i < kRound; i += NT) site_hist[s * kBins + (uint32_t)(j * kRound + i)] = 0u;
   }
-  int64_t base = 0;  // exclusive rank of the current round's first bin
+  unsigned long long sneed = 0ull;  // super-rounds holding a needed round
+#pragma unroll
+  for (int k = 0; k < kBins / LEN; ++k)
+    if ((need >> (k * SR)) & ((SR == 64 ? 0ull : (1ull << SR)) - 1ull)) sneed |= 1ull << k;
+  // this thread's bins lie in round (k * SR + tid * BPT / kRound) of super-round k
+  auto load = [&](int k, uint32_t (&c)[BPT]) {
+    const uint32_t b0 = (uint32_t)k * LEN + tid * BPT;
+    const bool live = (need >> (b0 / kRound)) & 1ull;
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) c[i] = live ? count(b0 + i) : 0u;
+  };
+  int64_t base = 0;  // exclusive rank of the current super-round's first bin
   int nscan = 0;
   uint32_t cn[BPT];
-  if (need) {
-    const uint32_t b0 = (uint32_t)__builtin_ctzll(need) * kRound + tid * BPT;
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) cn[i] = count(b0 + i);
-  }
-  while (need) {
-    const int j = __builtin_ctzll(need);
-    need &= need - 1ull;
+  if (sneed) load(__builtin_ctzll(sneed), cn);
+  while (sneed) {
+    const int k = __builtin_ctzll(sneed);
+    sneed &= sneed - 1ull;
     uint32_t c[BPT], inc[BPT];
 #pragma unroll
     for (int i = 0; i < BPT; ++i) c[i] = cn[i];
-    if (need) {
-      const uint32_t b0 = (uint32_t)__builtin_ctzll(need) * kRound + tid * BPT;
-#pragma unroll
-      for (int i = 0; i < BPT; ++i) cn[i] = count(b0 + i);
-    }
-    const uint32_t b0 = (uint32_t)j * kRound + tid * BPT;
+    if (sneed) load(__builtin_ctzll(sneed), cn);
+    const uint32_t b0 = (uint32_t)k * LEN + tid * BPT;
+    const bool live = (need >> (b0 / kRound)) & 1ull;
     uint32_t run = 0;
 #pragma unroll
     for (int i = 0; i < BPT; ++i) {
       run += c[i];
       inc[i] = run;  // inclusive prefix inside the thread's bins
       const uint32_t b = b0 + i;
-      if (site_hist) site_hist[s * kBins + b] = c[i];
+      if (live) {
+        if (site_hist) site_hist[s * kBins + b] = c[i];
+        done(b, c[i]);
+      }
       if (b == 0 && zero_counts) zero_counts[s] = c[i];
-      done(b, c[i]);
     }
     uint32_t total;
     // slots and R are double-buffered by scan parity: every scan flips it
     const int64_t r = base + block_exscan_t<NT>(run, slots, nscan, &total);
-    int32_t* R = starts + (nscan & 1) * kRound;
+    int32_t* R = starts + (nscan & 1) * LEN;
     ++nscan;
-    if (total == 0) continue;  // uniform: an empty round
+    if (total == 0) continue;  // uniform: an empty super-round
     const int64_t r0 = base;
     base += total;
 #pragma unroll
     for (int i = 0; i < BPT; ++i)
-      if (c[i] && !(ABL & 4)) atomicAdd(&pooled[b0 + i], (unsigned long long)c[i]);
+      if (c[i] && !(ABL & 4) && pooled) atomicAdd(&pooled[b0 + i], (unsigned long long)c[i]);
     if (ABL & 1) continue;
 #pragma unroll
     for (int i = 0; i < BPT; ++i) R[tid * BPT + i] = (int32_t)(r + inc[i]);
     __syncthreads();  // R visible; the other R buffer is rewritten only after the next scan
-    fill_groups<NT>(R, r0, base, (uint32_t)j * kRound, p, vlh, vec16);
+    fill_groups<NT, LEN>(R, r0, base, (uint32_t)k * LEN, p, vlh, vec16);
   }
 }
 
@@ -795,14 +820,22 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
 // at or above dense_rounds that hold counts; the others are known empty and
 // are not read (a microscopy site touches a handful of the 64).  The mask is
 // zero-maintained like the counts.
+// super-round width of the finalize: 4 rounds (4,096 bins, 16 KB of ranks
+// per buffer) for the 1,024-thread form, 1 for the narrow side-stream form
+template <int NT>
+struct FinSR {
+  static constexpr int value = NT >= 1024 ? 4 : 1;
+};
+
 template <int ABL = 0, int NT = kHistThreads>
 __global__ __launch_bounds__(NT, 8) void k_hist_finalize(
     uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask, int dense_rounds,
     const QPos p, uint32_t* __restrict__ vlh_all,
     unsigned long long* __restrict__ pooled, int n_pooled,
     int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist) {
+  constexpr int SR = FinSR<NT>::value;
   __shared__ uint32_t slots[32];
-  __shared__ int32_t starts[2 * kRound];
+  __shared__ int32_t starts[2 * SR * kRound];
   const int64_t s = blockIdx.x;
   const unsigned long long rm = rmask ? rmask[s] : ~0ull;
   __syncthreads();
@@ -810,14 +843,37 @@ __global__ __launch_bounds__(NT, 8) void k_hist_finalize(
   uint32_t* h = hist + s * (int64_t)kBins;
   // sites spread their pooled-histogram adds over n_pooled copies (fewer
   // same-address atomic collisions); k_pooled_fold sums the copies
-  unsigned long long* pl = pooled + (int64_t)(blockIdx.x % n_pooled) * kBins;
+  unsigned long long* pl = pooled ? pooled + (int64_t)(blockIdx.x % n_pooled) * kBins : nullptr;
   const unsigned long long dense = dense_rounds >= 64 ? ~0ull : ((1ull << dense_rounds) - 1ull);
-  hist_tail_rounds<ABL & 7, NT>(
+  hist_tail_rounds<ABL & 7, NT, SR>(
       dense | rm, [&](uint32_t b) -> uint32_t { return h[b]; },
       [&](uint32_t b, uint32_t c) {
         if (!(ABL & 8) && c) h[b] = 0u;
       },
       s, p, vlh_all, pl, zero_counts, site_hist, slots, starts);
+}
+
+// Pooled histogram of a fused launch's sites without per-site atomics:
+// pooled[b] += sum over the sites of hist[s][b], read only where site s's
+// round mask names b's 1,024-bin round (the other rounds are known empty).
+// Thread = bin, blockIdx.y = a chunk of kColSites sites: coalesced 1 KB rows,
+// one 64-bit atomic per bin and chunk.  Runs before k_hist_finalize, which
+// reads and resets the same counts; on bright sites (45 of 64 rounds in use)
+// this replaced ~30,000 per-site atomics per site in the finalize (1.2 ms of
+// its 2.4 ms at 3,456 sites: profiles/r2/mb_tail_bright_r2y.txt).
+constexpr int kColSites = 128;
+__global__ __launch_bounds__(256) void k_pooled_colsum(const uint32_t* __restrict__ hist,
+                                                       const unsigned long long* __restrict__ rmask,
+                                                       int64_t n_sites,
+                                                       unsigned long long* __restrict__ pooled) {
+  const int b = (int)blockIdx.x * 256 + threadIdx.x;
+  const int round = (int)blockIdx.x >> 2;  // 256 bins per workgroup, 4 workgroups per round
+  const int64_t s0 = (int64_t)blockIdx.y * kColSites;
+  const int64_t s1 = s0 + kColSites < n_sites ? s0 + kColSites : n_sites;
+  unsigned long long t = 0;
+  for (int64_t s = s0; s < s1; ++s)
+    if ((rmask[s] >> round) & 1ull) t += hist[s * kBins + b];
+  if (t) atomicAdd(&pooled[b], t);
 }
 
 // pooled[b] += sum of the copies; copies reset to zero (zero-maintained)
@@ -842,15 +898,23 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
   ProfScope prof(narrow ? "hist_finalize_side" : "hist_finalize", s);
   QPos pp = p;
   pp.tstride = vlh_ld * kOsTile;
+  // with a round mask the pooled histogram is a column sum ahead of the
+  // finalize; without one, the finalize adds into pooled copies, then folded
+  const bool colsum = rmask != nullptr && dense_rounds == 0;
+  if (colsum)
+    hipLaunchKernelGGL(k_pooled_colsum, dim3(kBins / 256, (unsigned)cdiv(n_sites, kColSites)),
+                       dim3(256), 0, s, hist, rmask, n_sites, pooled);
+  unsigned long long* fin_pooled = colsum ? nullptr : pooled_parts;
   if (narrow)
     hipLaunchKernelGGL((k_hist_finalize<0, 256>), dim3((unsigned)n_sites), dim3(256), 0, s, hist,
-                       rmask, dense_rounds, pp, vlh, pooled_parts, n_parts, zero_counts, site_hist);
+                       rmask, dense_rounds, pp, vlh, fin_pooled, n_parts, zero_counts, site_hist);
   else
     hipLaunchKernelGGL((k_hist_finalize<0, kHistThreads>), dim3((unsigned)n_sites),
-                       dim3(kHistThreads), 0, s, hist, rmask, dense_rounds, pp, vlh, pooled_parts,
+                       dim3(kHistThreads), 0, s, hist, rmask, dense_rounds, pp, vlh, fin_pooled,
                        n_parts, zero_counts, site_hist);
-  hipLaunchKernelGGL(k_pooled_fold, dim3(kBins / 256), dim3(256), 0, s, pooled, pooled_parts,
-                     n_parts);
+  if (!colsum)
+    hipLaunchKernelGGL(k_pooled_fold, dim3(kBins / 256), dim3(256), 0, s, pooled, pooled_parts,
+                       n_parts);
   TMH_HIP(hipGetLastError());
 }
 

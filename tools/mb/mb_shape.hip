@@ -6,7 +6,7 @@
 // member m of a team takes the unit's 16-B groups m*NT + tid + i*T*NT, so the
 // chip has n_teams*SPU concurrent site streams instead of G*SPU.  ORDER 0 =
 // units band-major (as production), 1 = site-major.
-// Usage: mb_shape [n_sites=3456] [reps=3]
+// Usage: mb_shape [n_sites=3456] [reps=3] [dist=0 standard|1 bright] [quick=0]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -100,7 +100,9 @@ int main(int argc, char** argv) {
   uint16_t *in, *out;
   CK(hipMalloc(&in, bytes));
   CK(hipMalloc(&out, bytes));
-  launch_synth(in, S, H, W, 12345, 0, 0, 0, 0);
+  const int dist = argc > 3 ? atoi(argv[3]) : 0;
+  const bool quick = argc > 4 && atoi(argv[4]) == 1;  // only the configuration x band sweep
+  launch_synth(in, S, H, W, 12345, 0, 0, dist, 0);
   CK(hipDeviceSynchronize());
   float4 *coef, *mconst2;
   uint32_t* hist;
@@ -169,6 +171,41 @@ int main(int argc, char** argv) {
     time(nm, [&] { fused(std::integral_constant<int, 0>()); });
   }
   nb = kFusedBands;
+  auto fcfg = [&](const char* nm2, auto spu_t, auto nt_t, auto lb_t, int grid) {
+    constexpr int SPU_ = decltype(spu_t)::value, NT_ = decltype(nt_t)::value, LB_ = decltype(lb_t)::value;
+    time(nm2, [&] {
+      CK(hipMemsetAsync(fn, 0, 4, 0));
+      hipLaunchKernelGGL((k_correct_hist<true, false, SPU_, 0, NT_, LB_>), dim3(grid), dim3(NT_), 0, 0,
+                         in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, nullptr, 0ull, 0ull);
+    });
+  };
+  using C8 = std::integral_constant<int, 8>;
+  using C4 = std::integral_constant<int, 4>;
+  using T256 = std::integral_constant<int, 256>;
+  using T512 = std::integral_constant<int, 512>;
+  using T1024 = std::integral_constant<int, 1024>;
+  using L8k = std::integral_constant<int, 8192>;
+  using L16k = std::integral_constant<int, 16384>;
+  using L32k = std::integral_constant<int, 32768>;
+  using C2 = std::integral_constant<int, 2>;
+  for (int b : {16, 8, 4, 2}) {
+    nb = b;
+    snprintf(nm, sizeof nm, "cfg (2,1024,32768) [wide] bands %d", b);
+    fcfg(nm, C2(), T1024(), L32k(), cus);
+    snprintf(nm, sizeof nm, "cfg (4,512,16384) [narrow] bands %d", b);
+    fcfg(nm, C4(), T512(), L16k(), 2 * cus);
+  }
+  nb = kFusedBands;
+  if (quick) {
+    printf("done\n");
+    return 0;
+  }
+  fcfg("cfg (8,512,32768) grid cus", C8(), T512(), L32k(), cus);
+  fcfg("cfg (8,1024,32768) grid cus", C8(), T1024(), L32k(), cus);
+  fcfg("cfg (4,512,16384) grid 2cus [prod]", C4(), T512(), L16k(), 2 * cus);
+  fcfg("cfg (4,256,16384) grid 2cus", C4(), T256(), L16k(), 2 * cus);
+  fcfg("cfg (4,256,8192) grid 4cus [2048 bins]", C4(), T256(), L8k(), 4 * cus);
+  fcfg("cfg (8,1024,32768) grid cus again", C8(), T1024(), L32k(), cus);
   time("fused no hist (ABL 1)", [&] { fused(std::integral_constant<int, 1>()); });
   time("fused no hist, const coef (ABL 3)", [&] { fused(std::integral_constant<int, 3>()); });
   time("fused no flush (ABL 8)", [&] { fused(std::integral_constant<int, 8>()); });
