@@ -866,13 +866,27 @@ __global__ __launch_bounds__(256) void k_pooled_colsum(const uint32_t* __restric
                                                        const unsigned long long* __restrict__ rmask,
                                                        int64_t n_sites,
                                                        unsigned long long* __restrict__ pooled) {
+  static_assert(kColSites <= 256, "one mask per thread");
+  __shared__ uint32_t use[kColSites];  // per site of the chunk: this round holds counts
+  __shared__ int any;
   const int b = (int)blockIdx.x * 256 + threadIdx.x;
   const int round = (int)blockIdx.x >> 2;  // 256 bins per workgroup, 4 workgroups per round
   const int64_t s0 = (int64_t)blockIdx.y * kColSites;
-  const int64_t s1 = s0 + kColSites < n_sites ? s0 + kColSites : n_sites;
+  const int ns = (int)(n_sites - s0 < kColSites ? n_sites - s0 : kColSites);
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
+  if ((int)threadIdx.x < kColSites) {
+    const uint32_t u = (int)threadIdx.x < ns ? (uint32_t)((rmask[s0 + threadIdx.x] >> round) & 1ull) : 0u;
+    use[threadIdx.x] = u;
+    if (u) any = 1;
+  }
+  __syncthreads();
+  if (!any) return;  // uniform: no site of the chunk uses this round
+  const uint32_t* h = hist + s0 * kBins + b;
   unsigned long long t = 0;
-  for (int64_t s = s0; s < s1; ++s)
-    if ((rmask[s] >> round) & 1ull) t += hist[s * kBins + b];
+#pragma unroll 8
+  for (int s = 0; s < ns; ++s)
+    if (use[s]) t += h[(int64_t)s * kBins];
   if (t) atomicAdd(&pooled[b], t);
 }
 
