@@ -275,6 +275,7 @@ struct tmh_corrector {
   DBuf<unsigned int> fix_n;
   DBuf<tmh_window> win;  // per-site alignment windows of the chain pass
   int n_wg = 256;
+  DBuf<int> queues;  // fused pass: per-XCD unit counters (dynamic deal)
   DBuf<double> sums, partial;
   DBuf<uint16_t> stage_in, stage_out;
   DBuf<uint8_t> stage8_in, stage8_out;
@@ -884,6 +885,7 @@ static void corrector_init(tmh_corrector* c, const double* d_mean, const double*
   c->rc.alloc(1);
   c->fix_n.alloc(1, true);
   TMH_HIP(hipDeviceGetAttribute(&c->n_wg, hipDeviceAttributeMultiprocessorCount, c->device));
+  c->queues.alloc(8, true);
   corrector_coeffs(c, d_mean, d_std, c->stream);
 }
 
@@ -1158,7 +1160,7 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         launch_correct_hist(dev_in + c0 * h->npx, dev_out + c0 * h->npx, c->npx, nc, c->coef2.p,
                             c->mconst2.p, fl, c->log_transform, clip_lo, clip_hi,
                             h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0,
-                            c->n_wg, h->fused_cfg, h->wide.p, wide_thresh, s);
+                            c->queues.p, c->n_wg, h->fused_cfg, h->wide.p, wide_thresh, s);
         launch_fix_correct(dev_in + c0 * h->npx, dev_out + c0 * h->npx, 2, c->npx, nc, fl,
                            c->coef64.p, c->rc.p, c->log_transform, clip_lo, clip_hi, s);
         const bool side = k < nch - 1;

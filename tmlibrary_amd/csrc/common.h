@@ -223,7 +223,7 @@ constexpr double kWideFrac = 0.02;
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, const FixList& fl,
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
-                         unsigned long long* rmask, int n_wg, int cfg,
+                         unsigned long long* rmask, int* queues, int n_wg, int cfg,
                          const unsigned long long* wide, unsigned long long wide_thresh,
                          hipStream_t s);
 // illuminati chain (chain_kernels.hip)

@@ -8,21 +8,21 @@
 // their own: HBM traffic is then the algorithmic 2 + 4 B/px per site.
 //
 // Layout of the work: the image is cut into n_bands = 16 pixel bands, and a
-// unit is SPU sites of one band.  Units are dealt out statically (units are
-// equal in size, so there is nothing to balance): workgroup b takes units b,
-// b + G, b + 2G, ... in a band-major sweep, the 8 XCDs two bands apart -- each
-// XCD's L2 holds the coefficients of the band it is on (8 B/px: 2.76 MB per
-// band at 2160x2560) while the site groups stream through.  Measured against
-// the previous per-XCD band queues with work stealing, same-box A/B of the
-// whole job (profiles/r2/ab_fused_sched_r2pqr.jsonl): 13.8 vs 14.3 ms on one
-// box, 14.5 vs 14.7 ms (5 runs each) on another; a sweep with every XCD on
-// the SAME band ran 15.5 ms -- its site streams all sit at one offset.  Each
-// lane loads its 8 pixels' coefficients once per group and applies them to
-// the SPU sites (L2 coefficient traffic 8/SPU B/px).  Each site of the unit
-// histograms its raw pixels into its own LDS slice (values below
-// kLdsBins/SPU; larger values go straight to the global histogram), and at
-// the end of the unit the slices are added to the sites' global histograms
-// with contiguous-lane atomics.
+// unit is SPU sites of one band.  The units form one band-major sweep with
+// the 8 XCDs two bands apart (each XCD's L2 holds the coefficients of the
+// band it is on -- 8 B/px: 2.76 MB per band at 2160x2560 -- while the site
+// groups stream through), dealt from per-XCD counters with stealing.
+// Same-box job A/B (profiles/r2/ab_fused_sched_r2pqr.txt, ab_fused_dyn_r2zd.jsonl):
+// this deal against round 1's per-XCD queues that each owned two whole bands,
+// 13.8 vs 14.3 ms on one box, 14.5 vs 14.7 on another; against the same
+// sweep dealt statically, +0.8% job throughput with one channel and +1.6%
+// with four channels sharing the GPU (a static deal cannot rebalance when
+// kernels co-run); every XCD on the same band ran 15.5 ms.  Each lane loads
+// its 8 pixels' coefficients once per group and applies them to the SPU sites
+// (L2 coefficient traffic 8/SPU B/px).  Each site of the unit histograms its
+// raw pixels into its own LDS slice (values below kLdsBins/SPU; larger values
+// go straight to the global histogram), and at the end of the unit the slices
+// are added to the sites' global histograms with contiguous-lane atomics.
 //
 // Arithmetic (ChannelImage._correct_illumination, tmlib/image.py:599-631), in
 // the log2 domain so 10**t is one v_exp_f32:
@@ -35,7 +35,13 @@
 
 namespace tmh {
 
-constexpr int kFusedBands = 16;  // pixel bands of the static schedule
+constexpr int kFusedBands = 16;  // pixel bands of the unit sweep
+
+__device__ __forceinline__ int xcc_id() {
+  int x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 7;
+}
 
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
@@ -148,7 +154,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
     const float4* __restrict__ coef, const float4* __restrict__ mconst2, FixList fl,
     int clip_lo, int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
-    int n_bands, const unsigned long long* __restrict__ wide,
+    int n_bands, int* __restrict__ queues, const unsigned long long* __restrict__ wide,
     unsigned long long wide_lo, unsigned long long wide_hi) {
   // launch-time selection (launch_correct_hist): this configuration runs only
   // when the Welford pass's count of wide pixel groups is in [wide_lo, wide_hi)
@@ -184,17 +190,33 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
       __builtin_amdgcn_make_buffer_rsrc((void*)coef, 0, (int)(npx * 8), 0x00020000);
   const float4 cc = make_float4(2.5f, 2.4f, 1.1f, 0.9f);
 
-  // Static deal: workgroup b takes units i = b, b + G, b + 2G, ... (G =
-  // gridDim.x, a multiple of 8, so i % 8 is b's XCD).  Unit i is site group
-  // i % n_groups_s of band (i / n_groups_s + 2 * (i % 8)) % n_bands: the
-  // sweep is band-major, with the 8 XCDs two bands apart.
-  int next_i = (int)blockIdx.x;
-  auto grab = [&]() -> int {
-    const int i = next_i;
-    next_i += (int)gridDim.x;
-    if (i >= n_units) return -1;
+  // Unit order: the sweep i = 0, 1, ... is band-major with the 8 XCDs two
+  // bands apart -- unit i is site group i % n_groups_s of band
+  // (i / n_groups_s + 2 * (i % 8)) % n_bands -- and XCD x deals the units
+  // i = x + 8 j from its own counter (queues[x]), stealing from the next
+  // queue once its own is drained.  The next unit is grabbed while the
+  // current one streams.
+  __shared__ int unit_sh;
+  int q = xcc_id(), exhausted = 0;
+  auto unit_of = [&](int i) -> int {
     const int band = (i / n_groups_s + 2 * (i % 8)) % n_bands;
     return band * n_groups_s + i % n_groups_s;
+  };
+  auto grab = [&]() -> int {
+    while (exhausted < 8) {
+      if (tid == 0) unit_sh = atomicAdd(&queues[q], 1);
+      __syncthreads();
+      const int j = __builtin_amdgcn_readfirstlane(unit_sh);
+      __syncthreads();
+      const int i = q + 8 * j;
+      if (i < n_units) {
+        exhausted = 0;
+        return unit_of(i);
+      }
+      q = (q + 1) & 7;  // this queue is drained: steal from the next
+      ++exhausted;
+    }
+    return -1;
   };
   struct Unit {
     int g0, g1, ns;
@@ -347,7 +369,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
 // (sites per unit, threads, LDS bins) of the fused pass, selected per handle
 // (tmh_stats_set_option, TMH_OPT_FUSED_CONFIG) or automatically per launch
 // (kFusedAuto: kFusedNarrow, or kFusedWide when the sites are bright).
-// bands: pixel bands of the static deal -- 8 for the wide configuration, whose
+// bands: pixel bands of the unit sweep -- 8 for the wide configuration, whose
 // 16,384-bin slices flush more counts per unit (fewer, longer units: 17.3 vs
 // 17.95 ms on bright sites, profiles/r2/mb_shape_bright_r2x.txt), 16 otherwise.
 struct FusedCfg {
@@ -370,9 +392,10 @@ static_assert(FusedCfgCheck<0>::ok && FusedCfgCheck<1>::ok && FusedCfgCheck<2>::
 static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                                     const float4* cf4, const float4* mconst2, const FixList& fl,
                                     int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
-                                    unsigned long long* rmask, int n_wg, int cfg,
+                                    unsigned long long* rmask, int* queues, int n_wg, int cfg,
                                     const unsigned long long* wide, unsigned long long wide_lo,
                                     unsigned long long wide_hi, hipStream_t s) {
+  TMH_HIP(hipMemsetAsync(queues, 0, 8 * sizeof(int), s));
 #define TMH_LAUNCH_CH(L_, K_)                                                                    \
   {                                                                                              \
     constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
@@ -380,12 +403,12 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
     if (clip_lo >= 0)                                                                            \
       hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, 0, c.threads, c.lds_bins>), grid,     \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, c.bands, wide, wide_lo,                  \
+                         clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
                          wide_hi);                                                               \
     else                                                                                         \
       hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, 0, c.threads, c.lds_bins>), grid,    \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, c.bands, wide, wide_lo,                  \
+                         clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
                          wide_hi);                                                               \
   }
 #define TMH_LAUNCH_CFG(L_)              \
@@ -415,7 +438,7 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, const FixList& fl,
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
-                         unsigned long long* rmask, int n_wg, int cfg,
+                         unsigned long long* rmask, int* queues, int n_wg, int cfg,
                          const unsigned long long* wide, unsigned long long wide_thresh,
                          hipStream_t s) {
   if (n_sites <= 0) return;
@@ -423,14 +446,14 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
   const float4* cf4 = reinterpret_cast<const float4*>(coef2);
   if (cfg >= 0 || !wide) {
     launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo,
-                            clip_hi, hist, rmask, n_wg, cfg >= 0 ? cfg : kFusedNarrow,
+                            clip_hi, hist, rmask, queues, n_wg, cfg >= 0 ? cfg : kFusedNarrow,
                             nullptr, 0, 0, s);
     return;
   }
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, n_wg, kFusedNarrow, wide, 0, wide_thresh, s);
+                          hist, rmask, queues, n_wg, kFusedNarrow, wide, 0, wide_thresh, s);
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, n_wg, kFusedWide, wide, wide_thresh, ~0ull, s);
+                          hist, rmask, queues, n_wg, kFusedWide, wide, wide_thresh, ~0ull, s);
 }
 
 }  // namespace tmh

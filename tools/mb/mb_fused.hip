@@ -152,7 +152,7 @@ int main(int argc, char** argv) {
     constexpr int ABL = decltype(abl_tag)::value;
     CK(hipMemsetAsync(fn, 0, 4, 0));
     hipLaunchKernelGGL((k_correct_hist<true, false, 4, ABL, 512, 16384>), fg, fb, 0, 0, in, out,
-                       npx, S, coef, mconst2, fl, -1, -1, hist, rmask, kFusedBands,
+                       npx, S, coef, mconst2, fl, -1, -1, hist, rmask, kFusedBands, nullptr,
                        nullptr, 0ull, 0ull);
   };
   time("fused prod (ABL 0)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 0>()); });
@@ -166,7 +166,7 @@ int main(int argc, char** argv) {
   time("fused auto (narrow runs, wide exits)", cb + 8.0 * npx, [&] {
     CK(hipMemsetAsync(fn, 0, 4, 0));
     launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                        cus, kFusedAuto, wide, 1000ull, 0);
+                        nullptr, cus, kFusedAuto, wide, 1000ull, 0);
   });
   for (int cfg = 0; cfg < kFusedConfigs; ++cfg) {
     char nm[64];
@@ -175,7 +175,7 @@ int main(int argc, char** argv) {
     time(nm, cb + 8.0 * npx, [&] {
       CK(hipMemsetAsync(fn, 0, 4, 0));
       launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist,
-                          rmask, cus, cfg,
+                          rmask, nullptr, cus, cfg,
                           nullptr, 0, 0);
     });
   }

@@ -118,7 +118,7 @@ int main(int argc, char** argv) {
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const FixList fl{fe, fn, (unsigned)(((size_t)1 << 23) / 8)};
   launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                      cus, dist == 0 ? kFusedNarrow : kFusedWide, nullptr, 0, 0);
+                      nullptr, cus, dist == 0 ? kFusedNarrow : kFusedWide, nullptr, 0, 0);
   CK(hipDeviceSynchronize());
   {
     std::vector<unsigned long long> rm(S);
