@@ -1,0 +1,120 @@
+// Microbenchmark (development tool, not shipped): the illuminati chain pass
+// (correct -> align -> clip -> scale u8, 3 B/px), per-site shifts as
+// bench.py's extra, with a device checksum of the uint8 output.  (Round 2
+// measured a variant staging SB = 2 / 4 sites per barrier pair: 17.65 / 16.74
+// ms vs 15.36 for one site, identical checksums: profiles/r2/mb_chain_r2zf.txt.)
+// Usage: mb_chain [n_sites=3456] [reps=3]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../tmlibrary_amd/csrc/common.h"
+#include "../../tmlibrary_amd/csrc/chain_kernels.hip"
+#include "../../tmlibrary_amd/csrc/synth_kernels.hip"
+
+#define CK(x)                                                                                  \
+  do {                                                                                         \
+    hipError_t e = (x);                                                                        \
+    if (e != hipSuccess) {                                                                     \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e));        \
+      exit(1);                                                                                 \
+    }                                                                                          \
+  } while (0)
+
+namespace tmh {  // no per-kernel event timing in this tool
+ProfScope::ProfScope(const char* n, hipStream_t s) : name_(n), s_(s), slot_(nullptr) {}
+ProfScope::~ProfScope() {}
+}  // namespace tmh
+
+using namespace tmh;
+
+__global__ void k_sum(const uint8_t* __restrict__ p, int64_t n, unsigned long long* out) {
+  unsigned long long t = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    t += (unsigned long long)p[i] * (unsigned long long)((i % 65521) + 1);
+  atomicAdd(out, t);
+}
+
+int main(int argc, char** argv) {
+  const int64_t S = argc > 1 ? atoll(argv[1]) : 3456;
+  const int reps = argc > 2 ? atoi(argv[2]) : 3;
+  const int H = 2160, W = 2560;
+  const int64_t npx = (int64_t)H * W;
+  uint16_t* in;
+  uint8_t* out;
+  CK(hipMalloc(&in, S * npx * 2));
+  CK(hipMalloc(&out, S * npx));
+  launch_synth(in, S, H, W, 12345, 0, 0, 0, 0);
+  float2* clin;
+  float4* mc2;
+  unsigned long long *fe, *sum;
+  unsigned int* fn;
+  tmh_window* dw;
+  CK(hipMalloc(&clin, npx * 8));
+  CK(hipMalloc(&mc2, 16));
+  CK(hipMalloc(&fe, (size_t)1 << 23));
+  CK(hipMalloc(&fn, 4));
+  CK(hipMalloc(&sum, 8));
+  CK(hipMalloc(&dw, S * sizeof(tmh_window)));
+  {
+    std::vector<float> c(npx * 2);
+    for (int64_t i = 0; i < npx; ++i) {
+      c[2 * i] = 8.3f + 0.1f * (float)((i * 7) % 13) / 13.0f;  // mu * log2(10)
+      c[2 * i + 1] = 1.0f + 0.05f * (float)((i * 5) % 11) / 11.0f;  // mean(std) / std
+    }
+    CK(hipMemcpy(clin, c.data(), npx * 8, hipMemcpyHostToDevice));
+    const float m[4] = {8.2f, 0.0f, 1e-10f, 3.0e38f};  // T huge: nothing flagged
+    CK(hipMemcpy(mc2, m, 16, hipMemcpyHostToDevice));
+    std::vector<tmh_window> w(S);
+    for (int64_t i = 0; i < S; ++i) {
+      const int dy = (int)(i % 7) - 3, dx = (int)(i % 9) - 4;
+      w[i].src_r0 = 3 - dy; w[i].src_c0 = 4 - dx; w[i].dst_r0 = 3; w[i].dst_c0 = 4;
+      w[i].rows = H - 6; w[i].cols = W - 8;
+    }
+    CK(hipMemcpy(dw, w.data(), S * sizeof(tmh_window), hipMemcpyHostToDevice));
+  }
+  const FixList fl{fe, fn, (unsigned)(((size_t)1 << 23) / 8)};
+  const int lo = 110, hi = 4000;
+  const double step = scale_step(lo, hi);
+  const int T = hi - lo - 1;
+  const int64_t parts = 8, per = (S + parts - 1) / parts;
+  const dim3 grid((unsigned)((npx / 8 + 255) / 256), (unsigned)((S + per - 1) / per));
+  const size_t shm = (size_t)((hi - lo + 1 + 15) & ~15);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  auto time = [&](const char* name, auto&& launch) {
+    launch();
+    CK(hipDeviceSynchronize());
+    float tot = 0.f;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(a, 0));
+      launch();
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      tot += ms;
+    }
+    CK(hipMemset(out, 0, S * npx));
+    launch();
+    CK(hipMemset(sum, 0, 8));
+    hipLaunchKernelGGL(k_sum, dim3(4096), dim3(256), 0, 0, out, S * npx, sum);
+    unsigned long long h = 0;
+    CK(hipMemcpy(&h, sum, 8, hipMemcpyDeviceToHost));
+    const double ms = tot / reps, bytes = 3.0 * S * npx;
+    printf("%-30s %8.3f ms %7.1f GB/s %5.1f%%  checksum %llu\n", name, ms, bytes / (ms * 1e-3) / 1e9,
+           100.0 * bytes / (ms * 1e-3) / 8e12, h);
+    fflush(stdout);
+  };
+  for (int r = 0; r < 2; ++r)
+    time("chain (production kernel)", [&] {
+      CK(hipMemsetAsync(fn, 0, 4, 0));
+      hipLaunchKernelGGL((k_chain_u8<true, true>), grid, dim3(256), shm, 0, in, out, H, W, S, per,
+                         clin, mc2, fl, dw, lo, hi, T, step);
+    });
+  printf("done\n");
+  return 0;
+}
