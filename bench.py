@@ -878,7 +878,9 @@ def main():
         if sharded:
             workload = ("illumstats+correct, %d channels x %d sites of %dx%d uint16, each channel's "
                         "sites sharded over %d GPU(s) (%d per GPU), one job per channel on its own "
-                        "stream (configs[2]: full plate 384 wells x 9 sites x 4 channels)"
+                        "stream (configs[2]: full plate 384 wells x 9 sites x 4 channels; the "
+                        "same job is configs[3]: exact 65,536-bin per-site percentile histograms + "
+                        "smoothed IllumstatsContainer apply, 4 channels at 2/4/8 GPUs)"
                         % (CH, S_total, H, W, world, S, ))
         elif CH == 1:
             workload = ("illumstats+correct, 1 channel, %d sites/GPU of %dx%d uint16 "

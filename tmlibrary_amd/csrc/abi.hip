@@ -885,7 +885,7 @@ static void corrector_init(tmh_corrector* c, const double* d_mean, const double*
   c->rc.alloc(1);
   c->fix_n.alloc(1, true);
   TMH_HIP(hipDeviceGetAttribute(&c->n_wg, hipDeviceAttributeMultiprocessorCount, c->device));
-  c->queues.alloc(8, true);
+  c->queues.alloc(kFusedQueueInts, true);
   corrector_coeffs(c, d_mean, d_std, c->stream);
 }
 
@@ -1174,7 +1174,11 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0, 0, nc,
                              h->qp, vlh + (size_t)c0 * kOsTile, ld, h->pooled.p, h->pooled_parts.p,
                              kPooledParts, h->zeros.p + c0, sh ? sh + (size_t)c0 * kBins : nullptr,
-                             side ? h->side : s, side);
+                             side ? h->side : s, side,
+                             // the launch-wide round union is rewritten by the
+                             // next chunk's fused launch: one chunk only
+                             nch == 1 ? reinterpret_cast<const unsigned long long*>(c->queues.p + 8)
+                                      : nullptr);
       }
       if (!(h->flags & TMH_STATS_DEFERRED_PCT))
         launch_pct_accumulate(vlh, n_sites, ld, h->Q, h->gamma.p, h->acc.p, s);

@@ -163,7 +163,8 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
                           int64_t n_sites, const QPos& p, uint32_t* vlh, int64_t vlh_ld,
                           unsigned long long* pooled,
                           unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
-                          uint32_t* site_hist, hipStream_t s, bool narrow = false);
+                          uint32_t* site_hist, hipStream_t s, bool narrow = false,
+                          const unsigned long long* rm_all = nullptr);
 void launch_pct_accumulate(const uint32_t* vlh, int64_t n_sites, int64_t vlh_ld, int Q,
                            const double* gamma, double* acc, hipStream_t s);
 // quantiles [q_begin, q_begin + q_count) only; acc points at the range
@@ -216,6 +217,7 @@ void launch_correct_u8(const uint8_t* in, uint8_t* out, int64_t npx, int64_t n_s
 // single site per unit keeps too few loads in flight, and 231 ms narrow:
 // profiles/r2/mb_fused_bright_r2f.txt).
 constexpr int kFusedConfigs = 5;
+constexpr int kFusedQueueInts = 16;  // fused pass scratch: 8 unit counters + 64-bit round union
 constexpr int kFusedAuto = -1;
 constexpr int kFusedNarrow = 3;
 constexpr int kFusedWide = 0;

@@ -59,9 +59,9 @@ constexpr float kCastTop = 2147418112.0f;
 // their one-pass hazard.  A zero pixel takes log2(zf), zf = 10**zero_log10 as
 // f32 (1e-10f: v_log_f32 is within 1 ulp of the reference's log10(1e-10) =
 // -10, scaled): one v_max instead of a compare + select.  The caller keeps zf
-// in [FLT_MIN, 1].  Returns the mask of the pixels whose f32 result reaches
-// T (mconst2.w, the f32 error bound's limit): the caller flags them for the
-// f64 refinement (common.h) -- rare, saturated pixels in dim corners.
+// in [FLT_MIN, 1].  Returns the mask of the pixels whose f32 result may be
+// more than 1 DN off (their own error bound, below): the caller flags them for
+// the f64 refinement (common.h) -- rare, saturated pixels in dim corners.
 template <bool LOG, bool CLIP>
 __device__ __forceinline__ uint32_t fcorrect8(const uint32_t (&w)[4], const float4 (&k)[4],
                                               float mh, float zf, float T, uint32_t clip_lo2,
@@ -90,13 +90,29 @@ __device__ __forceinline__ uint32_t fcorrect8(const uint32_t (&w)[4], const floa
     o[2 * p] = LOG ? __builtin_amdgcn_exp2f(t[p].x) : t[p].x;  // v_exp_f32
     o[2 * p + 1] = LOG ? __builtin_amdgcn_exp2f(t[p].y) : t[p].y;
   }
-  float mx = __builtin_fabsf(o[0]);  // one compare per 8 pixels; the mask only if needed
+  // the pixel's own f32 error bound (common.h): |o| (K1 a + K2) < 1 keeps the
+  // truncated value within 1 DN of the f64 one; K1, K2 carry a 0.2% margin
+  // for the f32 evaluation of the bound itself.  (The launch-wide threshold T
+  // = 1 / (K1 a_max + K2) flagged every bright pixel of an image with one
+  // low-variance pixel; the per-pixel bound flags only the pixels that need
+  // it.)  One compare per 8 pixels; the mask only if needed.
+  (void)T;
+  constexpr float K1 = (float)(kRefineK1 * 1.002), K2 = (float)(kRefineK2 * 1.002);
+  float e[8];
 #pragma unroll
-  for (int j = 1; j < 8; ++j) mx = __builtin_fmaxf(mx, __builtin_fabsf(o[j]));
-  uint32_t far = 0;  // pixels beyond the f32 bound
-  if (mx >= T) {
+  for (int p = 0; p < 4; ++p) {
+    const f32x2_t b = __builtin_elementwise_fma((f32x2_t){k[p].z, k[p].w}, (f32x2_t){K1, K1},
+                                                (f32x2_t){K2, K2});
+    e[2 * p] = __builtin_fabsf(o[2 * p]) * b.x;
+    e[2 * p + 1] = __builtin_fabsf(o[2 * p + 1]) * b.y;
+  }
+  float mx = e[0];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) far |= (__builtin_fabsf(o[j]) >= T ? 1u : 0u) << j;
+  for (int j = 1; j < 8; ++j) mx = __builtin_fmaxf(mx, e[j]);
+  uint32_t far = 0;  // pixels beyond their f32 bound
+  if (mx >= 0.998f) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) far |= (e[j] >= 0.998f ? 1u : 0u) << j;
   }
   int32_t iv[8];
 #pragma unroll
@@ -359,7 +375,10 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     // this one is not touched again before the next unit's first barrier
     if (tid < un.ns) {
       const unsigned long long r = rm[tid];
-      if (r) atomicOr(&rmask[un.s0 + tid], r);
+      if (r) {
+        atomicOr(&rmask[un.s0 + tid], r);
+        atomicOr(reinterpret_cast<unsigned long long*>(queues + 8), r);  // launch-wide union
+      }
       rm[tid] = 0ull;
     }
     par ^= 1;
@@ -395,7 +414,6 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
                                     unsigned long long* rmask, int* queues, int n_wg, int cfg,
                                     const unsigned long long* wide, unsigned long long wide_lo,
                                     unsigned long long wide_hi, hipStream_t s) {
-  TMH_HIP(hipMemsetAsync(queues, 0, 8 * sizeof(int), s));
 #define TMH_LAUNCH_CH(L_, K_)                                                                    \
   {                                                                                              \
     constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
@@ -443,6 +461,11 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
                          hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("correct_hist", s);
+  // queues[0..8): per-XCD unit counters; queues[8..10): the union of the
+  // sites' round masks (read by the pooled column sum).  Zeroed once for both
+  // configurations of an automatic launch: the one that does not run exits
+  // before touching either.
+  TMH_HIP(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), s));
   const float4* cf4 = reinterpret_cast<const float4*>(coef2);
   if (cfg >= 0 || !wide) {
     launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo,

@@ -861,9 +861,10 @@ __global__ __launch_bounds__(NT, 8) void k_hist_finalize(
 // reads and resets the same counts; on bright sites (45 of 64 rounds in use)
 // this replaced ~30,000 per-site atomics per site in the finalize (1.2 ms of
 // its 2.4 ms at 3,456 sites: profiles/r2/mb_tail_bright_r2y.txt).
-constexpr int kColSites = 128;
+constexpr int kColSites = 32;
 __global__ __launch_bounds__(256) void k_pooled_colsum(const uint32_t* __restrict__ hist,
                                                        const unsigned long long* __restrict__ rmask,
+                                                       const unsigned long long* __restrict__ rm_all,
                                                        int64_t n_sites,
                                                        unsigned long long* __restrict__ pooled) {
   static_assert(kColSites <= 256, "one mask per thread");
@@ -871,6 +872,8 @@ __global__ __launch_bounds__(256) void k_pooled_colsum(const uint32_t* __restric
   __shared__ int any;
   const int b = (int)blockIdx.x * 256 + threadIdx.x;
   const int round = (int)blockIdx.x >> 2;  // 256 bins per workgroup, 4 workgroups per round
+  // rounds no site of the launch uses (the fused pass's union of the masks)
+  if (rm_all && !((*rm_all >> round) & 1ull)) return;
   const int64_t s0 = (int64_t)blockIdx.y * kColSites;
   const int ns = (int)(n_sites - s0 < kColSites ? n_sites - s0 : kColSites);
   if (threadIdx.x == 0) any = 0;
@@ -884,7 +887,7 @@ __global__ __launch_bounds__(256) void k_pooled_colsum(const uint32_t* __restric
   if (!any) return;  // uniform: no site of the chunk uses this round
   const uint32_t* h = hist + s0 * kBins + b;
   unsigned long long t = 0;
-#pragma unroll 8
+#pragma unroll 16
   for (int s = 0; s < ns; ++s)
     if (use[s]) t += h[(int64_t)s * kBins];
   if (t) atomicAdd(&pooled[b], t);
@@ -907,7 +910,8 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
                           int64_t n_sites, const QPos& p, uint32_t* vlh, int64_t vlh_ld,
                           unsigned long long* pooled,
                           unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
-                          uint32_t* site_hist, hipStream_t s, bool narrow) {
+                          uint32_t* site_hist, hipStream_t s, bool narrow,
+                          const unsigned long long* rm_all) {
   if (n_sites <= 0) return;
   ProfScope prof(narrow ? "hist_finalize_side" : "hist_finalize", s);
   QPos pp = p;
@@ -917,7 +921,7 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
   const bool colsum = rmask != nullptr && dense_rounds == 0;
   if (colsum)
     hipLaunchKernelGGL(k_pooled_colsum, dim3(kBins / 256, (unsigned)cdiv(n_sites, kColSites)),
-                       dim3(256), 0, s, hist, rmask, n_sites, pooled);
+                       dim3(256), 0, s, hist, rmask, rm_all, n_sites, pooled);
   unsigned long long* fin_pooled = colsum ? nullptr : pooled_parts;
   if (narrow)
     hipLaunchKernelGGL((k_hist_finalize<0, 256>), dim3((unsigned)n_sites), dim3(256), 0, s, hist,
