@@ -332,3 +332,90 @@ def test_fused_multi_job_configs(L, cfg):
     L.tmh_stats_destroy(h)
     for b in planes + [d_in, d_out]:
         b.free()
+
+
+def _groups_ge(sites, v):
+    """8-pixel groups (row-major, per site) holding a value >= v."""
+    g = sites.reshape(sites.shape[0], -1, 8)
+    return int(np.count_nonzero((g >= v).any(axis=2)))
+
+
+@pytest.mark.parametrize("cfg", [-1, 3])
+def test_very_wide_jobs(L, cfg):
+    """Very wide sites (a third or more of the 8-pixel groups hold a value
+    >= 16,384): with the automatic configuration the fused pass runs without
+    its histogram and k_hist_site_u16 builds the exact per-site histograms in
+    LDS as u16 pairs from one more read of the sites.  Job 0 is uniform
+    0..65535; job 1 adds a value held by more than 65,535 pixels of one site
+    (the u16 half wraps: the carry is undone and the count finishes in the
+    global slab) and the extremes 0 / 65535.  cfg 3 forces the narrow slices
+    (every value >= 4,096 by global atomics) on the same jobs.  Histograms,
+    order statistics and percentile sums bit-exact, mean/std 1e-6, corrected
+    values within 1 DN of the oracle (stats.py:64-121, image.py:599-631)."""
+    import torch
+
+    from tmlibrary_amd import hip, synth
+    from tmlibrary_amd.image import ZERO_LOG10
+    H, W, n = 288, 320, 6  # 92,160 pixels per site: room for a 70,000-pixel value
+    npx = H * W
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    sp = C.c_void_p(stream.cuda_stream)
+    h = _stats_handle(L, H, W, hip.TMH_STATS_KEEP_SITE_HIST)
+    hip.check(L.tmh_stats_set_option(h, hip.TMH_OPT_FUSED_CONFIG, cfg))
+    hip.check(L.tmh_stats_set_stream(h, sp))
+    d_in, d_out = Dev(L, n * npx * 2), Dev(L, n * npx * 2)
+    planes = [Dev(L, npx * 8) for _ in range(5)]
+    mean, std, smean, sstd, tmp = planes
+    c = C.c_void_p()
+    L.tmh_synchronize(None)
+    hip.check(L.tmh_corrector_create_device(mean.p, std.p, H, W, 1, ZERO_LOG10, sp, C.byref(c)))
+    L.tmh_synchronize(None)
+    for k in range(2):
+        sites = np.stack([synth.synth_exact_host(H, W, 91 + k, 1, i, synth.UNIFORM)
+                          for i in range(n)])
+        if k == 1:
+            sites[2].reshape(-1)[:70000] = 30000  # one bin beyond 65,535 pixels
+            sites[3].reshape(-1)[:5] = 0
+            sites[4].reshape(-1)[-7:] = 65535
+        d_in.put(sites)
+        hip.check(L.tmh_stats_reset(h))
+        hip.check(L.tmh_stats_update_welford_device(h, d_in.p, n, 1, sp))
+        hip.check(L.tmh_stats_finalize_device(h, mean.p, std.p, sp))
+        hip.check(L.tmh_smooth_f64_device(mean.p, smean.p, tmp.p, H, W, 5.0, sp))
+        hip.check(L.tmh_smooth_f64_device(std.p, sstd.p, tmp.p, H, W, 5.0, sp))
+        hip.check(L.tmh_corrector_update_device(c, smean.p, sstd.p, sp))
+        assert _groups_ge(sites, 16384) >= 0.33 * n * npx // 8  # very wide
+        hip.check(L.tmh_correct_u16_hist_device(c, h, d_in.p, d_out.p, n, -1, -1, sp))
+        r = _results(L, h, H, W, n)
+        ref = orc.run_illumstats(list(sites))
+        assert r["n"] == n
+        assert_close_rel(r["mean"], ref.mean)
+        assert_close_rel(r["std"], ref.std)
+        assert np.array_equal(r["hist"], sum(orc.histogram_u16(s) for s in sites)), (cfg, k)
+        assert np.array_equal(r["acc"], ref.percentile_sums), (cfg, k)
+        for i in range(n):
+            sh = np.empty(65536, np.uint32)
+            hip.check(L.tmh_stats_site_histogram(h, i, hip.ptr(sh)))
+            assert np.array_equal(sh.astype(np.uint64), orc.histogram_u16(sites[i])), (cfg, k, i)
+        check_order_stats([sites[i] for i in (0, 2)], site_order_stats(L, h, (0, 2), 100000))
+        out = d_out.get(np.uint16, sites.shape)
+        sm_ref, ss_ref = orc.smooth_reflect(ref.mean, 5), orc.smooth_reflect(ref.std, 5)
+        for i in (0, 2, n - 1):
+            worst, flips, _ = dn_report(out[i], orc.correct_illumination(sites[i], sm_ref, ss_ref))
+            assert worst <= 1 and flips == 0, (cfg, k, i, worst, flips)
+    # the slab is zero-maintained: a third job on the same handle starts clean
+    sites = np.stack([synth.synth_exact_host(H, W, 99, 1, i, synth.STANDARD) for i in range(n)])
+    d_in.put(sites)
+    hip.check(L.tmh_stats_reset(h))
+    hip.check(L.tmh_stats_update_welford_device(h, d_in.p, n, 1, sp))
+    hip.check(L.tmh_stats_finalize_device(h, mean.p, std.p, sp))
+    hip.check(L.tmh_corrector_update_device(c, mean.p, std.p, sp))
+    hip.check(L.tmh_correct_u16_hist_device(c, h, d_in.p, d_out.p, n, -1, -1, sp))
+    r = _results(L, h, H, W, n)
+    assert np.array_equal(r["hist"], sum(orc.histogram_u16(s) for s in sites))
+    assert np.array_equal(r["acc"], orc.run_illumstats(list(sites)).percentile_sums)
+    L.tmh_corrector_destroy(c)
+    L.tmh_stats_destroy(h)
+    for b in planes + [d_in, d_out]:
+        b.free()

@@ -242,7 +242,7 @@ struct tmh_stats {
   int64_t n_deferred = 0;     // sites whose order statistics are stored
   int64_t last_batch = 0;
   int64_t pending = 0;        // Welford-updated sites whose histograms are still to come
-  DBuf<unsigned long long> wide;  // pixel groups with a value >= 4,096 in the pending sites
+  DBuf<unsigned long long> wide;  // pixel groups with a value >= 4,096 / >= 16,384 in the pending sites
   int64_t wide_sites = 0;         // sites that count covers
   bool pct_sum_external = false;
   DBuf<double> mean, m2, lut_log, gamma, acc, tmp_mean, tmp_std, rn;
@@ -393,7 +393,7 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
       h->mean.alloc(npx, true);
       h->m2.alloc(npx, true);
       h->wf_part.alloc((size_t)8 * npx);
-      h->wide.alloc(1, true);
+      h->wide.alloc(2, true);  // groups with a value >= 4,096 / >= 16,384
       h->acc.alloc(n_quantiles, true);
       h->pooled.alloc(kBins, true);
       h->lut_log.alloc(kBins);
@@ -491,7 +491,7 @@ int tmh_stats_reset(tmh_stats* h) {
     TMH_HIP(hipMemsetAsync(h->m2.p, 0, h->npx * 8, h->stream));
     TMH_HIP(hipMemsetAsync(h->acc.p, 0, (size_t)h->Q * 8, h->stream));
     TMH_HIP(hipMemsetAsync(h->pooled.p, 0, (size_t)kBins * 8, h->stream));
-    TMH_HIP(hipMemsetAsync(h->wide.p, 0, 8, h->stream));
+    TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, h->stream));
     h->wide_sites = 0;
     h->n = 0;
     h->n_deferred = 0;
@@ -1150,6 +1150,13 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       // overflow the narrow slices (their values then take global atomics)
       const unsigned long long wide_thresh = (unsigned long long)std::max<double>(
           1.0, kWideFrac * (double)h->wide_sites * (double)(h->npx >> 3));
+      // very wide sites: histograms from k_hist_site_u16 instead (automatic
+      // configuration only; ~0 = never)
+      const bool autocfg = h->fused_cfg == kFusedAuto;
+      const unsigned long long xwide_thresh =
+          autocfg ? (unsigned long long)std::max<double>(
+                        1.0, kXWideFrac * (double)h->wide_sites * (double)(h->npx >> 3))
+                  : ~0ull;
       if (nch > 1) {
         TMH_HIP(hipEventRecord(h->ev_fork, s));
         TMH_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
@@ -1160,10 +1167,12 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
         launch_correct_hist(dev_in + c0 * h->npx, dev_out + c0 * h->npx, c->npx, nc, c->coef2.p,
                             c->mconst2.p, fl, c->log_transform, clip_lo, clip_hi,
                             h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0,
-                            c->queues.p, c->n_wg, h->fused_cfg, h->wide.p, wide_thresh, s);
+                            c->queues.p, c->n_wg, h->fused_cfg, h->wide.p, wide_thresh,
+                            xwide_thresh, s);
         launch_fix_correct(dev_in + c0 * h->npx, dev_out + c0 * h->npx, 2, c->npx, nc, fl,
                            c->coef64.p, c->rc.p, c->log_transform, clip_lo, clip_hi, s);
         const bool side = k < nch - 1;
+        hipStream_t fs = side ? h->side : s;
         if (side) {
           TMH_HIP(hipEventRecord(h->ev_fork, s));
           TMH_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
@@ -1171,14 +1180,20 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
           TMH_HIP(hipEventRecord(h->ev_join, h->side));
           TMH_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
         }
+        if (autocfg)  // exits at once unless the launch is very wide
+          launch_hist_site_u16(dev_in + c0 * h->npx, h->npx, nc, h->hist_full.p + (size_t)c0 * kBins,
+                               h->qp, vlh + (size_t)c0 * kOsTile, ld, h->pooled.p,
+                               h->pooled_parts.p, kPooledParts, h->zeros.p + c0,
+                               sh ? sh + (size_t)c0 * kBins : nullptr, h->wide.p, xwide_thresh, fs);
         launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0, 0, nc,
                              h->qp, vlh + (size_t)c0 * kOsTile, ld, h->pooled.p, h->pooled_parts.p,
                              kPooledParts, h->zeros.p + c0, sh ? sh + (size_t)c0 * kBins : nullptr,
-                             side ? h->side : s, side,
+                             fs, side,
                              // the launch-wide round union is rewritten by the
                              // next chunk's fused launch: one chunk only
                              nch == 1 ? reinterpret_cast<const unsigned long long*>(c->queues.p + 8)
-                                      : nullptr);
+                                      : nullptr,
+                             h->wide.p, xwide_thresh);
       }
       if (!(h->flags & TMH_STATS_DEFERRED_PCT))
         launch_pct_accumulate(vlh, n_sites, ld, h->Q, h->gamma.p, h->acc.p, s);
@@ -1186,8 +1201,8 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       if (h->flags & TMH_STATS_DEFERRED_PCT) h->n_deferred += n_sites;
       h->last_batch = n_sites;
       h->pending -= n_sites;
-      if (h->pending == 0) {  // the wide count restarts with the next Welford batch
-        TMH_HIP(hipMemsetAsync(h->wide.p, 0, 8, s));
+      if (h->pending == 0) {  // the wide counts restart with the next Welford batch
+        TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, s));
         h->wide_sites = 0;
       }
       if (cross) {
@@ -1240,7 +1255,7 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       h->pending -= nc;
     }
     if (h->pending == 0 && h->wide_sites) {
-      TMH_HIP(hipMemsetAsync(h->wide.p, 0, 8, s));
+      TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, s));
       h->wide_sites = 0;
     }
     if (cross) {

@@ -164,7 +164,15 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
                           unsigned long long* pooled,
                           unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
                           uint32_t* site_hist, hipStream_t s, bool narrow = false,
-                          const unsigned long long* rm_all = nullptr);
+                          const unsigned long long* rm_all = nullptr,
+                          const unsigned long long* wide = nullptr, unsigned long long xthr = 0);
+// very wide launches (wide[1] >= xthr): the exact per-site histogram in LDS
+// as u16 pairs from one more read of the sites, scanned into order statistics
+void launch_hist_site_u16(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* slab,
+                          const QPos& p, uint32_t* vlh, int64_t vlh_ld,
+                          unsigned long long* pooled, unsigned long long* pooled_parts,
+                          int n_parts, int64_t* zero_counts, uint32_t* site_hist,
+                          const unsigned long long* wide, unsigned long long xthr, hipStream_t s);
 void launch_pct_accumulate(const uint32_t* vlh, int64_t n_sites, int64_t vlh_ld, int Q,
                            const double* gamma, double* acc, hipStream_t s);
 // quantiles [q_begin, q_begin + q_count) only; acc points at the range
@@ -222,12 +230,17 @@ constexpr int kFusedAuto = -1;
 constexpr int kFusedNarrow = 3;
 constexpr int kFusedWide = 0;
 constexpr double kWideFrac = 0.02;
+// very wide: a third of the 8-pixel groups hold a value >= 16,384 (~5% of the
+// pixels beyond the wide configuration's slices: from there its global atomics
+// cost more than one more read of the sites); the fused pass then runs without
+// its histogram and k_hist_site_u16 builds the histograms
+constexpr double kXWideFrac = 0.33;
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, const FixList& fl,
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
                          unsigned long long* rmask, int* queues, int n_wg, int cfg,
                          const unsigned long long* wide, unsigned long long wide_thresh,
-                         hipStream_t s);
+                         unsigned long long xwide_thresh, hipStream_t s);
 // illuminati chain (chain_kernels.hip)
 void launch_align(const void* in, void* out, int elem_bytes, int64_t n_sites, int H, int W, int oh,
                   int ow, const tmh_window* d_win, hipStream_t s);

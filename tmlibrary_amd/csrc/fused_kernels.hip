@@ -171,12 +171,15 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     const float4* __restrict__ coef, const float4* __restrict__ mconst2, FixList fl,
     int clip_lo, int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
     int n_bands, int* __restrict__ queues, const unsigned long long* __restrict__ wide,
-    unsigned long long wide_lo, unsigned long long wide_hi) {
+    unsigned long long wide_lo, unsigned long long wide_hi, unsigned long long x_lo,
+    unsigned long long x_hi) {
   // launch-time selection (launch_correct_hist): this configuration runs only
-  // when the Welford pass's count of wide pixel groups is in [wide_lo, wide_hi)
+  // when the Welford pass's counts of pixel groups with a value >= 4,096 and
+  // >= 16,384 are in [wide_lo, wide_hi) and [x_lo, x_hi)
   if (wide) {
     const unsigned long long w = __builtin_nontemporal_load(wide);
-    if (w < wide_lo || w >= wide_hi) return;
+    const unsigned long long x = __builtin_nontemporal_load(wide + 1);
+    if (w < wide_lo || w >= wide_hi || x < x_lo || x >= x_hi) return;
   }
   constexpr int BINS = LB / SPU;
   constexpr int SLICE = BINS + 1;
@@ -408,34 +411,39 @@ struct FusedCfgCheck {
 static_assert(FusedCfgCheck<0>::ok && FusedCfgCheck<1>::ok && FusedCfgCheck<2>::ok &&
               FusedCfgCheck<3>::ok && FusedCfgCheck<4>::ok, "");
 
+// cfg kFusedNoHist: the narrow shape without its histogram (very wide sites:
+// k_hist_site_u16 builds the histograms)
+constexpr int kFusedNoHist = 100;
 static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                                     const float4* cf4, const float4* mconst2, const FixList& fl,
                                     int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
                                     unsigned long long* rmask, int* queues, int n_wg, int cfg,
                                     const unsigned long long* wide, unsigned long long wide_lo,
-                                    unsigned long long wide_hi, hipStream_t s) {
-#define TMH_LAUNCH_CH(L_, K_)                                                                    \
+                                    unsigned long long wide_hi, unsigned long long x_lo,
+                                    unsigned long long x_hi, hipStream_t s) {
+#define TMH_LAUNCH_CH(L_, K_, A_)                                                                \
   {                                                                                              \
     constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
     const dim3 grid(n_wg * (1024 / c.threads));                                                  \
     if (clip_lo >= 0)                                                                            \
-      hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, 0, c.threads, c.lds_bins>), grid,     \
+      hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, A_, c.threads, c.lds_bins>), grid,    \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
                          clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
-                         wide_hi);                                                               \
+                         wide_hi, x_lo, x_hi);                                                   \
     else                                                                                         \
-      hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, 0, c.threads, c.lds_bins>), grid,    \
+      hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, A_, c.threads, c.lds_bins>), grid,   \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
                          clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
-                         wide_hi);                                                               \
+                         wide_hi, x_lo, x_hi);                                                   \
   }
-#define TMH_LAUNCH_CFG(L_)              \
-  switch (cfg) {                        \
-    case 0: TMH_LAUNCH_CH(L_, 0) break; \
-    case 1: TMH_LAUNCH_CH(L_, 1) break; \
-    case 2: TMH_LAUNCH_CH(L_, 2) break; \
-    case 3: TMH_LAUNCH_CH(L_, 3) break; \
-    default: TMH_LAUNCH_CH(L_, 4) break; \
+#define TMH_LAUNCH_CFG(L_)                                     \
+  switch (cfg) {                                               \
+    case 0: TMH_LAUNCH_CH(L_, 0, 0) break;                     \
+    case 1: TMH_LAUNCH_CH(L_, 1, 0) break;                     \
+    case 2: TMH_LAUNCH_CH(L_, 2, 0) break;                     \
+    case 3: TMH_LAUNCH_CH(L_, 3, 0) break;                     \
+    case kFusedNoHist: TMH_LAUNCH_CH(L_, kFusedNarrow, 1) break; \
+    default: TMH_LAUNCH_CH(L_, 4, 0) break;                    \
   }
   if (log_transform) {
     TMH_LAUNCH_CFG(true);
@@ -458,7 +466,7 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
                          unsigned long long* rmask, int* queues, int n_wg, int cfg,
                          const unsigned long long* wide, unsigned long long wide_thresh,
-                         hipStream_t s) {
+                         unsigned long long xwide_thresh, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("correct_hist", s);
   // queues[0..8): per-XCD unit counters; queues[8..10): the union of the
@@ -470,13 +478,16 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
   if (cfg >= 0 || !wide) {
     launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo,
                             clip_hi, hist, rmask, queues, n_wg, cfg >= 0 ? cfg : kFusedNarrow,
-                            nullptr, 0, 0, s);
+                            nullptr, 0, 0, 0, 0, s);
     return;
   }
+  const unsigned long long X = xwide_thresh;
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedNarrow, wide, 0, wide_thresh, s);
+                          hist, rmask, queues, n_wg, kFusedNarrow, wide, 0, wide_thresh, 0, X, s);
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedWide, wide, wide_thresh, ~0ull, s);
+                          hist, rmask, queues, n_wg, kFusedWide, wide, wide_thresh, ~0ull, 0, X, s);
+  launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
+                          hist, rmask, queues, n_wg, kFusedNoHist, wide, 0, ~0ull, X, ~0ull, s);
 }
 
 }  // namespace tmh

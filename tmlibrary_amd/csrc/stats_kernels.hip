@@ -118,20 +118,23 @@ __global__ void k_rn_table(double* __restrict__ rn, int64_t n0, int64_t n) {
 // Stats transform of eight pixels: LDS LUT gather of each value's low 12
 // bits (no clamp: the index stays in the table), then -- only when a word has
 // a value >= 4,096 -- those slots recomputed with log10_big (wc counts such
-// groups: the fused pass picks its LDS slice width from it).  The inner loop is VALU-issue bound (3 f64 ops per
+// groups, xc the groups with a value >= 16,384: the fused pass picks its
+// histogram configuration from them).  The inner loop is VALU-issue bound (3 f64 ops per
 // pixel), so the integer work per pixel is kept to the gather address.
 template <bool LOG, int INV>
 __device__ __forceinline__ void xform8(const uint4 v, const double* slut, const double* sinv,
-                                       double (&x)[8], uint32_t& wc) {
+                                       double (&x)[8], uint32_t& wc, uint32_t& xc) {
   const uint32_t u[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
                          v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
-  const bool wide = ((v.x | v.y | v.z | v.w) & 0xF000F000u) != 0;
+  const uint32_t any = v.x | v.y | v.z | v.w;
+  const bool wide = (any & 0xF000F000u) != 0;
   if (LOG) {
     constexpr uint32_t kIdx = kWfLut - 1;
 #pragma unroll
     for (int k = 0; k < 8; ++k) x[k] = slut[u[k] & kIdx];
     if (wide) {
       ++wc;
+      xc += (any & 0xC000C000u) ? 1u : 0u;  // a value >= 16,384
       // per pixel: on standard data ~7 % of wave-steps have one lane with
       // one such value, and a branch-free pass over all eight cost 0.2 ms
 #pragma unroll
@@ -140,6 +143,7 @@ __device__ __forceinline__ void xform8(const uint4 v, const double* slut, const 
     }
   } else {
     wc += wide ? 1u : 0u;
+    xc += (any & 0xC000C000u) ? 1u : 0u;
 #pragma unroll
     for (int k = 0; k < 8; ++k) x[k] = (double)u[k];
   }
@@ -180,9 +184,9 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
     const double* __restrict__ lut, double* __restrict__ part,
     unsigned long long* __restrict__ wide) {
   __shared__ double slut[kWfLut], sinv[INV == 1 ? kWfLut : 1];
-  __shared__ uint32_t wide_sh;
+  __shared__ uint32_t wide_sh[2];
   if (LOG) fill_wf_tables<INV>(lut, slut, sinv, NT);
-  if (threadIdx.x == 0) wide_sh = 0u;
+  if (threadIdx.x < 2) wide_sh[threadIdx.x] = 0u;
   __syncthreads();
   const int64_t ngroups = npx >> 3;
   const int64_t g = (int64_t)blockIdx.x * NT + threadIdx.x;
@@ -198,9 +202,9 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
 #pragma unroll
   for (int k = 0; k < kWfGroup; ++k) cur[k] = ld_site<NTL>(src + (k < last ? k : last) * ngroups);
   double K[8], s1[8], s2[8];
-  uint32_t wc = 0;  // this thread's wide groups (value >= 4,096) over its sites
-  xform8<LOG, INV>(cur[0], slut, sinv, K, wc);
-  wc = 0;
+  uint32_t wc = 0, xc = 0;  // this thread's groups with a value >= 4,096 / >= 16,384
+  xform8<LOG, INV>(cur[0], slut, sinv, K, wc, xc);
+  wc = xc = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.0;
   // 32-bit site counters: the per-site bounds test is then one scalar compare
@@ -217,7 +221,7 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
     for (int k = 0; k < kWfGroup; ++k) {
       if (s + k < ns) {
         double x[8];
-        xform8<LOG, INV>(cur[k], slut, sinv, x, wc);
+        xform8<LOG, INV>(cur[k], slut, sinv, x, wc, xc);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const double d = x[j] - K[j];
@@ -230,10 +234,12 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
     for (int k = 0; k < kWfGroup; ++k) cur[k] = nxt[k];
   }
 
-  if (wide) {  // one global add per workgroup (thread 0's group always exists)
-    if (wc) atomicAdd(&wide_sh, wc);
+  if (wide) {  // one global add per counter and workgroup (thread 0's group always exists)
+    if (wc) atomicAdd(&wide_sh[0], wc);
+    if (xc) atomicAdd(&wide_sh[1], xc);
     __syncthreads();
-    if (threadIdx.x == 0 && wide_sh) atomicAdd(wide, (unsigned long long)wide_sh);
+    if (threadIdx.x == 0 && wide_sh[0]) atomicAdd(wide, (unsigned long long)wide_sh[0]);
+    if (threadIdx.x == 0 && wide_sh[1]) atomicAdd(wide + 1, (unsigned long long)wide_sh[1]);
   }
 
   if (gridDim.y > 1) {  // partial (mean_l, M2_l) of this part
@@ -832,7 +838,10 @@ __global__ __launch_bounds__(NT, 8) void k_hist_finalize(
     uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask, int dense_rounds,
     const QPos p, uint32_t* __restrict__ vlh_all,
     unsigned long long* __restrict__ pooled, int n_pooled,
-    int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist) {
+    int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist,
+    const unsigned long long* __restrict__ wide = nullptr, unsigned long long xthr = 0) {
+  // a very wide launch: k_hist_site_u16 has written this site's outputs
+  if (wide && __builtin_nontemporal_load(wide + 1) >= xthr) return;
   constexpr int SR = FinSR<NT>::value;
   __shared__ uint32_t slots[32];
   __shared__ int32_t starts[2 * SR * kRound];
@@ -911,7 +920,8 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
                           unsigned long long* pooled,
                           unsigned long long* pooled_parts, int n_parts, int64_t* zero_counts,
                           uint32_t* site_hist, hipStream_t s, bool narrow,
-                          const unsigned long long* rm_all) {
+                          const unsigned long long* rm_all, const unsigned long long* wide,
+                          unsigned long long xthr) {
   if (n_sites <= 0) return;
   ProfScope prof(narrow ? "hist_finalize_side" : "hist_finalize", s);
   QPos pp = p;
@@ -925,14 +935,118 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
   unsigned long long* fin_pooled = colsum ? nullptr : pooled_parts;
   if (narrow)
     hipLaunchKernelGGL((k_hist_finalize<0, 256>), dim3((unsigned)n_sites), dim3(256), 0, s, hist,
-                       rmask, dense_rounds, pp, vlh, fin_pooled, n_parts, zero_counts, site_hist);
+                       rmask, dense_rounds, pp, vlh, fin_pooled, n_parts, zero_counts, site_hist,
+                       wide, xthr);
   else
     hipLaunchKernelGGL((k_hist_finalize<0, kHistThreads>), dim3((unsigned)n_sites),
                        dim3(kHistThreads), 0, s, hist, rmask, dense_rounds, pp, vlh, fin_pooled,
-                       n_parts, zero_counts, site_hist);
+                       n_parts, zero_counts, site_hist, wide, xthr);
   if (!colsum)
     hipLaunchKernelGGL(k_pooled_fold, dim3(kBins / 256), dim3(256), 0, s, pooled, pooled_parts,
                        n_parts);
+  TMH_HIP(hipGetLastError());
+}
+
+// Very wide sites (a third or more of the 8-pixel groups hold a value >=
+// 16,384, e.g. uniform 16-bit data): the per-site LDS slices of the fused pass
+// would send most pixels to global atomics (uniform sites ran the fused pass
+// at ~0.5 s for 3,456 sites), so the fused pass runs without its histogram
+// and this kernel builds each site's exact 65,536-bin histogram in LDS as u16
+// pairs (128 KB: value v in word v >> 1, half v & 1) from one more read of the
+// site, then scans it into order statistics as k_hist_finalize does.  A half
+// that wraps (a value with more than 65,535 pixels) is caught from the
+// returned old word: the carry into the upper half is undone and 65,536 goes
+// to the site's zero-maintained global slab, whose 1,024-bin round is flagged;
+// the scan adds (and resets) the slab's counts of the flagged rounds.  Runs
+// only when the Welford pass's count of such groups (wide[1]) is >= xthr.
+constexpr int kU16Threads = 1024;
+__global__ __launch_bounds__(kU16Threads) void k_hist_site_u16(
+    const uint16_t* __restrict__ sites, int64_t npx, uint32_t* __restrict__ slab, const QPos p,
+    uint32_t* __restrict__ vlh_all, unsigned long long* __restrict__ pooled, int n_pooled,
+    int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist,
+    const unsigned long long* __restrict__ wide, unsigned long long xthr) {
+  if (__builtin_nontemporal_load(wide + 1) < xthr) return;  // uniform: not a very wide launch
+  constexpr int SR = 2;  // 2,048-bin super-rounds: 16 KB of ranks beside the 128 KB histogram
+  __shared__ __attribute__((aligned(16))) uint32_t w16[kBins / 2];
+  __shared__ uint32_t slots[32];
+  __shared__ int32_t starts[2 * SR * kRound];
+  __shared__ unsigned long long ovf;  // rounds with counts in the slab
+  const int tid = threadIdx.x;
+  const int64_t s = blockIdx.x;
+  for (int i = tid; i < kBins / 8; i += kU16Threads)
+    reinterpret_cast<uint4*>(w16)[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (tid == 0) ovf = 0ull;
+  __syncthreads();
+  uint32_t* hs = slab + s * (int64_t)kBins;
+  auto add = [&](uint32_t u) {
+    const uint32_t sh = (u & 1u) << 4;
+    const uint32_t old = atomicAdd(&w16[u >> 1], 1u << sh);
+    if (((old >> sh) & 0xFFFFu) == 0xFFFFu) {  // this add wrapped the half: rare
+      if (!sh) atomicSub(&w16[u >> 1], 0x10000u);  // undo the carry into the upper half
+      atomicAdd(&hs[u], 65536u);
+      atomicOr(&ovf, 1ull << (u >> 10));
+    }
+  };
+  const uint4* src = reinterpret_cast<const uint4*>(sites + s * npx);
+  const int64_t n16 = npx >> 3;
+  int64_t i = tid;
+  for (; i + 3 * kU16Threads < n16; i += 4 * kU16Threads) {
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = ld_site<true>(src + i + k * kU16Threads);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t wd[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        add(wd[q] & 0xFFFFu);
+        add(wd[q] >> 16);
+      }
+    }
+  }
+  for (; i < n16; i += kU16Threads) {
+    const uint4 v = ld_site<true>(src + i);
+    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      add(wd[q] & 0xFFFFu);
+      add(wd[q] >> 16);
+    }
+  }
+  // the slab atomics must have been performed before the scan reads the slab
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const unsigned long long ov = ovf;
+  unsigned long long* pl = pooled + (int64_t)(blockIdx.x % n_pooled) * kBins;
+  hist_tail_rounds<0, kU16Threads, SR>(
+      ~0ull,
+      [&](uint32_t b) -> uint32_t {
+        uint32_t c = (w16[b >> 1] >> ((b & 1u) << 4)) & 0xFFFFu;
+        if ((ov >> (b >> 10)) & 1ull) {
+          const uint32_t g = hs[b];
+          if (g) {
+            hs[b] = 0u;  // zero-maintained
+            c += g;
+          }
+        }
+        return c;
+      },
+      [](uint32_t, uint32_t) {}, s, p, vlh_all, pl, zero_counts, site_hist, slots, starts);
+}
+
+void launch_hist_site_u16(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* slab,
+                          const QPos& p, uint32_t* vlh, int64_t vlh_ld,
+                          unsigned long long* pooled, unsigned long long* pooled_parts,
+                          int n_parts, int64_t* zero_counts, uint32_t* site_hist,
+                          const unsigned long long* wide, unsigned long long xthr, hipStream_t s) {
+  if (n_sites <= 0) return;
+  ProfScope prof("hist_u16", s);
+  QPos pp = p;
+  pp.tstride = vlh_ld * kOsTile;
+  hipLaunchKernelGGL(k_hist_site_u16, dim3((unsigned)n_sites), dim3(kU16Threads), 0, s, sites, npx,
+                     slab, pp, vlh, pooled_parts, n_parts, zero_counts, site_hist, wide, xthr);
+  hipLaunchKernelGGL(k_pooled_fold, dim3(kBins / 256), dim3(256), 0, s, pooled, pooled_parts,
+                     n_parts);
   TMH_HIP(hipGetLastError());
 }
 

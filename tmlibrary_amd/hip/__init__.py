@@ -118,6 +118,14 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         raise HipUnavailableError(
             "libtmhip.so not found at %s — build it with `python -c "
             "'import __graft_entry__ as g; g.build()'` or `make -C tmlibrary_amd/csrc`" % path)
+    # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7
+    # (same soname as /opt/rocm's).  Whichever loads first serves both; if
+    # ours came first, a later torch.cuda initialisation found no GPU
+    # (seen running a GPU test module on its own), so let torch's load first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

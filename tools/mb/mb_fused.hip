@@ -153,7 +153,7 @@ int main(int argc, char** argv) {
     CK(hipMemsetAsync(fn, 0, 4, 0));
     hipLaunchKernelGGL((k_correct_hist<true, false, 4, ABL, 512, 16384>), fg, fb, 0, 0, in, out,
                        npx, S, coef, mconst2, fl, -1, -1, hist, rmask, kFusedBands, nullptr,
-                       nullptr, 0ull, 0ull);
+                       nullptr, 0ull, 0ull, 0ull, 0ull);
   };
   time("fused prod (ABL 0)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 0>()); });
   time("fused no hist (ABL 1)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 1>()); });
@@ -166,7 +166,7 @@ int main(int argc, char** argv) {
   time("fused auto (narrow runs, wide exits)", cb + 8.0 * npx, [&] {
     CK(hipMemsetAsync(fn, 0, 4, 0));
     launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                        nullptr, cus, kFusedAuto, wide, 1000ull, 0);
+                        nullptr, cus, kFusedAuto, wide, 1000ull, ~0ull, 0);
   });
   for (int cfg = 0; cfg < kFusedConfigs; ++cfg) {
     char nm[64];
@@ -176,7 +176,7 @@ int main(int argc, char** argv) {
       CK(hipMemsetAsync(fn, 0, 4, 0));
       launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist,
                           rmask, nullptr, cus, cfg,
-                          nullptr, 0, 0);
+                          nullptr, 0, 0, 0);
     });
   }
   return 0;

@@ -162,7 +162,7 @@ int main(int argc, char** argv) {
     CK(hipMemsetAsync(fn, 0, 4, 0));
     hipLaunchKernelGGL((k_correct_hist<true, false, 4, ABL, 512, 16384>), dim3(cus * 2), dim3(512), 0, 0,
                        in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, nullptr,
-                       nullptr, 0ull, 0ull);
+                       nullptr, 0ull, 0ull, 0ull, 0ull);
   };
   char nm[96];
   for (int b : {16, 8, 12, 24, 32, 64}) {
@@ -176,7 +176,7 @@ int main(int argc, char** argv) {
     time(nm2, [&] {
       CK(hipMemsetAsync(fn, 0, 4, 0));
       hipLaunchKernelGGL((k_correct_hist<true, false, SPU_, 0, NT_, LB_>), dim3(grid), dim3(NT_), 0, 0,
-                         in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, nullptr, nullptr, 0ull, 0ull);
+                         in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, nullptr, nullptr, 0ull, 0ull, 0ull, 0ull);
     });
   };
   using C8 = std::integral_constant<int, 8>;
@@ -214,7 +214,7 @@ int main(int argc, char** argv) {
   time("fused auto (narrow runs, wide exits)", [&] {
     CK(hipMemsetAsync(fn, 0, 4, 0));
     launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                        nullptr, cus, kFusedAuto, wide, 1000ull, 0);
+                        nullptr, cus, kFusedAuto, wide, 1000ull, ~0ull, 0);
   });
   for (int cfg = 0; cfg < kFusedConfigs; ++cfg) {
     snprintf(nm, sizeof nm, "fused cfg %d (%d,%d,%d)", cfg, kFusedCfgs[cfg].spu,
@@ -222,7 +222,7 @@ int main(int argc, char** argv) {
     time(nm, [&] {
       CK(hipMemsetAsync(fn, 0, 4, 0));
       launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                          nullptr, cus, cfg, nullptr, 0, 0);
+                          nullptr, cus, cfg, nullptr, 0, 0, 0);
     });
   }
 #define TEAM(SPU_, NT_, ORD_, COEF_, G_, T_, NB_)                                                   \

@@ -118,7 +118,7 @@ int main(int argc, char** argv) {
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const FixList fl{fe, fn, (unsigned)(((size_t)1 << 23) / 8)};
   launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                      nullptr, cus, dist == 0 ? kFusedNarrow : kFusedWide, nullptr, 0, 0);
+                      nullptr, cus, dist == 0 ? kFusedNarrow : kFusedWide, nullptr, 0, 0, 0);
   CK(hipDeviceSynchronize());
   {
     std::vector<unsigned long long> rm(S);
@@ -184,7 +184,7 @@ int main(int argc, char** argv) {
   auto fin = [&](auto kern, int nt) {
     return [&, kern, nt] {
       hipLaunchKernelGGL(kern, dim3((unsigned)S), dim3(nt), 0, 0, hist, rmask, 0, qp, vlh, parts, 16,
-                         zeros, (uint32_t*)nullptr);
+                         zeros, (uint32_t*)nullptr, (const unsigned long long*)nullptr, 0ull);
     };
   };
   time("hfin 1024 (no reset)", osb, fin(k_hist_finalize<8, 1024>, 1024));

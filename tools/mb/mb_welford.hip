@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void k_wf_abl(const uint16_t* __restrict__ sit
   for (int k = 0; k < 4; ++k) cur[k] = ld_site<true>(src + (k < last ? k : last) * ng);
   double K[8], s1[8], s2[8];
   uint32_t isum = 0;
-  xform8<true, 1>(cur[0], slut, sinv, K, wc);
+  xform8<true, 1>(cur[0], slut, sinv, K, wc, wc);
 #pragma unroll
   for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.0;
   for (int64_t s = 0; s < n_sites; s += 4) {
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void k_wf_abl(const uint16_t* __restrict__ sit
 #pragma unroll
           for (int j = 0; j < 8; ++j) x[j] = (double)u[j];
         } else {
-          xform8<true, 1>(v, slut, sinv, x, wc);
+          xform8<true, 1>(v, slut, sinv, x, wc, wc);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256, WPS) void k_wf_var(const uint16_t* __restrict_
   for (int k = 0; k < G; ++k) cur[k] = ld_site<true>(src + (k < last ? k : last) * ng);
   double K[8], s1[8], s2[8];
   float Kf[8];
-  xform8<true, 1>(cur[0], slut, sinv, K, wc);
+  xform8<true, 1>(cur[0], slut, sinv, K, wc, wc);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     s1[k] = s2[k] = 0.0;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256, WPS) void k_wf_var(const uint16_t* __restrict_
     for (int k = 0; k < G; ++k) {
       if (s + k < n_sites) {
         double x[8];
-        xform8<true, 1>(cur[k], slut, sinv, x, wc);
+        xform8<true, 1>(cur[k], slut, sinv, x, wc, wc);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const double d = x[j] - (KF ? (double)Kf[j] : K[j]);
