@@ -22,6 +22,7 @@ namespace tmh {
 // ---------------------------------------------------------------------------
 
 __device__ __forceinline__ int reflect_idx(int i, int n) {
+  if ((unsigned)i < (unsigned)n) return i;  // inside: no integer division
   if (n == 1) return 0;
   const int p = 2 * n;
   i %= p;

@@ -904,7 +904,10 @@ __global__ __launch_bounds__(256) void k_pooled_colsum(const uint32_t* __restric
 
 // pooled[b] += sum of the copies; copies reset to zero (zero-maintained)
 __global__ void k_pooled_fold(unsigned long long* __restrict__ pooled,
-                              unsigned long long* __restrict__ parts, int n_parts) {
+                              unsigned long long* __restrict__ parts, int n_parts,
+                              const unsigned long long* __restrict__ wide = nullptr,
+                              unsigned long long xthr = 0) {
+  if (wide && __builtin_nontemporal_load(wide + 1) < xthr) return;  // nothing was added
   const int b = blockIdx.x * 256 + threadIdx.x;
   if (b >= kBins) return;
   unsigned long long t = 0;
@@ -961,7 +964,8 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
 // only when the Welford pass's count of such groups (wide[1]) is >= xthr.
 constexpr int kU16Threads = 1024;
 __global__ __launch_bounds__(kU16Threads) void k_hist_site_u16(
-    const uint16_t* __restrict__ sites, int64_t npx, uint32_t* __restrict__ slab, const QPos p,
+    const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites,
+    uint32_t* __restrict__ slab, const QPos p,
     uint32_t* __restrict__ vlh_all, unsigned long long* __restrict__ pooled, int n_pooled,
     int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist,
     const unsigned long long* __restrict__ wide, unsigned long long xthr) {
@@ -972,7 +976,10 @@ __global__ __launch_bounds__(kU16Threads) void k_hist_site_u16(
   __shared__ int32_t starts[2 * SR * kRound];
   __shared__ unsigned long long ovf;  // rounds with counts in the slab
   const int tid = threadIdx.x;
-  const int64_t s = blockIdx.x;
+  // persistent over the sites (one workgroup per CU fits): a launch that is
+  // not very wide costs one small grid, not one workgroup per site
+  for (int64_t s = blockIdx.x; s < n_sites; s += gridDim.x) {
+  __syncthreads();  // the previous site's scan is done with the LDS
   for (int i = tid; i < kBins / 8; i += kU16Threads)
     reinterpret_cast<uint4*>(w16)[i] = make_uint4(0u, 0u, 0u, 0u);
   if (tid == 0) ovf = 0ull;
@@ -1032,6 +1039,7 @@ __global__ __launch_bounds__(kU16Threads) void k_hist_site_u16(
         return c;
       },
       [](uint32_t, uint32_t) {}, s, p, vlh_all, pl, zero_counts, site_hist, slots, starts);
+  }
 }
 
 void launch_hist_site_u16(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* slab,
@@ -1043,10 +1051,14 @@ void launch_hist_site_u16(const uint16_t* sites, int64_t npx, int64_t n_sites, u
   ProfScope prof("hist_u16", s);
   QPos pp = p;
   pp.tstride = vlh_ld * kOsTile;
-  hipLaunchKernelGGL(k_hist_site_u16, dim3((unsigned)n_sites), dim3(kU16Threads), 0, s, sites, npx,
+  int dev = 0, cus = 256;
+  TMH_HIP(hipGetDevice(&dev));
+  TMH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const unsigned grid = (unsigned)std::min<int64_t>(n_sites, cus);
+  hipLaunchKernelGGL(k_hist_site_u16, dim3(grid), dim3(kU16Threads), 0, s, sites, npx, n_sites,
                      slab, pp, vlh, pooled_parts, n_parts, zero_counts, site_hist, wide, xthr);
   hipLaunchKernelGGL(k_pooled_fold, dim3(kBins / 256), dim3(256), 0, s, pooled, pooled_parts,
-                     n_parts);
+                     n_parts, wide, xthr);
   TMH_HIP(hipGetLastError());
 }
 
