@@ -148,11 +148,14 @@ int main(int argc, char** argv) {
   }
   time("read nt u4 grid2048 (2 B/px)", (double)bytes, [&] { hipLaunchKernelGGL((k_read<4>), dim3(2048), dim3(256), 0, 0, (const uint4*)in, n16, sink); });
   const dim3 fg(cus * 2), fb(512);
+  int* queues;  // per-XCD unit counters + round-mask union
+  CK(hipMalloc(&queues, kFusedQueueInts * sizeof(int)));
   auto fused = [&](auto abl_tag) {
     constexpr int ABL = decltype(abl_tag)::value;
     CK(hipMemsetAsync(fn, 0, 4, 0));
+    CK(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), 0));
     hipLaunchKernelGGL((k_correct_hist<true, false, 4, ABL, 512, 16384>), fg, fb, 0, 0, in, out,
-                       npx, S, coef, mconst2, fl, -1, -1, hist, rmask, kFusedBands, nullptr,
+                       npx, S, coef, mconst2, fl, -1, -1, hist, rmask, kFusedBands, queues,
                        nullptr, 0ull, 0ull, 0ull, 0ull);
   };
   time("fused prod (ABL 0)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 0>()); });
@@ -161,12 +164,12 @@ int main(int argc, char** argv) {
   time("fused no flush (ABL 8)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 8>()); });
   time("fused prod (ABL 0) again", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 0>()); });
   unsigned long long* wide;
-  CK(hipMalloc(&wide, 8));
-  CK(hipMemset(wide, 0, 8));
+  CK(hipMalloc(&wide, 16));
+  CK(hipMemset(wide, 0, 16));
   time("fused auto (narrow runs, wide exits)", cb + 8.0 * npx, [&] {
     CK(hipMemsetAsync(fn, 0, 4, 0));
     launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                        nullptr, cus, kFusedAuto, wide, 1000ull, ~0ull, 0);
+                        queues, cus, kFusedAuto, wide, 1000ull, ~0ull, 0);
   });
   for (int cfg = 0; cfg < kFusedConfigs; ++cfg) {
     char nm[64];
@@ -175,7 +178,7 @@ int main(int argc, char** argv) {
     time(nm, cb + 8.0 * npx, [&] {
       CK(hipMemsetAsync(fn, 0, 4, 0));
       launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist,
-                          rmask, nullptr, cus, cfg,
+                          rmask, queues, cus, cfg,
                           nullptr, 0, 0, 0);
     });
   }

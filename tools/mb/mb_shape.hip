@@ -124,8 +124,10 @@ int main(int argc, char** argv) {
   CK(hipMemset(hist, 0, (size_t)S * 65536 * 4));
   CK(hipMemset(rmask, 0, S * 8));
   unsigned long long* wide;
-  CK(hipMalloc(&wide, 8));
-  CK(hipMemset(wide, 0, 8));
+  CK(hipMalloc(&wide, 16));
+  CK(hipMemset(wide, 0, 16));
+  int* queues;  // per-XCD unit counters + round-mask union (zeroed before every launch)
+  CK(hipMalloc(&queues, kFusedQueueInts * sizeof(int)));
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const FixList fl{fe, fn, (unsigned)(((size_t)1 << 23) / 8)};
@@ -160,8 +162,9 @@ int main(int argc, char** argv) {
   auto fused = [&](auto abl_tag) {
     constexpr int ABL = decltype(abl_tag)::value;
     CK(hipMemsetAsync(fn, 0, 4, 0));
+    CK(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), 0));
     hipLaunchKernelGGL((k_correct_hist<true, false, 4, ABL, 512, 16384>), dim3(cus * 2), dim3(512), 0, 0,
-                       in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, nullptr,
+                       in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, queues,
                        nullptr, 0ull, 0ull, 0ull, 0ull);
   };
   char nm[96];
@@ -175,8 +178,9 @@ int main(int argc, char** argv) {
     constexpr int SPU_ = decltype(spu_t)::value, NT_ = decltype(nt_t)::value, LB_ = decltype(lb_t)::value;
     time(nm2, [&] {
       CK(hipMemsetAsync(fn, 0, 4, 0));
+      CK(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), 0));
       hipLaunchKernelGGL((k_correct_hist<true, false, SPU_, 0, NT_, LB_>), dim3(grid), dim3(NT_), 0, 0,
-                         in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, nullptr, nullptr, 0ull, 0ull, 0ull, 0ull);
+                         in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, queues, nullptr, 0ull, 0ull, 0ull, 0ull);
     });
   };
   using C8 = std::integral_constant<int, 8>;
@@ -214,7 +218,7 @@ int main(int argc, char** argv) {
   time("fused auto (narrow runs, wide exits)", [&] {
     CK(hipMemsetAsync(fn, 0, 4, 0));
     launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                        nullptr, cus, kFusedAuto, wide, 1000ull, ~0ull, 0);
+                        queues, cus, kFusedAuto, wide, 1000ull, ~0ull, 0);
   });
   for (int cfg = 0; cfg < kFusedConfigs; ++cfg) {
     snprintf(nm, sizeof nm, "fused cfg %d (%d,%d,%d)", cfg, kFusedCfgs[cfg].spu,
@@ -222,7 +226,7 @@ int main(int argc, char** argv) {
     time(nm, [&] {
       CK(hipMemsetAsync(fn, 0, 4, 0));
       launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                          nullptr, cus, cfg, nullptr, 0, 0, 0);
+                          queues, cus, cfg, nullptr, 0, 0, 0);
     });
   }
 #define TEAM(SPU_, NT_, ORD_, COEF_, G_, T_, NB_)                                                   \

@@ -117,8 +117,10 @@ int main(int argc, char** argv) {
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const FixList fl{fe, fn, (unsigned)(((size_t)1 << 23) / 8)};
+  int* queues;  // per-XCD unit counters + round-mask union
+  CK(hipMalloc(&queues, kFusedQueueInts * sizeof(int)));
   launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                      nullptr, cus, dist == 0 ? kFusedNarrow : kFusedWide, nullptr, 0, 0, 0);
+                      queues, cus, dist == 0 ? kFusedNarrow : kFusedWide, nullptr, 0, 0, 0);
   CK(hipDeviceSynchronize());
   {
     std::vector<unsigned long long> rm(S);
