@@ -346,9 +346,10 @@ def test_very_wide_jobs(L, cfg):
     >= 16,384): with the automatic configuration the fused pass runs without
     its histogram and k_hist_site_u16 builds the exact per-site histograms in
     LDS as u16 pairs from one more read of the sites.  Job 0 is uniform
-    0..65535; job 1 adds a value held by more than 65,535 pixels of one site
-    (the u16 half wraps: the carry is undone and the count finishes in the
-    global slab) and the extremes 0 / 65535.  cfg 3 forces the narrow slices
+    0..65535; job 1 adds a value held by more than 65,535 pixels of one site,
+    two values sharing one u16 pair held by 45,000 pixels each, a hot upper
+    half (each half spills 16,384 counts at a time to the global slab) and
+    the extremes 0 / 65535.  cfg 3 forces the narrow slices
     (every value >= 4,096 by global atomics) on the same jobs.  Histograms,
     order statistics and percentile sums bit-exact, mean/std 1e-6, corrected
     values within 1 DN of the oracle (stats.py:64-121, image.py:599-631)."""
@@ -378,6 +379,10 @@ def test_very_wide_jobs(L, cfg):
             sites[2].reshape(-1)[:70000] = 30000  # one bin beyond 65,535 pixels
             sites[3].reshape(-1)[:5] = 0
             sites[4].reshape(-1)[-7:] = 65535
+            # both halves of one u16 pair hot at once (45,000 pixels each,
+            # interleaved), and a hot upper half alone
+            sites[1].reshape(-1)[:90000] = 40000 + np.arange(90000, dtype=np.uint16) % 2
+            sites[5].reshape(-1)[:50000] = 12345
         d_in.put(sites)
         hip.check(L.tmh_stats_reset(h))
         hip.check(L.tmh_stats_update_welford_device(h, d_in.p, n, 1, sp))

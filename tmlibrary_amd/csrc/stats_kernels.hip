@@ -957,12 +957,19 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
 // and this kernel builds each site's exact 65,536-bin histogram in LDS as u16
 // pairs (128 KB: value v in word v >> 1, half v & 1) from one more read of the
 // site, then scans it into order statistics as k_hist_finalize does.  A half
-// that wraps (a value with more than 65,535 pixels) is caught from the
-// returned old word: the carry into the upper half is undone and 65,536 goes
-// to the site's zero-maintained global slab, whose 1,024-bin round is flagged;
-// the scan adds (and resets) the slab's counts of the flagged rounds.  Runs
-// only when the Welford pass's count of such groups (wide[1]) is >= xthr.
+// never wraps: the add that takes it to kU16Spill (seen in the returned old
+// word -- exactly one add sees kU16Spill - 1 each time) takes kU16Spill back
+// out of it and adds kU16Spill to the site's zero-maintained global slab,
+// whose 1,024-bin round is flagged; the scan adds (and resets) the slab's
+// counts of the flagged rounds.  Until that subtract lands other adds keep
+// landing on the half, so it is kept far below 65,535: 49,151 adds of
+// headroom, against at most 16 waves x 15 x 64 = 15,360 LDS adds the
+// workgroup has outstanding at once.  (Spilling at the wrap itself raced: a carry
+// into the upper half, not yet undone, could make an add to the upper half
+// see -- and spill -- a wrap that was not there.)  Runs only when the Welford
+// pass's count of such groups (wide[1]) is >= xthr.
 constexpr int kU16Threads = 1024;
+constexpr uint32_t kU16Spill = 0x4000u;
 __global__ __launch_bounds__(kU16Threads) void k_hist_site_u16(
     const uint16_t* __restrict__ sites, int64_t npx, int64_t n_sites,
     uint32_t* __restrict__ slab, const QPos p,
@@ -988,9 +995,9 @@ __global__ __launch_bounds__(kU16Threads) void k_hist_site_u16(
   auto add = [&](uint32_t u) {
     const uint32_t sh = (u & 1u) << 4;
     const uint32_t old = atomicAdd(&w16[u >> 1], 1u << sh);
-    if (((old >> sh) & 0xFFFFu) == 0xFFFFu) {  // this add wrapped the half: rare
-      if (!sh) atomicSub(&w16[u >> 1], 0x10000u);  // undo the carry into the upper half
-      atomicAdd(&hs[u], 65536u);
+    if (((old >> sh) & 0xFFFFu) == kU16Spill - 1u) {  // this add took the half to kU16Spill: rare
+      atomicSub(&w16[u >> 1], kU16Spill << sh);
+      atomicAdd(&hs[u], kU16Spill);
       atomicOr(&ovf, 1ull << (u >> 10));
     }
   };
