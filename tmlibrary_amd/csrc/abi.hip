@@ -274,6 +274,7 @@ struct tmh_corrector {
   DBuf<unsigned long long> fix_e;    // pixels flagged for the f64 refinement (common.h)
   DBuf<unsigned int> fix_n;
   DBuf<tmh_window> win;  // per-site alignment windows of the chain pass
+  DBuf<uint8_t> lut8;    // the chain pass's 16-bit clip + scale table (64 KB)
   int n_wg = 256;
   DBuf<int> queues;  // fused pass: per-XCD unit counters (dynamic deal)
   DBuf<double> sums, partial;
@@ -1347,8 +1348,10 @@ int tmh_correct_chain_u8_device(tmh_corrector* c, const uint16_t* dev_in, uint8_
     TMH_HIP(hipMemcpyAsync(c->win.p, host_windows, (size_t)n_sites * sizeof(tmh_window),
                            hipMemcpyHostToDevice, s));
     const FixList fl = corrector_fixlist(c, n_sites, s);
+    if (!c->lut8.n) c->lut8.alloc(65536);
     launch_chain_u8(dev_in, dev_out, c->H, c->W, n_sites, c->coef_lin.p, c->mconst2.p, fl,
-                    c->coef64.p, c->rc.p, c->log_transform, c->win.p, clip_lo, clip_hi, s);
+                    c->coef64.p, c->rc.p, c->log_transform, c->win.p, clip_lo, clip_hi,
+                    c->lut8.p, s);
     TMH_HIP(hipStreamSynchronize(s));  // the window buffer is reused by the next call
   });
 }

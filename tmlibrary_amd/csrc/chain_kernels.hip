@@ -141,21 +141,30 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-template <bool LOG, bool LUT>
-__global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ in,
-                                                   uint8_t* __restrict__ out, int H, int W,
-                                                   int64_t n_sites, int64_t per,
-                                                   const float2* __restrict__ coef_lin,
-                                                   const float4* __restrict__ mconst2,
-                                                   FixList fl,
-                                                   const tmh_window* __restrict__ win, int lo,
-                                                   int hi, int T, double step) {
-  // LUT: the reference's uint8 table for the clipped range [lo, hi] staged in
-  // LDS (hi - lo + 1 bytes), one ds_read_u8 per pixel instead of three f64 ops
-  extern __shared__ uint8_t slut[];
-  if (LUT) {
-    for (int i = threadIdx.x; i <= hi - lo; i += 256)
+// LUT 0: clip + scale in f64 arithmetic; 1: the reference's uint8 table for
+// the clipped range [lo, hi] staged in LDS (hi - lo + 1 bytes), one ds_read_u8
+// per pixel after the clip; 2: clip and table for every 16-bit value (64 KB,
+// copied from lut8, k_chain_lut8), indexed by the cast's low half directly --
+// the pass is VALU-bound (~24 ops + 2 transcendentals per pixel), and this
+// drops the clip's max/min and the index subtract.  NT threads per workgroup.
+template <bool LOG, int LUT, int NT = 256>
+__global__ __launch_bounds__(NT) void k_chain_u8(const uint16_t* __restrict__ in,
+                                                  uint8_t* __restrict__ out, int H, int W,
+                                                  int64_t n_sites, int64_t per,
+                                                  const float2* __restrict__ coef_lin,
+                                                  const float4* __restrict__ mconst2,
+                                                  FixList fl,
+                                                  const tmh_window* __restrict__ win, int lo,
+                                                  int hi, int T, double step,
+                                                  const uint8_t* __restrict__ lut8) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t slut[];
+  if (LUT == 1) {
+    for (int i = threadIdx.x; i <= hi - lo; i += NT)
       slut[i] = (uint8_t)(i >= T ? 255u : (uint32_t)((double)i * step));
+    __syncthreads();
+  } else if (LUT == 2) {
+    for (int i = threadIdx.x; i < 65536 / 16; i += NT)
+      reinterpret_cast<uint4*>(slut)[i] = reinterpret_cast<const uint4*>(lut8)[i];
     __syncthreads();
   }
   const int64_t npx = (int64_t)H * W;
@@ -165,12 +174,12 @@ __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ i
   // share a 128-B line at their seam, and a seam inside one XCD's L2 merges
   // instead of leaving two partial lines to write back.
   const int64_t tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int64_t g = tile * 256 + threadIdx.x;
+  const int64_t g = tile * NT + threadIdx.x;
   const bool live = g < ngroups;
   const int lane = threadIdx.x & 63;
-  const bool top_lane = threadIdx.x == 255 || g + 1 >= ngroups;  // no upper neighbour run
-  __shared__ uint64_t edge[256 / 64];
-  __shared__ __attribute__((aligned(16))) uint8_t stage[2048 + 256];
+  const bool top_lane = threadIdx.x == NT - 1 || g + 1 >= ngroups;  // no upper neighbour run
+  __shared__ uint64_t edge[NT / 64];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[NT * 8 + 256];
   const int64_t p0 = (live ? g : 0) * 8;
   const int r = (int)(p0 / W), c0 = (int)(p0 % W);
   const float4 m = mconst2[0];
@@ -227,10 +236,14 @@ __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ i
         x = __builtin_fminf(x, 2147418112.0f);  // >= 2^31, inf, NaN -> low half 0 (x86)
         if (!LOG) x = __builtin_fmaxf(x, -2147483648.0f);
         const uint32_t v16 = (uint32_t)(int32_t)x & 0xFFFFu;
-        const uint32_t v = min(max(v16, (uint32_t)lo), (uint32_t)hi);  // np.clip
-        o[2 * k + h] = LUT ? (uint32_t)slut[v - (uint32_t)lo]
-                           : (v - (uint32_t)lo >= (uint32_t)T ? 255u
-                                                              : (uint32_t)((double)(v - lo) * step));
+        if (LUT == 2) {
+          o[2 * k + h] = slut[v16];
+        } else {
+          const uint32_t v = min(max(v16, (uint32_t)lo), (uint32_t)hi);  // np.clip
+          o[2 * k + h] = LUT ? (uint32_t)slut[v - (uint32_t)lo]
+                             : (v - (uint32_t)lo >= (uint32_t)T ? 255u
+                                                                : (uint32_t)((double)(v - lo) * step));
+        }
       }
     }
     // rare: a pixel beyond the f32 bound flags its group of 8 for the f64
@@ -265,8 +278,8 @@ __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ i
     const uint32_t nhi = (uint32_t)__shfl_down((int)hi4, 1, 64);
     __syncthreads();  // (1) edge slots written; the previous site's stage is drained
     uint64_t n8 = ((uint64_t)nhi << 32) | nlo;
-    if (lane == 63 && wv < 256 / 64 - 1) n8 = edge[wv + 1];
-    const int64_t o0 = tile * 2048 + off;  // destination of thread 0's byte 0
+    if (lane == 63 && wv < NT / 64 - 1) n8 = edge[wv + 1];
+    const int64_t o0 = tile * NT * 8 + off;  // destination of thread 0's byte 0
     const int64_t L0 = o0 >= 0 ? (o0 & ~(int64_t)127) : -((-o0 + 127) & ~(int64_t)127);
     if (!live) {
       // no run (past the last group): nothing to stage
@@ -285,7 +298,7 @@ __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ i
     __syncthreads();  // (2) stage complete
     // valid destination bytes of this workgroup: [o0, o0 + 2048) within the
     // site (the last workgroup may own fewer groups)
-    const int64_t wg_bytes = (ngroups - tile * 256 < 256 ? ngroups - tile * 256 : 256) * 8;
+    const int64_t wg_bytes = (ngroups - tile * NT < NT ? ngroups - tile * NT : NT) * 8;
     const int64_t v0 = o0 > 0 ? o0 : 0;
     const int64_t v1 = o0 + wg_bytes < npx ? o0 + wg_bytes : npx;
     const int64_t c = L0 + 16 * (int64_t)threadIdx.x;  // this thread's 16-B chunk
@@ -296,6 +309,12 @@ __global__ __launch_bounds__(256) void k_chain_u8(const uint16_t* __restrict__ i
         if (c + b >= v0 && c + b < v1) o8[c + b] = stage[c + b - L0];
     }
   }
+}
+
+// The 16-bit clip + scale table of k_chain_u8<LUT = 2>: entry v = scale8(clip(v)).
+__global__ void k_chain_lut8(uint8_t* __restrict__ lut8, int lo, int hi, int T, double step) {
+  const int v = (int)blockIdx.x * 256 + threadIdx.x;
+  if (v < 65536) lut8[v] = (uint8_t)clip_scale8((uint32_t)v, lo, hi, T, step);
 }
 
 // The destinations no source pixel reaches: [0, off) for off > 0, [npx + off,
@@ -407,7 +426,7 @@ void launch_map_u8(const uint16_t* in, uint8_t* out, int64_t n, int lo, int hi, 
 void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_sites,
                      const float2* coef_lin, const float4* mconst2, const FixList& fl,
                      const double2* coef64, const RefineConst* rc, int log_transform,
-                     const tmh_window* d_win, int lo, int hi, hipStream_t s) {
+                     const tmh_window* d_win, int lo, int hi, uint8_t* lut8, hipStream_t s) {
   if (n_sites <= 0) return;
   ProfScope prof("chain", s);
   const int64_t npx = (int64_t)H * W;
@@ -419,17 +438,25 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
     // site parts even out the dispatch rounds (each thread streams its part)
     const int64_t parts = n_sites >= 64 ? 8 : 1;
     const int64_t per = cdiv(n_sites, parts);
-    const dim3 grid((unsigned)cdiv(npx >> 3, 256), (unsigned)cdiv(n_sites, per));
     const int lut_bytes = hi - lo + 1;
     const bool lut = lut_bytes <= 16384;  // else three f64 ops per pixel
     const size_t shm = lut ? (size_t)((lut_bytes + 15) & ~15) : 0;
-#define TMH_CHAIN(L_, U_)                                                                     \
-  hipLaunchKernelGGL((k_chain_u8<L_, U_>), grid, dim3(256), shm, s, in, out, H, W, n_sites, per, \
-                     coef_lin, mconst2, fl, d_win, lo, hi, T, step)
-    if (log_transform) {
-      if (lut) TMH_CHAIN(true, true); else TMH_CHAIN(true, false);
+#define TMH_CHAIN(L_, U_, NT_, SHM_, LUT8_)                                                      \
+  hipLaunchKernelGGL((k_chain_u8<L_, U_, NT_>),                                                  \
+                     dim3((unsigned)cdiv(npx >> 3, NT_), (unsigned)cdiv(n_sites, per)), dim3(NT_), \
+                     SHM_, s, in, out, H, W, n_sites, per, coef_lin, mconst2, fl, d_win, lo, hi, T,  \
+                     step, LUT8_)
+    if (lut8) {
+      // the whole 16-bit table: 1,024-thread workgroups (two per CU with the
+      // 64 KB table; smaller ones copy it too often: 256 threads ran 37 ms,
+      // 512 21.6, 1,024 14.6 against 15.0 for the clipped-range table,
+      // profiles/r2/mb_chain_lut64_r2lt.txt)
+      hipLaunchKernelGGL(k_chain_lut8, dim3(256), dim3(256), 0, s, lut8, lo, hi, T, step);
+      if (log_transform) TMH_CHAIN(true, 2, 1024, 65536, lut8); else TMH_CHAIN(false, 2, 1024, 65536, lut8);
+    } else if (log_transform) {
+      if (lut) TMH_CHAIN(true, 1, 256, shm, nullptr); else TMH_CHAIN(true, 0, 256, shm, nullptr);
     } else {
-      if (lut) TMH_CHAIN(false, true); else TMH_CHAIN(false, false);
+      if (lut) TMH_CHAIN(false, 1, 256, shm, nullptr); else TMH_CHAIN(false, 0, 256, shm, nullptr);
     }
 #undef TMH_CHAIN
     hipLaunchKernelGGL(k_chain_fill, dim3(64, (unsigned)n_sites), dim3(256), 0, s, out, H, W,

@@ -245,11 +245,12 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
 void launch_align(const void* in, void* out, int elem_bytes, int64_t n_sites, int H, int W, int oh,
                   int ow, const tmh_window* d_win, hipStream_t s);
 void launch_map_u8(const uint16_t* in, uint8_t* out, int64_t n, int lo, int hi, hipStream_t s);
-// (launches its own fixup kernel after the chain pass)
+// (launches its own fixup kernel after the chain pass; lut8: 64 KB of device
+// scratch for the 16-bit clip + scale table, or null for the clipped-range one)
 void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_sites,
                      const float2* coef_lin, const float4* mconst2, const FixList& fl,
                      const double2* coef64, const RefineConst* rc, int log_transform,
-                     const tmh_window* d_win, int lo, int hi, hipStream_t s);
+                     const tmh_window* d_win, int lo, int hi, uint8_t* lut8, hipStream_t s);
 void launch_clip_u16(const uint16_t* in, uint16_t* out, int64_t n, int lo, int hi, hipStream_t s);
 void launch_synth(uint16_t* out, int64_t n_sites, int H, int W, uint64_t seed, int channel,
                   int64_t first_site, int dist, hipStream_t s);

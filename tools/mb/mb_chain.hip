@@ -109,12 +109,35 @@ int main(int argc, char** argv) {
            100.0 * bytes / (ms * 1e-3) / 8e12, h);
     fflush(stdout);
   };
-  for (int r = 0; r < 2; ++r)
+  uint8_t* lut8;
+  CK(hipMalloc(&lut8, 65536));
+  hipLaunchKernelGGL(k_chain_lut8, dim3(256), dim3(256), 0, 0, lut8, lo, hi, T, step);
+  auto full = [&](const char* nm, auto nt_tag) {
+    constexpr int NT = decltype(nt_tag)::value;
+    const dim3 g((unsigned)((npx / 8 + NT - 1) / NT), grid.y);
+    time(nm, [&] {
+      CK(hipMemsetAsync(fn, 0, 4, 0));
+      hipLaunchKernelGGL((k_chain_u8<true, 2, NT>), g, dim3(NT), 65536, 0, in, out, H, W, S, per,
+                         clin, mc2, fl, dw, lo, hi, T, step, lut8);
+    });
+  };
+  for (int r = 0; r < 2; ++r) {
     time("chain (production kernel)", [&] {
       CK(hipMemsetAsync(fn, 0, 4, 0));
-      hipLaunchKernelGGL((k_chain_u8<true, true>), grid, dim3(256), shm, 0, in, out, H, W, S, per,
-                         clin, mc2, fl, dw, lo, hi, T, step);
+      hipLaunchKernelGGL((k_chain_u8<true, 1>), grid, dim3(256), shm, 0, in, out, H, W, S, per,
+                         clin, mc2, fl, dw, lo, hi, T, step, nullptr);
     });
+    full("chain 64 KB table, NT 256", std::integral_constant<int, 256>());
+    full("chain 64 KB table, NT 512", std::integral_constant<int, 512>());
+    full("chain 64 KB table, NT 1024", std::integral_constant<int, 1024>());
+  }
+  // VALU-bound check: the same pass without the log / exp (two transcendental
+  // ops per pixel; different output, same bytes)
+  time("chain without log/exp (LOG=false)", [&] {
+    CK(hipMemsetAsync(fn, 0, 4, 0));
+    hipLaunchKernelGGL((k_chain_u8<false, 1>), grid, dim3(256), shm, 0, in, out, H, W, S, per,
+                       clin, mc2, fl, dw, lo, hi, T, step, nullptr);
+  });
   printf("done\n");
   return 0;
 }
