@@ -5,7 +5,10 @@
 // Here one process allocates NB site-sized buffers (38 GB each at the bench
 // size), fills the first with the bench's sites and copies it to the others,
 // then times the production fused pass (narrow configuration) and the
-// Welford pass for several (input, output) buffer pairs.
+// Welford pass for several (input, output) buffer pairs.  (Round 2 also ran
+// the fused pass with each unit's band walk rotated by a hash of the unit, to
+// de-synchronise the concurrent streams' offsets: no better on any pair,
+// profiles/r2/mb_place_rot_r2pl.txt.)
 // Usage: mb_place [n_sites=3456] [n_buffers=6] [reps=3] [mode=0] [fill=0]
 #include <hip/hip_runtime.h>
 
