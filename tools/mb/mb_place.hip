@@ -49,10 +49,12 @@ int main(int argc, char** argv) {
   std::vector<uint16_t*> buf(NB);
   for (int i = 0; i < NB; ++i) {
     const bool contig = mode == 1 || (mode == 2 && (i & 1));
+    // + 64 MB of slack: the output offset sweep below writes at buf + delta
     if (contig)
-      CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&buf[i]), bytes, hipDeviceMallocContiguous));
+      CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&buf[i]), bytes + (64 << 20),
+                               hipDeviceMallocContiguous));
     else
-      CK(hipMalloc(&buf[i], bytes));
+      CK(hipMalloc(&buf[i], bytes + (64 << 20)));
     printf("buffer %d at %p%s\n", i, (void*)buf[i], contig ? " (contiguous)" : "");
   }
   // fill: buffer 0 by the generator kernel, the others by device copies
@@ -128,6 +130,17 @@ int main(int argc, char** argv) {
                           rmask, queues, cus, kFusedNarrow, nullptr, 0, 0, 0);
     });
   };
+  // output written at buf[o] + delta bytes: does the read/write address
+  // relation matter?
+  auto fused_at = [&](int i, int o, size_t delta) {
+    return time([&] {
+      CK(hipMemsetAsync(fn, 0, 4, 0));
+      CK(hipMemsetAsync(rmask, 0, S * 8, 0));
+      launch_correct_hist(buf[i], reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(buf[o]) + delta),
+                          npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask, queues,
+                          cus, kFusedNarrow, nullptr, 0, 0, 0);
+    });
+  };
   auto welford = [&](int i) {
     return time([&] {
       launch_welford(buf[i], npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 1, wide, 0);
@@ -141,6 +154,14 @@ int main(int argc, char** argv) {
       fflush(stdout);
     }
   printf("fused in 0 -> out 0 (in place): %8.3f ms\n", fused(0, 0));
+  const size_t deltas[] = {0, 4096, 65536, 1u << 20, (2u << 20) + 4096, 16u << 20, 48u << 20};
+  for (int i = 0; i < NB; ++i) {
+    const int o = (i + 1) % NB;
+    printf("fused in %d -> out %d + delta:", i, o);
+    for (size_t d : deltas) printf(" %zu:%.3f", d, fused_at(i, o, d));
+    printf("\n");
+    fflush(stdout);
+  }
   printf("done\n");
   return 0;
 }
