@@ -112,10 +112,15 @@ def test_chain_by_steps_vs_reference(L):
         assert d.max() <= 1
 
 
-@pytest.mark.parametrize("shape", [(256, 320), (70, 90)])
-def test_chain_device_random_windows(L, shape):
+@pytest.mark.parametrize("shape,bounds", [((256, 320), (100, 3000)), ((70, 90), (100, 3000)),
+                                          ((256, 320), (0, 65535)), ((256, 320), (700, 20000)),
+                                          ((256, 320), (500, 501))])
+def test_chain_device_random_windows(L, shape, bounds):
     """Device-resident batch with per-site shifts (incl. odd column shifts and
-    an empty window) vs the oracle chain; odd widths take the scalar path."""
+    an empty window) vs the oracle chain; odd widths take the scalar path.
+    Clip bounds: the usual range, the whole 16-bit range, one wider than the
+    old 16,384-entry table limit, and a single-step range (the lone 0 of
+    _map_to_uint8) -- all through the 64 KB clip + scale table."""
     import ctypes as C
     from tmlibrary_amd import hip
     from tmlibrary_amd.image import Corrector, align_window
@@ -130,7 +135,7 @@ def test_chain_device_random_windows(L, shape):
     res = (4, 4, 7, 7)
     wins = np.stack([align_window((H, W), y, x, *res, crop=False)[0] for y, x in shifts])
     wins[5]["rows"] = 0  # all padding
-    lo, hi = 100, 3000
+    lo, hi = bounds
     corr = Corrector(sm, ss)
     d_in = C.c_void_p()
     d_out = C.c_void_p()
