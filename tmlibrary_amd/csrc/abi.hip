@@ -243,6 +243,7 @@ struct tmh_stats {
   int64_t last_batch = 0;
   int64_t pending = 0;        // Welford-updated sites whose histograms are still to come
   DBuf<unsigned long long> wide;  // pixel groups with a value >= 4,096 / >= 16,384 in the pending sites
+  DBuf<unsigned int> probe;       // bright-site probe of the Welford launch (k_wf_probe)
   int64_t wide_sites = 0;         // sites that count covers
   bool pct_sum_external = false;
   DBuf<double> mean, m2, lut_log, gamma, acc, tmp_mean, tmp_std, rn;
@@ -395,6 +396,7 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
       h->m2.alloc(npx, true);
       h->wf_part.alloc((size_t)8 * npx);
       h->wide.alloc(2, true);  // groups with a value >= 4,096 / >= 16,384
+      h->probe.alloc(1);
       h->acc.alloc(n_quantiles, true);
       h->pooled.alloc(kBins, true);
       h->lut_log.alloc(kBins);
@@ -521,7 +523,7 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
     TMH_HIP(hipStreamWaitEvent(hs, h->ev_fork, 0));
   }
   launch_welford(d, h->npx, ns, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
-                 log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, nullptr, s);
+                 log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, nullptr, h->probe.p, s);
   // order statistics, in chunks so the per-site slabs stay bounded
   for (int64_t c0 = 0; c0 < ns; c0 += chunk) {
     const int64_t nc = std::min(chunk, ns - c0);
@@ -554,7 +556,8 @@ int tmh_stats_update_welford_device(tmh_stats* h, const uint16_t* dev_sites, int
       h->rn.alloc((size_t)n_sites);
     }
     launch_welford(dev_sites, h->npx, n_sites, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
-                   log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, h->wide.p, s);
+                   log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, h->wide.p,
+                   h->probe.p, s);
     if ((h->npx & 7) == 0) h->wide_sites += n_sites;
     h->n += n_sites;
     h->pending += n_sites;

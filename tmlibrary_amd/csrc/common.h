@@ -153,7 +153,7 @@ __device__ __forceinline__ int32_t correct_ref_f64(uint32_t x, double mean, doub
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
                     double* part, size_t part_cap, int forced_parts,
-                    unsigned long long* wide, hipStream_t s, int shape = -1);
+                    unsigned long long* wide, unsigned int* probe, hipStream_t s, int shape = -1);
 // vlh: the order statistics of the launch's first site (buffer + site *
 // kOsTile) in a buffer with room for vlh_ld sites (kOsTile layout above)
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,

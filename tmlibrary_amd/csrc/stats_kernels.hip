@@ -182,7 +182,16 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
     const uint16_t* __restrict__ sites, int64_t npx, int64_t n_total, int64_t per,
     const WfMerge mg, double* __restrict__ mean, double* __restrict__ m2,
     const double* __restrict__ lut, double* __restrict__ part,
-    unsigned long long* __restrict__ wide) {
+    unsigned long long* __restrict__ wide, const unsigned int* __restrict__ probe,
+    unsigned int probe_thr) {
+  // probe (k_wf_probe): the site split applies only to bright sites; otherwise
+  // the part-0 workgroups walk every site and the others leave at once
+  int parts = (int)gridDim.y;
+  if (probe && __builtin_nontemporal_load(probe) < probe_thr) {
+    if (blockIdx.y > 0) return;
+    parts = 1;
+    per = n_total;
+  }
   __shared__ double slut[kWfLut], sinv[INV == 1 ? kWfLut : 1];
   __shared__ uint32_t wide_sh[2];
   if (LOG) fill_wf_tables<INV>(lut, slut, sinv, NT);
@@ -242,7 +251,7 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
     if (threadIdx.x == 0 && wide_sh[1]) atomicAdd(wide + 1, (unsigned long long)wide_sh[1]);
   }
 
-  if (gridDim.y > 1) {  // partial (mean_l, M2_l) of this part
+  if (parts > 1) {  // partial (mean_l, M2_l) of this part
     const double inv = 1.0 / (double)n_sites;
     double2* pm = reinterpret_cast<double2*>(part + (2 * blockIdx.y) * npx) + g * 4;
     double2* pq = reinterpret_cast<double2*>(part + (2 * blockIdx.y + 1) * npx) + g * 4;
@@ -299,7 +308,9 @@ struct WfParts {
 // Fold the parts' (mean_l, M2_l) in part order (Chan's pairwise combine),
 // then into the running state (n0 sites before this launch).
 __global__ void k_wf_merge_parts(const double* __restrict__ part, int64_t npx, const WfParts pc,
-                                 double n0, double* __restrict__ mean, double* __restrict__ m2) {
+                                 double n0, double* __restrict__ mean, double* __restrict__ m2,
+                                 const unsigned int* __restrict__ probe, unsigned int probe_thr) {
+  if (probe && __builtin_nontemporal_load(probe) < probe_thr) return;  // one-part launch
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= npx) return;
   double na = pc.cnt[0], ma = part[i], qa = part[npx + i];
@@ -358,16 +369,46 @@ template <int NT, int INV>
 static void launch_welford_vec8(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t per,
                                 int f, const WfMerge& mg, double* mean, double* m2,
                                 const double* lut, int log_transform, double* part,
-                                unsigned long long* wide, hipStream_t s) {
+                                unsigned long long* wide, hipStream_t s,
+                                const unsigned int* probe = nullptr, unsigned int probe_thr = 0) {
   const dim3 grid((unsigned)cdiv(npx >> 3, NT), (unsigned)f);
   // site loads are non-temporal (streamed once; regular loads measured
   // 6.60-6.75 vs 6.19-6.34 ms at job level, profiles/r1/ab_welford_ntl.txt)
   if (log_transform)
     hipLaunchKernelGGL((k_welford_vec8<true, true, NT, INV>), grid, dim3(NT), 0, s, sites, npx,
-                       n_sites, per, mg, mean, m2, lut, part, wide);
+                       n_sites, per, mg, mean, m2, lut, part, wide, probe, probe_thr);
   else
     hipLaunchKernelGGL((k_welford_vec8<false, true, NT, INV>), grid, dim3(NT), 0, s, sites, npx,
-                       n_sites, per, mg, mean, m2, lut, part, wide);
+                       n_sites, per, mg, mean, m2, lut, part, wide, probe, probe_thr);
+}
+
+// Bright-site probe: of kProbeGroups 8-pixel groups spread over the launch's
+// first site, how many hold a value >= 4,096 (one workgroup, count to *out).
+// Bright sites make the log10 pass VALU-bound, where three site parts (three
+// times the workgroups) pay: 11.3 vs 12.4 ms on 3,456 bright sites, against
+// 6.0 vs 5.85 on standard ones (profiles/r2/mb_welford_bright_r2za.txt,
+// mb_welford_r2f.txt) -- so the split is chosen on the device, per launch.
+constexpr int kProbeGroups = 16384;
+constexpr int kWfBrightParts = 3;
+__global__ __launch_bounds__(1024) void k_wf_probe(const uint16_t* __restrict__ sites,
+                                                   int64_t ngroups, unsigned int* __restrict__ out) {
+  __shared__ unsigned int cnt;
+  if (threadIdx.x == 0) cnt = 0u;
+  __syncthreads();
+  // all 16 loads of a thread in flight at once (one DRAM latency, not 16)
+  uint4 v[kProbeGroups / 1024];
+#pragma unroll
+  for (int k = 0; k < kProbeGroups / 1024; ++k) {
+    const int64_t g = (int64_t)(threadIdx.x + 1024 * k) * ngroups / kProbeGroups;
+    v[k] = reinterpret_cast<const uint4*>(sites)[g];
+  }
+  unsigned int c = 0u;
+#pragma unroll
+  for (int k = 0; k < kProbeGroups / 1024; ++k)
+    c += ((v[k].x | v[k].y | v[k].z | v[k].w) & 0xF000F000u) ? 1u : 0u;
+  if (c) atomicAdd(&cnt, c);
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = cnt;
 }
 
 // shape = -1: production (kWfThreads, kWfInv); 0..5: (256|512 threads) x
@@ -375,12 +416,23 @@ static void launch_welford_vec8(const uint16_t* sites, int64_t npx, int64_t n_si
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
                     double* part, size_t part_cap, int forced_parts,
-                    unsigned long long* wide, hipStream_t s, int shape) {
+                    unsigned long long* wide, unsigned int* probe, hipStream_t s, int shape) {
   if (n_sites <= 0) return;
   ProfScope prof("welford", s);
   const bool vec = (npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0;
   if (vec) {
-    const int f = part ? welford_parts(n_sites, npx, part_cap, forced_parts) : 1;
+    int f = part ? welford_parts(n_sites, npx, part_cap, forced_parts) : 1;
+    // automatic split (no forced parts, log transform): k_wf_probe decides on
+    // the device between one part and kWfBrightParts (>= 10% of the sampled
+    // groups hold a value >= 4,096)
+    const unsigned int* pr = nullptr;
+    const unsigned int pthr = kProbeGroups / 10;
+    if (probe && part && !forced_parts && log_transform && shape < 0 &&
+        welford_parts(n_sites, npx, part_cap, kWfBrightParts) == kWfBrightParts) {
+      hipLaunchKernelGGL(k_wf_probe, dim3(1), dim3(1024), 0, s, sites, npx >> 3, probe);
+      f = kWfBrightParts;
+      pr = probe;
+    }
     const int64_t per = cdiv(n_sites, f);
     const double nl = (double)n_sites, n = (double)(n0 + n_sites);
     const WfMerge mg{1.0 / nl, nl / n, (double)n0 * nl / n, n0 == 0};
@@ -391,7 +443,7 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
       case 3: launch_welford_vec8<512, 1>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       case 4: launch_welford_vec8<256, 2>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       case 5: launch_welford_vec8<512, 2>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
-      default: launch_welford_vec8<kWfThreads, kWfInv>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
+      default: launch_welford_vec8<kWfThreads, kWfInv>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s, pr, pthr); break;
     }
     if (f > 1) {
       WfParts pc{};
@@ -399,7 +451,7 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
       for (int p = 0; p < f; ++p)
         pc.cnt[p] = (double)std::min<int64_t>(per, n_sites - (int64_t)p * per);
       hipLaunchKernelGGL(k_wf_merge_parts, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, part,
-                         npx, pc, (double)n0, mean, m2);
+                         npx, pc, (double)n0, mean, m2, pr, pthr);
     }
   } else {  // the per-pixel Welford of odd shapes reads 1/n per site
     const dim3 grid((unsigned)cdiv(npx, kWfScalarThreads));

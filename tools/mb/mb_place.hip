@@ -143,7 +143,7 @@ int main(int argc, char** argv) {
   };
   auto welford = [&](int i) {
     return time([&] {
-      launch_welford(buf[i], npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 1, wide, 0);
+      launch_welford(buf[i], npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 1, wide, nullptr, 0);
     });
   };
   for (int i = 0; i < NB; ++i) printf("welford on buffer %d: %8.3f ms\n", i, welford(i));

@@ -399,14 +399,21 @@ int main(int argc, char** argv) {
       char nm[80];
       snprintf(nm, sizeof nm, "welford shape %d (%s) parts %d", shape, shapes[shape], f);
       time(nm, [&] {
-        launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, f, nullptr, 0, shape);
+        launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, f, nullptr, nullptr, 0, shape);
       });
     }
   time("wf f32 G2 blk16", [&] { hipLaunchKernelGGL((k_wf_f32<2, 16>), ag, dim3(256), 0, 0, in, npx, S, lut, mean); });
   time("wf f32 G2 blk32", [&] { hipLaunchKernelGGL((k_wf_f32<2, 32>), ag, dim3(256), 0, 0, in, npx, S, lut, mean); });
   time("wf f32 G4 blk16", [&] { hipLaunchKernelGGL((k_wf_f32<4, 16>), ag, dim3(256), 0, 0, in, npx, S, lut, mean); });
-  time("welford production (parts 1)", [&] {
-    launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 1, nullptr, 0);
-  });
+  unsigned int* probe;
+  CK(hipMalloc(&probe, 4));
+  for (int r = 0; r < 2; ++r) {
+    time("welford production (parts 1)", [&] {
+      launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 1, nullptr, nullptr, 0);
+    });
+    time("welford automatic (probe, 1 or 3 parts)", [&] {
+      launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 0, nullptr, probe, 0);
+    });
+  }
   return 0;
 }
