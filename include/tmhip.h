@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define TMH_ABI_VERSION 2
+#define TMH_ABI_VERSION 3
 
 #define TMH_OK 0
 #define TMH_EINVAL (-22)  /* bad argument: maps to ValueError / TypeError */
@@ -80,23 +80,41 @@ int tmh_stats_set_stream(tmh_stats* h, void* stream);
  * handle's zero-maintained histogram slabs if a fused pass was interrupted. */
 int tmh_stats_reset(tmh_stats* h);
 
-/* Launch-shape options of a handle (results never depend on them):
+/* Options of a handle (results never depend on them):
  *   TMH_OPT_FUSED_CONFIG   0..4: (sites per unit, threads, LDS bins) of the
  *                          fused correct+histogram pass = (2, 1024, 32768),
  *                          (4, 1024, 32768), (2, 512, 16384), (4, 512, 16384),
- *                          (1, 1024, 32768); -1 (default): per launch, on the
- *                          device, 3 unless the Welford pass over the pending
- *                          sites saw >= 2% of 8-pixel groups holding a value
- *                          >= 4,096, then 0.  Results are identical for all.
- *   TMH_OPT_WELFORD_PARTS  0: automatic (one part); 1..4: split a Welford
- *                          launch's sites into that many parts, merged in
- *                          order, where the launch has >= 32 sites a part
+ *                          (1, 1024, 32768).  -1 (default): chosen per launch
+ *                          on the device from the Welford pass's counts over
+ *                          the pending sites -- 3; or 0 when >= 2% of the
+ *                          8-pixel groups hold a value >= 4,096; or, when
+ *                          >= 33% hold a value >= 16,384 ("very wide" sites,
+ *                          e.g. uniform 16-bit data), the pass runs without
+ *                          its histogram and a per-site u16-pair LDS
+ *                          histogram pass (one more read) builds them.
+ *   TMH_OPT_WELFORD_PARTS  0 (default): automatic -- a launch of >= 96 sites
+ *                          probes its first site on the device and splits
+ *                          into 3 site parts (merged in order) when >= 10% of
+ *                          the probed 8-pixel groups hold a value >= 4,096
+ *                          (bright sites: the log10 pass is VALU-bound),
+ *                          else runs as one part; 1..4: that many parts where
+ *                          the launch has >= 32 sites a part
  *   TMH_OPT_TAIL_CHUNKS    1..16: run the fused correct+histogram pass in that
  *                          many site chunks, each chunk's histogram finalize
- *                          overlapping the next chunk's streaming (1: off) */
+ *                          overlapping the next chunk's streaming (1: off)
+ *   TMH_OPT_COPY_THREADS   1..64 (default 8): host threads of the pageable <->
+ *                          pinned copies of the host-buffer entry points
+ *   TMH_OPT_HOST_STAGING   host-buffer entry points: 0 = the caller's buffers
+ *                          go straight to the copy engines; 1 = inputs AND
+ *                          outputs through pinned slots; 2 (default) =
+ *                          outputs only (the pageable H2D path is as fast as
+ *                          a pinned bounce; a pinned D2H slot copied out by
+ *                          several threads spreads a fresh output's faults) */
 #define TMH_OPT_FUSED_CONFIG 1
 #define TMH_OPT_WELFORD_PARTS 2
 #define TMH_OPT_TAIL_CHUNKS 3
+#define TMH_OPT_COPY_THREADS 4
+#define TMH_OPT_HOST_STAGING 5
 int tmh_stats_set_option(tmh_stats* h, int option, int value);
 
 /* update(image) for a run of sites.  zero_counts_out (host, n_sites, may be
@@ -147,6 +165,9 @@ int tmh_stats_site_order_stats(tmh_stats* h, int64_t site, uint16_t* host_vlo,
 /* ---- multi-GPU merge (one process per GPU; collectives done by the caller
  * over RCCL on the device buffers these functions fill/consume) --------- */
 int tmh_stats_get_n(tmh_stats* h, int64_t* n);
+/* The reference's plain attribute OnlineStatistics.n (stats.py:53): the count
+ * later Welford updates continue from and percentiles / var divide by. */
+int tmh_stats_set_n(tmh_stats* h, int64_t n);
 /* dev_nmean = n_r * mean_r (input of all_reduce(sum)) */
 int tmh_stats_merge_stage1(tmh_stats* h, double* dev_nmean, void* stream);
 /* mean = dev_sum_nmean / n_total; dev_m2c = M2_r + n_r * (mean_r - mean)^2 */
@@ -166,6 +187,11 @@ int tmh_stats_pct_accumulate(tmh_stats* h, double* dev_acc, void* stream);
 int tmh_stats_pct_accumulate_range(tmh_stats* h, double* dev_acc_range, int q_begin, int q_count,
                                    void* stream);
 int tmh_stats_set_pct_sum(tmh_stats* h, const double* dev_acc, void* stream);
+/* Device copy of the percentile sums (what tmh_stats_finalize's pct_sum
+ * returns; deferred mode: summed in site order first unless a chain result
+ * was installed), ordered on `stream` -- lets a pipelined caller keep a job's
+ * results before the handle is reused, without a host synchronisation. */
+int tmh_stats_get_pct_sum_device(tmh_stats* h, double* dev_acc, void* stream);
 /* Pooled 65,536-bin u64 histogram out of / into the handle (device buffers):
  * the histogram merge is get -> all_reduce(sum) -> set.  Sums of counts are
  * exact, so any reduction order gives the same bins. */
@@ -210,11 +236,13 @@ void tmh_corrector_destroy(tmh_corrector* c);
  * no synchronisation): one corrector serves every job of the same shape. */
 int tmh_corrector_update_device(tmh_corrector* c, const double* dev_mean, const double* dev_std,
                                 void* stream);
+/* Host-path options of a corrector: TMH_OPT_COPY_THREADS, TMH_OPT_HOST_STAGING
+ * (see tmh_stats_set_option). */
+int tmh_corrector_set_option(tmh_corrector* c, int option, int value);
 /* The two global means (np.mean(std), np.mean(mean), image.py:627). */
 int tmh_corrector_means(tmh_corrector* c, double* mean_of_std, double* mean_of_mean);
 /* Host buffers: chunks of <= 16 sites, H2D / kernel / D2H on three streams
- * with two device and two pinned output slots (TMH_HOST_STAGING=0: all
- * direct, =1: inputs through pinned slots too).  Returns when host_out is
+ * with two device and two pinned output slots (TMH_OPT_HOST_STAGING).  Returns when host_out is
  * complete; host_out must not overlap host_in. */
 int tmh_correct_u16(tmh_corrector* c, const uint16_t* host_in, uint16_t* host_out,
                     int64_t n_sites, int clip_lo, int clip_hi);

@@ -107,6 +107,13 @@ def test_run_job_read_ahead_order(tmp_path, prefetch, batch):
                 assert np.array_equal(s, want[fid]), (rep, fid)
             got_ids += list(ids)
         assert got_ids == order
+    # two live generators on one calculator: each owns its buffers
+    g1, g2 = calc._blocks(order), calc._blocks(order[::-1])
+    for (i1, s1), (i2, s2) in zip(g1, g2):
+        for fid, s in zip(i1, s1):
+            assert np.array_equal(s, want[fid]), ("interleaved", fid)
+        for fid, s in zip(i2, s2):
+            assert np.array_equal(s, want[fid]), ("interleaved reverse", fid)
     # abandoning the generator early does not hang
     gen = calc._blocks(order)
     next(gen)

@@ -91,7 +91,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, name, out_dir):
+def _worker(rank, world, port, name, out_dir, staged=False):
     import sys
     sys.path.insert(0, REPO)
     from oracle import corilla_oracle as orc
@@ -110,17 +110,21 @@ def _worker(rank, world, port, name, out_dir):
     cls = WholeOps if name == "stats_small" and world == 2 else HostOps
     local_hist = sum((orc.histogram_u16(s) for s in mine), np.zeros(65536, np.uint64))
     ops = cls(st.n, st.mean, st._M2, [orc.percentile_linear(s, q) for s in mine], local_hist)
-    n_total = merge_shards(ops, dist)
+    if staged:  # the same merge through the host-staging facade (sharded.HostStagedDist)
+        from tmlibrary_amd.workflow.corilla.sharded import HostStagedDist
+        n_total = merge_shards(ops, HostStagedDist(dist))
+    else:
+        n_total = merge_shards(ops, dist)
     np.savez(os.path.join(out_dir, "r%d.npz" % rank), n=n_total, mean=ops.mean.numpy(),
              m2=ops.m2.numpy(), acc=ops.acc.numpy(), hist=ops.hist.numpy().astype(np.uint64))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,name", [(2, "stats_medium"), (2, "stats_small"),
-                                        (3, "stats_small")])
-def test_merge_shards_gloo(tmp_path, world, name):
+@pytest.mark.parametrize("world,name,staged", [(2, "stats_medium", False), (2, "stats_small", False),
+                                               (3, "stats_small", False), (2, "stats_medium", True)])
+def test_merge_shards_gloo(tmp_path, world, name, staged):
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, name, str(tmp_path)), nprocs=world,
+    mp.start_processes(_worker, args=(world, port, name, str(tmp_path), staged), nprocs=world,
                        join=True, start_method="spawn")
     g = load_golden(name)
     want_var = g["std"] ** 2

@@ -264,9 +264,14 @@ def test_corrector_cache_sees_in_place_writes(L):
     assert_dn(second, orc.correct_illumination(img, cont.mean.array, std))
     assert not np.array_equal(first, second)
     assert not cont.mean.array.flags.writeable  # protected again
+    old_mean = cont.mean.array
     cont.smooth()  # replaced planes: rebuilt
     third = corrected()
     assert_dn(third, orc.correct_illumination(img, cont.mean.array, cont.std.array))
+    assert old_mean.flags.writeable  # the replaced plane is unlocked again
+    cont.release()  # drops the corrector, the current planes are writeable again
+    assert cont.mean.array.flags.writeable and cont.std.array.flags.writeable
+    cont.mean.array[0, 0] += 0.0
 
 
 def test_correct_channel_mismatch(L):

@@ -136,17 +136,12 @@ struct PinBuf {
   ~PinBuf() { release(); }
 };
 
-// memcpy between pageable and pinned host memory, split over a few threads
-// (TMH_COPY_THREADS, default 8): one thread moves <= 30 GB/s and much less
-// into a fresh (unfaulted) numpy output, below a PCIe 5 x16 link.
-static void par_copy(void* dst, const void* src, size_t bytes) {
+// memcpy between pageable and pinned host memory, split over up to max_t
+// threads (TMH_OPT_COPY_THREADS, default 8): one thread moves <= 30 GB/s and
+// much less into a fresh (unfaulted) numpy output, below a PCIe 5 x16 link.
+static void par_copy(void* dst, const void* src, size_t bytes, int max_t) {
   const size_t min_part = (size_t)4 << 20;
-  static const size_t max_t = [] {
-    const char* e = std::getenv("TMH_COPY_THREADS");
-    const long v = e ? std::strtol(e, nullptr, 10) : 8;
-    return (size_t)std::min(64L, std::max(1L, v));
-  }();
-  size_t nt = std::min<size_t>(max_t, std::max<size_t>(1, bytes / min_part));
+  size_t nt = std::min<size_t>((size_t)std::max(1, max_t), std::max<size_t>(1, bytes / min_part));
   nt = std::min<size_t>(nt, std::max(1u, std::thread::hardware_concurrency()));
   if (nt <= 1) {
     std::memcpy(dst, src, bytes);
@@ -164,20 +159,32 @@ static void par_copy(void* dst, const void* src, size_t bytes) {
   for (auto& t : ts) t.join();
 }
 
-// Staging mode of the host-buffer entry points.  Measured on MI355X boxes
-// (tools/diag_host.py, bench extras.host_path): the runtime's own pageable
-// H2D path already reaches ~56 GB/s, above a pinned bounce fed by 8 host
-// threads, so inputs go straight from the caller's buffer; outputs land in
-// pinned slots and are copied out by several threads, which also spreads the
-// first-touch page faults of a fresh numpy output.
-// TMH_HOST_STAGING=0: everything direct; =1: inputs through pinned slots too.
-static int host_staging_mode() {
-  static const int mode = [] {
-    const char* e = std::getenv("TMH_HOST_STAGING");
-    return e && e[0] == '0' ? 0 : e && e[0] == '1' ? 1 : 2;
-  }();
-  return mode;
-}
+// Staging of the host-buffer entry points (TMH_OPT_HOST_STAGING).  Measured
+// on MI355X boxes (tools/diag_host.py, bench extras.host_path): the runtime's
+// own pageable H2D path already reaches ~56 GB/s, above a pinned bounce fed by
+// 8 host threads, so by default inputs go straight from the caller's buffer;
+// outputs land in pinned slots and are copied out by several threads, which
+// also spreads the first-touch page faults of a fresh numpy output.
+// 0: everything direct; 1: inputs through pinned slots too; 2 (default).
+constexpr int kStagingDirect = 0, kStagingPinnedIn = 1, kStagingPinnedOut = 2;
+
+struct HostOpts {
+  int copy_threads = 8;
+  int staging = kStagingPinnedOut;
+  bool set(int option, int value) {
+    if (option == TMH_OPT_COPY_THREADS) {
+      TMH_CHECK(value >= 1 && value <= 64, TMH_EINVAL, "copy threads must be 1..64");
+      copy_threads = value;
+      return true;
+    }
+    if (option == TMH_OPT_HOST_STAGING) {
+      TMH_CHECK(value >= 0 && value <= 2, TMH_EINVAL, "host staging must be 0, 1 or 2");
+      staging = value;
+      return true;
+    }
+    return false;
+  }
+};
 
 struct HostPipe {
   PinBuf in[2], out[2];
@@ -237,6 +244,7 @@ struct tmh_stats {
   int fused_cfg = kFusedAuto;     // TMH_OPT_FUSED_CONFIG (-1: per launch, on the device)
   int wf_parts = 0;               // TMH_OPT_WELFORD_PARTS (0: automatic)
   int tail_chunks = 1;            // TMH_OPT_TAIL_CHUNKS (1: no overlap)
+  HostOpts host;                  // TMH_OPT_COPY_THREADS / TMH_OPT_HOST_STAGING
   bool hist_dirty = false;        // a fused launch may have left counts / round masks behind
   int64_t n = 0;              // sites accumulated (Welford count)
   int64_t n_deferred = 0;     // sites whose order statistics are stored
@@ -282,6 +290,7 @@ struct tmh_corrector {
   DBuf<uint16_t> stage_in, stage_out;
   DBuf<uint8_t> stage8_in, stage8_out;
   HostPipe pipe;
+  HostOpts host;  // TMH_OPT_COPY_THREADS / TMH_OPT_HOST_STAGING
 };
 
 static hipStream_t pick(hipStream_t own, void* s) { return s ? (hipStream_t)s : own; }
@@ -473,7 +482,7 @@ int tmh_stats_set_option(tmh_stats* h, int option, int value) {
         h->tail_chunks = value;
         break;
       default:
-        throw Error{TMH_EINVAL, "unknown option"};
+        if (!h->host.set(option, value)) throw Error{TMH_EINVAL, "unknown option"};
     }
   });
 }
@@ -585,7 +594,7 @@ int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites, 
       h->stage.ensure(2 * slot_px);
     }
     p.init();
-    const bool pinned = host_staging_mode() == 1;
+    const bool pinned = h->host.staging == kStagingPinnedIn;
     // retire chunk k-2 of this slot: its H2D, kernels and zero-count copy
     auto retire = [&](int slot) {
       if (!p.busy[slot]) return;
@@ -605,7 +614,7 @@ int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites, 
         const void* src = host_sites + s0 * h->npx;
         if (pinned) {
           p.in[slot].ensure(slot_px * 2);
-          par_copy(p.in[slot].p, src, bytes);
+          par_copy(p.in[slot].p, src, bytes, h->host.copy_threads);
           src = p.in[slot].p;
         }
         uint16_t* dev = h->stage.p + (size_t)slot * slot_px;
@@ -744,6 +753,13 @@ int tmh_stats_get_n(tmh_stats* h, int64_t* n) {
   });
 }
 
+int tmh_stats_set_n(tmh_stats* h, int64_t n) {
+  return guard([&] {
+    TMH_CHECK(h && n >= 0, TMH_EINVAL, "bad arguments");
+    h->n = n;
+  });
+}
+
 int tmh_stats_merge_stage1(tmh_stats* h, double* dev_nmean, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_nmean, TMH_EINVAL, "bad arguments");
@@ -796,6 +812,28 @@ int tmh_stats_set_pct_sum(tmh_stats* h, const double* dev_acc, void* stream) {
     TMH_CHECK(h && dev_acc, TMH_EINVAL, "bad arguments");
     launch_copy_f64(dev_acc, h->acc.p, h->Q, pick(h->stream, stream));
     h->pct_sum_external = true;
+  });
+}
+
+int tmh_stats_get_pct_sum_device(tmh_stats* h, double* dev_acc, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && dev_acc, TMH_EINVAL, "bad arguments");
+    hipStream_t s = pick(h->stream, stream);
+    const bool cross = s != h->stream;
+    if (cross) {  // after the handle's queued work, and the handle waits for the copy
+      TMH_HIP(hipEventRecord(h->ev_in, h->stream));
+      TMH_HIP(hipStreamWaitEvent(s, h->ev_in, 0));
+    }
+    if ((h->flags & TMH_STATS_DEFERRED_PCT) && !h->pct_sum_external) {
+      TMH_HIP(hipMemsetAsync(dev_acc, 0, (size_t)h->Q * 8, s));
+      launch_pct_accumulate(h->vlh.p, h->n_deferred, h->vlh_cap, h->Q, h->gamma.p, dev_acc, s);
+    } else {
+      TMH_HIP(hipMemcpyAsync(dev_acc, h->acc.p, (size_t)h->Q * 8, hipMemcpyDeviceToDevice, s));
+    }
+    if (cross) {
+      TMH_HIP(hipEventRecord(h->ev_out, s));
+      TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
+    }
   });
 }
 
@@ -957,6 +995,13 @@ void tmh_corrector_destroy(tmh_corrector* c) {
   delete c;
 }
 
+int tmh_corrector_set_option(tmh_corrector* c, int option, int value) {
+  return guard([&] {
+    TMH_CHECK(c, TMH_EINVAL, "corrector is NULL");
+    if (!c->host.set(option, value)) throw Error{TMH_EINVAL, "unknown corrector option"};
+  });
+}
+
 int tmh_corrector_update_device(tmh_corrector* c, const double* dev_mean, const double* dev_std,
                                 void* stream) {
   return guard([&] {
@@ -1013,12 +1058,14 @@ int tmh_correct_u16(tmh_corrector* c, const uint16_t* host_in, uint16_t* host_ou
     }
     HostPipe& p = c->pipe;
     p.init();
-    const bool pinned_in = host_staging_mode() == 1, pinned_out = host_staging_mode() != 0;
+    const bool pinned_in = c->host.staging == kStagingPinnedIn,
+               pinned_out = c->host.staging != kStagingDirect;
     auto retire = [&](int slot) {
       if (!p.busy[slot]) return;
       TMH_HIP(hipEventSynchronize(p.ev_done[slot]));
       if (pinned_out)
-        par_copy(host_out + p.s0[slot] * c->npx, p.out[slot].p, (size_t)p.ns[slot] * c->npx * 2);
+        par_copy(host_out + p.s0[slot] * c->npx, p.out[slot].p, (size_t)p.ns[slot] * c->npx * 2,
+                 c->host.copy_threads);
       p.busy[slot] = false;
     };
     int64_t k = 0;
@@ -1032,7 +1079,7 @@ int tmh_correct_u16(tmh_corrector* c, const uint16_t* host_in, uint16_t* host_ou
         void* dst = host_out + s0 * c->npx;
         if (pinned_in) {
           p.in[slot].ensure(slot_px * 2);
-          par_copy(p.in[slot].p, src, bytes);
+          par_copy(p.in[slot].p, src, bytes, c->host.copy_threads);
           src = p.in[slot].p;
         }
         if (pinned_out) {

@@ -235,12 +235,22 @@ constexpr double kWideFrac = 0.02;
 // cost more than one more read of the sites); the fused pass then runs without
 // its histogram and k_hist_site_u16 builds the histograms
 constexpr double kXWideFrac = 0.33;
+// Blocked site layout: the sites of a launch live in blocks of 1 << shift
+// consecutive sites each (device arrays of block base pointers; in == null:
+// one contiguous run at the launch's in / out pointers).  A block holds a
+// multiple of every configuration's sites per unit (shift >= 2).
+struct SiteTab {
+  const uint16_t* const* in = nullptr;
+  uint16_t* const* out = nullptr;
+  int shift = 0;
+};
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, const FixList& fl,
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
                          unsigned long long* rmask, int* queues, int n_wg, int cfg,
                          const unsigned long long* wide, unsigned long long wide_thresh,
-                         unsigned long long xwide_thresh, hipStream_t s);
+                         unsigned long long xwide_thresh, hipStream_t s,
+                         const SiteTab& tab = SiteTab{});
 // illuminati chain (chain_kernels.hip)
 void launch_align(const void* in, void* out, int elem_bytes, int64_t n_sites, int H, int W, int oh,
                   int ow, const tmh_window* d_win, hipStream_t s);

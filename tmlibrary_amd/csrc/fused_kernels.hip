@@ -172,7 +172,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     int clip_lo, int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
     int n_bands, int* __restrict__ queues, const unsigned long long* __restrict__ wide,
     unsigned long long wide_lo, unsigned long long wide_hi, unsigned long long x_lo,
-    unsigned long long x_hi) {
+    unsigned long long x_hi, const SiteTab tab) {
   // launch-time selection (launch_correct_hist): this configuration runs only
   // when the Welford pass's counts of pixel groups with a value >= 4,096 and
   // >= 16,384 are in [wide_lo, wide_hi) and [x_lo, x_hi)
@@ -249,10 +249,15 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     r.ns = (int)(n_sites - r.s0 < SPU ? n_sites - r.s0 : SPU);
     r.g0 = (int)((int64_t)band * ngroups / n_bands);
     r.g1 = (int)((int64_t)(band + 1) * ngroups / n_bands);
-    r.rin = __builtin_amdgcn_make_buffer_rsrc((void*)(in + r.s0 * npx), 0, r.ns * site_bytes,
-                                              0x00020000);
-    r.rout = __builtin_amdgcn_make_buffer_rsrc((void*)(out + r.s0 * npx), 0, r.ns * site_bytes,
-                                               0x00020000);
+    const uint16_t* ib = in + r.s0 * npx;
+    uint16_t* ob = out + r.s0 * npx;
+    if (tab.in) {  // blocked layout: the unit's sites lie inside one block
+      const int64_t b = r.s0 >> tab.shift, o = (r.s0 & ((1ll << tab.shift) - 1)) * npx;
+      ib = tab.in[b] + o;
+      ob = tab.out[b] + o;
+    }
+    r.rin = __builtin_amdgcn_make_buffer_rsrc((void*)ib, 0, r.ns * site_bytes, 0x00020000);
+    r.rout = __builtin_amdgcn_make_buffer_rsrc((void*)ob, 0, r.ns * site_bytes, 0x00020000);
     return r;
   };
   auto load = [&](const Unit& un, int g, uint4 (&v)[SPU], float4 (&c)[4]) {
@@ -420,7 +425,7 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
                                     unsigned long long* rmask, int* queues, int n_wg, int cfg,
                                     const unsigned long long* wide, unsigned long long wide_lo,
                                     unsigned long long wide_hi, unsigned long long x_lo,
-                                    unsigned long long x_hi, hipStream_t s) {
+                                    unsigned long long x_hi, hipStream_t s, const SiteTab& tab) {
 #define TMH_LAUNCH_CH(L_, K_, A_)                                                                \
   {                                                                                              \
     constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
@@ -429,12 +434,12 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
       hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, A_, c.threads, c.lds_bins>), grid,    \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
                          clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
-                         wide_hi, x_lo, x_hi);                                                   \
+                         wide_hi, x_lo, x_hi, tab);                                              \
     else                                                                                         \
       hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, A_, c.threads, c.lds_bins>), grid,   \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
                          clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
-                         wide_hi, x_lo, x_hi);                                                   \
+                         wide_hi, x_lo, x_hi, tab);                                              \
   }
 #define TMH_LAUNCH_CFG(L_)                                     \
   switch (cfg) {                                               \
@@ -466,7 +471,7 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
                          unsigned long long* rmask, int* queues, int n_wg, int cfg,
                          const unsigned long long* wide, unsigned long long wide_thresh,
-                         unsigned long long xwide_thresh, hipStream_t s) {
+                         unsigned long long xwide_thresh, hipStream_t s, const SiteTab& tab) {
   if (n_sites <= 0) return;
   ProfScope prof("correct_hist", s);
   // queues[0..8): per-XCD unit counters; queues[8..10): the union of the
@@ -478,16 +483,16 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
   if (cfg >= 0 || !wide) {
     launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo,
                             clip_hi, hist, rmask, queues, n_wg, cfg >= 0 ? cfg : kFusedNarrow,
-                            nullptr, 0, 0, 0, 0, s);
+                            nullptr, 0, 0, 0, 0, s, tab);
     return;
   }
   const unsigned long long X = xwide_thresh;
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedNarrow, wide, 0, wide_thresh, 0, X, s);
+                          hist, rmask, queues, n_wg, kFusedNarrow, wide, 0, wide_thresh, 0, X, s, tab);
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedWide, wide, wide_thresh, ~0ull, 0, X, s);
+                          hist, rmask, queues, n_wg, kFusedWide, wide, wide_thresh, ~0ull, 0, X, s, tab);
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedNoHist, wide, 0, ~0ull, X, ~0ull, s);
+                          hist, rmask, queues, n_wg, kFusedNoHist, wide, 0, ~0ull, X, ~0ull, s, tab);
 }
 
 }  // namespace tmh

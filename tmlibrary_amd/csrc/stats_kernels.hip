@@ -761,6 +761,8 @@ __device__ __forceinline__ void hist_tail_rounds(unsigned long long need, CountF
 #pragma unroll
   for (int k = 0; k < kBins / LEN; ++k)
     if ((need >> (k * SR)) & ((SR == 64 ? 0ull : (1ull << SR)) - 1ull)) sneed |= 1ull << k;
+  // bin 0 lies in super-round 0: a site whose masks skip it has no zeros
+  if (zero_counts && tid == 0 && !(sneed & 1ull)) zero_counts[s] = 0;
   // this thread's bins lie in round (k * SR + tid * BPT / kRound) of super-round k
   auto load = [&](int k, uint32_t (&c)[BPT]) {
     const uint32_t b0 = (uint32_t)k * LEN + tid * BPT;

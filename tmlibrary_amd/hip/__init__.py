@@ -26,10 +26,12 @@ TMH_STATS_SERIAL = 4
 TMH_OPT_FUSED_CONFIG = 1
 TMH_OPT_WELFORD_PARTS = 2
 TMH_OPT_TAIL_CHUNKS = 3
+TMH_OPT_COPY_THREADS = 4
+TMH_OPT_HOST_STAGING = 5
 TMH_SYNTH_STANDARD = 0
 TMH_SYNTH_BRIGHT = 1
 TMH_SYNTH_UNIFORM = 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _P = C.c_void_p
 _I64 = C.c_int64
@@ -60,18 +62,21 @@ SIGNATURES = {
     "tmh_stats_site_histogram": (_I, [_P, _I64, _P]),
     "tmh_stats_site_order_stats": (_I, [_P, _I64, _P, _P]),
     "tmh_stats_get_n": (_I, [_P, C.POINTER(_I64)]),
+    "tmh_stats_set_n": (_I, [_P, _I64]),
     "tmh_stats_merge_stage1": (_I, [_P, _P, _P]),
     "tmh_stats_merge_stage2": (_I, [_P, _P, _I64, _P, _P]),
     "tmh_stats_merge_stage3": (_I, [_P, _I64, _P, _P]),
     "tmh_stats_pct_accumulate": (_I, [_P, _P, _P]),
     "tmh_stats_pct_accumulate_range": (_I, [_P, _P, _I, _I, _P]),
     "tmh_stats_set_pct_sum": (_I, [_P, _P, _P]),
+    "tmh_stats_get_pct_sum_device": (_I, [_P, _P, _P]),
     "tmh_smooth_f64": (_I, [_P, _P, _I, _I, _D]),
     "tmh_smooth_f64_device": (_I, [_P, _P, _P, _I, _I, _D, _P]),
     "tmh_corrector_create": (_I, [_P, _P, _I, _I, _I, _D, C.POINTER(_P)]),
     "tmh_corrector_create_device": (_I, [_P, _P, _I, _I, _I, _D, _P, C.POINTER(_P)]),
     "tmh_corrector_destroy": (None, [_P]),
     "tmh_corrector_update_device": (_I, [_P, _P, _P, _P]),
+    "tmh_corrector_set_option": (_I, [_P, _I, _I]),
     "tmh_corrector_means": (_I, [_P, C.POINTER(_D), C.POINTER(_D)]),
     "tmh_correct_u16": (_I, [_P, _P, _P, _I64, _I, _I]),
     "tmh_correct_u16_device": (_I, [_P, _P, _P, _I64, _I, _I, _P]),

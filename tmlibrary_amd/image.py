@@ -417,6 +417,8 @@ class IllumstatsContainer(object):
         self.percentiles = percentiles
         self._corr = None
         self._corr_key = None
+        self._corr_arrays = None
+        self._corr_locked = []
 
     def smooth(self, sigma=5):
         """Gaussian-smooth mean and std in place (image.py:1172-1193)."""
@@ -437,20 +439,44 @@ class IllumstatsContainer(object):
         """Cached device corrector for the current mean/std planes.
 
         The cache is keyed on the plane objects AND their contents: building
-        the corrector marks both arrays read-only, so an in-place write into
-        ``mean.array`` / ``std.array`` raises instead of leaving stale device
-        coefficients behind.  Replacing a plane (``smooth`` does) or making it
-        writeable again (``arr.flags.writeable = True``, then writing) makes
-        the next call rebuild the corrector from the current values."""
+        the corrector marks both arrays read-only (those that were writeable),
+        so an in-place write into ``mean.array`` / ``std.array`` raises
+        instead of leaving stale device coefficients behind.  Replacing a
+        plane (``smooth`` does) or making it writeable again
+        (``arr.flags.writeable = True``, then writing) makes the next call
+        rebuild the corrector from the current values.  ``release()`` (also
+        run when the container is collected) drops the corrector and makes
+        the arrays this container locked writeable again."""
         m, s = self.mean.array, self.std.array
         key = (id(m), id(s), bool(log_transform))
         if (self._corr is None or self._corr_key != key or m.flags.writeable or
                 s.flags.writeable):
-            if self._corr is not None:
-                self._corr.close()
+            self.release()
             self._corr = Corrector(m, s, log_transform)
             self._corr_key = key
             self._corr_arrays = (m, s)  # keep the ids valid while cached
-            m.flags.writeable = False
-            s.flags.writeable = False
+            self._corr_locked = [a for a in (m, s) if a.flags.writeable]
+            for a in self._corr_locked:
+                a.flags.writeable = False
         return self._corr
+
+    def release(self):
+        """Drop the cached device corrector; the planes it locked are
+        writeable again (the reference's planes are plain arrays)."""
+        if self._corr is not None:
+            self._corr.close()
+        self._corr = None
+        self._corr_key = None
+        self._corr_arrays = None
+        for a in self._corr_locked:
+            try:
+                a.flags.writeable = True
+            except ValueError:  # a view of a read-only base: leave it
+                pass
+        self._corr_locked = []
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass

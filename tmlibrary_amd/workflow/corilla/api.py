@@ -66,7 +66,8 @@ class IllumstatsCalculator(object):
         self.batch_size = batch_size
         self.prefetch = prefetch
         self.decode_threads = decode_threads
-        self._buffers = {}  # (block, H, W, dtype) -> reused block buffers
+        self._buffers = {}  # (block, H, W, dtype) -> reused block buffers (idle sets)
+        self._buffers_lock = threading.Lock()
 
     def create_run_batches(self, args=None, channel_files=None, channel_names=None, seed=None):
         """One job per channel (corilla/api.py:45-105).
@@ -110,7 +111,13 @@ class IllumstatsCalculator(object):
         the next blocks overlaps the GPU update of the current one and no
         block pays fresh-page faults.  A worker takes a free buffer BEFORE it
         claims the next block index: buffers then go to blocks in order and a
-        run-ahead worker can never hold the buffer the next block needs."""
+        run-ahead worker can never hold the buffer the next block needs.
+
+        A yielded array is a view of a reused buffer: it is valid until the
+        generator is resumed.  Each live generator owns its buffer set (taken
+        from the calculator's idle sets under a lock and given back when it
+        ends), so concurrent run_job calls or a caller that keeps an earlier
+        generator open never share buffers."""
         step = max(1, self.batch_size)
         blocks = [file_ids[i:i + step] for i in range(0, len(file_ids), step)]
         if not blocks:
@@ -123,7 +130,9 @@ class IllumstatsCalculator(object):
         # the block buffers are kept on the calculator: pinning ~0.35 GB per
         # buffer costs more than decoding a short job
         key = (step, H, W, np.dtype(dt).str)
-        bufs = self._buffers.setdefault(key, [])
+        with self._buffers_lock:  # this generator's own set (another may be live)
+            sets = self._buffers.get(key, [])
+            bufs = sets.pop() if sets else []
         while len(bufs) < min(inflight + 1, len(blocks)):
             bufs.append(_block_buffer(step, H, W, dt))
         pool = queue.Queue()
@@ -171,6 +180,8 @@ class IllumstatsCalculator(object):
                 pool.put(None)  # wake workers waiting for a buffer
             for t in threads:
                 t.join()
+            with self._buffers_lock:  # idle again: the next generator may reuse it
+                self._buffers.setdefault(key, []).append(bufs)
 
     def run_job(self, batch, assume_clean_state=False):
         """corilla/api.py:115-146."""

@@ -67,8 +67,7 @@ class GpuChannelStats(object):
         ops = StatsOps(hip.lib(), st._h, h * w, len(st._q), dev)
         n_total = merge_shards(ops, dist, group, int_device=dev)
         torch.cuda.current_stream(dev).synchronize()
-        st._n_flushed = n_total  # the merged state is the whole channel's
-        st._cache = None
+        st.refresh()  # the handle holds the whole channel's merged state (n = n_total)
         self.histogram = st.histogram  # pooled over every rank's sites
         return n_total
 

@@ -97,6 +97,48 @@ class StatsOps(object):
                                                    self._stream()))
 
 
+class HostStagedDist(object):
+    """``torch.distributed`` facade that runs the merge collectives of device
+    buffers on a CPU (gloo) process group: each call copies the buffer to
+    host memory (``Tensor.cpu()`` waits for torch's current stream, where the
+    StatsOps launches were queued), runs the gloo collective and copies the
+    result back on the current stream.  For ranks that share one GPU -- RCCL
+    needs a GPU per rank -- and for hosts without RCCL; ``merge_welford`` /
+    ``merge_counts`` / ``merge_shards`` take it in place of the module."""
+
+    def __init__(self, dist):
+        self._d = dist
+        self.ReduceOp = dist.ReduceOp
+
+    def get_rank(self, group=None):
+        return self._d.get_rank(group)
+
+    def get_world_size(self, group=None):
+        return self._d.get_world_size(group)
+
+    def barrier(self, group=None):
+        self._d.barrier(group=group)
+
+    def all_reduce(self, t, op=None, group=None):
+        h = t.cpu()
+        self._d.all_reduce(h, op=self._d.ReduceOp.SUM if op is None else op, group=group)
+        t.copy_(h)
+
+    def send(self, t, dst, group=None):
+        self._d.send(t.cpu(), dst=dst, group=group)
+
+    def recv(self, t, src, group=None):
+        import torch
+        h = torch.empty(t.shape, dtype=t.dtype)
+        self._d.recv(h, src=src, group=group)
+        t.copy_(h)
+
+    def broadcast(self, t, src, group=None):
+        h = t.cpu()
+        self._d.broadcast(h, src=src, group=group)
+        t.copy_(h)
+
+
 def merge_welford(ops, dist, group=None, int_device=None, n_total=None):
     """All-reduce merge of every rank's Welford state (identical on all ranks).
     Returns the global site count.  ``n_total`` (optional) is the global site

@@ -55,7 +55,6 @@ class OnlineStatistics(object):
         self._stage = np.empty((self._batch_size, h, w), dtype=np.uint16)
         self._staged = 0
         self._staged_log = None
-        self._n_flushed = 0
         self._cache = None
         L = hip.lib()
         handle = C.c_void_p()
@@ -69,8 +68,26 @@ class OnlineStatistics(object):
     # -- reference attributes ---------------------------------------------------
     @property
     def n(self):
-        """Number of sites accumulated (stats.py:53, :89)."""
-        return self._n_flushed + self._staged
+        """Number of sites accumulated (stats.py:53, :89): the handle's count
+        plus the sites still staged on the host."""
+        c = C.c_int64()
+        hip.check(hip.lib().tmh_stats_get_n(self._h, C.byref(c)))
+        return c.value + self._staged
+
+    @n.setter
+    def n(self, value):
+        """The reference's ``n`` is a plain attribute (stats.py:53): setting
+        it changes the count later updates continue from and the divisor of
+        ``var`` / ``percentiles``.  Staged sites are flushed first."""
+        self._flush()
+        hip.check(hip.lib().tmh_stats_set_n(self._h, int(value)))
+        self._cache = None
+
+    def refresh(self):
+        """Forget cached results: the handle's state was changed through the
+        C-ABI (e.g. the multi-GPU merge, sharded.merge_shards)."""
+        self._flush()
+        self._cache = None
 
     def update(self, image, log_transform=True):
         """Add one site (stats.py:64-92)."""
@@ -109,7 +126,6 @@ class OnlineStatistics(object):
         zeros = np.zeros(n, dtype=np.int64)
         hip.check(hip.lib().tmh_stats_update(self._h, hip.ptr(sites), n, int(log_transform),
                                              hip.ptr(zeros)))
-        self._n_flushed += n
         self._cache = None
         if log_transform:
             for _ in range(int(np.count_nonzero(zeros))):

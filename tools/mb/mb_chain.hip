@@ -37,7 +37,7 @@ __global__ void k_sum(const uint8_t* __restrict__ p, int64_t n, unsigned long lo
   atomicAdd(out, t);
 }
 
-int main(int argc, char** argv) {
+static int run(int argc, char** argv) {
   const int64_t S = argc > 1 ? atoll(argv[1]) : 3456;
   const int reps = argc > 2 ? atoi(argv[2]) : 3;
   const int H = 2160, W = 2560;
@@ -140,4 +140,15 @@ int main(int argc, char** argv) {
   });
   printf("done\n");
   return 0;
+}
+
+// a library check or HIP call that fails throws tmh::Error: print its message
+// (which names the failing call) instead of dying in std::terminate
+int main(int argc, char** argv) {
+  try {
+    return run(argc, argv);
+  } catch (const tmh::Error& e) {
+    fprintf(stderr, "tmh::Error %d: %s\n", e.code, e.msg.c_str());
+    return 1;
+  }
 }

@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void k_read(const uint4* __restrict__ p, int64
   if (acc == 0x9u) sink[0] = acc;
 }
 
-int main(int argc, char** argv) {
+static int run(int argc, char** argv) {
   const int64_t S = argc > 1 ? atoll(argv[1]) : 3456;
   const int reps = argc > 2 ? atoi(argv[2]) : 3;
   const int H = argc > 3 ? atoi(argv[3]) : 2160, W = argc > 4 ? atoi(argv[4]) : 2560;
@@ -156,7 +156,7 @@ int main(int argc, char** argv) {
     CK(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), 0));
     hipLaunchKernelGGL((k_correct_hist<true, false, 4, ABL, 512, 16384>), fg, fb, 0, 0, in, out,
                        npx, S, coef, mconst2, fl, -1, -1, hist, rmask, kFusedBands, queues,
-                       nullptr, 0ull, 0ull, 0ull, 0ull);
+                       nullptr, 0ull, 0ull, 0ull, 0ull, SiteTab{});
   };
   time("fused prod (ABL 0)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 0>()); });
   time("fused no hist (ABL 1)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 1>()); });
@@ -183,4 +183,15 @@ int main(int argc, char** argv) {
     });
   }
   return 0;
+}
+
+// a library check or HIP call that fails throws tmh::Error: print its message
+// (which names the failing call) instead of dying in std::terminate
+int main(int argc, char** argv) {
+  try {
+    return run(argc, argv);
+  } catch (const tmh::Error& e) {
+    fprintf(stderr, "tmh::Error %d: %s\n", e.code, e.msg.c_str());
+    return 1;
+  }
 }

@@ -36,7 +36,7 @@ ProfScope::~ProfScope() {}
 }  // namespace tmh
 using namespace tmh;
 
-int main(int argc, char** argv) {
+static int run(int argc, char** argv) {
   const int64_t S = argc > 1 ? atoll(argv[1]) : 3456;
   const int NB = argc > 2 ? atoi(argv[2]) : 6;
   const int reps = argc > 3 ? atoi(argv[3]) : 3;
@@ -164,4 +164,15 @@ int main(int argc, char** argv) {
   }
   printf("done\n");
   return 0;
+}
+
+// a library check or HIP call that fails throws tmh::Error: print its message
+// (which names the failing call) instead of dying in std::terminate
+int main(int argc, char** argv) {
+  try {
+    return run(argc, argv);
+  } catch (const tmh::Error& e) {
+    fprintf(stderr, "tmh::Error %d: %s\n", e.code, e.msg.c_str());
+    return 1;
+  }
 }

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(NT) void k_team(const uint16_t* __restrict__ in, ui
   }
 }
 
-int main(int argc, char** argv) {
+static int run(int argc, char** argv) {
   const int64_t S = argc > 1 ? atoll(argv[1]) : 3456;
   const int reps = argc > 2 ? atoi(argv[2]) : 3;
   const int H = 2160, W = 2560;
@@ -165,7 +165,7 @@ int main(int argc, char** argv) {
     CK(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), 0));
     hipLaunchKernelGGL((k_correct_hist<true, false, 4, ABL, 512, 16384>), dim3(cus * 2), dim3(512), 0, 0,
                        in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, queues,
-                       nullptr, 0ull, 0ull, 0ull, 0ull);
+                       nullptr, 0ull, 0ull, 0ull, 0ull, SiteTab{});
   };
   char nm[96];
   for (int b : {16, 8, 12, 24, 32, 64}) {
@@ -180,7 +180,7 @@ int main(int argc, char** argv) {
       CK(hipMemsetAsync(fn, 0, 4, 0));
       CK(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), 0));
       hipLaunchKernelGGL((k_correct_hist<true, false, SPU_, 0, NT_, LB_>), dim3(grid), dim3(NT_), 0, 0,
-                         in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, queues, nullptr, 0ull, 0ull, 0ull, 0ull);
+                         in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, queues, nullptr, 0ull, 0ull, 0ull, 0ull, SiteTab{});
     });
   };
   using C8 = std::integral_constant<int, 8>;
@@ -248,4 +248,15 @@ int main(int argc, char** argv) {
   });
   printf("done\n");
   return 0;
+}
+
+// a library check or HIP call that fails throws tmh::Error: print its message
+// (which names the failing call) instead of dying in std::terminate
+int main(int argc, char** argv) {
+  try {
+    return run(argc, argv);
+  } catch (const tmh::Error& e) {
+    fprintf(stderr, "tmh::Error %d: %s\n", e.code, e.msg.c_str());
+    return 1;
+  }
 }

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void k_pct_acc_u(const uint32_t* __restrict__ 
   acc[q] = a;
 }
 
-int main(int argc, char** argv) {
+static int run(int argc, char** argv) {
   const int64_t S = argc > 1 ? atoll(argv[1]) : 3456;
   const int reps = argc > 2 ? atoi(argv[2]) : 5;
   const int dist = argc > 3 ? atoi(argv[3]) : 0;
@@ -202,4 +202,15 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   printf("done\n");
   return 0;
+}
+
+// a library check or HIP call that fails throws tmh::Error: print its message
+// (which names the failing call) instead of dying in std::terminate
+int main(int argc, char** argv) {
+  try {
+    return run(argc, argv);
+  } catch (const tmh::Error& e) {
+    fprintf(stderr, "tmh::Error %d: %s\n", e.code, e.msg.c_str());
+    return 1;
+  }
 }

@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256) void k_read(const uint4* __restrict__ p, int64
   if (acc == 0x9u) sink[0] = acc;
 }
 
-int main(int argc, char** argv) {
+static int run(int argc, char** argv) {
   const int64_t S = argc > 1 ? atoll(argv[1]) : 3456;
   const int reps = argc > 2 ? atoi(argv[2]) : 3;
   const int H = 2160, W = 2560;
@@ -416,4 +416,15 @@ int main(int argc, char** argv) {
     });
   }
   return 0;
+}
+
+// a library check or HIP call that fails throws tmh::Error: print its message
+// (which names the failing call) instead of dying in std::terminate
+int main(int argc, char** argv) {
+  try {
+    return run(argc, argv);
+  } catch (const tmh::Error& e) {
+    fprintf(stderr, "tmh::Error %d: %s\n", e.code, e.msg.c_str());
+    return 1;
+  }
 }
