@@ -84,6 +84,9 @@ def parse():
     p.add_argument("--fused-config", type=int, default=None,
                    help="fused pass (sites per unit, threads, LDS bins) configuration 0..3 "
                         "(TMH_OPT_FUSED_CONFIG; default: the library's)")
+    p.add_argument("--block-sites", type=int, default=64,
+                   help="sites per HBM allocation (a power of two >= 4; blocked site layout, input "
+                        "and output blocks allocated alternately); 0: one contiguous buffer each")
     p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
     p.add_argument("--pipeline", choices=["fused", "separate"], default="fused",
                    help="fused: histograms built from the correction's read (6 B/px); "
@@ -645,14 +648,33 @@ def main():
     torch.cuda.set_stream(stream)
     sp = C.c_void_p(stream.cuda_stream)
 
-    # resident inputs / outputs (int16 tensors = raw uint16 bytes); channel c
-    # owns local rows [c*S, (c+1)*S) = its global sites [s_begin, s_end)
+    # resident inputs / outputs (int16 tensors = raw uint16 bytes) of channel c
+    # = its global sites [s_begin, s_end): one contiguous buffer each, or
+    # (--block-sites B) blocks of B sites in separate allocations, input and
+    # output blocks allocated alternately.  The fused pass's speed depends on
+    # which HBM region holds its 38 GB output (12.8-15.2 ms for the same job
+    # on different buffers of one process; blocks ran 13.1 on every draw:
+    # DESIGN.md §3, profiles/r3/mb_place2_r3a.txt).
     dist_id = DISTRIBUTIONS[a.distribution]
-    sites = torch.empty((CH * S, H, W), dtype=torch.int16, device=dev)
-    out = torch.empty_like(sites)
+    B = a.block_sites if a.pipeline == "fused" else 0  # the separate pipeline is contiguous
+    if B:
+        assert B >= 4 and B & (B - 1) == 0, "--block-sites must be a power of two >= 4"
+    shift = B.bit_length() - 1 if B else 0
+    chan_sites = []  # per channel: (input blocks, output blocks); one block if contiguous
     for c in range(CH):
-        hip.check(L.tmh_synth_sites_device(C.c_void_p(sites[c * S].data_ptr()), S, H, W, SEED, c,
-                                           s_begin, dist_id, sp))
+        blk_in, blk_out = [], []
+        for b0 in range(0, S, B if B else S):
+            m = min(B, S - b0) if B else S
+            blk_in.append(torch.empty((m, H, W), dtype=torch.int16, device=dev))
+            blk_out.append(torch.empty((m, H, W), dtype=torch.int16, device=dev))
+            hip.check(L.tmh_synth_sites_device(C.c_void_p(blk_in[-1].data_ptr()), m, H, W, SEED, c,
+                                               s_begin + b0, dist_id, sp))
+        chan_sites.append((blk_in, blk_out))
+
+    def local_site(c, i, outputs=False):
+        """channel c's local site i (input or corrected output) as a tensor view"""
+        blks = chan_sites[c][1 if outputs else 0]
+        return blks[i // B][i % B] if B else blks[0][i]
     lo, hi, gamma = quantile_table(npx, np.linspace(0, 100, Q))
     lut = stats_log10_lut()
     flags = hip.TMH_STATS_DEFERRED_PCT if dist_on else 0
@@ -669,8 +691,17 @@ def main():
         def __init__(self, c):
             self.stream = stream if c == 0 else torch.cuda.Stream(dev)
             self.sp = C.c_void_p(self.stream.cuda_stream)
-            self.S_ptr = C.c_void_p(sites[c * S].data_ptr())
-            self.O_ptr = C.c_void_p(out[c * S].data_ptr())
+            blk_in, blk_out = chan_sites[c]
+            self.blocks = (blk_in, blk_out)
+            self.S_ptr = C.c_void_p(blk_in[0].data_ptr())
+            self.O_ptr = C.c_void_p(blk_out[0].data_ptr())
+            if B:  # device tables of the block base pointers
+                self.t_in = torch.tensor([t.data_ptr() for t in blk_in], dtype=torch.int64,
+                                         device=dev)
+                self.t_out = torch.tensor([t.data_ptr() for t in blk_out], dtype=torch.int64,
+                                          device=dev)
+                self.T_in = C.c_void_p(self.t_in.data_ptr())
+                self.T_out = C.c_void_p(self.t_out.data_ptr())
             self.mean = torch.empty(npx, dtype=torch.float64, device=dev)
             self.std = torch.empty_like(self.mean)
             self.smean = torch.empty_like(self.mean)
@@ -694,7 +725,10 @@ def main():
 
         def stats(self):
             hip.check(L.tmh_stats_reset(self.h))
-            if fused:  # Welford pass; histograms come from the correction's read
+            if fused and B:  # Welford pass; histograms come from the correction's read
+                hip.check(L.tmh_stats_update_welford_blocks_device(self.h, self.T_in, shift, S, 1,
+                                                                   self.sp))
+            elif fused:
                 hip.check(L.tmh_stats_update_welford_device(self.h, self.S_ptr, S, 1, self.sp))
             else:
                 hip.check(L.tmh_stats_update_device(self.h, self.S_ptr, S, 1, self.sp))
@@ -708,7 +742,11 @@ def main():
                                               self.sp))
             hip.check(L.tmh_corrector_update_device(self.corr, p(self.smean), p(self.sstd),
                                                     self.sp))
-            if fused:
+            if fused and B:
+                hip.check(L.tmh_correct_u16_hist_blocks_device(self.corr, self.h, self.T_in,
+                                                               self.T_out, shift, S, -1, -1,
+                                                               self.sp))
+            elif fused:
                 hip.check(L.tmh_correct_u16_hist_device(self.corr, self.h, self.S_ptr, self.O_ptr,
                                                         S, -1, -1, self.sp))
             else:
@@ -807,7 +845,7 @@ def main():
     fp, fp_path = load_fingerprint(H, W, S_total, a.distribution)
     check_ok = None
     if fp is not None and n_channel == S_total and fused:
-        held = {s: out[s - s_begin].cpu().numpy().view(np.uint16)
+        held = {s: local_site(0, s - s_begin, outputs=True).cpu().numpy().view(np.uint16)
                 for s in fp["corr_sites"].tolist() if s_begin <= s < s_end}
         oks, cnt = check_against_fingerprint(fp, res, ch0.smean.cpu().numpy(),
                                              ch0.sstd.cpu().numpy(), held)
@@ -831,7 +869,14 @@ def main():
     log("%.1f ms/step; check_vs_oracle %s" % (1e3 * elapsed / a.steps, check_ok))
     extras = {}
     if not a.no_extras and world == 1:
-        extras["chain_u8"] = bench_chain(L, ch0.corr, ch0.S_ptr, S, H, W, dev, sp)
+        # the chain pass reads one contiguous run of sites
+        if B:
+            flat = torch.cat(chan_sites[0][0])
+            extras["chain_u8"] = bench_chain(L, ch0.corr, C.c_void_p(flat.data_ptr()), S, H, W,
+                                             dev, sp)
+            del flat
+        else:
+            extras["chain_u8"] = bench_chain(L, ch0.corr, ch0.S_ptr, S, H, W, dev, sp)
         extras["host_path"] = bench_host_path(H, W)
 
     if rank == 0:
@@ -909,7 +954,9 @@ def main():
                        "parallelism": ("sites sharded (contiguous); RCCL all-reduce Welford "
                                        "merge, ordered percentile chain, histogram all-reduce")
                        if dist_on else "single GPU",
-                       "pipeline": a.pipeline},
+                       "pipeline": a.pipeline,
+                       "hbm_layout": ("blocks of %d sites, input and output blocks allocated "
+                                      "alternately" % B) if B else "contiguous"},
             "job_hbm_roofline_frac": round(job_bytes * a.steps / elapsed / 1e9 /
                                            (HBM_PEAK_GBS * world), 4),
             "roofline": roofline,

@@ -138,6 +138,20 @@ int tmh_stats_update_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_s
 int tmh_stats_update_welford_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
                                     int log_transform, void* stream);
 
+/* Blocked site layout (device entry points below): the n_sites sites, in
+ * site order, live in blocks of 2^block_shift consecutive sites (2 <= shift
+ * <= 24; the last block may be partial), block b at dev_blocks[b] -- a DEVICE
+ * array of device pointers, 16-byte aligned (hipMalloc's are), owned by the
+ * caller.  Sites that arrive one file at a time need not be copied into one
+ * allocation, and a job's 38 GB of sites and outputs spread over many
+ * allocations: the fused pass's speed depended on which 38 GB buffer held its
+ * output (12.8-15.2 ms on one box; blocks of 4-64 sites allocated in- and
+ * output alternately ran 13.1 on every draw).  Results are
+ * identical to the contiguous entry points.  Needs height*width % 8 == 0. */
+int tmh_stats_update_welford_blocks_device(tmh_stats* h, const uint16_t* const* dev_blocks,
+                                           int block_shift, int64_t n_sites, int log_transform,
+                                           void* stream);
+
 /* Host copies of the results; any output may be NULL.
  *   n            sites accumulated (stats.py:89)
  *   mean, std    [height*width] f64; std is NaN where n < 2 (stats.py:94-112)
@@ -256,6 +270,13 @@ int tmh_correct_u16_device(tmh_corrector* c, const uint16_t* dev_in, uint16_t* d
 int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* dev_in,
                                 uint16_t* dev_out, int64_t n_sites, int clip_lo, int clip_hi,
                                 void* stream);
+/* The same on the blocked layout (see tmh_stats_update_welford_blocks_device):
+ * input and output block tables with the same block_shift; the correction's
+ * zero_log10 must lie in [-37, 0] (the fused pass). */
+int tmh_correct_u16_hist_blocks_device(tmh_corrector* c, tmh_stats* h,
+                                       const uint16_t* const* dev_in_blocks,
+                                       uint16_t* const* dev_out_blocks, int block_shift,
+                                       int64_t n_sites, int clip_lo, int clip_hi, void* stream);
 int tmh_correct_u8(tmh_corrector* c, const uint8_t* host_in, uint8_t* host_out, int64_t n_sites,
                    int clip_lo, int clip_hi);
 /* ---- illuminati chain ------------------------------

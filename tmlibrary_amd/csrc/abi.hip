@@ -555,21 +555,51 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
   h->n += ns;
 }
 
+static void stats_welford_dev(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
+                              int log_transform, void* stream, const SiteTab& tab) {
+  hipStream_t s = pick(h->stream, stream);
+  if ((size_t)n_sites > h->rn.n) {
+    TMH_HIP(hipStreamSynchronize(s));
+    h->rn.alloc((size_t)n_sites);
+  }
+  launch_welford(dev_sites, h->npx, n_sites, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
+                 log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, h->wide.p, h->probe.p, s,
+                 -1, tab);
+  if ((h->npx & 7) == 0) h->wide_sites += n_sites;
+  h->n += n_sites;
+  h->pending += n_sites;
+}
+
 int tmh_stats_update_welford_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
                                     int log_transform, void* stream) {
   return guard([&] {
     TMH_CHECK(h && (dev_sites || n_sites == 0) && n_sites >= 0, TMH_EINVAL, "bad arguments");
-    hipStream_t s = pick(h->stream, stream);
-    if ((size_t)n_sites > h->rn.n) {
-      TMH_HIP(hipStreamSynchronize(s));
-      h->rn.alloc((size_t)n_sites);
-    }
-    launch_welford(dev_sites, h->npx, n_sites, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
-                   log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, h->wide.p,
-                   h->probe.p, s);
-    if ((h->npx & 7) == 0) h->wide_sites += n_sites;
-    h->n += n_sites;
-    h->pending += n_sites;
+    stats_welford_dev(h, dev_sites, n_sites, log_transform, stream, SiteTab{});
+  });
+}
+
+// a blocked site layout's table (include/tmhip.h): checked as far as the host can
+static SiteTab blocked_tab(const uint16_t* const* dev_in_blocks, uint16_t* const* dev_out_blocks,
+                           int block_shift, int64_t npx) {
+  TMH_CHECK(dev_in_blocks, TMH_EINVAL, "block table is NULL");
+  TMH_CHECK(block_shift >= 2 && block_shift <= 24, TMH_EINVAL, "block_shift must be 2..24");
+  TMH_CHECK((npx & 7) == 0, TMH_EINVAL,
+            "blocked site layouts need height * width divisible by 8 (16-byte pixel groups)");
+  SiteTab t;
+  t.in = dev_in_blocks;
+  t.out = dev_out_blocks;
+  t.shift = block_shift;
+  return t;
+}
+
+int tmh_stats_update_welford_blocks_device(tmh_stats* h, const uint16_t* const* dev_blocks,
+                                           int block_shift, int64_t n_sites, int log_transform,
+                                           void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && n_sites >= 0, TMH_EINVAL, "bad arguments");
+    if (n_sites == 0) return;
+    stats_welford_dev(h, nullptr, n_sites, log_transform, stream,
+                      blocked_tab(dev_blocks, nullptr, block_shift, h->npx));
   });
 }
 
@@ -1134,12 +1164,10 @@ int tmh_correct_u8(tmh_corrector* c, const uint8_t* host_in, uint8_t* host_out, 
   });
 }
 
-int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* dev_in,
-                                uint16_t* dev_out, int64_t n_sites, int clip_lo, int clip_hi,
-                                void* stream) {
-  return guard([&] {
-    TMH_CHECK(c && h && (dev_in && dev_out || n_sites == 0) && n_sites >= 0, TMH_EINVAL,
-              "bad arguments");
+static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev_in,
+                             uint16_t* dev_out, int64_t n_sites, int clip_lo, int clip_hi,
+                             void* stream, const SiteTab& tab) {
+  {
     TMH_CHECK(c->npx == h->npx, TMH_EINVAL, "corrector and statistics image sizes differ");
     TMH_CHECK(n_sites <= h->pending, TMH_ESTATE,
               "more sites than were passed to tmh_stats_update_welford_device");
@@ -1154,10 +1182,13 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       TMH_HIP(hipEventRecord(h->ev_in, h->stream));
       TMH_HIP(hipStreamWaitEvent(s, h->ev_in, 0));
     }
-    const bool vec = (h->npx & 7) == 0 && (reinterpret_cast<uintptr_t>(dev_in) & 15) == 0 &&
-                     (reinterpret_cast<uintptr_t>(dev_out) & 15) == 0 &&
-                     // the fused pass floors zero pixels at 10**zero_log10 in f32
-                     (!c->log_transform || (c->zero_log10 >= -37.0 && c->zero_log10 <= 0.0));
+    // the fused pass floors zero pixels at 10**zero_log10 in f32
+    const bool zl_ok = !c->log_transform || (c->zero_log10 >= -37.0 && c->zero_log10 <= 0.0);
+    const bool vec = zl_ok && (h->npx & 7) == 0 &&
+                     (tab.in || ((reinterpret_cast<uintptr_t>(dev_in) & 15) == 0 &&
+                                 (reinterpret_cast<uintptr_t>(dev_out) & 15) == 0));
+    TMH_CHECK(vec || !tab.in, TMH_EINVAL,
+              "a blocked site layout needs the fused pass (zero_log10 in [-37, 0])");
     if (vec) {
       const bool grow = (size_t)n_sites * kBins > h->hist_full.n || (size_t)n_sites > h->zeros.n ||
                         (size_t)n_sites > h->hist_rmask.n ||
@@ -1195,7 +1226,10 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       // pass's workgroups on a CU, while chunk k+1 streams.  The last chunk's
       // finalize runs on the whole GPU after both.  Chunks keep site order,
       // so the ordered percentile sum at the end is unchanged.
-      const int nch = (int)std::min<int64_t>(h->tail_chunks, n_sites / 64 > 0 ? n_sites / 64 : 1);
+      // (a blocked layout runs as one chunk)
+      const int nch = tab.in ? 1
+                             : (int)std::min<int64_t>(h->tail_chunks,
+                                                      n_sites / 64 > 0 ? n_sites / 64 : 1);
       uint32_t* sh = (h->flags & 2u) ? h->site_hist.p : nullptr;
       // the wide configuration pays off once a few % of the pixel groups
       // overflow the narrow slices (their values then take global atomics)
@@ -1219,9 +1253,9 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
                             c->mconst2.p, fl, c->log_transform, clip_lo, clip_hi,
                             h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0,
                             c->queues.p, c->n_wg, h->fused_cfg, h->wide.p, wide_thresh,
-                            xwide_thresh, s);
+                            xwide_thresh, s, tab);
         launch_fix_correct(dev_in + c0 * h->npx, dev_out + c0 * h->npx, 2, c->npx, nc, fl,
-                           c->coef64.p, c->rc.p, c->log_transform, clip_lo, clip_hi, s);
+                           c->coef64.p, c->rc.p, c->log_transform, clip_lo, clip_hi, s, tab);
         const bool side = k < nch - 1;
         hipStream_t fs = side ? h->side : s;
         if (side) {
@@ -1235,7 +1269,8 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
           launch_hist_site_u16(dev_in + c0 * h->npx, h->npx, nc, h->hist_full.p + (size_t)c0 * kBins,
                                h->qp, vlh + (size_t)c0 * kOsTile, ld, h->pooled.p,
                                h->pooled_parts.p, kPooledParts, h->zeros.p + c0,
-                               sh ? sh + (size_t)c0 * kBins : nullptr, h->wide.p, xwide_thresh, fs);
+                               sh ? sh + (size_t)c0 * kBins : nullptr, h->wide.p, xwide_thresh, fs,
+                               tab);
         launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0, 0, nc,
                              h->qp, vlh + (size_t)c0 * kOsTile, ld, h->pooled.p, h->pooled_parts.p,
                              kPooledParts, h->zeros.p + c0, sh ? sh + (size_t)c0 * kBins : nullptr,
@@ -1313,6 +1348,27 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
       TMH_HIP(hipEventRecord(h->ev_out, s));
       TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
     }
+  }
+}
+
+int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* dev_in,
+                                uint16_t* dev_out, int64_t n_sites, int clip_lo, int clip_hi,
+                                void* stream) {
+  return guard([&] {
+    TMH_CHECK(c && h && (dev_in && dev_out || n_sites == 0) && n_sites >= 0, TMH_EINVAL,
+              "bad arguments");
+    correct_hist_dev(c, h, dev_in, dev_out, n_sites, clip_lo, clip_hi, stream, SiteTab{});
+  });
+}
+
+int tmh_correct_u16_hist_blocks_device(tmh_corrector* c, tmh_stats* h,
+                                       const uint16_t* const* dev_in_blocks,
+                                       uint16_t* const* dev_out_blocks, int block_shift,
+                                       int64_t n_sites, int clip_lo, int clip_hi, void* stream) {
+  return guard([&] {
+    TMH_CHECK(c && h && n_sites >= 0 && dev_out_blocks, TMH_EINVAL, "bad arguments");
+    const SiteTab tab = blocked_tab(dev_in_blocks, dev_out_blocks, block_shift, h->npx);
+    correct_hist_dev(c, h, nullptr, nullptr, n_sites, clip_lo, clip_hi, stream, tab);
   });
 }
 

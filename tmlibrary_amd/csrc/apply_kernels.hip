@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void k_fix_correct(const T* __restrict__ in, T
                                                      int64_t npx, int64_t n_sites, FixList fl,
                                                      const double2* __restrict__ c64,
                                                      const RefineConst* __restrict__ rc,
-                                                     int clip_lo, int clip_hi) {
+                                                     int clip_lo, int clip_hi, const SiteTab tab) {
   const unsigned int n = *fl.n;
   const bool all = n > fl.cap;
   const int64_t total = all ? n_sites * ((npx + 7) / 8) : (int64_t)n;
@@ -330,45 +330,54 @@ __global__ __launch_bounds__(256) void k_fix_correct(const T* __restrict__ in, T
     int64_t s, p0;
     uint32_t mask;
     fix_entry(fl, all, i, npx, s, p0, mask);
+    const T* si = in + s * npx;
+    T* so = out + s * npx;
+    if (tab.in) {  // blocked layout (u16 launches only)
+      const int64_t b = site_block(tab, s), o = site_in_block(tab, s) * npx;
+      si = reinterpret_cast<const T*>(tab.in[b]) + o;
+      so = reinterpret_cast<T*>(tab.out[b]) + o;
+    }
     for (int j = 0; j < 8; ++j) {
       const int64_t p = p0 + j;
       if (!((mask >> j) & 1u) || p >= npx) continue;
       const double2 q = c64[p];
       uint32_t r =
-          (uint32_t)correct_ref_f64<LOG>(in[s * npx + p], q.x, q.y, k.S, k.M, k.zero_log10) &
+          (uint32_t)correct_ref_f64<LOG>(si[p], q.x, q.y, k.S, k.M, k.zero_log10) &
           ((1u << BITS) - 1u);
       if (clip_lo >= 0) {
         r = r < (uint32_t)clip_lo ? (uint32_t)clip_lo : r;
         r = r > (uint32_t)clip_hi ? (uint32_t)clip_hi : r;
       }
-      out[s * npx + p] = (T)r;
+      so[p] = (T)r;
     }
   }
 }
 
 void launch_fix_correct(const void* in, void* out, int elem_bytes, int64_t npx, int64_t n_sites,
                         const FixList& fl, const double2* coef64, const RefineConst* rc,
-                        int log_transform, int clip_lo, int clip_hi, hipStream_t s) {
+                        int log_transform, int clip_lo, int clip_hi, hipStream_t s,
+                        const SiteTab& tab) {
   if (n_sites <= 0) return;
   const dim3 grid(512), block(256);
+  TMH_CHECK(!tab.in || elem_bytes == 2, TMH_EINVAL, "blocked layouts are uint16 only");
   if (elem_bytes == 2) {
     auto i16 = static_cast<const uint16_t*>(in);
     auto o16 = static_cast<uint16_t*>(out);
     if (log_transform)
       hipLaunchKernelGGL((k_fix_correct<true, uint16_t, 16>), grid, block, 0, s, i16, o16, npx,
-                         n_sites, fl, coef64, rc, clip_lo, clip_hi);
+                         n_sites, fl, coef64, rc, clip_lo, clip_hi, tab);
     else
       hipLaunchKernelGGL((k_fix_correct<false, uint16_t, 16>), grid, block, 0, s, i16, o16, npx,
-                         n_sites, fl, coef64, rc, clip_lo, clip_hi);
+                         n_sites, fl, coef64, rc, clip_lo, clip_hi, tab);
   } else {
     auto i8 = static_cast<const uint8_t*>(in);
     auto o8 = static_cast<uint8_t*>(out);
     if (log_transform)
       hipLaunchKernelGGL((k_fix_correct<true, uint8_t, 8>), grid, block, 0, s, i8, o8, npx, n_sites,
-                         fl, coef64, rc, clip_lo, clip_hi);
+                         fl, coef64, rc, clip_lo, clip_hi, tab);
     else
       hipLaunchKernelGGL((k_fix_correct<false, uint8_t, 8>), grid, block, 0, s, i8, o8, npx,
-                         n_sites, fl, coef64, rc, clip_lo, clip_hi);
+                         n_sites, fl, coef64, rc, clip_lo, clip_hi, tab);
   }
   TMH_HIP(hipGetLastError());
 }

@@ -150,10 +150,27 @@ __device__ __forceinline__ int32_t correct_ref_f64(uint32_t x, double mean, doub
 // launches (defined in the .hip files) -------------------------------------------
 // part: optional scratch of part_cap doubles for site-split launches (null: one part)
 // forced_parts: 0 = pick the site split automatically, 1..4 = that many parts
+// Blocked site layout: the sites of a launch live in blocks of 1 << shift
+// consecutive sites each (device arrays of block base pointers; in == null:
+// one contiguous run at the launch's in / out pointers).  A block holds a
+// multiple of every configuration's sites per unit (shift >= 2).
+struct SiteTab {
+  const uint16_t* const* in = nullptr;
+  uint16_t* const* out = nullptr;
+  int shift = 0;
+};
+
+// site s of a launch in its layout (contiguous at base, or blocked)
+__device__ __forceinline__ int64_t site_block(const SiteTab& t, int64_t s) { return s >> t.shift; }
+__device__ __forceinline__ int64_t site_in_block(const SiteTab& t, int64_t s) {
+  return s & ((1ll << t.shift) - 1);
+}
+
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
                     double* part, size_t part_cap, int forced_parts,
-                    unsigned long long* wide, unsigned int* probe, hipStream_t s, int shape = -1);
+                    unsigned long long* wide, unsigned int* probe, hipStream_t s, int shape = -1,
+                    const SiteTab& tab = SiteTab{});
 // vlh: the order statistics of the launch's first site (buffer + site *
 // kOsTile) in a buffer with room for vlh_ld sites (kOsTile layout above)
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
@@ -172,7 +189,8 @@ void launch_hist_site_u16(const uint16_t* sites, int64_t npx, int64_t n_sites, u
                           const QPos& p, uint32_t* vlh, int64_t vlh_ld,
                           unsigned long long* pooled, unsigned long long* pooled_parts,
                           int n_parts, int64_t* zero_counts, uint32_t* site_hist,
-                          const unsigned long long* wide, unsigned long long xthr, hipStream_t s);
+                          const unsigned long long* wide, unsigned long long xthr, hipStream_t s,
+                          const SiteTab& tab = SiteTab{});
 void launch_pct_accumulate(const uint32_t* vlh, int64_t n_sites, int64_t vlh_ld, int Q,
                            const double* gamma, double* acc, hipStream_t s);
 // quantiles [q_begin, q_begin + q_count) only; acc points at the range
@@ -208,7 +226,8 @@ void launch_coeffs_all(const double* mean, const double* std, const double* sums
 // (u16 or u8 of in's type; clip as the launch); launched on the same stream.
 void launch_fix_correct(const void* in, void* out, int elem_bytes, int64_t npx, int64_t n_sites,
                         const FixList& fl, const double2* coef64, const RefineConst* rc,
-                        int log_transform, int clip_lo, int clip_hi, hipStream_t s);
+                        int log_transform, int clip_lo, int clip_hi, hipStream_t s,
+                        const SiteTab& tab = SiteTab{});
 void launch_correct_u16(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                         const float4* coef, const float2* lut, const float4* mconst,
                         const FixList& fl, int log_transform, int clip_lo, int clip_hi,
@@ -235,15 +254,6 @@ constexpr double kWideFrac = 0.02;
 // cost more than one more read of the sites); the fused pass then runs without
 // its histogram and k_hist_site_u16 builds the histograms
 constexpr double kXWideFrac = 0.33;
-// Blocked site layout: the sites of a launch live in blocks of 1 << shift
-// consecutive sites each (device arrays of block base pointers; in == null:
-// one contiguous run at the launch's in / out pointers).  A block holds a
-// multiple of every configuration's sites per unit (shift >= 2).
-struct SiteTab {
-  const uint16_t* const* in = nullptr;
-  uint16_t* const* out = nullptr;
-  int shift = 0;
-};
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, const FixList& fl,
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,

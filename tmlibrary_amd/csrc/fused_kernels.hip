@@ -252,7 +252,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     const uint16_t* ib = in + r.s0 * npx;
     uint16_t* ob = out + r.s0 * npx;
     if (tab.in) {  // blocked layout: the unit's sites lie inside one block
-      const int64_t b = r.s0 >> tab.shift, o = (r.s0 & ((1ll << tab.shift) - 1)) * npx;
+      const int64_t b = site_block(tab, r.s0), o = site_in_block(tab, r.s0) * npx;
       ib = tab.in[b] + o;
       ob = tab.out[b] + o;
     }

@@ -177,13 +177,16 @@ __device__ __forceinline__ uint4 ld_site(const uint4* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-template <bool LOG, bool NTL, int NT, int INV>
+// BLK: blocked site layout (common.h SiteTab): site t of the launch is site
+// t & (2^shift - 1) of block t >> shift; the block base is re-read (one scalar
+// load) only when the walk enters a new block.
+template <bool LOG, bool NTL, int NT, int INV, bool BLK = false>
 __global__ __launch_bounds__(NT) void k_welford_vec8(
     const uint16_t* __restrict__ sites, int64_t npx, int64_t n_total, int64_t per,
     const WfMerge mg, double* __restrict__ mean, double* __restrict__ m2,
     const double* __restrict__ lut, double* __restrict__ part,
     unsigned long long* __restrict__ wide, const unsigned int* __restrict__ probe,
-    unsigned int probe_thr) {
+    unsigned int probe_thr, const SiteTab tab) {
   // probe (k_wf_probe): the site split applies only to bright sites; otherwise
   // the part-0 workgroups walk every site and the others leave at once
   int parts = (int)gridDim.y;
@@ -205,11 +208,22 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
   const int64_t n_sites = n_total - s_begin < per ? n_total - s_begin : per;
   const uint4* src = reinterpret_cast<const uint4*>(sites) + s_begin * ngroups + g;
   const int64_t last = n_sites - 1;
+  int64_t cur_blk = -1;  // BLK: the block whose base is held (uniform)
+  const uint4* blk_base = nullptr;
+  auto site = [&](int64_t t) -> const uint4* {  // t: site of this part, non-decreasing
+    if (!BLK) return src + t * ngroups;
+    const int64_t gs = s_begin + t, b = gs >> tab.shift;
+    if (b != cur_blk) {
+      cur_blk = b;
+      blk_base = reinterpret_cast<const uint4*>(tab.in[b]);
+    }
+    return blk_base + (gs & ((1ll << tab.shift) - 1)) * ngroups + g;
+  };
   // two-stage pipeline: the next group's loads are in flight while the
   // current group is folded in (tail loads clamp to the last site: harmless)
   uint4 cur[kWfGroup], nxt[kWfGroup];
 #pragma unroll
-  for (int k = 0; k < kWfGroup; ++k) cur[k] = ld_site<NTL>(src + (k < last ? k : last) * ngroups);
+  for (int k = 0; k < kWfGroup; ++k) cur[k] = ld_site<NTL>(site(k < last ? k : last));
   double K[8], s1[8], s2[8];
   uint32_t wc = 0, xc = 0;  // this thread's groups with a value >= 4,096 / >= 16,384
   xform8<LOG, INV>(cur[0], slut, sinv, K, wc, xc);
@@ -224,7 +238,7 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
 #pragma unroll
     for (int k = 0; k < kWfGroup; ++k) {
       const int t = s + kWfGroup + k;
-      nxt[k] = ld_site<NTL>(src + (int64_t)(t < (int)last ? t : (int)last) * ngroups);
+      nxt[k] = ld_site<NTL>(site(t < (int)last ? t : (int)last));
     }
 #pragma unroll
     for (int k = 0; k < kWfGroup; ++k) {
@@ -370,16 +384,26 @@ static void launch_welford_vec8(const uint16_t* sites, int64_t npx, int64_t n_si
                                 int f, const WfMerge& mg, double* mean, double* m2,
                                 const double* lut, int log_transform, double* part,
                                 unsigned long long* wide, hipStream_t s,
-                                const unsigned int* probe = nullptr, unsigned int probe_thr = 0) {
+                                const unsigned int* probe = nullptr, unsigned int probe_thr = 0,
+                                const SiteTab& tab = SiteTab{}) {
   const dim3 grid((unsigned)cdiv(npx >> 3, NT), (unsigned)f);
   // site loads are non-temporal (streamed once; regular loads measured
   // 6.60-6.75 vs 6.19-6.34 ms at job level, profiles/r1/ab_welford_ntl.txt)
-  if (log_transform)
-    hipLaunchKernelGGL((k_welford_vec8<true, true, NT, INV>), grid, dim3(NT), 0, s, sites, npx,
-                       n_sites, per, mg, mean, m2, lut, part, wide, probe, probe_thr);
-  else
-    hipLaunchKernelGGL((k_welford_vec8<false, true, NT, INV>), grid, dim3(NT), 0, s, sites, npx,
-                       n_sites, per, mg, mean, m2, lut, part, wide, probe, probe_thr);
+#define TMH_WF(L_, B_)                                                                           \
+  hipLaunchKernelGGL((k_welford_vec8<L_, true, NT, INV, B_>), grid, dim3(NT), 0, s, sites, npx, \
+                     n_sites, per, mg, mean, m2, lut, part, wide, probe, probe_thr, tab)
+  if (tab.in) {
+    if (log_transform)
+      TMH_WF(true, true);
+    else
+      TMH_WF(false, true);
+  } else {
+    if (log_transform)
+      TMH_WF(true, false);
+    else
+      TMH_WF(false, false);
+  }
+#undef TMH_WF
 }
 
 // Bright-site probe: of kProbeGroups 8-pixel groups spread over the launch's
@@ -391,7 +415,9 @@ static void launch_welford_vec8(const uint16_t* sites, int64_t npx, int64_t n_si
 constexpr int kProbeGroups = 16384;
 constexpr int kWfBrightParts = 3;
 __global__ __launch_bounds__(1024) void k_wf_probe(const uint16_t* __restrict__ sites,
-                                                   int64_t ngroups, unsigned int* __restrict__ out) {
+                                                   int64_t ngroups, unsigned int* __restrict__ out,
+                                                   const SiteTab tab) {
+  if (tab.in) sites = tab.in[0];  // blocked layout: the first site opens block 0
   __shared__ unsigned int cnt;
   if (threadIdx.x == 0) cnt = 0u;
   __syncthreads();
@@ -416,10 +442,12 @@ __global__ __launch_bounds__(1024) void k_wf_probe(const uint16_t* __restrict__ 
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
                     double* part, size_t part_cap, int forced_parts,
-                    unsigned long long* wide, unsigned int* probe, hipStream_t s, int shape) {
+                    unsigned long long* wide, unsigned int* probe, hipStream_t s, int shape,
+                    const SiteTab& tab) {
   if (n_sites <= 0) return;
   ProfScope prof("welford", s);
-  const bool vec = (npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0;
+  // (a blocked layout is checked by the caller: npx % 8 == 0, 16-B aligned blocks)
+  const bool vec = tab.in || ((npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0);
   if (vec) {
     int f = part ? welford_parts(n_sites, npx, part_cap, forced_parts) : 1;
     // automatic split (no forced parts, log transform): k_wf_probe decides on
@@ -429,7 +457,7 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
     const unsigned int pthr = kProbeGroups / 10;
     if (probe && part && !forced_parts && log_transform && shape < 0 &&
         welford_parts(n_sites, npx, part_cap, kWfBrightParts) == kWfBrightParts) {
-      hipLaunchKernelGGL(k_wf_probe, dim3(1), dim3(1024), 0, s, sites, npx >> 3, probe);
+      hipLaunchKernelGGL(k_wf_probe, dim3(1), dim3(1024), 0, s, sites, npx >> 3, probe, tab);
       f = kWfBrightParts;
       pr = probe;
     }
@@ -443,7 +471,7 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
       case 3: launch_welford_vec8<512, 1>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       case 4: launch_welford_vec8<256, 2>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       case 5: launch_welford_vec8<512, 2>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
-      default: launch_welford_vec8<kWfThreads, kWfInv>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s, pr, pthr); break;
+      default: launch_welford_vec8<kWfThreads, kWfInv>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s, pr, pthr, tab); break;
     }
     if (f > 1) {
       WfParts pc{};
@@ -1029,7 +1057,7 @@ __global__ __launch_bounds__(kU16Threads) void k_hist_site_u16(
     uint32_t* __restrict__ slab, const QPos p,
     uint32_t* __restrict__ vlh_all, unsigned long long* __restrict__ pooled, int n_pooled,
     int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist,
-    const unsigned long long* __restrict__ wide, unsigned long long xthr) {
+    const unsigned long long* __restrict__ wide, unsigned long long xthr, const SiteTab tab) {
   if (__builtin_nontemporal_load(wide + 1) < xthr) return;  // uniform: not a very wide launch
   constexpr int SR = 2;  // 2,048-bin super-rounds: 16 KB of ranks beside the 128 KB histogram
   __shared__ __attribute__((aligned(16))) uint32_t w16[kBins / 2];
@@ -1055,7 +1083,8 @@ __global__ __launch_bounds__(kU16Threads) void k_hist_site_u16(
       atomicOr(&ovf, 1ull << (u >> 10));
     }
   };
-  const uint4* src = reinterpret_cast<const uint4*>(sites + s * npx);
+  const uint4* src = reinterpret_cast<const uint4*>(
+      tab.in ? tab.in[site_block(tab, s)] + site_in_block(tab, s) * npx : sites + s * npx);
   const int64_t n16 = npx >> 3;
   int64_t i = tid;
   for (; i + 3 * kU16Threads < n16; i += 4 * kU16Threads) {
@@ -1107,7 +1136,8 @@ void launch_hist_site_u16(const uint16_t* sites, int64_t npx, int64_t n_sites, u
                           const QPos& p, uint32_t* vlh, int64_t vlh_ld,
                           unsigned long long* pooled, unsigned long long* pooled_parts,
                           int n_parts, int64_t* zero_counts, uint32_t* site_hist,
-                          const unsigned long long* wide, unsigned long long xthr, hipStream_t s) {
+                          const unsigned long long* wide, unsigned long long xthr, hipStream_t s,
+                          const SiteTab& tab) {
   if (n_sites <= 0) return;
   ProfScope prof("hist_u16", s);
   QPos pp = p;
@@ -1117,7 +1147,7 @@ void launch_hist_site_u16(const uint16_t* sites, int64_t npx, int64_t n_sites, u
   TMH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const unsigned grid = (unsigned)std::min<int64_t>(n_sites, cus);
   hipLaunchKernelGGL(k_hist_site_u16, dim3(grid), dim3(kU16Threads), 0, s, sites, npx, n_sites,
-                     slab, pp, vlh, pooled_parts, n_parts, zero_counts, site_hist, wide, xthr);
+                     slab, pp, vlh, pooled_parts, n_parts, zero_counts, site_hist, wide, xthr, tab);
   hipLaunchKernelGGL(k_pooled_fold, dim3(kBins / 256), dim3(256), 0, s, pooled, pooled_parts,
                      n_parts, wide, xthr);
   TMH_HIP(hipGetLastError());

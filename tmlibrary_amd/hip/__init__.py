@@ -57,6 +57,7 @@ SIGNATURES = {
     "tmh_stats_update": (_I, [_P, _P, _I64, _I, _P]),
     "tmh_stats_update_device": (_I, [_P, _P, _I64, _I, _P]),
     "tmh_stats_update_welford_device": (_I, [_P, _P, _I64, _I, _P]),
+    "tmh_stats_update_welford_blocks_device": (_I, [_P, _P, _I, _I64, _I, _P]),
     "tmh_stats_finalize": (_I, [_P, _P, _P, _P, _P, _P]),
     "tmh_stats_finalize_device": (_I, [_P, _P, _P, _P]),
     "tmh_stats_site_histogram": (_I, [_P, _I64, _P]),
@@ -81,6 +82,7 @@ SIGNATURES = {
     "tmh_correct_u16": (_I, [_P, _P, _P, _I64, _I, _I]),
     "tmh_correct_u16_device": (_I, [_P, _P, _P, _I64, _I, _I, _P]),
     "tmh_correct_u16_hist_device": (_I, [_P, _P, _P, _P, _I64, _I, _I, _P]),
+    "tmh_correct_u16_hist_blocks_device": (_I, [_P, _P, _P, _P, _I, _I64, _I, _I, _P]),
     "tmh_correct_u8": (_I, [_P, _P, _P, _I64, _I, _I]),
     "tmh_clip_u16": (_I, [_P, _P, _I64, _I, _I]),
     "tmh_align": (_I, [_P, _P, _I, _I64, _I, _I, _P, _I, _I]),
