@@ -815,7 +815,7 @@ def main():
     kern = {}
     if prof:
         for name in ("welford", "hist", "pct_acc", "finalize", "smooth", "coeffs", "correct",
-                     "correct_hist", "hist_finalize", "hist_u16"):
+                     "correct_hist", "hist_finalize", "hist_u16", "pct_tail", "cdf_compact", "pct_fold"):
             ms, k = C.c_double(), C.c_int64()
             hip.check(L.tmh_profile_read(name.encode(), C.byref(ms), C.byref(k)))
             if k.value:

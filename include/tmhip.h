@@ -102,6 +102,12 @@ int tmh_stats_reset(tmh_stats* h);
  *   TMH_OPT_TAIL_CHUNKS    1..16: run the fused correct+histogram pass in that
  *                          many site chunks, each chunk's histogram finalize
  *                          overlapping the next chunk's streaming (1: off)
+ *   TMH_OPT_PCT_TAIL       percentile tail of the fused pass: 1 (default) =
+ *                          per-site compact CDFs folded in site order per
+ *                          quantile chunk; 0 = per-site order statistics
+ *                          written, then summed (deferred handles, launches in
+ *                          several chunks and non-linear quantile tables
+ *                          always use 0).  Bit-identical results.
  *   TMH_OPT_COPY_THREADS   1..64 (default 8): host threads of the pageable <->
  *                          pinned copies of the host-buffer entry points
  *   TMH_OPT_HOST_STAGING   host-buffer entry points: 0 = the caller's buffers
@@ -115,6 +121,7 @@ int tmh_stats_reset(tmh_stats* h);
 #define TMH_OPT_TAIL_CHUNKS 3
 #define TMH_OPT_COPY_THREADS 4
 #define TMH_OPT_HOST_STAGING 5
+#define TMH_OPT_PCT_TAIL 6
 int tmh_stats_set_option(tmh_stats* h, int option, int value);
 
 /* update(image) for a run of sites.  zero_counts_out (host, n_sites, may be

@@ -473,9 +473,10 @@ def test_run_job_end_to_end(L, tmp_path):
     assert np.allclose(cont.mean.array, orc.smooth_reflect(g["mean"]), rtol=1e-9, atol=1e-12)
 
 
-def _fused_job(L, sites, clip=(-1, -1), q=None):
+def _fused_job(L, sites, clip=(-1, -1), q=None, tail=1):
     """Split pipeline through the C-ABI: Welford-only update -> finalize ->
-    smooth -> corrector -> fused correct+histogram.  Returns host results."""
+    smooth -> corrector -> fused correct+histogram.  Returns host results.
+    tail: TMH_OPT_PCT_TAIL (1: compact CDF + fold, 0: per-site order statistics)."""
     from tmlibrary_amd import hip
     from tmlibrary_amd.image import ZERO_LOG10
     from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
@@ -488,6 +489,7 @@ def _fused_job(L, sites, clip=(-1, -1), q=None):
     h = C.c_void_p()
     hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
                                  hip.ptr(lut), 4, hip.TMH_STATS_KEEP_SITE_HIST, C.byref(h)))
+    hip.check(L.tmh_stats_set_option(h, hip.TMH_OPT_PCT_TAIL, tail))
     d_in, d_out = Dev(L, sites.nbytes), Dev(L, sites.nbytes)
     d_in.put(sites)
     planes = [Dev(L, npx * 8) for _ in range(5)]
@@ -525,8 +527,13 @@ def _fused_job(L, sites, clip=(-1, -1), q=None):
     return res
 
 
-@pytest.mark.parametrize("kind", ["synth", "extremes", "uniform", "tiny", "many", "saturated"])
-def test_fused_correct_hist_pipeline(L, kind):
+@pytest.mark.parametrize("tail", [1, 0])
+@pytest.mark.parametrize("kind", ["synth", "extremes", "uniform", "tiny", "many", "saturated",
+                                  "constant", "two_values"])
+def test_fused_correct_hist_pipeline(L, kind, tail):
+    """The fused pass with both percentile tails: the compact-CDF fold
+    (one-bin sites, Q > pixel count, sparse tails, the very wide path of the
+    uniform case) and the order-statistics tail, each bit-exact."""
     from tmlibrary_amd.synth import synth_exact_sites_host, synth_sites_host
     rng = np.random.default_rng(97)
     if kind == "saturated":  # corrected values far above 2**16 (f64 refinement, common.h)
@@ -544,9 +551,14 @@ def test_fused_correct_hist_pipeline(L, kind):
     elif kind == "many":  # several site groups per band, ragged last group
         sites = np.stack(synth_sites_host(37, 64, 96, seed=8))
         sites[::5, 3, :] = 65000
+    elif kind == "constant":  # one bin per site (one compact-CDF entry)
+        sites = np.stack([np.full((48, 64), v, np.uint16) for v in (0, 777, 65535, 4096)])
+    elif kind == "two_values":  # every quantile chunk inside one of two entries
+        sites = np.stack([np.where(rng.random((48, 64)) < 0.3, 3, 60000).astype(np.uint16)
+                          for _ in range(5)])
     else:
         sites = np.stack(load_golden("stats_extremes")["sites"])
-    r = _fused_job(L, sites)
+    r = _fused_job(L, sites, tail=tail)
     ref = orc.run_illumstats(list(sites))
     assert r["n"] == len(sites)
     assert_close_rel(r["mean"], ref.mean)

@@ -263,6 +263,12 @@ struct tmh_stats {
   QPos qp{};
   DBuf<uint16_t> stage;  // two device slots of batch_cap sites
   HostPipe pipe;
+  DBuf<uint2> cdf;        // fold tail: per-site compact CDFs (cdf_ld entries per site)
+  DBuf<int32_t> fbounds, fnnz;  // fold tail: chunk bounds [chunk][site], entries per site
+  bool fold = true;       // percentile tail by compact CDF + fold (TMH_OPT_PCT_TAIL)
+  bool last_fold = false; // the last fused launch took the fold tail (unless very wide)
+  unsigned long long last_xthr = ~0ull;  // its very-wide threshold
+  DBuf<unsigned long long> last_wide;    // its (wide, very wide) group counts
   DBuf<uint32_t> vlh;  // order statistics (previous | next << 16), quantile-tiled (common.h)
   int64_t vlh_cap = 0;   // deferred mode: sites the tiles have room for
   int64_t vlh_ld = 0;    // tile stride in sites of the current contents
@@ -481,6 +487,10 @@ int tmh_stats_set_option(tmh_stats* h, int option, int value) {
         TMH_CHECK(value >= 1 && value <= 16, TMH_EINVAL, "tail chunks must be 1..16");
         h->tail_chunks = value;
         break;
+      case TMH_OPT_PCT_TAIL:
+        TMH_CHECK(value == 0 || value == 1, TMH_EINVAL, "percentile tail must be 0 or 1");
+        h->fold = value == 1;
+        break;
       default:
         if (!h->host.set(option, value)) throw Error{TMH_EINVAL, "unknown option"};
     }
@@ -539,6 +549,7 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
     const bool deferred = (h->flags & TMH_STATS_DEFERRED_PCT) != 0;
     uint32_t* vlh = h->vlh.p + (deferred ? (size_t)h->n_deferred * kOsTile : 0);
     const int64_t ld = deferred ? h->vlh_cap : nc;
+    h->last_fold = false;
     launch_hist_scatter(d + c0 * h->npx, h->npx, nc, h->hist_hi.p, h->qp, vlh, ld, h->pooled.p,
                         h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr, hs);
     if (deferred)
@@ -761,6 +772,35 @@ int tmh_stats_site_order_stats(tmh_stats* h, int64_t site, uint16_t* host_vlo, u
     const bool deferred = h->flags & TMH_STATS_DEFERRED_PCT;
     const int64_t avail = deferred ? h->n_deferred : h->last_batch;
     TMH_CHECK(site >= 0 && site < avail, TMH_EINVAL, "site not available");
+    if (!deferred && h->last_fold) {
+      unsigned long long wc[2] = {0, 0};
+      TMH_HIP(hipStreamSynchronize(h->stream));
+      TMH_HIP(hipMemcpy(wc, h->last_wide.p, 16, hipMemcpyDeviceToHost));
+      if (wc[1] < h->last_xthr) {
+        // the fold tail kept the site's compact CDF, not its order statistics:
+        // (previous, next) value at every quantile's positions from it
+        int32_t nz = 0;
+        TMH_HIP(hipMemcpy(&nz, h->fnnz.p + site, 4, hipMemcpyDeviceToHost));
+        const int64_t cdf_ld = std::min<int64_t>(kBins, h->npx);
+        std::vector<uint2> e((size_t)nz);
+        TMH_HIP(hipMemcpy(e.data(), h->cdf.p + (size_t)site * cdf_ld, (size_t)nz * 8,
+                          hipMemcpyDeviceToHost));
+        std::vector<int32_t> lo(h->Q), hi(h->Q);
+        TMH_HIP(hipMemcpy(lo.data(), h->q_lo.p, (size_t)h->Q * 4, hipMemcpyDeviceToHost));
+        TMH_HIP(hipMemcpy(hi.data(), h->q_hi.p, (size_t)h->Q * 4, hipMemcpyDeviceToHost));
+        auto value_at = [&](int32_t pos) -> uint16_t {  // first entry with rank > pos
+          const auto it = std::upper_bound(e.begin(), e.end(), (uint32_t)pos,
+                                           [](uint32_t v, const uint2& x) { return v < x.x; });
+          TMH_CHECK(it != e.end(), TMH_EDEVICE, "compact CDF does not cover the position");
+          return (uint16_t)it->y;
+        };
+        for (int64_t q = 0; q < h->Q; ++q) {
+          host_vlo[q] = value_at(lo[q]);
+          host_vhi[q] = value_at(hi[q]);
+        }
+        return;
+      }
+    }
     // one site's column of every quantile tile
     const size_t row = (size_t)kOsTile * 4;
     std::vector<uint32_t> w((size_t)os_tiles(h->Q) * kOsTile);
@@ -1230,6 +1270,24 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
       const int nch = tab.in ? 1
                              : (int)std::min<int64_t>(h->tail_chunks,
                                                       n_sites / 64 > 0 ? n_sites / 64 : 1);
+      // percentile tail: compact CDF + in-order fold (no per-site order
+      // statistics through HBM) for one-chunk, non-deferred launches
+      const bool fold = h->fold && nch == 1 && !(h->flags & TMH_STATS_DEFERRED_PCT) &&
+                        h->qp.hi_next;
+      const int64_t cdf_ld = std::min<int64_t>(kBins, h->npx);
+      if (fold) {
+        const size_t nb = (size_t)fold_chunks_host(h->Q);
+        const bool fgrow = (size_t)n_sites * cdf_ld > h->cdf.n ||
+                           nb * (size_t)n_sites > h->fbounds.n || (size_t)n_sites > h->fnnz.n;
+        if (fgrow) {
+          TMH_HIP(hipStreamSynchronize(s));
+          TMH_HIP(hipStreamSynchronize(h->stream));
+        }
+        h->cdf.ensure((size_t)n_sites * cdf_ld);
+        // bounds are laid out [chunk][site] with a stride of exactly n_sites
+        if (nb * (size_t)n_sites != h->fbounds.n) h->fbounds.alloc(nb * (size_t)n_sites);
+        h->fnnz.ensure((size_t)n_sites);
+      }
       uint32_t* sh = (h->flags & 2u) ? h->site_hist.p : nullptr;
       // the wide configuration pays off once a few % of the pixel groups
       // overflow the narrow slices (their values then take global atomics)
@@ -1271,6 +1329,16 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
                                h->pooled_parts.p, kPooledParts, h->zeros.p + c0,
                                sh ? sh + (size_t)c0 * kBins : nullptr, h->wide.p, xwide_thresh, fs,
                                tab);
+        if (fold) {  // (one chunk: the fused launch's round union is current)
+          ProfScope prof("pct_tail", s);
+          launch_pooled_colsum(h->hist_full.p, h->hist_rmask.p,
+                               reinterpret_cast<const unsigned long long*>(c->queues.p + 8),
+                               n_sites, h->pooled.p, s);
+          launch_pct_fold(h->hist_full.p, h->hist_rmask.p, n_sites, h->qp, h->cdf.p, cdf_ld,
+                          h->fbounds.p, h->fnnz.p, h->zeros.p, sh, h->gamma.p, h->acc.p,
+                          h->wide.p, xwide_thresh, s);
+          continue;
+        }
         launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0, 0, nc,
                              h->qp, vlh + (size_t)c0 * kOsTile, ld, h->pooled.p, h->pooled_parts.p,
                              kPooledParts, h->zeros.p + c0, sh ? sh + (size_t)c0 * kBins : nullptr,
@@ -1281,7 +1349,17 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
                                       : nullptr,
                              h->wide.p, xwide_thresh);
       }
-      if (!(h->flags & TMH_STATS_DEFERRED_PCT))
+      h->last_fold = fold;
+      if (fold) {  // a very wide launch's order statistics (k_hist_site_u16) only
+        launch_pct_accumulate_range(vlh, n_sites, ld, 0, h->Q, h->gamma.p, h->acc.p, s, h->wide.p,
+                                    xwide_thresh);
+        // which tail ran is decided on the device: keep the counts for the
+        // debug accessor tmh_stats_site_order_stats
+        if (!h->last_wide.n) h->last_wide.alloc(2);
+        TMH_HIP(hipMemcpyAsync(h->last_wide.p, h->wide.p, 16, hipMemcpyDeviceToDevice, s));
+        h->last_xthr = xwide_thresh;
+      }
+      else if (!(h->flags & TMH_STATS_DEFERRED_PCT))
         launch_pct_accumulate(vlh, n_sites, ld, h->Q, h->gamma.p, h->acc.p, s);
       h->hist_dirty = false;
       if (h->flags & TMH_STATS_DEFERRED_PCT) h->n_deferred += n_sites;
@@ -1331,6 +1409,7 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
                          c->log_transform, clip_lo, clip_hi, s);
       launch_fix_correct(din, dout, 2, c->npx, nc, fl, c->coef64.p, c->rc.p, c->log_transform,
                          clip_lo, clip_hi, s);
+      h->last_fold = false;
       launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->qp, vlh, ld, h->pooled.p, h->zeros.p,
                           (h->flags & 2u) ? h->site_hist.p : nullptr, s);
       if (h->flags & TMH_STATS_DEFERRED_PCT)

@@ -195,7 +195,24 @@ void launch_pct_accumulate(const uint32_t* vlh, int64_t n_sites, int64_t vlh_ld,
                            const double* gamma, double* acc, hipStream_t s);
 // quantiles [q_begin, q_begin + q_count) only; acc points at the range
 void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t vlh_ld, int q_begin,
-                                 int q_count, const double* gamma, double* acc, hipStream_t s);
+                                 int q_count, const double* gamma, double* acc, hipStream_t s,
+                                 const unsigned long long* only_xwide = nullptr,
+                                 unsigned long long xthr = 0);
+// Percentile tail from the zero-maintained per-site histogram slab (round
+// masks rmask) without per-site order statistics: compact CDF per site
+// (cdf: cdf_ld >= min(65536, npx) entries per site) + chunk bounds (bounds:
+// fold_chunks(Q) x n_sites), then the in-order fold into acc[Q].  Needs
+// p.hi_next.  wide / xthr: skipped (device-side) for a very wide launch.
+void launch_pct_fold(uint32_t* hist, unsigned long long* rmask, int64_t n_sites, const QPos& p,
+                     uint2* cdf, int64_t cdf_ld, int32_t* bounds, int32_t* nnz,
+                     int64_t* zero_counts, uint32_t* site_hist, const double* gamma, double* acc,
+                     const unsigned long long* wide, unsigned long long xthr, hipStream_t s);
+int fold_chunks_host(int Q);
+// pooled[b] += sum over the sites of hist[s][b] for the rounds rmask names
+// (rm_all: the launch-wide union of the masks, or null)
+void launch_pooled_colsum(const uint32_t* hist, const unsigned long long* rmask,
+                          const unsigned long long* rm_all, int64_t n_sites,
+                          unsigned long long* pooled, hipStream_t s);
 void launch_finalize(const double* mean, const double* m2, int64_t n, int64_t npx, double* out_mean,
                      double* out_std, hipStream_t s);
 // var = M2 / (n - 1), NaN where n < 2 (stats.py:94-102)

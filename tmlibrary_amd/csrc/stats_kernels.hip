@@ -208,16 +208,24 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
   const int64_t n_sites = n_total - s_begin < per ? n_total - s_begin : per;
   const uint4* src = reinterpret_cast<const uint4*>(sites) + s_begin * ngroups + g;
   const int64_t last = n_sites - 1;
-  int64_t cur_blk = -1;  // BLK: the block whose base is held (uniform)
-  const uint4* blk_base = nullptr;
+  // BLK: a running (uniform) site base -- t advances by 0 or 1 per call; one
+  // scalar load of the next block's base where the walk enters a block
+  int64_t bt = 0;
+  const uint4* bbase = nullptr;
+  if (BLK)
+    bbase = reinterpret_cast<const uint4*>(tab.in[s_begin >> tab.shift]) +
+            (s_begin & ((1ll << tab.shift) - 1)) * ngroups;
   auto site = [&](int64_t t) -> const uint4* {  // t: site of this part, non-decreasing
     if (!BLK) return src + t * ngroups;
-    const int64_t gs = s_begin + t, b = gs >> tab.shift;
-    if (b != cur_blk) {
-      cur_blk = b;
-      blk_base = reinterpret_cast<const uint4*>(tab.in[b]);
+    if (t != bt) {
+      bt = t;
+      const int64_t gs = s_begin + t;
+      if (gs & ((1ll << tab.shift) - 1))
+        bbase += ngroups;
+      else
+        bbase = reinterpret_cast<const uint4*>(tab.in[gs >> tab.shift]);
     }
-    return blk_base + (gs & ((1ll << tab.shift) - 1)) * ngroups + g;
+    return bbase + g;
   };
   // two-stage pipeline: the next group's loads are in flight while the
   // current group is folded in (tail loads clamp to the last site: harmless)
@@ -1000,6 +1008,15 @@ __global__ void k_pooled_fold(unsigned long long* __restrict__ pooled,
   pooled[b] += t;
 }
 
+void launch_pooled_colsum(const uint32_t* hist, const unsigned long long* rmask,
+                          const unsigned long long* rm_all, int64_t n_sites,
+                          unsigned long long* pooled, hipStream_t s) {
+  if (n_sites <= 0) return;
+  hipLaunchKernelGGL(k_pooled_colsum, dim3(kBins / 256, (unsigned)cdiv(n_sites, kColSites)),
+                     dim3(256), 0, s, hist, rmask, rm_all, n_sites, pooled);
+  TMH_HIP(hipGetLastError());
+}
+
 void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_rounds,
                           int64_t n_sites, const QPos& p, uint32_t* vlh, int64_t vlh_ld,
                           unsigned long long* pooled,
@@ -1201,7 +1218,11 @@ __global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint32_t* __restr
                                                           int64_t n_sites, int64_t tstride,
                                                           int q_begin, int Q,
                                                           const double* __restrict__ gamma,
-                                                          double* __restrict__ acc) {
+                                                          double* __restrict__ acc,
+                                                          const unsigned long long* __restrict__ xw,
+                                                          unsigned long long xthr) {
+  // xw: run only for a very wide launch (the compact-CDF fold serves the rest)
+  if (xw && __builtin_nontemporal_load(xw + 1) < xthr) return;
   const int t = (int)blockIdx.x * kPctThreads + threadIdx.x;
   if (t >= Q) return;
   const int q = q_begin + t;
@@ -1237,7 +1258,8 @@ void launch_pct_accumulate(const uint32_t* vlh, int64_t n_sites, int64_t vlh_ld,
 }
 
 void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t vlh_ld, int q_begin,
-                                 int q_count, const double* gamma, double* acc, hipStream_t s) {
+                                 int q_count, const double* gamma, double* acc, hipStream_t s,
+                                 const unsigned long long* only_xwide, unsigned long long xthr) {
   if (n_sites <= 0 || q_count <= 0) return;
   ProfScope prof("pct_acc", s);
   // Regular (not non-temporal) loads of the order statistics.  PROVISIONAL:
@@ -1246,7 +1268,264 @@ void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t v
   // run-to-run spread of one build (profiles/r1/noise_same_build.txt).
   hipLaunchKernelGGL(k_pct_acc<false>, dim3((unsigned)cdiv(q_count, kPctThreads)),
                      dim3(kPctThreads), 0, s, vlh, n_sites, vlh_ld * kOsTile, q_begin, q_count,
-                     gamma, acc);
+                     gamma, acc, only_xwide, xthr);
+  TMH_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// percentile tail without per-site order statistics (the fold)
+// ---------------------------------------------------------------------------
+// The per-quantile order statistics of every site (Q x 4 B = 400 KB per site,
+// 1.38 GB for a 3,456-site job) were written by the histogram finalize and
+// read back by k_pct_acc: ~0.8 ms of a 21 ms job spent moving them through
+// HBM twice.  A site's histogram holds the same information in far fewer
+// bytes: its non-empty bins with their cumulative counts -- the compact CDF,
+// ~6,000 entries x 8 B on microscopy data.  So:
+//   k_cdf_compact  (one workgroup per site) scans the flagged rounds of the
+//                  site's zero-maintained histogram slab once (resetting them,
+//                  as k_hist_finalize did), writes the compact CDF -- entry k =
+//                  (inclusive rank, value) of the k-th non-empty bin -- and,
+//                  for every quantile chunk c, the index of the entry holding
+//                  the chunk's first previous position lo[c * kFoldQC];
+//   k_pct_fold     (one workgroup per chunk of kFoldQC quantiles) walks the
+//                  sites IN ORDER: wave w of round r resolves site 16 r + w's
+//                  previous / next values for the chunk's quantiles from the
+//                  entries between its two chunk bounds (one 64-entry window
+//                  on almost every chunk), the lerp goes to LDS, and after one
+//                  barrier the chunk's accumulator threads add the round's
+//                  16 sites in site order -- the same f64 adds, without
+//                  contraction, in the same order as k_pct_acc: bit-exact.
+// Bytes: ~0.17 GB written and read instead of 2 x 1.38 GB.
+constexpr int kFoldQPL = 4;                // quantiles per lane
+constexpr int kFoldQC = 64 * kFoldQPL;     // quantiles per chunk = per fold workgroup
+constexpr int kFoldWaves = 16;             // sites per fold round
+constexpr int kCdfSR = 4;                  // super-round: 4 x 1,024 bins
+constexpr int kCdfThreads = 1024;
+
+__host__ __device__ inline int fold_chunks(int Q) { return (Q + kFoldQC - 1) / kFoldQC; }
+
+__global__ __launch_bounds__(kCdfThreads) void k_cdf_compact(
+    uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask, const QPos p,
+    uint2* __restrict__ cdf, int64_t cdf_ld, int32_t* __restrict__ bounds, int64_t bounds_ld,
+    int32_t* __restrict__ nnz, int64_t* __restrict__ zero_counts,
+    uint32_t* __restrict__ site_hist, const unsigned long long* __restrict__ wide,
+    unsigned long long xthr) {
+  // a very wide launch: k_hist_site_u16 has produced this launch's order statistics
+  if (wide && __builtin_nontemporal_load(wide + 1) >= xthr) return;
+  constexpr int NT = kCdfThreads, LEN = kCdfSR * kRound, BPT = LEN / NT;
+  static_assert(BPT >= 1 && kRound % BPT == 0, "a thread's bins lie inside one round");
+  __shared__ uint32_t slots[32], slots_nz[32];
+  __shared__ int32_t R[LEN];   // inclusive rank of each bin of the super-round
+  __shared__ int32_t NZ[LEN];  // entry index of each bin (of the non-empty ones)
+  const int tid = threadIdx.x;
+  const int64_t s = blockIdx.x;
+  const unsigned long long need = rmask[s];
+  __syncthreads();
+  if (tid == 0) rmask[s] = 0ull;  // zero-maintained: every thread has read it
+  uint32_t* h = hist + s * (int64_t)kBins;
+  uint2* out = cdf + s * cdf_ld;
+  const int nb = fold_chunks(p.Q);
+  if (site_hist) {  // debug/parity copy: the rounds not visited are empty
+    for (int j = 0; j < kBins / kRound; ++j)
+      if (!((need >> j) & 1ull))
+        for (int i = tid; i < kRound; i += NT) site_hist[s * kBins + (uint32_t)(j * kRound + i)] = 0u;
+  }
+  unsigned long long sneed = 0ull;  // super-rounds holding a needed round
+#pragma unroll
+  for (int k = 0; k < kBins / LEN; ++k)
+    if ((need >> (k * kCdfSR)) & ((1ull << kCdfSR) - 1ull)) sneed |= 1ull << k;
+  if (zero_counts && tid == 0 && !(sneed & 1ull)) zero_counts[s] = 0;
+  auto load = [&](int k, uint32_t (&c)[BPT]) {
+    const uint32_t b0 = (uint32_t)k * LEN + tid * BPT;
+    const bool live = (need >> (b0 / kRound)) & 1ull;
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) c[i] = live ? h[b0 + i] : 0u;
+  };
+  int64_t base = 0;  // rank before the super-round
+  int32_t nzb = 0;   // entries before the super-round
+  int nscan = 0;
+  uint32_t cn[BPT];
+  if (sneed) load(__builtin_ctzll(sneed), cn);
+  while (sneed) {
+    const int k = __builtin_ctzll(sneed);
+    sneed &= sneed - 1ull;
+    uint32_t c[BPT], inc[BPT], nzi[BPT];
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) c[i] = cn[i];
+    if (sneed) load(__builtin_ctzll(sneed), cn);
+    const uint32_t b0 = (uint32_t)k * LEN + tid * BPT;
+    const bool live = (need >> (b0 / kRound)) & 1ull;
+    uint32_t run = 0, nzr = 0;
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      run += c[i];
+      inc[i] = run;
+      nzi[i] = nzr;
+      nzr += c[i] ? 1u : 0u;
+      const uint32_t b = b0 + i;
+      if (live) {
+        if (site_hist) site_hist[s * kBins + b] = c[i];
+        if (c[i]) h[b] = 0u;  // zero-maintained slab
+      }
+      if (b == 0 && zero_counts) zero_counts[s] = c[i];
+    }
+    uint32_t total, nz_total;
+    const int64_t r = base + block_exscan_t<NT>(run, slots, nscan, &total);
+    const int32_t e0 = nzb + (int32_t)block_exscan_t<NT>(nzr, slots_nz, nscan, &nz_total);
+    ++nscan;
+    if (total == 0) continue;  // uniform: an empty super-round
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      if (c[i]) out[e0 + nzi[i]] = make_uint2((uint32_t)(r + inc[i]), b0 + i);
+      R[tid * BPT + i] = (int32_t)(r + inc[i]);
+      NZ[tid * BPT + i] = e0 + (int32_t)nzi[i];
+    }
+    __syncthreads();  // R / NZ visible
+    const int64_t r1 = base + total;
+    for (int cc = tid; cc < nb; cc += NT) {
+      const int32_t P = p.lo[cc * kFoldQC];
+      if (P < base || P >= r1) continue;
+      int a = -1, b = LEN - 1;  // R[a] <= P < R[b] (R[LEN - 1] = r1 > P)
+      while (b - a > 1) {
+        const int m = (a + b) >> 1;
+        if (R[m] > P)
+          b = m;
+        else
+          a = m;
+      }
+      bounds[(int64_t)cc * bounds_ld + s] = NZ[b];
+    }
+    __syncthreads();  // done with R / NZ before the next super-round rewrites them
+    base = r1;
+    nzb += (int32_t)nz_total;
+  }
+  if (tid == 0) nnz[s] = nzb;
+}
+
+__global__ __launch_bounds__(kFoldWaves * 64) void k_pct_fold(
+    const uint2* __restrict__ cdf, int64_t cdf_ld, const int32_t* __restrict__ bounds,
+    int64_t bounds_ld, const int32_t* __restrict__ nnz, int64_t n_sites, const QPos p,
+    const double* __restrict__ gamma, double* __restrict__ acc,
+    const unsigned long long* __restrict__ wide, unsigned long long xthr) {
+  if (wide && __builtin_nontemporal_load(wide + 1) >= xthr) return;  // very wide: k_pct_acc
+  __shared__ double vals[2][kFoldWaves][kFoldQC];
+  __shared__ uint32_t wcum[kFoldWaves][64], wval[kFoldWaves][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c = blockIdx.x;
+  const int nb = fold_chunks(p.Q);
+  const int q0 = c * kFoldQC;
+  // this lane's quantiles (consecutive: positions non-decreasing along the wave)
+  int32_t lo[kFoldQPL];
+  double g[kFoldQPL];
+#pragma unroll
+  for (int j = 0; j < kFoldQPL; ++j) {
+    const int q = q0 + lane * kFoldQPL + j;
+    const bool ok = q < p.Q;
+    lo[j] = p.lo[ok ? q : p.Q - 1];
+    g[j] = ok ? gamma[q] : 0.0;
+  }
+  const bool adder = tid < kFoldQC && q0 + tid < p.Q;
+  double a = adder ? acc[q0 + tid] : 0.0;
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  // the window of one site (entries start .. start + 63, past kend: +inf)
+  auto window = [&](const uint2* e, int32_t start, int32_t kend) -> uint2 {
+    const int32_t i = start + lane;
+    return i <= kend ? e[i] : make_uint2(kInf, 0u);
+  };
+  struct Bnd {
+    int32_t k0, kend;
+  };
+  auto bnd = [&](int64_t s) -> Bnd {
+    if (s >= n_sites) return Bnd{0, -1};
+    const int32_t last_e = nnz[s] - 1;
+    const int32_t k0 = bounds[(int64_t)c * bounds_ld + s];
+    const int32_t k1 = c + 1 < nb ? bounds[(int64_t)(c + 1) * bounds_ld + s] : last_e;
+    return Bnd{k0, k1 + 1 < last_e ? k1 + 1 : last_e};
+  };
+  const int rounds = (int)((n_sites + kFoldWaves - 1) / kFoldWaves);
+  // pipeline: round r's first window was loaded during round r - 1, round
+  // r + 1's bounds during round r - 1 as well
+  Bnd bc = bnd(w), bn = bnd((int64_t)kFoldWaves + w);
+  uint2 wc = bc.kend >= 0 ? window(cdf + (int64_t)w * cdf_ld, bc.k0, bc.kend) : make_uint2(kInf, 0u);
+  for (int r = 0; r < rounds; ++r) {
+    const int64_t s = (int64_t)r * kFoldWaves + w;
+    const int buf = r & 1;
+    const int64_t sn = s + kFoldWaves;
+    const uint2 wn = bn.kend >= 0 ? window(cdf + sn * cdf_ld, bn.k0, bn.kend) : make_uint2(kInf, 0u);
+    const Bnd bn2 = bnd(sn + kFoldWaves);
+    if (s < n_sites) {  // uniform per wave
+      const uint2* e = cdf + s * cdf_ld;
+      uint32_t av[kFoldQPL], bv[kFoldQPL];
+      uint32_t done = 0u;
+      int32_t start = bc.k0;
+      uint2 cur = wc;
+      while (true) {
+        wcum[w][lane] = cur.x;
+        wval[w][lane] = cur.y;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const bool final = start + 63 > bc.kend;
+        // positions resolved in this window: entry index <= start + 62 (so
+        // the next position's entry, index + 1, is in the window too)
+        const uint32_t lim = final ? kInf : wcum[w][62];
+#pragma unroll
+        for (int j = 0; j < kFoldQPL; ++j) {
+          if ((done >> j) & 1u) continue;
+          const uint32_t P = (uint32_t)lo[j];
+          if (P >= lim) continue;
+          int x = -1, y = 63;  // wcum[x] <= P < wcum[y]
+          while (y - x > 1) {
+            const int m = (x + y) >> 1;
+            if (wcum[w][m] > P)
+              y = m;
+            else
+              x = m;
+          }
+          av[j] = wval[w][y];
+          // next position min(P + 1, n - 1): the same value unless P is the
+          // last position of its bin (then it opens the next entry)
+          const uint32_t Ph = P < (uint32_t)p.last ? P + 1u : P;
+          bv[j] = wcum[w][y] > Ph ? av[j] : wval[w][y < 63 ? y + 1 : 63];
+          done |= 1u << j;
+        }
+        if (final) break;
+        start += 63;
+        __builtin_amdgcn_wave_barrier();  // window reads done before it is overwritten
+        cur = window(e, start, bc.kend);
+      }
+#pragma unroll
+      for (int j = 0; j < kFoldQPL; ++j)
+        vals[buf][w][lane * kFoldQPL + j] = lerp_np(av[j], bv[j], g[j]);
+    }
+    __syncthreads();
+    if (adder) {
+#pragma unroll
+      for (int k = 0; k < kFoldWaves; ++k)
+        if ((int64_t)r * kFoldWaves + k < n_sites) a = add_nc(a, vals[buf][k][tid]);
+    }
+    bc = bn;
+    bn = bn2;
+    wc = wn;
+  }
+  if (adder) acc[q0 + tid] = a;
+}
+
+void launch_pct_fold(uint32_t* hist, unsigned long long* rmask, int64_t n_sites, const QPos& p,
+                     uint2* cdf, int64_t cdf_ld, int32_t* bounds, int32_t* nnz,
+                     int64_t* zero_counts, uint32_t* site_hist, const double* gamma, double* acc,
+                     const unsigned long long* wide, unsigned long long xthr, hipStream_t s) {
+  if (n_sites <= 0) return;
+  {
+    ProfScope prof("cdf_compact", s);
+    hipLaunchKernelGGL(k_cdf_compact, dim3((unsigned)n_sites), dim3(kCdfThreads), 0, s, hist, rmask,
+                       p, cdf, cdf_ld, bounds, n_sites, nnz, zero_counts, site_hist, wide, xthr);
+  }
+  {
+    ProfScope prof("pct_fold", s);
+    hipLaunchKernelGGL(k_pct_fold, dim3((unsigned)fold_chunks(p.Q)), dim3(kFoldWaves * 64), 0, s,
+                       cdf, cdf_ld, bounds, n_sites, nnz, n_sites, p, gamma, acc, wide, xthr);
+  }
   TMH_HIP(hipGetLastError());
 }
 
@@ -1326,4 +1605,8 @@ void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s) {
   TMH_HIP(hipGetLastError());
 }
 
+}  // namespace tmh
+
+namespace tmh {
+int fold_chunks_host(int Q) { return fold_chunks(Q); }
 }  // namespace tmh

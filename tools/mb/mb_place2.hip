@@ -13,6 +13,7 @@
 // Usage: mb_place2 [n_sites=3456] [n_buffers=4] [reps=2] [blocks="16,64"]
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -20,6 +21,7 @@
 
 #include "../../tmlibrary_amd/csrc/common.h"
 #include "../../tmlibrary_amd/csrc/fused_kernels.hip"
+#include "../../tmlibrary_amd/csrc/stats_kernels.hip"
 #include "../../tmlibrary_amd/csrc/synth_kernels.hip"
 
 #define CK(x)                                                                                  \
@@ -135,6 +137,25 @@ int main(int argc, char** argv) {
                             rmask, queues, cus, kFusedNarrow, nullptr, 0, 0, 0, tab);
       });
     };
+    double *mean, *m2, *lut, *rn, *part;
+    unsigned long long* wide;
+    CK(hipMalloc(&mean, npx * 8));
+    CK(hipMalloc(&m2, npx * 8));
+    CK(hipMalloc(&lut, 65536 * 8));
+    CK(hipMalloc(&rn, S * 8));
+    CK(hipMalloc(&part, 8 * npx * 8));
+    CK(hipMalloc(&wide, 16));
+    {
+      std::vector<double> l(65536);
+      for (int i = 0; i < 65536; ++i) l[i] = i ? std::log10((double)i) : 0.0;
+      CK(hipMemcpy(lut, l.data(), 65536 * 8, hipMemcpyHostToDevice));
+    }
+    auto welford = [&](const uint16_t* in, const SiteTab& tab) {
+      return time([&] {
+        launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 1, wide, nullptr, 0, -1,
+                       tab);
+      });
+    };
     const unsigned g16 = (unsigned)((n16 + 255) / 256);
     for (int i = 0; i < NB; ++i) {
       const float r = time([&] {
@@ -195,6 +216,10 @@ int main(int argc, char** argv) {
       for (int r = 0; r < 3; ++r) printf(" %8.3f", fused(nullptr, nullptr, tab));
       printf("   contiguous 0->1: %8.3f  1->0: %8.3f\n", fused(buf[0], buf[1], SiteTab{}),
              fused(buf[1], buf[0], SiteTab{}));
+      printf("  welford blocked:");
+      for (int r = 0; r < 3; ++r) printf(" %8.3f", welford(nullptr, tab));
+      printf("   contiguous 0: %8.3f  1: %8.3f\n", welford(buf[0], SiteTab{}),
+             welford(buf[1], SiteTab{}));
       fflush(stdout);
       for (int k = 0; k < nblk; ++k) {
         CK(hipFree(ib[k]));
