@@ -88,6 +88,8 @@ def parse():
                    help="sites per HBM allocation (a power of two >= 4; blocked site layout, input "
                         "and output blocks allocated alternately); 0: one contiguous buffer each")
     p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
+    p.add_argument("--no-same-workload", action="store_true",
+                   help="N > 1: skip rank 0's single-GPU run of the same (unsharded) workload")
     p.add_argument("--pipeline", choices=["fused", "separate"], default="fused",
                    help="fused: histograms built from the correction's read (6 B/px); "
                         "separate: Welford || histogram pass, then correct (8 B/px)")
@@ -313,186 +315,285 @@ def link_rates(dev, nbytes=2 << 30):
     return r
 
 
-def bench_stream_host(a, world, rank, local_rank, dist_on):
-    """configs[4]: a multi-plate batch (4 plates x 384 wells x 16 sites = 24,576
-    sites per channel, 5 channels) that does not live in HBM: the sites come
-    from pinned host memory over PCIe (corilla/api.py:69-83 reads them from
-    files one site at a time).  Each rank takes its contiguous share of every
-    channel.  A channel share that fits (--resident-gb) crosses the link once:
-    streamed in (H2D 2 B/px) chunk by chunk with the Welford pass chasing the
-    arrivals, kept resident for the fused correct + histogram pass, and the
-    corrected sites streamed out (D2H 2 B/px) while the NEXT channel streams in
-    on the other copy engine.  Sites beyond the resident budget are streamed
-    twice (stats, then correct).  The host side is a pinned ring of distinct
-    generated sites, cycled: the reference's file reads are not modelled."""
-    import torch
-    import torch.distributed as dist
+STREAM_RING = 64   # distinct host sites of --stream-host, cycled
+STREAM_CHUNK = 32  # sites per copy / Welford launch
+STREAM_STEP = 7    # channel c's global site g is ring site (g + 7 c) % ring
 
-    from tmlibrary_amd import hip
-    from tmlibrary_amd.image import ZERO_LOG10
-    from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
-    from tmlibrary_amd.workflow.corilla.sharded import (StatsOps, merge_counts, merge_welford,
-                                                         shard_bounds)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if dist_on:
-        dist.init_process_group("nccl", device_id=dev)
-    H, W = a.height, a.width
-    npx = H * W
-    site_b = npx * 2
-    Q = 100000
-    CH = a.stream_channels
-    S_total = a.stream_sites
-    s_begin, s_end = shard_bounds(S_total, world, rank)
-    S = s_end - s_begin
-    CK = 32  # sites per copy / Welford launch
-    R = min(S, int(a.resident_gb * 1e9 / 2 / site_b) // CK * CK)  # resident sites per channel
-    RING = 64  # distinct host sites
-    L = hip.lib()
-    hip.check(L.tmh_set_device(local_rank))
-    log("stream-host: %d channels x %d sites/rank (%d resident, %d streamed twice); link test"
-        % (CH, S, R, S - R))
-    link = link_rates(dev)
-    log("link: %s" % link)
 
-    h_ring = torch.empty((RING, H, W), dtype=torch.int16, pin_memory=True)
-    tmp = torch.empty((RING, H, W), dtype=torch.int16, device=dev)
-    hip.check(L.tmh_synth_sites_device(C.c_void_p(tmp.data_ptr()), RING, H, W, SEED, 0, s_begin,
-                                       hip.TMH_SYNTH_STANDARD, None))
-    h_ring.copy_(tmp)
-    del tmp
-    h_out = torch.empty((4, CK, H, W), dtype=torch.int16, pin_memory=True)
-    resident = [torch.empty((max(R, 1), H, W), dtype=torch.int16, device=dev) for _ in range(2)]
-    stage = [torch.empty((CK, H, W), dtype=torch.int16, device=dev) for _ in range(2)]
-    d_out = [torch.empty((CK, H, W), dtype=torch.int16, device=dev) for _ in range(4)]
-    s_h2d, s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    comp = [torch.cuda.Stream(dev) for _ in range(2)]
-    lo, hi, gamma = quantile_table(npx, np.linspace(0, 100, Q))
-    lut = stats_log10_lut()
-    flags = hip.TMH_STATS_DEFERRED_PCT if dist_on else 0
-    handles = []
-    for b in range(2):
-        h, corr = C.c_void_p(), C.c_void_p()
-        hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
-                                     hip.ptr(lut), 1, flags, C.byref(h)))
-        sp = C.c_void_p(comp[b].cuda_stream)
-        hip.check(L.tmh_stats_set_stream(h, sp))
-        planes = [torch.empty(npx, dtype=torch.float64, device=dev) for _ in range(5)]
-        torch.cuda.synchronize(dev)
-        hip.check(L.tmh_corrector_create_device(C.c_void_p(planes[0].data_ptr()),
-                                                C.c_void_p(planes[1].data_ptr()), H, W, 1,
-                                                ZERO_LOG10, sp, C.byref(corr)))
-        handles.append((h, corr, sp, planes, StatsOps(L, h, npx, Q, dev)))
-    ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
-    state = {"buf_free": [None, None], "stage_free": [None, None], "out_free": [None] * 4,
-             "k_in": 0, "k_out": 0}
-    marks = []  # (channel, phase, timing event) of the timed run
+def stream_ring_index(g, c, ring=STREAM_RING):
+    """configs[4]'s host input: global site g of channel c is site (g + 7c) %
+    ring of the host ring (the generator's sites 0 .. ring-1 of (SEED, channel
+    0)); the same on every rank, so results do not depend on the rank count."""
+    return (int(g) + STREAM_STEP * int(c)) % int(ring)
 
-    def record(stream):
-        e = torch.cuda.Event()
+
+class HostStreamJob(object):
+    """configs[4] on one rank: every channel's share of sites streamed from a
+    pinned host ring (corilla/api.py:69-83 reads them from files one site at a
+    time), the sites of one channel job per rank, contiguous in site order.
+
+    A channel share that fits (resident_gb) crosses the link once: streamed in
+    (H2D 2 B/px) chunk by chunk with the Welford pass chasing the arrivals,
+    kept resident for the fused correct + histogram pass, and the corrected
+    sites streamed out (D2H 2 B/px) while the NEXT channel streams in on the
+    other copy engine.  Sites beyond the resident budget are streamed twice
+    (stats, then correct).  Two statistics handles alternate between
+    channels; each channel's results (mean, std, percentile sums, pooled
+    histogram, smoothed planes) are copied to device buffers of its own at the
+    end of its job, on its stream, so a caller can check every channel without
+    stalling the pipeline; ``keep`` = {(channel, global site)} also keeps
+    those sites' corrected planes."""
+
+    def __init__(self, L, dev, H, W, S_total, world=1, rank=0, resident_gb=160.0,
+                 ring=STREAM_RING, chunk=STREAM_CHUNK, dist=None, keep=(), seed=SEED):
+        import torch
+
+        from tmlibrary_amd import hip
+        from tmlibrary_amd.image import ZERO_LOG10
+        from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
+        from tmlibrary_amd.workflow.corilla.sharded import StatsOps, shard_bounds
+        self.torch, self.hip, self.L, self.dev = torch, hip, L, dev
+        self.H, self.W, self.npx = H, W, H * W
+        self.S_total, self.world, self.rank, self.dist = S_total, world, rank, dist
+        self.ring, self.CK = ring, chunk
+        self.s_begin, self.s_end = shard_bounds(S_total, world, rank)
+        self.S = self.s_end - self.s_begin
+        site_b = self.npx * 2
+        self.R = min(self.S, int(resident_gb * 1e9 / 2 / site_b) // chunk * chunk)
+        Q = 100000
+        CK = chunk
+        # the host ring: the generator's sites 0 .. ring-1, pinned
+        self.h_ring = torch.empty((ring, H, W), dtype=torch.int16, pin_memory=True)
+        tmp = torch.empty((ring, H, W), dtype=torch.int16, device=dev)
+        hip.check(L.tmh_synth_sites_device(C.c_void_p(tmp.data_ptr()), ring, H, W, seed, 0, 0,
+                                           hip.TMH_SYNTH_STANDARD, None))
+        self.h_ring.copy_(tmp)
+        del tmp
+        self.h_out = torch.empty((4, CK, H, W), dtype=torch.int16, pin_memory=True)
+        self.resident = [torch.empty((max(self.R, 1), H, W), dtype=torch.int16, device=dev)
+                         for _ in range(2)]
+        self.stage = [torch.empty((CK, H, W), dtype=torch.int16, device=dev) for _ in range(2)]
+        self.d_out = [torch.empty((CK, H, W), dtype=torch.int16, device=dev) for _ in range(4)]
+        self.s_h2d, self.s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        self.comp = [torch.cuda.Stream(dev) for _ in range(2)]
+        lo, hi, gamma = quantile_table(self.npx, np.linspace(0, 100, Q))
+        lut = stats_log10_lut()
+        flags = hip.TMH_STATS_DEFERRED_PCT if dist is not None else 0
+        self.handles = []
+        for b in range(2):
+            h, corr = C.c_void_p(), C.c_void_p()
+            hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
+                                         hip.ptr(lut), 1, flags, C.byref(h)))
+            sp = C.c_void_p(self.comp[b].cuda_stream)
+            hip.check(L.tmh_stats_set_stream(h, sp))
+            planes = [torch.empty(self.npx, dtype=torch.float64, device=dev) for _ in range(5)]
+            torch.cuda.synchronize(dev)
+            hip.check(L.tmh_corrector_create_device(C.c_void_p(planes[0].data_ptr()),
+                                                    C.c_void_p(planes[1].data_ptr()), H, W, 1,
+                                                    ZERO_LOG10, sp, C.byref(corr)))
+            self.handles.append((h, corr, sp, planes, StatsOps(L, h, self.npx, Q, dev)))
+        self.keep = set((int(c), int(g)) for c, g in keep)
+        self.kept = {}   # (channel, global site) -> device plane
+        self.res = {}    # channel -> device result buffers
+        self.reset_state()
+        self.marks = []  # (channel, phase, timing event)
+        self.host_t = {}
+
+    def reset_state(self):
+        self.state = {"buf_free": [None, None], "stage_free": [None, None],
+                      "out_free": [None] * 4, "k_in": 0, "k_out": 0}
+
+    def _record(self, stream, timing=False):
+        e = self.torch.cuda.Event(enable_timing=timing)
         e.record(stream)
         return e
 
-    host_t = {}
+    def mark(self, c, phase, stream):
+        self.marks.append((c, phase, self._record(stream, True)))
+        self.host_t.setdefault("c%d" % c, {})["enq_" + phase] = time.perf_counter()
 
-    def mark(c, phase, stream):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record(stream)
-        marks.append((c, phase, e))
-        host_t.setdefault("c%d" % c, {})["enq_" + phase] = time.perf_counter()
+    def h2d(self, dst, g0, n, c):
+        """global sites g0 .. g0+n-1 of channel c from the host ring into dst
+        (contiguous runs of the ring; on the H2D engine)"""
+        torch = self.torch
+        i = 0
+        with torch.cuda.stream(self.s_h2d):
+            while i < n:
+                k = stream_ring_index(g0 + i, c, self.ring)
+                m = min(n - i, self.ring - k)
+                dst[i:i + m].copy_(self.h_ring[k:k + m], non_blocking=True)
+                i += m
+        return self._record(self.s_h2d)
 
-    def h2d(dst, j, c):
-        """chunk j of channel c from the host ring into dst (on the H2D engine)."""
-        src = h_ring[((j + c) * CK) % RING:((j + c) * CK) % RING + CK]
-        with torch.cuda.stream(s_h2d):
-            dst.copy_(src, non_blocking=True)
-        return record(s_h2d)
-
-    def channel(c):
+    def channel(self, c):
+        torch, hip, L = self.torch, self.hip, self.L
+        from tmlibrary_amd.workflow.corilla.sharded import merge_counts, merge_welford
+        H, W, CK, S, R = self.H, self.W, self.CK, self.S, self.R
+        st = self.state
         b = c % 2
-        h, corr, sp, planes, ops = handles[b]
-        cs = comp[b]
+        h, corr, sp, planes, ops = self.handles[b]
+        cs = self.comp[b]
         mean, std, smean, sstd, ptmp = planes
-        buf = resident[b]
-        if state["buf_free"][b] is not None:
-            s_h2d.wait_event(state["buf_free"][b])
+        buf = self.resident[b]
+        ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        if st["buf_free"][b] is not None:
+            self.s_h2d.wait_event(st["buf_free"][b])
         hip.check(L.tmh_stats_reset(h))
         nch = (S + CK - 1) // CK
-        mark(c, "h2d_begin", s_h2d)
+        self.mark(c, "h2d_begin", self.s_h2d)
         for j in range(nch):  # pass 1: arrivals -> Welford
             n = min(CK, S - j * CK)
+            g0 = self.s_begin + j * CK
             if j * CK < R:
                 dst = buf[j * CK:j * CK + n]
             else:
-                k = state["k_in"] % 2
-                state["k_in"] += 1
-                if state["stage_free"][k] is not None:
-                    s_h2d.wait_event(state["stage_free"][k])
-                dst = stage[k][:n]
-            cs.wait_event(h2d(dst, j, c))
+                k = st["k_in"] % 2
+                st["k_in"] += 1
+                if st["stage_free"][k] is not None:
+                    self.s_h2d.wait_event(st["stage_free"][k])
+                dst = self.stage[k][:n]
+            cs.wait_event(self.h2d(dst, g0, n, c))
             hip.check(L.tmh_stats_update_welford_device(h, ptr(dst), n, 1, sp))
             if j * CK >= R:
-                state["stage_free"][k] = record(cs)
-        mark(c, "h2d_end", s_h2d)
+                st["stage_free"][k] = self._record(cs)
+        self.mark(c, "h2d_end", self.s_h2d)
         with torch.cuda.stream(cs):
-            if dist_on:
-                merge_welford(ops, dist, n_total=S_total)
+            if self.dist is not None:
+                merge_welford(ops, self.dist, n_total=self.S_total)
             hip.check(L.tmh_stats_finalize_device(h, ptr(mean), ptr(std), sp))
             hip.check(L.tmh_smooth_f64_device(ptr(mean), ptr(smean), ptr(ptmp), H, W, 5.0, sp))
             hip.check(L.tmh_smooth_f64_device(ptr(std), ptr(sstd), ptr(ptmp), H, W, 5.0, sp))
             hip.check(L.tmh_corrector_update_device(corr, ptr(smean), ptr(sstd), sp))
         for j in range(nch):  # pass 2: correct + histogram -> out slots -> host
             n = min(CK, S - j * CK)
+            g0 = self.s_begin + j * CK
             if j * CK < R:
                 src = buf[j * CK:j * CK + n]
             else:
-                k = state["k_in"] % 2
-                state["k_in"] += 1
-                if state["stage_free"][k] is not None:
-                    s_h2d.wait_event(state["stage_free"][k])
-                src = stage[k][:n]
-                cs.wait_event(h2d(src, j, c))
-            o = state["k_out"] % 4
-            state["k_out"] += 1
-            if state["out_free"][o] is not None:
-                cs.wait_event(state["out_free"][o])
-            hip.check(L.tmh_correct_u16_hist_device(corr, h, ptr(src), ptr(d_out[o]), n, -1, -1,
-                                                    sp))
-            e = record(cs)
+                k = st["k_in"] % 2
+                st["k_in"] += 1
+                if st["stage_free"][k] is not None:
+                    self.s_h2d.wait_event(st["stage_free"][k])
+                src = self.stage[k][:n]
+                cs.wait_event(self.h2d(src, g0, n, c))
+            o = st["k_out"] % 4
+            st["k_out"] += 1
+            if st["out_free"][o] is not None:
+                cs.wait_event(st["out_free"][o])
+            hip.check(L.tmh_correct_u16_hist_device(corr, h, ptr(src), ptr(self.d_out[o]), n, -1,
+                                                    -1, sp))
+            with torch.cuda.stream(cs):  # corrected planes kept for a check
+                for g in range(g0, g0 + n):
+                    if (c, g) in self.keep:
+                        self.kept[(c, g)] = self.d_out[o][g - g0].clone()
+            e = self._record(cs)
             if j * CK >= R:
-                state["stage_free"][k] = e
-            s_d2h.wait_event(e)
-            with torch.cuda.stream(s_d2h):
-                h_out[o][:n].copy_(d_out[o][:n], non_blocking=True)
-            state["out_free"][o] = record(s_d2h)
-        mark(c, "d2h_end", s_d2h)
-        if dist_on:
-            with torch.cuda.stream(cs):
-                merge_counts(ops, dist)
-        state["buf_free"][b] = record(cs)
+                st["stage_free"][k] = e
+            self.s_d2h.wait_event(e)
+            with torch.cuda.stream(self.s_d2h):
+                self.h_out[o][:n].copy_(self.d_out[o][:n], non_blocking=True)
+            st["out_free"][o] = self._record(self.s_d2h)
+        self.mark(c, "d2h_end", self.s_d2h)
+        with torch.cuda.stream(cs):
+            if self.dist is not None:
+                merge_counts(ops, self.dist)
+            # the channel's results, before the handle serves channel c + 2
+            r = self.res.get(c)
+            if r is None:
+                r = self.res[c] = {k: torch.empty(self.npx, dtype=torch.float64, device=self.dev)
+                                   for k in ("mean", "std", "smean", "sstd")}
+                r["acc"] = torch.empty(100000, dtype=torch.float64, device=self.dev)
+                r["hist"] = torch.empty(65536, dtype=torch.int64, device=self.dev)
+            for k, t in (("mean", mean), ("std", std), ("smean", smean), ("sstd", sstd)):
+                r[k].copy_(t)
+            hip.check(L.tmh_stats_get_pct_sum_device(h, ptr(r["acc"]), sp))
+            hip.check(L.tmh_stats_get_hist_device(h, ptr(r["hist"]), sp))
+        st["buf_free"][b] = self._record(cs)
 
-    log("stream-host: warm-up (both buffers)")
-    channel(0)
-    channel(1)
+    def results(self, c):
+        """channel c's results on the host (synchronises)"""
+        self.torch.cuda.synchronize(self.dev)
+        r = self.res[c]
+        out = {k: r[k].cpu().numpy() for k in ("mean", "std", "smean", "sstd", "acc")}
+        out["hist"] = r["hist"].cpu().numpy().astype(np.uint64)
+        out["n"] = self.S_total
+        out["kept"] = {g: t.cpu().numpy().view(np.uint16)
+                       for (cc, g), t in self.kept.items() if cc == c}
+        return out
+
+    def close(self):
+        self.torch.cuda.synchronize(self.dev)
+        for h, corr, *_ in self.handles:
+            self.L.tmh_corrector_destroy(corr)
+            self.L.tmh_stats_destroy(h)
+        self.handles = []
+
+
+def stream_fingerprint_name(H, W, S, CH, ring):
+    return "stream_fp_%dx%d_s%d_ch%d_ring%d_seed%d.npz" % (H, W, S, CH, ring, SEED)
+
+
+def check_stream_channel(fp, c, res):
+    """One channel of --stream-host against the committed oracle fingerprint
+    (tests/golden/make_stream_fingerprint.py): n, percentile sums and pooled
+    histogram bit-exact, mean/std at the sampled pixels within 1e-6."""
+    sp = fp["stat_px"]
+    return {
+        "n": int(res["n"]) == int(fp["n"]),
+        "pct_sums_bit_exact": hashlib.sha256(res["acc"].tobytes()).hexdigest() ==
+        str(fp["pct_sums_sha256"][c]),
+        "hist_bit_exact": hashlib.sha256(res["hist"].tobytes()).hexdigest() ==
+        str(fp["hist_sha256"][c]),
+        "mean_1e-6": _close(res["mean"][sp], fp["mean_samples"][c]),
+        "std_1e-6": _close(res["std"][sp], fp["std_samples"][c]),
+    }
+
+
+def bench_stream_host(a, world, rank, local_rank, dist_on):
+    """configs[4]: a multi-plate batch (4 plates x 384 wells x 16 sites = 24,576
+    sites per channel, 5 channels) that does not live in HBM: HostStreamJob
+    on every rank, timed over all channels (PCIe-bound: never the headline)."""
+    import torch
+    import torch.distributed as dist
+
+    from tmlibrary_amd import hip
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if dist_on:
+        dist.init_process_group("nccl", device_id=dev)
+    H, W = a.height, a.width
+    site_b = H * W * 2
+    CH = a.stream_channels
+    S_total = a.stream_sites
+    L = hip.lib()
+    hip.check(L.tmh_set_device(local_rank))
+    log("stream-host: link test")
+    link = link_rates(dev)
+    log("link: %s" % link)
+    job = HostStreamJob(L, dev, H, W, S_total, world, rank, a.resident_gb,
+                        dist=dist if dist_on else None)
+    log("stream-host: %d channels x %d sites/rank (%d resident, %d streamed twice); warm-up"
+        % (CH, job.S, job.R, job.S - job.R))
+    job.channel(0)
+    job.channel(1)
     torch.cuda.synchronize(dev)
-    for k in list(state):
-        state[k] = [None] * len(state[k]) if isinstance(state[k], list) else 0
+    job.reset_state()
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     log("stream-host: timing %d channels" % CH)
-    marks.clear()
-    host_t.clear()
+    job.marks.clear()
+    job.host_t.clear()
     t0 = time.perf_counter()
     for c in range(CH):
-        channel(c)
+        job.channel(c)
     torch.cuda.synchronize(dev)
     timeline = {}
-    if marks:
-        e0 = marks[0][2]
-        for c, phase, e in marks:
+    if job.marks:
+        e0 = job.marks[0][2]
+        for c, phase, e in job.marks:
             timeline.setdefault("c%d" % c, {})[phase] = round(e0.elapsed_time(e), 1)
-        for c, d in host_t.items():  # host enqueue times, same origin (approximately)
+        for c, d in job.host_t.items():  # host enqueue times, same origin (approximately)
             for k, v in d.items():
                 timeline[c][k] = round(1e3 * (v - t0), 1)
     if dist_on:
@@ -502,20 +603,24 @@ def bench_stream_host(a, world, rank, local_rank, dist_on):
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # the last channel's statistics are complete: one sanity check of the job
-    h, corr, sp, planes, ops = handles[(CH - 1) % 2]
-    nn = C.c_int64()
-    mean = np.empty(npx)
-    hip.check(L.tmh_stats_finalize(h, C.byref(nn), hip.ptr(mean), None, None, None))
-    for h, corr, *_ in handles:
-        L.tmh_corrector_destroy(corr)
-        L.tmh_stats_destroy(h)
+    # every channel's results against the oracle fingerprint of the same input
+    path = os.path.join(REPO, "tests", "golden",
+                        stream_fingerprint_name(H, W, S_total, CH, job.ring))
+    checks, check_ok = {}, None
+    if os.path.exists(path):
+        with np.load(path, allow_pickle=False) as z:
+            fp = {k: z[k] for k in z.files}
+        for c in range(CH):
+            checks["c%d" % c] = check_stream_channel(fp, c, job.results(c))
+        check_ok = all(all(v.values()) for v in checks.values())
+    job.close()
     if dist_on:
         dist.destroy_process_group()
     if rank != 0:
         return None
     sites_done = CH * S_total
-    h2d_b = CH * (S_total * site_b + (S_total - min(S_total, R * world)) * site_b)
+    R_all = job.R * world
+    h2d_b = CH * (S_total * site_b + (S_total - min(S_total, R_all)) * site_b)
     d2h_b = CH * S_total * site_b
     per_link = elapsed * world
     return {
@@ -523,12 +628,13 @@ def bench_stream_host(a, world, rank, local_rank, dist_on):
         "value": round(sites_done / elapsed, 1), "unit": "sites/s", "n_gpus": world,
         "ms_total": round(1e3 * elapsed, 1), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f64 stats / f32 correct (±1 DN)",
-        "data": "synthetic, %d distinct sites in a pinned host ring, cycled" % RING,
+        "data": "synthetic, %d distinct sites in a pinned host ring, cycled (channel c's site g "
+                "is ring site (g + 7c) %% %d)" % (job.ring, job.ring),
         "config": {"workload": "configs[4]: %d channels x %d sites (4 plates x 384 wells x 16 "
                                "sites) of %dx%d uint16 streamed from host, sharded over %d GPU(s)"
                                % (CH, S_total, H, W, world),
-                   "resident_sites_per_channel_per_gpu": R, "sites_per_channel_per_gpu": S,
-                   "chunk_sites": CK},
+                   "resident_sites_per_channel_per_gpu": job.R,
+                   "sites_per_channel_per_gpu": job.S, "chunk_sites": job.CK},
         "pcie": {"h2d_bytes": h2d_b, "d2h_bytes": d2h_b,
                  "h2d_GBs_per_gpu": round(h2d_b / per_link / 1e9, 1),
                  "d2h_GBs_per_gpu": round(d2h_b / per_link / 1e9, 1),
@@ -536,8 +642,9 @@ def bench_stream_host(a, world, rank, local_rank, dist_on):
                  "frac_of_duplex_link": round(max(h2d_b, d2h_b) / per_link / 1e9 /
                                               link["duplex_each_way_GBs"], 4)},
         "timeline_ms": timeline,
-        "check": {"n_last_channel": int(nn.value), "expected": S_total,
-                  "mean_finite": bool(np.isfinite(mean).all())},
+        "check": checks,
+        "check_vs_oracle": check_ok,
+        "fingerprint": os.path.relpath(path, REPO) if check_ok is not None else None,
     }
 
 
@@ -593,6 +700,120 @@ def check_against_fingerprint(fp, res, smean, sstd, corr_sites):
 
 
 # ---------------------------------------------------------------------------
+# multi-GPU cost model
+# ---------------------------------------------------------------------------
+
+class CollectiveTimer(object):
+    """``timer(name)`` context for sharded.merge_*: synchronises the device
+    before the collective (so no kernel of any stream is in flight), then
+    brackets it with events on torch's current stream -- each collective's own
+    time, including the wait for its peers, isolated from the kernels."""
+
+    def __init__(self, torch, dev):
+        self.torch, self.dev = torch, dev
+        self.events = []
+        self._name = None
+
+    def __call__(self, name):
+        self._name = name
+        return self
+
+    def __enter__(self):
+        self.torch.cuda.synchronize(self.dev)
+        self._a = self.torch.cuda.Event(enable_timing=True)
+        self._a.record(self.torch.cuda.current_stream(self.dev))
+        return self
+
+    def __exit__(self, *exc):
+        b = self.torch.cuda.Event(enable_timing=True)
+        b.record(self.torch.cuda.current_stream(self.dev))
+        self.events.append((self._name, self._a, b))
+        return False
+
+    def summary(self):
+        self.torch.cuda.synchronize(self.dev)
+        out = {}
+        for name, a, b in self.events:
+            d = out.setdefault(name, {"calls": 0, "total_ms": 0.0})
+            d["calls"] += 1
+            d["total_ms"] += a.elapsed_time(b)
+        for d in out.values():
+            d["mean_ms"] = round(d["total_ms"] / d["calls"], 4)
+            d["total_ms"] = round(d["total_ms"], 4)
+        return out
+
+
+def single_gpu_same_workload(L, dev, H, W, CH, S_total, dist_id, steps=3, warmup=1, B=64):
+    """configs[2]/[3] on ONE GPU: the CH channel jobs of S_total sites that an
+    N > 1 run shards over its ranks, run here one after another on one stream
+    -- every channel's sites resident in B-site blocks, one set of output
+    blocks reused by every channel (CH x 2 x 38 GB would not fit) -- the
+    like-for-like N = 1 point of the strong-scaling curve."""
+    import torch
+
+    from tmlibrary_amd import hip
+    from tmlibrary_amd.image import ZERO_LOG10
+    from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
+    npx = H * W
+    shift = B.bit_length() - 1
+    stream = torch.cuda.Stream(dev)
+    sp = C.c_void_p(stream.cuda_stream)
+    ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    ins, outs = [], []
+    for c in range(CH):
+        blk = []
+        for b0 in range(0, S_total, B):
+            m = min(B, S_total - b0)
+            blk.append(torch.empty((m, H, W), dtype=torch.int16, device=dev))
+            if c == 0:
+                outs.append(torch.empty((m, H, W), dtype=torch.int16, device=dev))
+            hip.check(L.tmh_synth_sites_device(ptr(blk[-1]), m, H, W, SEED, c, b0, dist_id, sp))
+        ins.append(blk)
+    t_in = [torch.tensor([t.data_ptr() for t in blk], dtype=torch.int64, device=dev) for blk in ins]
+    t_out = torch.tensor([t.data_ptr() for t in outs], dtype=torch.int64, device=dev)
+    lo, hi, gamma = quantile_table(npx, np.linspace(0, 100, 100000))
+    lut = stats_log10_lut()
+    h, corr = C.c_void_p(), C.c_void_p()
+    hip.check(L.tmh_stats_create(H, W, 100000, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
+                                 hip.ptr(lut), 1, 0, C.byref(h)))
+    hip.check(L.tmh_stats_set_stream(h, sp))
+    mean, std, smean, sstd, tmp = [torch.empty(npx, dtype=torch.float64, device=dev)
+                                   for _ in range(5)]
+    torch.cuda.synchronize(dev)
+    hip.check(L.tmh_corrector_create_device(ptr(mean), ptr(std), H, W, 1, ZERO_LOG10, sp,
+                                            C.byref(corr)))
+
+    def job(c):
+        hip.check(L.tmh_stats_reset(h))
+        hip.check(L.tmh_stats_update_welford_blocks_device(h, ptr(t_in[c]), shift, S_total, 1, sp))
+        hip.check(L.tmh_stats_finalize_device(h, ptr(mean), ptr(std), sp))
+        hip.check(L.tmh_smooth_f64_device(ptr(mean), ptr(smean), ptr(tmp), H, W, 5.0, sp))
+        hip.check(L.tmh_smooth_f64_device(ptr(std), ptr(sstd), ptr(tmp), H, W, 5.0, sp))
+        hip.check(L.tmh_corrector_update_device(corr, ptr(smean), ptr(sstd), sp))
+        hip.check(L.tmh_correct_u16_hist_blocks_device(corr, h, ptr(t_in[c]), ptr(t_out), shift,
+                                                       S_total, -1, -1, sp))
+
+    for _ in range(warmup):
+        for c in range(CH):
+            job(c)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        for c in range(CH):
+            job(c)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    L.tmh_corrector_destroy(corr)
+    L.tmh_stats_destroy(h)
+    del ins, outs, t_in, t_out
+    torch.cuda.empty_cache()
+    return {"workload": "%d channels x %d sites of %dx%d uint16 on one GPU, channel jobs one "
+                        "after another (the N > 1 workload unsharded)" % (CH, S_total, H, W),
+            "value": round(CH * S_total * steps / el, 1), "unit": "sites/s",
+            "ms_per_step": round(1e3 * el / steps, 3), "steps": steps}
+
+
+# ---------------------------------------------------------------------------
 
 def main():
     a = parse()
@@ -643,6 +864,14 @@ def main():
     n_channel = S_total if sharded else world * S_total  # sites per channel job
     L = hip.lib()
     hip.check(L.tmh_set_device(local_rank))
+    same = None
+    if sharded and world > 1 and not a.no_same_workload:
+        if rank == 0:  # before this run's buffers exist: the GPU's whole HBM is free
+            log("rank 0: the same %d-channel workload on this GPU alone" % CH)
+            same = single_gpu_same_workload(L, dev, H, W, CH, S_total,
+                                            DISTRIBUTIONS[a.distribution])
+            log("single GPU, same workload: %.1f sites/s" % same["value"])
+        dist.barrier()
     # one non-null stream for our launches AND torch/RCCL work, so they order
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
@@ -821,6 +1050,20 @@ def main():
             if k.value:
                 kern[name] = (ms.value / k.value, k.value)
         L.tmh_profile_enable(0)
+    collectives = None
+    if dist_on and prof:  # one more step with every collective timed on its own
+        ct = CollectiveTimer(torch, dev)
+        for ch in chans:
+            ch.stats()
+        for ch in chans:
+            with torch.cuda.stream(ch.stream):
+                merge_welford(ch.ops, dist, n_total=n_channel, timer=ct)
+        for ch in chans:
+            ch.apply()
+        for ch in chans:
+            with torch.cuda.stream(ch.stream):
+                merge_counts(ch.ops, dist, timer=ct)
+        collectives = ct.summary()
     merge_ms = None
     if dist_on and prof:
         merge_ms = []
@@ -964,6 +1207,13 @@ def main():
         }
         if merge_ms is not None:
             resd["merge_per_channel"] = merge_ms
+        if collectives is not None:
+            resd["collectives_isolated"] = {
+                "note": "one extra step, the device synchronised before each collective: its own "
+                        "time incl. the wait for peers (%d channels' calls summed)" % CH,
+                "per_collective": collectives}
+        if same is not None:
+            resd["single_gpu_same_workload"] = same
         resd["check"] = check
         resd["check_vs_oracle"] = check_ok
         if extras:

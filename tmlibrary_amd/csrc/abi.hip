@@ -265,6 +265,7 @@ struct tmh_stats {
   HostPipe pipe;
   DBuf<uint2> cdf;        // fold tail: per-site compact CDFs (cdf_ld entries per site)
   DBuf<int32_t> fbounds, fnnz;  // fold tail: chunk bounds [chunk][site], entries per site
+  int64_t fb_cap = 0;           // fold tail: sites per row of fbounds
   bool fold = true;       // percentile tail by compact CDF + fold (TMH_OPT_PCT_TAIL)
   bool last_fold = false; // the last fused launch took the fold tail (unless very wide)
   unsigned long long last_xthr = ~0ull;  // its very-wide threshold
@@ -1277,15 +1278,17 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
       const int64_t cdf_ld = std::min<int64_t>(kBins, h->npx);
       if (fold) {
         const size_t nb = (size_t)fold_chunks_host(h->Q);
-        const bool fgrow = (size_t)n_sites * cdf_ld > h->cdf.n ||
-                           nb * (size_t)n_sites > h->fbounds.n || (size_t)n_sites > h->fnnz.n;
-        if (fgrow) {
+        const bool fgrow = (size_t)n_sites * cdf_ld > h->cdf.n || n_sites > h->fb_cap ||
+                           (size_t)n_sites > h->fnnz.n;
+        if (fgrow) {  // growing frees buffers earlier launches may still be using
           TMH_HIP(hipStreamSynchronize(s));
           TMH_HIP(hipStreamSynchronize(h->stream));
         }
         h->cdf.ensure((size_t)n_sites * cdf_ld);
-        // bounds are laid out [chunk][site] with a stride of exactly n_sites
-        if (nb * (size_t)n_sites != h->fbounds.n) h->fbounds.alloc(nb * (size_t)n_sites);
+        if (n_sites > h->fb_cap) {  // bounds: [chunk][site], row stride fb_cap
+          h->fbounds.alloc(nb * (size_t)n_sites);
+          h->fb_cap = n_sites;
+        }
         h->fnnz.ensure((size_t)n_sites);
       }
       uint32_t* sh = (h->flags & 2u) ? h->site_hist.p : nullptr;
@@ -1335,7 +1338,7 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
                                reinterpret_cast<const unsigned long long*>(c->queues.p + 8),
                                n_sites, h->pooled.p, s);
           launch_pct_fold(h->hist_full.p, h->hist_rmask.p, n_sites, h->qp, h->cdf.p, cdf_ld,
-                          h->fbounds.p, h->fnnz.p, h->zeros.p, sh, h->gamma.p, h->acc.p,
+                          h->fbounds.p, h->fb_cap, h->fnnz.p, h->zeros.p, sh, h->gamma.p, h->acc.p,
                           h->wide.p, xwide_thresh, s);
           continue;
         }

@@ -1512,19 +1512,19 @@ __global__ __launch_bounds__(kFoldWaves * 64) void k_pct_fold(
 }
 
 void launch_pct_fold(uint32_t* hist, unsigned long long* rmask, int64_t n_sites, const QPos& p,
-                     uint2* cdf, int64_t cdf_ld, int32_t* bounds, int32_t* nnz,
+                     uint2* cdf, int64_t cdf_ld, int32_t* bounds, int64_t bounds_ld, int32_t* nnz,
                      int64_t* zero_counts, uint32_t* site_hist, const double* gamma, double* acc,
                      const unsigned long long* wide, unsigned long long xthr, hipStream_t s) {
   if (n_sites <= 0) return;
   {
     ProfScope prof("cdf_compact", s);
     hipLaunchKernelGGL(k_cdf_compact, dim3((unsigned)n_sites), dim3(kCdfThreads), 0, s, hist, rmask,
-                       p, cdf, cdf_ld, bounds, n_sites, nnz, zero_counts, site_hist, wide, xthr);
+                       p, cdf, cdf_ld, bounds, bounds_ld, nnz, zero_counts, site_hist, wide, xthr);
   }
   {
     ProfScope prof("pct_fold", s);
     hipLaunchKernelGGL(k_pct_fold, dim3((unsigned)fold_chunks(p.Q)), dim3(kFoldWaves * 64), 0, s,
-                       cdf, cdf_ld, bounds, n_sites, nnz, n_sites, p, gamma, acc, wide, xthr);
+                       cdf, cdf_ld, bounds, bounds_ld, nnz, n_sites, p, gamma, acc, wide, xthr);
   }
   TMH_HIP(hipGetLastError());
 }

@@ -139,26 +139,46 @@ class HostStagedDist(object):
         t.copy_(h)
 
 
-def merge_welford(ops, dist, group=None, int_device=None, n_total=None):
+class _NoTimer(object):
+    def __call__(self, name):
+        return self
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NO_TIMER = _NoTimer()
+
+
+def merge_welford(ops, dist, group=None, int_device=None, n_total=None, timer=None):
     """All-reduce merge of every rank's Welford state (identical on all ranks).
     Returns the global site count.  ``n_total`` (optional) is the global site
     count when the caller already knows it (e.g. from the shard bounds): it
     saves the count all-reduce, whose host read would block the issuing
-    thread until this rank's statistics pass has finished."""
+    thread until this rank's statistics pass has finished.  ``timer(name)``
+    (optional) is a context manager wrapped around each collective (bench.py
+    times them one by one)."""
     import torch
+    timer = timer or _NO_TIMER
     if n_total is None:
         dev = int_device if int_device is not None else getattr(ops, "device", "cpu")
         n_t = torch.tensor([ops.n_local()], dtype=torch.int64, device=dev)
-        dist.all_reduce(n_t, group=group)
+        with timer("allreduce_n"):
+            dist.all_reduce(n_t, group=group)
         n_total = int(n_t.item())
     n_total = int(n_total)
     if n_total > 0:
         buf = ops.empty_plane()
         ops.stage1(buf)
-        dist.all_reduce(buf, group=group)
+        with timer("allreduce_nmean"):
+            dist.all_reduce(buf, group=group)
         m2c = ops.empty_plane()
         ops.stage2(buf, n_total, m2c)
-        dist.all_reduce(m2c, group=group)
+        with timer("allreduce_m2c"):
+            dist.all_reduce(m2c, group=group)
         ops.stage3(n_total, m2c)
     return n_total
 
@@ -177,13 +197,14 @@ def chain_chunks(n_quantiles, world, chunks=None):
     return [(a, b - a) for a, b in zip(edges[:-1], edges[1:]) if b > a]
 
 
-def merge_percentiles(ops, dist, group=None, chunks=None):
+def merge_percentiles(ops, dist, group=None, chunks=None, timer=None):
     """Ordered percentile chain: the f64 accumulator travels rank 0 -> N-1,
     each rank adding its own sites in order (bit-exact sequential sum), and
     the last rank broadcasts it.  The accumulator is split into quantile
     chunks that flow down the chain as a pipeline (rank r adds chunk c while
     rank r-1 adds chunk c+1); every quantile still sees the ranks' sites in
     global site order."""
+    timer = timer or _NO_TIMER
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     acc = ops.empty_acc()
@@ -192,31 +213,36 @@ def merge_percentiles(ops, dist, group=None, chunks=None):
     for q0, qn in spans:
         part = acc[q0:q0 + qn]
         if rank > 0:
-            dist.recv(part, src=rank - 1, group=group)
+            with timer("chain_recv"):
+                dist.recv(part, src=rank - 1, group=group)
         if ranged:
             ops.pct_accumulate_range(part, q0, qn)
         else:
             ops.pct_accumulate(acc)
         if rank < world - 1:
-            dist.send(part, dst=rank + 1, group=group)
-    dist.broadcast(acc, src=world - 1, group=group)
+            with timer("chain_send"):
+                dist.send(part, dst=rank + 1, group=group)
+    with timer("broadcast_pct"):
+        dist.broadcast(acc, src=world - 1, group=group)
     ops.set_pct_sum(acc)
 
 
-def merge_histogram(ops, dist, group=None):
+def merge_histogram(ops, dist, group=None, timer=None):
     """All-reduce of the pooled per-site histograms (exact integer sums)."""
+    timer = timer or _NO_TIMER
     buf = ops.empty_hist()
     ops.get_hist(buf)
-    dist.all_reduce(buf, group=group)
+    with timer("allreduce_hist"):
+        dist.all_reduce(buf, group=group)
     ops.set_hist(buf)
 
 
-def merge_counts(ops, dist, group=None, chunks=None):
+def merge_counts(ops, dist, group=None, chunks=None, timer=None):
     """The merges that need every site's histogram: the ordered percentile
     chain and the pooled-histogram all-reduce (after the fused correct pass
     in the split pipeline)."""
-    merge_percentiles(ops, dist, group, chunks)
-    merge_histogram(ops, dist, group)
+    merge_percentiles(ops, dist, group, chunks, timer)
+    merge_histogram(ops, dist, group, timer)
 
 
 def merge_shards(ops, dist, group=None, int_device=None):
