@@ -1338,8 +1338,8 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
                                reinterpret_cast<const unsigned long long*>(c->queues.p + 8),
                                n_sites, h->pooled.p, s);
           launch_pct_fold(h->hist_full.p, h->hist_rmask.p, n_sites, h->qp, h->cdf.p, cdf_ld,
-                          h->fbounds.p, h->fb_cap, h->fnnz.p, h->zeros.p, sh, h->gamma.p, h->acc.p,
-                          h->wide.p, xwide_thresh, s);
+                          h->fbounds.p, h->fb_cap, h->fnnz.p, vlh, ld, h->zeros.p, sh, h->gamma.p,
+                          h->acc.p, h->wide.p, xwide_thresh, s);
           continue;
         }
         launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0, 0, nc,

@@ -201,12 +201,15 @@ void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t v
 // Percentile tail from the zero-maintained per-site histogram slab (round
 // masks rmask) without per-site order statistics: compact CDF per site
 // (cdf: cdf_ld >= min(65536, npx) entries per site) + chunk bounds (bounds:
-// fold_chunks(Q) rows of bounds_ld >= n_sites), then the in-order fold into acc[Q].  Needs
+// fold_chunks(Q) rows of bounds_ld >= n_sites), the order statistics of the
+// (site, chunk) pairs whose positions span many entries (os: quantile-tiled,
+// room for os_ld >= n_sites sites), then the in-order fold into acc[Q].  Needs
 // p.hi_next.  wide / xthr: skipped (device-side) for a very wide launch.
 void launch_pct_fold(uint32_t* hist, unsigned long long* rmask, int64_t n_sites, const QPos& p,
                      uint2* cdf, int64_t cdf_ld, int32_t* bounds, int64_t bounds_ld, int32_t* nnz,
-                     int64_t* zero_counts, uint32_t* site_hist, const double* gamma, double* acc,
-                     const unsigned long long* wide, unsigned long long xthr, hipStream_t s);
+                     uint32_t* os, int64_t os_ld, int64_t* zero_counts, uint32_t* site_hist,
+                     const double* gamma, double* acc, const unsigned long long* wide,
+                     unsigned long long xthr, hipStream_t s);
 int fold_chunks_host(int Q);
 // pooled[b] += sum over the sites of hist[s][b] for the rounds rmask names
 // (rm_all: the launch-wide union of the masks, or null)

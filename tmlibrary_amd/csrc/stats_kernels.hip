@@ -177,6 +177,19 @@ __device__ __forceinline__ uint4 ld_site(const uint4* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// A site pointer read from a block table is a generic pointer: the compiler
+// then emits flat loads (slower than global loads, and counted on both the
+// vector-memory and LDS counters).  Site loads through a global-address-space
+// pointer stay global_load.
+typedef unsigned int u32x4g_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4g_t gsite_t;
+__device__ __forceinline__ gsite_t* to_global(const void* p) { return (gsite_t*)p; }
+template <bool NTL>
+__device__ __forceinline__ uint4 ld_site(gsite_t* p) {
+  const u32x4g_t v = NTL ? __builtin_nontemporal_load(p) : *p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // BLK: blocked site layout (common.h SiteTab): site t of the launch is site
 // t & (2^shift - 1) of block t >> shift; the block base is re-read (one scalar
 // load) only when the walk enters a new block.
@@ -215,8 +228,8 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
   if (BLK)
     bbase = reinterpret_cast<const uint4*>(tab.in[s_begin >> tab.shift]) +
             (s_begin & ((1ll << tab.shift) - 1)) * ngroups;
-  auto site = [&](int64_t t) -> const uint4* {  // t: site of this part, non-decreasing
-    if (!BLK) return src + t * ngroups;
+  auto site = [&](int64_t t) -> gsite_t* {  // t: site of this part, non-decreasing
+    if (!BLK) return to_global(src + t * ngroups);
     if (t != bt) {
       bt = t;
       const int64_t gs = s_begin + t;
@@ -225,7 +238,7 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
       else
         bbase = reinterpret_cast<const uint4*>(tab.in[gs >> tab.shift]);
     }
-    return bbase + g;
+    return to_global(bbase + g);
   };
   // two-stage pipeline: the next group's loads are in flight while the
   // current group is folded in (tail loads clamp to the last site: harmless)
@@ -1100,7 +1113,7 @@ __global__ __launch_bounds__(kU16Threads) void k_hist_site_u16(
       atomicOr(&ovf, 1ull << (u >> 10));
     }
   };
-  const uint4* src = reinterpret_cast<const uint4*>(
+  gsite_t* src = to_global(
       tab.in ? tab.in[site_block(tab, s)] + site_in_block(tab, s) * npx : sites + s * npx);
   const int64_t n16 = npx >> 3;
   int64_t i = tid;
@@ -1290,15 +1303,17 @@ void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t v
 //   k_pct_fold     (one workgroup per chunk of kFoldQC quantiles) walks the
 //                  sites IN ORDER: wave w of round r resolves site 16 r + w's
 //                  previous / next values for the chunk's quantiles from the
-//                  entries between its two chunk bounds (one 64-entry window
-//                  on almost every chunk), the lerp goes to LDS, and after one
-//                  barrier the chunk's accumulator threads add the round's
+//                  entries between its two chunk bounds (one window of up to
+//                  kFoldWin entries, loaded a round ahead; the rare wider
+//                  spans were resolved by k_fold_heavy), the lerp goes to LDS,
+//                  and after a barrier the chunk's accumulator threads add the round's
 //                  16 sites in site order -- the same f64 adds, without
 //                  contraction, in the same order as k_pct_acc: bit-exact.
 // Bytes: ~0.17 GB written and read instead of 2 x 1.38 GB.
 constexpr int kFoldQPL = 4;                // quantiles per lane
 constexpr int kFoldQC = 64 * kFoldQPL;     // quantiles per chunk = per fold workgroup
 constexpr int kFoldWaves = 16;             // sites per fold round
+constexpr int kFoldWin = 256;              // compact-CDF entries one wave resolves from
 constexpr int kCdfSR = 4;                  // super-round: 4 x 1,024 bins
 constexpr int kCdfThreads = 1024;
 
@@ -1402,129 +1417,210 @@ __global__ __launch_bounds__(kCdfThreads) void k_cdf_compact(
   if (tid == 0) nnz[s] = nzb;
 }
 
-__global__ __launch_bounds__(kFoldWaves * 64) void k_pct_fold(
+// Heavy chunks: a chunk whose quantile positions span more than kFoldWin
+// compact-CDF entries of a site (the sparse upper tail of microscopy sites:
+// the top 256 quantiles of a standard site span ~2,000 distinct values) would
+// make the in-order fold walk many windows per site -- latency on the fold's
+// serial path (measured: 10.4 ms for the whole fold, all of it in the top
+// chunk's workgroup).  k_fold_heavy resolves those (site, chunk) pairs up
+// front, in parallel over sites, into the quantile-tiled order statistics
+// layout (previous | next << 16, common.h): one workgroup per site, thread =
+// quantile, a binary search over the chunk's entries.  k_pct_fold then reads
+// them like k_pct_acc does.
+__global__ __launch_bounds__(kFoldQC) void k_fold_heavy(
+    const uint2* __restrict__ cdf, int64_t cdf_ld, const int32_t* __restrict__ bounds,
+    int64_t bounds_ld, const int32_t* __restrict__ nnz, const QPos p, uint32_t* __restrict__ os,
+    int64_t tstride, const unsigned long long* __restrict__ wide, unsigned long long xthr) {
+  if (wide && __builtin_nontemporal_load(wide + 1) >= xthr) return;
+  __shared__ int32_t heavy[1024];  // chunks of this site that are heavy
+  __shared__ int n_heavy;
+  const int t = threadIdx.x;
+  const int64_t s = blockIdx.x;
+  const int nb = fold_chunks(p.Q);
+  const int32_t last_e = nnz[s] - 1;
+  if (t == 0) n_heavy = 0;
+  __syncthreads();
+  for (int c = t; c < nb; c += kFoldQC) {
+    const int32_t k0 = bounds[(int64_t)c * bounds_ld + s];
+    const int32_t k1 = c + 1 < nb ? bounds[(int64_t)(c + 1) * bounds_ld + s] : last_e;
+    const int32_t kend = k1 + 1 < last_e ? k1 + 1 : last_e;
+    if (kend - k0 + 1 > kFoldWin) {
+      const int i = atomicAdd(&n_heavy, 1);
+      if (i < 1024) heavy[i] = c;
+    }
+  }
+  __syncthreads();
+  const int nh = n_heavy < 1024 ? n_heavy : 1024;
+  const uint2* e = cdf + s * cdf_ld;
+  for (int i = 0; i < nh; ++i) {
+    const int c = heavy[i];
+    const int q = c * kFoldQC + t;
+    if (q >= p.Q) continue;
+    const int32_t k0 = bounds[(int64_t)c * bounds_ld + s];
+    const int32_t k1 = c + 1 < nb ? bounds[(int64_t)(c + 1) * bounds_ld + s] : last_e;
+    const int32_t kend = k1 + 1 < last_e ? k1 + 1 : last_e;
+    const uint32_t P = (uint32_t)p.lo[q];
+    int32_t x = k0 - 1, y = kend;  // cum[x] <= P < cum[y]
+    while (y - x > 1) {
+      const int32_t m = (x + y) >> 1;
+      if (e[m].x > P)
+        y = m;
+      else
+        x = m;
+    }
+    const uint2 ey = e[y];
+    const uint32_t Ph = P < (uint32_t)p.last ? P + 1u : P;
+    const uint32_t nv = ey.x > Ph ? ey.y : e[y + 1 <= last_e ? y + 1 : last_e].y;
+    os[(int64_t)c * tstride + s * kOsTile + t] = ey.y | (nv << 16);
+  }
+}
+
+__global__ __launch_bounds__(kFoldWaves * 64, 2) void k_pct_fold(
     const uint2* __restrict__ cdf, int64_t cdf_ld, const int32_t* __restrict__ bounds,
     int64_t bounds_ld, const int32_t* __restrict__ nnz, int64_t n_sites, const QPos p,
-    const double* __restrict__ gamma, double* __restrict__ acc,
-    const unsigned long long* __restrict__ wide, unsigned long long xthr) {
+    const uint32_t* __restrict__ os, int64_t tstride, const double* __restrict__ gamma,
+    double* __restrict__ acc, const unsigned long long* __restrict__ wide,
+    unsigned long long xthr) {
   if (wide && __builtin_nontemporal_load(wide + 1) >= xthr) return;  // very wide: k_pct_acc
-  __shared__ double vals[2][kFoldWaves][kFoldQC];
-  __shared__ uint32_t wcum[kFoldWaves][64], wval[kFoldWaves][64];
+  constexpr int WPL = kFoldWin / 64;  // window entries per lane
+  __shared__ double vals[kFoldWaves][kFoldQC];
+  __shared__ uint32_t wcum[kFoldWaves][kFoldWin], wval[kFoldWaves][kFoldWin];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c = blockIdx.x;
   const int nb = fold_chunks(p.Q);
   const int q0 = c * kFoldQC;
   // this lane's quantiles (consecutive: positions non-decreasing along the wave)
-  int32_t lo[kFoldQPL];
+  uint32_t lo[kFoldQPL];
   double g[kFoldQPL];
 #pragma unroll
   for (int j = 0; j < kFoldQPL; ++j) {
     const int q = q0 + lane * kFoldQPL + j;
     const bool ok = q < p.Q;
-    lo[j] = p.lo[ok ? q : p.Q - 1];
+    lo[j] = (uint32_t)p.lo[ok ? q : p.Q - 1];
     g[j] = ok ? gamma[q] : 0.0;
   }
   const bool adder = tid < kFoldQC && q0 + tid < p.Q;
   double a = adder ? acc[q0 + tid] : 0.0;
   constexpr uint32_t kInf = 0xFFFFFFFFu;
-  // the window of one site (entries start .. start + 63, past kend: +inf)
-  auto window = [&](const uint2* e, int32_t start, int32_t kend) -> uint2 {
-    const int32_t i = start + lane;
-    return i <= kend ? e[i] : make_uint2(kInf, 0u);
+  struct Work {  // one site's data for this chunk: its window, or its heavy order statistics
+    bool heavy;
+    uint2 e[WPL];
+    uint4 v;
   };
-  struct Bnd {
-    int32_t k0, kend;
-  };
-  auto bnd = [&](int64_t s) -> Bnd {
-    if (s >= n_sites) return Bnd{0, -1};
+  auto fetch = [&](int64_t s) -> Work {
+    Work r;
+    r.heavy = false;
+#pragma unroll
+    for (int m = 0; m < WPL; ++m) r.e[m] = make_uint2(kInf, 0u);
+    r.v = make_uint4(0u, 0u, 0u, 0u);
+    if (s >= n_sites) return r;
     const int32_t last_e = nnz[s] - 1;
     const int32_t k0 = bounds[(int64_t)c * bounds_ld + s];
     const int32_t k1 = c + 1 < nb ? bounds[(int64_t)(c + 1) * bounds_ld + s] : last_e;
-    return Bnd{k0, k1 + 1 < last_e ? k1 + 1 : last_e};
+    const int32_t kend = k1 + 1 < last_e ? k1 + 1 : last_e;
+    r.heavy = kend - k0 + 1 > kFoldWin;
+    if (r.heavy) {
+      r.v = *reinterpret_cast<const uint4*>(os + (int64_t)c * tstride + s * kOsTile +
+                                            lane * kFoldQPL);
+    } else {
+      const uint2* e = cdf + s * cdf_ld + k0;
+      const int32_t n = kend - k0;  // window entries 0 .. n
+#pragma unroll
+      for (int m = 0; m < WPL; ++m)
+        if (lane + 64 * m <= n) r.e[m] = e[lane + 64 * m];
+    }
+    return r;
   };
   const int rounds = (int)((n_sites + kFoldWaves - 1) / kFoldWaves);
-  // pipeline: round r's first window was loaded during round r - 1, round
-  // r + 1's bounds during round r - 1 as well
-  Bnd bc = bnd(w), bn = bnd((int64_t)kFoldWaves + w);
-  uint2 wc = bc.kend >= 0 ? window(cdf + (int64_t)w * cdf_ld, bc.k0, bc.kend) : make_uint2(kInf, 0u);
+  Work cur = fetch(w);
   for (int r = 0; r < rounds; ++r) {
     const int64_t s = (int64_t)r * kFoldWaves + w;
-    const int buf = r & 1;
-    const int64_t sn = s + kFoldWaves;
-    const uint2 wn = bn.kend >= 0 ? window(cdf + sn * cdf_ld, bn.k0, bn.kend) : make_uint2(kInf, 0u);
-    const Bnd bn2 = bnd(sn + kFoldWaves);
+    const Work nxt = fetch(s + kFoldWaves);  // in flight while this round resolves
     if (s < n_sites) {  // uniform per wave
-      const uint2* e = cdf + s * cdf_ld;
       uint32_t av[kFoldQPL], bv[kFoldQPL];
-      uint32_t done = 0u;
-      int32_t start = bc.k0;
-      uint2 cur = wc;
-      while (true) {
-        wcum[w][lane] = cur.x;
-        wval[w][lane] = cur.y;
+      if (cur.heavy) {
+        const uint32_t v[4] = {cur.v.x, cur.v.y, cur.v.z, cur.v.w};
+#pragma unroll
+        for (int j = 0; j < kFoldQPL; ++j) {
+          av[j] = v[j] & 0xFFFFu;
+          bv[j] = v[j] >> 16;
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < WPL; ++m) {
+          wcum[w][lane + 64 * m] = cur.e[m].x;
+          wval[w][lane + 64 * m] = cur.e[m].y;
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const bool final = start + 63 > bc.kend;
-        // positions resolved in this window: entry index <= start + 62 (so
-        // the next position's entry, index + 1, is in the window too)
-        const uint32_t lim = final ? kInf : wcum[w][62];
-#pragma unroll
-        for (int j = 0; j < kFoldQPL; ++j) {
-          if ((done >> j) & 1u) continue;
-          const uint32_t P = (uint32_t)lo[j];
-          if (P >= lim) continue;
-          int x = -1, y = 63;  // wcum[x] <= P < wcum[y]
+        // the chunk's positions all lie in the window: first entry with rank
+        // > P (the window's padding ranks are +inf); the lane's later
+        // quantiles start from the previous one's entry
+        int y = kFoldWin - 1;
+        {
+          int x = -1;
           while (y - x > 1) {
             const int m = (x + y) >> 1;
-            if (wcum[w][m] > P)
+            if (wcum[w][m] > lo[0])
               y = m;
             else
               x = m;
           }
+        }
+#pragma unroll
+        for (int j = 0; j < kFoldQPL; ++j) {
+          if (j > 0 && wcum[w][y] <= lo[j]) {
+            int x = y, z = kFoldWin - 1;
+            while (z - x > 1) {
+              const int m = (x + z) >> 1;
+              if (wcum[w][m] > lo[j])
+                z = m;
+              else
+                x = m;
+            }
+            y = z;
+          }
           av[j] = wval[w][y];
           // next position min(P + 1, n - 1): the same value unless P is the
           // last position of its bin (then it opens the next entry)
-          const uint32_t Ph = P < (uint32_t)p.last ? P + 1u : P;
-          bv[j] = wcum[w][y] > Ph ? av[j] : wval[w][y < 63 ? y + 1 : 63];
-          done |= 1u << j;
+          const uint32_t Ph = lo[j] < (uint32_t)p.last ? lo[j] + 1u : lo[j];
+          bv[j] = wcum[w][y] > Ph ? av[j] : wval[w][y < kFoldWin - 1 ? y + 1 : y];
         }
-        if (final) break;
-        start += 63;
-        __builtin_amdgcn_wave_barrier();  // window reads done before it is overwritten
-        cur = window(e, start, bc.kend);
       }
 #pragma unroll
-      for (int j = 0; j < kFoldQPL; ++j)
-        vals[buf][w][lane * kFoldQPL + j] = lerp_np(av[j], bv[j], g[j]);
+      for (int j = 0; j < kFoldQPL; ++j) vals[w][lane * kFoldQPL + j] = lerp_np(av[j], bv[j], g[j]);
     }
     __syncthreads();
     if (adder) {
 #pragma unroll
       for (int k = 0; k < kFoldWaves; ++k)
-        if ((int64_t)r * kFoldWaves + k < n_sites) a = add_nc(a, vals[buf][k][tid]);
+        if ((int64_t)r * kFoldWaves + k < n_sites) a = add_nc(a, vals[k][tid]);
     }
-    bc = bn;
-    bn = bn2;
-    wc = wn;
+    __syncthreads();  // vals are rewritten next round
+    cur = nxt;
   }
   if (adder) acc[q0 + tid] = a;
 }
 
 void launch_pct_fold(uint32_t* hist, unsigned long long* rmask, int64_t n_sites, const QPos& p,
                      uint2* cdf, int64_t cdf_ld, int32_t* bounds, int64_t bounds_ld, int32_t* nnz,
-                     int64_t* zero_counts, uint32_t* site_hist, const double* gamma, double* acc,
-                     const unsigned long long* wide, unsigned long long xthr, hipStream_t s) {
+                     uint32_t* os, int64_t os_ld, int64_t* zero_counts, uint32_t* site_hist,
+                     const double* gamma, double* acc, const unsigned long long* wide,
+                     unsigned long long xthr, hipStream_t s) {
   if (n_sites <= 0) return;
   {
     ProfScope prof("cdf_compact", s);
     hipLaunchKernelGGL(k_cdf_compact, dim3((unsigned)n_sites), dim3(kCdfThreads), 0, s, hist, rmask,
                        p, cdf, cdf_ld, bounds, bounds_ld, nnz, zero_counts, site_hist, wide, xthr);
+    hipLaunchKernelGGL(k_fold_heavy, dim3((unsigned)n_sites), dim3(kFoldQC), 0, s, cdf, cdf_ld,
+                       bounds, bounds_ld, nnz, p, os, os_ld * kOsTile, wide, xthr);
   }
   {
     ProfScope prof("pct_fold", s);
     hipLaunchKernelGGL(k_pct_fold, dim3((unsigned)fold_chunks(p.Q)), dim3(kFoldWaves * 64), 0, s,
-                       cdf, cdf_ld, bounds, bounds_ld, nnz, n_sites, p, gamma, acc, wide, xthr);
+                       cdf, cdf_ld, bounds, bounds_ld, nnz, n_sites, p, os, os_ld * kOsTile, gamma,
+                       acc, wide, xthr);
   }
   TMH_HIP(hipGetLastError());
 }
