@@ -193,7 +193,7 @@ __device__ __forceinline__ uint4 ld_site(gsite_t* p) {
 // BLK: blocked site layout (common.h SiteTab): site t of the launch is site
 // t & (2^shift - 1) of block t >> shift; the block base is re-read (one scalar
 // load) only when the walk enters a new block.
-template <bool LOG, bool NTL, int NT, int INV, bool BLK = false>
+template <bool LOG, bool NTL, int NT, int INV, bool BLK = false, int G = kWfGroup>
 __global__ __launch_bounds__(NT) void k_welford_vec8(
     const uint16_t* __restrict__ sites, int64_t npx, int64_t n_total, int64_t per,
     const WfMerge mg, double* __restrict__ mean, double* __restrict__ m2,
@@ -242,9 +242,9 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
   };
   // two-stage pipeline: the next group's loads are in flight while the
   // current group is folded in (tail loads clamp to the last site: harmless)
-  uint4 cur[kWfGroup], nxt[kWfGroup];
+  uint4 cur[G], nxt[G];
 #pragma unroll
-  for (int k = 0; k < kWfGroup; ++k) cur[k] = ld_site<NTL>(site(k < last ? k : last));
+  for (int k = 0; k < G; ++k) cur[k] = ld_site<NTL>(site(k < last ? k : last));
   double K[8], s1[8], s2[8];
   uint32_t wc = 0, xc = 0;  // this thread's groups with a value >= 4,096 / >= 16,384
   xform8<LOG, INV>(cur[0], slut, sinv, K, wc, xc);
@@ -255,14 +255,14 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
   // (gfx9 has no 64-bit scalar less-than; an int64 test costs two VALU ops
   // per site in a VALU-issue-bound loop)
   const int ns = (int)n_sites;
-  for (int s = 0; s < ns; s += kWfGroup) {
+  for (int s = 0; s < ns; s += G) {
 #pragma unroll
-    for (int k = 0; k < kWfGroup; ++k) {
-      const int t = s + kWfGroup + k;
+    for (int k = 0; k < G; ++k) {
+      const int t = s + G + k;
       nxt[k] = ld_site<NTL>(site(t < (int)last ? t : (int)last));
     }
 #pragma unroll
-    for (int k = 0; k < kWfGroup; ++k) {
+    for (int k = 0; k < G; ++k) {
       if (s + k < ns) {
         double x[8];
         xform8<LOG, INV>(cur[k], slut, sinv, x, wc, xc);
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
       }
     }
 #pragma unroll
-    for (int k = 0; k < kWfGroup; ++k) cur[k] = nxt[k];
+    for (int k = 0; k < G; ++k) cur[k] = nxt[k];
   }
 
   if (wide) {  // one global add per counter and workgroup (thread 0's group always exists)
@@ -400,7 +400,7 @@ static int welford_parts(int64_t n_sites, int64_t npx, size_t part_cap, int forc
   return forced && fits(forced) ? forced : 1;
 }
 
-template <int NT, int INV>
+template <int NT, int INV, int G = kWfGroup>
 static void launch_welford_vec8(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t per,
                                 int f, const WfMerge& mg, double* mean, double* m2,
                                 const double* lut, int log_transform, double* part,
@@ -411,7 +411,7 @@ static void launch_welford_vec8(const uint16_t* sites, int64_t npx, int64_t n_si
   // site loads are non-temporal (streamed once; regular loads measured
   // 6.60-6.75 vs 6.19-6.34 ms at job level, profiles/r1/ab_welford_ntl.txt)
 #define TMH_WF(L_, B_)                                                                           \
-  hipLaunchKernelGGL((k_welford_vec8<L_, true, NT, INV, B_>), grid, dim3(NT), 0, s, sites, npx, \
+  hipLaunchKernelGGL((k_welford_vec8<L_, true, NT, INV, B_, G>), grid, dim3(NT), 0, s, sites, npx, \
                      n_sites, per, mg, mean, m2, lut, part, wide, probe, probe_thr, tab)
   if (tab.in) {
     if (log_transform)
@@ -492,6 +492,10 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
       case 3: launch_welford_vec8<512, 1>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       case 4: launch_welford_vec8<256, 2>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       case 5: launch_welford_vec8<512, 2>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
+      // pipeline depth: sites per stage (two stages in flight)
+      case 6: launch_welford_vec8<256, 2, 3>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
+      case 7: launch_welford_vec8<256, 2, 4>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
+      case 8: launch_welford_vec8<512, 2, 4>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       default: launch_welford_vec8<kWfThreads, kWfInv>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s, pr, pthr, tab); break;
     }
     if (f > 1) {
@@ -1502,22 +1506,42 @@ __global__ __launch_bounds__(kFoldWaves * 64, 2) void k_pct_fold(
   const bool adder = tid < kFoldQC && q0 + tid < p.Q;
   double a = adder ? acc[q0 + tid] : 0.0;
   constexpr uint32_t kInf = 0xFFFFFFFFu;
+  // Each wave's per-site bounds come in batches of 64 rounds, lane i holding
+  // round (64 b + i)'s: vector loads issued 63 rounds ahead and read back with
+  // v_readlane.  (Scalar loads of them would share lgkmcnt with the LDS
+  // searches, and every LDS wait would then also wait for the next rounds'
+  // bounds: one memory latency per round on the serial path.)
+  struct Batch {
+    int32_t k0, kend;
+  };
+  auto load_batch = [&](int b) -> Batch {
+    const int64_t sb = (int64_t)(64 * b + lane) * kFoldWaves + w;
+    Batch r{0, -1};
+    if (sb < n_sites) {
+      const int32_t last_e = nnz[sb] - 1;
+      r.k0 = bounds[(int64_t)c * bounds_ld + sb];
+      const int32_t k1 = c + 1 < nb ? bounds[(int64_t)(c + 1) * bounds_ld + sb] : last_e;
+      r.kend = k1 + 1 < last_e ? k1 + 1 : last_e;
+    }
+    return r;
+  };
+  Batch bat[2] = {load_batch(0), load_batch(1)};
   struct Work {  // one site's data for this chunk: its window, or its heavy order statistics
     bool heavy;
     uint2 e[WPL];
     uint4 v;
   };
-  auto fetch = [&](int64_t s) -> Work {
+  auto fetch = [&](int rr) -> Work {  // round rr's site of this wave
     Work r;
     r.heavy = false;
 #pragma unroll
     for (int m = 0; m < WPL; ++m) r.e[m] = make_uint2(kInf, 0u);
     r.v = make_uint4(0u, 0u, 0u, 0u);
+    const int64_t s = (int64_t)rr * kFoldWaves + w;
     if (s >= n_sites) return r;
-    const int32_t last_e = nnz[s] - 1;
-    const int32_t k0 = bounds[(int64_t)c * bounds_ld + s];
-    const int32_t k1 = c + 1 < nb ? bounds[(int64_t)(c + 1) * bounds_ld + s] : last_e;
-    const int32_t kend = k1 + 1 < last_e ? k1 + 1 : last_e;
+    const Batch& bb = bat[(rr >> 6) & 1];
+    const int32_t k0 = __builtin_amdgcn_readlane(bb.k0, rr & 63);
+    const int32_t kend = __builtin_amdgcn_readlane(bb.kend, rr & 63);
     r.heavy = kend - k0 + 1 > kFoldWin;
     if (r.heavy) {
       r.v = *reinterpret_cast<const uint4*>(os + (int64_t)c * tstride + s * kOsTile +
@@ -1532,10 +1556,12 @@ __global__ __launch_bounds__(kFoldWaves * 64, 2) void k_pct_fold(
     return r;
   };
   const int rounds = (int)((n_sites + kFoldWaves - 1) / kFoldWaves);
-  Work cur = fetch(w);
+  Work cur = fetch(0);
   for (int r = 0; r < rounds; ++r) {
     const int64_t s = (int64_t)r * kFoldWaves + w;
-    const Work nxt = fetch(s + kFoldWaves);  // in flight while this round resolves
+    // the batch after next replaces the one just finished (63 rounds ahead)
+    if ((r & 63) == 0 && r > 0) bat[((r >> 6) + 1) & 1] = load_batch((r >> 6) + 1);
+    const Work nxt = fetch(r + 1);  // in flight while this round resolves
     if (s < n_sites) {  // uniform per wave
       uint32_t av[kFoldQPL], bv[kFoldQPL];
       if (cur.heavy) {

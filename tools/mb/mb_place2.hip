@@ -228,6 +228,22 @@ int main(int argc, char** argv) {
       CK(hipFree(tin));
       CK(hipFree(tout));
     }
+    {  // the blocked code path over ONE contiguous buffer: code cost vs placement
+      const int B = 64, nblk = (int)((S + B - 1) / B);
+      std::vector<uint16_t*> ib(nblk);
+      for (int k = 0; k < nblk; ++k) ib[k] = buf[0] + (size_t)k * B * npx;
+      uint16_t** tin;
+      CK(hipMalloc(&tin, nblk * sizeof(void*)));
+      CK(hipMemcpy(tin, ib.data(), nblk * sizeof(void*), hipMemcpyHostToDevice));
+      SiteTab tab;
+      tab.in = tin;
+      tab.out = nullptr;
+      tab.shift = 6;
+      printf("welford, blocked path over contiguous buffer 0:");
+      for (int r = 0; r < 3; ++r) printf(" %8.3f", welford(nullptr, tab));
+      printf("   contiguous path: %8.3f %8.3f\n", welford(buf[0], SiteTab{}),
+             welford(buf[0], SiteTab{}));
+    }
     printf("done\n");
   } catch (const tmh::Error& e) {
     fprintf(stderr, "tmh::Error %d: %s\n", e.code, e.msg.c_str());

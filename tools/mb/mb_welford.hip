@@ -392,9 +392,9 @@ static int run(int argc, char** argv) {
   var("wf var G2 Kf32 wps6", I2(), B1(), W6());
   var("wf var G4 Kf32 wps5", I4(), B1(), W5());
   var("wf var G1 Kf32 wps6", I1(), B1(), W6());
-  static const char* shapes[6] = {"256 thr, Newton rcp", "256 thr, LDS rcp", "512 thr, Newton rcp",
+  static const char* shapes[9] = {"256 thr, Newton rcp", "256 thr, LDS rcp", "512 thr, Newton rcp",
                                   "512 thr, LDS rcp", "256 thr, f32 small term", "512 thr, f32 small term"};
-  for (int shape = 0; shape < 6; ++shape)
+  for (int shape = 0; shape < 9; ++shape)
     for (int f : {1, 3}) {
       char nm[80];
       snprintf(nm, sizeof nm, "welford shape %d (%s) parts %d", shape, shapes[shape], f);
