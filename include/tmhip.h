@@ -102,11 +102,11 @@ int tmh_stats_reset(tmh_stats* h);
  *   TMH_OPT_TAIL_CHUNKS    1..16: run the fused correct+histogram pass in that
  *                          many site chunks, each chunk's histogram finalize
  *                          overlapping the next chunk's streaming (1: off)
- *   TMH_OPT_PCT_TAIL       percentile tail of the fused pass: 1 (default) =
- *                          per-site compact CDFs folded in site order per
- *                          quantile chunk; 0 = per-site order statistics
- *                          written, then summed (deferred handles, launches in
- *                          several chunks and non-linear quantile tables
+ *   TMH_OPT_PCT_TAIL       percentile tail of the fused pass: 0 (default) =
+ *                          per-site order statistics written, then summed in
+ *                          site order; 1 = per-site compact CDFs folded in site
+ *                          order per quantile chunk (deferred handles, launches
+ *                          in several chunks and non-linear quantile tables
  *                          always use 0).  Bit-identical results.
  *   TMH_OPT_COPY_THREADS   1..64 (default 8): host threads of the pageable <->
  *                          pinned copies of the host-buffer entry points

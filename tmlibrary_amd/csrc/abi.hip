@@ -266,7 +266,7 @@ struct tmh_stats {
   DBuf<uint2> cdf;        // fold tail: per-site compact CDFs (cdf_ld entries per site)
   DBuf<int32_t> fbounds, fnnz;  // fold tail: chunk bounds [chunk][site], entries per site
   int64_t fb_cap = 0;           // fold tail: sites per row of fbounds
-  bool fold = true;       // percentile tail by compact CDF + fold (TMH_OPT_PCT_TAIL)
+  bool fold = false;      // percentile tail by compact CDF + fold (TMH_OPT_PCT_TAIL)
   bool last_fold = false; // the last fused launch took the fold tail (unless very wide)
   unsigned long long last_xthr = ~0ull;  // its very-wide threshold
   DBuf<unsigned long long> last_wide;    // its (wide, very wide) group counts

@@ -1304,19 +1304,25 @@ void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t v
 //                  (inclusive rank, value) of the k-th non-empty bin -- and,
 //                  for every quantile chunk c, the index of the entry holding
 //                  the chunk's first previous position lo[c * kFoldQC];
-//   k_pct_fold     (one workgroup per chunk of kFoldQC quantiles) walks the
-//                  sites IN ORDER: wave w of round r resolves site 16 r + w's
-//                  previous / next values for the chunk's quantiles from the
-//                  entries between its two chunk bounds (one window of up to
-//                  kFoldWin entries, loaded a round ahead; the rare wider
-//                  spans were resolved by k_fold_heavy), the lerp goes to LDS,
-//                  and after a barrier the chunk's accumulator threads add the round's
-//                  16 sites in site order -- the same f64 adds, without
-//                  contraction, in the same order as k_pct_acc: bit-exact.
-// Bytes: ~0.17 GB written and read instead of 2 x 1.38 GB.
+//   k_pct_fold2    (one workgroup per chunk of kFoldQC quantiles) walks the
+//                  sites IN ORDER: wave w of round r resolves site
+//                  kFoldWaves r + w's previous / next values for the chunk's
+//                  quantiles from the entries between its two chunk bounds
+//                  (one window of up to kFoldWin entries; the rare wider spans
+//                  were resolved by k_fold_heavy), and the chunk's accumulator
+//                  threads add the round's sites in site order -- the same f64
+//                  adds, without contraction, in the same order as k_pct_acc:
+//                  bit-exact.
+// Bytes: ~0.17 GB written and read instead of 2 x 1.38 GB.  Measured on 3,456
+// standard sites (tools/mb/mb_fold.hip, profiles/r3/mb_fold_r3f.txt): compact
+// + heavy 0.17 ms, fold 1.13 ms (of which the per-quantile window searches
+// ~0.65, the window fetches and round structure ~0.34, the in-order adds
+// ~0.12) against 0.87-0.90 ms for the dense tail (finalize + k_pct_acc): the
+// search is VALU/LDS-issue-bound, so the dense tail is the default and the
+// fold an option (TMH_OPT_PCT_TAIL = 1).
 constexpr int kFoldQPL = 4;                // quantiles per lane
 constexpr int kFoldQC = 64 * kFoldQPL;     // quantiles per chunk = per fold workgroup
-constexpr int kFoldWaves = 16;             // sites per fold round
+constexpr int kFoldWaves = 8;              // sites per fold round (k_pct_fold2: 1.13 ms vs 1.20 with 16, 1.69 with 4)
 constexpr int kFoldWin = 256;              // compact-CDF entries one wave resolves from
 constexpr int kCdfSR = 4;                  // super-round: 4 x 1,024 bins
 constexpr int kCdfThreads = 1024;
@@ -1479,7 +1485,24 @@ __global__ __launch_bounds__(kFoldQC) void k_fold_heavy(
   }
 }
 
-__global__ __launch_bounds__(kFoldWaves * 64, 2) void k_pct_fold(
+// Fold, second form.  The first form's serial path paid a memory latency per
+// round: its window loads were conditional (per-lane and per-site branches),
+// so the compiler could not count them and waited for ALL outstanding loads
+// -- the next round's prefetch included -- before writing the current window
+// to LDS; 72 VGPRs left one 1,024-thread workgroup per CU (391 chunks on 256
+// CUs: two waves of workgroups); and the 16 in-order adds each waited for
+// their own LDS read.  Here every global load of a round is unconditional
+// (clamped addresses; a heavy site's order statistics or a dummy line), so the
+// compiler waits only for the round being resolved (vmcnt(8)); a site's chunk
+// bounds are fetched two rounds ahead and its window one round ahead; the
+// resolved (previous | next) pairs of round r go to one of two LDS buffers and
+// are added (lerp in the adder, reads first, then the in-order f64 adds) in
+// round r + 1, beside round r + 1's searches: one barrier per round.  The
+// searches are branchless lower bounds over the window's n + 1 entries
+// (depth log2 n, wave-uniform), the lane's quantiles searched side by side.
+template <int WAVES, int ABL = 0>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2 * WAVES / 4)))
+void k_pct_fold2(
     const uint2* __restrict__ cdf, int64_t cdf_ld, const int32_t* __restrict__ bounds,
     int64_t bounds_ld, const int32_t* __restrict__ nnz, int64_t n_sites, const QPos p,
     const uint32_t* __restrict__ os, int64_t tstride, const double* __restrict__ gamma,
@@ -1487,145 +1510,151 @@ __global__ __launch_bounds__(kFoldWaves * 64, 2) void k_pct_fold(
     unsigned long long xthr) {
   if (wide && __builtin_nontemporal_load(wide + 1) >= xthr) return;  // very wide: k_pct_acc
   constexpr int WPL = kFoldWin / 64;  // window entries per lane
-  __shared__ double vals[kFoldWaves][kFoldQC];
-  __shared__ uint32_t wcum[kFoldWaves][kFoldWin], wval[kFoldWaves][kFoldWin];
+  constexpr int QPL = kFoldQPL;
+  static_assert(QPL == 4 && kFoldQC == kOsTile, "one uint4 of a heavy site's order statistics per lane");
+  __shared__ uint2 win[WAVES][kFoldWin];       // (inclusive rank, value) of the window's entries
+  __shared__ uint4 ov[2][WAVES][kFoldQC / 4];  // resolved previous | next << 16, by round parity
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c = blockIdx.x;
   const int nb = fold_chunks(p.Q);
   const int q0 = c * kFoldQC;
-  // this lane's quantiles (consecutive: positions non-decreasing along the wave)
-  uint32_t lo[kFoldQPL];
-  double g[kFoldQPL];
+  const bool last_chunk = c + 1 >= nb;
+  const int cn = last_chunk ? c : c + 1;
+  const int64_t last_site = n_sites - 1;
+  uint32_t lo[QPL];
 #pragma unroll
-  for (int j = 0; j < kFoldQPL; ++j) {
-    const int q = q0 + lane * kFoldQPL + j;
-    const bool ok = q < p.Q;
-    lo[j] = (uint32_t)p.lo[ok ? q : p.Q - 1];
-    g[j] = ok ? gamma[q] : 0.0;
+  for (int j = 0; j < QPL; ++j) {
+    const int q = q0 + lane * QPL + j;
+    lo[j] = (uint32_t)p.lo[q < p.Q ? q : p.Q - 1];
   }
+  const uint32_t plast = (uint32_t)p.last;
   const bool adder = tid < kFoldQC && q0 + tid < p.Q;
-  double a = adder ? acc[q0 + tid] : 0.0;
-  constexpr uint32_t kInf = 0xFFFFFFFFu;
-  // Each wave's per-site bounds come in batches of 64 rounds, lane i holding
-  // round (64 b + i)'s: vector loads issued 63 rounds ahead and read back with
-  // v_readlane.  (Scalar loads of them would share lgkmcnt with the LDS
-  // searches, and every LDS wait would then also wait for the next rounds'
-  // bounds: one memory latency per round on the serial path.)
-  struct Batch {
-    int32_t k0, kend;
+  const int qa = q0 + (tid % kFoldQC) < p.Q ? q0 + (tid % kFoldQC) : p.Q - 1;
+  const double g = gamma[qa];
+  double a = acc[qa];
+  struct Desc {
+    int32_t k0, k1, ne;
   };
-  auto load_batch = [&](int b) -> Batch {
-    const int64_t sb = (int64_t)(64 * b + lane) * kFoldWaves + w;
-    Batch r{0, -1};
-    if (sb < n_sites) {
-      const int32_t last_e = nnz[sb] - 1;
-      r.k0 = bounds[(int64_t)c * bounds_ld + sb];
-      const int32_t k1 = c + 1 < nb ? bounds[(int64_t)(c + 1) * bounds_ld + sb] : last_e;
-      r.kend = k1 + 1 < last_e ? k1 + 1 : last_e;
+  auto load_desc = [&](int rr) -> Desc {  // all lanes: the wave's site of round rr
+    int64_t s = (int64_t)rr * WAVES + w;
+    s = s < last_site ? s : last_site;
+    return Desc{bounds[(int64_t)c * bounds_ld + s], bounds[(int64_t)cn * bounds_ld + s], nnz[s]};
+  };
+  struct Win {
+    uint2 e[WPL];  // the window's entries lane + 64 m; a heavy site: e[0], e[1] = its
+                   // order statistics of the lane's quantiles
+    int32_t n;     // window entries 0 .. n (uniform)
+    bool heavy;
+  };
+  auto fetch = [&](int rr, const Desc& d) -> Win {
+    int64_t s = (int64_t)rr * WAVES + w;
+    s = s < last_site ? s : last_site;
+    const int32_t last_e = __builtin_amdgcn_readfirstlane(d.ne) - 1;
+    const int32_t b0 = __builtin_amdgcn_readfirstlane(d.k0);
+    const int32_t b1 = last_chunk ? last_e : __builtin_amdgcn_readfirstlane(d.k1);
+    const int32_t kend = b1 + 1 < last_e ? b1 + 1 : last_e;
+    Win r;
+    r.n = kend - b0;
+    r.heavy = r.n + 1 > kFoldWin;
+    const uint2* e = cdf + s * cdf_ld + b0;
+    const uint2* h = reinterpret_cast<const uint2*>(os + (int64_t)c * tstride + s * kOsTile) +
+                     lane * (QPL / 2);
+    const int32_t nc = r.n > 0 ? r.n : 0;
+#pragma unroll
+    for (int m = 0; m < WPL; ++m) {
+      const int32_t i = lane + 64 * m;
+      const uint2* src = (m < QPL / 2 && r.heavy) ? h + m : e + (i < nc ? i : nc);
+      r.e[m] = *src;
     }
     return r;
   };
-  Batch bat[2] = {load_batch(0), load_batch(1)};
-  struct Work {  // one site's data for this chunk: its window, or its heavy order statistics
-    bool heavy;
-    uint2 e[WPL];
-    uint4 v;
-  };
-  auto fetch = [&](int rr) -> Work {  // round rr's site of this wave
-    Work r;
-    r.heavy = false;
+  auto process = [&](int rr, const Win& W) {
+    const int64_t s = (int64_t)rr * WAVES + w;
+    if (s >= n_sites) return;  // uniform per wave
+    uint32_t av[QPL], bv[QPL];
+    if (W.heavy) {
+      const uint32_t v[4] = {W.e[0].x, W.e[0].y, W.e[1].x, W.e[1].y};
 #pragma unroll
-    for (int m = 0; m < WPL; ++m) r.e[m] = make_uint2(kInf, 0u);
-    r.v = make_uint4(0u, 0u, 0u, 0u);
-    const int64_t s = (int64_t)rr * kFoldWaves + w;
-    if (s >= n_sites) return r;
-    const Batch& bb = bat[(rr >> 6) & 1];
-    const int32_t k0 = __builtin_amdgcn_readlane(bb.k0, rr & 63);
-    const int32_t kend = __builtin_amdgcn_readlane(bb.kend, rr & 63);
-    r.heavy = kend - k0 + 1 > kFoldWin;
-    if (r.heavy) {
-      r.v = *reinterpret_cast<const uint4*>(os + (int64_t)c * tstride + s * kOsTile +
-                                            lane * kFoldQPL);
+      for (int j = 0; j < QPL; ++j) {
+        av[j] = v[j] & 0xFFFFu;
+        bv[j] = v[j] >> 16;
+      }
     } else {
-      const uint2* e = cdf + s * cdf_ld + k0;
-      const int32_t n = kend - k0;  // window entries 0 .. n
+      const int32_t n = W.n;
 #pragma unroll
       for (int m = 0; m < WPL; ++m)
-        if (lane + 64 * m <= n) r.e[m] = e[lane + 64 * m];
-    }
-    return r;
-  };
-  const int rounds = (int)((n_sites + kFoldWaves - 1) / kFoldWaves);
-  Work cur = fetch(0);
-  for (int r = 0; r < rounds; ++r) {
-    const int64_t s = (int64_t)r * kFoldWaves + w;
-    // the batch after next replaces the one just finished (63 rounds ahead)
-    if ((r & 63) == 0 && r > 0) bat[((r >> 6) + 1) & 1] = load_batch((r >> 6) + 1);
-    const Work nxt = fetch(r + 1);  // in flight while this round resolves
-    if (s < n_sites) {  // uniform per wave
-      uint32_t av[kFoldQPL], bv[kFoldQPL];
-      if (cur.heavy) {
-        const uint32_t v[4] = {cur.v.x, cur.v.y, cur.v.z, cur.v.w};
+        if (lane + 64 * m <= n) win[w][lane + 64 * m] = W.e[m];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // y = number of entries with rank <= P among 0 .. n - 1 (entry n's rank
+      // exceeds every position of the chunk): the first entry with rank > P
+      int32_t y[QPL];
 #pragma unroll
-        for (int j = 0; j < kFoldQPL; ++j) {
-          av[j] = v[j] & 0xFFFFu;
-          bv[j] = v[j] >> 16;
-        }
-      } else {
+      for (int j = 0; j < QPL; ++j) y[j] = 0;
+      for (int32_t step = (n > 0 && !(ABL & 2)) ? (int32_t)(1u << (31 - __builtin_clz((uint32_t)n))) : 0; step > 0;
+           step >>= 1) {
+        uint32_t cm[QPL];
 #pragma unroll
-        for (int m = 0; m < WPL; ++m) {
-          wcum[w][lane + 64 * m] = cur.e[m].x;
-          wval[w][lane + 64 * m] = cur.e[m].y;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // the chunk's positions all lie in the window: first entry with rank
-        // > P (the window's padding ranks are +inf); the lane's later
-        // quantiles start from the previous one's entry
-        int y = kFoldWin - 1;
-        {
-          int x = -1;
-          while (y - x > 1) {
-            const int m = (x + y) >> 1;
-            if (wcum[w][m] > lo[0])
-              y = m;
-            else
-              x = m;
-          }
+        for (int j = 0; j < QPL; ++j) {
+          const int32_t t = y[j] + step;
+          const uint32_t v = win[w][(t <= n ? t : n) - 1].x;
+          cm[j] = t <= n ? v : 0xFFFFFFFFu;
         }
 #pragma unroll
-        for (int j = 0; j < kFoldQPL; ++j) {
-          if (j > 0 && wcum[w][y] <= lo[j]) {
-            int x = y, z = kFoldWin - 1;
-            while (z - x > 1) {
-              const int m = (x + z) >> 1;
-              if (wcum[w][m] > lo[j])
-                z = m;
-              else
-                x = m;
-            }
-            y = z;
-          }
-          av[j] = wval[w][y];
-          // next position min(P + 1, n - 1): the same value unless P is the
-          // last position of its bin (then it opens the next entry)
-          const uint32_t Ph = lo[j] < (uint32_t)p.last ? lo[j] + 1u : lo[j];
-          bv[j] = wcum[w][y] > Ph ? av[j] : wval[w][y < kFoldWin - 1 ? y + 1 : y];
-        }
+        for (int j = 0; j < QPL; ++j)
+          if (cm[j] <= lo[j]) y[j] += step;
       }
 #pragma unroll
-      for (int j = 0; j < kFoldQPL; ++j) vals[w][lane * kFoldQPL + j] = lerp_np(av[j], bv[j], g[j]);
+      for (int j = 0; j < QPL; ++j) {
+        const uint2 ey = win[w][y[j]];
+        const uint32_t nv = win[w][y[j] < n ? y[j] + 1 : n].y;
+        av[j] = ey.y;
+        // next position min(P + 1, n - 1): the same value unless P is the
+        // last position of its bin (then it opens the next entry)
+        const uint32_t Ph = lo[j] < plast ? lo[j] + 1u : lo[j];
+        bv[j] = ey.x > Ph ? ey.y : nv;
+      }
     }
-    __syncthreads();
-    if (adder) {
+    ov[rr & 1][w][lane] = make_uint4(av[0] | (bv[0] << 16), av[1] | (bv[1] << 16),
+                                     av[2] | (bv[2] << 16), av[3] | (bv[3] << 16));
+  };
+  auto add_round = [&](int rr) {  // round rr's sites, in site order
+    if (!adder || (ABL & 1)) return;
+    const int64_t left = n_sites - (int64_t)rr * WAVES;
+    const int nk = left < WAVES ? (int)left : WAVES;
+    const uint32_t* o = reinterpret_cast<const uint32_t*>(&ov[rr & 1][0][0]) + tid;
+    constexpr int G = 4;
 #pragma unroll
-      for (int k = 0; k < kFoldWaves; ++k)
-        if ((int64_t)r * kFoldWaves + k < n_sites) a = add_nc(a, vals[k][tid]);
+    for (int k0 = 0; k0 < WAVES; k0 += G) {
+      uint32_t v[G];
+#pragma unroll
+      for (int k = 0; k < G; ++k) v[k] = o[(k0 + k) * kFoldQC];
+#pragma unroll
+      for (int k = 0; k < G; ++k) {
+        const double l = lerp_np(v[k] & 0xFFFFu, v[k] >> 16, g);
+        a = k0 + k < nk ? add_nc(a, l) : a;
+      }
     }
-    __syncthreads();  // vals are rewritten next round
-    cur = nxt;
+  };
+  // rounds in pairs (an odd count's last round is empty: its sites are
+  // past the end, process skips them and add_round adds nothing)
+  const int rounds2 = (int)((n_sites + 2 * WAVES - 1) / (2 * WAVES)) * 2;
+  Desc d0 = load_desc(0), d1 = load_desc(1);
+  Win w0 = fetch(0, d0), w1;
+  for (int r = 0; r < rounds2; r += 2) {
+    d0 = load_desc(r + 2);
+    w1 = fetch(r + 1, d1);
+    process(r, w0);
+    if (r > 0) add_round(r - 1);
+    __syncthreads();
+    d1 = load_desc(r + 3);
+    w0 = fetch(r + 2, d0);
+    process(r + 1, w1);
+    add_round(r);
+    __syncthreads();
   }
+  add_round(rounds2 - 1);
   if (adder) acc[q0 + tid] = a;
 }
 
@@ -1644,7 +1673,7 @@ void launch_pct_fold(uint32_t* hist, unsigned long long* rmask, int64_t n_sites,
   }
   {
     ProfScope prof("pct_fold", s);
-    hipLaunchKernelGGL(k_pct_fold, dim3((unsigned)fold_chunks(p.Q)), dim3(kFoldWaves * 64), 0, s,
+    hipLaunchKernelGGL(k_pct_fold2<kFoldWaves>, dim3((unsigned)fold_chunks(p.Q)), dim3(kFoldWaves * 64), 0, s,
                        cdf, cdf_ld, bounds, bounds_ld, nnz, n_sites, p, os, os_ld * kOsTile, gamma,
                        acc, wide, xthr);
   }

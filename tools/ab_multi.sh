@@ -17,7 +17,7 @@ for i in $(seq 1 $R); do
     ORDER=(); for ((j=${#LIBS[@]}-1; j>=0; j--)); do ORDER+=("${LIBS[j]}"); done
   fi
   for L in "${ORDER[@]}"; do
-    TMH_LIB=$L timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-sample 0 --no-extras $BENCH_ARGS \
+    TMH_LIB=$L timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-sample 0 --no-extras ${BENCH_ARGS:-} \
       > gpurun_out/ab_$TAG.tmp 2>> gpurun_out/ab_$TAG.err || exit $?
     python3 -c "import json,sys; d=json.loads([l for l in open('gpurun_out/ab_$TAG.tmp') if l.strip()][-1]); print(json.dumps({'lib': sys.argv[1], 'value': d['value'], 'ms': d['ms_per_step'], 'check': d['check_vs_oracle'], 'k': {k: v['avg_ms'] for k, v in d['kernels'].items()}}))" $L >> gpurun_out/ab_$TAG.jsonl
     tail -1 gpurun_out/ab_$TAG.jsonl
