@@ -85,8 +85,12 @@ def parse():
                    help="fused pass (sites per unit, threads, LDS bins) configuration 0..3 "
                         "(TMH_OPT_FUSED_CONFIG; default: the library's)")
     p.add_argument("--block-sites", type=int, default=64,
-                   help="sites per HBM allocation (a power of two >= 4; blocked site layout, input "
-                        "and output blocks allocated alternately); 0: one contiguous buffer each")
+                   help="sites per HBM allocation of the corrected output (a power of two >= 4; "
+                        "blocked site layout); 0: one contiguous buffer")
+    p.add_argument("--in-layout", choices=["contiguous", "blocked"], default="contiguous",
+                   help="with --block-sites B: the input sites in one buffer (the Welford pass "
+                        "takes its contiguous path, the fused pass a block table into it) or in "
+                        "B-site blocks allocated alternately with the output blocks")
     p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
     p.add_argument("--no-same-workload", action="store_true",
                    help="N > 1: skip rank 0's single-GPU run of the same (unsharded) workload")
@@ -815,8 +819,18 @@ def single_gpu_same_workload(L, dev, H, W, CH, S_total, dist_id, steps=3, warmup
 
 # ---------------------------------------------------------------------------
 
+def claim_stdout():
+    """The one JSON line keeps stdout; everything else written to fd 1 (RCCL's
+    version banner, library prints) goes to stderr."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
 def main():
     a = parse()
+    out = claim_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -824,7 +838,7 @@ def main():
         r = bench_stream_host(a, world, rank, local_rank,
                               world > 1 or os.environ.get("TMH_BENCH_FORCE_DIST") == "1")
         if r is not None:
-            print(json.dumps(r), flush=True)
+            print(json.dumps(r), file=out, flush=True)
         return
     H, W = a.height, a.width
     npx = H * W
@@ -889,15 +903,29 @@ def main():
     if B:
         assert B >= 4 and B & (B - 1) == 0, "--block-sites must be a power of two >= 4"
     shift = B.bit_length() - 1 if B else 0
+    # The Welford pass reads the sites once, in site order: its contiguous path
+    # runs 0.25-0.3 ms faster than its block-table path (profiles/r3/
+    # ab_block_sites_0_vs_64_r3f.jsonl, mb_place2_r3g.txt), while the fused
+    # pass gains from blocked outputs; so by default the input is one buffer
+    # (block views of it for the fused pass's table) and the outputs blocks.
+    in_contig = not B or a.in_layout == "contiguous"
     chan_sites = []  # per channel: (input blocks, output blocks); one block if contiguous
     for c in range(CH):
         blk_in, blk_out = [], []
+        big = None
+        if B and in_contig:
+            big = torch.empty((S, H, W), dtype=torch.int16, device=dev)
+            hip.check(L.tmh_synth_sites_device(C.c_void_p(big.data_ptr()), S, H, W, SEED, c,
+                                               s_begin, dist_id, sp))
         for b0 in range(0, S, B if B else S):
             m = min(B, S - b0) if B else S
-            blk_in.append(torch.empty((m, H, W), dtype=torch.int16, device=dev))
+            if big is not None:
+                blk_in.append(big[b0:b0 + m])
+            else:
+                blk_in.append(torch.empty((m, H, W), dtype=torch.int16, device=dev))
+                hip.check(L.tmh_synth_sites_device(C.c_void_p(blk_in[-1].data_ptr()), m, H, W,
+                                                   SEED, c, s_begin + b0, dist_id, sp))
             blk_out.append(torch.empty((m, H, W), dtype=torch.int16, device=dev))
-            hip.check(L.tmh_synth_sites_device(C.c_void_p(blk_in[-1].data_ptr()), m, H, W, SEED, c,
-                                               s_begin + b0, dist_id, sp))
         chan_sites.append((blk_in, blk_out))
 
     def local_site(c, i, outputs=False):
@@ -954,7 +982,7 @@ def main():
 
         def stats(self):
             hip.check(L.tmh_stats_reset(self.h))
-            if fused and B:  # Welford pass; histograms come from the correction's read
+            if fused and B and not in_contig:  # Welford pass; histograms from the correction's read
                 hip.check(L.tmh_stats_update_welford_blocks_device(self.h, self.T_in, shift, S, 1,
                                                                    self.sp))
             elif fused:
@@ -1198,8 +1226,10 @@ def main():
                                        "merge, ordered percentile chain, histogram all-reduce")
                        if dist_on else "single GPU",
                        "pipeline": a.pipeline,
-                       "hbm_layout": ("blocks of %d sites, input and output blocks allocated "
-                                      "alternately" % B) if B else "contiguous"},
+                       "hbm_layout": (("sites in one buffer, corrected output in blocks of %d "
+                                       "sites" % B) if in_contig else
+                                      ("blocks of %d sites, input and output blocks allocated "
+                                       "alternately" % B)) if B else "contiguous"},
             "job_hbm_roofline_frac": round(job_bytes * a.steps / elapsed / 1e9 /
                                            (HBM_PEAK_GBS * world), 4),
             "roofline": roofline,
@@ -1219,7 +1249,7 @@ def main():
         if extras:
             resd["extras"] = extras
         resd["cpu_baseline"] = cpu
-        print(json.dumps(resd), flush=True)
+        print(json.dumps(resd), file=out, flush=True)
 
     for ch in chans:
         ch.close()
