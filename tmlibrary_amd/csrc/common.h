@@ -104,11 +104,14 @@ struct FixList {
   unsigned int cap;
 };
 
+__device__ __forceinline__ unsigned long long fix_code8(uint32_t mask, int64_t site, int64_t p0) {
+  return ((unsigned long long)site << 40) | ((unsigned long long)(mask & 0xFFu) << 32) |
+         (unsigned long long)(uint32_t)p0;
+}
+
 __device__ __forceinline__ void fix_push8(const FixList& fl, uint32_t mask, int64_t site, int64_t p0) {
   const unsigned int i = atomicAdd(fl.n, 1u);
-  if (i < fl.cap)
-    fl.e[i] = ((unsigned long long)site << 40) | ((unsigned long long)(mask & 0xFFu) << 32) |
-              (unsigned long long)(uint32_t)p0;
+  if (i < fl.cap) fl.e[i] = fix_code8(mask, site, p0);
 }
 
 __device__ __forceinline__ void fix_push(const FixList& fl, int64_t site, int64_t px) {

@@ -37,6 +37,18 @@ namespace tmh {
 
 constexpr int kFusedBands = 16;  // pixel bands of the unit sweep
 
+// A pointer every lane holds the same value of, moved to scalar registers: a
+// buffer resource built from a pointer loaded with a vector load (a block
+// table entry) would otherwise live in VGPRs, and the compiler wraps every
+// buffer load and store that uses it in a waterfall loop.
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ int xcc_id() {
   int x;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
@@ -191,9 +203,18 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   // alternating by unit, so one is published while the next unit fills the
   // other.  k_hist_finalize reads exactly these rounds.
   __shared__ unsigned long long rm_sh[2][SPU];
+  // f64 fixups: the pixel groups a unit flags are staged in LDS (two sets,
+  // alternating by unit like rm_sh) and appended to the global list by wave 0
+  // after the unit's flush.  (A global atomic with a return value in the pixel
+  // loop makes the compiler wait, wherever it is taken, for every load in
+  // flight -- the next stage's included.)
+  constexpr int kFixSh = 256;
+  __shared__ unsigned long long fix_sh[2][kFixSh];
+  __shared__ unsigned int fix_cnt[2];
   const int tid = threadIdx.x;
   for (int i = tid; i < SPU * SLICE; i += NT) bins[i] = 0u;
   if (tid < 2 * SPU) rm_sh[tid / SPU][tid % SPU] = 0ull;
+  if (tid < 2) fix_cnt[tid] = 0u;
   __syncthreads();
 
   const float4 m = mconst2[0];
@@ -256,12 +277,19 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
       ib = tab.in[b] + o;
       ob = tab.out[b] + o;
     }
-    r.rin = __builtin_amdgcn_make_buffer_rsrc((void*)ib, 0, r.ns * site_bytes, 0x00020000);
-    r.rout = __builtin_amdgcn_make_buffer_rsrc((void*)ob, 0, r.ns * site_bytes, 0x00020000);
+    r.rin = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(ib), 0, r.ns * site_bytes,
+                                              0x00020000);
+    r.rout = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(ob), 0, r.ns * site_bytes,
+                                               0x00020000);
     return r;
   };
+  // a lane whose group lies past the unit's band loads from past the buffers'
+  // ends: raw buffer loads there return 0 without touching memory, so every
+  // load of the pixel loop is unconditional and the compiler's wait before a
+  // stage counts exactly the loads issued after it
+  constexpr int kOOB = 0x7FFFFF00;
   auto load = [&](const Unit& un, int g, uint4 (&v)[SPU], float4 (&c)[4]) {
-    const int off = g * 16;
+    const int off = g < un.g1 ? g * 16 : kOOB;
 #pragma unroll
     for (int k = 0; k < SPU; ++k) {
       const u32x4_t w = __builtin_amdgcn_raw_buffer_load_b128(un.rin, off, k * site_bytes, 2);
@@ -275,10 +303,10 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     }
   };
 
-  uint4 v[SPU];
-  float4 c[4] = {cc, cc, cc, cc};
+  uint4 vA[SPU], vB[SPU];
+  float4 cA[4] = {cc, cc, cc, cc}, cB[4] = {cc, cc, cc, cc};
 #pragma unroll
-  for (int k = 0; k < SPU; ++k) v[k] = make_uint4(0, 0, 0, 0);
+  for (int k = 0; k < SPU; ++k) vA[k] = vB[k] = make_uint4(0, 0, 0, 0);
   bool pre = false;  // v/c already hold this unit's first group (loaded by the previous unit)
   int cur = grab(), par = 0;
   while (cur >= 0) {
@@ -324,38 +352,45 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
         return r;
       }
       const uint32_t far = fcorrect8<LOG, CLIP>(wd, cf, m.x, m.z, m.w, clo2, chi2, o);
-      if (far) fix_push8(fl, far, un.s0 + k, (int64_t)g * 8);
+      if (far) {
+        const unsigned int i = atomicAdd(&fix_cnt[par], 1u);
+        if (i < (unsigned int)kFixSh)
+          fix_sh[par][i] = fix_code8(far, un.s0 + k, (int64_t)g * 8);
+        else
+          fix_push8(fl, far, un.s0 + k, (int64_t)g * 8);  // rare: the unit's LDS set is full
+      }
       const u32x4_t r = {o[0], o[1], o[2], o[3]};
       return r;
     };
 
-    int g = un.g0 + tid;
-    if (!pre && g < un.g1) load(un, g, v, c);
-    pre = false;
-    // two-stage pipeline over the unit's pixel groups; the last stage loads
-    // the next unit's first group
-    while (g < un.g1) {
-      const int gn = g + NT;
-      uint4 vn[SPU];
-      float4 cn[4] = {cc, cc, cc, cc};
+    // two stages (A, B) over the unit's pixel groups, a uniform number of
+    // steps; A holds the unit's first group when the previous unit loaded it
+    auto stage = [&](const uint4 (&v)[SPU], const float4 (&cf)[4], int g) {
+      if (g < un.g1) {
 #pragma unroll
-      for (int k = 0; k < SPU; ++k) vn[k] = make_uint4(0, 0, 0, 0);
-      if (gn < un.g1) {
-        load(un, gn, vn, cn);
-      } else if (nxt >= 0 && nu.g0 + tid < nu.g1) {
-        load(nu, nu.g0 + tid, vn, cn);
-        pre = true;
+        for (int k = 0; k < SPU; ++k)
+          if (k < un.ns)
+            __builtin_amdgcn_raw_buffer_store_b128(process(v[k], k, cf, g), un.rout, g * 16,
+                                                   k * site_bytes, 2);
       }
-#pragma unroll
-      for (int k = 0; k < SPU; ++k)
-        if (k < un.ns)
-          __builtin_amdgcn_raw_buffer_store_b128(process(v[k], k, c, g), un.rout, g * 16,
-                                                 k * site_bytes, 2);
-#pragma unroll
-      for (int k = 0; k < SPU; ++k) v[k] = vn[k];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) c[p] = cn[p];
-      g = gn;
+    };
+    const int iters = (un.g1 - un.g0 + NT - 1) / NT;
+    int g = un.g0 + tid;
+    if (!pre) load(un, g, vA, cA);
+    pre = false;
+    for (int it = 0; it < iters; it += 2) {
+      load(un, g + NT, vB, cB);
+      stage(vA, cA, g);
+      g += NT;
+      if (it + 1 >= iters) break;
+      load(un, g + NT, vA, cA);
+      stage(vB, cB, g);
+      g += NT;
+    }
+    // the next unit's first group is in flight during this unit's flush
+    if (nxt >= 0) {
+      load(nu, nu.g0 + tid, vA, cA);
+      pre = true;
     }
     cur = nxt;
     if (ABL & 9) continue;
@@ -388,6 +423,19 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
         atomicOr(reinterpret_cast<unsigned long long*>(queues + 8), r);  // launch-wide union
       }
       rm[tid] = 0ull;
+    }
+    // append the unit's staged fixups (wave 0; the set is next written two
+    // units on, after barriers wave 0 reaches only when done here)
+    if (tid < 64) {
+      const unsigned int nf = fix_cnt[par] < (unsigned int)kFixSh ? fix_cnt[par] : kFixSh;
+      if (nf) {
+        unsigned int base = 0u;
+        if (tid == 0) base = atomicAdd(fl.n, nf);
+        base = __builtin_amdgcn_readfirstlane(base);
+        for (unsigned int i = tid; i < nf; i += 64)
+          if (base + i < fl.cap) fl.e[base + i] = fix_sh[par][i];
+      }
+      if (tid == 0) fix_cnt[par] = 0u;
     }
     par ^= 1;
   }
