@@ -109,6 +109,11 @@ def main():
             res["run_job_fixed_s_est"] = round(
                 t_one - a.sites / max(res["run_job_marginal_sites_per_s"], 1e-9), 3)
         res["cpus_visible"] = os.cpu_count()
+        res["granted_cores"] = h5.granted_cores()
+        try:
+            res["affinity_cpus"] = len(os.sched_getaffinity(0))
+        except AttributeError:
+            pass
         res["threads"] = a.threads
         print(json.dumps(res), flush=True)
     finally:
