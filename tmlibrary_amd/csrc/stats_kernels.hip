@@ -77,14 +77,22 @@ __device__ __forceinline__ double log10_big(uint32_t u, const double* slut, cons
 // set (one OR/AND over the four packed words).
 constexpr int kWfLut = 4096;
 
-template <int INV>
+template <int INV, int LUTN = kWfLut>
 __device__ __forceinline__ void fill_wf_tables(const double* __restrict__ lut, double* slut,
                                                double* sinv, int nt) {
-  for (int i = threadIdx.x; i < kWfLut; i += nt) {
+  for (int i = threadIdx.x; i < LUTN; i += nt) {
     slut[i] = lut[i];
-    if (INV == 1) sinv[i] = i ? 1.0 / (16.0 * (double)i) : 0.0;
+    if (INV == 1 && i < kWfLut) sinv[i] = i ? 1.0 / (16.0 * (double)i) : 0.0;
   }
 }
+
+// Bright sites: the host LUT's first kWfLutBright entries (128 KB of LDS, one
+// 1,024-thread workgroup per CU) -- values below 16,384 take the exact table
+// like the standard pass's values below 4,096, and only the ~2% of bright
+// pixels >= 16,384 the log10_big path (with 4,096 entries most bright pixels
+// took it: the pass was VALU-bound, 11.3-12.3 ms against 6.0 on standard sites)
+constexpr int kWfLutBright = 16384;
+constexpr int kWfThreadsBright = 1024;
 
 template <bool LOG>
 __device__ __forceinline__ double xform(uint32_t u, const double* slut) {
@@ -121,14 +129,25 @@ __global__ void k_rn_table(double* __restrict__ rn, int64_t n0, int64_t n) {
 // groups, xc the groups with a value >= 16,384: the fused pass picks its
 // histogram configuration from them).  The inner loop is VALU-issue bound (3 f64 ops per
 // pixel), so the integer work per pixel is kept to the gather address.
-template <bool LOG, int INV>
+template <bool LOG, int INV, int LUTN = kWfLut>
 __device__ __forceinline__ void xform8(const uint4 v, const double* slut, const double* sinv,
                                        double (&x)[8], uint32_t& wc, uint32_t& xc) {
   const uint32_t u[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
                          v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
   const uint32_t any = v.x | v.y | v.z | v.w;
   const bool wide = (any & 0xF000F000u) != 0;
-  if (LOG) {
+  if (LOG && LUTN == kWfLutBright) {  // exact below 16,384
+    constexpr uint32_t kIdx = LUTN - 1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = slut[u[k] & kIdx];
+    wc += wide ? 1u : 0u;
+    if (any & 0xC000C000u) {  // a value >= 16,384
+      ++xc;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (u[k] > kIdx) x[k] = log10_big<INV>(u[k], slut, sinv);
+    }
+  } else if (LOG) {
     constexpr uint32_t kIdx = kWfLut - 1;
 #pragma unroll
     for (int k = 0; k < 8; ++k) x[k] = slut[u[k] & kIdx];
@@ -193,7 +212,11 @@ __device__ __forceinline__ uint4 ld_site(gsite_t* p) {
 // BLK: blocked site layout (common.h SiteTab): site t of the launch is site
 // t & (2^shift - 1) of block t >> shift; the block base is re-read (one scalar
 // load) only when the walk enters a new block.
-template <bool LOG, bool NTL, int NT, int INV, bool BLK = false, int G = kWfGroup>
+// SEL (with a probe): 0 = the probe picks one part or all of gridDim.y (the
+// standard pass), 1 = run only when the probe found standard sites (one
+// part), 2 = run only when it found bright ones (LUTN = kWfLutBright)
+template <bool LOG, bool NTL, int NT, int INV, bool BLK = false, int G = kWfGroup,
+          int LUTN = kWfLut, int SEL = 0>
 __global__ __launch_bounds__(NT) void k_welford_vec8(
     const uint16_t* __restrict__ sites, int64_t npx, int64_t n_total, int64_t per,
     const WfMerge mg, double* __restrict__ mean, double* __restrict__ m2,
@@ -203,14 +226,18 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
   // probe (k_wf_probe): the site split applies only to bright sites; otherwise
   // the part-0 workgroups walk every site and the others leave at once
   int parts = (int)gridDim.y;
-  if (probe && __builtin_nontemporal_load(probe) < probe_thr) {
-    if (blockIdx.y > 0) return;
-    parts = 1;
-    per = n_total;
+  if (probe) {
+    const bool bright = __builtin_nontemporal_load(probe) >= probe_thr;
+    if ((SEL == 1 && bright) || (SEL == 2 && !bright)) return;
+    if (SEL == 0 && !bright) {
+      if (blockIdx.y > 0) return;
+      parts = 1;
+      per = n_total;
+    }
   }
-  __shared__ double slut[kWfLut], sinv[INV == 1 ? kWfLut : 1];
+  __shared__ double slut[LUTN], sinv[INV == 1 ? kWfLut : 1];
   __shared__ uint32_t wide_sh[2];
-  if (LOG) fill_wf_tables<INV>(lut, slut, sinv, NT);
+  if (LOG) fill_wf_tables<INV, LUTN>(lut, slut, sinv, NT);
   if (threadIdx.x < 2) wide_sh[threadIdx.x] = 0u;
   __syncthreads();
   const int64_t ngroups = npx >> 3;
@@ -247,7 +274,7 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
   for (int k = 0; k < G; ++k) cur[k] = ld_site<NTL>(site(k < last ? k : last));
   double K[8], s1[8], s2[8];
   uint32_t wc = 0, xc = 0;  // this thread's groups with a value >= 4,096 / >= 16,384
-  xform8<LOG, INV>(cur[0], slut, sinv, K, wc, xc);
+  xform8<LOG, INV, LUTN>(cur[0], slut, sinv, K, wc, xc);
   wc = xc = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.0;
@@ -265,7 +292,7 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
     for (int k = 0; k < G; ++k) {
       if (s + k < ns) {
         double x[8];
-        xform8<LOG, INV>(cur[k], slut, sinv, x, wc, xc);
+        xform8<LOG, INV, LUTN>(cur[k], slut, sinv, x, wc, xc);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const double d = x[j] - K[j];
@@ -400,7 +427,7 @@ static int welford_parts(int64_t n_sites, int64_t npx, size_t part_cap, int forc
   return forced && fits(forced) ? forced : 1;
 }
 
-template <int NT, int INV, int G = kWfGroup>
+template <int NT, int INV, int G = kWfGroup, int LUTN = kWfLut, int SEL = 0>
 static void launch_welford_vec8(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t per,
                                 int f, const WfMerge& mg, double* mean, double* m2,
                                 const double* lut, int log_transform, double* part,
@@ -411,7 +438,8 @@ static void launch_welford_vec8(const uint16_t* sites, int64_t npx, int64_t n_si
   // site loads are non-temporal (streamed once; regular loads measured
   // 6.60-6.75 vs 6.19-6.34 ms at job level, profiles/r1/ab_welford_ntl.txt)
 #define TMH_WF(L_, B_)                                                                           \
-  hipLaunchKernelGGL((k_welford_vec8<L_, true, NT, INV, B_, G>), grid, dim3(NT), 0, s, sites, npx, \
+  hipLaunchKernelGGL((k_welford_vec8<L_, true, NT, INV, B_, G, LUTN, SEL>), grid, dim3(NT), 0, s, \
+                     sites, npx, \
                      n_sites, per, mg, mean, m2, lut, part, wide, probe, probe_thr, tab)
   if (tab.in) {
     if (log_transform)
@@ -496,7 +524,19 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
       case 6: launch_welford_vec8<256, 2, 3>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       case 7: launch_welford_vec8<256, 2, 4>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       case 8: launch_welford_vec8<512, 2, 4>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
-      default: launch_welford_vec8<kWfThreads, kWfInv>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s, pr, pthr, tab); break;
+      default:
+        if (pr) {  // the probe picks one of two passes on the device
+          launch_welford_vec8<kWfThreads, kWfInv, kWfGroup, kWfLut, 1>(
+              sites, npx, n_sites, n_sites, 1, mg, mean, m2, lut, log_transform, part, wide, s, pr,
+              pthr, tab);
+          launch_welford_vec8<kWfThreadsBright, kWfInv, kWfGroup, kWfLutBright, 2>(
+              sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s, pr, pthr,
+              tab);
+        } else {
+          launch_welford_vec8<kWfThreads, kWfInv>(sites, npx, n_sites, per, f, mg, mean, m2, lut,
+                                                  log_transform, part, wide, s, pr, pthr, tab);
+        }
+        break;
     }
     if (f > 1) {
       WfParts pc{};
