@@ -101,7 +101,7 @@ static int run(int argc, char** argv) {
   CK(hipMalloc(&in, bytes));
   CK(hipMalloc(&out, bytes));
   const int dist = argc > 3 ? atoi(argv[3]) : 0;
-  const bool quick = argc > 4 && atoi(argv[4]) == 1;  // only the configuration x band sweep
+  const int quick = argc > 4 ? atoi(argv[4]) : 0;  // 1: configuration x band sweep + bright breakdown
   launch_synth(in, S, H, W, 12345, 0, 0, dist, 0);
   CK(hipDeviceSynchronize());
   float4 *coef, *mconst2;
@@ -200,7 +200,30 @@ static int run(int argc, char** argv) {
     fcfg(nm, C4(), T512(), L16k(), 2 * cus);
   }
   nb = kFusedBands;
-  if (quick) {
+  if (quick == 2 || quick) {
+    // where the wide configuration's time goes (bright data): the same launch
+    // without histogram (ABL 1), without the per-unit flush (ABL 8), and the
+    // four-site shape without histogram
+    auto fabl = [&](const char* nm2, auto spu_t, auto nt_t, auto lb_t, auto abl_t, int grid, int bands) {
+      constexpr int SPU_ = decltype(spu_t)::value, NT_ = decltype(nt_t)::value,
+                    LB_ = decltype(lb_t)::value, ABL_ = decltype(abl_t)::value;
+      time(nm2, [&] {
+        CK(hipMemsetAsync(fn, 0, 4, 0));
+        CK(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), 0));
+        hipLaunchKernelGGL((k_correct_hist<true, false, SPU_, ABL_, NT_, LB_>), dim3(grid), dim3(NT_), 0, 0,
+                           in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, bands, queues, nullptr,
+                           0ull, 0ull, 0ull, 0ull, SiteTab{});
+      });
+    };
+    using A0 = std::integral_constant<int, 0>;
+    using A1 = std::integral_constant<int, 1>;
+    using A8 = std::integral_constant<int, 8>;
+    fabl("wide (2,1024,32768) b8 ABL0", C2(), T1024(), L32k(), A0(), cus, 8);
+    fabl("wide (2,1024,32768) b8 ABL1 no hist", C2(), T1024(), L32k(), A1(), cus, 8);
+    fabl("wide (2,1024,32768) b8 ABL8 no flush", C2(), T1024(), L32k(), A8(), cus, 8);
+    fabl("four (4,1024,32768) b16 ABL1 no hist", C4(), T1024(), L32k(), A1(), cus, 16);
+    fabl("four (4,1024,32768) b8 ABL1 no hist", C4(), T1024(), L32k(), A1(), cus, 8);
+    fabl("narrow (4,512,16384) b16 ABL1 no hist", C4(), T512(), L16k(), A1(), 2 * cus, 16);
     printf("done\n");
     return 0;
   }
