@@ -171,9 +171,12 @@ def test_bright_fullsize(L):
     """bright 16-bit data (lognormal(8.5, 0.6), about a third
     of the pixels >= 4,096) at full size.  The Welford pass takes its wide
     log10 path for most pixel groups and counts them; the automatic fused
-    configuration then runs the one-site, 32,768-bin slice (kFusedWide).  The
-    same job with the narrow slices forced (global adds for every pixel
-    >= 4,096) must give identical results, and both match the oracle."""
+    configuration then runs kFusedWide: two sites per unit, 16,384 u32 bins
+    each (2, 1024, 32768).  The same job with the narrow slices forced (global
+    adds for every pixel >= 4,096) must give identical results, and both
+    match the oracle.  (64 sites: below the 96 the bright Welford pass needs,
+    so this covers the standard pass's rare log10 path; tests/test_gpu_blocked.py
+    runs 100 bright sites through the 16,384-entry bright pass.)"""
     import torch
 
     from tmlibrary_amd import hip
