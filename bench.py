@@ -831,6 +831,14 @@ def claim_stdout():
 def main():
     a = parse()
     out = claim_stdout()
+    if a.stream_host:
+        # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 on the
+        # box) round-robin; with the copy, compute and library streams of the
+        # host pipeline that put the next channel's H2D behind the current
+        # channel's kernels (profiles/r3/stream_host_hwq_r3t.jsonl: 2,988 sites/s
+        # with 4, 3,408 with 8).  The resident multi-channel job runs best with
+        # 4 (dist4_hwq_r3u.jsonl), so only this mode changes it, before HIP starts.
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
