@@ -390,7 +390,7 @@ class HostStreamJob(object):
                                          hip.ptr(lut), 1, flags, C.byref(h)))
             sp = C.c_void_p(self.comp[b].cuda_stream)
             hip.check(L.tmh_stats_set_stream(h, sp))
-            planes = [torch.empty(self.npx, dtype=torch.float64, device=dev) for _ in range(5)]
+            planes = [torch.empty(self.npx, dtype=torch.float64, device=dev) for _ in range(6)]
             torch.cuda.synchronize(dev)
             hip.check(L.tmh_corrector_create_device(C.c_void_p(planes[0].data_ptr()),
                                                     C.c_void_p(planes[1].data_ptr()), H, W, 1,
@@ -437,7 +437,7 @@ class HostStreamJob(object):
         b = c % 2
         h, corr, sp, planes, ops = self.handles[b]
         cs = self.comp[b]
-        mean, std, smean, sstd, ptmp = planes
+        mean, std, smean, sstd, ptmp, ptmp2 = planes
         buf = self.resident[b]
         ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
         if st["buf_free"][b] is not None:
@@ -465,8 +465,8 @@ class HostStreamJob(object):
             if self.dist is not None:
                 merge_welford(ops, self.dist, n_total=self.S_total)
             hip.check(L.tmh_stats_finalize_device(h, ptr(mean), ptr(std), sp))
-            hip.check(L.tmh_smooth_f64_device(ptr(mean), ptr(smean), ptr(ptmp), H, W, 5.0, sp))
-            hip.check(L.tmh_smooth_f64_device(ptr(std), ptr(sstd), ptr(ptmp), H, W, 5.0, sp))
+            hip.check(L.tmh_smooth2_f64_device(ptr(mean), ptr(std), ptr(smean), ptr(sstd),
+                                               ptr(ptmp), ptr(ptmp2), H, W, 5.0, sp))
             hip.check(L.tmh_corrector_update_device(corr, ptr(smean), ptr(sstd), sp))
         for j in range(nch):  # pass 2: correct + histogram -> out slots -> host
             n = min(CK, S - j * CK)
@@ -781,8 +781,8 @@ def single_gpu_same_workload(L, dev, H, W, CH, S_total, dist_id, steps=3, warmup
     hip.check(L.tmh_stats_create(H, W, 100000, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
                                  hip.ptr(lut), 1, 0, C.byref(h)))
     hip.check(L.tmh_stats_set_stream(h, sp))
-    mean, std, smean, sstd, tmp = [torch.empty(npx, dtype=torch.float64, device=dev)
-                                   for _ in range(5)]
+    mean, std, smean, sstd, tmp, tmp2 = [torch.empty(npx, dtype=torch.float64, device=dev)
+                                         for _ in range(6)]
     torch.cuda.synchronize(dev)
     hip.check(L.tmh_corrector_create_device(ptr(mean), ptr(std), H, W, 1, ZERO_LOG10, sp,
                                             C.byref(corr)))
@@ -791,8 +791,8 @@ def single_gpu_same_workload(L, dev, H, W, CH, S_total, dist_id, steps=3, warmup
         hip.check(L.tmh_stats_reset(h))
         hip.check(L.tmh_stats_update_welford_blocks_device(h, ptr(t_in[c]), shift, S_total, 1, sp))
         hip.check(L.tmh_stats_finalize_device(h, ptr(mean), ptr(std), sp))
-        hip.check(L.tmh_smooth_f64_device(ptr(mean), ptr(smean), ptr(tmp), H, W, 5.0, sp))
-        hip.check(L.tmh_smooth_f64_device(ptr(std), ptr(sstd), ptr(tmp), H, W, 5.0, sp))
+        hip.check(L.tmh_smooth2_f64_device(ptr(mean), ptr(std), ptr(smean), ptr(sstd), ptr(tmp),
+                                           ptr(tmp2), H, W, 5.0, sp))
         hip.check(L.tmh_corrector_update_device(corr, ptr(smean), ptr(sstd), sp))
         hip.check(L.tmh_correct_u16_hist_blocks_device(corr, h, ptr(t_in[c]), ptr(t_out), shift,
                                                        S_total, -1, -1, sp))
@@ -972,6 +972,7 @@ def main():
             self.smean = torch.empty_like(self.mean)
             self.sstd = torch.empty_like(self.mean)
             self.tmp = torch.empty_like(self.mean)
+            self.tmp2 = torch.empty_like(self.mean)
             self.h = C.c_void_p()
             hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
                                          hip.ptr(lut), 1, flags, C.byref(self.h)))
@@ -1001,10 +1002,9 @@ def main():
         def apply(self):
             p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
             hip.check(L.tmh_stats_finalize_device(self.h, p(self.mean), p(self.std), self.sp))
-            hip.check(L.tmh_smooth_f64_device(p(self.mean), p(self.smean), p(self.tmp), H, W, 5.0,
-                                              self.sp))
-            hip.check(L.tmh_smooth_f64_device(p(self.std), p(self.sstd), p(self.tmp), H, W, 5.0,
-                                              self.sp))
+            hip.check(L.tmh_smooth2_f64_device(p(self.mean), p(self.std), p(self.smean),
+                                               p(self.sstd), p(self.tmp), p(self.tmp2), H, W, 5.0,
+                                               self.sp))
             hip.check(L.tmh_corrector_update_device(self.corr, p(self.smean), p(self.sstd),
                                                     self.sp))
             if fused and B:

@@ -227,6 +227,12 @@ int tmh_stats_set_hist_device(tmh_stats* h, const uint64_t* dev_hist, void* stre
 int tmh_smooth_f64(const double* host_in, double* host_out, int height, int width, double sigma);
 int tmh_smooth_f64_device(const double* dev_in, double* dev_out, double* dev_tmp, int height,
                           int width, double sigma, void* stream);
+/* The same for two planes (a job's mean and std, image.py:1185-1186) in one
+ * launch per axis; bit-identical to two tmh_smooth_f64_device calls.
+ * dev_tmp0 / dev_tmp1: scratch planes of their own. */
+int tmh_smooth2_f64_device(const double* dev_in0, const double* dev_in1, double* dev_out0,
+                           double* dev_out1, double* dev_tmp0, double* dev_tmp1, int height,
+                           int width, double sigma, void* stream);
 
 /* ---- correction ------------------------------------------------------------
  * Replaces tmlib/image.py:599-631 ChannelImage._correct_illumination,

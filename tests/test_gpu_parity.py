@@ -235,6 +235,36 @@ def test_smooth_small_planes(L, shape):
                            atol=1e-13)
 
 
+@pytest.mark.parametrize("shape,sigma", [((2160, 2560), 5.0), ((37, 53), 5.0), ((96, 128), 2.0),
+                                         ((8, 700), 40.0)])
+def test_smooth2_equals_two_planes(L, shape, sigma):
+    """tmh_smooth2_f64_device (a job's mean and std in one launch per axis)
+    is bit-identical to two tmh_smooth_f64_device calls, for the radius-20
+    strip kernel, the generic axis-0 kernel and the wide (radius > 128)
+    axis-1 kernel."""
+    from tmlibrary_amd import hip
+    H, W = shape
+    rng = np.random.default_rng(H * 7 + W)
+    a = rng.random(shape) * 3.0 + 0.5
+    b = rng.random(shape) * 0.2 + 0.01
+    bufs = [Dev(L, H * W * 8) for _ in range(8)]
+    ia, ib, o1a, o1b, o2a, o2b, t0, t1 = bufs
+    ia.put(a)
+    ib.put(b)
+    hip.check(L.tmh_smooth_f64_device(ia.p, o1a.p, t0.p, H, W, sigma, None))
+    hip.check(L.tmh_smooth_f64_device(ib.p, o1b.p, t0.p, H, W, sigma, None))
+    hip.check(L.tmh_smooth2_f64_device(ia.p, ib.p, o2a.p, o2b.p, t0.p, t1.p, H, W, sigma, None))
+    L.tmh_synchronize(None)
+    ra, rb = o1a.get(np.float64, shape), o1b.get(np.float64, shape)
+    assert np.array_equal(o2a.get(np.float64, shape), ra)
+    assert np.array_equal(o2b.get(np.float64, shape), rb)
+    assert np.allclose(ra, orc.smooth_reflect(a, sigma), rtol=1e-10, atol=1e-13)
+    # scratch aliasing an input or output is refused
+    assert L.tmh_smooth2_f64_device(ia.p, ib.p, o2a.p, o2b.p, ia.p, t1.p, H, W, sigma, None) == -22
+    for d in bufs:
+        d.free()
+
+
 def test_corrector_cache_sees_in_place_writes(L):
     """the container's cached corrector is keyed on content.
     Building it marks the planes read-only, so an in-place write raises; a

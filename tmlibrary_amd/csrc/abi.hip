@@ -957,6 +957,27 @@ int tmh_smooth_f64_device(const double* dev_in, double* dev_out, double* dev_tmp
   });
 }
 
+int tmh_smooth2_f64_device(const double* dev_in0, const double* dev_in1, double* dev_out0,
+                           double* dev_out1, double* dev_tmp0, double* dev_tmp1, int height,
+                           int width, double sigma, void* stream) {
+  return guard([&] {
+    TMH_CHECK(dev_in0 && dev_in1 && dev_out0 && dev_out1 && dev_tmp0 && dev_tmp1 && height > 0 &&
+                  width > 0,
+              TMH_EINVAL, "bad arguments");
+    TMH_CHECK(sigma >= 0.125, TMH_EINVAL, "sigma must be >= 0.125");
+    const double* ins[2] = {dev_in0, dev_in1};
+    const double* outs[2] = {dev_out0, dev_out1};
+    for (const double* t : {(const double*)dev_tmp0, (const double*)dev_tmp1})
+      for (int k = 0; k < 2; ++k)
+        TMH_CHECK(t != ins[k] && t != outs[k], TMH_EINVAL, "dev_tmp0/1 must be buffers of their own");
+    TMH_CHECK(dev_tmp0 != dev_tmp1, TMH_EINVAL, "dev_tmp0 and dev_tmp1 must differ");
+    TMH_CHECK(dev_out0 != dev_out1, TMH_EINVAL, "dev_out0 and dev_out1 must differ");
+    const auto t = taps_for(sigma);
+    launch_smooth2(dev_in0, dev_in1, dev_out0, dev_out1, dev_tmp0, dev_tmp1, height, width,
+                   t.first, t.second, (hipStream_t)stream);
+  });
+}
+
 int tmh_smooth_f64(const double* host_in, double* host_out, int height, int width, double sigma) {
   return guard([&] {
     TMH_CHECK(host_in && host_out && height > 0 && width > 0, TMH_EINVAL, "bad arguments");

@@ -30,10 +30,19 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
   return (i < n) ? i : p - 1 - i;
 }
 
+// Planes of one launch (gridDim.z = 1 or 2): the mean and std planes of a
+// job are smoothed by the same two launches, half the launches of plane by
+// plane (each ~0.035 ms at 2160x2560: launch and tail dominated).
+struct SmPlanes {
+  const double* in[2];
+  double* out[2];
+};
+
 // axis 0 (rows of the plane vary): out[y][x] = sum_j w[j] in[refl(y+j-r)][x]
-__global__ __launch_bounds__(256) void k_smooth_axis0(const double* __restrict__ in,
-                                                      double* __restrict__ out, int H, int W,
+__global__ __launch_bounds__(256) void k_smooth_axis0(const SmPlanes pl, int H, int W,
                                                       const double* __restrict__ w, int r) {
+  const double* __restrict__ in = pl.in[blockIdx.z];
+  double* __restrict__ out = pl.out[blockIdx.z];
   const int x = blockIdx.x * 256 + threadIdx.x;
   const int y = blockIdx.y;
   if (x >= W) return;
@@ -47,9 +56,10 @@ __global__ __launch_bounds__(256) void k_smooth_axis0(const double* __restrict__
 // same order as k_smooth_axis0 -> bit-identical results), instead of 2R + 1
 // loads per output.
 template <int T, int R>
-__global__ __launch_bounds__(256) void k_smooth_axis0_strip(const double* __restrict__ in,
-                                                            double* __restrict__ out, int H, int W,
+__global__ __launch_bounds__(256) void k_smooth_axis0_strip(const SmPlanes pl, int H, int W,
                                                             const double* __restrict__ w) {
+  const double* __restrict__ in = pl.in[blockIdx.z];
+  double* __restrict__ out = pl.out[blockIdx.z];
   const int x = blockIdx.x * 256 + threadIdx.x;
   const int y0 = blockIdx.y * T;
   if (x >= W) return;
@@ -73,10 +83,11 @@ __global__ __launch_bounds__(256) void k_smooth_axis0_strip(const double* __rest
 // axis 1 (along a row), row segment + halo staged in LDS
 constexpr int kSmTile = 256;
 constexpr int kSmMaxR = 128;
-__global__ __launch_bounds__(256) void k_smooth_axis1(const double* __restrict__ in,
-                                                      double* __restrict__ out, int H, int W,
+__global__ __launch_bounds__(256) void k_smooth_axis1(const SmPlanes pl, int H, int W,
                                                       const double* __restrict__ w, int r) {
   __shared__ double tile[kSmTile + 2 * kSmMaxR];
+  const double* __restrict__ in = pl.in[blockIdx.z];
+  double* __restrict__ out = pl.out[blockIdx.z];
   const int x0 = blockIdx.x * kSmTile;
   const int y = blockIdx.y;
   const double* row = in + (int64_t)y * W;
@@ -89,9 +100,10 @@ __global__ __launch_bounds__(256) void k_smooth_axis1(const double* __restrict__
   out[(int64_t)y * W + x] = acc;
 }
 
-__global__ __launch_bounds__(256) void k_smooth_axis1_wide(const double* __restrict__ in,
-                                                           double* __restrict__ out, int H, int W,
+__global__ __launch_bounds__(256) void k_smooth_axis1_wide(const SmPlanes pl, int H, int W,
                                                            const double* __restrict__ w, int r) {
+  const double* __restrict__ in = pl.in[blockIdx.z];
+  double* __restrict__ out = pl.out[blockIdx.z];
   const int x = blockIdx.x * 256 + threadIdx.x;
   const int y = blockIdx.y;
   if (x >= W) return;
@@ -101,23 +113,41 @@ __global__ __launch_bounds__(256) void k_smooth_axis1_wide(const double* __restr
   out[(int64_t)y * W + x] = acc;
 }
 
-void launch_smooth(const double* in, double* out, double* tmp, int H, int W, const double* d_w,
-                   int radius, hipStream_t s) {
+// np planes (1 or 2): in[k] -> tmp[k] (axis 0) -> out[k] (axis 1)
+static void launch_smooth_planes(const double* const* in, double* const* out, double* const* tmp,
+                                 int np, int H, int W, const double* d_w, int radius,
+                                 hipStream_t s) {
   ProfScope prof("smooth", s);
-  const dim3 grid((unsigned)cdiv(W, 256), (unsigned)H);
+  SmPlanes a0{{in[0], np > 1 ? in[1] : nullptr}, {tmp[0], np > 1 ? tmp[1] : nullptr}};
+  SmPlanes a1{{tmp[0], np > 1 ? tmp[1] : nullptr}, {out[0], np > 1 ? out[1] : nullptr}};
+  const dim3 grid((unsigned)cdiv(W, 256), (unsigned)H, (unsigned)np);
   if (radius == 20) {  // sigma = 5, the reference's default (image.py:1172)
-    // 16 rows per thread: 1,350 workgroups at 2160x2560 (8 / 32 measured slower)
-    const dim3 g2((unsigned)cdiv(W, 256), (unsigned)cdiv(H, 16));
-    hipLaunchKernelGGL((k_smooth_axis0_strip<16, 20>), g2, dim3(256), 0, s, in, tmp, H, W, d_w);
+    // 16 rows per thread: 1,350 workgroups per plane at 2160x2560 (8 / 32 measured slower)
+    const dim3 g2((unsigned)cdiv(W, 256), (unsigned)cdiv(H, 16), (unsigned)np);
+    hipLaunchKernelGGL((k_smooth_axis0_strip<16, 20>), g2, dim3(256), 0, s, a0, H, W, d_w);
   } else {
-    hipLaunchKernelGGL(k_smooth_axis0, grid, dim3(256), 0, s, in, tmp, H, W, d_w, radius);
+    hipLaunchKernelGGL(k_smooth_axis0, grid, dim3(256), 0, s, a0, H, W, d_w, radius);
   }
   if (radius <= kSmMaxR)
-    hipLaunchKernelGGL(k_smooth_axis1, dim3((unsigned)cdiv(W, kSmTile), (unsigned)H), dim3(256), 0,
-                       s, tmp, out, H, W, d_w, radius);
+    hipLaunchKernelGGL(k_smooth_axis1, dim3((unsigned)cdiv(W, kSmTile), (unsigned)H, (unsigned)np),
+                       dim3(256), 0, s, a1, H, W, d_w, radius);
   else
-    hipLaunchKernelGGL(k_smooth_axis1_wide, grid, dim3(256), 0, s, tmp, out, H, W, d_w, radius);
+    hipLaunchKernelGGL(k_smooth_axis1_wide, grid, dim3(256), 0, s, a1, H, W, d_w, radius);
   TMH_HIP(hipGetLastError());
+}
+
+void launch_smooth(const double* in, double* out, double* tmp, int H, int W, const double* d_w,
+                   int radius, hipStream_t s) {
+  launch_smooth_planes(&in, &out, &tmp, 1, H, W, d_w, radius, s);
+}
+
+void launch_smooth2(const double* in0, const double* in1, double* out0, double* out1,
+                    double* tmp0, double* tmp1, int H, int W, const double* d_w, int radius,
+                    hipStream_t s) {
+  const double* in[2] = {in0, in1};
+  double* out[2] = {out0, out1};
+  double* tmp[2] = {tmp0, tmp1};
+  launch_smooth_planes(in, out, tmp, 2, H, W, d_w, radius, s);
 }
 
 // ---------------------------------------------------------------------------

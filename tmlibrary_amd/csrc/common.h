@@ -230,6 +230,9 @@ void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s);
 
 void launch_smooth(const double* in, double* out, double* tmp, int H, int W, const double* d_w,
                    int radius, hipStream_t s);
+void launch_smooth2(const double* in0, const double* in1, double* out0, double* out1,
+                    double* tmp0, double* tmp1, int H, int W, const double* d_w, int radius,
+                    hipStream_t s);
 // out[0] = sum(x0), out[1] = sum(x1), out[2] = smallest positive finite x0
 // (+inf if none); partial holds 3 * n_partial
 void launch_reduce_sum2(const double* x0, const double* x1, int64_t n, double* partial,

@@ -74,6 +74,7 @@ SIGNATURES = {
     "tmh_stats_get_pct_sum_device": (_I, [_P, _P, _P]),
     "tmh_smooth_f64": (_I, [_P, _P, _I, _I, _D]),
     "tmh_smooth_f64_device": (_I, [_P, _P, _P, _I, _I, _D, _P]),
+    "tmh_smooth2_f64_device": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _D, _P]),
     "tmh_corrector_create": (_I, [_P, _P, _I, _I, _I, _D, C.POINTER(_P)]),
     "tmh_corrector_create_device": (_I, [_P, _P, _I, _I, _I, _D, _P, C.POINTER(_P)]),
     "tmh_corrector_destroy": (None, [_P]),
