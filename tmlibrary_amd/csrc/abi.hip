@@ -1560,7 +1560,7 @@ int tmh_correct_chain_u8_device(tmh_corrector* c, const uint16_t* dev_in, uint8_
     if (!c->lut8.n) c->lut8.alloc(65536);
     launch_chain_u8(dev_in, dev_out, c->H, c->W, n_sites, c->coef_lin.p, c->mconst2.p, fl,
                     c->coef64.p, c->rc.p, c->log_transform, c->win.p, clip_lo, clip_hi,
-                    c->lut8.p, s);
+                    c->lut8.p, s, c->zero_log10);
     TMH_HIP(hipStreamSynchronize(s));  // the window buffer is reused by the next call
   });
 }

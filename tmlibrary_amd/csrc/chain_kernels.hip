@@ -311,6 +311,189 @@ __global__ __launch_bounds__(NT) void k_chain_u8(const uint16_t* __restrict__ in
   }
 }
 
+// The production chain pass: k_chain_u8's 16-bit-table form with its VALU
+// trimmed (the pass is VALU-bound: ~24 issue slots per pixel, two of them
+// quarter-rate transcendentals).
+//  * no queue of site loads (below);
+//  * no min/max before the cast: every |o| >= T (T < 2^18 by construction,
+//    k_refine_const) flags its group for the f64 refinement, which rewrites
+//    all 8 pixels, so only |o| < T -- where v_cvt_i32_f32 truncates exactly as
+//    the x86 cast does -- reaches the stored bytes unrefined; NaN converts to 0
+//    on both;
+//  * ZADD: a zero pixel's floor as x + zf instead of max(x, zf) -- two pixels
+//    per v_pk_add_f32; exact for zf < 2^-25 (x >= 1 plus zf rounds to x);
+//  * the table bytes packed with v_perm (3 per 4 bytes) instead of shifts,
+//    ors and a masking bitop;
+//  * the align window's byte mask only for threads whose 8 pixels are not all
+//    inside it (a divergent branch: whole waves skip it).
+template <bool LOG, bool ZADD, int NT, bool PF = false>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2 * NT / 256))) void k_chain_u8t(const uint16_t* __restrict__ in,
+                                                   uint8_t* __restrict__ out, int H, int W,
+                                                   int64_t n_sites, int64_t per,
+                                                   const float2* __restrict__ coef_lin,
+                                                   const float4* __restrict__ mconst2, FixList fl,
+                                                   const tmh_window* __restrict__ win,
+                                                   const uint8_t* __restrict__ lut8) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t slut[];
+  for (int i = threadIdx.x; i < 65536 / 16; i += NT)
+    reinterpret_cast<uint4*>(slut)[i] = reinterpret_cast<const uint4*>(lut8)[i];
+  __syncthreads();
+  const int64_t npx = (int64_t)H * W;
+  const int64_t ngroups = npx >> 3;
+  const int64_t tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t g = tile * NT + threadIdx.x;
+  const bool live = g < ngroups;
+  const int lane = threadIdx.x & 63;
+  const bool top_lane = threadIdx.x == NT - 1 || g + 1 >= ngroups;
+  __shared__ uint64_t edge[NT / 64];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[NT * 8 + 256];
+  const int64_t p0 = (live ? g : 0) * 8;
+  const int r = (int)(p0 / W), c0 = (int)(p0 % W);
+  const float4 m = mconst2[0];
+  const f32x2c_t M = {m.x, m.x};
+  const f32x2c_t Z = {m.z, m.z};
+  f32x2c_t mu[4], a[4];
+  {
+    const float4* cf = reinterpret_cast<const float4*>(coef_lin + p0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 v0 = live ? cf[k] : make_float4(0.f, 1.f, 0.f, 1.f);
+      mu[k] = (f32x2c_t){v0.x, v0.z};
+      a[k] = (f32x2c_t){v0.y, v0.w};
+    }
+  }
+  const int64_t s0 = (int64_t)blockIdx.y * per;
+  const int64_t s1 = s0 + per < n_sites ? s0 + per : n_sites;
+  const uint4* src = reinterpret_cast<const uint4*>(in) + (live ? g : 0);
+
+  auto site = [&](const uint4 cur, const int64_t s) {
+    const tmh_window w = win[s];  // uniform: scalar loads
+    const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+    f32x2c_t t[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      t[k].x = (float)(wd[k] & 0xFFFFu);
+      t[k].y = (float)(wd[k] >> 16);
+    }
+    if (LOG) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (ZADD) {
+          t[k] += Z;
+        } else {
+          t[k].x = __builtin_fmaxf(t[k].x, m.z);
+          t[k].y = __builtin_fmaxf(t[k].y, m.z);
+        }
+        t[k].x = __builtin_amdgcn_logf(t[k].x);
+        t[k].y = __builtin_amdgcn_logf(t[k].y);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] = __builtin_elementwise_fma(t[k] - mu[k], a[k], M);
+    float mx = 0.0f;  // largest |result| of the 8 pixels (v_max3 with |.| modifiers)
+    uint32_t o[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float x = LOG ? __builtin_amdgcn_exp2f(t[k][h]) : t[k][h];
+        mx = __builtin_fmaxf(mx, __builtin_fabsf(x));
+        o[2 * k + h] = slut[(uint32_t)(int32_t)x & 0xFFFFu];
+      }
+    }
+    // bytes (o0, o1, o2, o3): v_perm pairs, then the pairs' low halves -- in
+    // the loads' basic block, where the compiler knows the bytes are
+    // zero-extended (sunk past the branch below it masks each byte first)
+    uint32_t lo4 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(o[3], o[2], 0x0c0c0400u),
+                                         __builtin_amdgcn_perm(o[1], o[0], 0x0c0c0400u), 0x05040100u);
+    uint32_t hi4 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(o[7], o[6], 0x0c0c0400u),
+                                         __builtin_amdgcn_perm(o[5], o[4], 0x0c0c0400u), 0x05040100u);
+    asm volatile("" : "+v"(lo4), "+v"(hi4));  // keeps the packing here (no code is emitted)
+    if (mx >= m.w && live) fix_push8(fl, 0xFFu, s, p0);
+    // pixels outside the source window write the padding value (0 after
+    // clip/scale); only threads with a pixel outside build the byte mask
+    const int cs = c0 - w.src_c0;
+    const bool inside = w.cols >= 8 && (unsigned)(r - w.src_r0) < (unsigned)w.rows &&
+                        (unsigned)cs <= (unsigned)(w.cols - 8);
+    if (!inside) {
+      int jlo = -cs < 0 ? 0 : (-cs > 8 ? 8 : -cs);
+      int jhi = w.cols - cs < 0 ? 0 : (w.cols - cs > 8 ? 8 : w.cols - cs);
+      if ((unsigned)(r - w.src_r0) >= (unsigned)w.rows) jhi = 0;
+      const uint64_t keep = jhi > jlo ? ((~0ull >> (8 * (8 - (jhi - jlo)))) << (8 * jlo)) : 0ull;
+      lo4 &= (uint32_t)keep;
+      hi4 &= (uint32_t)(keep >> 32);
+    }
+    const uint64_t v8 = ((uint64_t)hi4 << 32) | lo4;
+    // byte offsets inside one site fit in 32 bits (the launch checks npx < 2^30)
+    const int n32 = (int)npx;
+    const int off = (w.dst_r0 - w.src_r0) * W + (w.dst_c0 - w.src_c0);  // uniform
+    const int D = (int)p0 + off;  // destination of byte 0
+    const int rr = off & 7;       // uniform
+    uint8_t* o8 = out + s * npx;
+    if ((off & 127) == 0) {  // line-aligned destination: direct stores
+      if (live && (unsigned)D < (unsigned)n32) *reinterpret_cast<uint64_t*>(o8 + D) = v8;
+      return;
+    }
+    // as k_chain_u8: the workgroup's output bytes staged in LDS and stored as
+    // whole 16-B chunks of 128-B lines (runs first made 8-byte aligned with the
+    // upper neighbour's bytes: wave shuffle, LDS slot across waves)
+    const int wv = threadIdx.x >> 6;
+    if (lane == 0) edge[wv] = v8;
+    const uint32_t nlo = (uint32_t)__shfl_down((int)lo4, 1, 64);
+    const uint32_t nhi = (uint32_t)__shfl_down((int)hi4, 1, 64);
+    __syncthreads();  // (1) edge slots written; the previous site's stage is drained
+    uint64_t n8 = ((uint64_t)nhi << 32) | nlo;
+    if (lane == 63 && wv < NT / 64 - 1) n8 = edge[wv + 1];
+    const int o0 = (int)(tile * NT * 8) + off;  // uniform: destination of thread 0's byte 0
+    const int L0 = o0 & ~127;                   // its line (floor, also for o0 < 0)
+    if (!live) {
+      // past the last group: nothing to stage
+    } else if (rr == 0) {
+      *reinterpret_cast<uint64_t*>(stage + (D - L0)) = v8;
+    } else {
+      const int A = D - rr + 8;  // aligned word holding our bytes [8 - rr, 8)
+      if (!top_lane) {
+        *reinterpret_cast<uint64_t*>(stage + (A - L0)) = (v8 >> (8 * (8 - rr))) | (n8 << (8 * rr));
+      } else {
+        for (int b = 8 - rr; b < 8; ++b) stage[D + b - L0] = (uint8_t)(v8 >> (8 * b));
+      }
+      if (threadIdx.x == 0)
+        for (int b = 0; b < 8 - rr; ++b) stage[D + b - L0] = (uint8_t)(v8 >> (8 * b));
+    }
+    __syncthreads();  // (2) stage complete
+    // valid destination bytes of this workgroup: [v0, v1) (uniform)
+    const int wg_bytes = (int)((ngroups - tile * NT < NT ? ngroups - tile * NT : NT) * 8);
+    const int v0 = o0 > 0 ? o0 : 0;
+    const int v1 = o0 + wg_bytes < n32 ? o0 + wg_bytes : n32;
+    const int c = L0 + 16 * (int)threadIdx.x;  // this thread's 16-B chunk
+    if (c + 16 <= v1 && c >= v0) {
+      *reinterpret_cast<uint4*>(o8 + c) = *reinterpret_cast<const uint4*>(stage + (c - L0));
+    } else if (c < v1 && c + 16 > v0) {
+      for (int b = 0; b < 16; ++b)
+        if (c + b >= v0 && c + b < v1) o8[c + b] = stage[c + b - L0];
+    }
+  };
+
+  // one site's load, then its processing: k_chain_u8's queue of kChainDepth
+  // loads compiled to a full wait for the load just issued (a conditional load
+  // in the loop), i.e. this same order, plus 16 register moves per site; the
+  // 32 waves of a CU hide the latency.  (A pipeline that really keeps loads in
+  // flight across sites ran slower for this shape: 19.4 vs 14.5 ms,
+  // profiles/r3/mb_chain_pipeline_r3n.txt.)
+  if (PF) {  // the next site's load issued before this site's processing
+    if (s0 >= s1) return;
+    uint4 nxt = ld_nt16(src + s0 * ngroups);
+    for (int64_t s = s0; s < s1; ++s) {
+      const uint4 cur = nxt;
+      nxt = ld_nt16(src + (s + 1 < s1 ? s + 1 : s) * ngroups);  // unconditional
+      site(cur, s);
+    }
+  } else {
+    for (int64_t s = s0; s < s1; ++s)
+      site(live ? ld_nt16(src + s * ngroups) : make_uint4(0, 0, 0, 0), s);
+  }
+}
+
 // The 16-bit clip + scale table of k_chain_u8<LUT = 2>: entry v = scale8(clip(v)).
 __global__ void k_chain_lut8(uint8_t* __restrict__ lut8, int lo, int hi, int T, double step) {
   const int v = (int)blockIdx.x * 256 + threadIdx.x;
@@ -426,14 +609,15 @@ void launch_map_u8(const uint16_t* in, uint8_t* out, int64_t n, int lo, int hi, 
 void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_sites,
                      const float2* coef_lin, const float4* mconst2, const FixList& fl,
                      const double2* coef64, const RefineConst* rc, int log_transform,
-                     const tmh_window* d_win, int lo, int hi, uint8_t* lut8, hipStream_t s) {
+                     const tmh_window* d_win, int lo, int hi, uint8_t* lut8, hipStream_t s,
+                     double zero_log10) {
   if (n_sites <= 0) return;
   ProfScope prof("chain", s);
   const int64_t npx = (int64_t)H * W;
   const double step = scale_step(lo, hi);
   const int T = hi - lo > 1 ? hi - lo - 1 : 1;
   const bool vec = (W & 7) == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
-                   (reinterpret_cast<uintptr_t>(out) & 7) == 0;
+                   (reinterpret_cast<uintptr_t>(out) & 7) == 0 && npx < ((int64_t)1 << 30);
   if (vec) {
     // site parts even out the dispatch rounds (each thread streams its part)
     const int64_t parts = n_sites >= 64 ? 8 : 1;
@@ -452,7 +636,18 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
       // 512 21.6, 1,024 14.6 against 15.0 for the clipped-range table,
       // profiles/r2/mb_chain_lut64_r2lt.txt)
       hipLaunchKernelGGL(k_chain_lut8, dim3(256), dim3(256), 0, s, lut8, lo, hi, T, step);
-      if (log_transform) TMH_CHAIN(true, 2, 1024, 65536, lut8); else TMH_CHAIN(false, 2, 1024, 65536, lut8);
+      // 16 site parts: 3,456 sites of 2160x2560 ran 12.49 ms against 12.77
+      // with 8 (tools/mb/mb_chain.hip)
+      const int64_t tparts = n_sites >= 128 ? 16 : parts, tper = cdiv(n_sites, tparts);
+      const dim3 grid((unsigned)cdiv(npx >> 3, 1024), (unsigned)cdiv(n_sites, tper));
+#define TMH_CHAIN_T(L_, Z_)                                                                      \
+  hipLaunchKernelGGL((k_chain_u8t<L_, Z_, 1024, true>), grid, dim3(1024), 65536, s, in, out, H, \
+                     W, n_sites, tper, coef_lin, mconst2, fl, d_win, lut8)
+      // zf = 10**zero_log10 below 2^-25 (~2.98e-8): the floor as an add is exact
+      if (!log_transform) TMH_CHAIN_T(false, false);
+      else if (zero_log10 <= -8.0) TMH_CHAIN_T(true, true);
+      else TMH_CHAIN_T(true, false);
+#undef TMH_CHAIN_T
     } else if (log_transform) {
       if (lut) TMH_CHAIN(true, 1, 256, shm, nullptr); else TMH_CHAIN(true, 0, 256, shm, nullptr);
     } else {

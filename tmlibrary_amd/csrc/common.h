@@ -296,7 +296,8 @@ void launch_map_u8(const uint16_t* in, uint8_t* out, int64_t n, int lo, int hi, 
 void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_sites,
                      const float2* coef_lin, const float4* mconst2, const FixList& fl,
                      const double2* coef64, const RefineConst* rc, int log_transform,
-                     const tmh_window* d_win, int lo, int hi, uint8_t* lut8, hipStream_t s);
+                     const tmh_window* d_win, int lo, int hi, uint8_t* lut8, hipStream_t s,
+                     double zero_log10 = -10.0);
 void launch_clip_u16(const uint16_t* in, uint16_t* out, int64_t n, int lo, int hi, hipStream_t s);
 void launch_synth(uint16_t* out, int64_t n_sites, int H, int W, uint64_t seed, int channel,
                   int64_t first_site, int dist, hipStream_t s);

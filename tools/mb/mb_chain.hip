@@ -3,6 +3,8 @@
 // bench.py's extra, with a device checksum of the uint8 output.  (Round 2
 // measured a variant staging SB = 2 / 4 sites per barrier pair: 17.65 / 16.74
 // ms vs 15.36 for one site, identical checksums: profiles/r2/mb_chain_r2zf.txt.)
+// Round 3: k_chain_u8t (the production form, VALU trimmed) against
+// k_chain_u8's 64 KB-table form, same checksum expected.
 // Usage: mb_chain [n_sites=3456] [reps=3]
 #include <hip/hip_runtime.h>
 
@@ -121,8 +123,46 @@ static int run(int argc, char** argv) {
                          clin, mc2, fl, dw, lo, hi, T, step, lut8);
     });
   };
+  auto trimmed = [&](const char* nm, auto z_tag, auto pf_tag, int64_t prt) {
+    constexpr bool Z = decltype(z_tag)::value, PF = decltype(pf_tag)::value;
+    const int64_t pp = (S + prt - 1) / prt;
+    const dim3 g((unsigned)((npx / 8 + 1023) / 1024), (unsigned)((S + pp - 1) / pp));
+    time(nm, [&] {
+      CK(hipMemsetAsync(fn, 0, 4, 0));
+      hipLaunchKernelGGL((k_chain_u8t<true, Z, 1024, PF>), g, dim3(1024), 65536, 0, in, out, H, W,
+                         S, pp, clin, mc2, fl, dw, lut8);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
   for (int r = 0; r < 2; ++r) {
-    time("chain (production kernel)", [&] {
+    full("chain k_chain_u8 64 KB, NT 1024", std::integral_constant<int, 1024>());
+    trimmed("chain k_chain_u8t (zf add)", T_(), F_(), 8);
+    trimmed("chain k_chain_u8t (zf max)", F_(), F_(), 8);
+    trimmed("chain k_chain_u8t prefetch", T_(), T_(), 8);
+    trimmed("chain k_chain_u8t 6 parts", T_(), F_(), 6);
+    trimmed("chain k_chain_u8t 12 parts", T_(), F_(), 12);
+    trimmed("chain k_chain_u8t 16 parts", T_(), F_(), 16);
+    trimmed("chain k_chain_u8t pf 16 parts", T_(), T_(), 16);
+    trimmed("chain k_chain_u8t pf 24 parts", T_(), T_(), 24);
+    trimmed("chain k_chain_u8t pf 32 parts", T_(), T_(), 32);
+  }
+  {  // ablation: every site unshifted (line-aligned destination: no LDS staging, no barriers)
+    std::vector<tmh_window> w0(S);
+    for (int64_t i = 0; i < S; ++i) w0[i] = tmh_window{0, 0, 0, 0, H, W};
+    CK(hipMemcpy(dw, w0.data(), S * sizeof(tmh_window), hipMemcpyHostToDevice));
+    trimmed("ABLATION unshifted k_chain_u8t pf 16", T_(), T_(), 16);
+    full("ABLATION unshifted k_chain_u8 1024", std::integral_constant<int, 1024>());
+    std::vector<tmh_window> w(S);
+    for (int64_t i = 0; i < S; ++i) {
+      const int dy = (int)(i % 7) - 3, dx = (int)(i % 9) - 4;
+      w[i].src_r0 = 3 - dy; w[i].src_c0 = 4 - dx; w[i].dst_r0 = 3; w[i].dst_c0 = 4;
+      w[i].rows = H - 6; w[i].cols = W - 8;
+    }
+    CK(hipMemcpy(dw, w.data(), S * sizeof(tmh_window), hipMemcpyHostToDevice));
+  }
+  for (int r = 0; r < 1; ++r) {
+    time("chain (clipped-range table)", [&] {
       CK(hipMemsetAsync(fn, 0, 4, 0));
       hipLaunchKernelGGL((k_chain_u8<true, 1>), grid, dim3(256), shm, 0, in, out, H, W, S, per,
                          clin, mc2, fl, dw, lo, hi, T, step, nullptr);
