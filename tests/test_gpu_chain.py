@@ -158,6 +158,59 @@ def test_chain_device_random_windows(L, shape, bounds):
         assert d.max() <= 1, i
 
 
+@pytest.mark.parametrize("bounds", [(0, 65535), (100, 3000)])
+def test_chain_overflow_wrap_and_beyond_int32(L, bounds):
+    """Pixels with a tiny smoothed std (a = mean(std)/std ~ 1,000) whose
+    corrected values land below 65,536, wrap modulo 65,536 (x86 cast of values
+    in [65,536, 2^31)), pass 2^31 (the x86 cast gives INT_MIN: low half 0) or
+    overflow to inf: k_chain_u8t casts without clamping and relies on every
+    |value| >= T (T < 2^18) being refined in f64 -- checked here against the
+    oracle's x86 cast (oracle/corilla_oracle.py cast_float_to_uint_x86)."""
+    import ctypes as C
+    from tmlibrary_amd import hip
+    from tmlibrary_amd.image import Corrector, align_window
+    H, W = 64, 320
+    rng = np.random.default_rng(5)
+    mu = np.full((H, W), 2.5) + 0.01 * rng.random((H, W))
+    sd = np.full((H, W), 0.1)
+    sd[:, 96:160] = 1e-4  # a ~ 1,000 in these columns
+    sd[:, 200:208] = 1e-6  # a ~ 1e5: 10**t overflows to inf
+    # pixels around 10**mu: log10 offsets -0.02 .. +0.02 -> exponents far below
+    # and far above the uint16 range
+    off = rng.uniform(-0.02, 0.02, (4, H, W))
+    sites = np.clip(np.round(10.0 ** (mu + off)), 0, 65535).astype(np.uint16)
+    sites[1, :, :8] = 0
+    sites[2, 5, :] = 65535
+    shifts = [(0, 0), (2, -3), (-1, 5), (0, 8)]
+    res = (4, 4, 8, 8)
+    wins = np.stack([align_window((H, W), y, x, *res, crop=False)[0] for y, x in shifts])
+    lo, hi = bounds
+    corr = Corrector(mu, sd)
+    d_in, d_out = C.c_void_p(), C.c_void_p()
+    assert L.tmh_malloc_device(C.byref(d_in), sites.nbytes) == 0
+    assert L.tmh_malloc_device(C.byref(d_out), sites.size) == 0
+    assert L.tmh_memcpy(d_in, sites.ctypes.data, sites.nbytes, 0, None) == 0
+    hip.check(L.tmh_correct_chain_u8_device(corr._h, d_in, d_out, len(sites), hip.ptr(wins), lo,
+                                            hi, None))
+    got = np.empty(sites.shape, np.uint8)
+    assert L.tmh_memcpy(got.ctypes.data, d_out, got.nbytes, 1, None) == 0
+    L.tmh_free_device(d_in)
+    L.tmh_free_device(d_out)
+    corr.close()
+    # the case mix this test is about, from the oracle's own f64 values
+    a = sd.mean() / sd
+    t = (np.log10(np.maximum(sites.astype(np.float64), 1e-10)) - mu) * a + np.mean(mu)
+    with np.errstate(over="ignore"):
+        v = 10.0 ** t
+    assert (v >= 65536).any() and (v >= 2.0 ** 31).any() and np.isinf(v).any()
+    assert ((v > 1) & (v < 65536)).any()
+    for i, ((y, x), s) in enumerate(zip(shifts, sites)):
+        want = orc.illuminati_chain(s, mu, sd, (y, x), res, lo, hi)
+        d = np.abs(got[i].astype(np.int32) - want.astype(np.int32))
+        assert d.max() <= 1, (i, int(d.max()))
+        assert (d == 0).mean() > 0.99
+
+
 def test_chain_rejects_bad_windows(L):
     from tmlibrary_amd.image import Corrector, align_window
     g, wins = _chain_inputs()

@@ -315,18 +315,23 @@ __global__ __launch_bounds__(NT) void k_chain_u8(const uint16_t* __restrict__ in
 // trimmed (the pass is VALU-bound: ~24 issue slots per pixel, two of them
 // quarter-rate transcendentals).
 //  * no queue of site loads (below);
-//  * no min/max before the cast: every |o| >= T (T < 2^18 by construction,
-//    k_refine_const) flags its group for the f64 refinement, which rewrites
-//    all 8 pixels, so only |o| < T -- where v_cvt_i32_f32 truncates exactly as
-//    the x86 cast does -- reaches the stored bytes unrefined; NaN converts to 0
-//    on both;
+//  * a group flagged when its max |o| passes the f32 error bound of its
+//    largest a, |o| (K1 a_max8 + K2) >= 1 (the fused pass's per-pixel rule,
+//    fcorrect8, with the group's largest a), and k_fix_chain refines only the
+//    pixels beyond their own bound (the launch-wide T = 1 / (K1 a_max + K2)
+//    with whole groups refined ran 0.30 ms of f64 fixups per 3,456 bench
+//    sites);
+//  * no min/max before the cast: every |o| >= 1 / K2 (< 2^18) is flagged, and
+//    the f64 refinement rewrites all 8 pixels of a flagged group, so only
+//    values where v_cvt_i32_f32 truncates exactly as the x86 cast does reach
+//    the stored bytes unrefined; NaN converts to 0 on both;
 //  * ZADD: a zero pixel's floor as x + zf instead of max(x, zf) -- two pixels
 //    per v_pk_add_f32; exact for zf < 2^-25 (x >= 1 plus zf rounds to x);
 //  * the table bytes packed with v_perm (3 per 4 bytes) instead of shifts,
 //    ors and a masking bitop;
 //  * the align window's byte mask only for threads whose 8 pixels are not all
 //    inside it (a divergent branch: whole waves skip it).
-template <bool LOG, bool ZADD, int NT, bool PF = false>
+template <bool LOG, bool ZADD, int NT, bool PF = false, bool GB = true>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2 * NT / 256))) void k_chain_u8t(const uint16_t* __restrict__ in,
                                                    uint8_t* __restrict__ out, int H, int W,
                                                    int64_t n_sites, int64_t per,
@@ -353,14 +358,22 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2 * NT / 256
   const f32x2c_t M = {m.x, m.x};
   const f32x2c_t Z = {m.z, m.z};
   f32x2c_t mu[4], a[4];
+  float thr;  // this thread's flag threshold on max |o| (below)
   {
     const float4* cf = reinterpret_cast<const float4*>(coef_lin + p0);
+    float am = 0.0f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float4 v0 = live ? cf[k] : make_float4(0.f, 1.f, 0.f, 1.f);
       mu[k] = (f32x2c_t){v0.x, v0.z};
       a[k] = (f32x2c_t){v0.y, v0.w};
+      am = __builtin_fmaxf(am, __builtin_fmaxf(__builtin_fabsf(v0.y), __builtin_fabsf(v0.w)));
     }
+    // the fused pass's per-pixel bound |o| (K1 a + K2) >= 0.998 (fcorrect8),
+    // taken with the largest a of the thread's 8 pixels: max |o| >= thr flags
+    // the group (a superset of the pixels the per-pixel bound flags)
+    constexpr float K1 = (float)(kRefineK1 * 1.002), K2 = (float)(kRefineK2 * 1.002);
+    thr = 0.998f / __builtin_fmaf(am, K1, K2);
   }
   const int64_t s0 = (int64_t)blockIdx.y * per;
   const int64_t s1 = s0 + per < n_sites ? s0 + per : n_sites;
@@ -409,7 +422,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2 * NT / 256
     uint32_t hi4 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(o[7], o[6], 0x0c0c0400u),
                                          __builtin_amdgcn_perm(o[5], o[4], 0x0c0c0400u), 0x05040100u);
     asm volatile("" : "+v"(lo4), "+v"(hi4));  // keeps the packing here (no code is emitted)
-    if (mx >= m.w && live) fix_push8(fl, 0xFFu, s, p0);
+    if (mx >= (GB ? thr : m.w) && live) fix_push8(fl, 0xFFu, s, p0);
     // pixels outside the source window write the padding value (0 after
     // clip/scale); only threads with a pixel outside build the byte mask
     const int cs = c0 - w.src_c0;
@@ -430,6 +443,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2 * NT / 256
     const int D = (int)p0 + off;  // destination of byte 0
     const int rr = off & 7;       // uniform
     uint8_t* o8 = out + s * npx;
+    // the destinations no source pixel reaches -- [0, off) for off > 0,
+    // [npx + off, npx) for off < 0, all outside the destination window -- take
+    // the padding value, written by the site part's first / last workgroup
+    // (k_chain_fill's job for k_chain_u8)
+    if ((off > 0 && tile == 0) || (off < 0 && tile == (int64_t)gridDim.x - 1)) {
+      const int b0 = off > 0 ? 0 : n32 + off, b1 = off > 0 ? off : n32;
+      const uint8_t pad = slut[0];
+      for (int b = b0 + (int)threadIdx.x; b < b1; b += NT) o8[b] = pad;
+    }
     if ((off & 127) == 0) {  // line-aligned destination: direct stores
       if (live && (unsigned)D < (unsigned)n32) *reinterpret_cast<uint64_t*>(o8 + D) = v8;
       return;
@@ -547,6 +569,9 @@ __global__ __launch_bounds__(256) void k_chain_u8_scalar(const uint16_t* __restr
 // source pixels): the corrected value -> clip -> scale, written at the pixel's
 // aligned destination; pixels outside the source window were written as
 // padding and are left alone.  Overflowed list: every source pixel.
+// A pixel of a flagged group whose f32 value (recomputed with the streaming
+// kernels' own instructions) lies within its error bound |o| (K1 a + K2) <
+// 0.998 keeps the byte the streaming kernel wrote; the others are refined.
 template <bool LOG>
 __global__ __launch_bounds__(256) void k_fix_chain(const uint16_t* __restrict__ in,
                                                    uint8_t* __restrict__ out, int H, int W,
@@ -554,7 +579,9 @@ __global__ __launch_bounds__(256) void k_fix_chain(const uint16_t* __restrict__ 
                                                    const double2* __restrict__ c64,
                                                    const RefineConst* __restrict__ rc,
                                                    const tmh_window* __restrict__ win, int lo,
-                                                   int hi, int T, double step) {
+                                                   int hi, int T, double step,
+                                                   const float2* __restrict__ coef_lin,
+                                                   const float4* __restrict__ mconst2) {
   const int64_t npx = (int64_t)H * W;
   const unsigned int n = *fl.n;
   const bool all = n > fl.cap;
@@ -567,17 +594,32 @@ __global__ __launch_bounds__(256) void k_fix_chain(const uint16_t* __restrict__ 
     uint32_t mask;
     fix_entry(fl, all, i, npx, s, p0, mask);
     const tmh_window w = win[s];
+    const int r0 = (int)(p0 / W), c0 = (int)(p0 - (int64_t)r0 * W);  // one division per entry
     for (int j = 0; j < 8; ++j) {
       const int64_t p = p0 + j;
       if (!((mask >> j) & 1u) || p >= npx) continue;
-      const int r = (int)(p / W), c = (int)(p % W);
+      int r = r0, c = c0 + j;
+      if (c >= W) {  // a group of the scalar path may wrap into the next row(s)
+        r += c / W;
+        c %= W;
+      }
       if ((unsigned)(r - w.src_r0) >= (unsigned)w.rows ||
           (unsigned)(c - w.src_c0) >= (unsigned)w.cols)
         continue;
+      const uint16_t px = in[s * npx + p];
+      {  // the streaming kernels' f32 value and its bound
+        constexpr float K1 = (float)(kRefineK1 * 1.002), K2 = (float)(kRefineK2 * 1.002);
+        const float4 m = mconst2[0];
+        const float2 cf = coef_lin[p];
+        float L = (float)px;
+        if (LOG) L = __builtin_amdgcn_logf(__builtin_fmaxf(L, m.z));
+        const float t = __builtin_fmaf(L - cf.x, cf.y, m.x);
+        const float o = LOG ? __builtin_amdgcn_exp2f(t) : t;
+        if (__builtin_fabsf(o) * __builtin_fmaf(cf.y, K1, K2) < 0.998f) continue;
+      }
       const double2 q = c64[p];
       const uint32_t v16 =
-          (uint32_t)correct_ref_f64<LOG>(in[s * npx + p], q.x, q.y, k.S, k.M, k.zero_log10) &
-          0xFFFFu;
+          (uint32_t)correct_ref_f64<LOG>(px, q.x, q.y, k.S, k.M, k.zero_log10) & 0xFFFFu;
       const int64_t d = (int64_t)(r - w.src_r0 + w.dst_r0) * W + (c - w.src_c0 + w.dst_c0);
       out[s * npx + d] = (uint8_t)clip_scale8(v16, lo, hi, T, step);
     }
@@ -648,14 +690,16 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
       else if (zero_log10 <= -8.0) TMH_CHAIN_T(true, true);
       else TMH_CHAIN_T(true, false);
 #undef TMH_CHAIN_T
-    } else if (log_transform) {
-      if (lut) TMH_CHAIN(true, 1, 256, shm, nullptr); else TMH_CHAIN(true, 0, 256, shm, nullptr);
     } else {
-      if (lut) TMH_CHAIN(false, 1, 256, shm, nullptr); else TMH_CHAIN(false, 0, 256, shm, nullptr);
+      if (log_transform) {
+        if (lut) TMH_CHAIN(true, 1, 256, shm, nullptr); else TMH_CHAIN(true, 0, 256, shm, nullptr);
+      } else {
+        if (lut) TMH_CHAIN(false, 1, 256, shm, nullptr); else TMH_CHAIN(false, 0, 256, shm, nullptr);
+      }
+      hipLaunchKernelGGL(k_chain_fill, dim3(64, (unsigned)n_sites), dim3(256), 0, s, out, H, W,
+                         d_win, lo, hi, T, step);
     }
 #undef TMH_CHAIN
-    hipLaunchKernelGGL(k_chain_fill, dim3(64, (unsigned)n_sites), dim3(256), 0, s, out, H, W,
-                       d_win, lo, hi, T, step);
   } else {
     const dim3 grid((unsigned)cdiv(npx, 256));
     if (log_transform)
@@ -667,10 +711,10 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
   }
   if (log_transform)
     hipLaunchKernelGGL(k_fix_chain<true>, dim3(512), dim3(256), 0, s, in, out, H, W, n_sites, fl,
-                       coef64, rc, d_win, lo, hi, T, step);
+                       coef64, rc, d_win, lo, hi, T, step, coef_lin, mconst2);
   else
     hipLaunchKernelGGL(k_fix_chain<false>, dim3(512), dim3(256), 0, s, in, out, H, W, n_sites, fl,
-                       coef64, rc, d_win, lo, hi, T, step);
+                       coef64, rc, d_win, lo, hi, T, step, coef_lin, mconst2);
   TMH_HIP(hipGetLastError());
 }
 

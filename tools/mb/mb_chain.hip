@@ -123,13 +123,14 @@ static int run(int argc, char** argv) {
                          clin, mc2, fl, dw, lo, hi, T, step, lut8);
     });
   };
-  auto trimmed = [&](const char* nm, auto z_tag, auto pf_tag, int64_t prt) {
+  auto trimmed = [&](const char* nm, auto z_tag, auto pf_tag, int64_t prt, auto gb_tag) {
     constexpr bool Z = decltype(z_tag)::value, PF = decltype(pf_tag)::value;
+    constexpr bool GB = decltype(gb_tag)::value;
     const int64_t pp = (S + prt - 1) / prt;
     const dim3 g((unsigned)((npx / 8 + 1023) / 1024), (unsigned)((S + pp - 1) / pp));
     time(nm, [&] {
       CK(hipMemsetAsync(fn, 0, 4, 0));
-      hipLaunchKernelGGL((k_chain_u8t<true, Z, 1024, PF>), g, dim3(1024), 65536, 0, in, out, H, W,
+      hipLaunchKernelGGL((k_chain_u8t<true, Z, 1024, PF, GB>), g, dim3(1024), 65536, 0, in, out, H, W,
                          S, pp, clin, mc2, fl, dw, lut8);
     });
   };
@@ -137,21 +138,42 @@ static int run(int argc, char** argv) {
   using F_ = std::false_type;
   for (int r = 0; r < 2; ++r) {
     full("chain k_chain_u8 64 KB, NT 1024", std::integral_constant<int, 1024>());
-    trimmed("chain k_chain_u8t (zf add)", T_(), F_(), 8);
-    trimmed("chain k_chain_u8t (zf max)", F_(), F_(), 8);
-    trimmed("chain k_chain_u8t prefetch", T_(), T_(), 8);
-    trimmed("chain k_chain_u8t 6 parts", T_(), F_(), 6);
-    trimmed("chain k_chain_u8t 12 parts", T_(), F_(), 12);
-    trimmed("chain k_chain_u8t 16 parts", T_(), F_(), 16);
-    trimmed("chain k_chain_u8t pf 16 parts", T_(), T_(), 16);
-    trimmed("chain k_chain_u8t pf 24 parts", T_(), T_(), 24);
-    trimmed("chain k_chain_u8t pf 32 parts", T_(), T_(), 32);
+    trimmed("chain k_chain_u8t (zf add)", T_(), F_(), 8, T_());
+    trimmed("chain k_chain_u8t (zf max)", F_(), F_(), 8, T_());
+    trimmed("chain k_chain_u8t prefetch", T_(), T_(), 8, T_());
+    trimmed("chain k_chain_u8t 6 parts", T_(), F_(), 6, T_());
+    trimmed("chain k_chain_u8t 12 parts", T_(), F_(), 12, T_());
+    trimmed("chain k_chain_u8t 16 parts", T_(), F_(), 16, T_());
+    trimmed("chain k_chain_u8t pf 16 parts", T_(), T_(), 16, T_());
+    trimmed("chain k_chain_u8t pf 24 parts", T_(), T_(), 24, T_());
+    trimmed("chain k_chain_u8t pf 32 parts", T_(), T_(), 32, T_());
+    trimmed("chain k_chain_u8t pf 16, launch T", T_(), T_(), 16, F_());
+  }
+  {  // realistic flags: T from the coefficients (a_max 1.05 except 64 columns at a = 40)
+    std::vector<float> c(npx * 2);
+    for (int64_t i = 0; i < npx; ++i) {
+      c[2 * i] = 8.3f + 0.1f * (float)((i * 7) % 13) / 13.0f;
+      c[2 * i + 1] = (i % W) >= 1000 && (i % W) < 1064 ? 40.0f : 1.0f + 0.05f * (float)((i * 5) % 11) / 11.0f;
+    }
+    CK(hipMemcpy(clin, c.data(), npx * 8, hipMemcpyHostToDevice));
+    const float T = (float)(1.0 / (6.7e-6 * 40.0 + 4.2e-6));
+    const float m[4] = {8.2f, 0.0f, 1e-10f, T};
+    CK(hipMemcpy(mc2, m, 16, hipMemcpyHostToDevice));
+    unsigned int nf = 0;
+    for (int r = 0; r < 2; ++r) {
+      trimmed("FLAGS k_chain_u8t pf 16, group bound", T_(), T_(), 16, T_());
+      CK(hipMemcpy(&nf, fn, 4, hipMemcpyDeviceToHost));
+      printf("   flagged groups %u\n", nf);
+      trimmed("FLAGS k_chain_u8t pf 16, launch T", T_(), T_(), 16, F_());
+      CK(hipMemcpy(&nf, fn, 4, hipMemcpyDeviceToHost));
+      printf("   flagged groups %u\n", nf);
+    }
   }
   {  // ablation: every site unshifted (line-aligned destination: no LDS staging, no barriers)
     std::vector<tmh_window> w0(S);
     for (int64_t i = 0; i < S; ++i) w0[i] = tmh_window{0, 0, 0, 0, H, W};
     CK(hipMemcpy(dw, w0.data(), S * sizeof(tmh_window), hipMemcpyHostToDevice));
-    trimmed("ABLATION unshifted k_chain_u8t pf 16", T_(), T_(), 16);
+    trimmed("ABLATION unshifted k_chain_u8t pf 16", T_(), T_(), 16, T_());
     full("ABLATION unshifted k_chain_u8 1024", std::integral_constant<int, 1024>());
     std::vector<tmh_window> w(S);
     for (int64_t i = 0; i < S; ++i) {
