@@ -136,6 +136,11 @@ static int run(int argc, char** argv) {
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
+  // (Measured and removed: 960- and 896-thread workgroups with a
+  // double-buffered stage and one barrier per site -- the only shapes whose
+  // two stages fit beside the 64 KB table at two workgroups per CU: 12.68 /
+  // 17.04 ms against 12.06 for 1,024 threads with two barriers per site;
+  // profiles/r3/mb_chain_stage_db_r3z6.txt.)
   for (int r = 0; r < 2; ++r) {
     full("chain k_chain_u8 64 KB, NT 1024", std::integral_constant<int, 1024>());
     trimmed("chain k_chain_u8t (zf add)", T_(), F_(), 8, T_());
