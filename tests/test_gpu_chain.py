@@ -129,9 +129,10 @@ def test_chain_device_random_windows(L, shape, bounds):
     base = synth_sites_host(5, H, W, seed=41)
     st = orc.run_illumstats(base)
     sm, ss = orc.smooth_reflect(st.mean), orc.smooth_reflect(st.std)
-    sites = np.stack(synth_sites_host(6, H, W, seed=42))
+    sites = np.stack(synth_sites_host(7, H, W, seed=42))
     sites[0, 3, :9] = 0
-    shifts = [(0, 0), (3, -5), (-4, 7), (1, 1), (-2, -3), (0, 6)]
+    # (1, 0): a whole-row shift, 8-byte aligned but not line aligned when W = 320
+    shifts = [(0, 0), (3, -5), (-4, 7), (1, 1), (-2, -3), (0, 6), (1, 0)]
     res = (4, 4, 7, 7)
     wins = np.stack([align_window((H, W), y, x, *res, crop=False)[0] for y, x in shifts])
     wins[5]["rows"] = 0  # all padding

@@ -331,7 +331,7 @@ __global__ __launch_bounds__(NT) void k_chain_u8(const uint16_t* __restrict__ in
 //    ors and a masking bitop;
 //  * the align window's byte mask only for threads whose 8 pixels are not all
 //    inside it (a divergent branch: whole waves skip it).
-template <bool LOG, bool ZADD, int NT, bool PF = false, bool GB = true>
+template <bool LOG, bool ZADD, int NT, bool PF = false, bool GB = true, bool SEAM = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2 * NT / 256))) void k_chain_u8t(const uint16_t* __restrict__ in,
                                                    uint8_t* __restrict__ out, int H, int W,
                                                    int64_t n_sites, int64_t per,
@@ -350,8 +350,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2 * NT / 256
   const bool live = g < ngroups;
   const int lane = threadIdx.x & 63;
   const bool top_lane = threadIdx.x == NT - 1 || g + 1 >= ngroups;
-  __shared__ uint64_t edge[NT / 64];
-  __shared__ __attribute__((aligned(16))) uint8_t stage[NT * 8 + 256];
+  // SEAM: only the 128-B lines two waves share are staged (two sets, one
+  // barrier per site); otherwise the whole workgroup's bytes (k_chain_u8's
+  // staging, two barriers per site)
+  constexpr int kSeams = NT / 64 + 1;  // seam s = line L0 + 512 s
+  __shared__ uint64_t edge[SEAM ? 1 : NT / 64];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[SEAM ? 2 * kSeams * 128 : NT * 8 + 256];
   const int64_t p0 = (live ? g : 0) * 8;
   const int r = (int)(p0 / W), c0 = (int)(p0 % W);
   const float4 m = mconst2[0];
@@ -450,10 +454,64 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2 * NT / 256
     if ((off > 0 && tile == 0) || (off < 0 && tile == (int64_t)gridDim.x - 1)) {
       const int b0 = off > 0 ? 0 : n32 + off, b1 = off > 0 ? off : n32;
       const uint8_t pad = slut[0];
+#pragma unroll 1
       for (int b = b0 + (int)threadIdx.x; b < b1; b += NT) o8[b] = pad;
     }
     if ((off & 127) == 0) {  // line-aligned destination: direct stores
       if (live && (unsigned)D < (unsigned)n32) *reinterpret_cast<uint64_t*>(o8 + D) = v8;
+      return;
+    }
+    if (SEAM) {
+      // A wave's 512 output bytes [o0 + 512 w, +512) fully cover the three
+      // lines L0 + 512 w + 128 k (k = 1..3): its lanes store their aligned
+      // 8-byte words there directly.  The lines L0 + 512 s (s = 0..16) are
+      // shared with the neighbouring wave (or workgroup): their words and the
+      // partial words at the waves' edges go to an LDS copy of those lines,
+      // stored after one barrier as whole 16-B chunks.
+      const int o0 = (int)(tile * NT * 8) + off;  // uniform
+      const int L0 = o0 & ~127;
+      uint8_t* seam = stage + (int)(s & 1) * (kSeams * 128);
+      const uint32_t nlo = (uint32_t)__shfl_down((int)lo4, 1, 64);
+      const uint32_t nhi = (uint32_t)__shfl_down((int)hi4, 1, 64);
+      const uint64_t n8 = ((uint64_t)nhi << 32) | nlo;
+      const bool wtop = lane == 63 || g + 1 >= ngroups;  // no upper neighbour in the wave
+      if (live) {
+        const int X = rr == 0 ? D : D - rr + 8;  // the aligned word this lane completes
+        const int r = X - L0;
+        const bool in_seam = (r & 511) < 128;
+        uint8_t* sp = seam + (r >> 9) * 128 + (r & 127);
+        if (rr == 0 || !wtop) {  // a whole word: ours, or our [8 - rr, 8) + the upper lane's [0, 8 - rr)
+          const uint64_t v = rr == 0 ? v8 : (v8 >> (8 * (8 - rr))) | (n8 << (8 * rr));
+          if (in_seam)
+            *reinterpret_cast<uint64_t*>(sp) = v;
+          else if ((unsigned)X < (unsigned)n32)
+            *reinterpret_cast<uint64_t*>(o8 + X) = v;
+        } else {  // the wave's top lane: only our bytes of that word
+          if (in_seam)
+            store_head(sp, v8 >> (8 * (8 - rr)), rr);
+          else if ((unsigned)X < (unsigned)n32)
+            store_head(o8 + X, v8 >> (8 * (8 - rr)), rr);
+        }
+        if (rr != 0 && lane == 0) {  // our bytes [0, 8 - rr): the top of word X - 8, a seam line
+          const int q = X - 8 - L0;
+          store_tail(seam + (q >> 9) * 128 + (q & 127) + 8, v8, 8 - rr);
+        }
+      }
+      __syncthreads();  // seam lines complete (the other set was read before it)
+      const int wg_bytes = (int)((ngroups - tile * NT < NT ? ngroups - tile * NT : NT) * 8);
+      const int v0 = o0 > 0 ? o0 : 0;
+      const int v1 = o0 + wg_bytes < n32 ? o0 + wg_bytes : n32;
+      if ((int)threadIdx.x < kSeams * 8) {
+        const int sl = threadIdx.x >> 3, ch = threadIdx.x & 7;
+        const int c = L0 + 512 * sl + 16 * ch;
+        const uint8_t* src8 = seam + sl * 128 + 16 * ch;
+        if (c + 16 <= v1 && c >= v0) {
+          *reinterpret_cast<uint4*>(o8 + c) = *reinterpret_cast<const uint4*>(src8);
+        } else if (c < v1 && c + 16 > v0) {
+          for (int b = 0; b < 16; ++b)
+            if (c + b >= v0 && c + b < v1) o8[c + b] = src8[b];
+        }
+      }
       return;
     }
     // as k_chain_u8: the workgroup's output bytes staged in LDS and stored as
@@ -588,21 +646,20 @@ __global__ __launch_bounds__(256) void k_fix_chain(const uint16_t* __restrict__ 
   const int64_t total = all ? n_sites * ((npx + 7) / 8) : (int64_t)n;
   if (total == 0) return;
   const RefineConst k = *rc;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * 256) {
+  // one thread per (entry, pixel): the 8 lanes of an entry read its pixels
+  // and coefficients together, and the rare f64 refinements spread over lanes
+  for (int64_t it = (int64_t)blockIdx.x * 256 + threadIdx.x; it < total * 8;
+       it += (int64_t)gridDim.x * 256) {
+    const int64_t i = it >> 3;
+    const int j = (int)(it & 7);
     int64_t s, p0;
     uint32_t mask;
     fix_entry(fl, all, i, npx, s, p0, mask);
-    const tmh_window w = win[s];
-    const int r0 = (int)(p0 / W), c0 = (int)(p0 - (int64_t)r0 * W);  // one division per entry
-    for (int j = 0; j < 8; ++j) {
+    {
       const int64_t p = p0 + j;
       if (!((mask >> j) & 1u) || p >= npx) continue;
-      int r = r0, c = c0 + j;
-      if (c >= W) {  // a group of the scalar path may wrap into the next row(s)
-        r += c / W;
-        c %= W;
-      }
+      const tmh_window w = win[s];
+      const int r = (int)(p / W), c = (int)(p - (int64_t)r * W);
       if ((unsigned)(r - w.src_r0) >= (unsigned)w.rows ||
           (unsigned)(c - w.src_c0) >= (unsigned)w.cols)
         continue;
@@ -683,8 +740,8 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
       const int64_t tparts = n_sites >= 128 ? 16 : parts, tper = cdiv(n_sites, tparts);
       const dim3 grid((unsigned)cdiv(npx >> 3, 1024), (unsigned)cdiv(n_sites, tper));
 #define TMH_CHAIN_T(L_, Z_)                                                                      \
-  hipLaunchKernelGGL((k_chain_u8t<L_, Z_, 1024, true>), grid, dim3(1024), 65536, s, in, out, H, \
-                     W, n_sites, tper, coef_lin, mconst2, fl, d_win, lut8)
+  hipLaunchKernelGGL((k_chain_u8t<L_, Z_, 1024, true, true, true>), grid, dim3(1024), 65536, s, \
+                     in, out, H, W, n_sites, tper, coef_lin, mconst2, fl, d_win, lut8)
       // zf = 10**zero_log10 below 2^-25 (~2.98e-8): the floor as an add is exact
       if (!log_transform) TMH_CHAIN_T(false, false);
       else if (zero_log10 <= -8.0) TMH_CHAIN_T(true, true);
@@ -710,11 +767,11 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
                          coef_lin, mconst2, fl, d_win, lo, hi, T, step);
   }
   if (log_transform)
-    hipLaunchKernelGGL(k_fix_chain<true>, dim3(512), dim3(256), 0, s, in, out, H, W, n_sites, fl,
+    hipLaunchKernelGGL(k_fix_chain<true>, dim3(2048), dim3(256), 0, s, in, out, H, W, n_sites, fl,
                        coef64, rc, d_win, lo, hi, T, step, coef_lin, mconst2);
   else
-    hipLaunchKernelGGL(k_fix_chain<false>, dim3(512), dim3(256), 0, s, in, out, H, W, n_sites, fl,
-                       coef64, rc, d_win, lo, hi, T, step, coef_lin, mconst2);
+    hipLaunchKernelGGL(k_fix_chain<false>, dim3(2048), dim3(256), 0, s, in, out, H, W, n_sites,
+                       fl, coef64, rc, d_win, lo, hi, T, step, coef_lin, mconst2);
   TMH_HIP(hipGetLastError());
 }
 

@@ -136,6 +136,20 @@ static int run(int argc, char** argv) {
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
+  auto seamed = [&](const char* nm, auto seam_tag) {
+    constexpr bool SM = decltype(seam_tag)::value;
+    const int64_t pp = (S + 15) / 16;
+    const dim3 g((unsigned)((npx / 8 + 1023) / 1024), (unsigned)((S + pp - 1) / pp));
+    time(nm, [&] {
+      CK(hipMemsetAsync(fn, 0, 4, 0));
+      hipLaunchKernelGGL((k_chain_u8t<true, true, 1024, true, true, SM>), g, dim3(1024), 65536, 0,
+                         in, out, H, W, S, pp, clin, mc2, fl, dw, lut8);
+    });
+  };
+  for (int r = 0; r < 3; ++r) {
+    seamed("stage whole workgroup (2 barriers)", F_());
+    seamed("stage seam lines only (1 barrier)", T_());
+  }
   // (Measured and removed: 960- and 896-thread workgroups with a
   // double-buffered stage and one barrier per site -- the only shapes whose
   // two stages fit beside the 64 KB table at two workgroups per CU: 12.68 /
