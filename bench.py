@@ -92,6 +92,9 @@ def parse():
                         "takes its contiguous path, the fused pass a block table into it) or in "
                         "B-site blocks allocated alternately with the output blocks")
     p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
+    p.add_argument("--channel-streams", choices=["per-channel", "one"], default="per-channel",
+                   help="several channels: each on its own stream (its merges overlap the "
+                        "others' kernels), or all on one stream")
     p.add_argument("--no-same-workload", action="store_true",
                    help="N > 1: skip rank 0's single-GPU run of the same (unsharded) workload")
     p.add_argument("--pipeline", choices=["fused", "separate"], default="fused",
@@ -954,7 +957,7 @@ def main():
         others overlap on their own streams, configs[2]/[3])."""
 
         def __init__(self, c):
-            self.stream = stream if c == 0 else torch.cuda.Stream(dev)
+            self.stream = stream if c == 0 or a.channel_streams == "one" else torch.cuda.Stream(dev)
             self.sp = C.c_void_p(self.stream.cuda_stream)
             blk_in, blk_out = chan_sites[c]
             self.blocks = (blk_in, blk_out)
