@@ -1287,24 +1287,29 @@ __global__ __launch_bounds__(kPctThreads) void k_pct_acc(const uint32_t* __restr
   double a = acc[t];
   const uint32_t* p = vlh + (int64_t)(q / kOsTile) * tstride + (q % kOsTile);
   constexpr int64_t ld = kOsTile;
-  // software pipeline: the next kPctUnroll sites' loads are in flight while
-  // the current ones are folded in (tail loads clamp to the last site)
+  // software pipeline over two register sets used alternately (no copies
+  // between them: a copy of a pending load makes the compiler wait for every
+  // load in flight): the next kPctUnroll sites' loads are in flight while the
+  // current ones are folded in (tail loads clamp to the last site)
   const int64_t last = n_sites - 1;
-  uint32_t v[kPctUnroll];
+  auto ld1 = [&](int64_t u) -> uint32_t {
+    u = u < last ? u : last;
+    return NTL ? __builtin_nontemporal_load(p + u * ld) : p[u * ld];
+  };
+  uint32_t va[kPctUnroll], vb[kPctUnroll];
 #pragma unroll
-  for (int k = 0; k < kPctUnroll; ++k) v[k] = (NTL ? __builtin_nontemporal_load(p + (k < last ? k : last) * ld) : p[(k < last ? k : last) * ld]);
-  for (int64_t s = 0; s < n_sites; s += kPctUnroll) {
-    uint32_t vn[kPctUnroll];
+  for (int k = 0; k < kPctUnroll; ++k) va[k] = ld1(k);
+  for (int64_t s = 0; s < n_sites; s += 2 * kPctUnroll) {
 #pragma unroll
-    for (int k = 0; k < kPctUnroll; ++k) {
-      const int64_t u = s + kPctUnroll + k < last ? s + kPctUnroll + k : last;
-      vn[k] = NTL ? __builtin_nontemporal_load(p + u * ld) : p[u * ld];
-    }
+    for (int k = 0; k < kPctUnroll; ++k) vb[k] = ld1(s + kPctUnroll + k);
 #pragma unroll
     for (int k = 0; k < kPctUnroll; ++k)
-      if (s + k < n_sites) a = add_nc(a, lerp_np(v[k] & 0xFFFFu, v[k] >> 16, g));
+      if (s + k < n_sites) a = add_nc(a, lerp_np(va[k] & 0xFFFFu, va[k] >> 16, g));
 #pragma unroll
-    for (int k = 0; k < kPctUnroll; ++k) v[k] = vn[k];
+    for (int k = 0; k < kPctUnroll; ++k) va[k] = ld1(s + 2 * kPctUnroll + k);
+#pragma unroll
+    for (int k = 0; k < kPctUnroll; ++k)
+      if (s + kPctUnroll + k < n_sites) a = add_nc(a, lerp_np(vb[k] & 0xFFFFu, vb[k] >> 16, g));
   }
   acc[t] = a;
 }
