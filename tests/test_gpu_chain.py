@@ -212,6 +212,46 @@ def test_chain_overflow_wrap_and_beyond_int32(L, bounds):
         assert (d == 0).mean() > 0.99
 
 
+@pytest.mark.parametrize("bounds", [(0, 65535), (300, 5000)])
+def test_chain_without_log_transform(L, bounds):
+    """log_transform=False (raw-intensity statistics): k_chain_u8t<LOG=false>
+    -- no zero floor, values may be negative before the x86 cast -- against
+    the oracle chain with log_transform=False; one column of tiny std drives
+    values past 2^16 and 2^31 (refined in f64)."""
+    import ctypes as C
+    from tmlibrary_amd import hip
+    from tmlibrary_amd.image import Corrector, align_window
+    from tmlibrary_amd.synth import synth_sites_host
+    H, W = 96, 256
+    base = np.stack(synth_sites_host(6, H, W, seed=77)).astype(np.float64)
+    mu = base.mean(axis=0)
+    sd = base.std(axis=0) + 1.0
+    sd[:, 40:48] = 1e-3
+    sd[:, 44:46] = 1e-5
+    sites = np.stack(synth_sites_host(4, H, W, seed=78))
+    shifts = [(0, 0), (2, -3), (-1, 5), (1, 0)]
+    res = (4, 4, 8, 8)
+    wins = np.stack([align_window((H, W), y, x, *res, crop=False)[0] for y, x in shifts])
+    lo, hi = bounds
+    corr = Corrector(mu, sd, log_transform=False)
+    d_in, d_out = C.c_void_p(), C.c_void_p()
+    assert L.tmh_malloc_device(C.byref(d_in), sites.nbytes) == 0
+    assert L.tmh_malloc_device(C.byref(d_out), sites.size) == 0
+    assert L.tmh_memcpy(d_in, sites.ctypes.data, sites.nbytes, 0, None) == 0
+    hip.check(L.tmh_correct_chain_u8_device(corr._h, d_in, d_out, len(sites), hip.ptr(wins), lo,
+                                            hi, None))
+    got = np.empty(sites.shape, np.uint8)
+    assert L.tmh_memcpy(got.ctypes.data, d_out, got.nbytes, 1, None) == 0
+    L.tmh_free_device(d_in)
+    L.tmh_free_device(d_out)
+    corr.close()
+    for i, ((y, x), s) in enumerate(zip(shifts, sites)):
+        want = orc.illuminati_chain(s, mu, sd, (y, x), res, lo, hi, log_transform=False)
+        d = np.abs(got[i].astype(np.int32) - want.astype(np.int32))
+        assert d.max() <= 1, (i, int(d.max()))
+        assert (d == 0).mean() > 0.99
+
+
 def test_chain_rejects_bad_windows(L):
     from tmlibrary_amd.image import Corrector, align_window
     g, wins = _chain_inputs()
