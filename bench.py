@@ -92,6 +92,9 @@ def parse():
                         "takes its contiguous path, the fused pass a block table into it) or in "
                         "B-site blocks allocated alternately with the output blocks")
     p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
+    p.add_argument("--hbm-skip-gb", type=float, default=0.0,
+                   help="hold an allocation of this many GB before the sites' buffers "
+                        "(placement study: which HBM region the first buffer lands in)")
     p.add_argument("--channel-streams", choices=["per-channel", "one"], default="per-channel",
                    help="several channels: each on its own stream (its merges overlap the "
                         "others' kernels), or all on one stream")
@@ -920,6 +923,8 @@ def main():
     # pass gains from blocked outputs; so by default the input is one buffer
     # (block views of it for the fused pass's table) and the outputs blocks.
     in_contig = not B or a.in_layout == "contiguous"
+    skip = (torch.empty(int(a.hbm_skip_gb * 2 ** 30), dtype=torch.uint8, device=dev)
+            if a.hbm_skip_gb > 0 else None)
     chan_sites = []  # per channel: (input blocks, output blocks); one block if contiguous
     for c in range(CH):
         blk_in, blk_out = [], []
