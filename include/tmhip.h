@@ -81,13 +81,14 @@ int tmh_stats_set_stream(tmh_stats* h, void* stream);
 int tmh_stats_reset(tmh_stats* h);
 
 /* Options of a handle (results never depend on them):
- *   TMH_OPT_FUSED_CONFIG   0..4: (sites per unit, threads, LDS bins) of the
+ *   TMH_OPT_FUSED_CONFIG   0..5: (sites per unit, threads, LDS bins) of the
  *                          fused correct+histogram pass = (2, 1024, 32768),
  *                          (4, 1024, 32768), (2, 512, 16384), (4, 512, 16384),
- *                          (1, 1024, 32768).  -1 (default): chosen per launch
- *                          on the device from the Welford pass's counts over
- *                          the pending sites -- 3; or 0 when >= 2% of the
- *                          8-pixel groups hold a value >= 4,096; or, when
+ *                          (1, 1024, 32768), (4, 1024, 65536 u16 counters
+ *                          packed two sites to a word).  -1 (default): chosen
+ *                          per launch on the device from the Welford pass's
+ *                          counts over the pending sites -- 3; or 5 when >= 2%
+ *                          of the 8-pixel groups hold a value >= 4,096; or, when
  *                          >= 33% hold a value >= 16,384 ("very wide" sites,
  *                          e.g. uniform 16-bit data), the pass runs without
  *                          its histogram and a per-site u16-pair LDS

@@ -171,8 +171,10 @@ def test_bright_fullsize(L):
     """bright 16-bit data (lognormal(8.5, 0.6), about a third
     of the pixels >= 4,096) at full size.  The Welford pass takes its wide
     log10 path for most pixel groups and counts them; the automatic fused
-    configuration then runs kFusedWide: two sites per unit, 16,384 u32 bins
-    each (2, 1024, 32768).  The same job with the narrow slices forced (global
+    configuration then runs kFusedWide: four sites per unit, 16,384 bins each
+    as u16 counters packed two sites to a word (4, 1024, 65536; the flush's
+    wrap check is exercised by test_packed_counters_wrap).  The same job with
+    the narrow slices forced (global
     adds for every pixel >= 4,096) must give identical results, and both
     match the oracle.  (64 sites: below the 96 the bright Welford pass needs,
     so this covers the standard pass's rare log10 path; tests/test_gpu_blocked.py
@@ -269,7 +271,7 @@ def _wide_groups(sites):
     return int(np.count_nonzero((g >= 4096).any(axis=2)))
 
 
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5])
 def test_fused_multi_job_configs(L, cfg):
     """cfg -1 is the automatic choice: job 1 is bright (lognormal(8.5, 0.6)),
     so the Welford count must select the wide configuration for it, and the
@@ -343,7 +345,7 @@ def _groups_ge(sites, v):
     return int(np.count_nonzero((g >= v).any(axis=2)))
 
 
-@pytest.mark.parametrize("cfg", [-1, 3])
+@pytest.mark.parametrize("cfg", [-1, 3, 5])
 def test_very_wide_jobs(L, cfg):
     """Very wide sites (a third or more of the 8-pixel groups hold a value
     >= 16,384): with the automatic configuration the fused pass runs without
@@ -423,6 +425,56 @@ def test_very_wide_jobs(L, cfg):
     r = _results(L, h, H, W, n)
     assert np.array_equal(r["hist"], sum(orc.histogram_u16(s) for s in sites))
     assert np.array_equal(r["acc"], orc.run_illumstats(list(sites)).percentile_sums)
+    L.tmh_corrector_destroy(c)
+    L.tmh_stats_destroy(h)
+    for b in planes + [d_in, d_out]:
+        b.free()
+
+
+def test_packed_counters_wrap(L):
+    """Fused configuration 5 (four sites per unit, u16 LDS counters packed two
+    sites to a word, 8 bands): at 768 x 768 a band holds 73,728 pixels of a
+    site, so a value filling a band wraps its 16-bit counter.  The flush's
+    per-site sum check must catch it and recount the band from the pixels:
+    sites of one value (5,000 and 16,383, the top LDS bin), a half-constant
+    bright site, a bright site, and a site with a value >= 16,384 in every
+    pixel group.  Per-site histograms, percentile sums bit-exact; mean/std
+    1e-6 (stats.py:64-121)."""
+    from tmlibrary_amd import hip, synth
+    H, W, n = 768, 768, 5
+    npx = H * W
+    sites = np.stack([synth.synth_exact_host(H, W, 5 + i, 0, i, synth.BRIGHT) for i in range(n)])
+    sites[0] = 5000
+    sites[1] = 16383
+    sites[2, : H // 2] = 3000
+    sites[4, :, ::8] = 40000
+    h = _stats_handle(L, H, W, hip.TMH_STATS_KEEP_SITE_HIST)
+    hip.check(L.tmh_stats_set_option(h, hip.TMH_OPT_FUSED_CONFIG, 5))
+    d_in, d_out = Dev(L, n * npx * 2), Dev(L, n * npx * 2)
+    planes = [Dev(L, npx * 8) for _ in range(5)]
+    mean, std, smean, sstd, tmp = planes
+    from tmlibrary_amd.image import ZERO_LOG10
+    c = C.c_void_p()
+    L.tmh_synchronize(None)
+    hip.check(L.tmh_corrector_create_device(mean.p, std.p, H, W, 1, ZERO_LOG10, None, C.byref(c)))
+    d_in.put(sites)
+    hip.check(L.tmh_stats_reset(h))
+    hip.check(L.tmh_stats_update_welford_device(h, d_in.p, n, 1, None))
+    hip.check(L.tmh_stats_finalize_device(h, mean.p, std.p, None))
+    hip.check(L.tmh_smooth_f64_device(mean.p, smean.p, tmp.p, H, W, 5.0, None))
+    hip.check(L.tmh_smooth_f64_device(std.p, sstd.p, tmp.p, H, W, 5.0, None))
+    hip.check(L.tmh_corrector_update_device(c, smean.p, sstd.p, None))
+    hip.check(L.tmh_correct_u16_hist_device(c, h, d_in.p, d_out.p, n, -1, -1, None))
+    r = _results(L, h, H, W, n)
+    ref = orc.run_illumstats(list(sites))
+    assert r["n"] == n
+    assert_close_rel(r["mean"], ref.mean)
+    for i in range(n):
+        sh = np.empty(65536, np.uint32)
+        hip.check(L.tmh_stats_site_histogram(h, i, hip.ptr(sh)))
+        assert np.array_equal(sh.astype(np.uint64), orc.histogram_u16(sites[i])), i
+    assert np.array_equal(r["hist"], sum(orc.histogram_u16(s) for s in sites))
+    assert np.array_equal(r["acc"], ref.percentile_sums)
     L.tmh_corrector_destroy(c)
     L.tmh_stats_destroy(h)
     for b in planes + [d_in, d_out]:

@@ -265,15 +265,17 @@ void launch_correct_u8(const uint8_t* in, uint8_t* out, int64_t npx, int64_t n_s
 // fused pass configurations (fused_kernels.hip kFusedCfgs).  kFusedAuto picks
 // per launch, on the device: kFusedNarrow (four sites per unit, 4,096-bin
 // slices) unless the Welford pass counted at least kWideFrac of the pixel
-// groups with a value >= 4,096, then kFusedWide (two sites, 16,384 bins each;
-// on bright sites 18.6 ms against 22.4 ms for one site x 32,768 bins, whose
-// single site per unit keeps too few loads in flight, and 231 ms narrow:
-// profiles/r2/mb_fused_bright_r2f.txt).
-constexpr int kFusedConfigs = 5;
+// groups with a value >= 4,096, then kFusedWide: four sites, 16,384 bins
+// each as u16 counters packed two sites to a word (round 3: 15.95-16.11 ms
+// on 3,456 bright sites against 17.67-17.75 for configuration 0's two sites
+// x 16,384 u32 bins, profiles/r3/ab_fused_packed_bright_r3z20.jsonl; round 2:
+// configuration 0 18.6 ms against 22.4 for one site x 32,768 bins and 231 ms
+// narrow, profiles/r2/mb_fused_bright_r2f.txt).
+constexpr int kFusedConfigs = 6;
 constexpr int kFusedQueueInts = 16;  // fused pass scratch: 8 unit counters + 64-bit round union
 constexpr int kFusedAuto = -1;
 constexpr int kFusedNarrow = 3;
-constexpr int kFusedWide = 0;
+constexpr int kFusedWide = 5;
 constexpr double kWideFrac = 0.02;
 // very wide: a third of the 8-pixel groups hold a value >= 16,384 (~5% of the
 // pixels beyond the wide configuration's slices: from there its global atomics

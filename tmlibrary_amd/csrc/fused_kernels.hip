@@ -177,7 +177,15 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // Each workgroup issues its next unit's first loads before it flushes the
 // current unit's histogram slices, so the flush (LDS scan + global atomics +
 // barriers) runs with the next unit's pixels already in flight.
-template <bool LOG, bool CLIP, int SPU, int ABL, int NT, int LB>
+// PK (packed): the LDS counters are u16 halves of 32-bit words -- sites 2j
+// and 2j+1 share word array j (one ds_add of 1 or 0x10000 per pixel, no
+// extra VALU), so four sites get 16,384 bins each in 128 KB.  A half can
+// wrap only if one value fills more than 65,535 pixels of a site's band, so
+// every unit's flush first sums each site's counters (plus the site's
+// pixels that took the global path) against the band's pixel count; a site
+// whose sum falls short is recounted from its pixels with global atomics
+// instead of flushed.
+template <bool LOG, bool CLIP, int SPU, int ABL, int NT, int LB, bool PK = false>
 __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void k_correct_hist(
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
     const float4* __restrict__ coef, const float4* __restrict__ mconst2, FixList fl,
@@ -195,9 +203,15 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   }
   constexpr int BINS = LB / SPU;
   constexpr int SLICE = BINS + 1;
+  constexpr int NSL = PK ? SPU / 2 : SPU;  // word arrays (PK: two sites per array)
   constexpr uint32_t HIMASK = (0xFFFFu & ~(uint32_t)(BINS - 1)) * 0x00010001u;
   static_assert((BINS & (BINS - 1)) == 0, "slice size must be a power of two");
-  __shared__ __attribute__((aligned(16))) uint32_t bins[SPU * SLICE];
+  static_assert(!PK || (SPU % 2 == 0 && BINS <= 16384), "packed: site pairs, u16 headroom");
+  __shared__ __attribute__((aligned(16))) uint32_t bins[NSL * SLICE];
+  __shared__ uint32_t pk_red[PK ? NT / 64 : 1][PK ? SPU : 1];  // packed: per-wave site sums
+  uint32_t rare[SPU];  // packed: this thread's pixels of the unit that took the global path
+#pragma unroll
+  for (int k = 0; k < SPU; ++k) rare[k] = 0u;
   // per site of the unit: the 1,024-bin rounds holding counts (the rare
   // global adds and, at the flush, the slice's non-empty rounds); two sets,
   // alternating by unit, so one is published while the next unit fills the
@@ -212,7 +226,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   __shared__ unsigned long long fix_sh[2][kFixSh];
   __shared__ unsigned int fix_cnt[2];
   const int tid = threadIdx.x;
-  for (int i = tid; i < SPU * SLICE; i += NT) bins[i] = 0u;
+  for (int i = tid; i < NSL * SLICE; i += NT) bins[i] = 0u;
   if (tid < 2 * SPU) rm_sh[tid / SPU][tid % SPU] = 0ull;
   if (tid < 2) fix_cnt[tid] = 0u;
   __syncthreads();
@@ -320,12 +334,13 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     auto process = [&](const uint4 w, const int k, const float4 (&cf)[4], const int g) -> u32x4_t {
       const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
       if (!(ABL & 1)) {
-        uint32_t* sl = bins + k * SLICE;
+        uint32_t* sl = bins + (PK ? k >> 1 : k) * SLICE;
+        const uint32_t inc = PK && (k & 1) ? 0x10000u : 1u;  // compile-time per site
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           const uint32_t lo = wd[p] & 0xFFFFu, hi = wd[p] >> 16;
-          atomicAdd(&sl[lo < (uint32_t)BINS ? lo : (uint32_t)BINS], 1u);
-          atomicAdd(&sl[hi < (uint32_t)BINS ? hi : (uint32_t)BINS], 1u);
+          atomicAdd(&sl[lo < (uint32_t)BINS ? lo : (uint32_t)BINS], inc);
+          atomicAdd(&sl[hi < (uint32_t)BINS ? hi : (uint32_t)BINS], inc);
         }
         if ((w.x | w.y | w.z | w.w) & HIMASK) {  // rare: beyond this site's LDS slice
           uint32_t* h = hs + k * (int64_t)kBins;
@@ -336,10 +351,12 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
             if (lo >= (uint32_t)BINS) {
               atomicAdd(&h[lo], 1u);
               rounds |= 1ull << (lo >> 10);
+              if (PK) ++rare[k];
             }
             if (hi >= (uint32_t)BINS) {
               atomicAdd(&h[hi], 1u);
               rounds |= 1ull << (hi >> 10);
+              if (PK) ++rare[k];
             }
           }
           atomicOr(&rm[k], rounds);  // LDS: published once per unit
@@ -395,6 +412,85 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     cur = nxt;
     if (ABL & 9) continue;
     __syncthreads();
+    if (PK) {
+      // the check: each site's counters (a wrapped half comes up 65,536
+      // short) plus its global-path pixels against the band's pixel count
+      uint32_t sum[SPU];
+#pragma unroll
+      for (int k = 0; k < SPU; ++k) sum[k] = rare[k];
+#pragma unroll
+      for (int j = 0; j < NSL; ++j) {
+#pragma unroll 4
+        for (int b = tid; b < BINS; b += NT) {
+          const uint32_t w = bins[j * SLICE + b];
+          sum[2 * j] += w & 0xFFFFu;
+          sum[2 * j + 1] += w >> 16;
+        }
+      }
+      const int wv = tid >> 6;
+#pragma unroll
+      for (int k = 0; k < SPU; ++k) {
+        uint32_t v = sum[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off, 64);
+        if ((tid & 63) == 0) pk_red[wv][k] = v;
+        rare[k] = 0u;
+      }
+      __syncthreads();
+      const uint32_t band_px = (uint32_t)(un.g1 - un.g0) * 8u;
+      uint32_t bad = 0;  // sites whose counters wrapped
+#pragma unroll
+      for (int k = 0; k < SPU; ++k) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) t += pk_red[w][k];
+        if (k < un.ns && t != band_px) bad |= 1u << k;
+      }
+#pragma unroll
+      for (int j = 0; j < NSL; ++j) {
+        uint32_t* h0 = hs + (2 * j) * (int64_t)kBins;
+        uint32_t* h1 = hs + (2 * j + 1) * (int64_t)kBins;
+        const bool ok0 = 2 * j < un.ns && !((bad >> (2 * j)) & 1u);
+        const bool ok1 = 2 * j + 1 < un.ns && !((bad >> (2 * j + 1)) & 1u);
+        unsigned long long lm0 = 0ull, lm1 = 0ull;
+#pragma unroll 4
+        for (int b = tid; b < BINS; b += NT) {
+          const uint32_t w = bins[j * SLICE + b];
+          if (w) {
+            const uint32_t c0 = w & 0xFFFFu, c1 = w >> 16;
+            if (c0 && ok0) {
+              atomicAdd(&h0[b], c0);
+              lm0 |= 1ull << (b >> 10);
+            }
+            if (c1 && ok1) {
+              atomicAdd(&h1[b], c1);
+              lm1 |= 1ull << (b >> 10);
+            }
+            bins[j * SLICE + b] = 0u;
+          }
+        }
+        if (lm0) atomicOr(&rm[2 * j], lm0);
+        if (lm1) atomicOr(&rm[2 * j + 1], lm1);
+      }
+      if (bad) {  // rare: recount those sites' band pixels below BINS exactly
+        const uint16_t* ib = in + un.s0 * npx;
+        if (tab.in) ib = tab.in[site_block(tab, un.s0)] + site_in_block(tab, un.s0) * npx;
+        for (int k = 0; k < SPU; ++k) {
+          if (!((bad >> k) & 1u)) continue;
+          uint32_t* h = hs + k * (int64_t)kBins;
+          const uint16_t* src = ib + k * npx;
+          unsigned long long lm = 0ull;
+          for (int64_t i = (int64_t)un.g0 * 8 + tid; i < (int64_t)un.g1 * 8; i += NT) {
+            const uint32_t v = src[i];
+            if (v < (uint32_t)BINS) {
+              atomicAdd(&h[v], 1u);
+              lm |= 1ull << (v >> 10);
+            }
+          }
+          if (lm) atomicOr(&rm[k], lm);
+        }
+      }
+    } else {
     // fold this unit's slices into the sites' histograms (contiguous lanes ->
     // bins); the overflow counters are left to wrap, they are never read
 #pragma unroll
@@ -412,6 +508,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
         }
       }
       if (lm) atomicOr(&rm[k], lm);
+    }
     }
     __syncthreads();
     // publish the unit's round masks; the next unit fills the other set, and
@@ -449,12 +546,14 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
 // 17.95 ms on bright sites, profiles/r2/mb_shape_bright_r2x.txt), 16 otherwise.
 struct FusedCfg {
   int spu, threads, lds_bins, bands;
+  bool packed;  // u16 counters, two sites per word (k_correct_hist PK)
 };
-constexpr FusedCfg kFusedCfgs[kFusedConfigs] = {{2, 1024, 32768, 8},
-                                                {4, 1024, 32768, kFusedBands},
-                                                {2, 512, 16384, kFusedBands},
-                                                {4, 512, 16384, kFusedBands},
-                                                {1, 1024, 32768, kFusedBands}};
+constexpr FusedCfg kFusedCfgs[kFusedConfigs] = {{2, 1024, 32768, 8, false},
+                                                {4, 1024, 32768, kFusedBands, false},
+                                                {2, 512, 16384, kFusedBands, false},
+                                                {4, 512, 16384, kFusedBands, false},
+                                                {1, 1024, 32768, kFusedBands, false},
+                                                {4, 1024, 65536, 8, true}};
 template <int K>
 struct FusedCfgCheck {
   static_assert((kFusedCfgs[K].lds_bins / kFusedCfgs[K].spu) % 1024 == 0,
@@ -462,7 +561,7 @@ struct FusedCfgCheck {
   static constexpr bool ok = true;
 };
 static_assert(FusedCfgCheck<0>::ok && FusedCfgCheck<1>::ok && FusedCfgCheck<2>::ok &&
-              FusedCfgCheck<3>::ok && FusedCfgCheck<4>::ok, "");
+              FusedCfgCheck<3>::ok && FusedCfgCheck<4>::ok && FusedCfgCheck<5>::ok, "");
 
 // cfg kFusedNoHist: the narrow shape without its histogram (very wide sites:
 // k_hist_site_u16 builds the histograms)
@@ -479,12 +578,14 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
     constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
     const dim3 grid(n_wg * (1024 / c.threads));                                                  \
     if (clip_lo >= 0)                                                                            \
-      hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, A_, c.threads, c.lds_bins>), grid,    \
+      hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, A_, c.threads, c.lds_bins, c.packed>), \
+                         grid,                                                                   \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
                          clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
                          wide_hi, x_lo, x_hi, tab);                                              \
     else                                                                                         \
-      hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, A_, c.threads, c.lds_bins>), grid,   \
+      hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, A_, c.threads, c.lds_bins, c.packed>), \
+                         grid,                                                                   \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
                          clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
                          wide_hi, x_lo, x_hi, tab);                                              \
@@ -495,6 +596,7 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
     case 1: TMH_LAUNCH_CH(L_, 1, 0) break;                     \
     case 2: TMH_LAUNCH_CH(L_, 2, 0) break;                     \
     case 3: TMH_LAUNCH_CH(L_, 3, 0) break;                     \
+    case 5: TMH_LAUNCH_CH(L_, 5, 0) break;                     \
     case kFusedNoHist: TMH_LAUNCH_CH(L_, kFusedNarrow, 1) break; \
     default: TMH_LAUNCH_CH(L_, 4, 0) break;                    \
   }
