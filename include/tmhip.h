@@ -100,15 +100,12 @@ int tmh_stats_reset(tmh_stats* h);
  *                          (bright sites: the log10 pass is VALU-bound),
  *                          else runs as one part; 1..4: that many parts where
  *                          the launch has >= 32 sites a part
- *   TMH_OPT_TAIL_CHUNKS    1..16: run the fused correct+histogram pass in that
- *                          many site chunks, each chunk's histogram finalize
- *                          overlapping the next chunk's streaming (1: off)
- *   TMH_OPT_PCT_TAIL       percentile tail of the fused pass: 0 (default) =
- *                          per-site order statistics written, then summed in
- *                          site order; 1 = per-site compact CDFs folded in site
- *                          order per quantile chunk (deferred handles, launches
- *                          in several chunks and non-linear quantile tables
- *                          always use 0).  Bit-identical results.
+ *   TMH_OPT_FUSED_EPOCHS   0..64 (default 4): the fused pass writes the
+ *                          order statistics itself -- the workgroup that
+ *                          completes a site group's last pixel band finalizes
+ *                          the group -- over a unit sweep cut into that many
+ *                          epochs, so groups complete throughout the pass;
+ *                          0 = a separate finalize kernel after the pass
  *   TMH_OPT_COPY_THREADS   1..64 (default 8): host threads of the pageable <->
  *                          pinned copies of the host-buffer entry points
  *   TMH_OPT_HOST_STAGING   host-buffer entry points: 0 = the caller's buffers
@@ -119,10 +116,10 @@ int tmh_stats_reset(tmh_stats* h);
  *                          several threads spreads a fresh output's faults) */
 #define TMH_OPT_FUSED_CONFIG 1
 #define TMH_OPT_WELFORD_PARTS 2
-#define TMH_OPT_TAIL_CHUNKS 3
+/* 3 and 6 were TMH_OPT_TAIL_CHUNKS / TMH_OPT_PCT_TAIL (measured slower, removed) */
 #define TMH_OPT_COPY_THREADS 4
 #define TMH_OPT_HOST_STAGING 5
-#define TMH_OPT_PCT_TAIL 6
+#define TMH_OPT_FUSED_EPOCHS 7
 int tmh_stats_set_option(tmh_stats* h, int option, int value);
 
 /* update(image) for a run of sites.  zero_counts_out (host, n_sites, may be

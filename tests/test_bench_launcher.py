@@ -1,0 +1,68 @@
+"""bench.py --gpus N starts its own N rank processes.
+
+The driver runs ``python bench.py --gpus N`` as well as the torchrun form; a
+rank per GPU must exist either way (each channel's sites are
+sharded over one process per GPU; the reference's per-channel jobs,
+tmlib/workflow/corilla/api.py:64-105).  On CPU the launcher is exercised with
+``--dry-run``: every rank joins a gloo group and rank 0 prints the ranks'
+launch environment as the one JSON line.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from util import REPO
+
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _run(args, env_extra=None, timeout=180):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True,
+                          timeout=timeout, env=env)
+
+
+def test_launcher_dry_run_two_ranks():
+    r = _run(["--gpus", "2", "--dry-run"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout  # exactly rank 0's JSON line
+    d = json.loads(lines[0])
+    assert d["dry_run"] and d["n_gpus"] == 2 and d["world_size"] == 2
+    ranks = d["ranks"]
+    assert [e["RANK"] for e in ranks] == ["0", "1"]
+    assert [e["LOCAL_RANK"] for e in ranks] == ["0", "1"]
+    assert {e["WORLD_SIZE"] for e in ranks} == {"2"}
+    assert {e["MASTER_ADDR"] for e in ranks} == {"127.0.0.1"}
+    assert len({e["MASTER_PORT"] for e in ranks}) == 1
+
+
+def test_launcher_rank_failure_is_nonzero():
+    # rank 1 exits before joining the group: rank 0 would wait in the
+    # rendezvous forever, so the launcher must stop it and fail
+    r = _run(["--gpus", "2", "--dry-run"], {"TMH_BENCH_DRY_FAIL_RANK": "1"})
+    assert r.returncode == 3, (r.returncode, r.stderr[-3000:])
+    assert r.stdout.strip() == ""
+
+
+@pytest.mark.skipif(os.environ.get("HIP_VISIBLE_DEVICES") not in (None, ""),
+                    reason="device visibility restricted")
+def test_launcher_refuses_more_ranks_than_gpus():
+    import torch
+    have = torch.cuda.device_count()
+    n = max(2, have + 1)
+    r = _run(["--gpus", str(n), "--steps", "1", "--warmup", "0"], timeout=120)
+    assert r.returncode == 2
+    assert "needs %d visible GPU(s), found %d" % (n, have) in r.stderr
+    assert r.stdout.strip() == ""
+
+
+def test_gpus_must_match_world_size():
+    r = _run(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode == 2
+    assert "disagrees with WORLD_SIZE=2" in r.stderr

@@ -304,6 +304,41 @@ def test_corrector_cache_sees_in_place_writes(L):
     cont.mean.array[0, 0] += 0.0
 
 
+def test_corrector_outlives_container(L):
+    """a Corrector handed out by ``corrector()`` keeps working after
+    its container is released, rebuilt or collected (the cache only drops its
+    reference; the Corrector's own __del__ frees the handle)."""
+    import gc
+
+    from tmlibrary_amd.image import IllumstatsContainer, IllumstatsImage
+    from tmlibrary_amd.metadata import IllumstatsImageMetadata
+    rng = np.random.default_rng(10)
+    img = rng.integers(1, 5000, (40, 56), dtype=np.uint16)
+    mean = rng.random((40, 56)) * 0.2 + 2.5
+    std = rng.random((40, 56)) * 0.1 + 0.2
+    want = orc.correct_illumination(img, mean, std)
+    md = IllumstatsImageMetadata(channel_id=1)
+
+    def make():
+        return IllumstatsContainer(IllumstatsImage(mean.copy(), md),
+                                   IllumstatsImage(std.copy(), md), {})
+
+    corr = make().corrector()  # the container is a temporary
+    gc.collect()
+    assert_dn(corr.apply(img), want)
+    cont = make()
+    c1 = cont.corrector()
+    cont.release()
+    assert_dn(c1.apply(img), want)
+    c2 = cont.corrector()
+    cont.smooth()
+    cont.corrector()  # rebuilt: the old one is only dropped
+    assert_dn(c2.apply(img), want)
+    del cont
+    gc.collect()
+    assert_dn(c2.apply(img), want)
+
+
 def test_correct_channel_mismatch(L):
     from tmlibrary_amd.image import ChannelImage, IllumstatsContainer, IllumstatsImage
     from tmlibrary_amd.metadata import ChannelImageMetadata, IllumstatsImageMetadata
@@ -503,10 +538,12 @@ def test_run_job_end_to_end(L, tmp_path):
     assert np.allclose(cont.mean.array, orc.smooth_reflect(g["mean"]), rtol=1e-9, atol=1e-12)
 
 
-def _fused_job(L, sites, clip=(-1, -1), q=None, tail=1):
+def _fused_job(L, sites, clip=(-1, -1), q=None, epochs=4):
     """Split pipeline through the C-ABI: Welford-only update -> finalize ->
     smooth -> corrector -> fused correct+histogram.  Returns host results.
-    tail: TMH_OPT_PCT_TAIL (1: compact CDF + fold, 0: per-site order statistics)."""
+    epochs: TMH_OPT_FUSED_EPOCHS (>= 1: the order statistics are written by the
+    fused pass itself over that many epochs of its unit sweep; 0: by a
+    separate finalize kernel after it)."""
     from tmlibrary_amd import hip
     from tmlibrary_amd.image import ZERO_LOG10
     from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
@@ -519,7 +556,7 @@ def _fused_job(L, sites, clip=(-1, -1), q=None, tail=1):
     h = C.c_void_p()
     hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
                                  hip.ptr(lut), 4, hip.TMH_STATS_KEEP_SITE_HIST, C.byref(h)))
-    hip.check(L.tmh_stats_set_option(h, hip.TMH_OPT_PCT_TAIL, tail))
+    hip.check(L.tmh_stats_set_option(h, hip.TMH_OPT_FUSED_EPOCHS, epochs))
     d_in, d_out = Dev(L, sites.nbytes), Dev(L, sites.nbytes)
     d_in.put(sites)
     planes = [Dev(L, npx * 8) for _ in range(5)]
@@ -557,13 +594,13 @@ def _fused_job(L, sites, clip=(-1, -1), q=None, tail=1):
     return res
 
 
-@pytest.mark.parametrize("tail", [1, 0])
+@pytest.mark.parametrize("epochs", [4, 0, 1])
 @pytest.mark.parametrize("kind", ["synth", "extremes", "uniform", "tiny", "many", "saturated",
                                   "constant", "two_values"])
-def test_fused_correct_hist_pipeline(L, kind, tail):
-    """The fused pass with both percentile tails: the compact-CDF fold
-    (one-bin sites, Q > pixel count, sparse tails, the very wide path of the
-    uniform case) and the order-statistics tail, each bit-exact."""
+def test_fused_correct_hist_pipeline(L, kind, epochs):
+    """The fused pass with its in-pass finalize (4 epochs, 1 epoch) and with
+    the separate finalize kernel (0): one-bin sites, Q > pixel count, sparse
+    tails, the very wide path of the uniform case, each bit-exact."""
     from tmlibrary_amd.synth import synth_exact_sites_host, synth_sites_host
     rng = np.random.default_rng(97)
     if kind == "saturated":  # corrected values far above 2**16 (f64 refinement, common.h)
@@ -588,7 +625,7 @@ def test_fused_correct_hist_pipeline(L, kind, tail):
                           for _ in range(5)])
     else:
         sites = np.stack(load_golden("stats_extremes")["sites"])
-    r = _fused_job(L, sites, tail=tail)
+    r = _fused_job(L, sites, epochs=epochs)
     ref = orc.run_illumstats(list(sites))
     assert r["n"] == len(sites)
     assert_close_rel(r["mean"], ref.mean)

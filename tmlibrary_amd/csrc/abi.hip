@@ -243,7 +243,7 @@ struct tmh_stats {
   hipEvent_t ev_in = nullptr, ev_out = nullptr;  // ordering against a caller's stream
   int fused_cfg = kFusedAuto;     // TMH_OPT_FUSED_CONFIG (-1: per launch, on the device)
   int wf_parts = 0;               // TMH_OPT_WELFORD_PARTS (0: automatic)
-  int tail_chunks = 1;            // TMH_OPT_TAIL_CHUNKS (1: no overlap)
+  int fused_epochs = kFusedEpochsDefault;  // TMH_OPT_FUSED_EPOCHS (0: finalize after the pass)
   HostOpts host;                  // TMH_OPT_COPY_THREADS / TMH_OPT_HOST_STAGING
   bool hist_dirty = false;        // a fused launch may have left counts / round masks behind
   int64_t n = 0;              // sites accumulated (Welford count)
@@ -263,13 +263,7 @@ struct tmh_stats {
   QPos qp{};
   DBuf<uint16_t> stage;  // two device slots of batch_cap sites
   HostPipe pipe;
-  DBuf<uint2> cdf;        // fold tail: per-site compact CDFs (cdf_ld entries per site)
-  DBuf<int32_t> fbounds, fnnz;  // fold tail: chunk bounds [chunk][site], entries per site
-  int64_t fb_cap = 0;           // fold tail: sites per row of fbounds
-  bool fold = false;      // percentile tail by compact CDF + fold (TMH_OPT_PCT_TAIL)
-  bool last_fold = false; // the last fused launch took the fold tail (unless very wide)
-  unsigned long long last_xthr = ~0ull;  // its very-wide threshold
-  DBuf<unsigned long long> last_wide;    // its (wide, very wide) group counts
+  DBuf<int> gdone;  // fused pass, in-pass finalize: zero-maintained band counters per site group
   DBuf<uint32_t> vlh;  // order statistics (previous | next << 16), quantile-tiled (common.h)
   int64_t vlh_cap = 0;   // deferred mode: sites the tiles have room for
   int64_t vlh_ld = 0;    // tile stride in sites of the current contents
@@ -484,13 +478,9 @@ int tmh_stats_set_option(tmh_stats* h, int option, int value) {
         TMH_CHECK(value >= 0 && value <= 4, TMH_EINVAL, "Welford parts must be 0..4");
         h->wf_parts = value;
         break;
-      case TMH_OPT_TAIL_CHUNKS:
-        TMH_CHECK(value >= 1 && value <= 16, TMH_EINVAL, "tail chunks must be 1..16");
-        h->tail_chunks = value;
-        break;
-      case TMH_OPT_PCT_TAIL:
-        TMH_CHECK(value == 0 || value == 1, TMH_EINVAL, "percentile tail must be 0 or 1");
-        h->fold = value == 1;
+      case TMH_OPT_FUSED_EPOCHS:
+        TMH_CHECK(value >= 0 && value <= 64, TMH_EINVAL, "fused epochs must be 0..64");
+        h->fused_epochs = value;
         break;
       default:
         if (!h->host.set(option, value)) throw Error{TMH_EINVAL, "unknown option"};
@@ -508,6 +498,7 @@ int tmh_stats_reset(tmh_stats* h) {
       if (h->hist_rmask.n)
         TMH_HIP(hipMemsetAsync(h->hist_rmask.p, 0, h->hist_rmask.n * 8, h->stream));
       TMH_HIP(hipMemsetAsync(h->pooled_parts.p, 0, h->pooled_parts.n * 8, h->stream));
+      if (h->gdone.n) TMH_HIP(hipMemsetAsync(h->gdone.p, 0, h->gdone.n * 4, h->stream));
       h->hist_dirty = false;
     }
     TMH_HIP(hipMemsetAsync(h->mean.p, 0, h->npx * 8, h->stream));
@@ -550,7 +541,6 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
     const bool deferred = (h->flags & TMH_STATS_DEFERRED_PCT) != 0;
     uint32_t* vlh = h->vlh.p + (deferred ? (size_t)h->n_deferred * kOsTile : 0);
     const int64_t ld = deferred ? h->vlh_cap : nc;
-    h->last_fold = false;
     launch_hist_scatter(d + c0 * h->npx, h->npx, nc, h->hist_hi.p, h->qp, vlh, ld, h->pooled.p,
                         h->zeros.p, (h->flags & 2u) ? h->site_hist.p : nullptr, hs);
     if (deferred)
@@ -773,35 +763,6 @@ int tmh_stats_site_order_stats(tmh_stats* h, int64_t site, uint16_t* host_vlo, u
     const bool deferred = h->flags & TMH_STATS_DEFERRED_PCT;
     const int64_t avail = deferred ? h->n_deferred : h->last_batch;
     TMH_CHECK(site >= 0 && site < avail, TMH_EINVAL, "site not available");
-    if (!deferred && h->last_fold) {
-      unsigned long long wc[2] = {0, 0};
-      TMH_HIP(hipStreamSynchronize(h->stream));
-      TMH_HIP(hipMemcpy(wc, h->last_wide.p, 16, hipMemcpyDeviceToHost));
-      if (wc[1] < h->last_xthr) {
-        // the fold tail kept the site's compact CDF, not its order statistics:
-        // (previous, next) value at every quantile's positions from it
-        int32_t nz = 0;
-        TMH_HIP(hipMemcpy(&nz, h->fnnz.p + site, 4, hipMemcpyDeviceToHost));
-        const int64_t cdf_ld = std::min<int64_t>(kBins, h->npx);
-        std::vector<uint2> e((size_t)nz);
-        TMH_HIP(hipMemcpy(e.data(), h->cdf.p + (size_t)site * cdf_ld, (size_t)nz * 8,
-                          hipMemcpyDeviceToHost));
-        std::vector<int32_t> lo(h->Q), hi(h->Q);
-        TMH_HIP(hipMemcpy(lo.data(), h->q_lo.p, (size_t)h->Q * 4, hipMemcpyDeviceToHost));
-        TMH_HIP(hipMemcpy(hi.data(), h->q_hi.p, (size_t)h->Q * 4, hipMemcpyDeviceToHost));
-        auto value_at = [&](int32_t pos) -> uint16_t {  // first entry with rank > pos
-          const auto it = std::upper_bound(e.begin(), e.end(), (uint32_t)pos,
-                                           [](uint32_t v, const uint2& x) { return v < x.x; });
-          TMH_CHECK(it != e.end(), TMH_EDEVICE, "compact CDF does not cover the position");
-          return (uint16_t)it->y;
-        };
-        for (int64_t q = 0; q < h->Q; ++q) {
-          host_vlo[q] = value_at(lo[q]);
-          host_vhi[q] = value_at(hi[q]);
-        }
-        return;
-      }
-    }
     // one site's column of every quantile tile
     const size_t row = (size_t)kOsTile * 4;
     std::vector<uint32_t> w((size_t)os_tiles(h->Q) * kOsTile);
@@ -1282,36 +1243,6 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
       // fills them and k_hist_finalize resets what it read; if anything fails
       // in between, tmh_stats_reset clears them (hist_dirty)
       h->hist_dirty = true;
-      // Tail overlap (TMH_OPT_TAIL_CHUNKS = C > 1): the fused pass runs in C
-      // site chunks on s; chunk k's histogram finalize runs on the side
-      // stream in its narrow (256-thread) form, which fits beside the fused
-      // pass's workgroups on a CU, while chunk k+1 streams.  The last chunk's
-      // finalize runs on the whole GPU after both.  Chunks keep site order,
-      // so the ordered percentile sum at the end is unchanged.
-      // (a blocked layout runs as one chunk)
-      const int nch = tab.in ? 1
-                             : (int)std::min<int64_t>(h->tail_chunks,
-                                                      n_sites / 64 > 0 ? n_sites / 64 : 1);
-      // percentile tail: compact CDF + in-order fold (no per-site order
-      // statistics through HBM) for one-chunk, non-deferred launches
-      const bool fold = h->fold && nch == 1 && !(h->flags & TMH_STATS_DEFERRED_PCT) &&
-                        h->qp.hi_next;
-      const int64_t cdf_ld = std::min<int64_t>(kBins, h->npx);
-      if (fold) {
-        const size_t nb = (size_t)fold_chunks_host(h->Q);
-        const bool fgrow = (size_t)n_sites * cdf_ld > h->cdf.n || n_sites > h->fb_cap ||
-                           (size_t)n_sites > h->fnnz.n;
-        if (fgrow) {  // growing frees buffers earlier launches may still be using
-          TMH_HIP(hipStreamSynchronize(s));
-          TMH_HIP(hipStreamSynchronize(h->stream));
-        }
-        h->cdf.ensure((size_t)n_sites * cdf_ld);
-        if (n_sites > h->fb_cap) {  // bounds: [chunk][site], row stride fb_cap
-          h->fbounds.alloc(nb * (size_t)n_sites);
-          h->fb_cap = n_sites;
-        }
-        h->fnnz.ensure((size_t)n_sites);
-      }
       uint32_t* sh = (h->flags & 2u) ? h->site_hist.p : nullptr;
       // the wide configuration pays off once a few % of the pixel groups
       // overflow the narrow slices (their values then take global atomics)
@@ -1324,66 +1255,46 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
           autocfg ? (unsigned long long)std::max<double>(
                         1.0, kXWideFrac * (double)h->wide_sites * (double)(h->npx >> 3))
                   : ~0ull;
-      if (nch > 1) {
-        TMH_HIP(hipEventRecord(h->ev_fork, s));
-        TMH_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
-      }
-      for (int k = 0; k < nch; ++k) {
-        const int64_t c0 = n_sites * k / nch, nc = n_sites * (k + 1) / nch - c0;
-        const FixList fl = corrector_fixlist(c, nc, s);
-        launch_correct_hist(dev_in + c0 * h->npx, dev_out + c0 * h->npx, c->npx, nc, c->coef2.p,
-                            c->mconst2.p, fl, c->log_transform, clip_lo, clip_hi,
-                            h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0,
-                            c->queues.p, c->n_wg, h->fused_cfg, h->wide.p, wide_thresh,
-                            xwide_thresh, s, tab);
-        launch_fix_correct(dev_in + c0 * h->npx, dev_out + c0 * h->npx, 2, c->npx, nc, fl,
-                           c->coef64.p, c->rc.p, c->log_transform, clip_lo, clip_hi, s, tab);
-        const bool side = k < nch - 1;
-        hipStream_t fs = side ? h->side : s;
-        if (side) {
-          TMH_HIP(hipEventRecord(h->ev_fork, s));
-          TMH_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
-        } else if (nch > 1) {
-          TMH_HIP(hipEventRecord(h->ev_join, h->side));
-          TMH_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
+      // in-pass finalize (fused_kernels.hip): the order statistics are
+      // written inside the streaming pass; the pooled column sum then reads
+      // and zeroes the counts.  TMH_OPT_FUSED_EPOCHS = 0: k_hist_finalize after it.
+      InPassFin fin;
+      const int E = h->fused_epochs;
+      if (E > 0) {
+        if ((size_t)n_sites + 1 > h->gdone.n) {
+          TMH_HIP(hipStreamSynchronize(s));
+          h->gdone.alloc((size_t)n_sites + 1, true);
         }
-        if (autocfg)  // exits at once unless the launch is very wide
-          launch_hist_site_u16(dev_in + c0 * h->npx, h->npx, nc, h->hist_full.p + (size_t)c0 * kBins,
-                               h->qp, vlh + (size_t)c0 * kOsTile, ld, h->pooled.p,
-                               h->pooled_parts.p, kPooledParts, h->zeros.p + c0,
-                               sh ? sh + (size_t)c0 * kBins : nullptr, h->wide.p, xwide_thresh, fs,
-                               tab);
-        if (fold) {  // (one chunk: the fused launch's round union is current)
-          ProfScope prof("pct_tail", s);
-          launch_pooled_colsum(h->hist_full.p, h->hist_rmask.p,
-                               reinterpret_cast<const unsigned long long*>(c->queues.p + 8),
-                               n_sites, h->pooled.p, s);
-          launch_pct_fold(h->hist_full.p, h->hist_rmask.p, n_sites, h->qp, h->cdf.p, cdf_ld,
-                          h->fbounds.p, h->fb_cap, h->fnnz.p, vlh, ld, h->zeros.p, sh, h->gamma.p,
-                          h->acc.p, h->wide.p, xwide_thresh, s);
-          continue;
-        }
-        launch_hist_finalize(h->hist_full.p + (size_t)c0 * kBins, h->hist_rmask.p + c0, 0, nc,
-                             h->qp, vlh + (size_t)c0 * kOsTile, ld, h->pooled.p, h->pooled_parts.p,
-                             kPooledParts, h->zeros.p + c0, sh ? sh + (size_t)c0 * kBins : nullptr,
-                             fs, side,
-                             // the launch-wide round union is rewritten by the
-                             // next chunk's fused launch: one chunk only
-                             nch == 1 ? reinterpret_cast<const unsigned long long*>(c->queues.p + 8)
-                                      : nullptr,
-                             h->wide.p, xwide_thresh);
+        fin.p = h->qp;
+        fin.p.tstride = ld * kOsTile;
+        fin.vlh = vlh;
+        fin.gdone = h->gdone.p;
+        fin.zero_counts = h->zeros.p;
+        fin.site_hist = sh;
+        fin.epoch_sites = (int)std::min<int64_t>(n_sites, (n_sites + E - 1) / E);
       }
-      h->last_fold = fold;
-      if (fold) {  // a very wide launch's order statistics (k_hist_site_u16) only
-        launch_pct_accumulate_range(vlh, n_sites, ld, 0, h->Q, h->gamma.p, h->acc.p, s, h->wide.p,
-                                    xwide_thresh);
-        // which tail ran is decided on the device: keep the counts for the
-        // debug accessor tmh_stats_site_order_stats
-        if (!h->last_wide.n) h->last_wide.alloc(2);
-        TMH_HIP(hipMemcpyAsync(h->last_wide.p, h->wide.p, 16, hipMemcpyDeviceToDevice, s));
-        h->last_xthr = xwide_thresh;
+      const unsigned long long* rm_all = reinterpret_cast<const unsigned long long*>(c->queues.p + 8);
+      const FixList fl = corrector_fixlist(c, n_sites, s);
+      launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p, fl,
+                          c->log_transform, clip_lo, clip_hi, h->hist_full.p, h->hist_rmask.p,
+                          c->queues.p, c->n_wg, h->fused_cfg, h->wide.p, wide_thresh, xwide_thresh,
+                          s, tab, fin);
+      launch_fix_correct(dev_in, dev_out, 2, c->npx, n_sites, fl, c->coef64.p, c->rc.p,
+                         c->log_transform, clip_lo, clip_hi, s, tab);
+      if (autocfg)  // exits at once unless the launch is very wide
+        launch_hist_site_u16(dev_in, h->npx, n_sites, h->hist_full.p, h->qp, vlh, ld, h->pooled.p,
+                             h->pooled_parts.p, kPooledParts, h->zeros.p, sh, h->wide.p,
+                             xwide_thresh, s, tab);
+      if (E > 0) {
+        launch_pooled_colsum(h->hist_full.p, h->hist_rmask.p, rm_all, n_sites, h->pooled.p, s,
+                             true);
+        TMH_HIP(hipMemsetAsync(h->hist_rmask.p, 0, (size_t)n_sites * 8, s));
+      } else {
+        launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, n_sites, h->qp, vlh, ld,
+                             h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, sh, s,
+                             false, rm_all, h->wide.p, xwide_thresh);
       }
-      else if (!(h->flags & TMH_STATS_DEFERRED_PCT))
+      if (!(h->flags & TMH_STATS_DEFERRED_PCT))
         launch_pct_accumulate(vlh, n_sites, ld, h->Q, h->gamma.p, h->acc.p, s);
       h->hist_dirty = false;
       if (h->flags & TMH_STATS_DEFERRED_PCT) h->n_deferred += n_sites;
@@ -1433,7 +1344,6 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
                          c->log_transform, clip_lo, clip_hi, s);
       launch_fix_correct(din, dout, 2, c->npx, nc, fl, c->coef64.p, c->rc.p, c->log_transform,
                          clip_lo, clip_hi, s);
-      h->last_fold = false;
       launch_hist_scatter(din, h->npx, nc, h->hist_hi.p, h->qp, vlh, ld, h->pooled.p, h->zeros.p,
                           (h->flags & 2u) ? h->site_hist.p : nullptr, s);
       if (h->flags & TMH_STATS_DEFERRED_PCT)

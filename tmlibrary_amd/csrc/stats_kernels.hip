@@ -22,6 +22,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "hist_tail.h"
 
 namespace tmh {
 
@@ -588,169 +589,6 @@ __device__ __forceinline__ void count8(const uint4 v, uint32_t* bins, uint32_t* 
   }
 }
 
-// Exclusive scan of one value per thread over an NT-thread workgroup.
-// `slots` holds 2 x 16 wave totals (double-buffered by the parity of the
-// caller's scan counter, so one barrier per scan suffices).  Returns the
-// exclusive prefix; *total = sum.
-template <int NT>
-__device__ __forceinline__ uint32_t block_exscan_t(uint32_t c, uint32_t* slots, int round,
-                                                   uint32_t* total) {
-  static_assert(NT % 64 == 0 && NT <= 1024, "whole waves, at most 16");
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t incl = c;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += y;
-  }
-  uint32_t* ws = slots + (round & 1) * 16;
-  if (lane == 63) ws[wid] = incl;
-  __syncthreads();
-  uint32_t woff = 0, all = 0;
-#pragma unroll
-  for (int w = 0; w < NT / 64; ++w) {
-    const uint32_t t = ws[w];
-    woff += (w < wid) ? t : 0u;
-    all += t;
-  }
-  *total = all;
-  return woff + incl - c;
-}
-
-__device__ __forceinline__ uint32_t block_exscan(uint32_t c, uint32_t* slots, int round,
-                                                 uint32_t* total) {
-  return block_exscan_t<kHistThreads>(c, slots, round, total);
-}
-
-constexpr int kRound = 1024;  // histogram bins per round of the scans
-
-constexpr int kTailChunkDefault = 8;  // rounds whose counts are loaded together
-// Advance (t, Rt = R[t]) to the first index >= t with R[index] > x (R: LEN
-// non-decreasing inclusive prefix ranks in LDS; the caller guarantees
-// R[t - 1] <= x < R[LEN - 1]).  Consecutive quantile positions mostly stay in
-// one bin (no LDS read: Rt is cached) or step to the next (one read); the
-// rest finish with a binary search over (t+1, 1023].
-template <int LEN = kRound>
-__device__ __forceinline__ void advance_rank(const int32_t* R, int& t, int32_t& Rt, int32_t x) {
-  if (Rt > x) return;
-  const int32_t r1 = R[t + 1];
-  if (r1 > x) {
-    ++t;
-    Rt = r1;
-    return;
-  }
-  int lo = t + 1, hi = LEN - 1;  // R[lo] <= x < R[hi]
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (R[mid] > x)
-      hi = mid;
-    else
-      lo = mid;
-  }
-  t = hi;
-  Rt = R[hi];
-}
-
-// One round's order statistics.  R[t] = inclusive prefix rank of the round's
-// bin t (value bin0 + t); the round owns the sorted positions [r0, r1).
-// Quantile-centric: each thread takes groups of 8 quantiles, reads their
-// previous positions from the (L2-resident) table -- the next group's
-// positions are loaded while the current group is resolved -- keeps the ones
-// inside [r0, r1), and finds each owning bin by advancing through R from the
-// previous quantile's bin (one binary search per group).  The next position
-// is min(prev + 1, n - 1) for every q in [0, 100] (np.percentile 'linear'):
-// when it is still inside the previous statistic's bin (R[bin] > prev + 1,
-// nearly always) the next statistic is the same value and needs no search; a
-// general next table is read only if the caller's differs.  Each group is
-// written as one 32-B store of interleaved (previous, next) values (2-B
-// stores where a group straddles the round's ends).  The round's quantile
-// range is [r0 * scale, r1 * scale] up to rounding (and one position's worth
-// of quantiles), so the groups scanned carry a margin and the position test
-// decides membership exactly.
-template <int NT = kHistThreads, int LEN = kRound>
-__device__ __forceinline__ void fill_groups(const int32_t* R, int64_t r0, int64_t r1,
-                                            uint32_t bin0, const QPos& p,
-                                            uint32_t* __restrict__ vlh, bool vec16) {
-  const int64_t m = (int64_t)p.scale + 3;  // scale > 1 when Q exceeds the pixel count
-  int64_t qa = (int64_t)((double)r0 * p.scale) - m;
-  int64_t qb = (int64_t)((double)r1 * p.scale) + m;
-  qa = qa < 0 ? 0 : qa;
-  qb = qb > p.Q ? p.Q : qb;
-  if (qa >= qb) return;
-  const int64_t g0 = qa >> 3, g1 = (qb - 1) >> 3;
-  const bool tab16 = vec16;  // tables are 16-B aligned rows when Q % 8 == 0 (hipMalloc base)
-  const int32_t a = (int32_t)r0, b = (int32_t)r1;
-  auto positions = [&](int64_t q0, int32_t (&pl)[8]) {
-    if (tab16 && q0 + 8 <= p.Q) {
-      const int4 a0 = reinterpret_cast<const int4*>(p.lo + q0)[0];
-      const int4 a1 = reinterpret_cast<const int4*>(p.lo + q0)[1];
-      pl[0] = a0.x; pl[1] = a0.y; pl[2] = a0.z; pl[3] = a0.w;
-      pl[4] = a1.x; pl[5] = a1.y; pl[6] = a1.z; pl[7] = a1.w;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pl[j] = q0 + j < p.Q ? p.lo[q0 + j] : INT32_MAX;
-    }
-  };
-  int64_t g = g0 + (int64_t)threadIdx.x;
-  int32_t pn[8];
-  if (g <= g1) positions(g << 3, pn);
-  for (; g <= g1; g += NT) {
-    const int64_t q0 = g << 3;
-    int32_t pl[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) pl[j] = pn[j];
-    if (g + NT <= g1) positions((g + NT) << 3, pn);  // in flight while this group resolves
-    int tl = 0, th = 0;
-    int32_t Rl = R[0], Rh = Rl;
-    uint32_t ol[4] = {0u, 0u, 0u, 0u}, oh[4] = {0u, 0u, 0u, 0u};
-    uint32_t ml = 0, mh = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int32_t pj = pl[j];
-      const bool mine = pj >= a && pj < b;
-      if (mine) {
-        advance_rank<LEN>(R, tl, Rl, pj);
-        ol[j >> 1] |= (bin0 + (uint32_t)tl) << (16 * (j & 1));
-        ml |= 1u << j;
-      }
-      const int32_t hj = p.hi_next ? (pj < p.last ? pj + 1 : pj)
-                                   : (q0 + j < p.Q ? p.hi[q0 + j] : INT32_MAX);
-      if (p.hi_next && mine && hj < Rl) {  // next position in the same bin
-        oh[j >> 1] |= (bin0 + (uint32_t)tl) << (16 * (j & 1));
-        mh |= 1u << j;
-      } else if (hj >= a && hj < b) {
-        if (th < tl) {
-          th = tl;
-          Rh = Rl;
-        }
-        advance_rank<LEN>(R, th, Rh, hj);
-        oh[j >> 1] |= (bin0 + (uint32_t)th) << (16 * (j & 1));
-        mh |= 1u << j;
-      }
-    }
-    // interleaved (previous, next) order statistics: one u32 per quantile,
-    // a group of 8 is contiguous inside one quantile tile
-    uint32_t* og = vlh + (q0 / kOsTile) * p.tstride + (q0 % kOsTile);
-    if (vec16 && ml == 0xFFu && mh == 0xFFu) {
-      uint4* dst = reinterpret_cast<uint4*>(og);
-      dst[0] = make_uint4(__builtin_amdgcn_perm(oh[0], ol[0], 0x05040100u),
-                          __builtin_amdgcn_perm(oh[0], ol[0], 0x07060302u),
-                          __builtin_amdgcn_perm(oh[1], ol[1], 0x05040100u),
-                          __builtin_amdgcn_perm(oh[1], ol[1], 0x07060302u));
-      dst[1] = make_uint4(__builtin_amdgcn_perm(oh[2], ol[2], 0x05040100u),
-                          __builtin_amdgcn_perm(oh[2], ol[2], 0x07060302u),
-                          __builtin_amdgcn_perm(oh[3], ol[3], 0x05040100u),
-                          __builtin_amdgcn_perm(oh[3], ol[3], 0x07060302u));
-    } else if (ml | mh) {  // a round edge: write the halves this round owns
-      uint16_t* h16 = reinterpret_cast<uint16_t*>(og);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if ((ml >> j) & 1u) h16[2 * j] = (uint16_t)(ol[j >> 1] >> (16 * (j & 1)));
-        if ((mh >> j) & 1u) h16[2 * j + 1] = (uint16_t)(oh[j >> 1] >> (16 * (j & 1)));
-      }
-    }
-  }
-}
 
 // Walk the 65,536 bins in 64 rounds of 1024 consecutive bins, thread t
 // owning bin 1024*j + t: reads are conflict-free/coalesced, and the dense part
@@ -821,91 +659,6 @@ __device__ __forceinline__ void hist_tail(CountFn count, DoneFn done, int64_t s,
   }
 }
 
-// hist_tail for a histogram whose possibly non-empty 1,024-bin rounds are
-// known up front (need: bit j = round j): only those rounds are loaded, and
-// they are scanned SR rounds at a time (a super-round of SR * 1,024 bins: one
-// block scan and one rank table per super-round that holds any needed round,
-// bins of the rounds not needed taken as 0 without a load) -- BPT = SR *
-// 1024 / NT consecutive bins per thread, the next super-round's counts in
-// flight while the current one is scanned -- instead of walking all 64
-// rounds.  Same outputs as hist_tail (site_hist rows are zero-filled for the
-// rounds not visited).  NT = 256, SR = 1 is the narrow form that fits beside
-// the fused pass's workgroups on a CU.  starts: 2 * SR * 1024 int32 of LDS.
-template <int ABL, int NT, int SR, typename CountFn, typename DoneFn>
-__device__ __forceinline__ void hist_tail_rounds(unsigned long long need, CountFn count,
-                                                 DoneFn done, int64_t s, const QPos& p,
-                                                 uint32_t* __restrict__ vlh_all,
-                                                 unsigned long long* __restrict__ pooled,
-                                                 int64_t* __restrict__ zero_counts,
-                                                 uint32_t* __restrict__ site_hist,
-                                                 uint32_t* slots, int32_t* starts) {
-  constexpr int LEN = SR * kRound;
-  constexpr int BPT = LEN / NT;
-  static_assert(BPT >= 1 && kRound % BPT == 0, "a thread's bins lie inside one round");
-  const int tid = threadIdx.x;
-  uint32_t* vlh = vlh_all + s * (int64_t)kOsTile;  // this site's column of the tiles
-  const bool vec16 = (p.Q & 7) == 0;
-  if (site_hist) {  // debug/parity copy: the rounds not visited are empty
-    for (int j = 0; j < kBins / kRound; ++j)
-      if (!((need >> j) & 1ull))
-        for (int i = tid; i < kRound; i += NT) site_hist[s * kBins + (uint32_t)(j * kRound + i)] = 0u;
-  }
-  unsigned long long sneed = 0ull;  // super-rounds holding a needed round
-#pragma unroll
-  for (int k = 0; k < kBins / LEN; ++k)
-    if ((need >> (k * SR)) & ((SR == 64 ? 0ull : (1ull << SR)) - 1ull)) sneed |= 1ull << k;
-  // bin 0 lies in super-round 0: a site whose masks skip it has no zeros
-  if (zero_counts && tid == 0 && !(sneed & 1ull)) zero_counts[s] = 0;
-  // this thread's bins lie in round (k * SR + tid * BPT / kRound) of super-round k
-  auto load = [&](int k, uint32_t (&c)[BPT]) {
-    const uint32_t b0 = (uint32_t)k * LEN + tid * BPT;
-    const bool live = (need >> (b0 / kRound)) & 1ull;
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) c[i] = live ? count(b0 + i) : 0u;
-  };
-  int64_t base = 0;  // exclusive rank of the current super-round's first bin
-  int nscan = 0;
-  uint32_t cn[BPT];
-  if (sneed) load(__builtin_ctzll(sneed), cn);
-  while (sneed) {
-    const int k = __builtin_ctzll(sneed);
-    sneed &= sneed - 1ull;
-    uint32_t c[BPT], inc[BPT];
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) c[i] = cn[i];
-    if (sneed) load(__builtin_ctzll(sneed), cn);
-    const uint32_t b0 = (uint32_t)k * LEN + tid * BPT;
-    const bool live = (need >> (b0 / kRound)) & 1ull;
-    uint32_t run = 0;
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) {
-      run += c[i];
-      inc[i] = run;  // inclusive prefix inside the thread's bins
-      const uint32_t b = b0 + i;
-      if (live) {
-        if (site_hist) site_hist[s * kBins + b] = c[i];
-        done(b, c[i]);
-      }
-      if (b == 0 && zero_counts) zero_counts[s] = c[i];
-    }
-    uint32_t total;
-    // slots and R are double-buffered by scan parity: every scan flips it
-    const int64_t r = base + block_exscan_t<NT>(run, slots, nscan, &total);
-    int32_t* R = starts + (nscan & 1) * LEN;
-    ++nscan;
-    if (total == 0) continue;  // uniform: an empty super-round
-    const int64_t r0 = base;
-    base += total;
-#pragma unroll
-    for (int i = 0; i < BPT; ++i)
-      if (c[i] && !(ABL & 4) && pooled) atomicAdd(&pooled[b0 + i], (unsigned long long)c[i]);
-    if (ABL & 1) continue;
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) R[tid * BPT + i] = (int32_t)(r + inc[i]);
-    __syncthreads();  // R visible; the other R buffer is rewritten only after the next scan
-    fill_groups<NT, LEN>(R, r0, base, (uint32_t)k * LEN, p, vlh, vec16);
-  }
-}
 
 __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
     const uint16_t* __restrict__ sites, int64_t npx, int vec, uint32_t* __restrict__ hist_hi,
@@ -1018,7 +771,10 @@ __global__ __launch_bounds__(NT, 8) void k_hist_finalize(
 // this replaced ~30,000 per-site atomics per site in the finalize (1.2 ms of
 // its 2.4 ms at 3,456 sites: profiles/r2/mb_tail_bright_r2y.txt).
 constexpr int kColSites = 32;
-__global__ __launch_bounds__(256) void k_pooled_colsum(const uint32_t* __restrict__ hist,
+// RESET (the fused pass's in-pass finalize has already read the counts): the
+// counts read are also zeroed -- the slab is zero-maintained.
+template <bool RESET>
+__global__ __launch_bounds__(256) void k_pooled_colsum(uint32_t* __restrict__ hist,
                                                        const unsigned long long* __restrict__ rmask,
                                                        const unsigned long long* __restrict__ rm_all,
                                                        int64_t n_sites,
@@ -1041,11 +797,16 @@ __global__ __launch_bounds__(256) void k_pooled_colsum(const uint32_t* __restric
   }
   __syncthreads();
   if (!any) return;  // uniform: no site of the chunk uses this round
-  const uint32_t* h = hist + s0 * kBins + b;
+  uint32_t* h = hist + s0 * kBins + b;
   unsigned long long t = 0;
 #pragma unroll 16
-  for (int s = 0; s < ns; ++s)
-    if (use[s]) t += h[(int64_t)s * kBins];
+  for (int s = 0; s < ns; ++s) {
+    if (use[s]) {
+      const uint32_t c = h[(int64_t)s * kBins];
+      t += c;
+      if (RESET && c) h[(int64_t)s * kBins] = 0u;
+    }
+  }
   if (t) atomicAdd(&pooled[b], t);
 }
 
@@ -1065,12 +826,18 @@ __global__ void k_pooled_fold(unsigned long long* __restrict__ pooled,
   pooled[b] += t;
 }
 
-void launch_pooled_colsum(const uint32_t* hist, const unsigned long long* rmask,
+void launch_pooled_colsum(uint32_t* hist, const unsigned long long* rmask,
                           const unsigned long long* rm_all, int64_t n_sites,
-                          unsigned long long* pooled, hipStream_t s) {
+                          unsigned long long* pooled, hipStream_t s, bool reset) {
   if (n_sites <= 0) return;
-  hipLaunchKernelGGL(k_pooled_colsum, dim3(kBins / 256, (unsigned)cdiv(n_sites, kColSites)),
-                     dim3(256), 0, s, hist, rmask, rm_all, n_sites, pooled);
+  ProfScope prof("colsum", s);
+  const dim3 grid(kBins / 256, (unsigned)cdiv(n_sites, kColSites));
+  if (reset)
+    hipLaunchKernelGGL(k_pooled_colsum<true>, grid, dim3(256), 0, s, hist, rmask, rm_all, n_sites,
+                       pooled);
+  else
+    hipLaunchKernelGGL(k_pooled_colsum<false>, grid, dim3(256), 0, s, hist, rmask, rm_all,
+                       n_sites, pooled);
   TMH_HIP(hipGetLastError());
 }
 
@@ -1089,7 +856,7 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
   // finalize; without one, the finalize adds into pooled copies, then folded
   const bool colsum = rmask != nullptr && dense_rounds == 0;
   if (colsum)
-    hipLaunchKernelGGL(k_pooled_colsum, dim3(kBins / 256, (unsigned)cdiv(n_sites, kColSites)),
+    hipLaunchKernelGGL(k_pooled_colsum<false>, dim3(kBins / 256, (unsigned)cdiv(n_sites, kColSites)),
                        dim3(256), 0, s, hist, rmask, rm_all, n_sites, pooled);
   unsigned long long* fin_pooled = colsum ? nullptr : pooled_parts;
   if (narrow)
@@ -1335,397 +1102,6 @@ void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t v
 }
 
 // ---------------------------------------------------------------------------
-// percentile tail without per-site order statistics (the fold)
-// ---------------------------------------------------------------------------
-// The per-quantile order statistics of every site (Q x 4 B = 400 KB per site,
-// 1.38 GB for a 3,456-site job) were written by the histogram finalize and
-// read back by k_pct_acc: ~0.8 ms of a 21 ms job spent moving them through
-// HBM twice.  A site's histogram holds the same information in far fewer
-// bytes: its non-empty bins with their cumulative counts -- the compact CDF,
-// ~6,000 entries x 8 B on microscopy data.  So:
-//   k_cdf_compact  (one workgroup per site) scans the flagged rounds of the
-//                  site's zero-maintained histogram slab once (resetting them,
-//                  as k_hist_finalize did), writes the compact CDF -- entry k =
-//                  (inclusive rank, value) of the k-th non-empty bin -- and,
-//                  for every quantile chunk c, the index of the entry holding
-//                  the chunk's first previous position lo[c * kFoldQC];
-//   k_pct_fold2    (one workgroup per chunk of kFoldQC quantiles) walks the
-//                  sites IN ORDER: wave w of round r resolves site
-//                  kFoldWaves r + w's previous / next values for the chunk's
-//                  quantiles from the entries between its two chunk bounds
-//                  (one window of up to kFoldWin entries; the rare wider spans
-//                  were resolved by k_fold_heavy), and the chunk's accumulator
-//                  threads add the round's sites in site order -- the same f64
-//                  adds, without contraction, in the same order as k_pct_acc:
-//                  bit-exact.
-// Bytes: ~0.17 GB written and read instead of 2 x 1.38 GB.  Measured on 3,456
-// standard sites (tools/mb/mb_fold.hip, profiles/r3/mb_fold_r3f.txt): compact
-// + heavy 0.17 ms, fold 1.13 ms (of which the per-quantile window searches
-// ~0.65, the window fetches and round structure ~0.34, the in-order adds
-// ~0.12) against 0.87-0.90 ms for the dense tail (finalize + k_pct_acc): the
-// search is VALU/LDS-issue-bound, so the dense tail is the default and the
-// fold an option (TMH_OPT_PCT_TAIL = 1).
-constexpr int kFoldQPL = 4;                // quantiles per lane
-constexpr int kFoldQC = 64 * kFoldQPL;     // quantiles per chunk = per fold workgroup
-constexpr int kFoldWaves = 8;              // sites per fold round (k_pct_fold2: 1.13 ms vs 1.20 with 16, 1.69 with 4)
-constexpr int kFoldWin = 256;              // compact-CDF entries one wave resolves from
-constexpr int kCdfSR = 4;                  // super-round: 4 x 1,024 bins
-constexpr int kCdfThreads = 1024;
-
-__host__ __device__ inline int fold_chunks(int Q) { return (Q + kFoldQC - 1) / kFoldQC; }
-
-__global__ __launch_bounds__(kCdfThreads) void k_cdf_compact(
-    uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask, const QPos p,
-    uint2* __restrict__ cdf, int64_t cdf_ld, int32_t* __restrict__ bounds, int64_t bounds_ld,
-    int32_t* __restrict__ nnz, int64_t* __restrict__ zero_counts,
-    uint32_t* __restrict__ site_hist, const unsigned long long* __restrict__ wide,
-    unsigned long long xthr) {
-  // a very wide launch: k_hist_site_u16 has produced this launch's order statistics
-  if (wide && __builtin_nontemporal_load(wide + 1) >= xthr) return;
-  constexpr int NT = kCdfThreads, LEN = kCdfSR * kRound, BPT = LEN / NT;
-  static_assert(BPT >= 1 && kRound % BPT == 0, "a thread's bins lie inside one round");
-  __shared__ uint32_t slots[32], slots_nz[32];
-  __shared__ int32_t R[LEN];   // inclusive rank of each bin of the super-round
-  __shared__ int32_t NZ[LEN];  // entry index of each bin (of the non-empty ones)
-  const int tid = threadIdx.x;
-  const int64_t s = blockIdx.x;
-  const unsigned long long need = rmask[s];
-  __syncthreads();
-  if (tid == 0) rmask[s] = 0ull;  // zero-maintained: every thread has read it
-  uint32_t* h = hist + s * (int64_t)kBins;
-  uint2* out = cdf + s * cdf_ld;
-  const int nb = fold_chunks(p.Q);
-  if (site_hist) {  // debug/parity copy: the rounds not visited are empty
-    for (int j = 0; j < kBins / kRound; ++j)
-      if (!((need >> j) & 1ull))
-        for (int i = tid; i < kRound; i += NT) site_hist[s * kBins + (uint32_t)(j * kRound + i)] = 0u;
-  }
-  unsigned long long sneed = 0ull;  // super-rounds holding a needed round
-#pragma unroll
-  for (int k = 0; k < kBins / LEN; ++k)
-    if ((need >> (k * kCdfSR)) & ((1ull << kCdfSR) - 1ull)) sneed |= 1ull << k;
-  if (zero_counts && tid == 0 && !(sneed & 1ull)) zero_counts[s] = 0;
-  auto load = [&](int k, uint32_t (&c)[BPT]) {
-    const uint32_t b0 = (uint32_t)k * LEN + tid * BPT;
-    const bool live = (need >> (b0 / kRound)) & 1ull;
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) c[i] = live ? h[b0 + i] : 0u;
-  };
-  int64_t base = 0;  // rank before the super-round
-  int32_t nzb = 0;   // entries before the super-round
-  int nscan = 0;
-  uint32_t cn[BPT];
-  if (sneed) load(__builtin_ctzll(sneed), cn);
-  while (sneed) {
-    const int k = __builtin_ctzll(sneed);
-    sneed &= sneed - 1ull;
-    uint32_t c[BPT], inc[BPT], nzi[BPT];
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) c[i] = cn[i];
-    if (sneed) load(__builtin_ctzll(sneed), cn);
-    const uint32_t b0 = (uint32_t)k * LEN + tid * BPT;
-    const bool live = (need >> (b0 / kRound)) & 1ull;
-    uint32_t run = 0, nzr = 0;
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) {
-      run += c[i];
-      inc[i] = run;
-      nzi[i] = nzr;
-      nzr += c[i] ? 1u : 0u;
-      const uint32_t b = b0 + i;
-      if (live) {
-        if (site_hist) site_hist[s * kBins + b] = c[i];
-        if (c[i]) h[b] = 0u;  // zero-maintained slab
-      }
-      if (b == 0 && zero_counts) zero_counts[s] = c[i];
-    }
-    uint32_t total, nz_total;
-    const int64_t r = base + block_exscan_t<NT>(run, slots, nscan, &total);
-    const int32_t e0 = nzb + (int32_t)block_exscan_t<NT>(nzr, slots_nz, nscan, &nz_total);
-    ++nscan;
-    if (total == 0) continue;  // uniform: an empty super-round
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) {
-      if (c[i]) out[e0 + nzi[i]] = make_uint2((uint32_t)(r + inc[i]), b0 + i);
-      R[tid * BPT + i] = (int32_t)(r + inc[i]);
-      NZ[tid * BPT + i] = e0 + (int32_t)nzi[i];
-    }
-    __syncthreads();  // R / NZ visible
-    const int64_t r1 = base + total;
-    for (int cc = tid; cc < nb; cc += NT) {
-      const int32_t P = p.lo[cc * kFoldQC];
-      if (P < base || P >= r1) continue;
-      int a = -1, b = LEN - 1;  // R[a] <= P < R[b] (R[LEN - 1] = r1 > P)
-      while (b - a > 1) {
-        const int m = (a + b) >> 1;
-        if (R[m] > P)
-          b = m;
-        else
-          a = m;
-      }
-      bounds[(int64_t)cc * bounds_ld + s] = NZ[b];
-    }
-    __syncthreads();  // done with R / NZ before the next super-round rewrites them
-    base = r1;
-    nzb += (int32_t)nz_total;
-  }
-  if (tid == 0) nnz[s] = nzb;
-}
-
-// Heavy chunks: a chunk whose quantile positions span more than kFoldWin
-// compact-CDF entries of a site (the sparse upper tail of microscopy sites:
-// the top 256 quantiles of a standard site span ~2,000 distinct values) would
-// make the in-order fold walk many windows per site -- latency on the fold's
-// serial path (measured: 10.4 ms for the whole fold, all of it in the top
-// chunk's workgroup).  k_fold_heavy resolves those (site, chunk) pairs up
-// front, in parallel over sites, into the quantile-tiled order statistics
-// layout (previous | next << 16, common.h): one workgroup per site, thread =
-// quantile, a binary search over the chunk's entries.  k_pct_fold then reads
-// them like k_pct_acc does.
-__global__ __launch_bounds__(kFoldQC) void k_fold_heavy(
-    const uint2* __restrict__ cdf, int64_t cdf_ld, const int32_t* __restrict__ bounds,
-    int64_t bounds_ld, const int32_t* __restrict__ nnz, const QPos p, uint32_t* __restrict__ os,
-    int64_t tstride, const unsigned long long* __restrict__ wide, unsigned long long xthr) {
-  if (wide && __builtin_nontemporal_load(wide + 1) >= xthr) return;
-  __shared__ int32_t heavy[1024];  // chunks of this site that are heavy
-  __shared__ int n_heavy;
-  const int t = threadIdx.x;
-  const int64_t s = blockIdx.x;
-  const int nb = fold_chunks(p.Q);
-  const int32_t last_e = nnz[s] - 1;
-  if (t == 0) n_heavy = 0;
-  __syncthreads();
-  for (int c = t; c < nb; c += kFoldQC) {
-    const int32_t k0 = bounds[(int64_t)c * bounds_ld + s];
-    const int32_t k1 = c + 1 < nb ? bounds[(int64_t)(c + 1) * bounds_ld + s] : last_e;
-    const int32_t kend = k1 + 1 < last_e ? k1 + 1 : last_e;
-    if (kend - k0 + 1 > kFoldWin) {
-      const int i = atomicAdd(&n_heavy, 1);
-      if (i < 1024) heavy[i] = c;
-    }
-  }
-  __syncthreads();
-  const int nh = n_heavy < 1024 ? n_heavy : 1024;
-  const uint2* e = cdf + s * cdf_ld;
-  for (int i = 0; i < nh; ++i) {
-    const int c = heavy[i];
-    const int q = c * kFoldQC + t;
-    if (q >= p.Q) continue;
-    const int32_t k0 = bounds[(int64_t)c * bounds_ld + s];
-    const int32_t k1 = c + 1 < nb ? bounds[(int64_t)(c + 1) * bounds_ld + s] : last_e;
-    const int32_t kend = k1 + 1 < last_e ? k1 + 1 : last_e;
-    const uint32_t P = (uint32_t)p.lo[q];
-    int32_t x = k0 - 1, y = kend;  // cum[x] <= P < cum[y]
-    while (y - x > 1) {
-      const int32_t m = (x + y) >> 1;
-      if (e[m].x > P)
-        y = m;
-      else
-        x = m;
-    }
-    const uint2 ey = e[y];
-    const uint32_t Ph = P < (uint32_t)p.last ? P + 1u : P;
-    const uint32_t nv = ey.x > Ph ? ey.y : e[y + 1 <= last_e ? y + 1 : last_e].y;
-    os[(int64_t)c * tstride + s * kOsTile + t] = ey.y | (nv << 16);
-  }
-}
-
-// Fold, second form.  The first form's serial path paid a memory latency per
-// round: its window loads were conditional (per-lane and per-site branches),
-// so the compiler could not count them and waited for ALL outstanding loads
-// -- the next round's prefetch included -- before writing the current window
-// to LDS; 72 VGPRs left one 1,024-thread workgroup per CU (391 chunks on 256
-// CUs: two waves of workgroups); and the 16 in-order adds each waited for
-// their own LDS read.  Here every global load of a round is unconditional
-// (clamped addresses; a heavy site's order statistics or a dummy line), so the
-// compiler waits only for the round being resolved (vmcnt(8)); a site's chunk
-// bounds are fetched two rounds ahead and its window one round ahead; the
-// resolved (previous | next) pairs of round r go to one of two LDS buffers and
-// are added (lerp in the adder, reads first, then the in-order f64 adds) in
-// round r + 1, beside round r + 1's searches: one barrier per round.  The
-// searches are branchless lower bounds over the window's n + 1 entries
-// (depth log2 n, wave-uniform), the lane's quantiles searched side by side.
-template <int WAVES, int ABL = 0>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2 * WAVES / 4)))
-void k_pct_fold2(
-    const uint2* __restrict__ cdf, int64_t cdf_ld, const int32_t* __restrict__ bounds,
-    int64_t bounds_ld, const int32_t* __restrict__ nnz, int64_t n_sites, const QPos p,
-    const uint32_t* __restrict__ os, int64_t tstride, const double* __restrict__ gamma,
-    double* __restrict__ acc, const unsigned long long* __restrict__ wide,
-    unsigned long long xthr) {
-  if (wide && __builtin_nontemporal_load(wide + 1) >= xthr) return;  // very wide: k_pct_acc
-  constexpr int WPL = kFoldWin / 64;  // window entries per lane
-  constexpr int QPL = kFoldQPL;
-  static_assert(QPL == 4 && kFoldQC == kOsTile, "one uint4 of a heavy site's order statistics per lane");
-  __shared__ uint2 win[WAVES][kFoldWin];       // (inclusive rank, value) of the window's entries
-  __shared__ uint4 ov[2][WAVES][kFoldQC / 4];  // resolved previous | next << 16, by round parity
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int c = blockIdx.x;
-  const int nb = fold_chunks(p.Q);
-  const int q0 = c * kFoldQC;
-  const bool last_chunk = c + 1 >= nb;
-  const int cn = last_chunk ? c : c + 1;
-  const int64_t last_site = n_sites - 1;
-  uint32_t lo[QPL];
-#pragma unroll
-  for (int j = 0; j < QPL; ++j) {
-    const int q = q0 + lane * QPL + j;
-    lo[j] = (uint32_t)p.lo[q < p.Q ? q : p.Q - 1];
-  }
-  const uint32_t plast = (uint32_t)p.last;
-  const bool adder = tid < kFoldQC && q0 + tid < p.Q;
-  const int qa = q0 + (tid % kFoldQC) < p.Q ? q0 + (tid % kFoldQC) : p.Q - 1;
-  const double g = gamma[qa];
-  double a = acc[qa];
-  struct Desc {
-    int32_t k0, k1, ne;
-  };
-  auto load_desc = [&](int rr) -> Desc {  // all lanes: the wave's site of round rr
-    int64_t s = (int64_t)rr * WAVES + w;
-    s = s < last_site ? s : last_site;
-    return Desc{bounds[(int64_t)c * bounds_ld + s], bounds[(int64_t)cn * bounds_ld + s], nnz[s]};
-  };
-  struct Win {
-    uint2 e[WPL];  // the window's entries lane + 64 m; a heavy site: e[0], e[1] = its
-                   // order statistics of the lane's quantiles
-    int32_t n;     // window entries 0 .. n (uniform)
-    bool heavy;
-  };
-  auto fetch = [&](int rr, const Desc& d) -> Win {
-    int64_t s = (int64_t)rr * WAVES + w;
-    s = s < last_site ? s : last_site;
-    const int32_t last_e = __builtin_amdgcn_readfirstlane(d.ne) - 1;
-    const int32_t b0 = __builtin_amdgcn_readfirstlane(d.k0);
-    const int32_t b1 = last_chunk ? last_e : __builtin_amdgcn_readfirstlane(d.k1);
-    const int32_t kend = b1 + 1 < last_e ? b1 + 1 : last_e;
-    Win r;
-    r.n = kend - b0;
-    r.heavy = r.n + 1 > kFoldWin;
-    const uint2* e = cdf + s * cdf_ld + b0;
-    const uint2* h = reinterpret_cast<const uint2*>(os + (int64_t)c * tstride + s * kOsTile) +
-                     lane * (QPL / 2);
-    const int32_t nc = r.n > 0 ? r.n : 0;
-#pragma unroll
-    for (int m = 0; m < WPL; ++m) {
-      const int32_t i = lane + 64 * m;
-      const uint2* src = (m < QPL / 2 && r.heavy) ? h + m : e + (i < nc ? i : nc);
-      r.e[m] = *src;
-    }
-    return r;
-  };
-  auto process = [&](int rr, const Win& W) {
-    const int64_t s = (int64_t)rr * WAVES + w;
-    if (s >= n_sites) return;  // uniform per wave
-    uint32_t av[QPL], bv[QPL];
-    if (W.heavy) {
-      const uint32_t v[4] = {W.e[0].x, W.e[0].y, W.e[1].x, W.e[1].y};
-#pragma unroll
-      for (int j = 0; j < QPL; ++j) {
-        av[j] = v[j] & 0xFFFFu;
-        bv[j] = v[j] >> 16;
-      }
-    } else {
-      const int32_t n = W.n;
-#pragma unroll
-      for (int m = 0; m < WPL; ++m)
-        if (lane + 64 * m <= n) win[w][lane + 64 * m] = W.e[m];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // y = number of entries with rank <= P among 0 .. n - 1 (entry n's rank
-      // exceeds every position of the chunk): the first entry with rank > P
-      int32_t y[QPL];
-#pragma unroll
-      for (int j = 0; j < QPL; ++j) y[j] = 0;
-      for (int32_t step = (n > 0 && !(ABL & 2)) ? (int32_t)(1u << (31 - __builtin_clz((uint32_t)n))) : 0; step > 0;
-           step >>= 1) {
-        uint32_t cm[QPL];
-#pragma unroll
-        for (int j = 0; j < QPL; ++j) {
-          const int32_t t = y[j] + step;
-          const uint32_t v = win[w][(t <= n ? t : n) - 1].x;
-          cm[j] = t <= n ? v : 0xFFFFFFFFu;
-        }
-#pragma unroll
-        for (int j = 0; j < QPL; ++j)
-          if (cm[j] <= lo[j]) y[j] += step;
-      }
-#pragma unroll
-      for (int j = 0; j < QPL; ++j) {
-        const uint2 ey = win[w][y[j]];
-        const uint32_t nv = win[w][y[j] < n ? y[j] + 1 : n].y;
-        av[j] = ey.y;
-        // next position min(P + 1, n - 1): the same value unless P is the
-        // last position of its bin (then it opens the next entry)
-        const uint32_t Ph = lo[j] < plast ? lo[j] + 1u : lo[j];
-        bv[j] = ey.x > Ph ? ey.y : nv;
-      }
-    }
-    ov[rr & 1][w][lane] = make_uint4(av[0] | (bv[0] << 16), av[1] | (bv[1] << 16),
-                                     av[2] | (bv[2] << 16), av[3] | (bv[3] << 16));
-  };
-  auto add_round = [&](int rr) {  // round rr's sites, in site order
-    if (!adder || (ABL & 1)) return;
-    const int64_t left = n_sites - (int64_t)rr * WAVES;
-    const int nk = left < WAVES ? (int)left : WAVES;
-    const uint32_t* o = reinterpret_cast<const uint32_t*>(&ov[rr & 1][0][0]) + tid;
-    constexpr int G = 4;
-#pragma unroll
-    for (int k0 = 0; k0 < WAVES; k0 += G) {
-      uint32_t v[G];
-#pragma unroll
-      for (int k = 0; k < G; ++k) v[k] = o[(k0 + k) * kFoldQC];
-#pragma unroll
-      for (int k = 0; k < G; ++k) {
-        const double l = lerp_np(v[k] & 0xFFFFu, v[k] >> 16, g);
-        a = k0 + k < nk ? add_nc(a, l) : a;
-      }
-    }
-  };
-  // rounds in pairs (an odd count's last round is empty: its sites are
-  // past the end, process skips them and add_round adds nothing)
-  const int rounds2 = (int)((n_sites + 2 * WAVES - 1) / (2 * WAVES)) * 2;
-  Desc d0 = load_desc(0), d1 = load_desc(1);
-  Win w0 = fetch(0, d0), w1;
-  for (int r = 0; r < rounds2; r += 2) {
-    d0 = load_desc(r + 2);
-    w1 = fetch(r + 1, d1);
-    process(r, w0);
-    if (r > 0) add_round(r - 1);
-    __syncthreads();
-    d1 = load_desc(r + 3);
-    w0 = fetch(r + 2, d0);
-    process(r + 1, w1);
-    add_round(r);
-    __syncthreads();
-  }
-  add_round(rounds2 - 1);
-  if (adder) acc[q0 + tid] = a;
-}
-
-void launch_pct_fold(uint32_t* hist, unsigned long long* rmask, int64_t n_sites, const QPos& p,
-                     uint2* cdf, int64_t cdf_ld, int32_t* bounds, int64_t bounds_ld, int32_t* nnz,
-                     uint32_t* os, int64_t os_ld, int64_t* zero_counts, uint32_t* site_hist,
-                     const double* gamma, double* acc, const unsigned long long* wide,
-                     unsigned long long xthr, hipStream_t s) {
-  if (n_sites <= 0) return;
-  {
-    ProfScope prof("cdf_compact", s);
-    hipLaunchKernelGGL(k_cdf_compact, dim3((unsigned)n_sites), dim3(kCdfThreads), 0, s, hist, rmask,
-                       p, cdf, cdf_ld, bounds, bounds_ld, nnz, zero_counts, site_hist, wide, xthr);
-    hipLaunchKernelGGL(k_fold_heavy, dim3((unsigned)n_sites), dim3(kFoldQC), 0, s, cdf, cdf_ld,
-                       bounds, bounds_ld, nnz, p, os, os_ld * kOsTile, wide, xthr);
-  }
-  {
-    ProfScope prof("pct_fold", s);
-    hipLaunchKernelGGL(k_pct_fold2<kFoldWaves>, dim3((unsigned)fold_chunks(p.Q)), dim3(kFoldWaves * 64), 0, s,
-                       cdf, cdf_ld, bounds, bounds_ld, nnz, n_sites, p, os, os_ld * kOsTile, gamma,
-                       acc, wide, xthr);
-  }
-  TMH_HIP(hipGetLastError());
-}
-
-// ---------------------------------------------------------------------------
 // finalize (stats.py:94-112) and multi-rank merge
 // ---------------------------------------------------------------------------
 
@@ -1801,8 +1177,4 @@ void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s) {
   TMH_HIP(hipGetLastError());
 }
 
-}  // namespace tmh
-
-namespace tmh {
-int fold_chunks_host(int Q) { return fold_chunks(Q); }
 }  // namespace tmh

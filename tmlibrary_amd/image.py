@@ -446,7 +446,9 @@ class IllumstatsContainer(object):
         (``arr.flags.writeable = True``, then writing) makes the next call
         rebuild the corrector from the current values.  ``release()`` (also
         run when the container is collected) drops the corrector and makes
-        the arrays this container locked writeable again."""
+        the arrays this container locked writeable again.  Neither closes the
+        Corrector itself: a caller may hold it past the container (its own
+        ``__del__``/``close`` frees the device handle)."""
         m, s = self.mean.array, self.std.array
         key = (id(m), id(s), bool(log_transform))
         if (self._corr is None or self._corr_key != key or m.flags.writeable or
@@ -461,10 +463,10 @@ class IllumstatsContainer(object):
         return self._corr
 
     def release(self):
-        """Drop the cached device corrector; the planes it locked are
-        writeable again (the reference's planes are plain arrays)."""
-        if self._corr is not None:
-            self._corr.close()
+        """Drop the cache's reference to the device corrector (a caller that
+        still holds it keeps a working handle; the last reference frees it);
+        the planes it locked are writeable again (the reference's planes are
+        plain arrays)."""
         self._corr = None
         self._corr_key = None
         self._corr_arrays = None

@@ -156,7 +156,7 @@ static int run(int argc, char** argv) {
     CK(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), 0));
     hipLaunchKernelGGL((k_correct_hist<true, false, 4, ABL, 512, 16384>), fg, fb, 0, 0, in, out,
                        npx, S, coef, mconst2, fl, -1, -1, hist, rmask, kFusedBands, queues,
-                       nullptr, 0ull, 0ull, 0ull, 0ull, SiteTab{});
+                       nullptr, 0ull, 0ull, 0ull, 0ull, SiteTab{}, InPassFin{});
   };
   time("fused prod (ABL 0)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 0>()); });
   time("fused no hist (ABL 1)", cb + 8.0 * npx, [&] { fused(std::integral_constant<int, 1>()); });

@@ -165,7 +165,7 @@ static int run(int argc, char** argv) {
     CK(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), 0));
     hipLaunchKernelGGL((k_correct_hist<true, false, 4, ABL, 512, 16384>), dim3(cus * 2), dim3(512), 0, 0,
                        in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, queues,
-                       nullptr, 0ull, 0ull, 0ull, 0ull, SiteTab{});
+                       nullptr, 0ull, 0ull, 0ull, 0ull, SiteTab{}, InPassFin{});
   };
   char nm[96];
   for (int b : {16, 8, 12, 24, 32, 64}) {
@@ -180,7 +180,7 @@ static int run(int argc, char** argv) {
       CK(hipMemsetAsync(fn, 0, 4, 0));
       CK(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), 0));
       hipLaunchKernelGGL((k_correct_hist<true, false, SPU_, 0, NT_, LB_>), dim3(grid), dim3(NT_), 0, 0,
-                         in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, queues, nullptr, 0ull, 0ull, 0ull, 0ull, SiteTab{});
+                         in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, nb, queues, nullptr, 0ull, 0ull, 0ull, 0ull, SiteTab{}, InPassFin{});
     });
   };
   using C8 = std::integral_constant<int, 8>;
@@ -212,7 +212,7 @@ static int run(int argc, char** argv) {
         CK(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), 0));
         hipLaunchKernelGGL((k_correct_hist<true, false, SPU_, ABL_, NT_, LB_>), dim3(grid), dim3(NT_), 0, 0,
                            in, out, npx, S, coef, mconst2, fl, -1, -1, hist, rmask, bands, queues, nullptr,
-                           0ull, 0ull, 0ull, 0ull, SiteTab{});
+                           0ull, 0ull, 0ull, 0ull, SiteTab{}, InPassFin{});
       });
     };
     using A0 = std::integral_constant<int, 0>;

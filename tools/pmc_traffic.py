@@ -36,6 +36,7 @@ SHORT = {
     "k_pct_acc": "pct_acc",
     "k_wf_merge_parts": "welford_merge",
     "k_chain_u8": "chain",
+    "k_pooled_colsum": "colsum",
 }
 
 
@@ -70,6 +71,7 @@ def main():
     p.add_argument("--sites", type=int, required=True)
     p.add_argument("--height", type=int, required=True)
     p.add_argument("--width", type=int, required=True)
+    p.add_argument("--distribution", default="synthetic")
     p.add_argument("-o", "--out", required=True)
     a = p.parse_args()
     fetch = read_counter(a.fetch_dir, "FETCH_SIZE")
@@ -80,7 +82,8 @@ def main():
            "correct": 2 * a.sites * site_bytes + 16 * npx,
            "correct_hist": 2 * a.sites * site_bytes + 8 * npx,
            "chain": 3 * a.sites * npx}
-    res = {"config": {"sites": a.sites, "height": a.height, "width": a.width},
+    res = {"config": {"sites": a.sites, "height": a.height, "width": a.width,
+                      "distribution": a.distribution},
            "method": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch (separate --pmc passes; "
                      "gfx950 FETCH_SIZE halving corrected); median over the headline-sized launches "
                      "(>= 1/4 of the kernel's largest)",
