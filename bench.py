@@ -93,10 +93,6 @@ def parse():
     p.add_argument("--cpu-procs", type=int, default=4,
                    help="P of the P-process CPU variant (one channel job per process; "
                         "P = min(this, cores))")
-    p.add_argument("--fused-epochs", type=int, default=None,
-                   help="TMH_OPT_FUSED_EPOCHS: the fused pass finalizes each site group's "
-                        "order statistics itself, over this many epochs of its unit sweep "
-                        "(0: a separate finalize kernel after it; default: the library's)")
     p.add_argument("--fused-config", type=int, default=None,
                    help="fused pass (sites per unit, threads, LDS bins) configuration 0..3 "
                         "(TMH_OPT_FUSED_CONFIG; default: the library's)")
@@ -1126,8 +1122,6 @@ def main():
             hip.check(L.tmh_stats_set_stream(self.h, self.sp))
             if a.fused_config is not None:
                 hip.check(L.tmh_stats_set_option(self.h, hip.TMH_OPT_FUSED_CONFIG, a.fused_config))
-            if a.fused_epochs is not None:
-                hip.check(L.tmh_stats_set_option(self.h, hip.TMH_OPT_FUSED_EPOCHS, a.fused_epochs))
             self.corr = C.c_void_p()
             torch.cuda.synchronize(dev)
             hip.check(L.tmh_corrector_create_device(C.c_void_p(self.mean.data_ptr()),

@@ -100,12 +100,6 @@ int tmh_stats_reset(tmh_stats* h);
  *                          (bright sites: the log10 pass is VALU-bound),
  *                          else runs as one part; 1..4: that many parts where
  *                          the launch has >= 32 sites a part
- *   TMH_OPT_FUSED_EPOCHS   0..64 (default 4): the fused pass writes the
- *                          order statistics itself -- the workgroup that
- *                          completes a site group's last pixel band finalizes
- *                          the group -- over a unit sweep cut into that many
- *                          epochs, so groups complete throughout the pass;
- *                          0 = a separate finalize kernel after the pass
  *   TMH_OPT_COPY_THREADS   1..64 (default 8): host threads of the pageable <->
  *                          pinned copies of the host-buffer entry points
  *   TMH_OPT_HOST_STAGING   host-buffer entry points: 0 = the caller's buffers
@@ -116,10 +110,10 @@ int tmh_stats_reset(tmh_stats* h);
  *                          several threads spreads a fresh output's faults) */
 #define TMH_OPT_FUSED_CONFIG 1
 #define TMH_OPT_WELFORD_PARTS 2
-/* 3 and 6 were TMH_OPT_TAIL_CHUNKS / TMH_OPT_PCT_TAIL (measured slower, removed) */
+/* 3, 6 and 7 were TMH_OPT_TAIL_CHUNKS / TMH_OPT_PCT_TAIL / TMH_OPT_FUSED_EPOCHS
+ * (percentile-tail variants measured slower than the default, removed) */
 #define TMH_OPT_COPY_THREADS 4
 #define TMH_OPT_HOST_STAGING 5
-#define TMH_OPT_FUSED_EPOCHS 7
 int tmh_stats_set_option(tmh_stats* h, int option, int value);
 
 /* update(image) for a run of sites.  zero_counts_out (host, n_sites, may be

@@ -538,12 +538,9 @@ def test_run_job_end_to_end(L, tmp_path):
     assert np.allclose(cont.mean.array, orc.smooth_reflect(g["mean"]), rtol=1e-9, atol=1e-12)
 
 
-def _fused_job(L, sites, clip=(-1, -1), q=None, epochs=4):
+def _fused_job(L, sites, clip=(-1, -1), q=None):
     """Split pipeline through the C-ABI: Welford-only update -> finalize ->
-    smooth -> corrector -> fused correct+histogram.  Returns host results.
-    epochs: TMH_OPT_FUSED_EPOCHS (>= 1: the order statistics are written by the
-    fused pass itself over that many epochs of its unit sweep; 0: by a
-    separate finalize kernel after it)."""
+    smooth -> corrector -> fused correct+histogram.  Returns host results."""
     from tmlibrary_amd import hip
     from tmlibrary_amd.image import ZERO_LOG10
     from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
@@ -556,7 +553,6 @@ def _fused_job(L, sites, clip=(-1, -1), q=None, epochs=4):
     h = C.c_void_p()
     hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
                                  hip.ptr(lut), 4, hip.TMH_STATS_KEEP_SITE_HIST, C.byref(h)))
-    hip.check(L.tmh_stats_set_option(h, hip.TMH_OPT_FUSED_EPOCHS, epochs))
     d_in, d_out = Dev(L, sites.nbytes), Dev(L, sites.nbytes)
     d_in.put(sites)
     planes = [Dev(L, npx * 8) for _ in range(5)]
@@ -594,13 +590,12 @@ def _fused_job(L, sites, clip=(-1, -1), q=None, epochs=4):
     return res
 
 
-@pytest.mark.parametrize("epochs", [4, 0, 1])
 @pytest.mark.parametrize("kind", ["synth", "extremes", "uniform", "tiny", "many", "saturated",
                                   "constant", "two_values"])
-def test_fused_correct_hist_pipeline(L, kind, epochs):
-    """The fused pass with its in-pass finalize (4 epochs, 1 epoch) and with
-    the separate finalize kernel (0): one-bin sites, Q > pixel count, sparse
-    tails, the very wide path of the uniform case, each bit-exact."""
+def test_fused_correct_hist_pipeline(L, kind):
+    """The fused pass and its percentile tail: one-bin sites, Q > pixel
+    count, sparse tails, the very wide path of the uniform case, each
+    bit-exact."""
     from tmlibrary_amd.synth import synth_exact_sites_host, synth_sites_host
     rng = np.random.default_rng(97)
     if kind == "saturated":  # corrected values far above 2**16 (f64 refinement, common.h)
@@ -625,7 +620,7 @@ def test_fused_correct_hist_pipeline(L, kind, epochs):
                           for _ in range(5)])
     else:
         sites = np.stack(load_golden("stats_extremes")["sites"])
-    r = _fused_job(L, sites, epochs=epochs)
+    r = _fused_job(L, sites)
     ref = orc.run_illumstats(list(sites))
     assert r["n"] == len(sites)
     assert_close_rel(r["mean"], ref.mean)

@@ -243,7 +243,6 @@ struct tmh_stats {
   hipEvent_t ev_in = nullptr, ev_out = nullptr;  // ordering against a caller's stream
   int fused_cfg = kFusedAuto;     // TMH_OPT_FUSED_CONFIG (-1: per launch, on the device)
   int wf_parts = 0;               // TMH_OPT_WELFORD_PARTS (0: automatic)
-  int fused_epochs = kFusedEpochsDefault;  // TMH_OPT_FUSED_EPOCHS (0: finalize after the pass)
   HostOpts host;                  // TMH_OPT_COPY_THREADS / TMH_OPT_HOST_STAGING
   bool hist_dirty = false;        // a fused launch may have left counts / round masks behind
   int64_t n = 0;              // sites accumulated (Welford count)
@@ -263,7 +262,6 @@ struct tmh_stats {
   QPos qp{};
   DBuf<uint16_t> stage;  // two device slots of batch_cap sites
   HostPipe pipe;
-  DBuf<int> gdone;  // fused pass, in-pass finalize: zero-maintained band counters per site group
   DBuf<uint32_t> vlh;  // order statistics (previous | next << 16), quantile-tiled (common.h)
   int64_t vlh_cap = 0;   // deferred mode: sites the tiles have room for
   int64_t vlh_ld = 0;    // tile stride in sites of the current contents
@@ -478,10 +476,6 @@ int tmh_stats_set_option(tmh_stats* h, int option, int value) {
         TMH_CHECK(value >= 0 && value <= 4, TMH_EINVAL, "Welford parts must be 0..4");
         h->wf_parts = value;
         break;
-      case TMH_OPT_FUSED_EPOCHS:
-        TMH_CHECK(value >= 0 && value <= 64, TMH_EINVAL, "fused epochs must be 0..64");
-        h->fused_epochs = value;
-        break;
       default:
         if (!h->host.set(option, value)) throw Error{TMH_EINVAL, "unknown option"};
     }
@@ -498,7 +492,6 @@ int tmh_stats_reset(tmh_stats* h) {
       if (h->hist_rmask.n)
         TMH_HIP(hipMemsetAsync(h->hist_rmask.p, 0, h->hist_rmask.n * 8, h->stream));
       TMH_HIP(hipMemsetAsync(h->pooled_parts.p, 0, h->pooled_parts.n * 8, h->stream));
-      if (h->gdone.n) TMH_HIP(hipMemsetAsync(h->gdone.p, 0, h->gdone.n * 4, h->stream));
       h->hist_dirty = false;
     }
     TMH_HIP(hipMemsetAsync(h->mean.p, 0, h->npx * 8, h->stream));
@@ -1255,45 +1248,21 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
           autocfg ? (unsigned long long)std::max<double>(
                         1.0, kXWideFrac * (double)h->wide_sites * (double)(h->npx >> 3))
                   : ~0ull;
-      // in-pass finalize (fused_kernels.hip): the order statistics are
-      // written inside the streaming pass; the pooled column sum then reads
-      // and zeroes the counts.  TMH_OPT_FUSED_EPOCHS = 0: k_hist_finalize after it.
-      InPassFin fin;
-      const int E = h->fused_epochs;
-      if (E > 0) {
-        if ((size_t)n_sites + 1 > h->gdone.n) {
-          TMH_HIP(hipStreamSynchronize(s));
-          h->gdone.alloc((size_t)n_sites + 1, true);
-        }
-        fin.p = h->qp;
-        fin.p.tstride = ld * kOsTile;
-        fin.vlh = vlh;
-        fin.gdone = h->gdone.p;
-        fin.zero_counts = h->zeros.p;
-        fin.site_hist = sh;
-        fin.epoch_sites = (int)std::min<int64_t>(n_sites, (n_sites + E - 1) / E);
-      }
       const unsigned long long* rm_all = reinterpret_cast<const unsigned long long*>(c->queues.p + 8);
       const FixList fl = corrector_fixlist(c, n_sites, s);
       launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p, fl,
                           c->log_transform, clip_lo, clip_hi, h->hist_full.p, h->hist_rmask.p,
                           c->queues.p, c->n_wg, h->fused_cfg, h->wide.p, wide_thresh, xwide_thresh,
-                          s, tab, fin);
+                          s, tab);
       launch_fix_correct(dev_in, dev_out, 2, c->npx, n_sites, fl, c->coef64.p, c->rc.p,
                          c->log_transform, clip_lo, clip_hi, s, tab);
       if (autocfg)  // exits at once unless the launch is very wide
         launch_hist_site_u16(dev_in, h->npx, n_sites, h->hist_full.p, h->qp, vlh, ld, h->pooled.p,
                              h->pooled_parts.p, kPooledParts, h->zeros.p, sh, h->wide.p,
                              xwide_thresh, s, tab);
-      if (E > 0) {
-        launch_pooled_colsum(h->hist_full.p, h->hist_rmask.p, rm_all, n_sites, h->pooled.p, s,
-                             true);
-        TMH_HIP(hipMemsetAsync(h->hist_rmask.p, 0, (size_t)n_sites * 8, s));
-      } else {
-        launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, n_sites, h->qp, vlh, ld,
-                             h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, sh, s,
-                             false, rm_all, h->wide.p, xwide_thresh);
-      }
+      launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, n_sites, h->qp, vlh, ld,
+                           h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, sh, s, false,
+                           rm_all, h->wide.p, xwide_thresh);
       if (!(h->flags & TMH_STATS_DEFERRED_PCT))
         launch_pct_accumulate(vlh, n_sites, ld, h->Q, h->gamma.p, h->acc.p, s);
       h->hist_dirty = false;

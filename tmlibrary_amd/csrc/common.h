@@ -202,11 +202,10 @@ void launch_pct_accumulate_range(const uint32_t* vlh, int64_t n_sites, int64_t v
                                  const unsigned long long* only_xwide = nullptr,
                                  unsigned long long xthr = 0);
 // pooled[b] += sum over the sites of hist[s][b] for the rounds rmask names
-// (rm_all: the launch-wide union of the masks, or null); reset: those counts
-// are zeroed as they are read (the fused pass finalized them in-pass)
-void launch_pooled_colsum(uint32_t* hist, const unsigned long long* rmask,
+// (rm_all: the launch-wide union of the masks, or null)
+void launch_pooled_colsum(const uint32_t* hist, const unsigned long long* rmask,
                           const unsigned long long* rm_all, int64_t n_sites,
-                          unsigned long long* pooled, hipStream_t s, bool reset = false);
+                          unsigned long long* pooled, hipStream_t s);
 void launch_finalize(const double* mean, const double* m2, int64_t n, int64_t npx, double* out_mean,
                      double* out_std, hipStream_t s);
 // var = M2 / (n - 1), NaN where n < 2 (stats.py:94-102)
@@ -270,31 +269,13 @@ constexpr double kWideFrac = 0.02;
 // cost more than one more read of the sites); the fused pass then runs without
 // its histogram and k_hist_site_u16 builds the histograms
 constexpr double kXWideFrac = 0.33;
-// In-pass histogram finalize of the fused pass: the workgroup that completes
-// a site group's last band reads the group's finished histograms (the rounds
-// its round masks name) and writes their order statistics, so the finalize
-// runs inside the streaming pass instead of after it.  The unit sweep is cut
-// into epochs of epoch_sites sites (band-major inside an epoch), so groups
-// complete throughout the pass rather than all in its last sixteenth.
-// gdone: one zero-maintained band counter per site group.  The counts stay in
-// the slab (the pooled column sum reads and zeroes them afterwards).
-// epoch_sites == 0: off (k_hist_finalize after the pass).
-struct InPassFin {
-  QPos p{};                       // tstride set
-  uint32_t* vlh = nullptr;        // the launch's first site's column of the tiles
-  int* gdone = nullptr;
-  int64_t* zero_counts = nullptr;
-  uint32_t* site_hist = nullptr;  // debug copy (TMH_STATS flag 2) or null
-  int epoch_sites = 0;            // sites per epoch (0: off)
-};
-constexpr int kFusedEpochsDefault = 4;
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, const FixList& fl,
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
                          unsigned long long* rmask, int* queues, int n_wg, int cfg,
                          const unsigned long long* wide, unsigned long long wide_thresh,
                          unsigned long long xwide_thresh, hipStream_t s,
-                         const SiteTab& tab = SiteTab{}, const InPassFin& fin = InPassFin{});
+                         const SiteTab& tab = SiteTab{});
 // illuminati chain (chain_kernels.hip)
 void launch_align(const void* in, void* out, int elem_bytes, int64_t n_sites, int H, int W, int oh,
                   int ow, const tmh_window* d_win, hipStream_t s);

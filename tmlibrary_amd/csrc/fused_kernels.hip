@@ -32,7 +32,6 @@
 // mean(std)/std are f32 (mean's rounding adds <= 0.05*a DN at 65535); zero
 // pixels take the reference's log10(1e-10) = -10.  Parity bar: +-1 DN.
 #include "common.h"
-#include "hist_tail.h"
 
 namespace tmh {
 
@@ -193,7 +192,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     int clip_lo, int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
     int n_bands, int* __restrict__ queues, const unsigned long long* __restrict__ wide,
     unsigned long long wide_lo, unsigned long long wide_hi, unsigned long long x_lo,
-    unsigned long long x_hi, const SiteTab tab, const InPassFin fin) {
+    unsigned long long x_hi, const SiteTab tab) {
   // launch-time selection (launch_correct_hist): this configuration runs only
   // when the Welford pass's counts of pixel groups with a value >= 4,096 and
   // >= 16,384 are in [wide_lo, wide_hi) and [x_lo, x_hi)
@@ -250,29 +249,13 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   // (i / n_groups_s + 2 * (i % 8)) % n_bands -- and XCD x deals the units
   // i = x + 8 j from its own counter (queues[x]), stealing from the next
   // queue once its own is drained.  The next unit is grabbed while the
-  // current one streams.  With the in-pass finalize the sweep is cut into
-  // epochs of gpe site groups, each band-major as above (an epoch starts at a
-  // multiple of 8 units, so i % 8 keeps naming the XCD's band offset): a group
-  // completes in its epoch's last sixteenth, so finalizes are spread over the
-  // pass instead of crowding its end.
+  // current one streams.
   __shared__ int unit_sh;
   int q = xcc_id(), exhausted = 0;
-  const int gpe = fin.epoch_sites > 0 ? (fin.epoch_sites + SPU - 1) / SPU : n_groups_s;
   auto unit_of = [&](int i) -> int {
-    const int per = n_bands * gpe;
-    const int e = i / per;
-    const int j = i - e * per;
-    const int g0 = e * gpe;
-    const int ng = n_groups_s - g0 < gpe ? n_groups_s - g0 : gpe;
-    const int band = (j / ng + 2 * (j % 8)) % n_bands;
-    return band * n_groups_s + g0 + j % ng;
+    const int band = (i / n_groups_s + 2 * (i % 8)) % n_bands;
+    return band * n_groups_s + i % n_groups_s;
   };
-  // in-pass finalize: LDS scan slots and the "this workgroup finishes the
-  // group" flag; the rank tables reuse the (then empty) histogram slices
-  constexpr int SRF = NT >= 1024 ? 4 : 2;
-  static_assert(2 * SRF * kRound <= NSL * SLICE, "rank tables fit in the slices");
-  __shared__ uint32_t fslots[32];
-  __shared__ int fin_sh;
   auto grab = [&]() -> int {
     while (exhausted < 8) {
       if (tid == 0) unit_sh = atomicAdd(&queues[q], 1);
@@ -552,41 +535,6 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
       if (tid == 0) fix_cnt[par] = 0u;
     }
     par ^= 1;
-    if (!fin.gdone) continue;
-    // In-pass finalize.  Every thread's slab atomics and the round masks are
-    // made visible (agent-scope release) before one thread counts the unit's
-    // band; the workgroup whose band completes the group (all n_bands counted)
-    // reads the group's histograms after an acquire -- nothing waits on
-    // anyone, so no workgroup can stall the pass.
-    __threadfence();
-    __syncthreads();
-    const int grp = (int)(un.s0 / SPU);
-    if (tid == 0) fin_sh = atomicAdd(&fin.gdone[grp], 1) == n_bands - 1;
-    __syncthreads();
-    if (!fin_sh) continue;
-    if (tid == 0) fin.gdone[grp] = 0;  // zero-maintained: no unit of the group remains
-    __threadfence();
-    int32_t* starts = reinterpret_cast<int32_t*>(bins);  // empty after the flush
-    for (int k = 0; k < un.ns; ++k) {
-      const int64_t st = un.s0 + k;
-      const uint32_t* h = hist + st * (int64_t)kBins;
-      hist_tail_rounds<0, NT, SRF>(
-          rmask[st], [&](uint32_t b) -> uint32_t { return h[b]; }, [](uint32_t, uint32_t) {},
-          st, fin.p, fin.vlh, nullptr, fin.zero_counts, fin.site_hist, fslots, starts);
-      __syncthreads();  // the rank tables and slots are rewritten by the next site
-    }
-    for (int i = tid; i < 2 * SRF * kRound; i += NT) bins[i] = 0u;
-    __syncthreads();
-    // the next unit's first group again (the earlier loads' registers were
-    // given up to the finalize: vA / cA are rewritten on every path here)
-    if (nxt >= 0) {
-      load(nu, nu.g0 + tid, vA, cA);
-    } else {
-#pragma unroll
-      for (int k = 0; k < SPU; ++k) vA[k] = make_uint4(0, 0, 0, 0);
-#pragma unroll
-      for (int p = 0; p < 4; ++p) cA[p] = cc;
-    }
   }
 }
 
@@ -624,8 +572,7 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
                                     unsigned long long* rmask, int* queues, int n_wg, int cfg,
                                     const unsigned long long* wide, unsigned long long wide_lo,
                                     unsigned long long wide_hi, unsigned long long x_lo,
-                                    unsigned long long x_hi, hipStream_t s, const SiteTab& tab,
-                                    const InPassFin& fin) {
+                                    unsigned long long x_hi, hipStream_t s, const SiteTab& tab) {
 #define TMH_LAUNCH_CH(L_, K_, A_)                                                                \
   {                                                                                              \
     constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
@@ -635,13 +582,13 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
                          grid,                                                                   \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
                          clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
-                         wide_hi, x_lo, x_hi, tab, fin);                                         \
+                         wide_hi, x_lo, x_hi, tab);                                              \
     else                                                                                         \
       hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, A_, c.threads, c.lds_bins, c.packed>), \
                          grid,                                                                   \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
                          clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
-                         wide_hi, x_lo, x_hi, tab, fin);                                         \
+                         wide_hi, x_lo, x_hi, tab);                                              \
   }
 #define TMH_LAUNCH_CFG(L_)                                     \
   switch (cfg) {                                               \
@@ -674,8 +621,7 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
                          unsigned long long* rmask, int* queues, int n_wg, int cfg,
                          const unsigned long long* wide, unsigned long long wide_thresh,
-                         unsigned long long xwide_thresh, hipStream_t s, const SiteTab& tab,
-                         const InPassFin& fin) {
+                         unsigned long long xwide_thresh, hipStream_t s, const SiteTab& tab) {
   if (n_sites <= 0) return;
   ProfScope prof("correct_hist", s);
   // queues[0..8): per-XCD unit counters; queues[8..10): the union of the
@@ -687,16 +633,16 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
   if (cfg >= 0 || !wide) {
     launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo,
                             clip_hi, hist, rmask, queues, n_wg, cfg >= 0 ? cfg : kFusedNarrow,
-                            nullptr, 0, 0, 0, 0, s, tab, fin);
+                            nullptr, 0, 0, 0, 0, s, tab);
     return;
   }
   const unsigned long long X = xwide_thresh;
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedNarrow, wide, 0, wide_thresh, 0, X, s, tab, fin);
+                          hist, rmask, queues, n_wg, kFusedNarrow, wide, 0, wide_thresh, 0, X, s, tab);
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedWide, wide, wide_thresh, ~0ull, 0, X, s, tab, fin);
+                          hist, rmask, queues, n_wg, kFusedWide, wide, wide_thresh, ~0ull, 0, X, s, tab);
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedNoHist, wide, 0, ~0ull, X, ~0ull, s, tab, fin);
+                          hist, rmask, queues, n_wg, kFusedNoHist, wide, 0, ~0ull, X, ~0ull, s, tab);
 }
 
 }  // namespace tmh

@@ -771,10 +771,7 @@ __global__ __launch_bounds__(NT, 8) void k_hist_finalize(
 // this replaced ~30,000 per-site atomics per site in the finalize (1.2 ms of
 // its 2.4 ms at 3,456 sites: profiles/r2/mb_tail_bright_r2y.txt).
 constexpr int kColSites = 32;
-// RESET (the fused pass's in-pass finalize has already read the counts): the
-// counts read are also zeroed -- the slab is zero-maintained.
-template <bool RESET>
-__global__ __launch_bounds__(256) void k_pooled_colsum(uint32_t* __restrict__ hist,
+__global__ __launch_bounds__(256) void k_pooled_colsum(const uint32_t* __restrict__ hist,
                                                        const unsigned long long* __restrict__ rmask,
                                                        const unsigned long long* __restrict__ rm_all,
                                                        int64_t n_sites,
@@ -797,16 +794,11 @@ __global__ __launch_bounds__(256) void k_pooled_colsum(uint32_t* __restrict__ hi
   }
   __syncthreads();
   if (!any) return;  // uniform: no site of the chunk uses this round
-  uint32_t* h = hist + s0 * kBins + b;
+  const uint32_t* h = hist + s0 * kBins + b;
   unsigned long long t = 0;
 #pragma unroll 16
-  for (int s = 0; s < ns; ++s) {
-    if (use[s]) {
-      const uint32_t c = h[(int64_t)s * kBins];
-      t += c;
-      if (RESET && c) h[(int64_t)s * kBins] = 0u;
-    }
-  }
+  for (int s = 0; s < ns; ++s)
+    if (use[s]) t += h[(int64_t)s * kBins];
   if (t) atomicAdd(&pooled[b], t);
 }
 
@@ -826,18 +818,12 @@ __global__ void k_pooled_fold(unsigned long long* __restrict__ pooled,
   pooled[b] += t;
 }
 
-void launch_pooled_colsum(uint32_t* hist, const unsigned long long* rmask,
+void launch_pooled_colsum(const uint32_t* hist, const unsigned long long* rmask,
                           const unsigned long long* rm_all, int64_t n_sites,
-                          unsigned long long* pooled, hipStream_t s, bool reset) {
+                          unsigned long long* pooled, hipStream_t s) {
   if (n_sites <= 0) return;
-  ProfScope prof("colsum", s);
-  const dim3 grid(kBins / 256, (unsigned)cdiv(n_sites, kColSites));
-  if (reset)
-    hipLaunchKernelGGL(k_pooled_colsum<true>, grid, dim3(256), 0, s, hist, rmask, rm_all, n_sites,
-                       pooled);
-  else
-    hipLaunchKernelGGL(k_pooled_colsum<false>, grid, dim3(256), 0, s, hist, rmask, rm_all,
-                       n_sites, pooled);
+  hipLaunchKernelGGL(k_pooled_colsum, dim3(kBins / 256, (unsigned)cdiv(n_sites, kColSites)),
+                     dim3(256), 0, s, hist, rmask, rm_all, n_sites, pooled);
   TMH_HIP(hipGetLastError());
 }
 
@@ -856,7 +842,7 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
   // finalize; without one, the finalize adds into pooled copies, then folded
   const bool colsum = rmask != nullptr && dense_rounds == 0;
   if (colsum)
-    hipLaunchKernelGGL(k_pooled_colsum<false>, dim3(kBins / 256, (unsigned)cdiv(n_sites, kColSites)),
+    hipLaunchKernelGGL(k_pooled_colsum, dim3(kBins / 256, (unsigned)cdiv(n_sites, kColSites)),
                        dim3(256), 0, s, hist, rmask, rm_all, n_sites, pooled);
   unsigned long long* fin_pooled = colsum ? nullptr : pooled_parts;
   if (narrow)

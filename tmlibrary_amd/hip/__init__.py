@@ -27,7 +27,6 @@ TMH_OPT_FUSED_CONFIG = 1
 TMH_OPT_WELFORD_PARTS = 2
 TMH_OPT_COPY_THREADS = 4
 TMH_OPT_HOST_STAGING = 5
-TMH_OPT_FUSED_EPOCHS = 7
 TMH_SYNTH_STANDARD = 0
 TMH_SYNTH_BRIGHT = 1
 TMH_SYNTH_UNIFORM = 2
