@@ -93,6 +93,12 @@ def parse():
     p.add_argument("--cpu-procs", type=int, default=4,
                    help="P of the P-process CPU variant (one channel job per process; "
                         "P = min(this, cores))")
+    p.add_argument("--fused-cus", type=int, default=None,
+                   help="TMH_OPT_FUSED_CUS: CUs' worth of workgroups of the fused pass's "
+                        "persistent grid (default: the library's, all CUs)")
+    p.add_argument("--welford-parts", type=int, default=None,
+                   help="TMH_OPT_WELFORD_PARTS (1..4 forces that split and skips the device-side "
+                        "choice between the standard and bright passes; default: automatic)")
     p.add_argument("--fused-config", type=int, default=None,
                    help="fused pass (sites per unit, threads, LDS bins) configuration 0..3 "
                         "(TMH_OPT_FUSED_CONFIG; default: the library's)")
@@ -1120,6 +1126,8 @@ def main():
             hip.check(L.tmh_stats_create(H, W, Q, hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
                                          hip.ptr(lut), 1, flags, C.byref(self.h)))
             hip.check(L.tmh_stats_set_stream(self.h, self.sp))
+            if a.welford_parts is not None:
+                hip.check(L.tmh_stats_set_option(self.h, hip.TMH_OPT_WELFORD_PARTS, a.welford_parts))
             if a.fused_config is not None:
                 hip.check(L.tmh_stats_set_option(self.h, hip.TMH_OPT_FUSED_CONFIG, a.fused_config))
             self.corr = C.c_void_p()
@@ -1127,6 +1135,8 @@ def main():
             hip.check(L.tmh_corrector_create_device(C.c_void_p(self.mean.data_ptr()),
                                                     C.c_void_p(self.std.data_ptr()), H, W, 1,
                                                     ZERO_LOG10, self.sp, C.byref(self.corr)))
+            if a.fused_cus is not None:
+                hip.check(L.tmh_corrector_set_option(self.corr, hip.TMH_OPT_FUSED_CUS, a.fused_cus))
             self.ops = StatsOps(L, self.h, npx, Q, dev)
             self.merge_ev = []  # (welford start, end, counts start, end) per timed step
 

@@ -46,6 +46,27 @@ int tmh5_read_channel_image(const char* path, void* out);
  * (the input path of run_job / configs[4]). */
 int tmh5_read_channel_images(const char* const* paths, int64_t n_files, void* out, int n_threads);
 
+/* The still-compressed chunks of n_files channel images for the GPU inflate
+ * (libtmhip tmh_inflate_device / tmh_place_chunks_device; tmh5_chunk has the
+ * layout of tmh_zchunk): every chunk's zlib stream is copied into blob
+ * (blob_cap bytes) and described by one table entry (table_cap entries) --
+ * src_off / src_len in blob, raw_off / raw_len of its decompressed bytes in a
+ * raw buffer of *n_chunks full chunks (file order), image = the file's index,
+ * (row0, col0) its origin, flags 1 = stored (the filter was skipped).
+ * geom = {height, width, elem_bytes, chunk_rows, chunk_cols}.  *blob_used and
+ * *n_chunks are set also when a capacity is too small (-28, nothing read).
+ * Files must share shape, dtype and chunk shape and be chunked with exactly
+ * the deflate filter, all chunks written (-95 otherwise: read those with
+ * tmh5_read_channel_images).  The HDF5 metadata is read under libhdf5's
+ * lock, the chunk bytes with pread() by n_threads workers outside it. */
+typedef struct tmh5_chunk {
+  int64_t src_off, src_len, raw_off, raw_len, image;
+  int32_t row0, col0, flags, reserved;
+} tmh5_chunk;
+int tmh5_read_raw_chunks(const char* const* paths, int64_t n_files, int n_threads, uint8_t* blob,
+                         int64_t blob_cap, tmh5_chunk* table, int64_t table_cap,
+                         int64_t* blob_used, int64_t* n_chunks, int32_t* geom);
+
 #ifdef __cplusplus
 }
 #endif

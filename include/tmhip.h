@@ -255,8 +255,12 @@ void tmh_corrector_destroy(tmh_corrector* c);
  * no synchronisation): one corrector serves every job of the same shape. */
 int tmh_corrector_update_device(tmh_corrector* c, const double* dev_mean, const double* dev_std,
                                 void* stream);
-/* Host-path options of a corrector: TMH_OPT_COPY_THREADS, TMH_OPT_HOST_STAGING
- * (see tmh_stats_set_option). */
+/* Options of a corrector: TMH_OPT_COPY_THREADS, TMH_OPT_HOST_STAGING (see
+ * tmh_stats_set_option), and TMH_OPT_FUSED_CUS: the fused correct+histogram
+ * pass's persistent grid spans this many CUs' worth of workgroups (0 or the
+ * CU count, default: all) -- fewer leave room for other streams' kernels
+ * (several channel jobs sharing a GPU).  Results never depend on them. */
+#define TMH_OPT_FUSED_CUS 8
 int tmh_corrector_set_option(tmh_corrector* c, int option, int value);
 /* The two global means (np.mean(std), np.mean(mean), image.py:627). */
 int tmh_corrector_means(tmh_corrector* c, double* mean_of_std, double* mean_of_mean);
@@ -328,6 +332,47 @@ int tmh_synth_sites_device(uint16_t* dev_out, int64_t n_sites, int height, int w
  * (vignetting factors, 2^15 = 1). */
 int tmh_synth_tables(int distribution, int height, int width, int32_t* ln16, int32_t* nz16,
                      int32_t* ey, int32_t* ex);
+
+/* ---- site-image input: GPU inflate of HDF5 gzip chunks ------------------
+ * Replaces the deflate filter libhdf5 runs under h5py for every chunk of a
+ * ChannelImageFile's /array (tmlib/models/file.py:322-351,
+ * tmlib/readers.py:367-389; written by file.py:353-363, writers.py:384-387):
+ * each chunk is an independent zlib stream (RFC 1950/1951), decoded by one
+ * GPU lane.  The compressed chunks of many files (libtmh5's
+ * tmh5_read_raw_chunks fills the same table layout) sit in one device
+ * buffer; tmh_inflate_device writes chunk i's raw_len decompressed bytes at
+ * dev_raw + raw_off and its status (TMH_Z_*; 0 = ok) -- byte-identical to
+ * zlib's inflate, Adler-32 checked.  tmh_place_chunks_device then copies
+ * every chunk's rows into dev_images[image][height][width] (elem_bytes per
+ * element), clipping edge chunks to the dataset's extent. */
+#define TMH_ZCHUNK_STORED 1 /* the deflate filter was skipped: raw bytes stored */
+typedef struct tmh_zchunk {
+  int64_t src_off;    /* the chunk's zlib stream in the compressed buffer */
+  int64_t src_len;
+  int64_t raw_off;    /* its decompressed bytes in the raw buffer */
+  int64_t raw_len;    /* chunk_rows * chunk_cols * elem_bytes */
+  int64_t image;      /* destination image of tmh_place_chunks_device */
+  int32_t row0, col0; /* chunk origin in the image, elements */
+  int32_t flags;      /* TMH_ZCHUNK_STORED */
+  int32_t reserved;
+} tmh_zchunk;
+#define TMH_Z_OK 0
+#define TMH_Z_HEADER 1     /* not a zlib stream (CM/CINFO/FCHECK/FDICT) */
+#define TMH_Z_BLOCKTYPE 2  /* deflate block type 3 */
+#define TMH_Z_CODE 3       /* a code the block's Huffman tables do not hold */
+#define TMH_Z_DIST 4       /* a back-reference before the start of the chunk */
+#define TMH_Z_OVERFLOW 5   /* more than raw_len bytes */
+#define TMH_Z_INPUT 6      /* ran past the chunk's bytes / bad offsets */
+#define TMH_Z_ADLER 7      /* Adler-32 mismatch */
+#define TMH_Z_SIZE 8       /* fewer than raw_len bytes */
+#define TMH_Z_STORED 9     /* stored block LEN / NLEN mismatch */
+#define TMH_Z_TABLE 10     /* invalid code lengths (over-subscribed, no end code) */
+int tmh_inflate_device(const uint8_t* dev_src, int64_t src_bytes, const tmh_zchunk* dev_chunks,
+                       int64_t n_chunks, uint8_t* dev_raw, int64_t raw_bytes, int32_t* dev_status,
+                       void* stream);
+int tmh_place_chunks_device(const uint8_t* dev_raw, const tmh_zchunk* dev_chunks, int64_t n_chunks,
+                            int height, int width, int elem_bytes, int chunk_rows, int chunk_cols,
+                            void* dev_images, void* stream);
 
 /* ---- device memory helpers for callers without another allocator -------- */
 int tmh_malloc_device(void** dev_ptr, size_t bytes);

@@ -1,0 +1,58 @@
+// Host build of the GPU inflate core (tmlibrary_amd/csrc/inflate_core.h) for
+// tests/test_inflate_host.py: the same decode code, run lane by lane on the
+// CPU, so its output can be compared with zlib byte for byte without a GPU.
+//   inflate_host TABLE BLOB RAW_BYTES OUT STATUS
+// TABLE: tmh_zchunk records; BLOB: the compressed bytes; writes RAW_BYTES of
+// decompressed output and one int32 status per chunk.
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+static inline uint32_t bitrev32(uint32_t x) {
+  x = ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
+  x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);
+  x = ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);
+  x = ((x >> 8) & 0x00FF00FFu) | ((x & 0x00FF00FFu) << 8);
+  return (x >> 16) | (x << 16);
+}
+#define TMH_ZDEV static inline
+#define TMH_ZCONST static const
+#define TMH_ZBITREV32(x) bitrev32(x)
+#define __restrict__
+#include "../tmlibrary_amd/csrc/inflate_core.h"
+
+static std::vector<uint8_t> slurp(const char* p) {
+  FILE* f = fopen(p, "rb");
+  if (!f) exit(2);
+  std::vector<uint8_t> v;
+  uint8_t buf[1 << 16];
+  size_t n;
+  while ((n = fread(buf, 1, sizeof buf, f)) > 0) v.insert(v.end(), buf, buf + n);
+  fclose(f);
+  return v;
+}
+
+int main(int argc, char** argv) {
+  if (argc != 6) return 2;
+  const std::vector<uint8_t> tab = slurp(argv[1]), blob = slurp(argv[2]);
+  const long long raw_bytes = atoll(argv[3]);
+  const size_t n = tab.size() / sizeof(tmh_zchunk);
+  std::vector<uint8_t> out((size_t)raw_bytes + 1, 0);
+  std::vector<int32_t> st(n, 0);
+  static tmh::ZShared z;
+  for (size_t i = 0; i < n; ++i) {
+    tmh_zchunk c;
+    memcpy(&c, tab.data() + i * sizeof(tmh_zchunk), sizeof c);
+    st[i] = tmh::inflate_stream(blob.data(), (int64_t)blob.size(), c, out.data(), raw_bytes, z,
+                                (int)(i % tmh::kZW));
+  }
+  FILE* fo = fopen(argv[4], "wb");
+  fwrite(out.data(), 1, (size_t)raw_bytes, fo);
+  fclose(fo);
+  FILE* fs = fopen(argv[5], "wb");
+  fwrite(st.data(), 4, n, fs);
+  fclose(fs);
+  return 0;
+}

@@ -1044,6 +1044,13 @@ void tmh_corrector_destroy(tmh_corrector* c) {
 int tmh_corrector_set_option(tmh_corrector* c, int option, int value) {
   return guard([&] {
     TMH_CHECK(c, TMH_EINVAL, "corrector is NULL");
+    if (option == TMH_OPT_FUSED_CUS) {
+      int cus = 256;
+      TMH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+      TMH_CHECK(value >= 0 && value <= cus, TMH_EINVAL, "fused CUs must be 0..CU count");
+      c->n_wg = value ? value : cus;
+      return;
+    }
     if (!c->host.set(option, value)) throw Error{TMH_EINVAL, "unknown corrector option"};
   });
 }
@@ -1503,6 +1510,32 @@ int tmh_synth_tables(int distribution, int height, int width, int32_t* ln16, int
     TMH_CHECK(distribution >= TMH_SYNTH_STANDARD && distribution <= TMH_SYNTH_UNIFORM, TMH_EINVAL,
               "unknown distribution");
     synth_tables_host(distribution, height, width, ln16, nz16, ey, ex);
+  });
+}
+
+int tmh_inflate_device(const uint8_t* dev_src, int64_t src_bytes, const tmh_zchunk* dev_chunks,
+                       int64_t n_chunks, uint8_t* dev_raw, int64_t raw_bytes, int32_t* dev_status,
+                       void* stream) {
+  return guard([&] {
+    TMH_CHECK(n_chunks >= 0 && src_bytes >= 0 && raw_bytes >= 0, TMH_EINVAL, "bad sizes");
+    if (n_chunks == 0) return;
+    TMH_CHECK(dev_src && dev_chunks && dev_raw && dev_status, TMH_EINVAL, "bad arguments");
+    launch_inflate(dev_src, src_bytes, dev_chunks, n_chunks, dev_raw, raw_bytes, dev_status,
+                   (hipStream_t)stream);
+  });
+}
+
+int tmh_place_chunks_device(const uint8_t* dev_raw, const tmh_zchunk* dev_chunks, int64_t n_chunks,
+                            int height, int width, int elem_bytes, int chunk_rows, int chunk_cols,
+                            void* dev_images, void* stream) {
+  return guard([&] {
+    TMH_CHECK(n_chunks >= 0 && height > 0 && width > 0 && chunk_rows > 0 && chunk_cols > 0 &&
+                  (elem_bytes == 1 || elem_bytes == 2 || elem_bytes == 4 || elem_bytes == 8),
+              TMH_EINVAL, "bad geometry");
+    if (n_chunks == 0) return;
+    TMH_CHECK(dev_raw && dev_chunks && dev_images, TMH_EINVAL, "bad arguments");
+    launch_place_chunks(dev_raw, dev_chunks, n_chunks, height, width, elem_bytes, chunk_rows,
+                        chunk_cols, static_cast<uint8_t*>(dev_images), (hipStream_t)stream);
   });
 }
 

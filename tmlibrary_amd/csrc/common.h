@@ -287,6 +287,13 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
                      const double2* coef64, const RefineConst* rc, int log_transform,
                      const tmh_window* d_win, int lo, int hi, uint8_t* lut8, hipStream_t s,
                      double zero_log10 = -10.0);
+// site-image input (inflate_kernels.hip)
+void launch_inflate(const uint8_t* src, int64_t src_bytes, const tmh_zchunk* chunks,
+                    int64_t n_chunks, uint8_t* dst, int64_t dst_bytes, int32_t* status,
+                    hipStream_t s);
+void launch_place_chunks(const uint8_t* raw, const tmh_zchunk* chunks, int64_t n_chunks,
+                         int height, int width, int esize, int chunk_rows, int chunk_cols,
+                         uint8_t* images, hipStream_t s);
 void launch_clip_u16(const uint16_t* in, uint16_t* out, int64_t n, int lo, int hi, hipStream_t s);
 void launch_synth(uint16_t* out, int64_t n_sites, int H, int W, uint64_t seed, int channel,
                   int64_t first_site, int dist, hipStream_t s);

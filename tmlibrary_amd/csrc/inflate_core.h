@@ -1,0 +1,360 @@
+// Deflate decode of one zlib stream per GPU lane: the core of k_inflate
+// (inflate_kernels.hip), kept free of HIP headers so the same code also
+// builds for the host (tests/inflate_host.cpp: the decoder checked
+// byte-for-byte against zlib on CPU).  See inflate_kernels.hip.
+#pragma once
+
+#include <cstdint>
+
+#include "../../include/tmhip.h"
+
+#ifndef TMH_ZDEV
+#define TMH_ZDEV __device__ __forceinline__
+#define TMH_ZCONST __constant__
+#define TMH_ZBITREV32(x) __builtin_bitreverse32(x)
+#endif
+
+namespace tmh {
+
+namespace {
+
+constexpr int kZW = 64;  // lanes per workgroup (one wave); one stream per lane
+
+// LDS layout: u16 arrays [n][kZW]
+constexpr int kLsym = 288, kDsym = 32, kLens = 320;
+struct ZShared {
+  uint16_t llim[16][kZW];   // left-justified limit of code length l (index 1..15)
+  uint16_t lbase[16][kZW];  // symbol index base of code length l (mod 2^16)
+  uint16_t lsym[kLsym][kZW];
+  uint16_t dlim[16][kZW];
+  uint16_t dbase[16][kZW];
+  uint16_t dsym[kDsym][kZW];
+  uint16_t tmp[16][kZW];    // table build: counts, then offsets
+  uint8_t lens[kLens][kZW]; // code lengths of a dynamic block
+};
+
+// status codes (tmhip.h TMH_Z_*)
+constexpr int kZOk = 0, kZHeader = 1, kZBlockType = 2, kZCode = 3, kZDist = 4, kZOverflow = 5,
+              kZInput = 6, kZAdler = 7, kZSize = 8, kZStored = 9, kZTable = 10;
+
+struct Bits {
+  uint64_t bb;  // bit buffer (LSB first)
+  int nb;       // valid bits
+  int64_t p;    // next aligned dword to load (byte offset into src)
+  int64_t end;  // src bytes (loads at or past it read 0)
+  int64_t used; // bits consumed so far
+};
+
+// the aligned dword at byte p; bytes at or past `end` (the buffer's size) read 0
+TMH_ZDEV uint32_t ld32(const uint8_t* src, int64_t p, int64_t end) {
+  if (p + 4 <= end) return *reinterpret_cast<const uint32_t*>(src + p);
+  uint32_t v = 0;
+  for (int i = 0; i < 4; ++i)
+    if (p + i < end) v |= (uint32_t)src[p + i] << (8 * i);
+  return v;
+}
+
+TMH_ZDEV void refill(Bits& b, const uint8_t* src) {
+  if (b.nb <= 32) {
+    b.bb |= (uint64_t)ld32(src, b.p, b.end) << b.nb;
+    b.p += 4;
+    b.nb += 32;
+  }
+}
+
+TMH_ZDEV uint32_t getb(Bits& b, const uint8_t* src, int n) {
+  refill(b, src);
+  const uint32_t v = (uint32_t)(b.bb & ((1ull << n) - 1ull));
+  b.bb >>= n;
+  b.nb -= n;
+  b.used += n;
+  return v;
+}
+
+// Canonical Huffman decode: v = the next 15 bits in code order (bit-reversed
+// peek); the code length is the smallest l with v < lim[l] (lim
+// non-decreasing), found by binary search; returns -1 for a code the table
+// does not hold.
+TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, uint16_t (*lim)[kZW],
+                                       uint16_t (*base)[kZW], uint16_t (*sym)[kZW], int nsym,
+                                       int lane) {
+  refill(b, src);
+  const uint32_t v = TMH_ZBITREV32((uint32_t)b.bb) >> 17;
+  int l = 0;  // largest l with lim[l] <= v (lim[0] = 0)
+#pragma unroll
+  for (int step = 8; step >= 1; step >>= 1)
+    if (l + step <= 15 && v >= (uint32_t)lim[l + step][lane]) l += step;
+  const int len = l + 1;
+  if (len > 15) return -1;
+  const uint32_t code = v >> (15 - len);
+  b.bb >>= len;
+  b.nb -= len;
+  b.used += len;
+  // in range for every code hbuild accepted; clamped so no input can index past the table
+  const uint32_t i = (uint16_t)(base[len][lane] + code);
+  return sym[i < (uint32_t)nsym ? i : (uint32_t)nsym - 1u][lane];
+}
+
+// Canonical tables from n code lengths (lens column of this lane, or the
+// fixed code); returns false for an over-subscribed code.
+TMH_ZDEV bool hbuild(ZShared& z, int lane, const uint8_t (*lens)[kZW], int off,
+                                       int n, uint16_t (*lim)[kZW], uint16_t (*base)[kZW],
+                                       uint16_t (*sym)[kZW]) {
+  for (int l = 0; l < 16; ++l) z.tmp[l][lane] = 0;
+  for (int s = 0; s < n; ++s) {
+    const int l = lens[off + s][lane];
+    if (l) z.tmp[l][lane] += 1;
+  }
+  uint32_t code = 0, offs = 0;
+  for (int l = 1; l < 16; ++l) {
+    const uint32_t cnt = z.tmp[l][lane];
+    base[l][lane] = (uint16_t)(offs - code);
+    code += cnt;
+    if (code > (1u << l)) return false;
+    lim[l][lane] = (uint16_t)(code << (15 - l));
+    z.tmp[l][lane] = (uint16_t)offs;
+    offs += cnt;
+    code <<= 1;
+  }
+  for (int s = 0; s < n; ++s) {
+    const int l = lens[off + s][lane];
+    if (l) {
+      const int i = z.tmp[l][lane];
+      sym[i][lane] = (uint16_t)s;
+      z.tmp[l][lane] = (uint16_t)(i + 1);
+    }
+  }
+  return true;
+}
+
+TMH_ZCONST uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+TMH_ZCONST uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
+                                      2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+TMH_ZCONST uint16_t kDistBase[30] = {1,    2,    3,    4,    5,    7,     9,     13,    17,  25,
+                                       33,   49,   65,   97,   129,  193,   257,   385,   513, 769,
+                                       1025, 1537, 2049, 3073, 4097, 6145,  8193,  12289, 16385,
+                                       24577};
+TMH_ZCONST uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2,  3,  3,  4,  4,  5,  5,  6,
+                                       6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+TMH_ZCONST uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+enum : int { kStBlock = 0, kStData = 1, kStStored = 2, kStTrailer = 3, kStDone = 4 };
+
+// Decode chunk c (one zlib stream) into dst; returns its TMH_Z_* status.
+TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
+                            const tmh_zchunk& c, uint8_t* __restrict__ dst, int64_t dst_bytes,
+                            ZShared& z, int lane) {
+  int err = kZOk;
+  if (c.src_off < 0 || c.src_len < 0 || c.src_off + c.src_len > src_bytes || c.raw_off < 0 ||
+      c.raw_len < 0 || c.raw_off + c.raw_len > dst_bytes) {
+    return kZInput;
+  }
+  uint8_t* out = dst + c.raw_off;
+  const int64_t olen = c.raw_len;
+  if (c.flags & 1) {  // the HDF5 filter was skipped: raw bytes
+    if (c.src_len != c.raw_len) return kZSize;
+    for (int64_t i = 0; i < olen; ++i) out[i] = src[c.src_off + i];
+    return kZOk;
+  }
+  Bits b;
+  {
+    const int64_t a = c.src_off & ~3ll;
+    const int sh = (int)(c.src_off - a) * 8;
+    b.end = c.src_off + c.src_len;
+    b.bb = (uint64_t)ld32(src, a, src_bytes) >> sh;
+    b.nb = 32 - sh;
+    b.p = a + 4;
+    b.used = 0;
+  }
+  // loads past the stream's own bytes read the next stream's (harmless: the
+  // consumed-bit count is checked) but never past the buffer
+  b.end = src_bytes;
+  const int64_t in_bits = (int64_t)c.src_len * 8;
+  // zlib header (RFC 1950): CM = 8, CINFO <= 7, FCHECK, no preset dictionary
+  const uint32_t cmf = getb(b, src, 8), flg = getb(b, src, 8);
+  if ((cmf & 15u) != 8u || (cmf >> 4) > 7u || ((cmf << 8) | flg) % 31u != 0u || (flg & 0x20u))
+    err = kZHeader;
+  int64_t o = 0;                // bytes written
+  uint32_t s1 = 1, s2 = 0, k = 0;  // Adler-32 (reduced every 5,552 bytes)
+  int state = err ? kStDone : kStBlock;
+  int last = 0;
+  int64_t stored_left = 0;
+  auto put = [&](uint32_t v) {
+    out[o++] = (uint8_t)v;
+    s1 += v;
+    s2 += s1;
+    if (++k == 5552u) {
+      s1 %= 65521u;
+      s2 %= 65521u;
+      k = 0;
+    }
+  };
+  while (state != kStDone) {
+    if (b.used > in_bits + 64) {  // ran far past the stream: corrupt
+      err = kZInput;
+      break;
+    }
+    if (state == kStData) {
+      const int s = hdecode(b, src, z.llim, z.lbase, z.lsym, kLsym, lane);
+      if (s < 256) {
+        if (s < 0) {
+          err = kZCode;
+          break;
+        }
+        if (o >= olen) {
+          err = kZOverflow;
+          break;
+        }
+        put((uint32_t)s);
+      } else if (s == 256) {
+        state = last ? kStTrailer : kStBlock;
+      } else {
+        const int li = s - 257;
+        if (li >= 29) {
+          err = kZCode;
+          break;
+        }
+        const int len = kLenBase[li] + (int)getb(b, src, kLenExtra[li]);
+        const int ds = hdecode(b, src, z.dlim, z.dbase, z.dsym, kDsym, lane);
+        if (ds < 0 || ds >= 30) {
+          err = kZCode;
+          break;
+        }
+        const int dist = kDistBase[ds] + (int)getb(b, src, kDistExtra[ds]);
+        if (dist > o) {
+          err = kZDist;
+          break;
+        }
+        if (o + len > olen) {
+          err = kZOverflow;
+          break;
+        }
+        const uint8_t* from = out + o - dist;
+        if (dist >= len) {  // no overlap: all loads, then the stores
+          for (int i = 0; i < len; i += 4) {
+            uint32_t v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = i + j < len ? from[i + j] : 0u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (i + j < len) put(v[j]);
+          }
+        } else {  // overlapping: byte by byte (each load sees the previous store)
+          for (int i = 0; i < len; ++i) put(from[i]);
+        }
+      }
+    } else if (state == kStBlock) {
+      last = (int)getb(b, src, 1);
+      const uint32_t type = getb(b, src, 2);
+      if (type == 0) {  // stored: byte-align, LEN, NLEN
+        const int drop = b.nb & 7;
+        b.bb >>= drop;
+        b.nb -= drop;
+        b.used += drop;
+        const uint32_t len = getb(b, src, 16), nlen = getb(b, src, 16);
+        if ((len ^ nlen) != 0xFFFFu) {
+          err = kZStored;
+          break;
+        }
+        stored_left = len;
+        state = kStStored;
+      } else if (type == 1) {  // fixed Huffman code
+        for (int s = 0; s < 288; ++s)
+          z.lens[s][lane] = (uint8_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
+        for (int s = 0; s < 32; ++s) z.lens[288 + s][lane] = 5;
+        if (!hbuild(z, lane, z.lens, 0, 288, z.llim, z.lbase, z.lsym) ||
+            !hbuild(z, lane, z.lens, 288, 32, z.dlim, z.dbase, z.dsym)) {
+          err = kZTable;
+          break;
+        }
+        state = kStData;
+      } else if (type == 2) {  // dynamic: code-length code, then the two codes' lengths
+        const int hlit = (int)getb(b, src, 5) + 257, hdist = (int)getb(b, src, 5) + 1;
+        const int hclen = (int)getb(b, src, 4) + 4;
+        if (hlit > 286 || hdist > 30) {
+          err = kZTable;
+          break;
+        }
+        for (int i = 0; i < 19; ++i) z.lens[i][lane] = 0;
+        for (int i = 0; i < hclen; ++i) z.lens[kClOrder[i]][lane] = (uint8_t)getb(b, src, 3);
+        // the code-length code lives in the distance tables until the real ones are built
+        if (!hbuild(z, lane, z.lens, 0, 19, z.dlim, z.dbase, z.dsym)) {
+          err = kZTable;
+          break;
+        }
+        int n = 0;
+        const int total = hlit + hdist;
+        while (n < total) {
+          const int s = hdecode(b, src, z.dlim, z.dbase, z.dsym, kDsym, lane);
+          if (s < 0) {
+            err = kZCode;
+            break;
+          }
+          int rep = 0, val = 0;
+          if (s < 16) {
+            z.lens[n++][lane] = (uint8_t)s;
+            continue;
+          } else if (s == 16) {
+            if (n == 0) {
+              err = kZTable;
+              break;
+            }
+            val = z.lens[n - 1][lane];
+            rep = 3 + (int)getb(b, src, 2);
+          } else if (s == 17) {
+            rep = 3 + (int)getb(b, src, 3);
+          } else {
+            rep = 11 + (int)getb(b, src, 7);
+          }
+          if (n + rep > total) {
+            err = kZTable;
+            break;
+          }
+          for (int i = 0; i < rep; ++i) z.lens[n++][lane] = (uint8_t)val;
+        }
+        if (err) break;
+        if (z.lens[256][lane] == 0 ||  // no end-of-block code
+            !hbuild(z, lane, z.lens, 0, hlit, z.llim, z.lbase, z.lsym) ||
+            !hbuild(z, lane, z.lens, hlit, hdist, z.dlim, z.dbase, z.dsym)) {
+          err = kZTable;
+          break;
+        }
+        state = kStData;
+      } else {
+        err = kZBlockType;
+        break;
+      }
+    } else if (state == kStStored) {
+      if (stored_left == 0) {
+        state = last ? kStTrailer : kStBlock;
+        continue;
+      }
+      if (o >= olen) {
+        err = kZOverflow;
+        break;
+      }
+      put(getb(b, src, 8));
+      --stored_left;
+    } else {  // trailer: byte-align, Adler-32 big-endian
+      const int drop = b.nb & 7;
+      b.bb >>= drop;
+      b.nb -= drop;
+      b.used += drop;
+      uint32_t want = 0;
+      for (int i = 0; i < 4; ++i) want = (want << 8) | getb(b, src, 8);
+      s1 %= 65521u;
+      s2 %= 65521u;
+      if (((s2 << 16) | s1) != want) err = kZAdler;
+      else if (o != olen) err = kZSize;
+      else if (b.used > in_bits) err = kZInput;
+      state = kStDone;
+    }
+  }
+  return err;
+}
+
+
+}  // namespace
+
+}  // namespace tmh

@@ -16,6 +16,9 @@
 #include <hdf5.h>
 #include <zlib.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -292,6 +295,169 @@ void read_one_parallel(const char* path, uint8_t* out, int height, int width, in
 }
 
 }  // namespace
+
+// Raw chunks for the GPU inflate (tmh_inflate_device): per file, under
+// libhdf5's lock, the /array layout checks and every chunk's (coordinates,
+// filter mask, file address, size); then the compressed bytes are read with
+// pread() by n_threads workers outside the lock, straight into the caller's
+// blob.  (H5Dread_chunk would move the bytes under the lock; the addresses
+// H5Dget_chunk_info reports are relative to the file's base address, the
+// userblock size.)
+namespace {
+
+struct FileChunks {
+  std::vector<tmh5_chunk> ch;  // src_off relative to the file's first chunk in the blob
+  std::vector<int64_t> addr;   // absolute file offset of each chunk
+  int64_t bytes = 0;
+};
+
+void file_chunks(const char* path, int64_t image, int h, int w, int esize, hsize_t* ch,
+                 FileChunks& fc) {
+  Hid f(H5Fopen(path, H5F_ACC_RDONLY, H5P_DEFAULT), H5Fclose);
+  hsize_t ub = 0;
+  {
+    Hid fcpl(H5Fget_create_plist(f), H5Pclose);
+    H5Pget_userblock(fcpl, &ub);
+  }
+  Hid ds(H5Dopen2(f, "array", H5P_DEFAULT), H5Dclose);
+  Hid t(H5Dget_type(ds), H5Tclose);
+  Hid sp(H5Dget_space(ds), H5Sclose);
+  hsize_t d[2] = {0, 0};
+  if (H5Sget_simple_extent_ndims(sp) != 2) throw H5Err{-22, std::string(path) + ": /array is not 2-D"};
+  H5Sget_simple_extent_dims(sp, d, nullptr);
+  if ((int)d[0] != h || (int)d[1] != w || (int)H5Tget_size(t) != esize ||
+      H5Tget_class(t) != H5T_INTEGER || H5Tget_sign(t) != H5T_SGN_NONE)
+    throw H5Err{-22, std::string(path) + ": shape or dtype differs from the first image"};
+  Hid dcpl(H5Dget_create_plist(ds), H5Pclose);
+  hsize_t c[2] = {0, 0};
+  unsigned flags = 0, cd[8];
+  size_t ncd = 8;
+  if (H5Pget_layout(dcpl) != H5D_CHUNKED || H5Pget_nfilters(dcpl) != 1 ||
+      H5Tget_order(t) != H5T_ORDER_LE || H5Pget_chunk(dcpl, 2, c) != 2 ||
+      H5Pget_filter2(dcpl, 0, &flags, &ncd, cd, 0, nullptr, nullptr) != H5Z_FILTER_DEFLATE)
+    throw H5Err{-95, std::string(path) + ": /array is not chunked with the deflate filter only"};
+  if (ch[0] == 0) {
+    ch[0] = c[0];
+    ch[1] = c[1];
+  } else if (c[0] != ch[0] || c[1] != ch[1]) {
+    throw H5Err{-95, std::string(path) + ": chunk shape differs from the first image"};
+  }
+  hsize_t n = 0;
+  if (H5Dget_num_chunks(ds, sp, &n) < 0) throw H5Err{-5, "H5Dget_num_chunks failed"};
+  if (n != ((d[0] + c[0] - 1) / c[0]) * ((d[1] + c[1] - 1) / c[1]))  // unwritten chunks: fill values
+    throw H5Err{-95, std::string(path) + ": /array has unwritten chunks"};
+  const int64_t raw = (int64_t)(c[0] * c[1]) * esize;
+  fc.ch.resize(n);
+  fc.addr.resize(n);
+  fc.bytes = 0;
+  for (hsize_t i = 0; i < n; ++i) {
+    hsize_t coord[2];
+    unsigned fmask = 0;
+    haddr_t addr;
+    hsize_t size = 0;
+    if (H5Dget_chunk_info(ds, sp, i, coord, &fmask, &addr, &size) < 0)
+      throw H5Err{-5, "H5Dget_chunk_info failed"};
+    tmh5_chunk& e = fc.ch[i];
+    e.src_off = fc.bytes;
+    e.src_len = (int64_t)size;
+    e.raw_len = raw;
+    e.image = image;
+    e.row0 = (int32_t)coord[0];
+    e.col0 = (int32_t)coord[1];
+    e.flags = (fmask & 1u) ? 1 : 0;  // deflate skipped for this chunk: stored
+    e.reserved = 0;
+    fc.addr[i] = (int64_t)(ub + addr);
+    fc.bytes += (int64_t)size;
+  }
+}
+
+}  // namespace
+
+int tmh5_read_raw_chunks(const char* const* paths, int64_t n_files, int n_threads, uint8_t* blob,
+                         int64_t blob_cap, tmh5_chunk* table, int64_t table_cap,
+                         int64_t* blob_used, int64_t* n_chunks, int32_t* geom) {
+  return guard([&] {
+    silence();
+    if (n_files < 0 || (n_files > 0 && !paths) || !blob_used || !n_chunks || !geom)
+      throw H5Err{-22, "bad arguments"};
+    *blob_used = 0;
+    *n_chunks = 0;
+    if (n_files == 0) return;
+    int h = 0, w = 0, bits = 0;
+    int rc = tmh5_channel_image_shape(paths[0], &h, &w, &bits);
+    if (rc) throw H5Err{rc, g_err};
+    const int esize = bits / 8;
+    hsize_t ch[2] = {0, 0};
+    std::vector<FileChunks> fc((size_t)n_files);
+    for (int64_t i = 0; i < n_files; ++i) file_chunks(paths[i], i, h, w, esize, ch, fc[i]);
+    int64_t total = 0, nch = 0;
+    for (auto& f : fc) {
+      total += f.bytes;
+      nch += (int64_t)f.ch.size();
+    }
+    geom[0] = h;
+    geom[1] = w;
+    geom[2] = esize;
+    geom[3] = (int32_t)ch[0];
+    geom[4] = (int32_t)ch[1];
+    *blob_used = total;
+    *n_chunks = nch;
+    if (total > blob_cap || nch > table_cap || (total && !blob) || (nch && !table))
+      throw H5Err{-28, "raw chunk buffers too small"};
+    // table: blob offsets and raw offsets (chunk raw bytes, file order)
+    int64_t off = 0, k = 0;
+    const int64_t raw = (int64_t)(ch[0] * ch[1]) * esize;
+    for (auto& f : fc) {
+      for (auto& e : f.ch) {
+        tmh5_chunk t = e;
+        t.src_off += off;
+        t.raw_off = k * raw;
+        table[k++] = t;
+      }
+      off += f.bytes;
+    }
+    // the bytes, one file per task, outside the HDF5 lock
+    std::vector<int64_t> base((size_t)n_files, 0);
+    for (int64_t i = 1; i < n_files; ++i) base[i] = base[i - 1] + fc[i - 1].bytes;
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(n_threads > 0 ? n_threads : 1, n_files));
+    std::atomic<int64_t> next{0};
+    std::atomic<bool> failed{false};
+    std::string first_err;
+    std::mutex m;
+    auto work = [&] {
+      for (;;) {
+        const int64_t i = next.fetch_add(1);
+        if (i >= n_files || failed.load()) return;
+        const int fd = open(paths[i], O_RDONLY);
+        bool ok = fd >= 0;
+        for (size_t j = 0; ok && j < fc[i].ch.size(); ++j) {
+          uint8_t* dst = blob + base[i] + fc[i].ch[j].src_off;
+          int64_t left = fc[i].ch[j].src_len, pos = fc[i].addr[j];
+          while (left > 0) {
+            const ssize_t r = pread(fd, dst, (size_t)left, (off_t)pos);
+            if (r <= 0) {
+              ok = false;
+              break;
+            }
+            dst += r;
+            pos += r;
+            left -= r;
+          }
+        }
+        if (fd >= 0) close(fd);
+        if (!ok) {
+          std::lock_guard<std::mutex> lk(m);
+          if (!failed.exchange(true)) first_err = std::string(paths[i]) + ": reading chunks failed";
+        }
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    if (failed) throw H5Err{-5, first_err};
+  });
+}
 
 int tmh5_read_channel_images(const char* const* paths, int64_t n_files, void* out, int n_threads) {
   return guard([&] {

@@ -27,6 +27,7 @@ TMH_OPT_FUSED_CONFIG = 1
 TMH_OPT_WELFORD_PARTS = 2
 TMH_OPT_COPY_THREADS = 4
 TMH_OPT_HOST_STAGING = 5
+TMH_OPT_FUSED_CUS = 8
 TMH_SYNTH_STANDARD = 0
 TMH_SYNTH_BRIGHT = 1
 TMH_SYNTH_UNIFORM = 2
@@ -91,6 +92,8 @@ SIGNATURES = {
     "tmh_correct_chain_u8": (_I, [_P, _P, _P, _I64, _P, _I, _I]),
     "tmh_synth_sites_device": (_I, [_P, _I64, _I, _I, C.c_uint64, _I, _I64, _I, _P]),
     "tmh_synth_tables": (_I, [_I, _I, _I, _P, _P, _P, _P]),
+    "tmh_inflate_device": (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _P]),
+    "tmh_place_chunks_device": (_I, [_P, _P, _I64, _I, _I, _I, _I, _I, _P, _P]),
     "tmh_malloc_device": (_I, [C.POINTER(_P), C.c_size_t]),
     "tmh_free_device": (_I, [_P]),
     "tmh_memcpy": (_I, [_P, _P, C.c_size_t, _I, _P]),
@@ -103,6 +106,20 @@ SIGNATURES = {
 #: struct tmh_window (include/tmhip.h) as a numpy record: one alignment window per site
 WINDOW_DTYPE = np.dtype([("src_r0", np.int32), ("src_c0", np.int32), ("dst_r0", np.int32),
                          ("dst_c0", np.int32), ("rows", np.int32), ("cols", np.int32)])
+
+
+#: struct tmh_zchunk (include/tmhip.h): one HDF5 gzip chunk of the input path
+ZCHUNK_DTYPE = np.dtype([("src_off", np.int64), ("src_len", np.int64), ("raw_off", np.int64),
+                         ("raw_len", np.int64), ("image", np.int64), ("row0", np.int32),
+                         ("col0", np.int32), ("flags", np.int32), ("reserved", np.int32)])
+assert ZCHUNK_DTYPE.itemsize == 56
+TMH_ZCHUNK_STORED = 1
+#: tmh_inflate_device per-chunk status codes (TMH_Z_*)
+Z_STATUS = {0: "ok", 1: "not a zlib stream", 2: "invalid deflate block type",
+            3: "invalid Huffman code", 4: "back-reference before the chunk start",
+            5: "more output than the chunk holds", 6: "ran past the chunk's bytes",
+            7: "Adler-32 mismatch", 8: "less output than the chunk holds",
+            9: "stored block length mismatch", 10: "invalid code lengths"}
 
 
 class HipUnavailableError(RuntimeError):

@@ -1,0 +1,133 @@
+"""GPU decode of channel image files: HDF5 gzip chunks inflated on the device.
+
+The reference reads every site with h5py (tmlib/models/file.py:322-351,
+tmlib/readers.py:367-389), i.e. libhdf5's deflate filter runs zlib's inflate
+on the host, one chunk after another -- on the GPU box's 16 granted cores that
+caps the corilla job at ~290 sites/s (profiles/r3/input_path_threads_r3l.jsonl).
+Here the host only copies the still-compressed chunks out of the files
+(libtmh5 ``tmh5_read_raw_chunks``: HDF5 metadata under its lock, the bytes by
+parallel ``pread``), the compressed bytes cross PCIe, and libtmhip inflates
+every chunk on the GPU (``tmh_inflate_device``: one lane per zlib stream,
+byte-identical to zlib, Adler-32 checked) and places the chunks' rows into a
+device ``[n, H, W]`` site buffer (``tmh_place_chunks_device``) that the
+statistics pass reads in place.
+
+No CPU fallback inside: a file the GPU path cannot take (not chunked with the
+deflate filter only) raises ``RawChunksUnsupported`` and the caller decides
+(``IllumstatsCalculator`` decodes such blocks on the host, as the reference).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from tmlibrary_amd import hip
+from tmlibrary_amd.models.file import read_raw_chunks
+
+
+class DeviceChunkDecoder(object):
+    """Inflate blocks of channel image files into device site buffers.
+
+    Device buffers (compressed bytes, chunk table, raw chunks, statuses) and
+    pinned host staging are kept across calls and grown on demand.  ``decode``
+    enqueues on ``stream`` and returns; ``check()`` (called by the next
+    ``decode`` of the same slot, or explicitly) raises if any chunk failed."""
+
+    def __init__(self, device=None, stream=None, slots=2, n_threads=None):
+        import torch
+        self.torch = torch
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.stream = stream if stream is not None else torch.cuda.Stream(self.device)
+        self.n_threads = n_threads
+        self.slots = [dict() for _ in range(max(1, slots))]
+        self.k = 0
+
+    def _grow(self, slot, name, n, dtype, pinned=False):
+        torch = self.torch
+        t = slot.get(name)
+        if t is None or t.numel() < n:
+            n = max(int(n * 1.25), 1)
+            if pinned:
+                t = torch.empty(n, dtype=dtype, pin_memory=True)
+            else:
+                t = torch.empty(n, dtype=dtype, device=self.device)
+            slot[name] = t
+        return t
+
+    def decode(self, paths, out_ptr, n_out=None):
+        """Decode ``paths`` into the device buffer at ``out_ptr`` ([n, H, W] of
+        the files' dtype, contiguous).  Returns (H, W, elem_bytes).  The work is
+        queued on ``self.stream``; the slot's buffers are reused two calls later
+        (the caller orders its consumers after ``self.stream``)."""
+        torch = self.torch
+        L = hip.lib()
+        slot = self.slots[self.k % len(self.slots)]
+        self.k += 1
+        if slot.get("event") is not None:
+            slot["event"].synchronize()  # the slot's previous block is done
+            self._raise_failed(slot)
+        hb = slot.get("h_blob")
+        ht = slot.get("h_tab")
+        blob, table, geom = read_raw_chunks(
+            paths, self.n_threads, None if hb is None else hb.numpy(),
+            None if ht is None else ht.numpy().view(hip.ZCHUNK_DTYPE))
+        H, W, es, cr, cc = geom
+        n = len(table)
+        if hb is None or blob.ctypes.data != hb.data_ptr():  # grown: pin the new size
+            hb = self._grow(slot, "h_blob", blob.nbytes, torch.uint8, pinned=True)
+            hb.numpy()[:blob.nbytes] = blob
+            slot["h_blob"] = hb
+        tb = table.view(np.uint8).reshape(-1)
+        if ht is None or table.ctypes.data != ht.data_ptr():
+            esz = hip.ZCHUNK_DTYPE.itemsize  # whole entries, so the pinned bytes view as a table
+            ht = torch.empty(max(int(n * 1.25), 1) * esz, dtype=torch.uint8, pin_memory=True)
+            ht.numpy()[:tb.nbytes] = tb
+            slot["h_tab"] = ht
+        d_src = self._grow(slot, "d_src", blob.nbytes + 16, torch.uint8)
+        d_tab = self._grow(slot, "d_tab", tb.nbytes, torch.uint8)
+        raw_bytes = n * cr * cc * es
+        d_raw = self._grow(slot, "d_raw", raw_bytes, torch.uint8)
+        d_st = self._grow(slot, "d_status", n, torch.int32)
+        with torch.cuda.stream(self.stream):
+            d_src[:blob.nbytes].copy_(hb[:blob.nbytes], non_blocking=True)
+            d_tab[:tb.nbytes].copy_(ht[:tb.nbytes], non_blocking=True)
+        sp = C.c_void_p(self.stream.cuda_stream)
+        hip.check(L.tmh_inflate_device(C.c_void_p(d_src.data_ptr()), blob.nbytes,
+                                       C.c_void_p(d_tab.data_ptr()), n,
+                                       C.c_void_p(d_raw.data_ptr()), raw_bytes,
+                                       C.c_void_p(d_st.data_ptr()), sp))
+        hip.check(L.tmh_place_chunks_device(C.c_void_p(d_raw.data_ptr()),
+                                            C.c_void_p(d_tab.data_ptr()), n, H, W, es, cr, cc,
+                                            C.c_void_p(int(out_ptr)), sp))
+        h_st = self._grow(slot, "h_status", n, torch.int32, pinned=True)
+        with torch.cuda.stream(self.stream):
+            h_st[:n].copy_(d_st[:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        slot["event"] = ev
+        slot["n"] = n
+        slot["paths"] = list(paths)
+        slot["images"] = table["image"].copy()
+        return H, W, es
+
+    def _raise_failed(self, slot):
+        n = slot.get("n", 0)
+        if not n:
+            return
+        st = slot["h_status"][:n].numpy()
+        bad = np.nonzero(st)[0]
+        slot["n"] = 0
+        if bad.size:
+            i = int(bad[0])
+            path = slot["paths"][int(slot["images"][i])]
+            raise IOError("%s: chunk %d: %s (%d of %d chunks failed to inflate)"
+                          % (path, i, hip.Z_STATUS.get(int(st[i]), "error %d" % st[i]),
+                             bad.size, n))
+
+    def check(self):
+        """Wait for every queued block; raise if a chunk failed to inflate."""
+        for slot in self.slots:
+            if slot.get("event") is not None:
+                slot["event"].synchronize()
+                self._raise_failed(slot)

@@ -46,7 +46,20 @@ _SIGS = {
                                                    C.c_void_p, C.c_int, C.c_int, C.c_int]),
     "tmh5_read_channel_images": (C.c_int, [C.POINTER(C.c_char_p), C.c_int64, C.c_void_p,
                                            C.c_int]),
+    "tmh5_read_raw_chunks": (C.c_int, [C.POINTER(C.c_char_p), C.c_int64, C.c_int, C.c_void_p,
+                                       C.c_int64, C.c_void_p, C.c_int64, C.POINTER(C.c_int64),
+                                       C.POINTER(C.c_int64), C.c_void_p]),
 }
+
+#: struct tmh5_chunk (include/tmh5.h) = struct tmh_zchunk (include/tmhip.h)
+CHUNK_DTYPE = np.dtype([("src_off", np.int64), ("src_len", np.int64), ("raw_off", np.int64),
+                        ("raw_len", np.int64), ("image", np.int64), ("row0", np.int32),
+                        ("col0", np.int32), ("flags", np.int32), ("reserved", np.int32)])
+
+
+class RawChunksUnsupported(IOError):
+    """A file's /array is not chunked with the deflate filter only (contiguous,
+    shuffle, other filters, unwritten chunks): decode it on the host."""
 
 
 def h5lib():
@@ -194,6 +207,41 @@ def read_channel_images(paths, n_threads=None, out=None):
     nt = default_decode_threads() if n_threads is None else int(n_threads)
     _check(L.tmh5_read_channel_images(arr, len(paths), out.ctypes.data, nt), paths[0])
     return out
+
+
+def read_raw_chunks(paths, n_threads=None, blob=None, table=None):
+    """The still-compressed chunks of channel image files for the GPU inflate
+    (libtmh5 tmh5_read_raw_chunks): returns (blob, table, geom) -- blob a
+    uint8 view holding every chunk's zlib stream, table a CHUNK_DTYPE array
+    (one entry per chunk: its bytes in blob, its decompressed bytes in a raw
+    buffer of len(table) full chunks, file index, origin), geom =
+    (height, width, elem_bytes, chunk_rows, chunk_cols).  ``blob`` / ``table``:
+    buffers to fill (e.g. pinned memory reused across calls); grown (fresh
+    numpy arrays) when too small.  Raises RawChunksUnsupported for files the
+    GPU path cannot take."""
+    paths = list(paths)
+    L = h5lib()
+    arr = (C.c_char_p * len(paths))(*[_b(p) for p in paths])
+    nt = default_decode_threads() if n_threads is None else int(n_threads)
+    geom = np.zeros(5, np.int32)
+    used, nch = C.c_int64(), C.c_int64()
+    for attempt in range(2):
+        bcap = 0 if blob is None else blob.nbytes
+        tcap = 0 if table is None else len(table)
+        rc = L.tmh5_read_raw_chunks(arr, len(paths), nt, None if blob is None else blob.ctypes.data,
+                                    bcap, None if table is None else table.ctypes.data, tcap,
+                                    C.byref(used), C.byref(nch), geom.ctypes.data)
+        if rc == -28 and attempt == 0:  # too small: size them and read again
+            if blob is None or blob.nbytes < used.value:
+                blob = np.empty(max(used.value, 1), np.uint8)
+            if table is None or len(table) < nch.value:
+                table = np.empty(max(nch.value, 1), CHUNK_DTYPE)
+            continue
+        if rc == -95:
+            raise RawChunksUnsupported(h5lib().tmh5_last_error().decode())
+        _check(rc, paths[0] if paths else "")
+        break
+    return blob[:used.value], table[:nch.value], tuple(int(x) for x in geom)
 
 
 class ChannelImageFile(object):

@@ -1,0 +1,26 @@
+#!/bin/bash
+# r4e: 4 channels x 432 sites forced-distributed: how much do the idle
+# candidate launches cost?  default vs forced (standard Welford, narrow fused:
+# no candidate launches), plus a kernel trace of the forced run
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+: > gpurun_out/dist432_r4e.jsonl
+run() {  # run TAG ARGS...
+  local tag=$1; shift
+  TMH_BENCH_FORCE_DIST=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \
+    timeout -k 10 300 python bench.py --layout sharded --channels 4 --sites 432 --steps 10 --warmup 3 \
+    --no-extras --cpu-sample 0 "$@" > gpurun_out/d.tmp 2>> gpurun_out/dist432_r4e.err || return $?
+  python3 -c "import json,sys; d=json.loads(open('gpurun_out/d.tmp').read().strip().splitlines()[-1]); print(json.dumps({'tag': sys.argv[1], 'value': d['value'], 'ms': d['ms_per_step'], 'check': d['check_vs_oracle'], 'k': {k: v['avg_ms'] for k, v in d['kernels'].items()}}))" $tag >> gpurun_out/dist432_r4e.jsonl
+  tail -1 gpurun_out/dist432_r4e.jsonl
+}
+run default || exit $?
+run forced --welford-parts 1 --fused-config 3 || exit $?
+run default || exit $?
+run forced --welford-parts 1 --fused-config 3 || exit $?
+run forced_cus192 --welford-parts 1 --fused-config 3 --fused-cus 192 || exit $?
+TMH_BENCH_FORCE_DIST=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29518 \
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace432f_r4e -o run -- \
+  python3 bench.py --layout sharded --channels 4 --sites 432 --steps 3 --warmup 1 --no-extras --cpu-sample 0 --no-profile --welford-parts 1 --fused-config 3 \
+  > gpurun_out/trace432f_r4e.log 2>&1 || exit $?
+echo r4e-ok
