@@ -125,6 +125,10 @@ int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites,
                      int log_transform, int64_t* zero_counts_out);
 int tmh_stats_update_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
                             int log_transform, void* stream);
+/* Per-site zero-pixel counts of the last tmh_stats_update_device call (its
+ * first n sites; n <= 4,096), copied to host_out on `stream` after the
+ * handle's queued work (asynchronous for pinned host_out). */
+int tmh_stats_zero_counts(tmh_stats* h, int64_t* host_out, int64_t n, void* stream);
 
 /* Split job pipeline (one read of the sites per pass):
  *   tmh_stats_update_welford_device  Welford only; the sites' percentile

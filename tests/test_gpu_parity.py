@@ -218,6 +218,24 @@ def test_smooth_and_correct_vs_golden(L, name):
         assert np.array_equal(clipped.array, want_clip)
 
 
+@pytest.mark.parametrize("shape", [(2160, 2560), (300, 217), (37, 53), (20, 30), (1, 300),
+                                   (300, 1), (5, 5)])
+def test_smooth_one_pass_bit_identical(L, shape, monkeypatch):
+    """The one-pass 2-D smoothing kernel (k_smooth_2d, sigma 5) equals the
+    two separable passes bit for bit, edges and planes narrower than the
+    kernel included, and matches the oracle."""
+    from tmlibrary_amd.image import smooth_f64
+    rng = np.random.default_rng(shape[0] * 7 + shape[1])
+    plane = rng.random(shape) * 4.0 + 1.0
+    one = smooth_f64(plane, 5)
+    monkeypatch.setenv("TMH_SMOOTH_2PASS", "1")
+    two = smooth_f64(plane, 5)
+    monkeypatch.delenv("TMH_SMOOTH_2PASS")
+    assert np.array_equal(one, two)
+    if plane.size <= 1e6:
+        assert np.allclose(one, orc.smooth_reflect(plane, 5), rtol=1e-10, atol=1e-13)
+
+
 @pytest.mark.parametrize("shape", [(1, 1), (1, 9), (3, 5), (20, 40), (40, 41), (41, 3), (7, 100)])
 def test_smooth_small_planes(L, shape):
     """Planes smaller than the 41-tap kernel (sigma 5, radius 20): the
@@ -509,9 +527,12 @@ def test_profile_counters(L):
     L.tmh_profile_enable(0)
 
 
-def test_run_job_end_to_end(L, tmp_path):
+@pytest.mark.parametrize("decode,block", [("host", 128), ("gpu", 128), ("gpu", 3)])
+def test_run_job_end_to_end(L, tmp_path, decode, block, caplog):
     """IllumstatsCalculator.run_job: gzip HDF5 sites in batch order -> GPU stats
-    -> IllumstatsFile (4 datasets) -> IllumstatsFile.get (smoothed)."""
+    -> IllumstatsFile (4 datasets) -> IllumstatsFile.get (smoothed).  The
+    sites decoded on the host (libhdf5 + zlib) or inflated on the GPU, in one
+    device block or in blocks of 3 (several blocks in flight): the same bits."""
     pytest.importorskip("tmlibrary_amd.models.file")
     from tmlibrary_amd.models import file as h5
     try:
@@ -527,7 +548,11 @@ def test_run_job_end_to_end(L, tmp_path):
         h5.write_channel_image(store.channel_image_file(100 + i).location, s)
     batch = {"id": 1, "channel_image_files_ids": [[100 + i] for i in range(len(sites))],
              "channel_id": 5}
-    IllumstatsCalculator(1, store=store, batch_size=2).run_job(batch)
+    with caplog.at_level("WARNING"):
+        IllumstatsCalculator(1, store=store, batch_size=2, decode=decode,
+                             device_block=block).run_job(batch)
+    n_warn = sum("image contains zero values" in r.message for r in caplog.records)
+    assert n_warn == sum(int(np.any(s == 0)) for s in sites)
     mean, std, keys, vals = h5.read_illumstats(store.illumstats_file(5).location)
     assert_close_rel(mean, g["mean"])
     assert_close_rel(std, g["std"])

@@ -494,11 +494,13 @@ int tmh_stats_reset(tmh_stats* h) {
       TMH_HIP(hipMemsetAsync(h->pooled_parts.p, 0, h->pooled_parts.n * 8, h->stream));
       h->hist_dirty = false;
     }
-    TMH_HIP(hipMemsetAsync(h->mean.p, 0, h->npx * 8, h->stream));
-    TMH_HIP(hipMemsetAsync(h->m2.p, 0, h->npx * 8, h->stream));
-    TMH_HIP(hipMemsetAsync(h->acc.p, 0, (size_t)h->Q * 8, h->stream));
-    TMH_HIP(hipMemsetAsync(h->pooled.p, 0, (size_t)kBins * 8, h->stream));
-    TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, h->stream));
+    ZeroList z;  // one launch for the job's fresh state
+    z.add(h->mean.p, h->npx);
+    z.add(h->m2.p, h->npx);
+    z.add(h->acc.p, h->Q);
+    z.add(h->pooled.p, kBins);
+    z.add(h->wide.p, 2);
+    launch_zero_u64(z, h->stream);
     h->wide_sites = 0;
     h->n = 0;
     h->n_deferred = 0;
@@ -603,6 +605,21 @@ int tmh_stats_update_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_s
   return guard([&] {
     TMH_CHECK(h && (dev_sites || n_sites == 0) && n_sites >= 0, TMH_EINVAL, "bad arguments");
     stats_update_dev(h, dev_sites, n_sites, log_transform, pick(h->stream, stream));
+  });
+}
+
+int tmh_stats_zero_counts(tmh_stats* h, int64_t* host_out, int64_t n, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && (host_out || n == 0) && n >= 0, TMH_EINVAL, "bad arguments");
+    TMH_CHECK(n <= h->last_batch && (size_t)n <= h->zeros.n, TMH_EINVAL,
+              "more sites than the last update held");
+    if (n == 0) return;
+    hipStream_t s = pick(h->stream, stream);
+    if (s != h->stream) {
+      TMH_HIP(hipEventRecord(h->ev_in, h->stream));
+      TMH_HIP(hipStreamWaitEvent(s, h->ev_in, 0));
+    }
+    TMH_HIP(hipMemcpyAsync(host_out, h->zeros.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
   });
 }
 

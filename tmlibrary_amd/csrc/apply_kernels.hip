@@ -113,6 +113,52 @@ __global__ __launch_bounds__(256) void k_smooth_axis1_wide(const SmPlanes pl, in
   out[(int64_t)y * W + x] = acc;
 }
 
+// Both axes in one pass for a compile-time radius: a workgroup owns TW =
+// 256 - 2R output columns x TH rows; its 256 threads first run the axis-0
+// taps down the tile's TW + 2R columns (halo columns are the reflected
+// columns, as the axis-1 pass reads them), keep the TH x 256 results in LDS,
+// then each thread runs the axis-1 taps along one output column.  Every tap
+// is added in the same order as k_smooth_axis0(_strip) then k_smooth_axis1,
+// so the result is bit-identical, without the intermediate plane's HBM
+// write and read (2 x 44 MB per plane at 2160 x 2560).
+template <int TH, int R>
+__global__ __launch_bounds__(256) void k_smooth_2d(const SmPlanes pl, int H, int W,
+                                                   const double* __restrict__ w) {
+  constexpr int CW = 256, TW = CW - 2 * R;
+  __shared__ double vt[TH][CW];
+  const double* __restrict__ in = pl.in[blockIdx.z];
+  double* __restrict__ out = pl.out[blockIdx.z];
+  const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
+  {
+    const int x = reflect_idx(x0 - R + (int)threadIdx.x, W);
+    double acc[TH];
+#pragma unroll
+    for (int t = 0; t < TH; ++t) acc[t] = 0.0;
+#pragma unroll
+    for (int u = 0; u < TH + 2 * R; ++u) {
+      const double v = in[(int64_t)reflect_idx(y0 + u - R, H) * W + x];
+#pragma unroll
+      for (int t = 0; t < TH; ++t) {
+        const int k = u - t;
+        if (k >= 0 && k <= 2 * R) acc[t] = fma(w[k], v, acc[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < TH; ++t) vt[t][threadIdx.x] = acc[t];
+  }
+  __syncthreads();
+  const int x = x0 + (int)threadIdx.x;
+  if ((int)threadIdx.x >= TW || x >= W) return;
+#pragma unroll 4
+  for (int t = 0; t < TH; ++t) {
+    if (y0 + t >= H) break;
+    double a = 0.0;
+#pragma unroll
+    for (int j = 0; j <= 2 * R; ++j) a = fma(w[j], vt[t][threadIdx.x + j], a);
+    out[(int64_t)(y0 + t) * W + x] = a;
+  }
+}
+
 // np planes (1 or 2): in[k] -> tmp[k] (axis 0) -> out[k] (axis 1)
 static void launch_smooth_planes(const double* const* in, double* const* out, double* const* tmp,
                                  int np, int H, int W, const double* d_w, int radius,
@@ -121,6 +167,15 @@ static void launch_smooth_planes(const double* const* in, double* const* out, do
   SmPlanes a0{{in[0], np > 1 ? in[1] : nullptr}, {tmp[0], np > 1 ? tmp[1] : nullptr}};
   SmPlanes a1{{tmp[0], np > 1 ? tmp[1] : nullptr}, {out[0], np > 1 ? out[1] : nullptr}};
   const dim3 grid((unsigned)cdiv(W, 256), (unsigned)H, (unsigned)np);
+  if (radius == 20 && W >= 2 * radius + 1 && !getenv("TMH_SMOOTH_2PASS")) {
+    // sigma = 5, the reference's default (image.py:1172): one pass, both axes
+    constexpr int TH = 16, TW = 256 - 2 * 20;
+    SmPlanes a{{in[0], np > 1 ? in[1] : nullptr}, {out[0], np > 1 ? out[1] : nullptr}};
+    const dim3 g((unsigned)cdiv(W, TW), (unsigned)cdiv(H, TH), (unsigned)np);
+    hipLaunchKernelGGL((k_smooth_2d<TH, 20>), g, dim3(256), 0, s, a, H, W, d_w);
+    TMH_HIP(hipGetLastError());
+    return;
+  }
   if (radius == 20) {  // sigma = 5, the reference's default (image.py:1172)
     // 16 rows per thread: 1,350 workgroups per plane at 2160x2560 (8 / 32 measured slower)
     const dim3 g2((unsigned)cdiv(W, 256), (unsigned)cdiv(H, 16), (unsigned)np);

@@ -214,6 +214,16 @@ void launch_merge1(const double* mean, int64_t n, int64_t npx, double* nmean, hi
 void launch_merge2(double* mean, const double* m2, int64_t n_r, const double* sum_nmean,
                    int64_t n_total, int64_t npx, double* m2c, hipStream_t s);
 void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s);
+struct ZeroList {
+  unsigned long long* p[8];
+  int64_t count[8];  // u64 elements
+  int n = 0;
+  void add(void* ptr, int64_t elems) {
+    p[n] = static_cast<unsigned long long*>(ptr);
+    count[n++] = elems;
+  }
+};
+void launch_zero_u64(const ZeroList& z, hipStream_t s);
 
 void launch_smooth(const double* in, double* out, double* tmp, int H, int W, const double* d_w,
                    int radius, hipStream_t s);

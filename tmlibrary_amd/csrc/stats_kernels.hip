@@ -1153,6 +1153,27 @@ void launch_merge2(double* mean, const double* m2, int64_t n_r, const double* su
   TMH_HIP(hipGetLastError());
 }
 
+// Zero several u64/f64 arrays in one launch (a job reset: mean, M2, the
+// percentile accumulator, the pooled histogram, the wide-group counters) --
+// one kernel instead of a fill launch per array.
+__global__ void k_zero_u64(const ZeroList z) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int k = 0; k < z.n; ++k) {
+    unsigned long long* p = z.p[k];
+    const int64_t n = z.count[k];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = 0ull;
+  }
+}
+
+void launch_zero_u64(const ZeroList& z, hipStream_t s) {
+  int64_t total = 0;
+  for (int k = 0; k < z.n; ++k) total += z.count[k];
+  if (!total) return;
+  const unsigned g = (unsigned)std::min<int64_t>(cdiv(total, 256 * 4), 2048);
+  hipLaunchKernelGGL(k_zero_u64, dim3(g), dim3(256), 0, s, z);
+  TMH_HIP(hipGetLastError());
+}
+
 __global__ void k_copy_f64(const double* __restrict__ src, double* __restrict__ dst, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) dst[i] = src[i];

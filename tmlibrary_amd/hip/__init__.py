@@ -56,6 +56,7 @@ SIGNATURES = {
     "tmh_stats_set_hist_device": (_I, [_P, _P, _P]),
     "tmh_stats_update": (_I, [_P, _P, _I64, _I, _P]),
     "tmh_stats_update_device": (_I, [_P, _P, _I64, _I, _P]),
+    "tmh_stats_zero_counts": (_I, [_P, _P, _I64, _P]),
     "tmh_stats_update_welford_device": (_I, [_P, _P, _I64, _I, _P]),
     "tmh_stats_update_welford_blocks_device": (_I, [_P, _P, _I, _I64, _I, _P]),
     "tmh_stats_finalize": (_I, [_P, _P, _P, _P, _P, _P]),

@@ -20,8 +20,9 @@ import threading
 import numpy as np
 
 from tmlibrary_amd.image import IllumstatsContainer
-from tmlibrary_amd.models.file import (ExperimentStore, channel_image_shape,
-                                       default_decode_threads, read_channel_images)
+from tmlibrary_amd.models.file import (ExperimentStore, RawChunksUnsupported,
+                                       channel_image_shape, default_decode_threads,
+                                       read_channel_images)
 from tmlibrary_amd.workflow.corilla.stats import OnlineStatistics
 
 logger = logging.getLogger(__name__)
@@ -53,10 +54,18 @@ def _file_id(fid):
 class IllumstatsCalculator(object):
     """Calculation of illumination statistics (corilla/api.py:31-146)."""
 
-    def __init__(self, experiment_id, store=None, batch_size=32, prefetch=2, decode_threads=None):
+    def __init__(self, experiment_id, store=None, batch_size=32, prefetch=2, decode_threads=None,
+                 decode="auto", device_block=128):
         """prefetch: blocks of ``batch_size`` files decoded concurrently ahead of
         the GPU update; decode_threads: inflate workers over all of them (None:
-        the cores granted, models/file.py:granted_cores)."""
+        the cores granted, models/file.py:granted_cores).
+
+        decode: where the sites' gzip chunks are inflated -- "gpu": the host
+        reads the compressed chunks, the GPU inflates them into a device
+        buffer the statistics pass reads in place (models/device_decode.py;
+        ``device_block`` files per block, two blocks in flight); "host":
+        libhdf5 + zlib on the cores; "auto": the GPU path when the files
+        allow it (uint16, chunked with the deflate filter only), else host."""
         self.experiment_id = experiment_id
         if store is None:
             raise ValueError("an ExperimentStore is required (no database in this build)")
@@ -68,6 +77,11 @@ class IllumstatsCalculator(object):
         self.decode_threads = decode_threads
         self._buffers = {}  # (block, H, W, dtype) -> reused block buffers (idle sets)
         self._buffers_lock = threading.Lock()
+        if decode not in ("auto", "gpu", "host"):
+            raise ValueError('decode must be "auto", "gpu" or "host"')
+        self.decode = decode
+        self.device_block = max(1, int(device_block))
+        self._dev = None  # device decode state, kept across jobs (buffers, decoder)
 
     def create_run_batches(self, args=None, channel_files=None, channel_names=None, seed=None):
         """One job per channel (corilla/api.py:45-105).
@@ -183,6 +197,52 @@ class IllumstatsCalculator(object):
             with self._buffers_lock:  # idle again: the next generator may reuse it
                 self._buffers.setdefault(key, []).append(bufs)
 
+    def _update_device(self, file_ids, stats):
+        """The job's sites through the GPU inflate into the statistics, in order:
+        block k+1's host chunk read and H2D copy overlap block k's inflate and
+        statistics update (decoder stream D, statistics stream S; two device
+        site buffers, each reused once S has consumed it)."""
+        import torch
+
+        from tmlibrary_amd.models.device_decode import DeviceChunkDecoder
+        from tmlibrary_amd.workflow.corilla.stats import log_zero_warnings
+        paths = [self.store.channel_image_file(f).location for f in file_ids]
+        H, W, dt = channel_image_shape(paths[0])
+        if np.dtype(dt) != np.uint16 or (H, W) != tuple(stats.image_dimensions):
+            raise RawChunksUnsupported("GPU decode takes uint16 sites of the job's shape")
+        B = self.device_block
+        dev = torch.device("cuda", torch.cuda.current_device())
+        st = self._dev
+        if st is None or st["key"] != (B, H, W):
+            st = self._dev = {
+                "key": (B, H, W),
+                "bufs": [torch.empty((B, H, W), dtype=torch.int16, device=dev) for _ in range(2)],
+                "dec": DeviceChunkDecoder(device=dev, slots=2, n_threads=self.decode_threads),
+                "S": torch.cuda.Stream(dev)}
+        dec, S, bufs = st["dec"], st["S"], st["bufs"]
+        zc = torch.zeros(len(file_ids), dtype=torch.int64, pin_memory=True).numpy()
+        used = [None, None]
+        try:
+            for k in range(0, len(file_ids), B):
+                b = (k // B) % 2
+                if used[b] is not None:
+                    dec.stream.wait_event(used[b])  # S has read the buffer's previous block
+                blk = paths[k:k + B]
+                dec.decode(blk, bufs[b].data_ptr())
+                ready = torch.cuda.Event()
+                ready.record(dec.stream)
+                S.wait_event(ready)
+                for fid in file_ids[k:k + B]:
+                    logger.info("update statistics for image: %d", fid)
+                stats.update_device(bufs[b].data_ptr(), len(blk), stream=S.cuda_stream,
+                                    zero_counts=zc[k:k + len(blk)])
+                used[b] = torch.cuda.Event()
+                used[b].record(S)
+        finally:
+            S.synchronize()
+        dec.check()  # a chunk that failed to inflate raises here
+        log_zero_warnings(zc)
+
     def run_job(self, batch, assume_clean_state=False):
         """corilla/api.py:115-146."""
         file_ids = [_file_id(f) for f in batch["channel_image_files_ids"]]
@@ -191,10 +251,20 @@ class IllumstatsCalculator(object):
         stats = OnlineStatistics(image_dimensions=first.dimensions[0:2],
                                  batch_size=self.batch_size)
         try:
-            for ids, sites in self._blocks(file_ids):
-                for fid in ids:
-                    logger.info("update statistics for image: %d", fid)
-                stats.update_batch(sites)
+            done = False
+            if self.decode != "host":
+                try:
+                    self._update_device(file_ids, stats)
+                    done = True
+                except RawChunksUnsupported:
+                    if self.decode == "gpu":
+                        raise
+                    logger.info("channel image files not GPU-decodable: decoding on the host")
+            if not done:
+                for ids, sites in self._blocks(file_ids):
+                    for fid in ids:
+                        logger.info("update statistics for image: %d", fid)
+                    stats.update_batch(sites)
             stats_file = self.store.illumstats_file(batch["channel_id"])
             logger.info("write calculated statistics to file")
             illumstats = IllumstatsContainer(stats.mean, stats.std, stats.percentiles)

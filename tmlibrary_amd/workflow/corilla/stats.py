@@ -33,6 +33,13 @@ logger = logging.getLogger(__name__)
 DEFAULT_BATCH = 32
 
 
+def log_zero_warnings(zero_counts):
+    """stats.py:81-82: one 'image contains zero values' warning per site with a
+    zero pixel (log-transformed updates)."""
+    for _ in range(int(np.count_nonzero(np.asarray(zero_counts)))):
+        logger.warning("image contains zero values")
+
+
 class OnlineStatistics(object):
     """Welford mean/variance + percentile accumulator (stats.py:35-121)."""
 
@@ -118,6 +125,33 @@ class OnlineStatistics(object):
             raise ValueError("sites must be uint8 or uint16")
         self._flush()
         self._push(sites, bool(log_transform))
+
+    def update_device(self, dev_sites, n_sites, log_transform=True, stream=None,
+                      zero_counts=None):
+        """Add ``n_sites`` sites that already sit in device memory ([n, H, W]
+        uint16 at address ``dev_sites``, e.g. decoded by the GPU inflate), in
+        order, on ``stream`` (a HIP stream handle; None: the handle's).
+        ``zero_counts``: a host int64 array (pinned: asynchronous) that receives
+        the sites' zero-pixel counts; the caller logs the warnings
+        (``log_zero_warnings``) once the stream has reached them.  Without it
+        the counts are read back here (synchronising) and logged at once."""
+        n = int(n_sites)
+        if n <= 0:
+            return
+        self._flush()
+        L = hip.lib()
+        sp = None if stream is None else C.c_void_p(int(stream))
+        hip.check(L.tmh_stats_update_device(self._h, C.c_void_p(int(dev_sites)), n,
+                                            int(bool(log_transform)), sp))
+        self._cache = None
+        own = zero_counts is None
+        if own:
+            zero_counts = np.zeros(n, dtype=np.int64)
+        hip.check(L.tmh_stats_zero_counts(self._h, hip.ptr(zero_counts), n, sp))
+        if own:
+            hip.check(L.tmh_synchronize(sp))
+            if log_transform:
+                log_zero_warnings(zero_counts)
 
     def _push(self, sites, log_transform):
         n = sites.shape[0]

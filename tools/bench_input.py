@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--width", type=int, default=2560)
     ap.add_argument("--no-gpu", action="store_true")
+    ap.add_argument("--device-block", type=int, default=128,
+                    help="files per device block of run_job's GPU decode")
     ap.add_argument("--repeat", type=int, default=4,
                     help="run_job batch = the files listed this many times (a longer job from "
                          "the same files; the page cache holds them, decode stays CPU-bound)")
@@ -88,26 +90,35 @@ def main():
             store = ExperimentStore(root)
             batch = {"id": 1, "channel_id": 1,
                      "channel_image_files_ids": [[i] for i in range(a.sites)]}
-            calc = IllumstatsCalculator(1, store=store, batch_size=32, decode_threads=a.threads)
-            calc.run_job(batch)  # warm-up (library load, GPU init)
-            t0 = time.perf_counter()
-            calc.run_job(batch)
-            t_one = time.perf_counter() - t0
-            res["run_job_sites_per_s"] = round(a.sites / t_one, 1)
-            # a longer job over the same files: the per-job fixed cost (first
-            # block's decode before the GPU can start, finalize, smoothing-free
-            # statistics read-back, HDF5 write) is then amortised, and the
-            # marginal rate between the two lengths is the steady-state one
-            ids = [[i] for i in range(a.sites)] * a.repeat
-            big = {"id": 1, "channel_id": 1, "channel_image_files_ids": ids}
-            t0 = time.perf_counter()
-            calc.run_job(big)
-            t_big = time.perf_counter() - t0
-            res["run_job_%d_sites_per_s" % len(ids)] = round(len(ids) / t_big, 1)
-            res["run_job_marginal_sites_per_s"] = round(
-                (len(ids) - a.sites) / max(t_big - t_one, 1e-9), 1)
-            res["run_job_fixed_s_est"] = round(
-                t_one - a.sites / max(res["run_job_marginal_sites_per_s"], 1e-9), 3)
+            for dec in ("host", "gpu"):
+                calc = IllumstatsCalculator(1, store=store, batch_size=32, decode_threads=a.threads,
+                                            decode=dec, device_block=a.device_block)
+                calc.run_job(batch)  # warm-up (library load, GPU init, buffers)
+                t0 = time.perf_counter()
+                calc.run_job(batch)
+                t_one = time.perf_counter() - t0
+                pre = "run_job" if dec == "host" else "run_job_gpu_decode"
+                res["%s_sites_per_s" % pre] = round(a.sites / t_one, 1)
+                # a longer job over the same files: the per-job fixed cost (first
+                # block's decode before the GPU can start, finalize, smoothing-free
+                # statistics read-back, HDF5 write) is then amortised, and the
+                # marginal rate between the two lengths is the steady-state one
+                ids = [[i] for i in range(a.sites)] * a.repeat
+                big = {"id": 1, "channel_id": 1, "channel_image_files_ids": ids}
+                t0 = time.perf_counter()
+                calc.run_job(big)
+                t_big = time.perf_counter() - t0
+                res["%s_%d_sites_per_s" % (pre, len(ids))] = round(len(ids) / t_big, 1)
+                res["%s_marginal_sites_per_s" % pre] = round(
+                    (len(ids) - a.sites) / max(t_big - t_one, 1e-9), 1)
+                res["%s_fixed_s_est" % pre] = round(
+                    t_one - a.sites / max(res["%s_marginal_sites_per_s" % pre], 1e-9), 3)
+                if dec == "gpu":  # same statistics either way
+                    m_gpu = h5.read_illumstats(store.illumstats_file(1).location)
+                else:
+                    m_host = h5.read_illumstats(store.illumstats_file(1).location)
+            res["gpu_decode_same_results"] = bool(all(np.array_equal(x, y)
+                                                      for x, y in zip(m_host, m_gpu)))
         res["cpus_visible"] = os.cpu_count()
         res["granted_cores"] = h5.granted_cores()
         try:
