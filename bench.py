@@ -312,6 +312,65 @@ def bench_host_path(H, W, n_sites=64, reps=3):
             "job_sites_per_s": round(n_sites / (t_stats + t_corr), 1)}
 
 
+def bench_input_path(H, W, dev, distinct=8, block=64, reps=2):
+    """§8(f) rank 1 beside the headline: site images from gzip HDF5 files
+    (the reference's ChannelImageFile layout, level 4, h5py-style 270 x 320
+    chunks) into HBM -- decoded on the host (libhdf5 + zlib on the granted
+    cores) vs inflated on the GPU (compressed chunks read by pread, PCIe,
+    tmh_inflate_device + placement); the GPU result is checked against the
+    host one.  Never the headline."""
+    import shutil
+    import tempfile
+
+    import torch
+
+    from tmlibrary_amd.models.device_decode import DeviceChunkDecoder
+    from tmlibrary_amd.models.file import (default_decode_threads, read_channel_images,
+                                           write_channel_image)
+    from tmlibrary_amd.synth import synth_exact_host
+    d = tempfile.mkdtemp(prefix="tmh_bench_input_")
+    try:
+        files = []
+        for i in range(distinct):
+            p = os.path.join(d, "channel_image_file_%d.h5" % i)
+            write_channel_image(p, synth_exact_host(H, W, SEED, 0, i), 4, chunks=(270, 320))
+            files.append(p)
+        paths = [files[i % distinct] for i in range(block)]
+        nt = default_decode_threads()
+        host = np.empty((block, H, W), np.uint16)
+        read_channel_images(paths, nt, out=host)
+        t_host = 1e30
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            read_channel_images(paths, nt, out=host)
+            t_host = min(t_host, time.perf_counter() - t0)
+        out = torch.empty((block, H, W), dtype=torch.int16, device=dev)
+        dec = DeviceChunkDecoder(device=dev, n_threads=nt)
+        dec.decode(paths, out.data_ptr())
+        dec.check()
+        torch.cuda.synchronize(dev)
+        same = bool(np.array_equal(out.cpu().numpy().view(np.uint16), host))
+        t_gpu = 1e30
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            dec.decode(paths, out.data_ptr())
+            dec.check()
+            torch.cuda.synchronize(dev)
+            t_gpu = min(t_gpu, time.perf_counter() - t0)
+        comp = sum(os.path.getsize(p) for p in paths)
+        del out
+        return {"workload": "%d gzip HDF5 site files of %dx%d uint16 (%d distinct, cycled; level 4, "
+                            "270x320 chunks) decoded into HBM" % (block, H, W, distinct),
+                "compressed_MB_per_site": round(comp / block / 1e6, 2),
+                "host_threads": nt,
+                "host_inflate_sites_per_s": round(block / t_host, 1),
+                "gpu_inflate_sites_per_s": round(block / t_gpu, 1),
+                "gpu_equals_host": same}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def link_rates(dev, nbytes=2 << 30):
     """Pinned host <-> HBM copy rates on this box (GB/s): H2D alone, D2H alone,
     both at once on two streams -- the PCIe roofline of --stream-host."""
@@ -1322,6 +1381,10 @@ def main():
         else:
             extras["chain_u8"] = bench_chain(L, ch0.corr, ch0.S_ptr, S, H, W, dev, sp)
         extras["host_path"] = bench_host_path(H, W)
+        try:
+            extras["input_path"] = bench_input_path(H, W, dev)
+        except Exception as e:  # libhdf5 missing on the box: report, never fail the headline
+            extras["input_path"] = {"error": "%s: %s" % (type(e).__name__, e)}
 
     if rank == 0:
         site_bytes = npx * 2

@@ -279,7 +279,11 @@ int tmh_correct_u16_device(tmh_corrector* c, const uint16_t* dev_in, uint16_t* d
  * into h (see tmh_stats_update_welford_device).  Stream contract: the work
  * runs on `stream` (NULL: the corrector's stream), ordered after everything
  * already queued on h's stream, and h's stream waits for it before any later
- * work on h -- the two handles may live on different streams. */
+ * work on h -- the two handles may live on different streams.  dev_in and
+ * dev_out must not overlap (the pass re-reads its input after storing
+ * outputs: f64 fixups, packed-counter recounts; overlapping runs are
+ * rejected with TMH_EINVAL, and the block entry point's tables must name
+ * separate blocks). */
 int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* dev_in,
                                 uint16_t* dev_out, int64_t n_sites, int clip_lo, int clip_hi,
                                 void* stream);

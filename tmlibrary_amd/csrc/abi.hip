@@ -1363,6 +1363,11 @@ int tmh_correct_u16_hist_device(tmh_corrector* c, tmh_stats* h, const uint16_t* 
   return guard([&] {
     TMH_CHECK(c && h && (dev_in && dev_out || n_sites == 0) && n_sites >= 0, TMH_EINVAL,
               "bad arguments");
+    // the pass re-reads its input after storing outputs (f64 fixups, packed
+    // counter recounts): input and output must not overlap
+    TMH_CHECK(n_sites == 0 || dev_in + n_sites * h->npx <= dev_out ||
+                  dev_out + n_sites * h->npx <= dev_in,
+              TMH_EINVAL, "input and output sites must not overlap");
     correct_hist_dev(c, h, dev_in, dev_out, n_sites, clip_lo, clip_hi, stream, SiteTab{});
   });
 }
@@ -1373,6 +1378,8 @@ int tmh_correct_u16_hist_blocks_device(tmh_corrector* c, tmh_stats* h,
                                        int64_t n_sites, int clip_lo, int clip_hi, void* stream) {
   return guard([&] {
     TMH_CHECK(c && h && n_sites >= 0 && dev_out_blocks, TMH_EINVAL, "bad arguments");
+    TMH_CHECK(dev_in_blocks != (const uint16_t* const*)dev_out_blocks, TMH_EINVAL,
+              "input and output block tables must differ");
     const SiteTab tab = blocked_tab(dev_in_blocks, dev_out_blocks, block_shift, h->npx);
     correct_hist_dev(c, h, nullptr, nullptr, n_sites, clip_lo, clip_hi, stream, tab);
   });

@@ -321,10 +321,11 @@ __global__ __launch_bounds__(NT) void k_chain_u8(const uint16_t* __restrict__ in
 //    pixels beyond their own bound (the launch-wide T = 1 / (K1 a_max + K2)
 //    with whole groups refined ran 0.30 ms of f64 fixups per 3,456 bench
 //    sites);
-//  * no min/max before the cast: every |o| >= 1 / K2 (< 2^18) is flagged, and
-//    the f64 refinement rewrites all 8 pixels of a flagged group, so only
-//    values where v_cvt_i32_f32 truncates exactly as the x86 cast does reach
-//    the stored bytes unrefined; NaN converts to 0 on both;
+//  * no min/max before the cast: every |o| >= 1 / K2 (< 2^18) fails its own
+//    f32 bound and is refined in f64; k_fix_chain refines only the pixels
+//    beyond their own bound and keeps the streamed byte of the others, whose
+//    |o| < 0.998 / K2 < 2^18 -- there v_cvt_i32_f32 truncates exactly as the
+//    x86 cast does, so no clamp is needed; NaN converts to 0 on both;
 //  * ZADD: a zero pixel's floor as x + zf instead of max(x, zf) -- two pixels
 //    per v_pk_add_f32; exact for zf < 2^-25 (x >= 1 plus zf rounds to x);
 //  * the table bytes packed with v_perm (3 per 4 bytes) instead of shifts,

@@ -22,7 +22,13 @@ constexpr int kZW = 64;  // lanes per workgroup (one wave); one stream per lane
 
 // LDS layout: u16 arrays [n][kZW]
 constexpr int kLsym = 288, kDsym = 32, kLens = 320;
+// first-level tables: the codes of at most kLFast (literal/length) or kDFast
+// (distance) bits decode with one lookup of the peeked bits (entry = symbol
+// | length << 12, 0 = a longer code: the canonical search below)
+constexpr int kLFast = 9, kDFast = 6;
 struct ZShared {
+  uint16_t lfast[1 << kLFast][kZW];
+  uint16_t dfast[1 << kDFast][kZW];
   uint16_t llim[16][kZW];   // left-justified limit of code length l (index 1..15)
   uint16_t lbase[16][kZW];  // symbol index base of code length l (mod 2^16)
   uint16_t lsym[kLsym][kZW];
@@ -71,14 +77,23 @@ TMH_ZDEV uint32_t getb(Bits& b, const uint8_t* src, int n) {
   return v;
 }
 
-// Canonical Huffman decode: v = the next 15 bits in code order (bit-reversed
-// peek); the code length is the smallest l with v < lim[l] (lim
-// non-decreasing), found by binary search; returns -1 for a code the table
-// does not hold.
-TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, uint16_t (*lim)[kZW],
-                                       uint16_t (*base)[kZW], uint16_t (*sym)[kZW], int nsym,
-                                       int lane) {
+// Canonical Huffman decode.  A code of at most FB bits is one lookup of the
+// next FB stream bits in `fast`; a longer one: v = the next 15 bits in code
+// order (bit-reversed peek), the code length is the smallest l with v <
+// lim[l] (lim non-decreasing), found by binary search.  Returns -1 for a code
+// the table does not hold.
+template <int FB>
+TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, uint16_t (*fast)[kZW], uint16_t (*lim)[kZW],
+                     uint16_t (*base)[kZW], uint16_t (*sym)[kZW], int nsym, int lane) {
   refill(b, src);
+  const uint32_t e = fast[(uint32_t)b.bb & ((1u << FB) - 1u)][lane];
+  if (e >> 12) {
+    const int len = (int)(e >> 12);
+    b.bb >>= len;
+    b.nb -= len;
+    b.used += len;
+    return (int)(e & 0x1FFu);
+  }
   const uint32_t v = TMH_ZBITREV32((uint32_t)b.bb) >> 17;
   int l = 0;  // largest l with lim[l] <= v (lim[0] = 0)
 #pragma unroll
@@ -96,10 +111,13 @@ TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, uint16_t (*lim)[kZW],
 }
 
 // Canonical tables from n code lengths (lens column of this lane, or the
-// fixed code); returns false for an over-subscribed code.
-TMH_ZDEV bool hbuild(ZShared& z, int lane, const uint8_t (*lens)[kZW], int off,
-                                       int n, uint16_t (*lim)[kZW], uint16_t (*base)[kZW],
-                                       uint16_t (*sym)[kZW]) {
+// fixed code), with the first-level table of the codes of at most FB bits;
+// returns false for an over-subscribed code.
+template <int FB>
+TMH_ZDEV bool hbuild(ZShared& z, int lane, const uint8_t (*lens)[kZW], int off, int n,
+                     uint16_t (*fast)[kZW], uint16_t (*lim)[kZW], uint16_t (*base)[kZW],
+                     uint16_t (*sym)[kZW]) {
+  for (int i = 0; i < (1 << FB); ++i) fast[i][lane] = 0;
   for (int l = 0; l < 16; ++l) z.tmp[l][lane] = 0;
   for (int s = 0; s < n; ++s) {
     const int l = lens[off + s][lane];
@@ -122,6 +140,12 @@ TMH_ZDEV bool hbuild(ZShared& z, int lane, const uint8_t (*lens)[kZW], int off,
       const int i = z.tmp[l][lane];
       sym[i][lane] = (uint16_t)s;
       z.tmp[l][lane] = (uint16_t)(i + 1);
+      if (l <= FB) {  // its canonical code, stream bit order: every FB-bit peek starting with it
+        const uint32_t code = (uint16_t)(i - base[l][lane]);
+        const uint32_t rev = TMH_ZBITREV32(code) >> (32 - l);
+        const uint16_t ent = (uint16_t)(s | (l << 12));
+        for (uint32_t k = rev; k < (1u << FB); k += 1u << l) fast[k][lane] = ent;
+      }
     }
   }
   return true;
@@ -196,7 +220,7 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
       break;
     }
     if (state == kStData) {
-      const int s = hdecode(b, src, z.llim, z.lbase, z.lsym, kLsym, lane);
+      const int s = hdecode<kLFast>(b, src, z.lfast, z.llim, z.lbase, z.lsym, kLsym, lane);
       if (s < 256) {
         if (s < 0) {
           err = kZCode;
@@ -216,7 +240,7 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
           break;
         }
         const int len = kLenBase[li] + (int)getb(b, src, kLenExtra[li]);
-        const int ds = hdecode(b, src, z.dlim, z.dbase, z.dsym, kDsym, lane);
+        const int ds = hdecode<kDFast>(b, src, z.dfast, z.dlim, z.dbase, z.dsym, kDsym, lane);
         if (ds < 0 || ds >= 30) {
           err = kZCode;
           break;
@@ -263,8 +287,8 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
         for (int s = 0; s < 288; ++s)
           z.lens[s][lane] = (uint8_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
         for (int s = 0; s < 32; ++s) z.lens[288 + s][lane] = 5;
-        if (!hbuild(z, lane, z.lens, 0, 288, z.llim, z.lbase, z.lsym) ||
-            !hbuild(z, lane, z.lens, 288, 32, z.dlim, z.dbase, z.dsym)) {
+        if (!hbuild<kLFast>(z, lane, z.lens, 0, 288, z.lfast, z.llim, z.lbase, z.lsym) ||
+            !hbuild<kDFast>(z, lane, z.lens, 288, 32, z.dfast, z.dlim, z.dbase, z.dsym)) {
           err = kZTable;
           break;
         }
@@ -279,14 +303,14 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
         for (int i = 0; i < 19; ++i) z.lens[i][lane] = 0;
         for (int i = 0; i < hclen; ++i) z.lens[kClOrder[i]][lane] = (uint8_t)getb(b, src, 3);
         // the code-length code lives in the distance tables until the real ones are built
-        if (!hbuild(z, lane, z.lens, 0, 19, z.dlim, z.dbase, z.dsym)) {
+        if (!hbuild<kDFast>(z, lane, z.lens, 0, 19, z.dfast, z.dlim, z.dbase, z.dsym)) {
           err = kZTable;
           break;
         }
         int n = 0;
         const int total = hlit + hdist;
         while (n < total) {
-          const int s = hdecode(b, src, z.dlim, z.dbase, z.dsym, kDsym, lane);
+          const int s = hdecode<kDFast>(b, src, z.dfast, z.dlim, z.dbase, z.dsym, kDsym, lane);
           if (s < 0) {
             err = kZCode;
             break;
@@ -315,8 +339,8 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
         }
         if (err) break;
         if (z.lens[256][lane] == 0 ||  // no end-of-block code
-            !hbuild(z, lane, z.lens, 0, hlit, z.llim, z.lbase, z.lsym) ||
-            !hbuild(z, lane, z.lens, hlit, hdist, z.dlim, z.dbase, z.dsym)) {
+            !hbuild<kLFast>(z, lane, z.lens, 0, hlit, z.lfast, z.llim, z.lbase, z.lsym) ||
+            !hbuild<kDFast>(z, lane, z.lens, hlit, hdist, z.dfast, z.dlim, z.dbase, z.dsym)) {
           err = kZTable;
           break;
         }
