@@ -375,8 +375,16 @@ typedef struct tmh_zchunk {
 #define TMH_Z_SIZE 8       /* fewer than raw_len bytes */
 #define TMH_Z_STORED 9     /* stored block LEN / NLEN mismatch */
 #define TMH_Z_TABLE 10     /* invalid code lengths (over-subscribed, no end code) */
+/* Two kernels: each lane Huffman-decodes one chunk, writing its literal bytes
+ * and listing its back-references in dev_scratch (no lane waits on a load of
+ * earlier output); then one wave per chunk resolves the list in order, 64
+ * matches at a time, and checks the Adler-32.  raw_max: the largest raw_len
+ * of the table; dev_scratch: at least tmh_inflate_scratch_bytes(n_chunks,
+ * raw_max) bytes. */
+int64_t tmh_inflate_scratch_bytes(int64_t n_chunks, int64_t raw_max);
 int tmh_inflate_device(const uint8_t* dev_src, int64_t src_bytes, const tmh_zchunk* dev_chunks,
-                       int64_t n_chunks, uint8_t* dev_raw, int64_t raw_bytes, int32_t* dev_status,
+                       int64_t n_chunks, int64_t raw_max, uint8_t* dev_raw, int64_t raw_bytes,
+                       void* dev_scratch, int64_t scratch_bytes, int32_t* dev_status,
                        void* stream);
 int tmh_place_chunks_device(const uint8_t* dev_raw, const tmh_zchunk* dev_chunks, int64_t n_chunks,
                             int height, int width, int elem_bytes, int chunk_rows, int chunk_cols,

@@ -18,6 +18,7 @@ static inline uint32_t bitrev32(uint32_t x) {
   return (x >> 16) | (x << 16);
 }
 #define TMH_ZDEV static inline
+#define TMH_ZHD static inline
 #define TMH_ZCONST static const
 #define TMH_ZBITREV32(x) bitrev32(x)
 #define __restrict__
@@ -42,12 +43,21 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> out((size_t)raw_bytes + 1, 0);
   std::vector<int32_t> st(n, 0);
   static tmh::ZShared z;
+  std::vector<tmh_zchunk> cs(n);
+  int64_t raw_max = 0;
   for (size_t i = 0; i < n; ++i) {
-    tmh_zchunk c;
-    memcpy(&c, tab.data() + i * sizeof(tmh_zchunk), sizeof c);
-    st[i] = tmh::inflate_stream(blob.data(), (int64_t)blob.size(), c, out.data(), raw_bytes, z,
-                                (int)(i % tmh::kZW));
+    memcpy(&cs[i], tab.data() + i * sizeof(tmh_zchunk), sizeof(tmh_zchunk));
+    if (cs[i].raw_len > raw_max) raw_max = cs[i].raw_len;
   }
+  const int64_t mw = tmh::match_words(raw_max);
+  std::vector<uint32_t> ml((size_t)(mw * (int64_t)n + 2), 0);
+  const tmh::ZCodes tc{tmh::kLenCode, tmh::kDistCode};
+  for (size_t i = 0; i < n; ++i)  // phase 1, lane by lane
+    st[i] = tmh::inflate_tokens(blob.data(), (int64_t)blob.size(), cs[i], out.data(), raw_bytes,
+                                ml.data() + i * mw, mw / 2 - 1, tc, z, (int)(i % tmh::kZW));
+  for (size_t i = 0; i < n; ++i)  // phase 2
+    if (st[i] == 0 && cs[i].raw_off >= 0 && cs[i].raw_off + cs[i].raw_len <= raw_bytes)
+      st[i] = tmh::resolve_matches(out.data() + cs[i].raw_off, cs[i].raw_len, ml.data() + i * mw);
   FILE* fo = fopen(argv[4], "wb");
   fwrite(out.data(), 1, (size_t)raw_bytes, fo);
   fclose(fo);

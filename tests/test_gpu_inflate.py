@@ -76,14 +76,18 @@ def _run(L, streams, raw_lens=None):
         roff += rl
     d_src, d_tab = Dev(L, max(len(blob), 1)), Dev(L, tab.nbytes)
     d_raw, d_st = Dev(L, max(roff, 1)), Dev(L, 4 * n)
+    raw_max = int(tab["raw_len"].max())
+    scr = int(L.tmh_inflate_scratch_bytes(n, raw_max))
+    d_scr = Dev(L, scr)
     d_src.put(np.frombuffer(blob, np.uint8))
     d_tab.put(tab)
-    hip.check(L.tmh_inflate_device(d_src.p, len(blob), d_tab.p, n, d_raw.p, roff, d_st.p, None))
+    hip.check(L.tmh_inflate_device(d_src.p, len(blob), d_tab.p, n, raw_max, d_raw.p, roff,
+                                   d_scr.p, scr, d_st.p, None))
     assert L.tmh_synchronize(None) == 0
     rawout = d_raw.get(np.uint8, (max(roff, 1),))
     st = d_st.get(np.int32, (n,))
     outs = [rawout[t["raw_off"]:t["raw_off"] + t["raw_len"]].tobytes() for t in tab]
-    for b in (d_src, d_tab, d_raw, d_st):
+    for b in (d_src, d_tab, d_raw, d_st, d_scr):
         b.free()
     return outs, st
 

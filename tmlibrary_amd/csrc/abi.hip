@@ -1537,15 +1537,25 @@ int tmh_synth_tables(int distribution, int height, int width, int32_t* ln16, int
   });
 }
 
+int64_t tmh_inflate_scratch_bytes(int64_t n_chunks, int64_t raw_max) {
+  return n_chunks > 0 && raw_max >= 0 ? inflate_scratch_bytes(n_chunks, raw_max) : 0;
+}
+
 int tmh_inflate_device(const uint8_t* dev_src, int64_t src_bytes, const tmh_zchunk* dev_chunks,
-                       int64_t n_chunks, uint8_t* dev_raw, int64_t raw_bytes, int32_t* dev_status,
+                       int64_t n_chunks, int64_t raw_max, uint8_t* dev_raw, int64_t raw_bytes,
+                       void* dev_scratch, int64_t scratch_bytes, int32_t* dev_status,
                        void* stream) {
   return guard([&] {
-    TMH_CHECK(n_chunks >= 0 && src_bytes >= 0 && raw_bytes >= 0, TMH_EINVAL, "bad sizes");
+    TMH_CHECK(n_chunks >= 0 && src_bytes >= 0 && raw_bytes >= 0 && raw_max >= 0, TMH_EINVAL,
+              "bad sizes");
     if (n_chunks == 0) return;
-    TMH_CHECK(dev_src && dev_chunks && dev_raw && dev_status, TMH_EINVAL, "bad arguments");
-    launch_inflate(dev_src, src_bytes, dev_chunks, n_chunks, dev_raw, raw_bytes, dev_status,
-                   (hipStream_t)stream);
+    TMH_CHECK(dev_src && dev_chunks && dev_raw && dev_status && dev_scratch, TMH_EINVAL,
+              "bad arguments");
+    TMH_CHECK(raw_max < (int64_t(1) << 32), TMH_EINVAL, "chunks must hold fewer than 2^32 bytes");
+    TMH_CHECK(scratch_bytes >= inflate_scratch_bytes(n_chunks, raw_max), TMH_EINVAL,
+              "scratch smaller than tmh_inflate_scratch_bytes");
+    launch_inflate(dev_src, src_bytes, dev_chunks, n_chunks, raw_max, dev_raw, raw_bytes,
+                   static_cast<uint32_t*>(dev_scratch), dev_status, (hipStream_t)stream);
   });
 }
 

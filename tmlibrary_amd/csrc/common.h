@@ -298,9 +298,10 @@ void launch_chain_u8(const uint16_t* in, uint8_t* out, int H, int W, int64_t n_s
                      const tmh_window* d_win, int lo, int hi, uint8_t* lut8, hipStream_t s,
                      double zero_log10 = -10.0);
 // site-image input (inflate_kernels.hip)
+int64_t inflate_scratch_bytes(int64_t n_chunks, int64_t raw_max);
 void launch_inflate(const uint8_t* src, int64_t src_bytes, const tmh_zchunk* chunks,
-                    int64_t n_chunks, uint8_t* dst, int64_t dst_bytes, int32_t* status,
-                    hipStream_t s);
+                    int64_t n_chunks, int64_t raw_max, uint8_t* dst, int64_t dst_bytes,
+                    uint32_t* scratch, int32_t* status, hipStream_t s);
 void launch_place_chunks(const uint8_t* raw, const tmh_zchunk* chunks, int64_t n_chunks,
                          int height, int width, int esize, int chunk_rows, int chunk_cols,
                          uint8_t* images, hipStream_t s);

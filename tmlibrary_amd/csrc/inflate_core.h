@@ -10,6 +10,7 @@
 
 #ifndef TMH_ZDEV
 #define TMH_ZDEV __device__ __forceinline__
+#define TMH_ZHD __host__ __device__ __forceinline__
 #define TMH_ZCONST __constant__
 #define TMH_ZBITREV32(x) __builtin_bitreverse32(x)
 #endif
@@ -44,11 +45,12 @@ constexpr int kZOk = 0, kZHeader = 1, kZBlockType = 2, kZCode = 3, kZDist = 4, k
               kZInput = 6, kZAdler = 7, kZSize = 8, kZStored = 9, kZTable = 10;
 
 struct Bits {
-  uint64_t bb;  // bit buffer (LSB first)
-  int nb;       // valid bits
-  int64_t p;    // next aligned dword to load (byte offset into src)
-  int64_t end;  // src bytes (loads at or past it read 0)
-  int64_t used; // bits consumed so far
+  uint64_t bb;   // bit buffer (LSB first)
+  int nb;        // valid bits
+  uint32_t pre;  // the dword at p, loaded one refill ahead (its latency hides behind decoding)
+  int64_t p;     // byte offset of pre in src
+  int64_t end;   // src bytes (loads at or past it read 0)
+  int64_t used;  // bits consumed so far
 };
 
 // the aligned dword at byte p; bytes at or past `end` (the buffer's size) read 0
@@ -62,9 +64,10 @@ TMH_ZDEV uint32_t ld32(const uint8_t* src, int64_t p, int64_t end) {
 
 TMH_ZDEV void refill(Bits& b, const uint8_t* src) {
   if (b.nb <= 32) {
-    b.bb |= (uint64_t)ld32(src, b.p, b.end) << b.nb;
-    b.p += 4;
+    b.bb |= (uint64_t)b.pre << b.nb;
     b.nb += 32;
+    b.p += 4;
+    b.pre = ld32(src, b.p, b.end);
   }
 }
 
@@ -151,23 +154,42 @@ TMH_ZDEV bool hbuild(ZShared& z, int lane, const uint8_t (*lens)[kZW], int off, 
   return true;
 }
 
-TMH_ZCONST uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-TMH_ZCONST uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
-                                      2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-TMH_ZCONST uint16_t kDistBase[30] = {1,    2,    3,    4,    5,    7,     9,     13,    17,  25,
-                                       33,   49,   65,   97,   129,  193,   257,   385,   513, 769,
-                                       1025, 1537, 2049, 3073, 4097, 6145,  8193,  12289, 16385,
-                                       24577};
-TMH_ZCONST uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2,  3,  3,  4,  4,  5,  5,  6,
-                                       6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+TMH_ZCONST uint32_t kLenCode[29] = {
+    3,  4,  5,  6,  7,  8,  9,  10, 11 | 1 << 16, 13 | 1 << 16, 15 | 1 << 16, 17 | 1 << 16,
+    19 | 2 << 16, 23 | 2 << 16, 27 | 2 << 16, 31 | 2 << 16, 35 | 3 << 16, 43 | 3 << 16,
+    51 | 3 << 16, 59 | 3 << 16, 67 | 4 << 16, 83 | 4 << 16, 99 | 4 << 16, 115 | 4 << 16,
+    131 | 5 << 16, 163 | 5 << 16, 195 | 5 << 16, 227 | 5 << 16, 258};
+TMH_ZCONST uint32_t kDistCode[30] = {
+    1, 2, 3, 4, 5 | 1 << 16, 7 | 1 << 16, 9 | 2 << 16, 13 | 2 << 16, 17 | 3 << 16, 25 | 3 << 16,
+    33 | 4 << 16, 49 | 4 << 16, 65 | 5 << 16, 97 | 5 << 16, 129 | 6 << 16, 193 | 6 << 16,
+    257 | 7 << 16, 385 | 7 << 16, 513 | 8 << 16, 769 | 8 << 16, 1025 | 9 << 16, 1537 | 9 << 16,
+    2049 | 10 << 16, 3073 | 10 << 16, 4097 | 11 << 16, 6145 | 11 << 16, 8193 | 12 << 16,
+    12289 | 12 << 16, 16385 | 13 << 16, 24577 | 13 << 16};
 TMH_ZCONST uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 enum : int { kStBlock = 0, kStData = 1, kStStored = 2, kStTrailer = 3, kStDone = 4 };
 
-// Decode chunk c (one zlib stream) into dst; returns its TMH_Z_* status.
-TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
+// length / distance symbol -> base | extra bits << 16 (the kernel keeps a copy in LDS)
+struct ZCodes {
+  const uint32_t* len;   // [29]
+  const uint32_t* dist;  // [30]
+};
+
+// Per chunk, the match list the decode leaves for the resolver (scratch,
+// 32-bit words): [0] matches, [1] the stream's Adler-32 (big-endian value),
+// then per match (output position, length | distance << 9).  A match needs
+// at least 3 output bytes, so raw_len / 3 + 2 entries of 8 bytes always fit.
+TMH_ZHD int64_t match_words(int64_t raw_max) { return 2 * (raw_max / 3 + 2); }
+
+// Phase 1 of a chunk (one zlib stream): Huffman-decode every symbol, write
+// the literal (and stored) bytes at their output positions, and append each
+// back-reference to the chunk's match list `ml` (match_words above) instead
+// of copying it -- so no step of the lane's serial decode waits on a load of
+// earlier output.  Returns the TMH_Z_* status (Adler-32 is checked once the
+// matches are resolved: resolve_matches / k_resolve_matches).
+TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
                             const tmh_zchunk& c, uint8_t* __restrict__ dst, int64_t dst_bytes,
+                            uint32_t* __restrict__ ml, int64_t ml_cap, const ZCodes& tc,
                             ZShared& z, int lane) {
   int err = kZOk;
   if (c.src_off < 0 || c.src_len < 0 || c.src_off + c.src_len > src_bytes || c.raw_off < 0 ||
@@ -176,9 +198,11 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
   }
   uint8_t* out = dst + c.raw_off;
   const int64_t olen = c.raw_len;
-  if (c.flags & 1) {  // the HDF5 filter was skipped: raw bytes
+  ml[0] = 0u;
+  if (c.flags & 1) {  // the HDF5 filter was skipped: raw bytes, nothing to check
     if (c.src_len != c.raw_len) return kZSize;
     for (int64_t i = 0; i < olen; ++i) out[i] = src[c.src_off + i];
+    ml[1] = 0xFFFFFFFFu;  // no Adler-32 to check
     return kZOk;
   }
   Bits b;
@@ -189,6 +213,7 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
     b.bb = (uint64_t)ld32(src, a, src_bytes) >> sh;
     b.nb = 32 - sh;
     b.p = a + 4;
+    b.pre = ld32(src, b.p, src_bytes);
     b.used = 0;
   }
   // loads past the stream's own bytes read the next stream's (harmless: the
@@ -199,21 +224,11 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
   const uint32_t cmf = getb(b, src, 8), flg = getb(b, src, 8);
   if ((cmf & 15u) != 8u || (cmf >> 4) > 7u || ((cmf << 8) | flg) % 31u != 0u || (flg & 0x20u))
     err = kZHeader;
-  int64_t o = 0;                // bytes written
-  uint32_t s1 = 1, s2 = 0, k = 0;  // Adler-32 (reduced every 5,552 bytes)
+  int64_t o = 0;   // output bytes (literals written, matches listed)
+  int64_t nm = 0;  // matches listed
   int state = err ? kStDone : kStBlock;
   int last = 0;
   int64_t stored_left = 0;
-  auto put = [&](uint32_t v) {
-    out[o++] = (uint8_t)v;
-    s1 += v;
-    s2 += s1;
-    if (++k == 5552u) {
-      s1 %= 65521u;
-      s2 %= 65521u;
-      k = 0;
-    }
-  };
   while (state != kStDone) {
     if (b.used > in_bits + 64) {  // ran far past the stream: corrupt
       err = kZInput;
@@ -230,7 +245,7 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
           err = kZOverflow;
           break;
         }
-        put((uint32_t)s);
+        out[o++] = (uint8_t)s;
       } else if (s == 256) {
         state = last ? kStTrailer : kStBlock;
       } else {
@@ -239,13 +254,15 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
           err = kZCode;
           break;
         }
-        const int len = kLenBase[li] + (int)getb(b, src, kLenExtra[li]);
+        const uint32_t le = tc.len[li];
+        const int len = (int)(le & 0xFFFFu) + (int)getb(b, src, (int)(le >> 16));
         const int ds = hdecode<kDFast>(b, src, z.dfast, z.dlim, z.dbase, z.dsym, kDsym, lane);
         if (ds < 0 || ds >= 30) {
           err = kZCode;
           break;
         }
-        const int dist = kDistBase[ds] + (int)getb(b, src, kDistExtra[ds]);
+        const uint32_t de = tc.dist[ds];
+        const int dist = (int)(de & 0xFFFFu) + (int)getb(b, src, (int)(de >> 16));
         if (dist > o) {
           err = kZDist;
           break;
@@ -254,19 +271,14 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
           err = kZOverflow;
           break;
         }
-        const uint8_t* from = out + o - dist;
-        if (dist >= len) {  // no overlap: all loads, then the stores
-          for (int i = 0; i < len; i += 4) {
-            uint32_t v[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = i + j < len ? from[i + j] : 0u;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (i + j < len) put(v[j]);
-          }
-        } else {  // overlapping: byte by byte (each load sees the previous store)
-          for (int i = 0; i < len; ++i) put(from[i]);
+        if (nm >= ml_cap) {
+          err = kZOverflow;
+          break;
         }
+        ml[2 + 2 * nm] = (uint32_t)o;
+        ml[3 + 2 * nm] = (uint32_t)len | ((uint32_t)dist << 9);
+        ++nm;
+        o += len;
       }
     } else if (state == kStBlock) {
       last = (int)getb(b, src, 1);
@@ -358,7 +370,7 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
         err = kZOverflow;
         break;
       }
-      put(getb(b, src, 8));
+      out[o++] = (uint8_t)getb(b, src, 8);
       --stored_left;
     } else {  // trailer: byte-align, Adler-32 big-endian
       const int drop = b.nb & 7;
@@ -367,15 +379,44 @@ TMH_ZDEV int inflate_stream(const uint8_t* __restrict__ src, int64_t src_bytes,
       b.used += drop;
       uint32_t want = 0;
       for (int i = 0; i < 4; ++i) want = (want << 8) | getb(b, src, 8);
-      s1 %= 65521u;
-      s2 %= 65521u;
-      if (((s2 << 16) | s1) != want) err = kZAdler;
-      else if (o != olen) err = kZSize;
+      ml[1] = want;
+      if (o != olen) err = kZSize;
       else if (b.used > in_bits) err = kZInput;
       state = kStDone;
     }
   }
+  ml[0] = (uint32_t)nm;
   return err;
+}
+
+// Adler-32 of n bytes from partial sums: a = 1 + sum x_i, b = n + sum (n - i) x_i.
+TMH_ZHD uint32_t adler_from_sums(uint64_t sa, uint64_t sb, int64_t n) {
+  const uint64_t a = (1u + sa % 65521u) % 65521u;
+  const uint64_t b = ((uint64_t)(n % 65521) + sb % 65521u) % 65521u;
+  return (uint32_t)((b << 16) | a);
+}
+
+// Phase 2 on the host (tests/inflate_host.cpp): the matches in order, then
+// the Adler-32 check.  The device resolves the same list with a wave per
+// chunk (k_resolve_matches).
+inline int resolve_matches(uint8_t* out, int64_t olen, const uint32_t* ml) {
+  const int64_t nm = ml[0];
+  for (int64_t m = 0; m < nm; ++m) {
+    const int64_t o = ml[2 + 2 * m];
+    const int len = (int)(ml[3 + 2 * m] & 511u), dist = (int)(ml[3 + 2 * m] >> 9);
+    for (int i = 0; i < len; ++i) out[o + i] = out[o - dist + i];
+  }
+  if (ml[1] == 0xFFFFFFFFu) return kZOk;  // stored chunk
+  uint64_t sa = 0, sb = 0;
+  for (int64_t i = 0; i < olen; ++i) {
+    sa += out[i];
+    sb += (uint64_t)(olen - i) * out[i];
+    if ((i & 0xFFFFF) == 0xFFFFF) {
+      sa %= 65521u;
+      sb %= 65521u;
+    }
+  }
+  return adler_from_sums(sa, sb, olen) == ml[1] ? kZOk : kZAdler;
 }
 
 

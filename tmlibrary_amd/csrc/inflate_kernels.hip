@@ -8,7 +8,13 @@
 // Each HDF5 chunk is an independent zlib stream (RFC 1950 header, RFC 1951
 // deflate blocks, Adler-32 trailer), so a batch of sites is thousands of
 // independent streams: here one LANE decodes one stream, 64 streams per
-// wave, and the GPU's thousands of waves hide the serial decode's latency.
+// wave, in two kernels.  Phase 1 (k_inflate_tokens) is the serial Huffman
+// decode: literal bytes go straight to their output positions and every
+// back-reference is only listed -- a lane copying its matches itself waited
+// one memory round trip per match, and with 64 lanes per wave some lane had
+// a match in nearly every step (3.6 GB/s for 128 sites,
+// profiles/r4/bench_inflate_*_r4g.json).  Phase 2 (k_resolve_matches) is
+// one wave per chunk copying its matches in order, 64 at a time.
 // Host cores then only move compressed bytes (raw chunks read straight from
 // the files, libtmh5) and the PCIe link carries compressed data.
 //
@@ -20,9 +26,9 @@
 // code lengths; a count/offset scratch for the table build.  The lane's loop
 // is a flat state machine (one deflate symbol, or one whole block header, per
 // iteration) so lanes at different points of their streams stay converged
-// on the symbol path.  Output bytes go to the chunk's region of a raw
-// buffer; back-references read the lane's own earlier output (same thread,
-// same address: program order).  Adler-32 is checked like zlib's inflate.
+// on the symbol path; the bit buffer's next dword is loaded one refill
+// ahead.  Output bytes go to the chunk's region of a raw buffer.  Adler-32
+// is checked like zlib's inflate, in phase 2.
 // tmh_place_chunks_device then moves each chunk's rows into [image][H][W]
 // (edge chunks carry padding past the dataset extent).
 #include "common.h"
@@ -30,15 +36,110 @@
 
 namespace tmh {
 
-__global__ __launch_bounds__(kZW) void k_inflate(const uint8_t* __restrict__ src, int64_t src_bytes,
-                                                 const tmh_zchunk* __restrict__ chunks,
-                                                 int64_t n_chunks, uint8_t* __restrict__ dst,
-                                                 int64_t dst_bytes, int32_t* __restrict__ status) {
+// Phase 1: one lane per chunk (inflate_core.h inflate_tokens); the length /
+// distance code tables in LDS, shared by the wave.
+__global__ __launch_bounds__(kZW) void k_inflate_tokens(
+    const uint8_t* __restrict__ src, int64_t src_bytes, const tmh_zchunk* __restrict__ chunks,
+    int64_t n_chunks, uint8_t* __restrict__ dst, int64_t dst_bytes, uint32_t* __restrict__ ml_all,
+    int64_t mw, int32_t* __restrict__ status) {
   __shared__ ZShared z;
+  __shared__ uint32_t lenc[29], distc[30];
   const int lane = threadIdx.x;
+  if (lane < 29) lenc[lane] = kLenCode[lane];
+  if (lane < 30) distc[lane] = kDistCode[lane];
+  __syncthreads();
   const int64_t ci = (int64_t)blockIdx.x * kZW + lane;
   if (ci >= n_chunks) return;
-  status[ci] = inflate_stream(src, src_bytes, chunks[ci], dst, dst_bytes, z, lane);
+  status[ci] = inflate_tokens(src, src_bytes, chunks[ci], dst, dst_bytes, ml_all + ci * mw,
+                              mw / 2 - 1, ZCodes{lenc, distc}, z, lane);
+}
+
+__device__ __forceinline__ uint32_t wave_excl_min(uint32_t v, int lane) {
+  uint32_t incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, off, 64);
+    if (lane >= off) incl = y < incl ? y : incl;
+  }
+  const uint32_t ex = (uint32_t)__shfl_up((int)incl, 1, 64);
+  return lane == 0 ? 0xFFFFFFFFu : ex;
+}
+
+// Phase 2: one wave per chunk resolves its match list in order, 64 matches
+// at a time.  A match's source lies before its own position; in a round,
+// every pending match whose source ends before the first still-pending
+// destination of the earlier lanes copies (a copy that overlaps itself,
+// distance < length, runs byte by byte in its lane, in order), so each round
+// makes progress and a batch usually needs one or two rounds -- one memory
+// round trip per 64 matches instead of one per match.  Then the chunk's
+// Adler-32 from its bytes (a = 1 + sum x_i, b = n + sum (n - i) x_i, a wave
+// reduction) against the stream's trailer.
+__global__ __launch_bounds__(kZW) void k_resolve_matches(const tmh_zchunk* __restrict__ chunks,
+                                                         uint8_t* __restrict__ dst,
+                                                         const uint32_t* __restrict__ ml_all,
+                                                         int64_t mw, int32_t* __restrict__ status) {
+  const int64_t ci = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (status[ci] != 0) return;  // phase 1 failed: nothing to resolve (uniform)
+  const tmh_zchunk c = chunks[ci];
+  uint8_t* out = dst + c.raw_off;
+  const int64_t olen = c.raw_len;
+  const uint32_t* ml = ml_all + ci * mw;
+  const int64_t nm = ml[0];
+  const uint32_t want = ml[1];
+  for (int64_t base = 0; base < nm; base += kZW) {
+    const int64_t i = base + lane;
+    const bool act = i < nm;
+    const uint32_t o = act ? ml[2 + 2 * i] : 0u, e = act ? ml[3 + 2 * i] : 0u;
+    const uint32_t len = e & 511u, d = e >> 9;
+    const uint32_t src_end = o - d + (len < d ? len : d);  // source bytes before its own output
+    bool todo = act;
+    while (__builtin_amdgcn_ballot_w64(todo)) {
+      const uint32_t fu = wave_excl_min(todo ? o : 0xFFFFFFFFu, lane);
+      const bool go = todo && src_end <= fu;
+      if (go) {
+        uint8_t* to = out + o;
+        const uint8_t* from = out + o - d;
+        if (d >= len) {  // the loads of up to 8 bytes together, then the stores
+          for (uint32_t k = 0; k < len; k += 8) {
+            uint8_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = k + j < len ? from[k + j] : 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (k + j < len) to[k + j] = v[j];
+          }
+        } else {
+          for (uint32_t k = 0; k < len; ++k) to[k] = from[k];
+        }
+      }
+      // this round's stores before the next round's loads (other lanes)
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      todo = todo && !go;
+    }
+  }
+  if (want == 0xFFFFFFFFu) return;  // a stored chunk (filter skipped): no checksum
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  uint64_t sa = 0, sb = 0;
+  int64_t k = 0;
+  for (int64_t j = lane; j < olen; j += kZW) {
+    const uint32_t x = out[j];
+    sa += x;
+    sb += (uint64_t)(olen - j) * x;
+    if (++k == 65536) {
+      sa %= 65521u;
+      sb %= 65521u;
+      k = 0;
+    }
+  }
+  sa %= 65521u;
+  sb %= 65521u;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    sa += (uint64_t)__shfl_xor((long long)sa, off, 64);
+    sb += (uint64_t)__shfl_xor((long long)sb, off, 64);
+  }
+  if (lane == 0 && adler_from_sums(sa, sb, olen) != want) status[ci] = kZAdler;
 }
 
 // Chunk i's raw bytes (chunk_rows x chunk_cols elements, row-major) into
@@ -75,13 +176,25 @@ __global__ __launch_bounds__(256) void k_place_chunks(const uint8_t* __restrict_
   }
 }
 
+int64_t inflate_scratch_bytes(int64_t n_chunks, int64_t raw_max) {
+  return n_chunks * match_words(raw_max) * 4;
+}
+
 void launch_inflate(const uint8_t* src, int64_t src_bytes, const tmh_zchunk* chunks,
-                    int64_t n_chunks, uint8_t* dst, int64_t dst_bytes, int32_t* status,
-                    hipStream_t s) {
+                    int64_t n_chunks, int64_t raw_max, uint8_t* dst, int64_t dst_bytes,
+                    uint32_t* scratch, int32_t* status, hipStream_t s) {
   if (n_chunks <= 0) return;
-  ProfScope prof("inflate", s);
-  hipLaunchKernelGGL(k_inflate, dim3((unsigned)cdiv(n_chunks, kZW)), dim3(kZW), 0, s, src,
-                     src_bytes, chunks, n_chunks, dst, dst_bytes, status);
+  const int64_t mw = match_words(raw_max);
+  {
+    ProfScope prof("inflate", s);
+    hipLaunchKernelGGL(k_inflate_tokens, dim3((unsigned)cdiv(n_chunks, kZW)), dim3(kZW), 0, s,
+                       src, src_bytes, chunks, n_chunks, dst, dst_bytes, scratch, mw, status);
+  }
+  {
+    ProfScope prof("inflate_matches", s);
+    hipLaunchKernelGGL(k_resolve_matches, dim3((unsigned)n_chunks), dim3(kZW), 0, s, chunks, dst,
+                       scratch, mw, status);
+  }
   TMH_HIP(hipGetLastError());
 }
 

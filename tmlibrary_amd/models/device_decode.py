@@ -89,13 +89,17 @@ class DeviceChunkDecoder(object):
         raw_bytes = n * cr * cc * es
         d_raw = self._grow(slot, "d_raw", raw_bytes, torch.uint8)
         d_st = self._grow(slot, "d_status", n, torch.int32)
+        raw_max = int(table["raw_len"].max()) if n else 0
+        scr_bytes = int(L.tmh_inflate_scratch_bytes(n, raw_max))
+        d_scr = self._grow(slot, "d_scratch", max(scr_bytes, 4), torch.uint8)
         with torch.cuda.stream(self.stream):
             d_src[:blob.nbytes].copy_(hb[:blob.nbytes], non_blocking=True)
             d_tab[:tb.nbytes].copy_(ht[:tb.nbytes], non_blocking=True)
         sp = C.c_void_p(self.stream.cuda_stream)
         hip.check(L.tmh_inflate_device(C.c_void_p(d_src.data_ptr()), blob.nbytes,
-                                       C.c_void_p(d_tab.data_ptr()), n,
+                                       C.c_void_p(d_tab.data_ptr()), n, raw_max,
                                        C.c_void_p(d_raw.data_ptr()), raw_bytes,
+                                       C.c_void_p(d_scr.data_ptr()), d_scr.numel(),
                                        C.c_void_p(d_st.data_ptr()), sp))
         hip.check(L.tmh_place_chunks_device(C.c_void_p(d_raw.data_ptr()),
                                             C.c_void_p(d_tab.data_ptr()), n, H, W, es, cr, cc,
