@@ -380,7 +380,8 @@ typedef struct tmh_zchunk {
  * earlier output); then one wave per chunk resolves the list in order, 64
  * matches at a time, and checks the Adler-32.  raw_max: the largest raw_len
  * of the table; dev_scratch: at least tmh_inflate_scratch_bytes(n_chunks,
- * raw_max) bytes. */
+ * raw_max) bytes, 16-byte aligned.  TMH_INFLATE_LANES (4..64, env) sets the
+ * streams per phase-1 workgroup (default: from n_chunks and the CU count). */
 int64_t tmh_inflate_scratch_bytes(int64_t n_chunks, int64_t raw_max);
 int tmh_inflate_device(const uint8_t* dev_src, int64_t src_bytes, const tmh_zchunk* dev_chunks,
                        int64_t n_chunks, int64_t raw_max, uint8_t* dev_raw, int64_t raw_bytes,

@@ -22,6 +22,11 @@ static inline uint32_t bitrev32(uint32_t x) {
 #define TMH_ZCONST static const
 #define TMH_ZBITREV32(x) bitrev32(x)
 #define __restrict__
+#define TMH_ZST16(p, lo, hi)               \
+  do {                                     \
+    const uint64_t v_[2] = {(lo), (hi)};   \
+    memcpy((p), v_, 16);                   \
+  } while (0)
 #include "../tmlibrary_amd/csrc/inflate_core.h"
 
 static std::vector<uint8_t> slurp(const char* p) {
@@ -42,7 +47,7 @@ int main(int argc, char** argv) {
   const size_t n = tab.size() / sizeof(tmh_zchunk);
   std::vector<uint8_t> out((size_t)raw_bytes + 1, 0);
   std::vector<int32_t> st(n, 0);
-  static tmh::ZShared z;
+  static tmh::ZShared<> z;
   std::vector<tmh_zchunk> cs(n);
   int64_t raw_max = 0;
   for (size_t i = 0; i < n; ++i) {
@@ -54,7 +59,7 @@ int main(int argc, char** argv) {
   const tmh::ZCodes tc{tmh::kLenCode, tmh::kDistCode};
   for (size_t i = 0; i < n; ++i)  // phase 1, lane by lane
     st[i] = tmh::inflate_tokens(blob.data(), (int64_t)blob.size(), cs[i], out.data(), raw_bytes,
-                                ml.data() + i * mw, mw / 2 - 1, tc, z, (int)(i % tmh::kZW));
+                                ml.data() + i * mw, tmh::match_cap(mw), tc, z, (int)(i % tmh::kZW));
   for (size_t i = 0; i < n; ++i)  // phase 2
     if (st[i] == 0 && cs[i].raw_off >= 0 && cs[i].raw_off + cs[i].raw_len <= raw_bytes)
       st[i] = tmh::resolve_matches(out.data() + cs[i].raw_off, cs[i].raw_len, ml.data() + i * mw);

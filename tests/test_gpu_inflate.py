@@ -92,7 +92,11 @@ def _run(L, streams, raw_lens=None):
     return outs, st
 
 
-def test_inflate_every_block_kind_bit_exact(L):
+@pytest.mark.parametrize("lanes", [None, 4, 64])
+def test_inflate_every_block_kind_bit_exact(L, monkeypatch, lanes):
+    """Every workgroup width the phase-1 launch can pick decodes the same."""
+    if lanes:
+        monkeypatch.setenv("TMH_INFLATE_LANES", str(lanes))
     streams = _streams()
     outs, st = _run(L, streams)
     bad = [(name, int(s)) for (name, _, _), s in zip(streams, st) if s]

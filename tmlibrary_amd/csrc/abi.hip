@@ -1554,6 +1554,8 @@ int tmh_inflate_device(const uint8_t* dev_src, int64_t src_bytes, const tmh_zchu
     TMH_CHECK(raw_max < (int64_t(1) << 32), TMH_EINVAL, "chunks must hold fewer than 2^32 bytes");
     TMH_CHECK(scratch_bytes >= inflate_scratch_bytes(n_chunks, raw_max), TMH_EINVAL,
               "scratch smaller than tmh_inflate_scratch_bytes");
+    TMH_CHECK((reinterpret_cast<uintptr_t>(dev_scratch) & 15) == 0, TMH_EINVAL,
+              "scratch must be 16-byte aligned");
     launch_inflate(dev_src, src_bytes, dev_chunks, n_chunks, raw_max, dev_raw, raw_bytes,
                    static_cast<uint32_t*>(dev_scratch), dev_status, (hipStream_t)stream);
   });

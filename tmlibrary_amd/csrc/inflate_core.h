@@ -19,25 +19,27 @@ namespace tmh {
 
 namespace {
 
-constexpr int kZW = 64;  // lanes per workgroup (one wave); one stream per lane
+constexpr int kZW = 64;  // lanes of a wave; a workgroup runs W <= kZW streams (one per lane)
 
-// LDS layout: u16 arrays [n][kZW]
+// LDS layout: u16 arrays [n][W], W = the streams of a workgroup
 constexpr int kLsym = 288, kDsym = 32, kLens = 320;
 // first-level tables: the codes of at most kLFast (literal/length) or kDFast
 // (distance) bits decode with one lookup of the peeked bits (entry = symbol
 // | length << 12, 0 = a longer code: the canonical search below)
 constexpr int kLFast = 9, kDFast = 6;
+template <int W = kZW>
 struct ZShared {
-  uint16_t lfast[1 << kLFast][kZW];
-  uint16_t dfast[1 << kDFast][kZW];
-  uint16_t llim[16][kZW];   // left-justified limit of code length l (index 1..15)
-  uint16_t lbase[16][kZW];  // symbol index base of code length l (mod 2^16)
-  uint16_t lsym[kLsym][kZW];
-  uint16_t dlim[16][kZW];
-  uint16_t dbase[16][kZW];
-  uint16_t dsym[kDsym][kZW];
-  uint16_t tmp[16][kZW];    // table build: counts, then offsets
-  uint8_t lens[kLens][kZW]; // code lengths of a dynamic block
+  static constexpr int kW = W;
+  uint16_t lfast[1 << kLFast][W];
+  uint16_t dfast[1 << kDFast][W];
+  uint16_t llim[16][W];   // left-justified limit of code length l (index 1..15)
+  uint16_t lbase[16][W];  // symbol index base of code length l (mod 2^16)
+  uint16_t lsym[kLsym][W];
+  uint16_t dlim[16][W];
+  uint16_t dbase[16][W];
+  uint16_t dsym[kDsym][W];
+  uint16_t tmp[16][W];    // table build: counts, then offsets
+  uint8_t lens[kLens][W]; // code lengths of a dynamic block
 };
 
 // status codes (tmhip.h TMH_Z_*)
@@ -45,10 +47,11 @@ constexpr int kZOk = 0, kZHeader = 1, kZBlockType = 2, kZCode = 3, kZDist = 4, k
               kZInput = 6, kZAdler = 7, kZSize = 8, kZStored = 9, kZTable = 10;
 
 struct Bits {
-  uint64_t bb;   // bit buffer (LSB first)
-  int nb;        // valid bits
-  uint32_t pre;  // the dword at p, loaded one refill ahead (its latency hides behind decoding)
-  int64_t p;     // byte offset of pre in src
+  uint64_t bb;    // bit buffer (LSB first)
+  int nb;         // valid bits
+  uint32_t pre0;  // the dwords at p and p + 4, loaded two refills ahead (the
+  uint32_t pre1;  // latency of the stream's loads hides behind decoding)
+  int64_t p;      // byte offset of pre0 in src
   int64_t end;   // src bytes (loads at or past it read 0)
   int64_t used;  // bits consumed so far
 };
@@ -64,10 +67,11 @@ TMH_ZDEV uint32_t ld32(const uint8_t* src, int64_t p, int64_t end) {
 
 TMH_ZDEV void refill(Bits& b, const uint8_t* src) {
   if (b.nb <= 32) {
-    b.bb |= (uint64_t)b.pre << b.nb;
+    b.bb |= (uint64_t)b.pre0 << b.nb;
     b.nb += 32;
     b.p += 4;
-    b.pre = ld32(src, b.p, b.end);
+    b.pre0 = b.pre1;
+    b.pre1 = ld32(src, b.p + 4, b.end);
   }
 }
 
@@ -85,9 +89,9 @@ TMH_ZDEV uint32_t getb(Bits& b, const uint8_t* src, int n) {
 // order (bit-reversed peek), the code length is the smallest l with v <
 // lim[l] (lim non-decreasing), found by binary search.  Returns -1 for a code
 // the table does not hold.
-template <int FB>
-TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, uint16_t (*fast)[kZW], uint16_t (*lim)[kZW],
-                     uint16_t (*base)[kZW], uint16_t (*sym)[kZW], int nsym, int lane) {
+template <int FB, int W>
+TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, uint16_t (*fast)[W], uint16_t (*lim)[W],
+                     uint16_t (*base)[W], uint16_t (*sym)[W], int nsym, int lane) {
   refill(b, src);
   const uint32_t e = fast[(uint32_t)b.bb & ((1u << FB) - 1u)][lane];
   if (e >> 12) {
@@ -116,10 +120,10 @@ TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, uint16_t (*fast)[kZW], uint16_
 // Canonical tables from n code lengths (lens column of this lane, or the
 // fixed code), with the first-level table of the codes of at most FB bits;
 // returns false for an over-subscribed code.
-template <int FB>
-TMH_ZDEV bool hbuild(ZShared& z, int lane, const uint8_t (*lens)[kZW], int off, int n,
-                     uint16_t (*fast)[kZW], uint16_t (*lim)[kZW], uint16_t (*base)[kZW],
-                     uint16_t (*sym)[kZW]) {
+template <int FB, int W>
+TMH_ZDEV bool hbuild(ZShared<W>& z, int lane, const uint8_t (*lens)[W], int off, int n,
+                     uint16_t (*fast)[W], uint16_t (*lim)[W], uint16_t (*base)[W],
+                     uint16_t (*sym)[W]) {
   for (int i = 0; i < (1 << FB); ++i) fast[i][lane] = 0;
   for (int l = 0; l < 16; ++l) z.tmp[l][lane] = 0;
   for (int s = 0; s < n; ++s) {
@@ -176,10 +180,66 @@ struct ZCodes {
 };
 
 // Per chunk, the match list the decode leaves for the resolver (scratch,
-// 32-bit words): [0] matches, [1] the stream's Adler-32 (big-endian value),
-// then per match (output position, length | distance << 9).  A match needs
-// at least 3 output bytes, so raw_len / 3 + 2 entries of 8 bytes always fit.
-TMH_ZHD int64_t match_words(int64_t raw_max) { return 2 * (raw_max / 3 + 2); }
+// 32-bit words, 16-byte aligned): [0] matches, [1] the stream's Adler-32
+// (big-endian value), [2..3] unused, then from word kMlHead per match (output
+// position, length | distance << 9), written two matches per 16-byte store.
+// A match needs at least 3 output bytes, so raw_len / 3 + 2 entries always fit.
+constexpr int kMlHead = 4;
+TMH_ZHD int64_t match_words(int64_t raw_max) {
+  return (kMlHead + 2 * (raw_max / 3 + 2) + 3) & ~int64_t(3);
+}
+TMH_ZHD int64_t match_cap(int64_t mw) { return (mw - kMlHead) / 2; }
+
+#ifndef TMH_ZST16
+// one 16-byte store; p is 16-byte aligned
+#define TMH_ZST16(p, lo, hi)                                         \
+  do {                                                               \
+    struct alignas(16) Z16_ { uint64_t a, b; };                      \
+    *reinterpret_cast<Z16_*>(p) = Z16_{(lo), (hi)};                  \
+  } while (0)
+#endif
+
+// The literal bytes of a chunk gathered into 16-byte groups in registers
+// and written with one 16-byte store per group: a lane's byte stores went
+// to 64 different lines per wave instruction, and on gfx9 a wait for the
+// bit buffer's next load also waits for every store issued before it.
+// Output positions only grow, so each group is written once, when the
+// decode leaves it; bytes of the group that belong to back-references are
+// written as 0 and filled by phase 2.  The chunk's first and last groups may
+// be shared with the neighbouring chunks: only their bytes inside
+// [out, out + olen) are stored, one by one.
+struct OutBuf {
+  uint8_t* out;
+  int64_t olen;
+  uintptr_t g;  // address of the current group (0: none)
+  uint64_t lo, hi;
+};
+
+TMH_ZDEV void ob_flush(OutBuf& w) {
+  if (!w.g) return;
+  uint8_t* gp = reinterpret_cast<uint8_t*>(w.g);
+  if (gp >= w.out && gp + 16 <= w.out + w.olen) {
+    TMH_ZST16(gp, w.lo, w.hi);
+  } else {
+    for (int i = 0; i < 16; ++i)
+      if (gp + i >= w.out && gp + i < w.out + w.olen)
+        gp[i] = (uint8_t)((i < 8 ? w.lo >> (8 * i) : w.hi >> (8 * (i - 8))) & 0xFFu);
+  }
+}
+
+TMH_ZDEV void ob_put(OutBuf& w, int64_t o, uint32_t byte) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(w.out + o);
+  const uintptr_t g = a & ~uintptr_t(15);
+  if (g != w.g) {
+    ob_flush(w);
+    w.g = g;
+    w.lo = 0;
+    w.hi = 0;
+  }
+  const int sh = (int)(a & 7) * 8;
+  if (a & 8) w.hi |= (uint64_t)byte << sh;
+  else w.lo |= (uint64_t)byte << sh;
+}
 
 // Phase 1 of a chunk (one zlib stream): Huffman-decode every symbol, write
 // the literal (and stored) bytes at their output positions, and append each
@@ -187,10 +247,11 @@ TMH_ZHD int64_t match_words(int64_t raw_max) { return 2 * (raw_max / 3 + 2); }
 // of copying it -- so no step of the lane's serial decode waits on a load of
 // earlier output.  Returns the TMH_Z_* status (Adler-32 is checked once the
 // matches are resolved: resolve_matches / k_resolve_matches).
+template <int W>
 TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
                             const tmh_zchunk& c, uint8_t* __restrict__ dst, int64_t dst_bytes,
                             uint32_t* __restrict__ ml, int64_t ml_cap, const ZCodes& tc,
-                            ZShared& z, int lane) {
+                            ZShared<W>& z, int lane) {
   int err = kZOk;
   if (c.src_off < 0 || c.src_len < 0 || c.src_off + c.src_len > src_bytes || c.raw_off < 0 ||
       c.raw_len < 0 || c.raw_off + c.raw_len > dst_bytes) {
@@ -213,13 +274,16 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
     b.bb = (uint64_t)ld32(src, a, src_bytes) >> sh;
     b.nb = 32 - sh;
     b.p = a + 4;
-    b.pre = ld32(src, b.p, src_bytes);
+    b.pre0 = ld32(src, b.p, src_bytes);
+    b.pre1 = ld32(src, b.p + 4, src_bytes);
     b.used = 0;
   }
   // loads past the stream's own bytes read the next stream's (harmless: the
   // consumed-bit count is checked) but never past the buffer
   b.end = src_bytes;
   const int64_t in_bits = (int64_t)c.src_len * 8;
+  OutBuf w{out, olen, 0, 0, 0};
+  uint32_t mp0 = 0, mp1 = 0;  // an odd match waiting for its pair's store
   // zlib header (RFC 1950): CM = 8, CINFO <= 7, FCHECK, no preset dictionary
   const uint32_t cmf = getb(b, src, 8), flg = getb(b, src, 8);
   if ((cmf & 15u) != 8u || (cmf >> 4) > 7u || ((cmf << 8) | flg) % 31u != 0u || (flg & 0x20u))
@@ -235,7 +299,7 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
       break;
     }
     if (state == kStData) {
-      const int s = hdecode<kLFast>(b, src, z.lfast, z.llim, z.lbase, z.lsym, kLsym, lane);
+      const int s = hdecode<kLFast, W>(b, src, z.lfast, z.llim, z.lbase, z.lsym, kLsym, lane);
       if (s < 256) {
         if (s < 0) {
           err = kZCode;
@@ -245,7 +309,7 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
           err = kZOverflow;
           break;
         }
-        out[o++] = (uint8_t)s;
+        ob_put(w, o++, (uint32_t)s);
       } else if (s == 256) {
         state = last ? kStTrailer : kStBlock;
       } else {
@@ -256,7 +320,7 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
         }
         const uint32_t le = tc.len[li];
         const int len = (int)(le & 0xFFFFu) + (int)getb(b, src, (int)(le >> 16));
-        const int ds = hdecode<kDFast>(b, src, z.dfast, z.dlim, z.dbase, z.dsym, kDsym, lane);
+        const int ds = hdecode<kDFast, W>(b, src, z.dfast, z.dlim, z.dbase, z.dsym, kDsym, lane);
         if (ds < 0 || ds >= 30) {
           err = kZCode;
           break;
@@ -275,8 +339,14 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
           err = kZOverflow;
           break;
         }
-        ml[2 + 2 * nm] = (uint32_t)o;
-        ml[3 + 2 * nm] = (uint32_t)len | ((uint32_t)dist << 9);
+        const uint32_t e = (uint32_t)len | ((uint32_t)dist << 9);
+        if (nm & 1) {
+          TMH_ZST16(ml + kMlHead + 2 * (nm - 1), (uint64_t)mp0 | (uint64_t)mp1 << 32,
+                    (uint64_t)(uint32_t)o | (uint64_t)e << 32);
+        } else {
+          mp0 = (uint32_t)o;
+          mp1 = e;
+        }
         ++nm;
         o += len;
       }
@@ -299,8 +369,8 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
         for (int s = 0; s < 288; ++s)
           z.lens[s][lane] = (uint8_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
         for (int s = 0; s < 32; ++s) z.lens[288 + s][lane] = 5;
-        if (!hbuild<kLFast>(z, lane, z.lens, 0, 288, z.lfast, z.llim, z.lbase, z.lsym) ||
-            !hbuild<kDFast>(z, lane, z.lens, 288, 32, z.dfast, z.dlim, z.dbase, z.dsym)) {
+        if (!hbuild<kLFast, W>(z, lane, z.lens, 0, 288, z.lfast, z.llim, z.lbase, z.lsym) ||
+            !hbuild<kDFast, W>(z, lane, z.lens, 288, 32, z.dfast, z.dlim, z.dbase, z.dsym)) {
           err = kZTable;
           break;
         }
@@ -315,14 +385,14 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
         for (int i = 0; i < 19; ++i) z.lens[i][lane] = 0;
         for (int i = 0; i < hclen; ++i) z.lens[kClOrder[i]][lane] = (uint8_t)getb(b, src, 3);
         // the code-length code lives in the distance tables until the real ones are built
-        if (!hbuild<kDFast>(z, lane, z.lens, 0, 19, z.dfast, z.dlim, z.dbase, z.dsym)) {
+        if (!hbuild<kDFast, W>(z, lane, z.lens, 0, 19, z.dfast, z.dlim, z.dbase, z.dsym)) {
           err = kZTable;
           break;
         }
         int n = 0;
         const int total = hlit + hdist;
         while (n < total) {
-          const int s = hdecode<kDFast>(b, src, z.dfast, z.dlim, z.dbase, z.dsym, kDsym, lane);
+          const int s = hdecode<kDFast, W>(b, src, z.dfast, z.dlim, z.dbase, z.dsym, kDsym, lane);
           if (s < 0) {
             err = kZCode;
             break;
@@ -351,8 +421,8 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
         }
         if (err) break;
         if (z.lens[256][lane] == 0 ||  // no end-of-block code
-            !hbuild<kLFast>(z, lane, z.lens, 0, hlit, z.lfast, z.llim, z.lbase, z.lsym) ||
-            !hbuild<kDFast>(z, lane, z.lens, hlit, hdist, z.dfast, z.dlim, z.dbase, z.dsym)) {
+            !hbuild<kLFast, W>(z, lane, z.lens, 0, hlit, z.lfast, z.llim, z.lbase, z.lsym) ||
+            !hbuild<kDFast, W>(z, lane, z.lens, hlit, hdist, z.dfast, z.dlim, z.dbase, z.dsym)) {
           err = kZTable;
           break;
         }
@@ -370,7 +440,7 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
         err = kZOverflow;
         break;
       }
-      out[o++] = (uint8_t)getb(b, src, 8);
+      ob_put(w, o++, getb(b, src, 8));
       --stored_left;
     } else {  // trailer: byte-align, Adler-32 big-endian
       const int drop = b.nb & 7;
@@ -384,6 +454,11 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
       else if (b.used > in_bits) err = kZInput;
       state = kStDone;
     }
+  }
+  ob_flush(w);
+  if (nm & 1) {
+    ml[kMlHead + 2 * (nm - 1)] = mp0;
+    ml[kMlHead + 2 * (nm - 1) + 1] = mp1;
   }
   ml[0] = (uint32_t)nm;
   return err;
@@ -402,8 +477,9 @@ TMH_ZHD uint32_t adler_from_sums(uint64_t sa, uint64_t sb, int64_t n) {
 inline int resolve_matches(uint8_t* out, int64_t olen, const uint32_t* ml) {
   const int64_t nm = ml[0];
   for (int64_t m = 0; m < nm; ++m) {
-    const int64_t o = ml[2 + 2 * m];
-    const int len = (int)(ml[3 + 2 * m] & 511u), dist = (int)(ml[3 + 2 * m] >> 9);
+    const int64_t o = ml[kMlHead + 2 * m];
+    const uint32_t e = ml[kMlHead + 2 * m + 1];
+    const int len = (int)(e & 511u), dist = (int)(e >> 9);
     for (int i = 0; i < len; ++i) out[o + i] = out[o - dist + i];
   }
   if (ml[1] == 0xFFFFFFFFu) return kZOk;  // stored chunk

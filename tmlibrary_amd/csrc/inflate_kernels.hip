@@ -36,22 +36,26 @@
 
 namespace tmh {
 
-// Phase 1: one lane per chunk (inflate_core.h inflate_tokens); the length /
-// distance code tables in LDS, shared by the wave.
-__global__ __launch_bounds__(kZW) void k_inflate_tokens(
+// Phase 1: one lane per chunk (inflate_core.h inflate_tokens), W chunks per
+// workgroup (a wave with W active lanes); the length / distance code tables
+// in LDS, shared by the workgroup.
+template <int W>
+__global__ __launch_bounds__(W) void k_inflate_tokens(
     const uint8_t* __restrict__ src, int64_t src_bytes, const tmh_zchunk* __restrict__ chunks,
     int64_t n_chunks, uint8_t* __restrict__ dst, int64_t dst_bytes, uint32_t* __restrict__ ml_all,
     int64_t mw, int32_t* __restrict__ status) {
-  __shared__ ZShared z;
+  __shared__ ZShared<W> z;
   __shared__ uint32_t lenc[29], distc[30];
   const int lane = threadIdx.x;
-  if (lane < 29) lenc[lane] = kLenCode[lane];
-  if (lane < 30) distc[lane] = kDistCode[lane];
+  for (int i = lane; i < 30; i += W) {
+    if (i < 29) lenc[i] = kLenCode[i];
+    distc[i] = kDistCode[i];
+  }
   __syncthreads();
-  const int64_t ci = (int64_t)blockIdx.x * kZW + lane;
+  const int64_t ci = (int64_t)blockIdx.x * W + lane;
   if (ci >= n_chunks) return;
-  status[ci] = inflate_tokens(src, src_bytes, chunks[ci], dst, dst_bytes, ml_all + ci * mw,
-                              mw / 2 - 1, ZCodes{lenc, distc}, z, lane);
+  status[ci] = inflate_tokens<W>(src, src_bytes, chunks[ci], dst, dst_bytes, ml_all + ci * mw,
+                                 match_cap(mw), ZCodes{lenc, distc}, z, lane);
 }
 
 __device__ __forceinline__ uint32_t wave_excl_min(uint32_t v, int lane) {
@@ -90,7 +94,8 @@ __global__ __launch_bounds__(kZW) void k_resolve_matches(const tmh_zchunk* __res
   for (int64_t base = 0; base < nm; base += kZW) {
     const int64_t i = base + lane;
     const bool act = i < nm;
-    const uint32_t o = act ? ml[2 + 2 * i] : 0u, e = act ? ml[3 + 2 * i] : 0u;
+    const uint2 oe = act ? reinterpret_cast<const uint2*>(ml + kMlHead)[i] : make_uint2(0u, 0u);
+    const uint32_t o = oe.x, e = oe.y;
     const uint32_t len = e & 511u, d = e >> 9;
     const uint32_t src_end = o - d + (len < d ? len : d);  // source bytes before its own output
     bool todo = act;
@@ -180,6 +185,37 @@ int64_t inflate_scratch_bytes(int64_t n_chunks, int64_t raw_max) {
   return n_chunks * match_words(raw_max) * 4;
 }
 
+// Streams per phase-1 workgroup.  Every chunk of a launch decodes at once
+// (the kernel time is one chunk's serial decode), so the choice only trades
+// divergence -- a wave runs a block header or a slow-path code whenever ANY of
+// its lanes needs one -- against waves per SIMD; ~4 waves per CU of few
+// lanes each is the default (profiles/r4/bench_inflate_lanes_*.json).
+// TMH_INFLATE_LANES=4|8|16|32|64 overrides it.
+static int inflate_lanes(int64_t n_chunks) {
+  if (const char* e = getenv("TMH_INFLATE_LANES")) {
+    const int w = atoi(e);
+    if (w == 4 || w == 8 || w == 16 || w == 32 || w == 64) return w;
+  }
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    TMH_HIP(hipGetDevice(&dev));
+    TMH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (cus <= 0) cus = 256;
+  }
+  int w = 8;
+  while (w < 64 && cdiv(n_chunks, w) > 4 * (int64_t)cus) w *= 2;
+  return w;
+}
+
+template <int W>
+static void launch_tokens(const uint8_t* src, int64_t src_bytes, const tmh_zchunk* chunks,
+                          int64_t n_chunks, uint8_t* dst, int64_t dst_bytes, uint32_t* scratch,
+                          int64_t mw, int32_t* status, hipStream_t s) {
+  hipLaunchKernelGGL(k_inflate_tokens<W>, dim3((unsigned)cdiv(n_chunks, W)), dim3(W), 0, s, src,
+                     src_bytes, chunks, n_chunks, dst, dst_bytes, scratch, mw, status);
+}
+
 void launch_inflate(const uint8_t* src, int64_t src_bytes, const tmh_zchunk* chunks,
                     int64_t n_chunks, int64_t raw_max, uint8_t* dst, int64_t dst_bytes,
                     uint32_t* scratch, int32_t* status, hipStream_t s) {
@@ -187,8 +223,13 @@ void launch_inflate(const uint8_t* src, int64_t src_bytes, const tmh_zchunk* chu
   const int64_t mw = match_words(raw_max);
   {
     ProfScope prof("inflate", s);
-    hipLaunchKernelGGL(k_inflate_tokens, dim3((unsigned)cdiv(n_chunks, kZW)), dim3(kZW), 0, s,
-                       src, src_bytes, chunks, n_chunks, dst, dst_bytes, scratch, mw, status);
+    switch (inflate_lanes(n_chunks)) {
+      case 4: launch_tokens<4>(src, src_bytes, chunks, n_chunks, dst, dst_bytes, scratch, mw, status, s); break;
+      case 8: launch_tokens<8>(src, src_bytes, chunks, n_chunks, dst, dst_bytes, scratch, mw, status, s); break;
+      case 16: launch_tokens<16>(src, src_bytes, chunks, n_chunks, dst, dst_bytes, scratch, mw, status, s); break;
+      case 32: launch_tokens<32>(src, src_bytes, chunks, n_chunks, dst, dst_bytes, scratch, mw, status, s); break;
+      default: launch_tokens<64>(src, src_bytes, chunks, n_chunks, dst, dst_bytes, scratch, mw, status, s); break;
+    }
   }
   {
     ProfScope prof("inflate_matches", s);

@@ -9,7 +9,7 @@ D files cycled) R times each way:
   raw:   read_raw_chunks only (the host half of the GPU path)
   gpu:   DeviceChunkDecoder (raw chunks -> H2D -> tmh_inflate_device -> place)
 and checks the GPU result equals the host one.  One JSON line.
-    python tools/bench_inflate.py [--distinct 16] [--block 128] [--reps 3]
+    python tools/bench_inflate.py [--distinct 16] [--block 128] [--reps 3] [--lanes 4,8,16,32,64]
 """
 import argparse
 import json
@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--width", type=int, default=2560)
     ap.add_argument("--level", type=int, default=4)
     ap.add_argument("--dir", default=None)
+    ap.add_argument("--lanes", default="", help="comma list of TMH_INFLATE_LANES to sweep")
     a = ap.parse_args()
     import torch
 
@@ -84,29 +85,53 @@ def main():
     dec.check()
     torch.cuda.synchronize()
     ok = bool(np.array_equal(out.cpu().numpy().view(np.uint16), host))
-    L.tmh_profile_enable(1)
-    L.tmh_profile_reset()
-    tt = []
-    for _ in range(a.reps):
-        torch.cuda.synchronize()
-        t = time.perf_counter()
+    import ctypes as C
+
+    def timed(lanes):
+        if lanes:
+            os.environ["TMH_INFLATE_LANES"] = str(lanes)
+        else:
+            os.environ.pop("TMH_INFLATE_LANES", None)
         dec.decode(paths, out.data_ptr())
         dec.check()
         torch.cuda.synchronize()
-        tt.append(time.perf_counter() - t)
-    import ctypes as C
-    kern = {}
-    for name in ("inflate", "place_chunks"):
-        ms, k = C.c_double(), C.c_int64()
-        hip.check(L.tmh_profile_read(name.encode(), C.byref(ms), C.byref(k)))
-        if k.value:
-            kern[name] = round(ms.value / k.value, 3)
-    L.tmh_profile_enable(0)
-    res["gpu_sites_per_s"] = round(a.block / min(tt), 1)
+        good = bool(np.array_equal(out.cpu().numpy().view(np.uint16), host))
+        L.tmh_profile_enable(1)
+        L.tmh_profile_reset()
+        tt = []
+        for _ in range(a.reps):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            dec.decode(paths, out.data_ptr())
+            dec.check()
+            torch.cuda.synchronize()
+            tt.append(time.perf_counter() - t)
+        kern = {}
+        for name in ("inflate", "inflate_matches", "place_chunks"):
+            ms, k = C.c_double(), C.c_int64()
+            hip.check(L.tmh_profile_read(name.encode(), C.byref(ms), C.byref(k)))
+            if k.value:
+                kern[name] = round(ms.value / k.value, 3)
+        L.tmh_profile_enable(0)
+        return good, round(a.block / min(tt), 1), kern
+
+    ok2, sps, kern = timed(0)
+    ok = ok and ok2
+    res["gpu_sites_per_s"] = sps
     res["gpu_kernel_ms_per_block"] = kern
     if "inflate" in kern:
-        res["inflate_kernel_sites_per_s"] = round(a.block / (kern["inflate"] * 1e-3), 1)
-        res["inflate_kernel_out_GBs"] = round(a.block * H * W * 2 / (kern["inflate"] * 1e-3) / 1e9, 1)
+        tot = kern["inflate"] + kern.get("inflate_matches", 0.0)
+        res["inflate_kernels_sites_per_s"] = round(a.block / (tot * 1e-3), 1)
+        res["inflate_kernels_out_GBs"] = round(a.block * H * W * 2 / (tot * 1e-3) / 1e9, 1)
+    if a.lanes:
+        sweep = {}
+        for w in [int(x) for x in a.lanes.split(",")]:
+            g, sps, kern = timed(w)
+            ok = ok and g
+            sweep[str(w)] = {"gpu_sites_per_s": sps, "kernel_ms": kern, "equal": g}
+            print(json.dumps({"lanes": w, **sweep[str(w)]}), file=sys.stderr, flush=True)
+        res["lanes_sweep"] = sweep
+        os.environ.pop("TMH_INFLATE_LANES", None)
     res["gpu_equals_host"] = ok
     print(json.dumps(res), flush=True)
     if a.dir is None:

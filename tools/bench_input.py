@@ -117,8 +117,20 @@ def main():
                     m_gpu = h5.read_illumstats(store.illumstats_file(1).location)
                 else:
                     m_host = h5.read_illumstats(store.illumstats_file(1).location)
-            res["gpu_decode_same_results"] = bool(all(np.array_equal(x, y)
-                                                      for x, y in zip(m_host, m_gpu)))
+            # the GPU path folds sites into the Welford state in blocks of
+            # device_block, the host one in batches of 32: mean/std agree to
+            # the merge order's rounding (the 1e-6 parity bar), percentiles
+            # (integer counts) exactly
+            cmp = {}
+            for i, (x, y) in enumerate(zip(m_host, m_gpu)):
+                x, y = np.asarray(x), np.asarray(y)
+                if np.array_equal(x, y):
+                    cmp[str(i)] = "equal"
+                else:
+                    d = np.abs(x.astype(np.float64) - y) / np.maximum(np.abs(x.astype(np.float64)), 1e-30)
+                    cmp[str(i)] = float(d.max())
+            res["gpu_vs_host_decode_stats"] = cmp
+            res["gpu_decode_same_results"] = bool(all(v == "equal" or v <= 1e-6 for v in cmp.values()))
         res["cpus_visible"] = os.cpu_count()
         res["granted_cores"] = h5.granted_cores()
         try:
