@@ -22,11 +22,27 @@ static inline uint32_t bitrev32(uint32_t x) {
 #define TMH_ZCONST static const
 #define TMH_ZBITREV32(x) bitrev32(x)
 #define __restrict__
+#define TMH_ZGLOBAL
 #define TMH_ZST16(p, lo, hi)               \
   do {                                     \
     const uint64_t v_[2] = {(lo), (hi)};   \
     memcpy((p), v_, 16);                   \
   } while (0)
+#define TMH_ZLD16(p, a, b, c, d) \
+  do {                           \
+    uint32_t v_[4];              \
+    memcpy(v_, (p), 16);         \
+    (a) = v_[0];                 \
+    (b) = v_[1];                 \
+    (c) = v_[2];                 \
+    (d) = v_[3];                 \
+  } while (0)
+#define TMH_ZLDS16(p, a, b, c, d)          \
+  do {                                     \
+    const uint32_t v_[4] = {(a), (b), (c), (d)}; \
+    memcpy((p), v_, 16);                   \
+  } while (0)
+#define TMH_ZANY(pred) (pred)
 #include "../tmlibrary_amd/csrc/inflate_core.h"
 
 static std::vector<uint8_t> slurp(const char* p) {

@@ -14,6 +14,39 @@
 #define TMH_ZCONST __constant__
 #define TMH_ZBITREV32(x) __builtin_bitreverse32(x)
 #endif
+#ifndef TMH_ZPROF
+#define TMH_ZPROF 0  // 1: per-chunk decode counters in the match list's head (tools/inflate_prof.py)
+#endif
+#ifndef TMH_ZCLOCK
+#define TMH_ZCLOCK() __builtin_readcyclecounter()
+#endif
+#ifndef TMH_ZLD16
+// one 16-byte load from a 16-byte aligned p into four dwords
+#define TMH_ZLD16(p, a, b, c, d)                                        \
+  do {                                                                  \
+    typedef uint32_t W4_ __attribute__((ext_vector_type(4)));          \
+    const W4_ v_ = *reinterpret_cast<const W4_*>(p);                    \
+    (a) = v_.x;                                                         \
+    (b) = v_.y;                                                         \
+    (c) = v_.z;                                                         \
+    (d) = v_.w;                                                         \
+  } while (0)
+#endif
+#ifndef TMH_ZLDS16
+// one 16-byte LDS store to a 16-byte aligned p
+#define TMH_ZLDS16(p, a, b, c, d)                                       \
+  do {                                                                  \
+    typedef uint32_t W4s_ __attribute__((ext_vector_type(4)));         \
+    *reinterpret_cast<W4s_*>(p) = W4s_{(a), (b), (c), (d)};            \
+  } while (0)
+#define TMH_ZANY(pred) (__builtin_amdgcn_ballot_w64(pred) != 0)
+#endif
+#ifndef TMH_ZGLOBAL
+// the output pointers in the global address space: a generic (flat) store
+// also counts against the LDS wait counter, so every table lookup after it
+// would wait for the store to reach memory
+#define TMH_ZGLOBAL __attribute__((address_space(1)))
+#endif
 
 namespace tmh {
 
@@ -27,9 +60,14 @@ constexpr int kLsym = 288, kDsym = 32, kLens = 320;
 // (distance) bits decode with one lookup of the peeked bits (entry = symbol
 // | length << 12, 0 = a longer code: the canonical search below)
 constexpr int kLFast = 9, kDFast = 6;
+// Per lane, the next bytes of its stream in LDS (a ring of kRing dwords; rows
+// padded to kRingStride, 16-byte aligned, so lanes at different positions
+// fall in different banks)
+constexpr int kRing = 32, kRingStride = 36, kRingLow = 4;
 template <int W = kZW>
 struct ZShared {
   static constexpr int kW = W;
+  alignas(16) uint32_t ring[W][kRingStride];
   uint16_t lfast[1 << kLFast][W];
   uint16_t dfast[1 << kDFast][W];
   uint16_t llim[16][W];   // left-justified limit of code length l (index 1..15)
@@ -46,14 +84,27 @@ struct ZShared {
 constexpr int kZOk = 0, kZHeader = 1, kZBlockType = 2, kZCode = 3, kZDist = 4, kZOverflow = 5,
               kZInput = 6, kZAdler = 7, kZSize = 8, kZStored = 9, kZTable = 10;
 
+// The bit buffer, fed from the lane's ring in LDS.  The ring is topped up
+// for all lanes of the wave at once (ring_top_up, at the top of every
+// iteration of the decode loop, when any lane runs low): up to eight 16-byte
+// loads per lane in flight together, one memory round trip for the whole
+// wave every ~80 symbols.  A lane waiting alone on its own loads stalled the
+// wave once per few symbols (a load in flight across iterations is waited
+// for at the loop's back edge by the compiler's register copies, and a
+// synchronous window load is a round trip per window per lane).  The ring
+// running dry inside an iteration (long block headers) falls back to one
+// synchronous 16-byte load (ring_load_unit).
 struct Bits {
-  uint64_t bb;    // bit buffer (LSB first)
-  int nb;         // valid bits
-  uint32_t pre0;  // the dwords at p and p + 4, loaded two refills ahead (the
-  uint32_t pre1;  // latency of the stream's loads hides behind decoding)
-  int64_t p;      // byte offset of pre0 in src
-  int64_t end;   // src bytes (loads at or past it read 0)
-  int64_t used;  // bits consumed so far
+  uint64_t bb;     // bit buffer (LSB first)
+  int nb;          // valid bits
+  uint32_t head;   // dwords taken from the ring
+  uint32_t fill;   // dwords put into the ring (a multiple of 4)
+  int64_t p;       // byte offset in src of the ring's next 16 bytes (16-byte aligned)
+  int64_t end;     // src bytes (loads at or past it read 0)
+  int64_t used;    // bits consumed so far
+#if TMH_ZPROF
+  uint32_t slow;  // codes decoded by the canonical search
+#endif
 };
 
 // the aligned dword at byte p; bytes at or past `end` (the buffer's size) read 0
@@ -65,18 +116,68 @@ TMH_ZDEV uint32_t ld32(const uint8_t* src, int64_t p, int64_t end) {
   return v;
 }
 
-TMH_ZDEV void refill(Bits& b, const uint8_t* src) {
-  if (b.nb <= 32) {
-    b.bb |= (uint64_t)b.pre0 << b.nb;
-    b.nb += 32;
-    b.p += 4;
-    b.pre0 = b.pre1;
-    b.pre1 = ld32(src, b.p + 4, b.end);
+// one 16-byte unit of the stream into the ring, synchronously
+template <int W>
+TMH_ZDEV void ring_load_unit(const uint8_t* src, Bits& b, ZShared<W>& z, int lane) {
+  uint32_t a0, a1, a2, a3;
+  if (b.p + 16 <= b.end) {
+    TMH_ZLD16(src + b.p, a0, a1, a2, a3);
+  } else {
+    a0 = ld32(src, b.p, b.end);
+    a1 = ld32(src, b.p + 4, b.end);
+    a2 = ld32(src, b.p + 8, b.end);
+    a3 = ld32(src, b.p + 12, b.end);
+  }
+  TMH_ZLDS16(&z.ring[lane][b.fill % kRing], a0, a1, a2, a3);
+  b.fill += 4;
+  b.p += 16;
+}
+
+// Called by every active lane of the wave at the same point: if any lane has
+// fewer than kRingLow dwords left, every lane fills its ring's free 16-byte
+// units that lie wholly inside the buffer (the loads first, then the LDS
+// stores; the buffer's last partial unit comes through ring_load_unit).
+template <int W>
+TMH_ZDEV void ring_top_up(const uint8_t* src, Bits& b, ZShared<W>& z, int lane) {
+  if (!TMH_ZANY(b.fill - b.head < (uint32_t)kRingLow)) return;
+  const int64_t in_buf = b.end - b.p >= 16 ? (b.end - b.p) >> 4 : 0;  // whole units left
+  const int room = (int)((kRing - (b.fill - b.head)) >> 2);
+  const int k = room < in_buf ? room : (int)in_buf;
+  if (k > 0) {
+    // eight loads in one block (units past k re-read unit k - 1: no branches,
+    // no partly-defined registers), then the k stores
+    uint32_t v[8][4];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      TMH_ZLD16(src + b.p + 16 * (u < k ? u : k - 1), v[u][0], v[u][1], v[u][2], v[u][3]);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (u < k)
+        TMH_ZLDS16(&z.ring[lane][(b.fill + 4 * u) % kRing], v[u][0], v[u][1], v[u][2], v[u][3]);
+    b.fill += 4 * k;
+    b.p += 16 * k;
   }
 }
 
-TMH_ZDEV uint32_t getb(Bits& b, const uint8_t* src, int n) {
-  refill(b, src);
+template <int W>
+TMH_ZDEV uint32_t next_dword(const uint8_t* src, Bits& b, ZShared<W>& z, int lane) {
+  if (b.head == b.fill) ring_load_unit<W>(src, b, z, lane);
+  const uint32_t v = z.ring[lane][b.head % kRing];
+  b.head += 1;
+  return v;
+}
+
+template <int W>
+TMH_ZDEV void refill(Bits& b, const uint8_t* src, ZShared<W>& z, int lane) {
+  if (b.nb <= 32) {
+    b.bb |= (uint64_t)next_dword<W>(src, b, z, lane) << b.nb;
+    b.nb += 32;
+  }
+}
+
+template <int W>
+TMH_ZDEV uint32_t getb(Bits& b, const uint8_t* src, ZShared<W>& z, int lane, int n) {
+  refill<W>(b, src, z, lane);
   const uint32_t v = (uint32_t)(b.bb & ((1ull << n) - 1ull));
   b.bb >>= n;
   b.nb -= n;
@@ -90,9 +191,10 @@ TMH_ZDEV uint32_t getb(Bits& b, const uint8_t* src, int n) {
 // lim[l] (lim non-decreasing), found by binary search.  Returns -1 for a code
 // the table does not hold.
 template <int FB, int W>
-TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, uint16_t (*fast)[W], uint16_t (*lim)[W],
-                     uint16_t (*base)[W], uint16_t (*sym)[W], int nsym, int lane) {
-  refill(b, src);
+TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, ZShared<W>& z, uint16_t (*fast)[W],
+                     uint16_t (*lim)[W], uint16_t (*base)[W], uint16_t (*sym)[W], int nsym,
+                     int lane) {
+  refill<W>(b, src, z, lane);
   const uint32_t e = fast[(uint32_t)b.bb & ((1u << FB) - 1u)][lane];
   if (e >> 12) {
     const int len = (int)(e >> 12);
@@ -101,6 +203,9 @@ TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, uint16_t (*fast)[W], uint16_t 
     b.used += len;
     return (int)(e & 0x1FFu);
   }
+#if TMH_ZPROF
+  b.slow += 1;
+#endif
   const uint32_t v = TMH_ZBITREV32((uint32_t)b.bb) >> 17;
   int l = 0;  // largest l with lim[l] <= v (lim[0] = 0)
 #pragma unroll
@@ -181,10 +286,11 @@ struct ZCodes {
 
 // Per chunk, the match list the decode leaves for the resolver (scratch,
 // 32-bit words, 16-byte aligned): [0] matches, [1] the stream's Adler-32
-// (big-endian value), [2..3] unused, then from word kMlHead per match (output
+// (big-endian value), [2..7] unused (TMH_ZPROF counters), then from word
+// kMlHead per match (output
 // position, length | distance << 9), written two matches per 16-byte store.
 // A match needs at least 3 output bytes, so raw_len / 3 + 2 entries always fit.
-constexpr int kMlHead = 4;
+constexpr int kMlHead = 8;
 TMH_ZHD int64_t match_words(int64_t raw_max) {
   return (kMlHead + 2 * (raw_max / 3 + 2) + 3) & ~int64_t(3);
 }
@@ -194,8 +300,8 @@ TMH_ZHD int64_t match_cap(int64_t mw) { return (mw - kMlHead) / 2; }
 // one 16-byte store; p is 16-byte aligned
 #define TMH_ZST16(p, lo, hi)                                         \
   do {                                                               \
-    struct alignas(16) Z16_ { uint64_t a, b; };                      \
-    *reinterpret_cast<Z16_*>(p) = Z16_{(lo), (hi)};                  \
+    typedef uint64_t Z16_ __attribute__((ext_vector_type(2)));      \
+    *(TMH_ZGLOBAL Z16_*)(p) = Z16_{(lo), (hi)};                      \
   } while (0)
 #endif
 
@@ -209,27 +315,31 @@ TMH_ZHD int64_t match_cap(int64_t mw) { return (mw - kMlHead) / 2; }
 // be shared with the neighbouring chunks: only their bytes inside
 // [out, out + olen) are stored, one by one.
 struct OutBuf {
-  uint8_t* out;
+  TMH_ZGLOBAL uint8_t* out;
   int64_t olen;
-  uintptr_t g;  // address of the current group (0: none)
+  int64_t mis;   // out's offset past a 16-byte boundary
+  int64_t g;     // current group: bytes [16 g - mis, 16 g - mis + 16) of out (-1: none)
   uint64_t lo, hi;
 };
 
 TMH_ZDEV void ob_flush(OutBuf& w) {
-  if (!w.g) return;
-  uint8_t* gp = reinterpret_cast<uint8_t*>(w.g);
-  if (gp >= w.out && gp + 16 <= w.out + w.olen) {
-    TMH_ZST16(gp, w.lo, w.hi);
+#if TMH_ZPROF == 2  // timing experiment: no output stores
+  if (w.g != -7) return;
+#endif
+  if (w.g < 0) return;
+  const int64_t s0 = 16 * w.g - w.mis;
+  if (s0 >= 0 && s0 + 16 <= w.olen) {
+    TMH_ZST16(w.out + s0, w.lo, w.hi);
   } else {
     for (int i = 0; i < 16; ++i)
-      if (gp + i >= w.out && gp + i < w.out + w.olen)
-        gp[i] = (uint8_t)((i < 8 ? w.lo >> (8 * i) : w.hi >> (8 * (i - 8))) & 0xFFu);
+      if (s0 + i >= 0 && s0 + i < w.olen)
+        w.out[s0 + i] = (uint8_t)((i < 8 ? w.lo >> (8 * i) : w.hi >> (8 * (i - 8))) & 0xFFu);
   }
 }
 
 TMH_ZDEV void ob_put(OutBuf& w, int64_t o, uint32_t byte) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(w.out + o);
-  const uintptr_t g = a & ~uintptr_t(15);
+  const int64_t a = o + w.mis;
+  const int64_t g = a >> 4;
   if (g != w.g) {
     ob_flush(w);
     w.g = g;
@@ -257,7 +367,7 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
       c.raw_len < 0 || c.raw_off + c.raw_len > dst_bytes) {
     return kZInput;
   }
-  uint8_t* out = dst + c.raw_off;
+  TMH_ZGLOBAL uint8_t* out = (TMH_ZGLOBAL uint8_t*)(dst + c.raw_off);
   const int64_t olen = c.raw_len;
   ml[0] = 0u;
   if (c.flags & 1) {  // the HDF5 filter was skipped: raw bytes, nothing to check
@@ -268,24 +378,22 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
   }
   Bits b;
   {
-    const int64_t a = c.src_off & ~3ll;
-    const int sh = (int)(c.src_off - a) * 8;
-    b.end = c.src_off + c.src_len;
-    b.bb = (uint64_t)ld32(src, a, src_bytes) >> sh;
+    b.end = src_bytes;  // loads past the stream's own bytes read the next stream's
+    b.p = c.src_off & ~15ll;  // (harmless: the consumed-bit count is checked), never past the buffer
+    b.head = 0;
+    b.fill = 0;
+    ring_load_unit<W>(src, b, z, lane);
+    b.head = (uint32_t)((c.src_off >> 2) & 3);
+    const int sh = (int)(c.src_off & 3) * 8;
+    b.bb = (uint64_t)next_dword<W>(src, b, z, lane) >> sh;
     b.nb = 32 - sh;
-    b.p = a + 4;
-    b.pre0 = ld32(src, b.p, src_bytes);
-    b.pre1 = ld32(src, b.p + 4, src_bytes);
     b.used = 0;
   }
-  // loads past the stream's own bytes read the next stream's (harmless: the
-  // consumed-bit count is checked) but never past the buffer
-  b.end = src_bytes;
   const int64_t in_bits = (int64_t)c.src_len * 8;
-  OutBuf w{out, olen, 0, 0, 0};
+  OutBuf w{out, olen, (int64_t)((uintptr_t)(dst + c.raw_off) & 15u), -1, 0, 0};
   uint32_t mp0 = 0, mp1 = 0;  // an odd match waiting for its pair's store
   // zlib header (RFC 1950): CM = 8, CINFO <= 7, FCHECK, no preset dictionary
-  const uint32_t cmf = getb(b, src, 8), flg = getb(b, src, 8);
+  const uint32_t cmf = getb<W>(b, src, z, lane, 8), flg = getb<W>(b, src, z, lane, 8);
   if ((cmf & 15u) != 8u || (cmf >> 4) > 7u || ((cmf << 8) | flg) % 31u != 0u || (flg & 0x20u))
     err = kZHeader;
   int64_t o = 0;   // output bytes (literals written, matches listed)
@@ -293,13 +401,26 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
   int state = err ? kStDone : kStBlock;
   int last = 0;
   int64_t stored_left = 0;
+#if TMH_ZPROF
+  b.slow = 0;
+  uint64_t pc_it = 0, pc_cyc = 0, pc_hdr = 0, pc_hcyc = 0, pc_lit = 0, pc_a = 0;
+#endif
   while (state != kStDone) {
+    ring_top_up<W>(src, b, z, lane);
+#if TMH_ZPROF
+    const uint64_t t0 = TMH_ZCLOCK();
+    const int st0 = state;
+    const int64_t o0 = o, nm0 = nm;
+#endif
     if (b.used > in_bits + 64) {  // ran far past the stream: corrupt
       err = kZInput;
       break;
     }
     if (state == kStData) {
-      const int s = hdecode<kLFast, W>(b, src, z.lfast, z.llim, z.lbase, z.lsym, kLsym, lane);
+      const int s = hdecode<kLFast, W>(b, src, z, z.lfast, z.llim, z.lbase, z.lsym, kLsym, lane);
+#if TMH_ZPROF
+      pc_a += TMH_ZCLOCK() - t0;
+#endif
       if (s < 256) {
         if (s < 0) {
           err = kZCode;
@@ -319,14 +440,14 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
           break;
         }
         const uint32_t le = tc.len[li];
-        const int len = (int)(le & 0xFFFFu) + (int)getb(b, src, (int)(le >> 16));
-        const int ds = hdecode<kDFast, W>(b, src, z.dfast, z.dlim, z.dbase, z.dsym, kDsym, lane);
+        const int len = (int)(le & 0xFFFFu) + (int)getb<W>(b, src, z, lane, (int)(le >> 16));
+        const int ds = hdecode<kDFast, W>(b, src, z, z.dfast, z.dlim, z.dbase, z.dsym, kDsym, lane);
         if (ds < 0 || ds >= 30) {
           err = kZCode;
           break;
         }
         const uint32_t de = tc.dist[ds];
-        const int dist = (int)(de & 0xFFFFu) + (int)getb(b, src, (int)(de >> 16));
+        const int dist = (int)(de & 0xFFFFu) + (int)getb<W>(b, src, z, lane, (int)(de >> 16));
         if (dist > o) {
           err = kZDist;
           break;
@@ -340,7 +461,7 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
           break;
         }
         const uint32_t e = (uint32_t)len | ((uint32_t)dist << 9);
-        if (nm & 1) {
+        if ((nm & 1) && TMH_ZPROF != 2) {
           TMH_ZST16(ml + kMlHead + 2 * (nm - 1), (uint64_t)mp0 | (uint64_t)mp1 << 32,
                     (uint64_t)(uint32_t)o | (uint64_t)e << 32);
         } else {
@@ -351,14 +472,14 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
         o += len;
       }
     } else if (state == kStBlock) {
-      last = (int)getb(b, src, 1);
-      const uint32_t type = getb(b, src, 2);
+      last = (int)getb<W>(b, src, z, lane, 1);
+      const uint32_t type = getb<W>(b, src, z, lane, 2);
       if (type == 0) {  // stored: byte-align, LEN, NLEN
         const int drop = b.nb & 7;
         b.bb >>= drop;
         b.nb -= drop;
         b.used += drop;
-        const uint32_t len = getb(b, src, 16), nlen = getb(b, src, 16);
+        const uint32_t len = getb<W>(b, src, z, lane, 16), nlen = getb<W>(b, src, z, lane, 16);
         if ((len ^ nlen) != 0xFFFFu) {
           err = kZStored;
           break;
@@ -376,14 +497,14 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
         }
         state = kStData;
       } else if (type == 2) {  // dynamic: code-length code, then the two codes' lengths
-        const int hlit = (int)getb(b, src, 5) + 257, hdist = (int)getb(b, src, 5) + 1;
-        const int hclen = (int)getb(b, src, 4) + 4;
+        const int hlit = (int)getb<W>(b, src, z, lane, 5) + 257, hdist = (int)getb<W>(b, src, z, lane, 5) + 1;
+        const int hclen = (int)getb<W>(b, src, z, lane, 4) + 4;
         if (hlit > 286 || hdist > 30) {
           err = kZTable;
           break;
         }
         for (int i = 0; i < 19; ++i) z.lens[i][lane] = 0;
-        for (int i = 0; i < hclen; ++i) z.lens[kClOrder[i]][lane] = (uint8_t)getb(b, src, 3);
+        for (int i = 0; i < hclen; ++i) z.lens[kClOrder[i]][lane] = (uint8_t)getb<W>(b, src, z, lane, 3);
         // the code-length code lives in the distance tables until the real ones are built
         if (!hbuild<kDFast, W>(z, lane, z.lens, 0, 19, z.dfast, z.dlim, z.dbase, z.dsym)) {
           err = kZTable;
@@ -392,7 +513,7 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
         int n = 0;
         const int total = hlit + hdist;
         while (n < total) {
-          const int s = hdecode<kDFast, W>(b, src, z.dfast, z.dlim, z.dbase, z.dsym, kDsym, lane);
+          const int s = hdecode<kDFast, W>(b, src, z, z.dfast, z.dlim, z.dbase, z.dsym, kDsym, lane);
           if (s < 0) {
             err = kZCode;
             break;
@@ -407,11 +528,11 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
               break;
             }
             val = z.lens[n - 1][lane];
-            rep = 3 + (int)getb(b, src, 2);
+            rep = 3 + (int)getb<W>(b, src, z, lane, 2);
           } else if (s == 17) {
-            rep = 3 + (int)getb(b, src, 3);
+            rep = 3 + (int)getb<W>(b, src, z, lane, 3);
           } else {
-            rep = 11 + (int)getb(b, src, 7);
+            rep = 11 + (int)getb<W>(b, src, z, lane, 7);
           }
           if (n + rep > total) {
             err = kZTable;
@@ -440,7 +561,7 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
         err = kZOverflow;
         break;
       }
-      ob_put(w, o++, getb(b, src, 8));
+      ob_put(w, o++, getb<W>(b, src, z, lane, 8));
       --stored_left;
     } else {  // trailer: byte-align, Adler-32 big-endian
       const int drop = b.nb & 7;
@@ -448,13 +569,31 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
       b.nb -= drop;
       b.used += drop;
       uint32_t want = 0;
-      for (int i = 0; i < 4; ++i) want = (want << 8) | getb(b, src, 8);
+      for (int i = 0; i < 4; ++i) want = (want << 8) | getb<W>(b, src, z, lane, 8);
       ml[1] = want;
       if (o != olen) err = kZSize;
       else if (b.used > in_bits) err = kZInput;
       state = kStDone;
     }
+#if TMH_ZPROF
+    const uint64_t dt = TMH_ZCLOCK() - t0;
+    pc_it += 1;
+    pc_cyc += dt;
+    if (st0 == kStBlock) {
+      pc_hdr += 1;
+      pc_hcyc += dt;
+    }
+    if (st0 == kStData && nm == nm0 && o == o0 + 1) pc_lit += 1;
+#endif
   }
+#if TMH_ZPROF
+  ml[2] = (uint32_t)pc_it;
+  ml[3] = (uint32_t)(pc_cyc >> 8);
+  ml[4] = b.slow;
+  ml[5] = (uint32_t)(pc_a >> 8);  // cycles from the iteration's start to the literal/length code
+  ml[6] = (uint32_t)(pc_hcyc >> 8);
+  ml[7] = (uint32_t)pc_lit;
+#endif
   ob_flush(w);
   if (nm & 1) {
     ml[kMlHead + 2 * (nm - 1)] = mp0;
