@@ -312,13 +312,15 @@ def bench_host_path(H, W, n_sites=64, reps=3):
             "job_sites_per_s": round(n_sites / (t_stats + t_corr), 1)}
 
 
-def bench_input_path(H, W, dev, distinct=8, block=64, reps=2):
+def bench_input_path(H, W, dev, distinct=8, block=128, reps=2):
     """§8(f) rank 1 beside the headline: site images from gzip HDF5 files
-    (the reference's ChannelImageFile layout, level 4, h5py-style 270 x 320
-    chunks) into HBM -- decoded on the host (libhdf5 + zlib on the granted
-    cores) vs inflated on the GPU (compressed chunks read by pread, PCIe,
-    tmh_inflate_device + placement); the GPU result is checked against the
-    host one.  Never the headline."""
+    (the reference's ChannelImageFile layout: level 4, h5py's own 135 x 160
+    chunks, models/file.py h5py_chunk_shape) into HBM -- decoded on the host
+    (libhdf5 + zlib on the granted cores) vs inflated on the GPU (compressed
+    chunks read by pread, PCIe, tmh_inflate_device + placement), one block at
+    a time and as a stream of blocks (the host read of block k+1 under the
+    GPU work of block k, as run_job does); the GPU result is checked against
+    the host one.  Never the headline."""
     import shutil
     import tempfile
 
@@ -333,7 +335,7 @@ def bench_input_path(H, W, dev, distinct=8, block=64, reps=2):
         files = []
         for i in range(distinct):
             p = os.path.join(d, "channel_image_file_%d.h5" % i)
-            write_channel_image(p, synth_exact_host(H, W, SEED, 0, i), 4, chunks=(270, 320))
+            write_channel_image(p, synth_exact_host(H, W, SEED, 0, i), 4)
             files.append(p)
         paths = [files[i % distinct] for i in range(block)]
         nt = default_decode_threads()
@@ -358,14 +360,26 @@ def bench_input_path(H, W, dev, distinct=8, block=64, reps=2):
             dec.check()
             torch.cuda.synchronize(dev)
             t_gpu = min(t_gpu, time.perf_counter() - t0)
+        out2 = torch.empty_like(out)
+        n_pipe = 4
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(n_pipe):
+            dec.decode(paths, (out if k % 2 == 0 else out2).data_ptr())
+        dec.check()
+        torch.cuda.synchronize(dev)
+        t_pipe = time.perf_counter() - t0
         comp = sum(os.path.getsize(p) for p in paths)
-        del out
+        del out, out2
+        from tmlibrary_amd.models.file import h5py_chunk_shape
         return {"workload": "%d gzip HDF5 site files of %dx%d uint16 (%d distinct, cycled; level 4, "
-                            "270x320 chunks) decoded into HBM" % (block, H, W, distinct),
+                            "%dx%d chunks) decoded into HBM" % ((block, H, W, distinct)
+                                                                + h5py_chunk_shape((H, W), 2)),
                 "compressed_MB_per_site": round(comp / block / 1e6, 2),
                 "host_threads": nt,
                 "host_inflate_sites_per_s": round(block / t_host, 1),
                 "gpu_inflate_sites_per_s": round(block / t_gpu, 1),
+                "gpu_inflate_stream_sites_per_s": round(n_pipe * block / t_pipe, 1),
                 "gpu_equals_host": same}
     finally:
         shutil.rmtree(d, ignore_errors=True)

@@ -57,6 +57,15 @@ static std::vector<uint8_t> slurp(const char* p) {
 }
 
 int main(int argc, char** argv) {
+  // the data loop's length / distance arithmetic equals RFC 1951's tables
+  for (int i = 0; i < 29; ++i)
+    if ((int)(tmh::kLenCode[i] & 0xFFFF) != tmh::len_base(i) ||
+        (int)(tmh::kLenCode[i] >> 16) != tmh::len_extra(i))
+      return 3;
+  for (int d = 0; d < 30; ++d)
+    if ((int)(tmh::kDistCode[d] & 0xFFFF) != tmh::dist_base(d) ||
+        (int)(tmh::kDistCode[d] >> 16) != tmh::dist_extra(d))
+      return 3;
   if (argc != 6) return 2;
   const std::vector<uint8_t> tab = slurp(argv[1]), blob = slurp(argv[2]);
   const long long raw_bytes = atoll(argv[3]);
@@ -72,10 +81,9 @@ int main(int argc, char** argv) {
   }
   const int64_t mw = tmh::match_words(raw_max);
   std::vector<uint32_t> ml((size_t)(mw * (int64_t)n + 2), 0);
-  const tmh::ZCodes tc{tmh::kLenCode, tmh::kDistCode};
   for (size_t i = 0; i < n; ++i)  // phase 1, lane by lane
     st[i] = tmh::inflate_tokens(blob.data(), (int64_t)blob.size(), cs[i], out.data(), raw_bytes,
-                                ml.data() + i * mw, tmh::match_cap(mw), tc, z, (int)(i % tmh::kZW));
+                                ml.data() + i * mw, tmh::match_cap(mw), z, (int)(i % tmh::kZW));
   for (size_t i = 0; i < n; ++i)  // phase 2
     if (st[i] == 0 && cs[i].raw_off >= 0 && cs[i].raw_off + cs[i].raw_len <= raw_bytes)
       st[i] = tmh::resolve_matches(out.data() + cs[i].raw_off, cs[i].raw_len, ml.data() + i * mw);

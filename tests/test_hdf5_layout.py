@@ -57,6 +57,19 @@ def test_channel_image_is_gzip(tmp_path):
     assert "DEFLATE" in out and "H5T_STD_U16LE" in out
 
 
+def test_h5py_chunk_shape():
+    """h5py's guess_chunk as restated in models/file.py (h5py is not
+    installed here: values from the algorithm, the site case worked by hand in
+    the docstring).  The reference's sites are written this way
+    (tmlib/writers.py:384-387: create_dataset(..., compression='gzip'))."""
+    assert h5.h5py_chunk_shape((2160, 2560), 2) == (135, 160)
+    assert h5.h5py_chunk_shape((2160, 2560), 1) == (135, 160)
+    assert h5.h5py_chunk_shape((4, 4), 2) == (4, 4)          # below the 8 KiB floor: one chunk
+    assert h5.h5py_chunk_shape((64, 80), 2) == (64, 80)
+    r, c = h5.h5py_chunk_shape((101, 157), 2)
+    assert r * c * 2 < 1024 * 1024 and r <= 101 and c <= 157
+
+
 def test_missing_dataset_is_keyerror(tmp_path):
     p = str(tmp_path / "channel_image_file_1.h5")
     h5.write_channel_image(p, np.zeros((4, 4), np.uint16))
@@ -65,7 +78,8 @@ def test_missing_dataset_is_keyerror(tmp_path):
 
 
 @pytest.mark.parametrize("dtype,chunks,gzip", [
-    (np.uint16, None, 4),          # whole-row chunks (our default)
+    (np.uint16, None, 4),          # h5py's chunk choice (the default: the reference's layout)
+    (np.uint16, "rows", 4),        # whole-row chunks
     (np.uint16, (37, 50), 4),      # 2-D chunks with partial edge chunks (h5py-style)
     (np.uint16, (64, 64), 1),
     (np.uint8, (30, 41), 6),

@@ -104,6 +104,8 @@ struct Bits {
   int64_t used;    // bits consumed so far
 #if TMH_ZPROF
   uint32_t slow;  // codes decoded by the canonical search
+  uint32_t priv;  // synchronous 16-byte units (ring ran dry)
+  uint32_t tops;  // top-ups that loaded
 #endif
 };
 
@@ -131,12 +133,16 @@ TMH_ZDEV void ring_load_unit(const uint8_t* src, Bits& b, ZShared<W>& z, int lan
   TMH_ZLDS16(&z.ring[lane][b.fill % kRing], a0, a1, a2, a3);
   b.fill += 4;
   b.p += 16;
+#if TMH_ZPROF
+  b.priv += 1;
+#endif
 }
 
 // Called by every active lane of the wave at the same point: if any lane has
 // fewer than kRingLow dwords left, every lane fills its ring's free 16-byte
 // units that lie wholly inside the buffer (the loads first, then the LDS
-// stores; the buffer's last partial unit comes through ring_load_unit).
+// stores; the buffer's last partial unit, and zeros past it, come through
+// ring_load_unit), so the data loop's refills never find the ring empty.
 template <int W>
 TMH_ZDEV void ring_top_up(const uint8_t* src, Bits& b, ZShared<W>& z, int lane) {
   if (!TMH_ZANY(b.fill - b.head < (uint32_t)kRingLow)) return;
@@ -155,8 +161,13 @@ TMH_ZDEV void ring_top_up(const uint8_t* src, Bits& b, ZShared<W>& z, int lane) 
       if (u < k)
         TMH_ZLDS16(&z.ring[lane][(b.fill + 4 * u) % kRing], v[u][0], v[u][1], v[u][2], v[u][3]);
     b.fill += 4 * k;
+#if TMH_ZPROF
+    b.tops += 1;
+#endif
     b.p += 16 * k;
   }
+  // at the buffer's end: the last partial unit, then zeros, one unit at a time
+  while (b.fill - b.head < (uint32_t)kRingLow) ring_load_unit<W>(src, b, z, lane);
 }
 
 template <int W>
@@ -175,6 +186,27 @@ TMH_ZDEV void refill(Bits& b, const uint8_t* src, ZShared<W>& z, int lane) {
   }
 }
 
+// refill for the data loop, where the ring is known to hold the dwords
+// (ring_top_up leaves at least kRingLow, an iteration takes at most two):
+// no branch, the ring's next dword read whether it is needed or not
+template <int W>
+TMH_ZDEV void refill_ring(Bits& b, ZShared<W>& z, int lane) {
+  const uint32_t v = z.ring[lane][b.head % kRing];
+  const bool need = b.nb <= 32;
+  b.bb |= need ? (uint64_t)v << b.nb : 0ull;
+  b.nb += need ? 32 : 0;
+  b.head += need ? 1u : 0u;
+}
+
+template <int W>
+TMH_ZDEV uint32_t take(Bits& b, int n) {  // n <= the bits in the buffer
+  const uint32_t v = (uint32_t)(b.bb & ((1ull << n) - 1ull));
+  b.bb >>= n;
+  b.nb -= n;
+  b.used += n;
+  return v;
+}
+
 template <int W>
 TMH_ZDEV uint32_t getb(Bits& b, const uint8_t* src, ZShared<W>& z, int lane, int n) {
   refill<W>(b, src, z, lane);
@@ -190,11 +222,12 @@ TMH_ZDEV uint32_t getb(Bits& b, const uint8_t* src, ZShared<W>& z, int lane, int
 // order (bit-reversed peek), the code length is the smallest l with v <
 // lim[l] (lim non-decreasing), found by binary search.  Returns -1 for a code
 // the table does not hold.
-template <int FB, int W>
+template <int FB, int W, bool RingSafe = false>
 TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, ZShared<W>& z, uint16_t (*fast)[W],
                      uint16_t (*lim)[W], uint16_t (*base)[W], uint16_t (*sym)[W], int nsym,
                      int lane) {
-  refill<W>(b, src, z, lane);
+  if (RingSafe) refill_ring<W>(b, z, lane);
+  else refill<W>(b, src, z, lane);
   const uint32_t e = fast[(uint32_t)b.bb & ((1u << FB) - 1u)][lane];
   if (e >> 12) {
     const int len = (int)(e >> 12);
@@ -263,6 +296,8 @@ TMH_ZDEV bool hbuild(ZShared<W>& z, int lane, const uint8_t (*lens)[W], int off,
   return true;
 }
 
+// RFC 1951 3.2.5: length / distance symbol -> base | extra bits << 16 (the
+// reference the arithmetic below is checked against, tests/inflate_host.cpp)
 TMH_ZCONST uint32_t kLenCode[29] = {
     3,  4,  5,  6,  7,  8,  9,  10, 11 | 1 << 16, 13 | 1 << 16, 15 | 1 << 16, 17 | 1 << 16,
     19 | 2 << 16, 23 | 2 << 16, 27 | 2 << 16, 31 | 2 << 16, 35 | 3 << 16, 43 | 3 << 16,
@@ -276,21 +311,26 @@ TMH_ZCONST uint32_t kDistCode[30] = {
     12289 | 12 << 16, 16385 | 13 << 16, 24577 | 13 << 16};
 TMH_ZCONST uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
+// RFC 1951 3.2.5's length and distance tables (kLenCode / kDistCode) as
+// arithmetic, for the data loop: a few dependent ALU operations instead of
+// an LDS round trip.  li = length symbol - 257 (0..28), d = distance code.
+TMH_ZHD int len_extra(int li) { return li < 8 || li == 28 ? 0 : (li - 4) >> 2; }
+TMH_ZHD int len_base(int li) {
+  return li < 8 ? li + 3 : li == 28 ? 258 : ((4 + (li & 3)) << ((li - 4) >> 2)) + 3;
+}
+TMH_ZHD int dist_extra(int d) { return d < 4 ? 0 : (d >> 1) - 1; }
+TMH_ZHD int dist_base(int d) { return d < 4 ? d + 1 : ((2 + (d & 1)) << ((d >> 1) - 1)) + 1; }
+
 enum : int { kStBlock = 0, kStData = 1, kStStored = 2, kStTrailer = 3, kStDone = 4 };
 
-// length / distance symbol -> base | extra bits << 16 (the kernel keeps a copy in LDS)
-struct ZCodes {
-  const uint32_t* len;   // [29]
-  const uint32_t* dist;  // [30]
-};
 
 // Per chunk, the match list the decode leaves for the resolver (scratch,
 // 32-bit words, 16-byte aligned): [0] matches, [1] the stream's Adler-32
-// (big-endian value), [2..7] unused (TMH_ZPROF counters), then from word
+// (big-endian value), [2..15] unused (TMH_ZPROF counters), then from word
 // kMlHead per match (output
 // position, length | distance << 9), written two matches per 16-byte store.
 // A match needs at least 3 output bytes, so raw_len / 3 + 2 entries always fit.
-constexpr int kMlHead = 8;
+constexpr int kMlHead = 16;
 TMH_ZHD int64_t match_words(int64_t raw_max) {
   return (kMlHead + 2 * (raw_max / 3 + 2) + 3) & ~int64_t(3);
 }
@@ -327,7 +367,11 @@ TMH_ZDEV void ob_flush(OutBuf& w) {
   if (w.g != -7) return;
 #endif
   if (w.g < 0) return;
+#if TMH_ZPROF == 3  // timing experiment: the stores wrapped into the first 4 KB
+  const int64_t s0 = (16 * w.g - w.mis) & 4095;
+#else
   const int64_t s0 = 16 * w.g - w.mis;
+#endif
   if (s0 >= 0 && s0 + 16 <= w.olen) {
     TMH_ZST16(w.out + s0, w.lo, w.hi);
   } else {
@@ -360,7 +404,7 @@ TMH_ZDEV void ob_put(OutBuf& w, int64_t o, uint32_t byte) {
 template <int W>
 TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
                             const tmh_zchunk& c, uint8_t* __restrict__ dst, int64_t dst_bytes,
-                            uint32_t* __restrict__ ml, int64_t ml_cap, const ZCodes& tc,
+                            uint32_t* __restrict__ ml, int64_t ml_cap,
                             ZShared<W>& z, int lane) {
   int err = kZOk;
   if (c.src_off < 0 || c.src_len < 0 || c.src_off + c.src_len > src_bytes || c.raw_off < 0 ||
@@ -403,74 +447,78 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
   int64_t stored_left = 0;
 #if TMH_ZPROF
   b.slow = 0;
-  uint64_t pc_it = 0, pc_cyc = 0, pc_hdr = 0, pc_hcyc = 0, pc_lit = 0, pc_a = 0;
+  b.priv = 0;
+  b.tops = 0;
+  uint64_t pc_sym = 0, pc_runs = 0, pc_data = 0, pc_hdr = 0, pc_hcyc = 0;
+  const uint64_t tstart = TMH_ZCLOCK();
 #endif
   while (state != kStDone) {
-    ring_top_up<W>(src, b, z, lane);
 #if TMH_ZPROF
     const uint64_t t0 = TMH_ZCLOCK();
     const int st0 = state;
-    const int64_t o0 = o, nm0 = nm;
 #endif
     if (b.used > in_bits + 64) {  // ran far past the stream: corrupt
       err = kZInput;
       break;
     }
     if (state == kStData) {
-      const int s = hdecode<kLFast, W>(b, src, z, z.lfast, z.llim, z.lbase, z.lsym, kLsym, lane);
+      // The data path as a loop of its own: every active lane decodes
+      // symbols until any lane leaves its block (end-of-block or an error),
+      // with the stream ring topped up for the wave and branch-free refills
 #if TMH_ZPROF
-      pc_a += TMH_ZCLOCK() - t0;
+      const uint64_t td = TMH_ZCLOCK();
+      pc_runs += 1;
 #endif
-      if (s < 256) {
-        if (s < 0) {
-          err = kZCode;
-          break;
-        }
-        if (o >= olen) {
-          err = kZOverflow;
-          break;
-        }
-        ob_put(w, o++, (uint32_t)s);
-      } else if (s == 256) {
-        state = last ? kStTrailer : kStBlock;
-      } else {
-        const int li = s - 257;
-        if (li >= 29) {
-          err = kZCode;
-          break;
-        }
-        const uint32_t le = tc.len[li];
-        const int len = (int)(le & 0xFFFFu) + (int)getb<W>(b, src, z, lane, (int)(le >> 16));
-        const int ds = hdecode<kDFast, W>(b, src, z, z.dfast, z.dlim, z.dbase, z.dsym, kDsym, lane);
-        if (ds < 0 || ds >= 30) {
-          err = kZCode;
-          break;
-        }
-        const uint32_t de = tc.dist[ds];
-        const int dist = (int)(de & 0xFFFFu) + (int)getb<W>(b, src, z, lane, (int)(de >> 16));
-        if (dist > o) {
-          err = kZDist;
-          break;
-        }
-        if (o + len > olen) {
-          err = kZOverflow;
-          break;
-        }
-        if (nm >= ml_cap) {
-          err = kZOverflow;
-          break;
-        }
-        const uint32_t e = (uint32_t)len | ((uint32_t)dist << 9);
-        if ((nm & 1) && TMH_ZPROF != 2) {
-          TMH_ZST16(ml + kMlHead + 2 * (nm - 1), (uint64_t)mp0 | (uint64_t)mp1 << 32,
-                    (uint64_t)(uint32_t)o | (uint64_t)e << 32);
+      do {
+        ring_top_up<W>(src, b, z, lane);
+        int ecode = 0;
+        const int s = hdecode<kLFast, W, true>(b, src, z, z.lfast, z.llim, z.lbase, z.lsym, kLsym,
+                                               lane);
+        if (s < 256) {
+          if (s < 0) ecode = kZCode;
+          else if (o >= olen) ecode = kZOverflow;
+          else ob_put(w, o++, (uint32_t)s);
+        } else if (s == 256) {
+          state = last ? kStTrailer : kStBlock;
         } else {
-          mp0 = (uint32_t)o;
-          mp1 = e;
+          const int li = s - 257 < 29 ? s - 257 : 28;
+          // <= 15 + 5 bits since the refill: no refill before the length's extra bits
+          const int lx = len_extra(li);
+          const int len = len_base(li) + (int)take<W>(b, lx);
+          const int ds = hdecode<kDFast, W, true>(b, src, z, z.dfast, z.dlim, z.dbase, z.dsym,
+                                                  kDsym, lane);
+          const int dsc = ds >= 0 && ds < 30 ? ds : 0;
+          const int dist = dist_base(dsc) + (int)take<W>(b, dist_extra(dsc));
+          if (s - 257 >= 29 || ds < 0 || ds >= 30) ecode = kZCode;
+          else if (dist > o) ecode = kZDist;
+          else if (o + len > olen || nm >= ml_cap) ecode = kZOverflow;
+          else {
+            const uint32_t e = (uint32_t)len | ((uint32_t)dist << 9);
+            if ((nm & 1) && TMH_ZPROF != 2) {
+              TMH_ZST16(ml + kMlHead + (TMH_ZPROF == 3 ? (2 * (nm - 1)) & 1023 : 2 * (nm - 1)),
+                        (uint64_t)mp0 | (uint64_t)mp1 << 32,
+                        (uint64_t)(uint32_t)o | (uint64_t)e << 32);
+            } else {
+              mp0 = (uint32_t)o;
+              mp1 = e;
+            }
+            ++nm;
+            o += len;
+          }
         }
-        ++nm;
-        o += len;
-      }
+        if (b.used > in_bits + 64) ecode = kZInput;  // ran far past the stream: corrupt
+        if (ecode) {
+          err = ecode;
+          state = kStDone;
+        }
+#if TMH_ZPROF
+        pc_sym += 1;
+#endif
+      } while (!TMH_ZANY(state != kStData));
+#if TMH_ZPROF
+      pc_data += TMH_ZCLOCK() - td;
+#endif
+      if (err) break;
     } else if (state == kStBlock) {
       last = (int)getb<W>(b, src, z, lane, 1);
       const uint32_t type = getb<W>(b, src, z, lane, 2);
@@ -576,23 +624,22 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
       state = kStDone;
     }
 #if TMH_ZPROF
-    const uint64_t dt = TMH_ZCLOCK() - t0;
-    pc_it += 1;
-    pc_cyc += dt;
     if (st0 == kStBlock) {
       pc_hdr += 1;
-      pc_hcyc += dt;
+      pc_hcyc += TMH_ZCLOCK() - t0;
     }
-    if (st0 == kStData && nm == nm0 && o == o0 + 1) pc_lit += 1;
 #endif
   }
 #if TMH_ZPROF
-  ml[2] = (uint32_t)pc_it;
-  ml[3] = (uint32_t)(pc_cyc >> 8);
+  ml[2] = (uint32_t)pc_sym;                            // symbols decoded in the data loop
+  ml[3] = (uint32_t)((TMH_ZCLOCK() - tstart) >> 8);   // cycles of the whole stream
   ml[4] = b.slow;
-  ml[5] = (uint32_t)(pc_a >> 8);  // cycles from the iteration's start to the literal/length code
-  ml[6] = (uint32_t)(pc_hcyc >> 8);
-  ml[7] = (uint32_t)pc_lit;
+  ml[5] = (uint32_t)(pc_data >> 8);  // cycles in the data loop
+  ml[6] = (uint32_t)(pc_hcyc >> 8);  // cycles in block headers
+  ml[7] = (uint32_t)pc_runs;         // entries into the data loop
+  ml[8] = b.priv;
+  ml[9] = b.tops;
+  ml[10] = (uint32_t)pc_hdr;
 #endif
   ob_flush(w);
   if (nm & 1) {

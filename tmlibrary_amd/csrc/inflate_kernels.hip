@@ -37,25 +37,18 @@
 namespace tmh {
 
 // Phase 1: one lane per chunk (inflate_core.h inflate_tokens), W chunks per
-// workgroup (a wave with W active lanes); the length / distance code tables
-// in LDS, shared by the workgroup.
+// workgroup (a wave with W active lanes).
 template <int W>
 __global__ __launch_bounds__(W) void k_inflate_tokens(
     const uint8_t* __restrict__ src, int64_t src_bytes, const tmh_zchunk* __restrict__ chunks,
     int64_t n_chunks, uint8_t* __restrict__ dst, int64_t dst_bytes, uint32_t* __restrict__ ml_all,
     int64_t mw, int32_t* __restrict__ status) {
   __shared__ ZShared<W> z;
-  __shared__ uint32_t lenc[29], distc[30];
   const int lane = threadIdx.x;
-  for (int i = lane; i < 30; i += W) {
-    if (i < 29) lenc[i] = kLenCode[i];
-    distc[i] = kDistCode[i];
-  }
-  __syncthreads();
   const int64_t ci = (int64_t)blockIdx.x * W + lane;
   if (ci >= n_chunks) return;
   status[ci] = inflate_tokens<W>(src, src_bytes, chunks[ci], dst, dst_bytes, ml_all + ci * mw,
-                                 match_cap(mw), ZCodes{lenc, distc}, z, lane);
+                                 match_cap(mw), z, lane);
 }
 
 __device__ __forceinline__ uint32_t wave_excl_min(uint32_t v, int lane) {
@@ -185,27 +178,20 @@ int64_t inflate_scratch_bytes(int64_t n_chunks, int64_t raw_max) {
   return n_chunks * match_words(raw_max) * 4;
 }
 
-// Streams per phase-1 workgroup.  Every chunk of a launch decodes at once
-// (the kernel time is one chunk's serial decode), so the choice only trades
-// divergence -- a wave runs a block header or a slow-path code whenever ANY of
-// its lanes needs one -- against waves per SIMD; ~4 waves per CU of few
-// lanes each is the default (profiles/r4/bench_inflate_lanes_*.json).
-// TMH_INFLATE_LANES=4|8|16|32|64 overrides it.
-static int inflate_lanes(int64_t n_chunks) {
+// Streams per phase-1 workgroup.  A lane's decode is a serial chain of
+// dependent LDS lookups and ALU steps, so a wave of few lanes is as fast per
+// symbol as a full one while its divergence (block headers, long codes, the
+// literal and match paths) is paid for fewer lanes; LDS (~2.5 KB per stream)
+// caps the streams resident at once at ~16k.  W = 8 (two to four waves per
+// SIMD when a launch fills the chip) measured fastest at 128 and 384 sites
+// per launch (profiles/r4/bench_inflate_*_r4n.json).  TMH_INFLATE_LANES =
+// 4|8|16|32|64 overrides it.
+static int inflate_lanes() {
   if (const char* e = getenv("TMH_INFLATE_LANES")) {
     const int w = atoi(e);
     if (w == 4 || w == 8 || w == 16 || w == 32 || w == 64) return w;
   }
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    TMH_HIP(hipGetDevice(&dev));
-    TMH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    if (cus <= 0) cus = 256;
-  }
-  int w = 8;
-  while (w < 64 && cdiv(n_chunks, w) > 4 * (int64_t)cus) w *= 2;
-  return w;
+  return 8;
 }
 
 template <int W>
@@ -223,7 +209,7 @@ void launch_inflate(const uint8_t* src, int64_t src_bytes, const tmh_zchunk* chu
   const int64_t mw = match_words(raw_max);
   {
     ProfScope prof("inflate", s);
-    switch (inflate_lanes(n_chunks)) {
+    switch (inflate_lanes()) {
       case 4: launch_tokens<4>(src, src_bytes, chunks, n_chunks, dst, dst_bytes, scratch, mw, status, s); break;
       case 8: launch_tokens<8>(src, src_bytes, chunks, n_chunks, dst, dst_bytes, scratch, mw, status, s); break;
       case 16: launch_tokens<16>(src, src_bytes, chunks, n_chunks, dst, dst_bytes, scratch, mw, status, s); break;

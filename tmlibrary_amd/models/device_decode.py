@@ -39,6 +39,9 @@ class DeviceChunkDecoder(object):
         self.torch = torch
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.stream = stream if stream is not None else torch.cuda.Stream(self.device)
+        # the H2D copies on their own stream: block k+1's compressed bytes
+        # cross PCIe while block k inflates on ``stream``
+        self.copy_stream = torch.cuda.Stream(self.device)
         self.n_threads = n_threads
         self.slots = [dict() for _ in range(max(1, slots))]
         self.k = 0
@@ -92,9 +95,15 @@ class DeviceChunkDecoder(object):
         raw_max = int(table["raw_len"].max()) if n else 0
         scr_bytes = int(L.tmh_inflate_scratch_bytes(n, raw_max))
         d_scr = self._grow(slot, "d_scratch", max(scr_bytes, 4), torch.uint8)
-        with torch.cuda.stream(self.stream):
+        prev = slot.get("inflated")  # the slot's device buffers are free once its last block inflated
+        with torch.cuda.stream(self.copy_stream):
+            if prev is not None:
+                self.copy_stream.wait_event(prev)
             d_src[:blob.nbytes].copy_(hb[:blob.nbytes], non_blocking=True)
             d_tab[:tb.nbytes].copy_(ht[:tb.nbytes], non_blocking=True)
+            copied = torch.cuda.Event()
+            copied.record(self.copy_stream)
+        self.stream.wait_event(copied)
         sp = C.c_void_p(self.stream.cuda_stream)
         hip.check(L.tmh_inflate_device(C.c_void_p(d_src.data_ptr()), blob.nbytes,
                                        C.c_void_p(d_tab.data_ptr()), n, raw_max,
@@ -104,6 +113,9 @@ class DeviceChunkDecoder(object):
         hip.check(L.tmh_place_chunks_device(C.c_void_p(d_raw.data_ptr()),
                                             C.c_void_p(d_tab.data_ptr()), n, H, W, es, cr, cc,
                                             C.c_void_p(int(out_ptr)), sp))
+        inflated = torch.cuda.Event()
+        inflated.record(self.stream)
+        slot["inflated"] = inflated
         h_st = self._grow(slot, "h_status", n, torch.int32, pinned=True)
         with torch.cuda.stream(self.stream):
             h_st[:n].copy_(d_st[:n], non_blocking=True)

@@ -118,14 +118,44 @@ def read_illumstats(path):
     return mean, std, keys, vals
 
 
+def h5py_chunk_shape(shape, itemsize):
+    """The chunk shape h5py picks for a gzip dataset created without explicit
+    chunks -- what the reference's files carry: DatasetWriter.write(...,
+    compression=True) calls ``create_dataset(path, data=data,
+    compression='gzip')`` (tmlib/writers.py:384-387), and h5py chunks such a
+    dataset with its ``guess_chunk`` (h5py/_hl/filters.py, a dependency not
+    vendored in the reference; the algorithm, unchanged across h5py 2.x-3.x,
+    is restated here): a target of 16 KiB x 2^log10(dataset MiB), clamped to
+    [8 KiB, 1 MiB]; halve the axes in turn until the chunk is below the target
+    or within 50% of it (and below 1 MiB).  A 2160 x 2560 uint16 site: 135 x
+    160 (43,200 bytes, 256 chunks per site)."""
+    chunks = [float(x if x != 0 else 1024) for x in shape]
+    dset = float(np.prod(chunks)) * itemsize
+    target = 16 * 1024 * (2 ** np.log10(dset / (1024.0 * 1024)))
+    target = min(max(target, 8 * 1024), 1024 * 1024)
+    i = 0
+    while True:
+        cb = float(np.prod(chunks)) * itemsize
+        if (cb < target or abs(cb - target) / target < 0.5) and cb < 1024 * 1024:
+            break
+        if np.prod(chunks) == 1:
+            break
+        chunks[i % len(chunks)] = float(np.ceil(chunks[i % len(chunks)] / 2.0))
+        i += 1
+    return tuple(int(x) for x in chunks)
+
+
 def write_channel_image(path, array, gzip_level=4, chunks=None):
     """``/array`` gzip-compressed (gzip_level < 0: contiguous, uncompressed);
-    ``chunks`` = (rows, cols) or None for whole-row ~256 KiB chunks."""
+    ``chunks`` = (rows, cols), "rows" for whole-row ~256 KiB chunks, or None
+    for h5py's own choice (h5py_chunk_shape: the reference's layout)."""
     L = h5lib()
     a = np.ascontiguousarray(array)
     if a.dtype not in (np.uint8, np.uint16) or a.ndim != 2:
         raise ValueError("channel images are 2-D uint8/uint16")
-    cr, cc = (0, 0) if chunks is None else (int(chunks[0]), int(chunks[1]))
+    if chunks is None:
+        chunks = h5py_chunk_shape(a.shape, a.itemsize)
+    cr, cc = (0, 0) if chunks == "rows" else (int(chunks[0]), int(chunks[1]))
     _check(L.tmh5_write_channel_image_chunked(_b(path), a.shape[0], a.shape[1], 8 * a.itemsize,
                                               a.ctypes.data, int(gzip_level), cr, cc), path)
 

@@ -3,9 +3,9 @@
 decoded by the parallel inflate reader, and of IllumstatsCalculator.run_job
 (decode -> GPU statistics -> illumstats HDF5) end to end.
 
-Files are written first (synthetic 2160x2560 uint16, gzip level 4, h5py-style
-2-D chunks of 270x320 like the reference's DatasetWriter.write(compression=
-True) output).  Prints one JSON line.
+Files are written first (synthetic 2160x2560 uint16, gzip level 4, h5py's own
+135x160 chunks like the reference's DatasetWriter.write(compression=True)
+output, models/file.py h5py_chunk_shape).  Prints one JSON line.
 
     python tools/bench_input.py --sites 64 --threads 16
 """
@@ -48,7 +48,7 @@ def main():
         paths = []
         for i, s in enumerate(sites):
             p = os.path.join(d, "channel_image_file_%d.h5" % i)
-            h5.write_channel_image(p, s, gzip_level=4, chunks=(270, 320))
+            h5.write_channel_image(p, s, gzip_level=4)
             paths.append(p)
         res = {"sites": a.sites, "shape": [a.height, a.width],
                "file_mb": round(os.path.getsize(paths[0]) / 1e6, 2)}

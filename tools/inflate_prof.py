@@ -55,34 +55,37 @@ def main():
         L.tmh_profile_enable(1)
         L.tmh_profile_reset()
         dec.decode(paths, out.data_ptr())
+        torch.cuda.synchronize()
+        n_chunks = dec.slots[0]["n"]
         try:
             dec.check()
         except IOError:
             pass
-        torch.cuda.synchronize()
         ms, k = C.c_double(), C.c_int64()
         hip.check(L.tmh_profile_read(b"inflate", C.byref(ms), C.byref(k)))
         L.tmh_profile_enable(0)
         slot = dec.slots[0]
-        n = slot["n"] if slot.get("n") else 42 * a.block
-        n = 42 * a.block
-        raw_max = 52 * W * 2
-        mw = (8 + 2 * (raw_max // 3 + 2) + 3) & ~3
+        from tmlibrary_amd.models.file import h5py_chunk_shape
+        cr, cc = h5py_chunk_shape((H, W), 2)
+        n = n_chunks
+        raw_max = cr * cc * 2
+        mw = (16 + 2 * (raw_max // 3 + 2) + 3) & ~3
         scr = slot["d_scratch"][:n * mw * 4].view(torch.int32).cpu().numpy().view(np.uint32).reshape(n, mw)
-        head = scr[:, :8].astype(np.float64)
-        it, cyc, slow, acyc, hcyc, lit = (head[:, i] for i in range(2, 8))
-        cyc *= 256
-        hcyc *= 256
-        acyc *= 256
+        head = scr[:, :16].astype(np.float64)
+        sym, cyc, slow, dcyc, hcyc, runs, priv, tops, hdr = (head[:, i] for i in range(2, 11))
+        cyc, dcyc, hcyc = cyc * 256, dcyc * 256, hcyc * 256
         r = {"kernel_ms": round(ms.value / max(k.value, 1), 3),
-             "iterations_per_chunk": float(it.mean()), "matches_per_chunk": float(head[:, 0].mean()),
-             "literal_iterations_per_chunk": float(lit.mean()),
+             "symbols_per_chunk": float(sym.mean()), "matches_per_chunk": float(head[:, 0].mean()),
              "slow_codes_per_chunk": float(slow.mean()),
-             "code_cycle_share": float((acyc / np.maximum(cyc, 1)).mean()),
+             "data_loop_entries_per_chunk": float(runs.mean()),
+             "headers_per_chunk": float(hdr.mean()),
+             "private_unit_loads_per_chunk": float(priv.mean()),
+             "top_ups_per_chunk": float(tops.mean()),
              "cycles_per_chunk_mean": float(cyc.mean()), "cycles_per_chunk_max": float(cyc.max()),
-             "cycles_per_iteration": float((cyc / np.maximum(it, 1)).mean()),
+             "data_cycles_per_symbol": float((dcyc / np.maximum(sym, 1)).mean()),
+             "data_cycle_share": float((dcyc / np.maximum(cyc, 1)).mean()),
              "header_cycle_share": float((hcyc / np.maximum(cyc, 1)).mean()),
-             }
+             "cycles_per_header": float((hcyc / np.maximum(hdr, 1)).mean())}
         r["clock_ghz_est"] = round(r["cycles_per_chunk_max"] / (r["kernel_ms"] * 1e6), 3)
         res[lanes] = r
         print(json.dumps({"lanes": lanes, **r}), file=sys.stderr, flush=True)
