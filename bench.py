@@ -363,12 +363,14 @@ def bench_input_path(H, W, dev, distinct=8, block=128, reps=2):
         out2 = torch.empty_like(out)
         n_pipe = 4
         torch.cuda.synchronize(dev)
+        dec.times = {k: 0.0 for k in dec.times}
         t0 = time.perf_counter()
         for k in range(n_pipe):
             dec.decode(paths, (out if k % 2 == 0 else out2).data_ptr())
         dec.check()
         torch.cuda.synchronize(dev)
         t_pipe = time.perf_counter() - t0
+        host_ms = {k: round(v / n_pipe * 1e3, 1) for k, v in dec.times.items()}
         comp = sum(os.path.getsize(p) for p in paths)
         del out, out2
         from tmlibrary_amd.models.file import h5py_chunk_shape
@@ -380,6 +382,7 @@ def bench_input_path(H, W, dev, distinct=8, block=128, reps=2):
                 "host_inflate_sites_per_s": round(block / t_host, 1),
                 "gpu_inflate_sites_per_s": round(block / t_gpu, 1),
                 "gpu_inflate_stream_sites_per_s": round(n_pipe * block / t_pipe, 1),
+                "gpu_inflate_stream_host_ms_per_block": host_ms,
                 "gpu_equals_host": same}
     finally:
         shutil.rmtree(d, ignore_errors=True)

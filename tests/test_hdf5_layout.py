@@ -118,3 +118,31 @@ def test_read_channel_images_errors(tmp_path):
     with pytest.raises(Exception):
         h5.read_channel_images([p0, str(tmp_path / "missing.h5")], n_threads=2)
     assert h5.read_channel_images([], n_threads=2).shape[0] == 0
+
+
+@pytest.mark.parametrize("shape,dtype,chunks,level", [
+    ((270, 320), np.uint16, None, 4),        # h5py's chunks (135 x 160 at full size)
+    ((300, 500), np.uint16, (64, 96), 1),    # 2-D chunks, edges padded
+    ((257, 333), np.uint8, (50, 50), 9),
+    ((200, 300), np.uint16, "rows", 4),
+    ((2160, 2560), np.uint16, None, 1),      # a full-size site: 256 chunks, a 2-level B-tree
+])
+def test_raw_chunk_index_parse_equals_libhdf5(tmp_path, monkeypatch, shape, dtype, chunks, level):
+    """read_raw_chunks reads each file's chunk index itself (the version-1
+    B-tree behind /array's layout message, outside the HDF5 lock): the table
+    and bytes equal the ones libhdf5's H5Dget_chunk_info_by_coord gives."""
+    rng = np.random.default_rng(3)
+    paths = []
+    for i in range(3):
+        a = rng.integers(0, 4000, shape).astype(dtype)
+        p = str(tmp_path / ("channel_image_file_%d.h5" % i))
+        h5.write_channel_image(p, a, gzip_level=level, chunks=chunks)
+        paths.append(p)
+    monkeypatch.setenv("TMH5_CHUNK_INDEX", "parse")  # fail rather than fall back
+    blob, tab, geom = h5.read_raw_chunks(paths, 3)
+    blob, tab = blob.copy(), tab.copy()
+    monkeypatch.setenv("TMH5_CHUNK_INDEX", "hdf5")
+    blob2, tab2, geom2 = h5.read_raw_chunks(paths, 3)
+    assert tuple(geom) == tuple(geom2)
+    assert np.array_equal(tab, tab2)
+    assert np.array_equal(blob, blob2)

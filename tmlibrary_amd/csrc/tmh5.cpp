@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <mutex>
@@ -254,16 +255,24 @@ void read_one_parallel(const char* path, uint8_t* out, int height, int width, in
     if (H5Dget_num_chunks(ds, sp, &nchunks) < 0) throw H5Err{-5, "H5Dget_num_chunks failed"};
     if (nchunks < (hsize_t)(((d[0] + ch[0] - 1) / ch[0]) * ((d[1] + ch[1] - 1) / ch[1])))
       memset(out, 0, (size_t)height * width * esize);  // unwritten chunks read as fill (0)
-    raw.resize(nchunks);
-    offs.resize(nchunks);
-    stored.resize(nchunks);
-    for (hsize_t i = 0; i < nchunks; ++i) {
-      hsize_t coord[2];
+    raw.reserve(nchunks);
+    offs.reserve(nchunks);
+    stored.reserve(nchunks);
+    // every chunk of the grid by coordinates (unwritten ones have no address):
+    // H5Dget_chunk_info by index walks the chunk index from its start per call
+    const hsize_t gr = (d[0] + ch[0] - 1) / ch[0], gc = (d[1] + ch[1] - 1) / ch[1];
+    for (hsize_t g = 0; g < gr * gc; ++g) {
+      hsize_t coord[2] = {(g / gc) * ch[0], (g % gc) * ch[1]};
       unsigned fmask = 0;
-      haddr_t addr;
+      haddr_t addr = HADDR_UNDEF;
       hsize_t size = 0;
-      if (H5Dget_chunk_info(ds, sp, i, coord, &fmask, &addr, &size) < 0)
-        throw H5Err{-5, "H5Dget_chunk_info failed"};
+      if (H5Dget_chunk_info_by_coord(ds, coord, &fmask, &addr, &size) < 0)
+        throw H5Err{-5, std::string(path) + ": H5Dget_chunk_info_by_coord failed"};
+      if (addr == HADDR_UNDEF) continue;  // unwritten: fill value
+      const size_t i = raw.size();
+      raw.emplace_back();
+      offs.emplace_back();
+      stored.push_back(0);
       raw[i].resize(size);
       uint32_t fm = 0;
       if (H5Dread_chunk(ds, H5P_DEFAULT, coord, &fm, raw[i].data()) < 0)
@@ -309,9 +318,18 @@ struct FileChunks {
   std::vector<tmh5_chunk> ch;  // src_off relative to the file's first chunk in the blob
   std::vector<int64_t> addr;   // absolute file offset of each chunk
   int64_t bytes = 0;
+  // from the HDF5 pass, for the index parse
+  uint64_t ub = 0;       // userblock = base address
+  uint64_t oh = 0;       // /array's object header address
+  hsize_t d[2] = {0, 0};  // dataset extent
+  hsize_t n = 0;          // chunks
+  bool parsed = false;
 };
 
-void file_chunks(const char* path, int64_t image, int h, int w, int esize, hsize_t* ch,
+// Under the HDF5 lock: the /array checks, the chunk count, and where its
+// object header is.  The chunk index itself is read by parse_chunk_index
+// (outside the lock, in parallel) or, failing that, by chunks_by_hdf5.
+void file_header(const char* path, int64_t image, int h, int w, int esize, hsize_t* ch,
                  FileChunks& fc) {
   Hid f(H5Fopen(path, H5F_ACC_RDONLY, H5P_DEFAULT), H5Fclose);
   hsize_t ub = 0;
@@ -346,29 +364,168 @@ void file_chunks(const char* path, int64_t image, int h, int w, int esize, hsize
   if (H5Dget_num_chunks(ds, sp, &n) < 0) throw H5Err{-5, "H5Dget_num_chunks failed"};
   if (n != ((d[0] + c[0] - 1) / c[0]) * ((d[1] + c[1] - 1) / c[1]))  // unwritten chunks: fill values
     throw H5Err{-95, std::string(path) + ": /array has unwritten chunks"};
+  H5O_info_t oi;
+  fc.oh = H5Oget_info2(ds, &oi, H5O_INFO_BASIC) >= 0 ? (uint64_t)oi.addr : 0;
+  fc.ub = ub;
+  fc.d[0] = d[0];
+  fc.d[1] = d[1];
+  fc.n = n;
+  fc.ch.assign(n, tmh5_chunk{});
+  fc.addr.assign(n, 0);
+  for (auto& e : fc.ch) e.image = image;
+}
+
+// The table from libhdf5, chunk by chunk (any chunk index; ~1.5 us a chunk
+// under the lock -- the fallback of parse_chunk_index).
+void chunks_by_hdf5(const char* path, int esize, const hsize_t* c, FileChunks& fc) {
+  Hid f(H5Fopen(path, H5F_ACC_RDONLY, H5P_DEFAULT), H5Fclose);
+  Hid ds(H5Dopen2(f, "array", H5P_DEFAULT), H5Dclose);
   const int64_t raw = (int64_t)(c[0] * c[1]) * esize;
-  fc.ch.resize(n);
-  fc.addr.resize(n);
+  const hsize_t gc = (fc.d[1] + c[1] - 1) / c[1];
   fc.bytes = 0;
-  for (hsize_t i = 0; i < n; ++i) {
-    hsize_t coord[2];
+  for (hsize_t i = 0; i < fc.n; ++i) {
+    hsize_t coord[2] = {(i / gc) * c[0], (i % gc) * c[1]};
     unsigned fmask = 0;
-    haddr_t addr;
+    haddr_t addr = HADDR_UNDEF;
     hsize_t size = 0;
-    if (H5Dget_chunk_info(ds, sp, i, coord, &fmask, &addr, &size) < 0)
-      throw H5Err{-5, "H5Dget_chunk_info failed"};
+    if (H5Dget_chunk_info_by_coord(ds, coord, &fmask, &addr, &size) < 0 || addr == HADDR_UNDEF)
+      throw H5Err{-5, std::string(path) + ": H5Dget_chunk_info_by_coord failed"};
     tmh5_chunk& e = fc.ch[i];
     e.src_off = fc.bytes;
     e.src_len = (int64_t)size;
     e.raw_len = raw;
-    e.image = image;
     e.row0 = (int32_t)coord[0];
     e.col0 = (int32_t)coord[1];
     e.flags = (fmask & 1u) ? 1 : 0;  // deflate skipped for this chunk: stored
     e.reserved = 0;
-    fc.addr[i] = (int64_t)(ub + addr);
+    fc.addr[i] = (int64_t)(fc.ub + addr);
     fc.bytes += (int64_t)size;
   }
+}
+
+uint64_t le(const uint8_t* p, int n) {
+  uint64_t v = 0;
+  for (int i = 0; i < n; ++i) v |= (uint64_t)p[i] << (8 * i);
+  return v;
+}
+
+bool pread_all(int fd, void* dst, size_t n, uint64_t pos) {
+  uint8_t* d = static_cast<uint8_t*>(dst);
+  while (n > 0) {
+    const ssize_t r = pread(fd, d, n, (off_t)pos);
+    if (r <= 0) return false;
+    d += r;
+    pos += (uint64_t)r;
+    n -= (size_t)r;
+  }
+  return true;
+}
+
+// The chunk table read straight from the file's bytes, without libhdf5 (so
+// outside its lock, one file per worker): the HDF5 file format's version-1
+// object header of /array -> its data layout message (version 3, chunked) ->
+// the version-1 B-tree of raw data chunks, whose leaf keys hold each chunk's
+// size, filter mask and offset and whose children are the chunk addresses.
+// This is the layout libhdf5 writes at its default (earliest) format
+// bounds, as h5py does for the reference's files.  Anything else (version-2
+// object headers, other chunk indexes, 4-byte addresses) returns false and
+// the file goes through chunks_by_hdf5.  The result is checked for exactly
+// one chunk per grid cell.
+bool parse_chunk_index(const char* path, int esize, const hsize_t* c, FileChunks& fc) {
+  if (!fc.oh) return false;
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return false;
+  struct Close {
+    int fd;
+    ~Close() { close(fd); }
+  } cl{fd};
+  uint8_t sb[16];
+  if (!pread_all(fd, sb, 16, fc.ub) || memcmp(sb, "\x89HDF\r\n\x1a\n", 8) != 0) return false;
+  const int sbv = sb[8];
+  const int so = sbv <= 1 ? sb[13] : sb[9], sl = sbv <= 1 ? sb[14] : sb[10];
+  if (so != 8 || sl != 8) return false;
+  // object header v1: version, reserved, #messages (2), refcount (4), header size (4), pad to 16
+  uint8_t oh[16];
+  if (!pread_all(fd, oh, 16, fc.ub + fc.oh) || oh[0] != 1) return false;
+  const uint64_t nmsg = le(oh + 2, 2);
+  std::vector<std::pair<uint64_t, uint64_t>> blocks{{fc.ub + fc.oh + 16, le(oh + 8, 4)}};
+  uint64_t bt = 0;
+  bool found = false;
+  uint64_t seen = 0;
+  std::vector<uint8_t> buf;
+  for (size_t bi = 0; bi < blocks.size() && !found && seen < nmsg && bi < 64; ++bi) {
+    buf.resize(blocks[bi].second);
+    if (buf.size() > (1u << 20) || !pread_all(fd, buf.data(), buf.size(), blocks[bi].first))
+      return false;
+    for (size_t o = 0; o + 8 <= buf.size() && seen < nmsg;) {
+      const uint64_t type = le(&buf[o], 2), size = le(&buf[o + 2], 2);
+      const uint8_t* m = &buf[o + 8];
+      if (o + 8 + size > buf.size()) return false;
+      ++seen;
+      if (type == 0x10 && size >= 16) {  // continuation
+        blocks.push_back({fc.ub + le(m, 8), le(m + 8, 8)});
+      } else if (type == 0x08) {  // data layout
+        if (size < 3 + 8 + 12 || m[0] != 3 || m[1] != 2 || m[2] != 3) return false;
+        if (le(m + 11, 4) != c[0] || le(m + 15, 4) != c[1] || (int)le(m + 19, 4) != esize)
+          return false;
+        bt = le(m + 3, 8);
+        found = true;
+        break;
+      }
+      o += 8 + size;
+    }
+  }
+  if (!found || bt == ~0ull) return false;
+  // B-tree v1 (type 1): "TREE", type, level, entries (2), left, right (8 + 8),
+  // then key, child, ..., key; key = size (4), filter mask (4), 3 offsets (8 each)
+  constexpr size_t kKey = 32;
+  const hsize_t gr = (fc.d[0] + c[0] - 1) / c[0], gc = (fc.d[1] + c[1] - 1) / c[1];
+  std::vector<char> have(fc.n, 0);
+  std::vector<uint64_t> stack{bt};
+  const int64_t raw = (int64_t)(c[0] * c[1]) * esize;
+  hsize_t got = 0;
+  size_t visits = 0;
+  while (!stack.empty()) {
+    const uint64_t a = stack.back();
+    stack.pop_back();
+    if (++visits > 4 * fc.n + 64) return false;
+    uint8_t hd[24];
+    if (!pread_all(fd, hd, 24, fc.ub + a) || memcmp(hd, "TREE", 4) != 0 || hd[4] != 1) return false;
+    const int level = hd[5];
+    const uint64_t ne = le(hd + 6, 2);
+    buf.resize(ne * (kKey + 8) + kKey);
+    if (!pread_all(fd, buf.data(), buf.size(), fc.ub + a + 24)) return false;
+    for (uint64_t i = 0; i < ne; ++i) {
+      const uint8_t* k = &buf[i * (kKey + 8)];
+      const uint64_t child = le(k + kKey, 8);
+      if (level > 0) {
+        stack.push_back(child);
+        continue;
+      }
+      const uint64_t r0 = le(k + 8, 8), c0 = le(k + 16, 8);
+      if (r0 % c[0] || c0 % c[1] || r0 / c[0] >= gr || c0 / c[1] >= gc) return false;
+      const hsize_t g = (r0 / c[0]) * gc + c0 / c[1];
+      if (have[g]) return false;
+      have[g] = 1;
+      ++got;
+      tmh5_chunk& e = fc.ch[g];
+      e.src_len = (int64_t)le(k, 4);
+      e.raw_len = raw;
+      e.row0 = (int32_t)r0;
+      e.col0 = (int32_t)c0;
+      e.flags = (le(k + 4, 4) & 1u) ? 1 : 0;
+      e.reserved = 0;
+      fc.addr[g] = (int64_t)(fc.ub + child);
+    }
+  }
+  if (got != fc.n) return false;
+  fc.bytes = 0;
+  for (auto& e : fc.ch) {  // grid order, as chunks_by_hdf5
+    e.src_off = fc.bytes;
+    fc.bytes += e.src_len;
+  }
+  fc.parsed = true;
+  return true;
 }
 
 }  // namespace
@@ -389,7 +546,32 @@ int tmh5_read_raw_chunks(const char* const* paths, int64_t n_files, int n_thread
     const int esize = bits / 8;
     hsize_t ch[2] = {0, 0};
     std::vector<FileChunks> fc((size_t)n_files);
-    for (int64_t i = 0; i < n_files; ++i) file_chunks(paths[i], i, h, w, esize, ch, fc[i]);
+    for (int64_t i = 0; i < n_files; ++i) file_header(paths[i], i, h, w, esize, ch, fc[i]);
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(n_threads > 0 ? n_threads : 1, n_files));
+    // the chunk indexes, in parallel outside the HDF5 lock; TMH5_CHUNK_INDEX:
+    // "hdf5" = libhdf5's lookups only, "parse" = the parse only (tests)
+    const char* ci = getenv("TMH5_CHUNK_INDEX");
+    const bool use_hdf5 = ci && strcmp(ci, "hdf5") == 0;
+    const bool parse_only = ci && strcmp(ci, "parse") == 0;
+    {
+      std::atomic<int64_t> next{0};
+      auto parse = [&] {
+        for (;;) {
+          const int64_t i = next.fetch_add(1);
+          if (i >= n_files) return;
+          if (!use_hdf5) parse_chunk_index(paths[i], esize, ch, fc[i]);
+        }
+      };
+      std::vector<std::thread> pool;
+      for (int t = 1; t < nt; ++t) pool.emplace_back(parse);
+      parse();
+      for (auto& t : pool) t.join();
+    }
+    for (int64_t i = 0; i < n_files; ++i) {
+      if (fc[i].parsed) continue;
+      if (parse_only) throw H5Err{-95, std::string(paths[i]) + ": chunk index not parsed"};
+      chunks_by_hdf5(paths[i], esize, ch, fc[i]);
+    }
     int64_t total = 0, nch = 0;
     for (auto& f : fc) {
       total += f.bytes;
@@ -419,7 +601,6 @@ int tmh5_read_raw_chunks(const char* const* paths, int64_t n_files, int n_thread
     // the bytes, one file per task, outside the HDF5 lock
     std::vector<int64_t> base((size_t)n_files, 0);
     for (int64_t i = 1; i < n_files; ++i) base[i] = base[i - 1] + fc[i - 1].bytes;
-    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(n_threads > 0 ? n_threads : 1, n_files));
     std::atomic<int64_t> next{0};
     std::atomic<bool> failed{false};
     std::string first_err;

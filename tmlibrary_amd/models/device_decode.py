@@ -19,6 +19,7 @@ deflate filter only) raises ``RawChunksUnsupported`` and the caller decides
 from __future__ import annotations
 
 import ctypes as C
+import time
 
 import numpy as np
 
@@ -45,6 +46,9 @@ class DeviceChunkDecoder(object):
         self.n_threads = n_threads
         self.slots = [dict() for _ in range(max(1, slots))]
         self.k = 0
+        # host seconds: waiting for a slot's previous block, reading raw chunks
+        # (libhdf5 metadata + pread), the whole decode() call
+        self.times = {"slot_wait": 0.0, "read": 0.0, "call": 0.0}
 
     def _grow(self, slot, name, n, dtype, pinned=False):
         torch = self.torch
@@ -65,16 +69,19 @@ class DeviceChunkDecoder(object):
         (the caller orders its consumers after ``self.stream``)."""
         torch = self.torch
         L = hip.lib()
+        t0 = time.perf_counter()
         slot = self.slots[self.k % len(self.slots)]
         self.k += 1
         if slot.get("event") is not None:
             slot["event"].synchronize()  # the slot's previous block is done
             self._raise_failed(slot)
+        t1 = time.perf_counter()
         hb = slot.get("h_blob")
         ht = slot.get("h_tab")
         blob, table, geom = read_raw_chunks(
             paths, self.n_threads, None if hb is None else hb.numpy(),
             None if ht is None else ht.numpy().view(hip.ZCHUNK_DTYPE))
+        t2 = time.perf_counter()
         H, W, es, cr, cc = geom
         n = len(table)
         if hb is None or blob.ctypes.data != hb.data_ptr():  # grown: pin the new size
@@ -125,6 +132,10 @@ class DeviceChunkDecoder(object):
         slot["n"] = n
         slot["paths"] = list(paths)
         slot["images"] = table["image"].copy()
+        t3 = time.perf_counter()
+        self.times["slot_wait"] += t1 - t0
+        self.times["read"] += t2 - t1
+        self.times["call"] += t3 - t0
         return H, W, es
 
     def _raise_failed(self, slot):
