@@ -113,6 +113,11 @@ def parse():
     p.add_argument("--hbm-skip-gb", type=float, default=0.0,
                    help="hold an allocation of this many GB before the sites' buffers "
                         "(placement study: which HBM region the first buffer lands in)")
+    p.add_argument("--jobs-in-flight", type=int, default=2,
+                   help="one channel on one rank: consecutive jobs (steps) alternate between "
+                        "this many statistics handles / correctors / streams, so job k+1's "
+                        "Welford pass runs while job k's histogram tail finishes (each job "
+                        "still complete and checked; 1 = one job at a time)")
     p.add_argument("--channel-streams", choices=["per-channel", "one"], default="per-channel",
                    help="several channels: each on its own stream (its merges overlap the "
                         "others' kernels), or all on one stream")
@@ -1178,9 +1183,16 @@ def main():
         stream (channel 0 runs on the main stream; with several channels the
         others overlap on their own streams, configs[2]/[3])."""
 
-        def __init__(self, c):
-            self.stream = stream if c == 0 or a.channel_streams == "one" else torch.cuda.Stream(dev)
+        def __init__(self, c, lane=0):
+            self.lane = lane
+            self.stream = (stream if (c == 0 and lane == 0) or a.channel_streams == "one"
+                           else torch.cuda.Stream(dev))
             self.sp = C.c_void_p(self.stream.cuda_stream)
+            # jobs in flight: the corrected pass on a stream of its own, so the
+            # histogram tail runs on the statistics handle's stream after it
+            # (tmhip.h stream contract) and the next job need not wait for it
+            self.cstream = torch.cuda.Stream(dev) if jobs_in_flight > 1 else self.stream
+            self.csp = C.c_void_p(self.cstream.cuda_stream)
             blk_in, blk_out = chan_sites[c]
             self.blocks = (blk_in, blk_out)
             self.S_ptr = C.c_void_p(blk_in[0].data_ptr())
@@ -1237,10 +1249,10 @@ def main():
             if fused and B:
                 hip.check(L.tmh_correct_u16_hist_blocks_device(self.corr, self.h, self.T_in,
                                                                self.T_out, shift, S, -1, -1,
-                                                               self.sp))
+                                                               self.csp))
             elif fused:
                 hip.check(L.tmh_correct_u16_hist_device(self.corr, self.h, self.S_ptr, self.O_ptr,
-                                                        S, -1, -1, self.sp))
+                                                        S, -1, -1, self.csp))
             else:
                 hip.check(L.tmh_correct_u16_device(self.corr, self.S_ptr, self.O_ptr, S, -1, -1,
                                                    self.sp))
@@ -1254,12 +1266,30 @@ def main():
             L.tmh_corrector_destroy(self.corr)
             L.tmh_stats_destroy(self.h)
 
+    # jobs in flight (one channel, one rank): lanes share the sites and the
+    # output blocks; job k runs on lane k % J after job k-1's corrected pass
+    # (outputs written in job order, HBM passes one at a time), so what
+    # overlaps is job k's Welford pass with job k-1's histogram tail
+    J = jobs_in_flight = max(1, a.jobs_in_flight) if (CH == 1 and not dist_on and fused) else 1
     chans = [Channel(c) for c in range(CH)]
+    lanes = chans + [Channel(0, lane=j) for j in range(1, J)]
+    jobs = {"k": 0, "applied": None}
     log("%d channel(s) x %d sites resident; warm-up" % (CH, S))
 
     timing = {"on": False}
 
     def step():
+        if J > 1:
+            ch = lanes[jobs["k"] % J]
+            jobs["k"] += 1
+            if jobs["applied"] is not None:  # after the previous job's corrected pass
+                ch.stream.wait_event(jobs["applied"])
+            ch.stats()
+            ch.apply()
+            ev = torch.cuda.Event()
+            ev.record(ch.cstream)
+            jobs["applied"] = ev
+            return
         for ch in chans:
             ch.stats()
         evs = {}
@@ -1340,7 +1370,7 @@ def main():
     # against its oracle fingerprint (tests/golden/make_bench_fingerprint.py)
     check, check_ok = {}, None
     per_channel = {}
-    for c, ch in enumerate(chans):
+    for c, ch in list(enumerate(chans)) + [(0, ln) for ln in lanes[1:]]:
         nn = C.c_int64()
         res = {"mean": np.empty(npx), "std": np.empty(npx), "acc": np.empty(Q),
                "hist": np.empty(65536, np.uint64)}
@@ -1374,8 +1404,10 @@ def main():
                 "frac_equal": round(cnt[0] / tot, 6), "frac_plus1": round(cnt[1] / tot, 6),
                 "frac_minus1": round(cnt[2] / tot, 6), "beyond_1DN": int(cnt[3]),
                 "wrap_flips": int(cnt[4])}
-            per_channel[c] = all(oks.values())
-        if c == 0:
+            per_channel[c] = per_channel.get(c, True) and all(oks.values())
+        if ch.lane > 0:  # the other jobs-in-flight lane(s): their own statistics, same outputs
+            check.setdefault("lanes", {})["lane%d" % ch.lane] = chk
+        elif c == 0:
             check = chk
         else:
             check.setdefault("channels", {})["c%d" % c] = chk
@@ -1388,6 +1420,17 @@ def main():
 
     log("%.1f ms/step; check_vs_oracle %s" % (1e3 * elapsed / a.steps, check_ok))
     extras = {}
+    if J > 1 and not a.no_extras:
+        # the same K jobs one at a time (lane 0 only), for comparison
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(a.steps):
+            chans[0].stats()
+            chans[0].apply()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter() - t1
+        extras["one_job_at_a_time"] = {"sites_per_s": round(CH * S * a.steps / t1, 1),
+                                       "ms_per_step": round(1e3 * t1 / a.steps, 3)}
     if not a.no_extras and world == 1:
         # the chain pass reads one contiguous run of sites
         if B:
@@ -1486,6 +1529,7 @@ def main():
                        "corrected_outputs": ("channels share output blocks except the checked "
                                              "sites' blocks" if share_out else "private"),
                        "pipeline": a.pipeline,
+                       "jobs_in_flight": J,
                        "hbm_layout": (("sites in one buffer, corrected output in blocks of %d "
                                        "sites" % B) if in_contig else
                                       ("blocks of %d sites, input and output blocks allocated "
@@ -1511,7 +1555,7 @@ def main():
         resd["cpu_baseline"] = cpu
         print(json.dumps(resd), file=out, flush=True)
 
-    for ch in chans:
+    for ch in lanes:
         ch.close()
     if dist_on:
         dist.destroy_process_group()

@@ -290,6 +290,10 @@ struct tmh_corrector {
   DBuf<uint8_t> stage8_in, stage8_out;
   HostPipe pipe;
   HostOpts host;  // TMH_OPT_COPY_THREADS / TMH_OPT_HOST_STAGING
+  // a histogram tail still reading queues (round masks) on a statistics
+  // handle's stream (correct_hist_dev, cross-stream calls)
+  hipEvent_t ev_tail = nullptr;
+  bool tail_pending = false;
 };
 
 static hipStream_t pick(hipStream_t own, void* s) { return s ? (hipStream_t)s : own; }
@@ -1055,6 +1059,10 @@ int tmh_corrector_create(const double* host_mean, const double* host_std, int he
 void tmh_corrector_destroy(tmh_corrector* c) {
   if (!c) return;
   (void)hipStreamSynchronize(c->stream);
+  if (c->ev_tail) {
+    (void)hipEventSynchronize(c->ev_tail);
+    (void)hipEventDestroy(c->ev_tail);
+  }
   delete c;
 }
 
@@ -1222,6 +1230,10 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
       TMH_HIP(hipEventRecord(h->ev_in, h->stream));
       TMH_HIP(hipStreamWaitEvent(s, h->ev_in, 0));
     }
+    if (c->tail_pending) {  // an earlier call's tail still reads this corrector's round masks
+      TMH_HIP(hipStreamWaitEvent(s, c->ev_tail, 0));
+      c->tail_pending = false;
+    }
     // the fused pass floors zero pixels at 10**zero_log10 in f32
     const bool zl_ok = !c->log_transform || (c->zero_log10 >= -37.0 && c->zero_log10 <= 0.0);
     const bool vec = zl_ok && (h->npx & 7) == 0 &&
@@ -1284,22 +1296,34 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
         launch_hist_site_u16(dev_in, h->npx, n_sites, h->hist_full.p, h->qp, vlh, ld, h->pooled.p,
                              h->pooled_parts.p, kPooledParts, h->zeros.p, sh, h->wide.p,
                              xwide_thresh, s, tab);
+      // The histogram tail (order statistics, percentile sums) reads only the
+      // handle's buffers: called on another stream than the handle's, it runs
+      // on the handle's stream, so s is free as soon as the corrected sites
+      // are written (a caller pipelining jobs starts the next one's Welford
+      // pass under this one's tail).
+      hipStream_t ts = s;
+      if (cross) {
+        TMH_HIP(hipEventRecord(h->ev_out, s));
+        TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
+        ts = h->stream;
+      }
       launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, n_sites, h->qp, vlh, ld,
-                           h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, sh, s, false,
+                           h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, sh, ts, false,
                            rm_all, h->wide.p, xwide_thresh);
       if (!(h->flags & TMH_STATS_DEFERRED_PCT))
-        launch_pct_accumulate(vlh, n_sites, ld, h->Q, h->gamma.p, h->acc.p, s);
+        launch_pct_accumulate(vlh, n_sites, ld, h->Q, h->gamma.p, h->acc.p, ts);
       h->hist_dirty = false;
       if (h->flags & TMH_STATS_DEFERRED_PCT) h->n_deferred += n_sites;
       h->last_batch = n_sites;
       h->pending -= n_sites;
       if (h->pending == 0) {  // the wide counts restart with the next Welford batch
-        TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, s));
+        TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, ts));
         h->wide_sites = 0;
       }
       if (cross) {
-        TMH_HIP(hipEventRecord(h->ev_out, s));
-        TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
+        if (!c->ev_tail) TMH_HIP(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
+        TMH_HIP(hipEventRecord(c->ev_tail, ts));
+        c->tail_pending = true;
       }
       return;
     }
