@@ -1575,7 +1575,7 @@ int tmh_inflate_device(const uint8_t* dev_src, int64_t src_bytes, const tmh_zchu
     if (n_chunks == 0) return;
     TMH_CHECK(dev_src && dev_chunks && dev_raw && dev_status && dev_scratch, TMH_EINVAL,
               "bad arguments");
-    TMH_CHECK(raw_max < (int64_t(1) << 32), TMH_EINVAL, "chunks must hold fewer than 2^32 bytes");
+    TMH_CHECK(raw_max < (int64_t(1) << 31), TMH_EINVAL, "chunks must hold fewer than 2^31 bytes");
     TMH_CHECK(scratch_bytes >= inflate_scratch_bytes(n_chunks, raw_max), TMH_EINVAL,
               "scratch smaller than tmh_inflate_scratch_bytes");
     TMH_CHECK((reinterpret_cast<uintptr_t>(dev_scratch) & 15) == 0, TMH_EINVAL,

@@ -101,7 +101,6 @@ struct Bits {
   uint32_t fill;   // dwords put into the ring (a multiple of 4)
   int64_t p;       // byte offset in src of the ring's next 16 bytes (16-byte aligned)
   int64_t end;     // src bytes (loads at or past it read 0)
-  int64_t used;    // bits consumed so far
 #if TMH_ZPROF
   uint32_t slow;  // codes decoded by the canonical search
   uint32_t priv;  // synchronous 16-byte units (ring ran dry)
@@ -198,12 +197,16 @@ TMH_ZDEV void refill_ring(Bits& b, ZShared<W>& z, int lane) {
   b.head += need ? 1u : 0u;
 }
 
+// stream bits consumed: loaded from src_off on, less what the ring and the buffer hold
+TMH_ZDEV int64_t consumed_bits(const Bits& b, int64_t src_off) {
+  return (b.p - src_off) * 8 - (int64_t)(b.fill - b.head) * 32 - b.nb;
+}
+
 template <int W>
 TMH_ZDEV uint32_t take(Bits& b, int n) {  // n <= the bits in the buffer
   const uint32_t v = (uint32_t)(b.bb & ((1ull << n) - 1ull));
   b.bb >>= n;
   b.nb -= n;
-  b.used += n;
   return v;
 }
 
@@ -213,7 +216,6 @@ TMH_ZDEV uint32_t getb(Bits& b, const uint8_t* src, ZShared<W>& z, int lane, int
   const uint32_t v = (uint32_t)(b.bb & ((1ull << n) - 1ull));
   b.bb >>= n;
   b.nb -= n;
-  b.used += n;
   return v;
 }
 
@@ -233,7 +235,6 @@ TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, ZShared<W>& z, uint16_t (*fast
     const int len = (int)(e >> 12);
     b.bb >>= len;
     b.nb -= len;
-    b.used += len;
     return (int)(e & 0x1FFu);
   }
 #if TMH_ZPROF
@@ -249,7 +250,6 @@ TMH_ZDEV int hdecode(Bits& b, const uint8_t* src, ZShared<W>& z, uint16_t (*fast
   const uint32_t code = v >> (15 - len);
   b.bb >>= len;
   b.nb -= len;
-  b.used += len;
   // in range for every code hbuild accepted; clamped so no input can index past the table
   const uint32_t i = (uint16_t)(base[len][lane] + code);
   return sym[i < (uint32_t)nsym ? i : (uint32_t)nsym - 1u][lane];
@@ -356,9 +356,9 @@ TMH_ZHD int64_t match_cap(int64_t mw) { return (mw - kMlHead) / 2; }
 // [out, out + olen) are stored, one by one.
 struct OutBuf {
   TMH_ZGLOBAL uint8_t* out;
-  int64_t olen;
-  int64_t mis;   // out's offset past a 16-byte boundary
-  int64_t g;     // current group: bytes [16 g - mis, 16 g - mis + 16) of out (-1: none)
+  int olen;
+  int mis;  // out's offset past a 16-byte boundary
+  int g;    // current group: bytes [16 g - mis, 16 g - mis + 16) of out (-1: none)
   uint64_t lo, hi;
 };
 
@@ -368,9 +368,9 @@ TMH_ZDEV void ob_flush(OutBuf& w) {
 #endif
   if (w.g < 0) return;
 #if TMH_ZPROF == 3  // timing experiment: the stores wrapped into the first 4 KB
-  const int64_t s0 = (16 * w.g - w.mis) & 4095;
+  const int s0 = (16 * w.g - w.mis) & 4095;
 #else
-  const int64_t s0 = 16 * w.g - w.mis;
+  const int s0 = 16 * w.g - w.mis;
 #endif
   if (s0 >= 0 && s0 + 16 <= w.olen) {
     TMH_ZST16(w.out + s0, w.lo, w.hi);
@@ -381,16 +381,16 @@ TMH_ZDEV void ob_flush(OutBuf& w) {
   }
 }
 
-TMH_ZDEV void ob_put(OutBuf& w, int64_t o, uint32_t byte) {
-  const int64_t a = o + w.mis;
-  const int64_t g = a >> 4;
+TMH_ZDEV void ob_put(OutBuf& w, int o, uint32_t byte) {
+  const int a = o + w.mis;
+  const int g = a >> 4;
   if (g != w.g) {
     ob_flush(w);
     w.g = g;
     w.lo = 0;
     w.hi = 0;
   }
-  const int sh = (int)(a & 7) * 8;
+  const int sh = (a & 7) * 8;
   if (a & 8) w.hi |= (uint64_t)byte << sh;
   else w.lo |= (uint64_t)byte << sh;
 }
@@ -404,7 +404,7 @@ TMH_ZDEV void ob_put(OutBuf& w, int64_t o, uint32_t byte) {
 template <int W>
 TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
                             const tmh_zchunk& c, uint8_t* __restrict__ dst, int64_t dst_bytes,
-                            uint32_t* __restrict__ ml, int64_t ml_cap,
+                            uint32_t* __restrict__ ml, int ml_cap,
                             ZShared<W>& z, int lane) {
   int err = kZOk;
   if (c.src_off < 0 || c.src_len < 0 || c.src_off + c.src_len > src_bytes || c.raw_off < 0 ||
@@ -412,11 +412,11 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
     return kZInput;
   }
   TMH_ZGLOBAL uint8_t* out = (TMH_ZGLOBAL uint8_t*)(dst + c.raw_off);
-  const int64_t olen = c.raw_len;
+  const int olen = (int)c.raw_len;  // < 2^31 (tmh_inflate_device checks raw_max)
   ml[0] = 0u;
   if (c.flags & 1) {  // the HDF5 filter was skipped: raw bytes, nothing to check
     if (c.src_len != c.raw_len) return kZSize;
-    for (int64_t i = 0; i < olen; ++i) out[i] = src[c.src_off + i];
+    for (int i = 0; i < olen; ++i) out[i] = src[c.src_off + i];
     ml[1] = 0xFFFFFFFFu;  // no Adler-32 to check
     return kZOk;
   }
@@ -431,20 +431,22 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
     const int sh = (int)(c.src_off & 3) * 8;
     b.bb = (uint64_t)next_dword<W>(src, b, z, lane) >> sh;
     b.nb = 32 - sh;
-    b.used = 0;
   }
   const int64_t in_bits = (int64_t)c.src_len * 8;
-  OutBuf w{out, olen, (int64_t)((uintptr_t)(dst + c.raw_off) & 15u), -1, 0, 0};
+  // loads running this far past the stream mean a corrupt stream (checked per
+  // symbol on the ring's load position; exactly at the trailer)
+  const int64_t p_limit = c.src_off + c.src_len + 256;
+  OutBuf w{out, olen, (int)((uintptr_t)(dst + c.raw_off) & 15u), -1, 0, 0};
   uint32_t mp0 = 0, mp1 = 0;  // an odd match waiting for its pair's store
   // zlib header (RFC 1950): CM = 8, CINFO <= 7, FCHECK, no preset dictionary
   const uint32_t cmf = getb<W>(b, src, z, lane, 8), flg = getb<W>(b, src, z, lane, 8);
   if ((cmf & 15u) != 8u || (cmf >> 4) > 7u || ((cmf << 8) | flg) % 31u != 0u || (flg & 0x20u))
     err = kZHeader;
-  int64_t o = 0;   // output bytes (literals written, matches listed)
-  int64_t nm = 0;  // matches listed
+  int o = 0;   // output bytes (literals written, matches listed)
+  int nm = 0;  // matches listed
   int state = err ? kStDone : kStBlock;
   int last = 0;
-  int64_t stored_left = 0;
+  int stored_left = 0;
 #if TMH_ZPROF
   b.slow = 0;
   b.priv = 0;
@@ -457,7 +459,7 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
     const uint64_t t0 = TMH_ZCLOCK();
     const int st0 = state;
 #endif
-    if (b.used > in_bits + 64) {  // ran far past the stream: corrupt
+    if (consumed_bits(b, c.src_off) > in_bits + 64) {  // ran far past the stream: corrupt
       err = kZInput;
       break;
     }
@@ -506,7 +508,7 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
             o += len;
           }
         }
-        if (b.used > in_bits + 64) ecode = kZInput;  // ran far past the stream: corrupt
+        if (b.p > p_limit) ecode = kZInput;  // ran far past the stream: corrupt
         if (ecode) {
           err = ecode;
           state = kStDone;
@@ -526,7 +528,7 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
         const int drop = b.nb & 7;
         b.bb >>= drop;
         b.nb -= drop;
-        b.used += drop;
+  
         const uint32_t len = getb<W>(b, src, z, lane, 16), nlen = getb<W>(b, src, z, lane, 16);
         if ((len ^ nlen) != 0xFFFFu) {
           err = kZStored;
@@ -615,12 +617,12 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
       const int drop = b.nb & 7;
       b.bb >>= drop;
       b.nb -= drop;
-      b.used += drop;
+
       uint32_t want = 0;
       for (int i = 0; i < 4; ++i) want = (want << 8) | getb<W>(b, src, z, lane, 8);
       ml[1] = want;
       if (o != olen) err = kZSize;
-      else if (b.used > in_bits) err = kZInput;
+      else if (consumed_bits(b, c.src_off) > in_bits) err = kZInput;
       state = kStDone;
     }
 #if TMH_ZPROF
