@@ -1370,7 +1370,7 @@ def main():
     # against its oracle fingerprint (tests/golden/make_bench_fingerprint.py)
     check, check_ok = {}, None
     per_channel = {}
-    for c, ch in list(enumerate(chans)) + [(0, ln) for ln in lanes[1:]]:
+    for c, ch in list(enumerate(chans)) + [(0, ln) for ln in lanes[len(chans):]]:
         nn = C.c_int64()
         res = {"mean": np.empty(npx), "std": np.empty(npx), "acc": np.empty(Q),
                "hist": np.empty(65536, np.uint64)}

@@ -281,8 +281,9 @@ int tmh_correct_u16_device(tmh_corrector* c, const uint16_t* dev_in, uint16_t* d
  * already queued on h's stream, and h's stream waits for it before any later
  * work on h -- the two handles may live on different streams.  On another
  * stream than h's, the histogram tail (per-site order statistics, percentile
- * sums) runs on h's stream: `stream` is free once the corrected sites are
- * written, so a caller can start its next job there under this one's tail.
+ * sums) runs on a stream of h's own, which h's stream waits for:
+ * `stream` is free once the corrected sites are written, so a caller can
+ * start its next job under this one's tail.
  * dev_in and
  * dev_out must not overlap (the pass re-reads its input after storing
  * outputs: f64 fixups, packed-counter recounts; overlapping runs are

@@ -239,6 +239,12 @@ struct tmh_stats {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;   // histogram pass runs here, concurrent with Welford
+  // the fused pass's histogram tail when the pass runs on another stream
+  // (correct_hist_dev).  (At the lowest priority, with the caller's streams
+  // above it, a two-jobs-in-flight bench ran 4-6% slower: profiles/r4/
+  // ab_jobs_in_flight_priority_r4y.txt.)
+  hipStream_t tail = nullptr;
+  hipEvent_t ev_tail = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;  // ordering against a caller's stream
   int fused_cfg = kFusedAuto;     // TMH_OPT_FUSED_CONFIG (-1: per launch, on the device)
@@ -399,6 +405,8 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
       h->batch_cap = std::min(4096, batch_capacity > 0 ? batch_capacity : 1);
       TMH_HIP(hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking));
       TMH_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+      TMH_HIP(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
+      TMH_HIP(hipEventCreateWithFlags(&h->ev_tail, hipEventDisableTiming));
       TMH_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
       TMH_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
       TMH_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
@@ -449,8 +457,10 @@ void tmh_stats_destroy(tmh_stats* h) {
   if (!h) return;
   if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
   if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
-  hipStream_t s = h->own_stream, side = h->side;
+  hipStream_t s = h->own_stream, side = h->side, tail = h->tail;
   if (side) (void)hipStreamSynchronize(side);
+  if (tail) (void)hipStreamSynchronize(tail);
+  if (h->ev_tail) (void)hipEventDestroy(h->ev_tail);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
@@ -458,6 +468,7 @@ void tmh_stats_destroy(tmh_stats* h) {
   delete h;
   if (s) (void)hipStreamDestroy(s);
   if (side) (void)hipStreamDestroy(side);
+  if (tail) (void)hipStreamDestroy(tail);
 }
 
 int tmh_stats_set_stream(tmh_stats* h, void* stream) {
@@ -1298,14 +1309,15 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
                              xwide_thresh, s, tab);
       // The histogram tail (order statistics, percentile sums) reads only the
       // handle's buffers: called on another stream than the handle's, it runs
-      // on the handle's stream, so s is free as soon as the corrected sites
-      // are written (a caller pipelining jobs starts the next one's Welford
-      // pass under this one's tail).
+      // on the handle's tail stream (the handle's stream waits for it), so s
+      // is free as soon as the corrected sites are written (a caller
+      // pipelining jobs starts the next one's Welford pass under this one's
+      // tail).
       hipStream_t ts = s;
       if (cross) {
         TMH_HIP(hipEventRecord(h->ev_out, s));
-        TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
-        ts = h->stream;
+        TMH_HIP(hipStreamWaitEvent(h->tail, h->ev_out, 0));
+        ts = h->tail;
       }
       launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, n_sites, h->qp, vlh, ld,
                            h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, sh, ts, false,
@@ -1320,7 +1332,9 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
         TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, ts));
         h->wide_sites = 0;
       }
-      if (cross) {
+      if (cross) {  // the handle's later work, and this corrector's next pass, after the tail
+        TMH_HIP(hipEventRecord(h->ev_tail, ts));
+        TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_tail, 0));
         if (!c->ev_tail) TMH_HIP(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
         TMH_HIP(hipEventRecord(c->ev_tail, ts));
         c->tail_pending = true;
