@@ -118,6 +118,10 @@ def parse():
                         "this many statistics handles / correctors / streams, so job k+1's "
                         "Welford pass runs while job k's histogram tail finishes (each job "
                         "still complete and checked; 1 = one job at a time)")
+    p.add_argument("--jobs-order", choices=["welford", "corrected"], default="welford",
+                   help="jobs in flight: job k+1's Welford pass starts after job k's Welford pass "
+                        "(it then shares HBM with job k's corrected pass and hides job k's small "
+                        "kernels and tail) or after job k's corrected pass (hides only the tail)")
     p.add_argument("--channel-streams", choices=["per-channel", "one"], default="per-channel",
                    help="several channels: each on its own stream (its merges overlap the "
                         "others' kernels), or all on one stream")
@@ -1273,7 +1277,7 @@ def main():
     J = jobs_in_flight = max(1, a.jobs_in_flight) if (CH == 1 and not dist_on and fused) else 1
     chans = [Channel(c) for c in range(CH)]
     lanes = chans + [Channel(0, lane=j) for j in range(1, J)]
-    jobs = {"k": 0, "applied": None}
+    jobs = {"k": 0, "applied": None, "welford": None}
     log("%d channel(s) x %d sites resident; warm-up" % (CH, S))
 
     timing = {"on": False}
@@ -1282,9 +1286,15 @@ def main():
         if J > 1:
             ch = lanes[jobs["k"] % J]
             jobs["k"] += 1
-            if jobs["applied"] is not None:  # after the previous job's corrected pass
-                ch.stream.wait_event(jobs["applied"])
+            gate = jobs["welford"] if a.jobs_order == "welford" else jobs["applied"]
+            if gate is not None:  # after the previous job's Welford (or corrected) pass
+                ch.stream.wait_event(gate)
             ch.stats()
+            ev_w = torch.cuda.Event()
+            ev_w.record(ch.stream)
+            jobs["welford"] = ev_w
+            if jobs["applied"] is not None:  # corrected passes in job order (shared outputs)
+                ch.cstream.wait_event(jobs["applied"])
             ch.apply()
             ev = torch.cuda.Event()
             ev.record(ch.cstream)
@@ -1420,17 +1430,30 @@ def main():
 
     log("%.1f ms/step; check_vs_oracle %s" % (1e3 * elapsed / a.steps, check_ok))
     extras = {}
+    solo_kern = {}
     if J > 1 and not a.no_extras:
-        # the same K jobs one at a time (lane 0 only), for comparison
+        # the same K jobs one at a time (lane 0 only), for comparison, with
+        # each kernel's duration when no other job shares the GPU
         torch.cuda.synchronize(dev)
+        if prof:
+            L.tmh_profile_enable(1)
+            L.tmh_profile_reset()
         t1 = time.perf_counter()
         for _ in range(a.steps):
             chans[0].stats()
             chans[0].apply()
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter() - t1
+        if prof:
+            for name in ("welford", "correct_hist", "hist_finalize", "pct_acc"):
+                ms, k = C.c_double(), C.c_int64()
+                hip.check(L.tmh_profile_read(name.encode(), C.byref(ms), C.byref(k)))
+                if k.value:
+                    solo_kern[name] = ms.value / k.value
+            L.tmh_profile_enable(0)
         extras["one_job_at_a_time"] = {"sites_per_s": round(CH * S * a.steps / t1, 1),
-                                       "ms_per_step": round(1e3 * t1 / a.steps, 3)}
+                                       "ms_per_step": round(1e3 * t1 / a.steps, 3),
+                                       "kernel_avg_ms": {k: round(v, 4) for k, v in solo_kern.items()}}
     if not a.no_extras and world == 1:
         # the chain pass reads one contiguous run of sites
         if B:
@@ -1484,6 +1507,16 @@ def main():
             roofline = {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                         "traffic": traffic, "alg_bytes_per_launch": alg[dominant]}
+            if J > 1:
+                roofline["note"] = ("%d jobs in flight: this pass shares HBM with the next job's "
+                                    "Welford pass, so its launches last longer than alone"
+                                    % J) if a.jobs_order == "welford" else (
+                                    "%d jobs in flight (the next job's Welford pass after this "
+                                    "pass)" % J)
+                if dominant in solo_kern:
+                    solo = alg[dominant] / (solo_kern[dominant] * 1e-3) / 1e9
+                    roofline["achieved_one_job_at_a_time"] = round(solo, 1)
+                    roofline["frac_one_job_at_a_time"] = round(solo / HBM_PEAK_GBS, 4)
         total_sites = world * CH * S * a.steps if not sharded else CH * S_total * a.steps
         value = total_sites / elapsed
         job_bytes = total_sites // a.steps * 6 * npx  # 6 B/px algorithmic per site-image
@@ -1530,6 +1563,7 @@ def main():
                                              "sites' blocks" if share_out else "private"),
                        "pipeline": a.pipeline,
                        "jobs_in_flight": J,
+                       "jobs_order": a.jobs_order if J > 1 else None,
                        "hbm_layout": (("sites in one buffer, corrected output in blocks of %d "
                                        "sites" % B) if in_contig else
                                       ("blocks of %d sites, input and output blocks allocated "
