@@ -405,8 +405,7 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
       h->batch_cap = std::min(4096, batch_capacity > 0 ? batch_capacity : 1);
       TMH_HIP(hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking));
       TMH_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-      TMH_HIP(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
-      TMH_HIP(hipEventCreateWithFlags(&h->ev_tail, hipEventDisableTiming));
+
       TMH_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
       TMH_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
       TMH_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
@@ -1315,6 +1314,10 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
       // tail).
       hipStream_t ts = s;
       if (cross) {
+        if (!h->tail) {  // created on first use: every stream takes a hardware queue slot
+          TMH_HIP(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
+          TMH_HIP(hipEventCreateWithFlags(&h->ev_tail, hipEventDisableTiming));
+        }
         TMH_HIP(hipEventRecord(h->ev_out, s));
         TMH_HIP(hipStreamWaitEvent(h->tail, h->ev_out, 0));
         ts = h->tail;
