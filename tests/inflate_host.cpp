@@ -23,6 +23,7 @@ static inline uint32_t bitrev32(uint32_t x) {
 #define TMH_ZBITREV32(x) bitrev32(x)
 #define __restrict__
 #define TMH_ZGLOBAL
+#define TMH_ZBFE(x, n) ((n) ? ((x) & (0xFFFFFFFFu >> (32 - (n)))) : 0u)
 #define TMH_ZST16(p, lo, hi)               \
   do {                                     \
     const uint64_t v_[2] = {(lo), (hi)};   \
@@ -43,6 +44,11 @@ static inline uint32_t bitrev32(uint32_t x) {
     memcpy((p), v_, 16);                   \
   } while (0)
 #define TMH_ZANY(pred) (pred)
+#define TMH_ZST8(p, a, b)                                    \
+  do {                                                       \
+    const uint32_t v8_[2] = {(uint32_t)(a), (uint32_t)(b)};  \
+    memcpy((p), v8_, 8);                                     \
+  } while (0)
 #include "../tmlibrary_amd/csrc/inflate_core.h"
 
 static std::vector<uint8_t> slurp(const char* p) {
@@ -57,15 +63,6 @@ static std::vector<uint8_t> slurp(const char* p) {
 }
 
 int main(int argc, char** argv) {
-  // the data loop's length / distance arithmetic equals RFC 1951's tables
-  for (int i = 0; i < 29; ++i)
-    if ((int)(tmh::kLenCode[i] & 0xFFFF) != tmh::len_base(i) ||
-        (int)(tmh::kLenCode[i] >> 16) != tmh::len_extra(i))
-      return 3;
-  for (int d = 0; d < 30; ++d)
-    if ((int)(tmh::kDistCode[d] & 0xFFFF) != tmh::dist_base(d) ||
-        (int)(tmh::kDistCode[d] >> 16) != tmh::dist_extra(d))
-      return 3;
   if (argc != 6) return 2;
   const std::vector<uint8_t> tab = slurp(argv[1]), blob = slurp(argv[2]);
   const long long raw_bytes = atoll(argv[3]);
@@ -73,6 +70,10 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> out((size_t)raw_bytes + 1, 0);
   std::vector<int32_t> st(n, 0);
   static tmh::ZShared<> z;
+  for (int i = 0; i < 30; ++i) {  // the kernel's per-workgroup copy of the code tables
+    if (i < 29) z.ltab[i] = tmh::kLenCode[i];
+    z.dtab[i] = tmh::kDistCode[i];
+  }
   std::vector<tmh_zchunk> cs(n);
   int64_t raw_max = 0;
   for (size_t i = 0; i < n; ++i) {

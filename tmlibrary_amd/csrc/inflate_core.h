@@ -20,6 +20,17 @@
 #ifndef TMH_ZCLOCK
 #define TMH_ZCLOCK() __builtin_readcyclecounter()
 #endif
+#ifndef TMH_ZST8
+#define TMH_ZST8(p, a, b)                                            \
+  do {                                                               \
+    typedef uint32_t Z8_ __attribute__((ext_vector_type(2)));       \
+    *reinterpret_cast<Z8_*>(p) = Z8_{(uint32_t)(a), (uint32_t)(b)};  \
+  } while (0)
+#endif
+#ifndef TMH_ZBFE
+// the low n bits of x (0 <= n <= 31): one v_bfe_u32
+#define TMH_ZBFE(x, n) __builtin_amdgcn_ubfe((x), 0u, (unsigned)(n))
+#endif
 #ifndef TMH_ZLD16
 // one 16-byte load from a 16-byte aligned p into four dwords
 #define TMH_ZLD16(p, a, b, c, d)                                        \
@@ -68,6 +79,7 @@ template <int W = kZW>
 struct ZShared {
   static constexpr int kW = W;
   alignas(16) uint32_t ring[W][kRingStride];
+  uint32_t ltab[29], dtab[30];  // kLenCode / kDistCode, shared by the workgroup
   uint16_t lfast[1 << kLFast][W];
   uint16_t dfast[1 << kDFast][W];
   uint16_t llim[16][W];   // left-justified limit of code length l (index 1..15)
@@ -203,8 +215,8 @@ TMH_ZDEV int64_t consumed_bits(const Bits& b, int64_t src_off) {
 }
 
 template <int W>
-TMH_ZDEV uint32_t take(Bits& b, int n) {  // n <= the bits in the buffer
-  const uint32_t v = (uint32_t)(b.bb & ((1ull << n) - 1ull));
+TMH_ZDEV uint32_t take(Bits& b, int n) {  // n <= 16 and <= the bits in the buffer
+  const uint32_t v = TMH_ZBFE((uint32_t)b.bb, n);
   b.bb >>= n;
   b.nb -= n;
   return v;
@@ -213,7 +225,7 @@ TMH_ZDEV uint32_t take(Bits& b, int n) {  // n <= the bits in the buffer
 template <int W>
 TMH_ZDEV uint32_t getb(Bits& b, const uint8_t* src, ZShared<W>& z, int lane, int n) {
   refill<W>(b, src, z, lane);
-  const uint32_t v = (uint32_t)(b.bb & ((1ull << n) - 1ull));
+  const uint32_t v = TMH_ZBFE((uint32_t)b.bb, n);  // n <= 16
   b.bb >>= n;
   b.nb -= n;
   return v;
@@ -296,8 +308,9 @@ TMH_ZDEV bool hbuild(ZShared<W>& z, int lane, const uint8_t (*lens)[W], int off,
   return true;
 }
 
-// RFC 1951 3.2.5: length / distance symbol -> base | extra bits << 16 (the
-// reference the arithmetic below is checked against, tests/inflate_host.cpp)
+// RFC 1951 3.2.5: length / distance symbol -> base | extra bits << 16 (copied
+// into each workgroup's LDS: one lookup beat the arithmetic, 39.0 vs 40.4 ms
+// per 128 sites, profiles/r4/ab_inflate_ml8_ltab_r4zv.txt)
 TMH_ZCONST uint32_t kLenCode[29] = {
     3,  4,  5,  6,  7,  8,  9,  10, 11 | 1 << 16, 13 | 1 << 16, 15 | 1 << 16, 17 | 1 << 16,
     19 | 2 << 16, 23 | 2 << 16, 27 | 2 << 16, 31 | 2 << 16, 35 | 3 << 16, 43 | 3 << 16,
@@ -311,16 +324,6 @@ TMH_ZCONST uint32_t kDistCode[30] = {
     12289 | 12 << 16, 16385 | 13 << 16, 24577 | 13 << 16};
 TMH_ZCONST uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// RFC 1951 3.2.5's length and distance tables (kLenCode / kDistCode) as
-// arithmetic, for the data loop: a few dependent ALU operations instead of
-// an LDS round trip.  li = length symbol - 257 (0..28), d = distance code.
-TMH_ZHD int len_extra(int li) { return li < 8 || li == 28 ? 0 : (li - 4) >> 2; }
-TMH_ZHD int len_base(int li) {
-  return li < 8 ? li + 3 : li == 28 ? 258 : ((4 + (li & 3)) << ((li - 4) >> 2)) + 3;
-}
-TMH_ZHD int dist_extra(int d) { return d < 4 ? 0 : (d >> 1) - 1; }
-TMH_ZHD int dist_base(int d) { return d < 4 ? d + 1 : ((2 + (d & 1)) << ((d >> 1) - 1)) + 1; }
-
 enum : int { kStBlock = 0, kStData = 1, kStStored = 2, kStTrailer = 3, kStDone = 4 };
 
 
@@ -328,7 +331,7 @@ enum : int { kStBlock = 0, kStData = 1, kStStored = 2, kStTrailer = 3, kStDone =
 // 32-bit words, 16-byte aligned): [0] matches, [1] the stream's Adler-32
 // (big-endian value), [2..15] unused (TMH_ZPROF counters), then from word
 // kMlHead per match (output
-// position, length | distance << 9), written two matches per 16-byte store.
+// position, length | distance << 9), one 8-byte store per match.
 // A match needs at least 3 output bytes, so raw_len / 3 + 2 entries always fit.
 constexpr int kMlHead = 16;
 TMH_ZHD int64_t match_words(int64_t raw_max) {
@@ -344,56 +347,6 @@ TMH_ZHD int64_t match_cap(int64_t mw) { return (mw - kMlHead) / 2; }
     *(TMH_ZGLOBAL Z16_*)(p) = Z16_{(lo), (hi)};                      \
   } while (0)
 #endif
-
-// The literal bytes of a chunk gathered into 16-byte groups in registers
-// and written with one 16-byte store per group: a lane's byte stores went
-// to 64 different lines per wave instruction, and on gfx9 a wait for the
-// bit buffer's next load also waits for every store issued before it.
-// Output positions only grow, so each group is written once, when the
-// decode leaves it; bytes of the group that belong to back-references are
-// written as 0 and filled by phase 2.  The chunk's first and last groups may
-// be shared with the neighbouring chunks: only their bytes inside
-// [out, out + olen) are stored, one by one.
-struct OutBuf {
-  TMH_ZGLOBAL uint8_t* out;
-  int olen;
-  int mis;  // out's offset past a 16-byte boundary
-  int g;    // current group: bytes [16 g - mis, 16 g - mis + 16) of out (-1: none)
-  uint64_t lo, hi;
-};
-
-TMH_ZDEV void ob_flush(OutBuf& w) {
-#if TMH_ZPROF == 2  // timing experiment: no output stores
-  if (w.g != -7) return;
-#endif
-  if (w.g < 0) return;
-#if TMH_ZPROF == 3  // timing experiment: the stores wrapped into the first 4 KB
-  const int s0 = (16 * w.g - w.mis) & 4095;
-#else
-  const int s0 = 16 * w.g - w.mis;
-#endif
-  if (s0 >= 0 && s0 + 16 <= w.olen) {
-    TMH_ZST16(w.out + s0, w.lo, w.hi);
-  } else {
-    for (int i = 0; i < 16; ++i)
-      if (s0 + i >= 0 && s0 + i < w.olen)
-        w.out[s0 + i] = (uint8_t)((i < 8 ? w.lo >> (8 * i) : w.hi >> (8 * (i - 8))) & 0xFFu);
-  }
-}
-
-TMH_ZDEV void ob_put(OutBuf& w, int o, uint32_t byte) {
-  const int a = o + w.mis;
-  const int g = a >> 4;
-  if (g != w.g) {
-    ob_flush(w);
-    w.g = g;
-    w.lo = 0;
-    w.hi = 0;
-  }
-  const int sh = (a & 7) * 8;
-  if (a & 8) w.hi |= (uint64_t)byte << sh;
-  else w.lo |= (uint64_t)byte << sh;
-}
 
 // Phase 1 of a chunk (one zlib stream): Huffman-decode every symbol, write
 // the literal (and stored) bytes at their output positions, and append each
@@ -436,8 +389,6 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
   // loads running this far past the stream mean a corrupt stream (checked per
   // symbol on the ring's load position; exactly at the trailer)
   const int64_t p_limit = c.src_off + c.src_len + 256;
-  OutBuf w{out, olen, (int)((uintptr_t)(dst + c.raw_off) & 15u), -1, 0, 0};
-  uint32_t mp0 = 0, mp1 = 0;  // an odd match waiting for its pair's store
   // zlib header (RFC 1950): CM = 8, CINFO <= 7, FCHECK, no preset dictionary
   const uint32_t cmf = getb<W>(b, src, z, lane, 8), flg = getb<W>(b, src, z, lane, 8);
   if ((cmf & 15u) != 8u || (cmf >> 4) > 7u || ((cmf << 8) | flg) % 31u != 0u || (flg & 0x20u))
@@ -479,31 +430,26 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
         if (s < 256) {
           if (s < 0) ecode = kZCode;
           else if (o >= olen) ecode = kZOverflow;
-          else ob_put(w, o++, (uint32_t)s);
+          else out[o++] = (uint8_t)s;
         } else if (s == 256) {
           state = last ? kStTrailer : kStBlock;
         } else {
           const int li = s - 257 < 29 ? s - 257 : 28;
           // <= 15 + 5 bits since the refill: no refill before the length's extra bits
-          const int lx = len_extra(li);
-          const int len = len_base(li) + (int)take<W>(b, lx);
+          const uint32_t le = z.ltab[li];  // base | extra bits << 16
+          const int len = (int)(le & 0xFFFFu) + (int)take<W>(b, (int)(le >> 16));
           const int ds = hdecode<kDFast, W, true>(b, src, z, z.dfast, z.dlim, z.dbase, z.dsym,
                                                   kDsym, lane);
           const int dsc = ds >= 0 && ds < 30 ? ds : 0;
-          const int dist = dist_base(dsc) + (int)take<W>(b, dist_extra(dsc));
-          if (s - 257 >= 29 || ds < 0 || ds >= 30) ecode = kZCode;
-          else if (dist > o) ecode = kZDist;
-          else if (o + len > olen || nm >= ml_cap) ecode = kZOverflow;
-          else {
+          const uint32_t de = z.dtab[dsc];
+          const int dist = (int)(de & 0xFFFFu) + (int)take<W>(b, (int)(de >> 16));
+          ecode = (s - 257 >= 29 || ds < 0 || ds >= 30) ? kZCode
+                  : dist > o                              ? kZDist
+                  : (o + len > olen || nm >= ml_cap)      ? kZOverflow
+                                                          : kZOk;
+          if (ecode == kZOk) {
             const uint32_t e = (uint32_t)len | ((uint32_t)dist << 9);
-            if ((nm & 1) && TMH_ZPROF != 2) {
-              TMH_ZST16(ml + kMlHead + (TMH_ZPROF == 3 ? (2 * (nm - 1)) & 1023 : 2 * (nm - 1)),
-                        (uint64_t)mp0 | (uint64_t)mp1 << 32,
-                        (uint64_t)(uint32_t)o | (uint64_t)e << 32);
-            } else {
-              mp0 = (uint32_t)o;
-              mp1 = e;
-            }
+            TMH_ZST8(ml + kMlHead + 2 * nm, o, e);  // one 8-byte store per match
             ++nm;
             o += len;
           }
@@ -611,7 +557,7 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
         err = kZOverflow;
         break;
       }
-      ob_put(w, o++, getb<W>(b, src, z, lane, 8));
+      out[o++] = (uint8_t)getb<W>(b, src, z, lane, 8);
       --stored_left;
     } else {  // trailer: byte-align, Adler-32 big-endian
       const int drop = b.nb & 7;
@@ -643,11 +589,6 @@ TMH_ZDEV int inflate_tokens(const uint8_t* __restrict__ src, int64_t src_bytes,
   ml[9] = b.tops;
   ml[10] = (uint32_t)pc_hdr;
 #endif
-  ob_flush(w);
-  if (nm & 1) {
-    ml[kMlHead + 2 * (nm - 1)] = mp0;
-    ml[kMlHead + 2 * (nm - 1) + 1] = mp1;
-  }
   ml[0] = (uint32_t)nm;
   return err;
 }

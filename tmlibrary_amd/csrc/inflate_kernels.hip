@@ -45,6 +45,11 @@ __global__ __launch_bounds__(W) void k_inflate_tokens(
     int64_t mw, int32_t* __restrict__ status) {
   __shared__ ZShared<W> z;
   const int lane = threadIdx.x;
+  for (int i = lane; i < 30; i += W) {
+    if (i < 29) z.ltab[i] = kLenCode[i];
+    z.dtab[i] = kDistCode[i];
+  }
+  __syncthreads();
   const int64_t ci = (int64_t)blockIdx.x * W + lane;
   if (ci >= n_chunks) return;
   status[ci] = inflate_tokens<W>(src, src_bytes, chunks[ci], dst, dst_bytes, ml_all + ci * mw,
