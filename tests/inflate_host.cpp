@@ -24,11 +24,6 @@ static inline uint32_t bitrev32(uint32_t x) {
 #define __restrict__
 #define TMH_ZGLOBAL
 #define TMH_ZBFE(x, n) ((n) ? ((x) & (0xFFFFFFFFu >> (32 - (n)))) : 0u)
-#define TMH_ZST16(p, lo, hi)               \
-  do {                                     \
-    const uint64_t v_[2] = {(lo), (hi)};   \
-    memcpy((p), v_, 16);                   \
-  } while (0)
 #define TMH_ZLD16(p, a, b, c, d) \
   do {                           \
     uint32_t v_[4];              \

@@ -339,14 +339,6 @@ TMH_ZHD int64_t match_words(int64_t raw_max) {
 }
 TMH_ZHD int64_t match_cap(int64_t mw) { return (mw - kMlHead) / 2; }
 
-#ifndef TMH_ZST16
-// one 16-byte store; p is 16-byte aligned
-#define TMH_ZST16(p, lo, hi)                                         \
-  do {                                                               \
-    typedef uint64_t Z16_ __attribute__((ext_vector_type(2)));      \
-    *(TMH_ZGLOBAL Z16_*)(p) = Z16_{(lo), (hi)};                      \
-  } while (0)
-#endif
 
 // Phase 1 of a chunk (one zlib stream): Huffman-decode every symbol, write
 // the literal (and stored) bytes at their output positions, and append each
