@@ -23,6 +23,7 @@ static inline uint32_t bitrev32(uint32_t x) {
 #define TMH_ZBITREV32(x) bitrev32(x)
 #define __restrict__
 #define TMH_ZGLOBAL
+#define TMH_ZKEEP(v) (void)(v)
 #define TMH_ZBFE(x, n) ((n) ? ((x) & (0xFFFFFFFFu >> (32 - (n)))) : 0u)
 #define TMH_ZLD16(p, a, b, c, d) \
   do {                           \
