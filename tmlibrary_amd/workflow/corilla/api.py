@@ -82,6 +82,7 @@ class IllumstatsCalculator(object):
         self.decode = decode
         self.device_block = max(1, int(device_block))
         self._dev = None  # device decode state, kept across jobs (buffers, decoder)
+        self.last_timing = None  # the last run_job's phases (seconds)
 
     def create_run_batches(self, args=None, channel_files=None, channel_names=None, seed=None):
         """One job per channel (corilla/api.py:45-105).
@@ -244,12 +245,17 @@ class IllumstatsCalculator(object):
         log_zero_warnings(zc)
 
     def run_job(self, batch, assume_clean_state=False):
-        """corilla/api.py:115-146."""
+        """corilla/api.py:115-146.  The reference reads the first site to learn
+        the image dimensions; here the file's dataset shape gives them without
+        decoding it (~40 ms per job).  ``last_timing`` holds the job's phases
+        in seconds (sites -> statistics, read-back, illumstats write)."""
+        import time
+        t0 = time.perf_counter()
         file_ids = [_file_id(f) for f in batch["channel_image_files_ids"]]
         logger.info("calculate illumination statistics")
-        first = self.store.channel_image_file(file_ids[0]).get()
-        stats = OnlineStatistics(image_dimensions=first.dimensions[0:2],
-                                 batch_size=self.batch_size)
+        H, W, _ = channel_image_shape(self.store.channel_image_file(file_ids[0]).location)
+        stats = OnlineStatistics(image_dimensions=(H, W), batch_size=self.batch_size)
+        timing = {}
         try:
             done = False
             if self.decode != "host":
@@ -265,10 +271,16 @@ class IllumstatsCalculator(object):
                     for fid in ids:
                         logger.info("update statistics for image: %d", fid)
                     stats.update_batch(sites)
+            t1 = time.perf_counter()
+            timing["sites"] = t1 - t0
             stats_file = self.store.illumstats_file(batch["channel_id"])
             logger.info("write calculated statistics to file")
             illumstats = IllumstatsContainer(stats.mean, stats.std, stats.percentiles)
+            t2 = time.perf_counter()
+            timing["read_back"] = t2 - t1
             stats_file.put(illumstats)
+            timing["write"] = time.perf_counter() - t2
         finally:
             stats.close()
+        self.last_timing = timing
         return illumstats

@@ -99,6 +99,7 @@ def main():
                 t_one = time.perf_counter() - t0
                 pre = "run_job" if dec == "host" else "run_job_gpu_decode"
                 res["%s_sites_per_s" % pre] = round(a.sites / t_one, 1)
+                res["%s_phases_s" % pre] = {k: round(v, 4) for k, v in calc.last_timing.items()}
                 # a longer job over the same files: the per-job fixed cost (first
                 # block's decode before the GPU can start, finalize, smoothing-free
                 # statistics read-back, HDF5 write) is then amortised, and the
