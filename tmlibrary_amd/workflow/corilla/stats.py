@@ -19,6 +19,7 @@ Behavioural notes vs the reference
 from __future__ import annotations
 
 import ctypes as C
+import functools
 import logging
 
 import numpy as np
@@ -40,6 +41,16 @@ def log_zero_warnings(zero_counts):
         logger.warning("image contains zero values")
 
 
+@functools.lru_cache(maxsize=8)
+def _percentile_keys(decimals):
+    """The percentile keys as the reference builds them (Python's round of
+    each np.linspace(0, 100, 10**(decimals + 2)) value, stats.py:44-47):
+    100,000 rounds cost ~0.16 s, so once per process, not per job."""
+    q = np.linspace(0, 100, 10 ** (decimals + 2))
+    q.setflags(write=False)  # shared by every OnlineStatistics of the process
+    return q, tuple(round(x, decimals) for x in q)
+
+
 class OnlineStatistics(object):
     """Welford mean/variance + percentile accumulator (stats.py:35-121)."""
 
@@ -52,8 +63,7 @@ class OnlineStatistics(object):
             raise ValueError('Argument "decimals" must lie in range [0, 3].')
         self.decimals = decimals
         precision = 10 ** (decimals + 2)
-        self._q = np.linspace(0, 100, precision)
-        self._keys = [round(x, decimals) for x in self._q]
+        self._q, self._keys = _percentile_keys(decimals)
         h, w = self.image_dimensions
         self._npx = h * w
         lo, hi, gamma = quantile_table(self._npx, self._q)
