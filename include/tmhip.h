@@ -392,17 +392,6 @@ int tmh_inflate_device(const uint8_t* dev_src, int64_t src_bytes, const tmh_zchu
                        int64_t n_chunks, int64_t raw_max, uint8_t* dev_raw, int64_t raw_bytes,
                        void* dev_scratch, int64_t scratch_bytes, int32_t* dev_status,
                        void* stream);
-/* tmh_inflate_device + tmh_place_chunks_device in one call: chunks of at most
- * 64 KiB (h5py's 135 x 160 uint16 chunks are 43,200 bytes) have their matches
- * resolved in LDS and their rows written straight into dev_images (dev_raw
- * then holds only the literal bytes); larger chunks take the two calls'
- * path.  Same statuses; a chunk whose status is not TMH_Z_OK is not placed. */
-int tmh_inflate_place_device(const uint8_t* dev_src, int64_t src_bytes,
-                             const tmh_zchunk* dev_chunks, int64_t n_chunks, int64_t raw_max,
-                             uint8_t* dev_raw, int64_t raw_bytes, void* dev_scratch,
-                             int64_t scratch_bytes, int32_t* dev_status, int height, int width,
-                             int elem_bytes, int chunk_rows, int chunk_cols, void* dev_images,
-                             void* stream);
 int tmh_place_chunks_device(const uint8_t* dev_raw, const tmh_zchunk* dev_chunks, int64_t n_chunks,
                             int height, int width, int elem_bytes, int chunk_rows, int chunk_cols,
                             void* dev_images, void* stream);

@@ -194,16 +194,13 @@ def test_device_decode_channel_image_files(L, tmp_path, H, W, dtype, chunks, lev
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("chunks", [None, "rows"])
-def test_device_decode_fullsize_sites(L, tmp_path, chunks):
+def test_device_decode_fullsize_sites(L, tmp_path):
     """Eight 2160x2560 synthetic sites, written as the reference-layout files
-    (gzip level 4, h5py's 135x160 chunks: resolved and placed from LDS) and
-    with whole-row chunks (266 KB: the global-memory resolve and the placement
-    kernel), decoded on the GPU = the host read."""
+    (gzip level 4, whole-row chunks), decoded on the GPU = the host read."""
     import torch
 
     from tmlibrary_amd.models.device_decode import DeviceChunkDecoder
-    paths, want = _files(tmp_path, 8, 2160, 2560, np.uint16, chunks, 4, seed=12345)
+    paths, want = _files(tmp_path, 8, 2160, 2560, np.uint16, None, 4, seed=12345)
     out = torch.empty((8, 2160, 2560), dtype=torch.int16, device="cuda")
     dec = DeviceChunkDecoder()
     dec.decode(paths, out.data_ptr())

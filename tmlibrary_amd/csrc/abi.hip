@@ -1602,35 +1602,6 @@ int tmh_inflate_device(const uint8_t* dev_src, int64_t src_bytes, const tmh_zchu
   });
 }
 
-int tmh_inflate_place_device(const uint8_t* dev_src, int64_t src_bytes,
-                             const tmh_zchunk* dev_chunks, int64_t n_chunks, int64_t raw_max,
-                             uint8_t* dev_raw, int64_t raw_bytes, void* dev_scratch,
-                             int64_t scratch_bytes, int32_t* dev_status, int height, int width,
-                             int elem_bytes, int chunk_rows, int chunk_cols, void* dev_images,
-                             void* stream) {
-  return guard([&] {
-    TMH_CHECK(n_chunks >= 0 && src_bytes >= 0 && raw_bytes >= 0 && raw_max >= 0, TMH_EINVAL,
-              "bad sizes");
-    if (n_chunks == 0) return;
-    TMH_CHECK(dev_src && dev_chunks && dev_raw && dev_status && dev_scratch && dev_images,
-              TMH_EINVAL, "bad arguments");
-    TMH_CHECK(raw_max < (int64_t(1) << 31), TMH_EINVAL, "chunks must hold fewer than 2^31 bytes");
-    TMH_CHECK(scratch_bytes >= inflate_scratch_bytes(n_chunks, raw_max), TMH_EINVAL,
-              "scratch smaller than tmh_inflate_scratch_bytes");
-    TMH_CHECK((reinterpret_cast<uintptr_t>(dev_scratch) & 15) == 0, TMH_EINVAL,
-              "scratch must be 16-byte aligned");
-    TMH_CHECK(height > 0 && width > 0 && chunk_rows > 0 && chunk_cols > 0 &&
-                  (elem_bytes == 1 || elem_bytes == 2 || elem_bytes == 4 || elem_bytes == 8),
-              TMH_EINVAL, "bad image or chunk geometry");
-    TMH_CHECK((int64_t)chunk_rows * chunk_cols * elem_bytes >= raw_max, TMH_EINVAL,
-              "chunk geometry smaller than raw_max");
-    launch_inflate_place(dev_src, src_bytes, dev_chunks, n_chunks, raw_max, dev_raw, raw_bytes,
-                         static_cast<uint32_t*>(dev_scratch), dev_status, height, width,
-                         elem_bytes, chunk_rows, chunk_cols, static_cast<uint8_t*>(dev_images),
-                         (hipStream_t)stream);
-  });
-}
-
 int tmh_place_chunks_device(const uint8_t* dev_raw, const tmh_zchunk* dev_chunks, int64_t n_chunks,
                             int height, int width, int elem_bytes, int chunk_rows, int chunk_cols,
                             void* dev_images, void* stream) {

@@ -302,10 +302,6 @@ int64_t inflate_scratch_bytes(int64_t n_chunks, int64_t raw_max);
 void launch_inflate(const uint8_t* src, int64_t src_bytes, const tmh_zchunk* chunks,
                     int64_t n_chunks, int64_t raw_max, uint8_t* dst, int64_t dst_bytes,
                     uint32_t* scratch, int32_t* status, hipStream_t s);
-void launch_inflate_place(const uint8_t* src, int64_t src_bytes, const tmh_zchunk* chunks,
-                          int64_t n_chunks, int64_t raw_max, uint8_t* raw, int64_t raw_bytes,
-                          uint32_t* scratch, int32_t* status, int height, int width, int esize,
-                          int chunk_rows, int chunk_cols, uint8_t* images, hipStream_t s);
 void launch_place_chunks(const uint8_t* raw, const tmh_zchunk* chunks, int64_t n_chunks,
                          int height, int width, int esize, int chunk_rows, int chunk_cols,
                          uint8_t* images, hipStream_t s);

@@ -145,101 +145,6 @@ __global__ __launch_bounds__(kZW) void k_resolve_matches(const tmh_zchunk* __res
   if (lane == 0 && adler_from_sums(sa, sb, olen) != want) status[ci] = kZAdler;
 }
 
-// Phase 2 and the placement in one kernel for chunks that fit LDS (h5py's
-// 43,200-byte chunks do): one wave per chunk loads the chunk's literal bytes
-// into LDS, resolves its matches there in the same rounds as
-// k_resolve_matches (an LDS round trip per round instead of two memory ones),
-// checks the Adler-32 from LDS and writes the rows straight into the site
-// buffer -- the raw buffer is then written once and read once.
-__global__ __launch_bounds__(kZW) void k_resolve_place_lds(
-    const tmh_zchunk* __restrict__ chunks, const uint8_t* __restrict__ raw,
-    const uint32_t* __restrict__ ml_all, int64_t mw, int32_t* __restrict__ status, int height,
-    int width, int esize, int chunk_rows, int chunk_cols, uint8_t* __restrict__ images) {
-  extern __shared__ uint4 zbuf4[];
-  uint8_t* buf = reinterpret_cast<uint8_t*>(zbuf4);
-  const int64_t ci = blockIdx.x;
-  const int lane = threadIdx.x;
-  const tmh_zchunk c = chunks[ci];
-  const int olen = (int)c.raw_len;
-  const uint8_t* src = raw + c.raw_off;
-  const bool ok1 = status[ci] == 0;  // phase 1 failed: nothing to resolve (uniform)
-  if (!ok1) return;
-  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-    for (int i = lane; i < olen / 16; i += kZW) zbuf4[i] = reinterpret_cast<const uint4*>(src)[i];
-    for (int i = (olen & ~15) + lane; i < olen; i += kZW) buf[i] = src[i];
-  } else {
-    for (int i = lane; i < olen; i += kZW) buf[i] = src[i];
-  }
-  __syncthreads();
-  const uint32_t* ml = ml_all + ci * mw;
-  const int64_t nm = ml[0];
-  const uint32_t want = ml[1];
-  for (int64_t base = 0; base < nm; base += kZW) {
-    const int64_t i = base + lane;
-    const bool act = i < nm;
-    const uint2 oe = act ? reinterpret_cast<const uint2*>(ml + kMlHead)[i] : make_uint2(0u, 0u);
-    const uint32_t o = oe.x, e = oe.y;
-    const uint32_t len = e & 511u, d = e >> 9;
-    const uint32_t src_end = o - d + (len < d ? len : d);
-    bool todo = act;
-    while (__builtin_amdgcn_ballot_w64(todo)) {
-      const uint32_t fu = wave_excl_min(todo ? o : 0xFFFFFFFFu, lane);
-      const bool go = todo && src_end <= fu;
-      if (go) {
-        for (uint32_t k = 0; k < len; ++k) buf[o + k] = buf[o - d + k];
-      }
-      __syncthreads();  // this round's LDS stores before the next round's loads
-      todo = todo && !go;
-    }
-  }
-  if (want != 0xFFFFFFFFu) {  // a stored chunk (filter skipped) has no checksum
-    uint64_t sa = 0, sb = 0;
-    int k = 0;
-    for (int j = lane; j < olen; j += kZW) {
-      const uint32_t x = buf[j];
-      sa += x;
-      sb += (uint64_t)(olen - j) * x;
-      if (++k == 65536) {
-        sa %= 65521u;
-        sb %= 65521u;
-        k = 0;
-      }
-    }
-    sa %= 65521u;
-    sb %= 65521u;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      sa += (uint64_t)__shfl_xor((long long)sa, off, 64);
-      sb += (uint64_t)__shfl_xor((long long)sb, off, 64);
-    }
-    if (adler_from_sums(sa, sb, olen) != want) {
-      if (lane == 0) status[ci] = kZAdler;
-      return;  // uniform: every lane holds the same sums
-    }
-  }
-  const int rows = min(chunk_rows, height - c.row0);
-  const int cols = min(chunk_cols, width - c.col0);
-  if (rows <= 0 || cols <= 0) return;
-  const int64_t rb = (int64_t)cols * esize;
-  const int64_t sstride = (int64_t)chunk_cols * esize;
-  const int64_t dstride = (int64_t)width * esize;
-  uint8_t* d = images + (c.image * height + c.row0) * dstride + (int64_t)c.col0 * esize;
-  const bool v16 = (reinterpret_cast<uintptr_t>(d) & 15) == 0 && (rb & 15) == 0 &&
-                   (sstride & 15) == 0 && (dstride & 15) == 0;
-  if (v16) {
-    const int per_row = (int)(rb / 16);
-    for (int t = lane; t < rows * per_row; t += kZW) {
-      const int r = t / per_row, q = t - r * per_row;
-      reinterpret_cast<uint4*>(d + r * dstride)[q] = zbuf4[(r * sstride) / 16 + q];
-    }
-  } else {
-    for (int64_t t = lane; t < (int64_t)rows * rb; t += kZW) {
-      const int64_t r = t / rb, q = t - r * rb;
-      d[r * dstride + q] = buf[r * sstride + q];
-    }
-  }
-}
-
 // Chunk i's raw bytes (chunk_rows x chunk_cols elements, row-major) into
 // image c.image of [*][height][width] at (row0, col0), clipped to the
 // dataset's extent.  One workgroup per (chunk, 64 rows), 16-byte copies
@@ -321,41 +226,6 @@ void launch_inflate(const uint8_t* src, int64_t src_bytes, const tmh_zchunk* chu
     ProfScope prof("inflate_matches", s);
     hipLaunchKernelGGL(k_resolve_matches, dim3((unsigned)n_chunks), dim3(kZW), 0, s, chunks, dst,
                        scratch, mw, status);
-  }
-  TMH_HIP(hipGetLastError());
-}
-
-// chunks up to this size are resolved and placed from LDS (k_resolve_place_lds)
-constexpr int64_t kLdsChunkMax = 64 * 1024;
-
-void launch_inflate_place(const uint8_t* src, int64_t src_bytes, const tmh_zchunk* chunks,
-                          int64_t n_chunks, int64_t raw_max, uint8_t* raw, int64_t raw_bytes,
-                          uint32_t* scratch, int32_t* status, int height, int width, int esize,
-                          int chunk_rows, int chunk_cols, uint8_t* images, hipStream_t s) {
-  if (n_chunks <= 0) return;
-  const int64_t lds = ((int64_t)chunk_rows * chunk_cols * esize + 15) & ~int64_t(15);
-  if (raw_max > kLdsChunkMax || lds > kLdsChunkMax || raw_max > lds) {
-    launch_inflate(src, src_bytes, chunks, n_chunks, raw_max, raw, raw_bytes, scratch, status, s);
-    launch_place_chunks(raw, chunks, n_chunks, height, width, esize, chunk_rows, chunk_cols,
-                        images, s);
-    return;
-  }
-  const int64_t mw = match_words(raw_max);
-  {
-    ProfScope prof("inflate", s);
-    switch (inflate_lanes()) {
-      case 4: launch_tokens<4>(src, src_bytes, chunks, n_chunks, raw, raw_bytes, scratch, mw, status, s); break;
-      case 8: launch_tokens<8>(src, src_bytes, chunks, n_chunks, raw, raw_bytes, scratch, mw, status, s); break;
-      case 16: launch_tokens<16>(src, src_bytes, chunks, n_chunks, raw, raw_bytes, scratch, mw, status, s); break;
-      case 32: launch_tokens<32>(src, src_bytes, chunks, n_chunks, raw, raw_bytes, scratch, mw, status, s); break;
-      default: launch_tokens<64>(src, src_bytes, chunks, n_chunks, raw, raw_bytes, scratch, mw, status, s); break;
-    }
-  }
-  {
-    ProfScope prof("inflate_matches", s);
-    hipLaunchKernelGGL(k_resolve_place_lds, dim3((unsigned)n_chunks), dim3(kZW), (size_t)lds, s,
-                       chunks, raw, scratch, mw, status, height, width, esize, chunk_rows,
-                       chunk_cols, images);
   }
   TMH_HIP(hipGetLastError());
 }

@@ -96,8 +96,6 @@ SIGNATURES = {
     "tmh_inflate_scratch_bytes": (_I64, [_I64, _I64]),
     "tmh_inflate_device": (_I, [_P, _I64, _P, _I64, _I64, _P, _I64, _P, _I64, _P, _P]),
     "tmh_place_chunks_device": (_I, [_P, _P, _I64, _I, _I, _I, _I, _I, _P, _P]),
-    "tmh_inflate_place_device": (_I, [_P, _I64, _P, _I64, _I64, _P, _I64, _P, _I64, _P, _I, _I,
-                                      _I, _I, _I, _P, _P]),
     "tmh_malloc_device": (_I, [C.POINTER(_P), C.c_size_t]),
     "tmh_free_device": (_I, [_P]),
     "tmh_memcpy": (_I, [_P, _P, C.c_size_t, _I, _P]),

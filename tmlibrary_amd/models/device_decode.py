@@ -7,10 +7,10 @@ caps the corilla job at ~290 sites/s (profiles/r3/input_path_threads_r3l.jsonl).
 Here the host only copies the still-compressed chunks out of the files
 (libtmh5 ``tmh5_read_raw_chunks``: HDF5 metadata under its lock, the bytes by
 parallel ``pread``), the compressed bytes cross PCIe, and libtmhip inflates
-every chunk on the GPU and places the chunks' rows into a device ``[n, H, W]``
-site buffer that the statistics pass reads in place
-(``tmh_inflate_place_device``: one lane per zlib stream, byte-identical to
-zlib, Adler-32 checked; h5py-sized chunks finished and placed from LDS).
+every chunk on the GPU (``tmh_inflate_device``: one lane per zlib stream,
+byte-identical to zlib, Adler-32 checked) and places the chunks' rows into a
+device ``[n, H, W]`` site buffer (``tmh_place_chunks_device``) that the
+statistics pass reads in place.
 
 No CPU fallback inside: a file the GPU path cannot take (not chunked with the
 deflate filter only) raises ``RawChunksUnsupported`` and the caller decides
@@ -112,12 +112,14 @@ class DeviceChunkDecoder(object):
             copied.record(self.copy_stream)
         self.stream.wait_event(copied)
         sp = C.c_void_p(self.stream.cuda_stream)
-        hip.check(L.tmh_inflate_place_device(C.c_void_p(d_src.data_ptr()), blob.nbytes,
-                                             C.c_void_p(d_tab.data_ptr()), n, raw_max,
-                                             C.c_void_p(d_raw.data_ptr()), raw_bytes,
-                                             C.c_void_p(d_scr.data_ptr()), d_scr.numel(),
-                                             C.c_void_p(d_st.data_ptr()), H, W, es, cr, cc,
-                                             C.c_void_p(int(out_ptr)), sp))
+        hip.check(L.tmh_inflate_device(C.c_void_p(d_src.data_ptr()), blob.nbytes,
+                                       C.c_void_p(d_tab.data_ptr()), n, raw_max,
+                                       C.c_void_p(d_raw.data_ptr()), raw_bytes,
+                                       C.c_void_p(d_scr.data_ptr()), d_scr.numel(),
+                                       C.c_void_p(d_st.data_ptr()), sp))
+        hip.check(L.tmh_place_chunks_device(C.c_void_p(d_raw.data_ptr()),
+                                            C.c_void_p(d_tab.data_ptr()), n, H, W, es, cr, cc,
+                                            C.c_void_p(int(out_ptr)), sp))
         inflated = torch.cuda.Event()
         inflated.record(self.stream)
         slot["inflated"] = inflated
