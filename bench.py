@@ -374,7 +374,7 @@ def bench_input_path(H, W, dev, distinct=8, block=128, reps=2):
             torch.cuda.synchronize(dev)
             t_gpu = min(t_gpu, time.perf_counter() - t0)
         out2 = torch.empty_like(out)
-        n_pipe = 4
+        n_pipe = 8
         torch.cuda.synchronize(dev)
         dec.times = {k: 0.0 for k in dec.times}
         t0 = time.perf_counter()
