@@ -118,14 +118,11 @@ def parse():
                         "this many statistics handles / correctors / streams, so job k+1's "
                         "Welford pass runs while job k's histogram tail finishes (each job "
                         "still complete and checked; 1 = one job at a time)")
-    p.add_argument("--jobs-order", choices=["pipelined", "welford", "corrected"],
-                   default="welford",
-                   help="jobs in flight: 'pipelined' (3 lanes): the HBM passes alternate W(k+1), "
-                        "C(k) -- job k's corrected pass waits for job k+1's Welford pass, job k's "
-                        "small kernels run under job k-1's corrected pass and its histogram tail "
-                        "under job k+2's Welford pass; 'welford': job k+1's Welford pass starts "
-                        "after job k's (sharing HBM with job k's corrected pass); 'corrected': "
-                        "after job k's corrected pass (hides only the tail)")
+    p.add_argument("--jobs-order", choices=["welford", "corrected"], default="welford",
+                   help="jobs in flight: job k+1's Welford pass starts after job k's Welford pass "
+                        "(sharing HBM with job k's corrected pass, hiding job k's small kernels "
+                        "and tail) or after job k's corrected pass (hiding only the tail); a "
+                        "third, pipelined order measured no better (DESIGN.md 9.5)")
     p.add_argument("--channel-streams", choices=["per-channel", "one"], default="per-channel",
                    help="several channels: each on its own stream (its merges overlap the "
                         "others' kernels), or all on one stream")
@@ -1283,49 +1280,15 @@ def main():
     # overlaps is job k's Welford pass with job k-1's histogram tail
     shared_streams = {}
     J = jobs_in_flight = max(1, a.jobs_in_flight) if (CH == 1 and not dist_on and fused) else 1
-    if J > 1 and a.jobs_order == "pipelined":
-        J = jobs_in_flight = max(J, 3)  # job k+1's lane last ran job k-2: its tail is done
     chans = [Channel(c) for c in range(CH)]
     lanes = chans + [Channel(0, lane=j) for j in range(1, J)]
-    jobs = {"k": 0, "applied": None, "welford": None, "primed": False}
+    jobs = {"k": 0, "applied": None, "welford": None}
 
-    def drain():
-        """pipelined order: the job whose Welford pass the last step issued
-        gets its corrected pass (after the timed region: every lane's last
-        job complete for the oracle check)"""
-        if J > 1 and a.jobs_order == "pipelined" and jobs["primed"]:
-            cur = lanes[jobs["k"] % J]
-            if jobs["applied"] is not None:
-                cur.cstream.wait_event(jobs["applied"])
-            cur.apply()
-            jobs["primed"] = False
     log("%d channel(s) x %d sites resident; warm-up" % (CH, S))
 
     timing = {"on": False}
 
     def step():
-        if J > 1 and a.jobs_order == "pipelined":
-            # one step = job k+1's Welford pass, then job k's small kernels and
-            # corrected pass; HBM passes alternate W(k+1), C(k)
-            k = jobs["k"]
-            cur, nxt = lanes[k % J], lanes[(k + 1) % J]
-            if not jobs["primed"]:  # the first job's Welford pass
-                cur.stats()
-                jobs["primed"] = True
-            if jobs["applied"] is not None:  # W(k+1) after C(k-1)
-                nxt.stream.wait_event(jobs["applied"])
-            nxt.stats()
-            ev_w = torch.cuda.Event()
-            ev_w.record(nxt.stream)
-            cur.cstream.wait_event(ev_w)  # C(k) after W(k+1)
-            if jobs["applied"] is not None:
-                cur.cstream.wait_event(jobs["applied"])
-            cur.apply()
-            ev = torch.cuda.Event()
-            ev.record(cur.cstream)
-            jobs["applied"] = ev
-            jobs["k"] = k + 1
-            return
         if J > 1:
             ch = lanes[jobs["k"] % J]
             jobs["k"] += 1
@@ -1396,7 +1359,6 @@ def main():
             if k.value:
                 kern[name] = (ms.value / k.value, k.value)
         L.tmh_profile_enable(0)
-    drain()  # outside the timed region and the profile
     collectives = None
     if dist_on and prof:  # one more step with every collective timed on its own
         ct = CollectiveTimer(torch, dev)
