@@ -147,8 +147,8 @@ __global__ __launch_bounds__(kZW) void k_resolve_matches(const tmh_zchunk* __res
 
 // Chunk i's raw bytes (chunk_rows x chunk_cols elements, row-major) into
 // image c.image of [*][height][width] at (row0, col0), clipped to the
-// dataset's extent.  One workgroup per (chunk, 64 rows), 16-byte copies
-// where the row segments allow, else per element.
+// dataset's extent.  Workgroups of 256 threads, up to 64 per chunk, 16-byte
+// copies where the row segments allow, else per byte.
 __global__ __launch_bounds__(256) void k_place_chunks(const uint8_t* __restrict__ raw,
                                                       const tmh_zchunk* __restrict__ chunks,
                                                       int64_t n_chunks, int height, int width,
@@ -167,14 +167,20 @@ __global__ __launch_bounds__(256) void k_place_chunks(const uint8_t* __restrict_
   uint8_t* d = images + (c.image * height + c.row0) * dstride + (int64_t)c.col0 * esize;
   const bool v16 = ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0 &&
                    (rb & 15) == 0 && (sstride & 15) == 0 && (dstride & 15) == 0;
-  for (int r = blockIdx.y; r < rows; r += gridDim.y) {
-    const uint8_t* sr = s + r * sstride;
-    uint8_t* dr = d + r * dstride;
-    if (v16) {
-      for (int64_t i = threadIdx.x; i < rb / 16; i += 256)
-        reinterpret_cast<uint4*>(dr)[i] = reinterpret_cast<const uint4*>(sr)[i];
-    } else {
-      for (int64_t i = threadIdx.x; i < rb; i += 256) dr[i] = sr[i];
+  // the chunk's (row, 16-byte column) pairs spread over every thread of the
+  // grid's y blocks (rows of a 160-column chunk are 20 vectors: a block per
+  // row left 236 of 256 threads idle)
+  const int64_t step = (int64_t)gridDim.y * 256;
+  if (v16) {
+    const int64_t per_row = rb / 16;
+    for (int64_t t = (int64_t)blockIdx.y * 256 + threadIdx.x; t < rows * per_row; t += step) {
+      const int64_t r = t / per_row, q = t - r * per_row;
+      reinterpret_cast<uint4*>(d + r * dstride)[q] = reinterpret_cast<const uint4*>(s + r * sstride)[q];
+    }
+  } else {
+    for (int64_t t = (int64_t)blockIdx.y * 256 + threadIdx.x; t < rows * rb; t += step) {
+      const int64_t r = t / rb, q = t - r * rb;
+      d[r * dstride + q] = s[r * sstride + q];
     }
   }
 }
@@ -235,7 +241,9 @@ void launch_place_chunks(const uint8_t* raw, const tmh_zchunk* chunks, int64_t n
                          uint8_t* images, hipStream_t s) {
   if (n_chunks <= 0) return;
   ProfScope prof("place_chunks", s);
-  const unsigned ry = (unsigned)std::min<int64_t>(64, std::max(1, chunk_rows));
+  // ~one 16-byte vector per thread: y blocks of 256 threads per chunk
+  const int64_t vecs = ((int64_t)chunk_rows * chunk_cols * esize + 15) / 16;
+  const unsigned ry = (unsigned)std::min<int64_t>(64, std::max<int64_t>(1, cdiv(vecs, 256)));
   hipLaunchKernelGGL(k_place_chunks, dim3((unsigned)n_chunks, ry), dim3(256), 0, s, raw, chunks,
                      n_chunks, height, width, esize, chunk_rows, chunk_cols, images);
   TMH_HIP(hipGetLastError());
