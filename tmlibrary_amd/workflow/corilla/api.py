@@ -55,7 +55,7 @@ class IllumstatsCalculator(object):
     """Calculation of illumination statistics (corilla/api.py:31-146)."""
 
     def __init__(self, experiment_id, store=None, batch_size=32, prefetch=2, decode_threads=None,
-                 decode="auto", device_block=128):
+                 decode="auto", device_block=64):
         """prefetch: blocks of ``batch_size`` files decoded concurrently ahead of
         the GPU update; decode_threads: inflate workers over all of them (None:
         the cores granted, models/file.py:granted_cores).
@@ -63,7 +63,10 @@ class IllumstatsCalculator(object):
         decode: where the sites' gzip chunks are inflated -- "gpu": the host
         reads the compressed chunks, the GPU inflates them into a device
         buffer the statistics pass reads in place (models/device_decode.py;
-        ``device_block`` files per block, two blocks in flight); "host":
+        ``device_block`` files per block, two blocks in flight; 64 sites of
+        h5py's 256 chunks fill the GPU's ~16k resident inflate streams once:
+        run_job 2,472 sites/s on 1,536 sites against 2,380 with 128, and a
+        0.1 s instead of 0.3 s fixed cost, profiles/r4/run_job_device_block_r4db.txt); "host":
         libhdf5 + zlib on the cores; "auto": the GPU path when the files
         allow it (uint16, chunked with the deflate filter only), else host."""
         self.experiment_id = experiment_id

@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--width", type=int, default=2560)
     ap.add_argument("--no-gpu", action="store_true")
-    ap.add_argument("--device-block", type=int, default=128,
+    ap.add_argument("--device-block", type=int, default=64,
                     help="files per device block of run_job's GPU decode")
     ap.add_argument("--repeat", type=int, default=4,
                     help="run_job batch = the files listed this many times (a longer job from "
