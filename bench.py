@@ -322,7 +322,7 @@ def bench_host_path(H, W, n_sites=64, reps=3):
             "job_sites_per_s": round(n_sites / (t_stats + t_corr), 1)}
 
 
-def bench_input_path(H, W, dev, distinct=8, block=128, reps=2):
+def bench_input_path(H, W, dev, distinct=8, block=64, reps=2):
     """§8(f) rank 1 beside the headline: site images from gzip HDF5 files
     (the reference's ChannelImageFile layout: level 4, h5py's own 135 x 160
     chunks, models/file.py h5py_chunk_shape) into HBM -- decoded on the host
@@ -371,7 +371,7 @@ def bench_input_path(H, W, dev, distinct=8, block=128, reps=2):
             torch.cuda.synchronize(dev)
             t_gpu = min(t_gpu, time.perf_counter() - t0)
         out2 = torch.empty_like(out)
-        n_pipe = 8
+        n_pipe = 16
         torch.cuda.synchronize(dev)
         dec.times = {k: 0.0 for k in dec.times}
         t0 = time.perf_counter()
