@@ -123,12 +123,9 @@ def parse():
                         "(sharing HBM with job k's corrected pass, hiding job k's small kernels "
                         "and tail) or after job k's corrected pass (hiding only the tail); a "
                         "third, pipelined order measured no better (DESIGN.md 9.5)")
-    p.add_argument("--channel-streams", choices=["per-channel", "one", "staggered"],
-                   default="per-channel",
+    p.add_argument("--channel-streams", choices=["per-channel", "one"], default="per-channel",
                    help="several channels: each on its own stream (its merges overlap the "
-                        "others' kernels), all on one stream, or staggered (own streams, but "
-                        "channel c's Welford pass after channel c-1's and the corrected passes "
-                        "one at a time in channel order, so at most one of each runs)")
+                        "others' kernels), or all on one stream")
     p.add_argument("--no-same-workload", action="store_true",
                    help="N > 1: skip rank 0's single-GPU run of the same (unsharded) workload")
     p.add_argument("--pipeline", choices=["fused", "separate"], default="fused",
@@ -1200,10 +1197,9 @@ def main():
             # histogram tail runs on the statistics handle's stream after it
             # (tmhip.h stream contract) and the next job need not wait for it
             # (one stream for every lane's corrected pass: they run in job order)
-            shared_c = jobs_in_flight > 1 or staggered
-            if shared_c and "cstream" not in shared_streams:
+            if jobs_in_flight > 1 and "cstream" not in shared_streams:
                 shared_streams["cstream"] = torch.cuda.Stream(dev)
-            self.cstream = shared_streams["cstream"] if shared_c else self.stream
+            self.cstream = shared_streams["cstream"] if jobs_in_flight > 1 else self.stream
             self.csp = C.c_void_p(self.cstream.cuda_stream)
             blk_in, blk_out = chan_sites[c]
             self.blocks = (blk_in, blk_out)
@@ -1283,7 +1279,6 @@ def main():
     # (outputs written in job order, HBM passes one at a time), so what
     # overlaps is job k's Welford pass with job k-1's histogram tail
     shared_streams = {}
-    staggered = CH > 1 and a.channel_streams == "staggered" and fused
     J = jobs_in_flight = max(1, a.jobs_in_flight) if (CH == 1 and not dist_on and fused) else 1
     chans = [Channel(c) for c in range(CH)]
     lanes = chans + [Channel(0, lane=j) for j in range(1, J)]
@@ -1310,31 +1305,6 @@ def main():
             ev = torch.cuda.Event()
             ev.record(ch.cstream)
             jobs["applied"] = ev
-            return
-        if staggered:  # one Welford pass and one corrected pass at a time, in channel order
-            prev_w = prev_c = None
-            for ch in chans:
-                if prev_w is not None:
-                    ch.stream.wait_event(prev_w)
-                ch.stats()
-                prev_w = torch.cuda.Event()
-                prev_w.record(ch.stream)
-                if dist_on:
-                    with torch.cuda.stream(ch.stream):
-                        e0 = ch.event() if timing["on"] else None
-                        merge_welford(ch.ops, D, n_total=n_channel)
-                        ev_m = [e0, ch.event() if timing["on"] else None]
-                if prev_c is not None:
-                    ch.cstream.wait_event(prev_c)
-                ch.apply()
-                prev_c = torch.cuda.Event()
-                prev_c.record(ch.cstream)
-                if dist_on:
-                    with torch.cuda.stream(ch.stream):
-                        e2 = ch.event() if timing["on"] else None
-                        merge_counts(ch.ops, D)
-                        if timing["on"]:
-                            ch.merge_ev.append(ev_m + [e2, ch.event()])
             return
         for ch in chans:
             ch.stats()
@@ -1600,7 +1570,6 @@ def main():
                        "pipeline": a.pipeline,
                        "jobs_in_flight": J,
                        "jobs_order": a.jobs_order if J > 1 else None,
-                       "channel_streams": a.channel_streams if CH > 1 else None,
                        "hbm_layout": (("sites in one buffer, corrected output in blocks of %d "
                                        "sites" % B) if in_contig else
                                       ("blocks of %d sites, input and output blocks allocated "

@@ -11,11 +11,6 @@ chunks, the histogram all-reduce) -- run two ways on one GPU:
   (the launcher of VERDICT r3 item 1; gloo with host-staged collectives, so the
   chain's send/recv and the broadcast really cross ranks).
 
-Both with per-channel streams and with staggered channels (one Welford pass
-and one corrected pass at a time, in channel order; the corrected passes on
-one shared stream, so each channel's histogram tail runs on its handle's tail
-stream).
-
 Every channel's results are compared with its committed oracle fingerprint
 (tests/golden/make_bench_fingerprint.py --sites 48 --channel c): n, mean/std
 and the smoothed planes within 1e-6 at 16,384 sampled pixels, the pooled
@@ -78,22 +73,18 @@ def _assert_all_channels(d):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("order", ["per-channel", "staggered"])
-def test_four_channels_forced_distributed_rccl(order):
-    d = _bench(ARGS + ["--channel-streams", order],
-               {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0",
-                "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_port()),
-                "TMH_BENCH_FORCE_DIST": "1"})
+def test_four_channels_forced_distributed_rccl():
+    d = _bench(ARGS, {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0",
+                      "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_port()),
+                      "TMH_BENCH_FORCE_DIST": "1"})
     assert d["config"]["rccl_world_size"] == 1
     assert d["config"]["channels"] == 4
-    assert d["config"]["channel_streams"] == order
     _assert_all_channels(d)
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("order", ["per-channel", "staggered"])
-def test_four_channels_two_ranks_share_gpu(order):
-    d = _bench(["--gpus", "2", "--share-gpu"] + ARGS + ["--channel-streams", order], {})
+def test_four_channels_two_ranks_share_gpu():
+    d = _bench(["--gpus", "2", "--share-gpu"] + ARGS, {})
     assert d["ranks"] == 2 and d["config"]["collective_world_size"] == 2
     assert d["config"]["sites_per_gpu"] == 4 * 24  # rank 0's shard of every channel
     _assert_all_channels(d)
