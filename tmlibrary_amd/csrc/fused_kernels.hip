@@ -345,19 +345,25 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
         if ((w.x | w.y | w.z | w.w) & HIMASK) {  // rare: beyond this site's LDS slice
           uint32_t* h = hs + k * (int64_t)kBins;
           unsigned long long rounds = 0ull;  // 1,024-bin rounds this site touches
+          // the lane's rare halves as a bit mask (bit 2p + j: half j of word p),
+          // then one iteration per rare half: a wave runs max-popcount
+          // iterations (~1-2 on bright sites) instead of eight masked sections
+          uint32_t msk = 0u;
 #pragma unroll
           for (int p = 0; p < 4; ++p) {
-            const uint32_t lo = wd[p] & 0xFFFFu, hi = wd[p] >> 16;
-            if (lo >= (uint32_t)BINS) {
-              atomicAdd(&h[lo], 1u);
-              rounds |= 1ull << (lo >> 10);
-              if (PK) ++rare[k];
-            }
-            if (hi >= (uint32_t)BINS) {
-              atomicAdd(&h[hi], 1u);
-              rounds |= 1ull << (hi >> 10);
-              if (PK) ++rare[k];
-            }
+            const uint32_t t = wd[p] & HIMASK;
+            msk |= ((t & 0xFFFFu) ? 1u : 0u) << (2 * p);
+            msk |= ((t >> 16) ? 2u : 0u) << (2 * p);
+          }
+          if (PK) rare[k] += __builtin_popcount(msk);
+          while (msk) {
+            const uint32_t b = __builtin_ctz(msk);
+            msk &= msk - 1u;
+            const uint32_t p = b >> 1;
+            const uint32_t word = p == 0 ? wd[0] : p == 1 ? wd[1] : p == 2 ? wd[2] : wd[3];
+            const uint32_t v = (word >> ((b & 1u) << 4)) & 0xFFFFu;
+            atomicAdd(&h[v], 1u);
+            rounds |= 1ull << (v >> 10);
           }
           atomicOr(&rm[k], rounds);  // LDS: published once per unit
         }
