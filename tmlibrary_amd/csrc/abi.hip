@@ -265,6 +265,8 @@ struct tmh_stats {
   DBuf<unsigned long long> pooled, pooled_parts;  // parts: kPooledParts zero-maintained copies
   DBuf<uint32_t> hist_hi, site_hist, hist_full;
   DBuf<unsigned long long> hist_rmask;  // per site: touched high rounds of hist_full
+  DBuf<uint16_t> rare_v;                // fused pass, packed configuration: per-site rare lists
+  DBuf<unsigned int> rare_n;
   QPos qp{};
   DBuf<uint16_t> stage;  // two device slots of batch_cap sites
   HostPipe pipe;
@@ -1252,8 +1254,15 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
     TMH_CHECK(vec || !tab.in, TMH_EINVAL,
               "a blocked site layout needs the fused pass (zero_log10 in [-37, 0])");
     if (vec) {
+      // rare lists (RareList, common.h): the auto choice or configuration 5 may
+      // run the packed configuration
+      const bool rl_on = h->fused_cfg == kFusedAuto || h->fused_cfg == kFusedWide;
+      const unsigned int rl_cap =
+          (unsigned int)std::min<int64_t>(65536, std::max<int64_t>(1024, h->npx / 64));
       const bool grow = (size_t)n_sites * kBins > h->hist_full.n || (size_t)n_sites > h->zeros.n ||
                         (size_t)n_sites > h->hist_rmask.n ||
+                        (rl_on && ((size_t)n_sites * rl_cap > h->rare_v.n ||
+                                   (size_t)n_sites > h->rare_n.n)) ||
                         ((h->flags & 2u) && (size_t)n_sites * kBins > h->site_hist.n) ||
                         (!(h->flags & TMH_STATS_DEFERRED_PCT) && os_words(h, n_sites) > h->vlh.n);
       if (grow) {
@@ -1264,6 +1273,13 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
       if ((size_t)n_sites * kBins > h->hist_full.n)
         h->hist_full.alloc((size_t)n_sites * kBins, true);
       if ((size_t)n_sites > h->hist_rmask.n) h->hist_rmask.alloc((size_t)n_sites, true);
+      RareList rl{};
+      if (rl_on) {
+        h->rare_v.ensure((size_t)n_sites * rl_cap);
+        h->rare_n.ensure((size_t)n_sites);
+        TMH_HIP(hipMemsetAsync(h->rare_n.p, 0, (size_t)n_sites * sizeof(unsigned int), s));
+        rl = RareList{h->rare_v.p, h->rare_n.p, rl_cap};
+      }
       h->zeros.ensure((size_t)n_sites);
       if (h->flags & 2u) h->site_hist.ensure((size_t)n_sites * kBins);
       uint32_t* vlh;
@@ -1299,7 +1315,8 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
       launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p, fl,
                           c->log_transform, clip_lo, clip_hi, h->hist_full.p, h->hist_rmask.p,
                           c->queues.p, c->n_wg, h->fused_cfg, h->wide.p, wide_thresh, xwide_thresh,
-                          s, tab);
+                          s, tab, rl);
+      launch_rare_count(rl, h->hist_full.p, n_sites, s);
       launch_fix_correct(dev_in, dev_out, 2, c->npx, n_sites, fl, c->coef64.p, c->rc.p,
                          c->log_transform, clip_lo, clip_hi, s, tab);
       if (autocfg)  // exits at once unless the launch is very wide

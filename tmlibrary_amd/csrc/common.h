@@ -163,6 +163,19 @@ struct SiteTab {
   int shift = 0;
 };
 
+// Values beyond the packed fused configuration's LDS slices (>= 16,384 on
+// bright sites): appended per site as u16 (staged in LDS, one reservation per
+// site and unit) instead of one global atomic each (~61 B of HBM traffic per
+// atomic, profiles/r4/abl_rare_atomics_r4ab.jsonl); k_rare_count folds each
+// site's list into its histogram.  cnt[s] counts every append; entries past
+// cap took the global atomic instead.  v == null: atomics only.
+struct RareList {
+  uint16_t* v = nullptr;      // site s: v[s * cap, s * cap + min(cnt[s], cap))
+  unsigned int* cnt = nullptr;
+  unsigned int cap = 0;
+};
+constexpr int kRareLo = 16384;  // the packed configuration's slice size
+
 // site s of a launch in its layout (contiguous at base, or blocked)
 __device__ __forceinline__ int64_t site_block(const SiteTab& t, int64_t s) { return s >> t.shift; }
 __device__ __forceinline__ int64_t site_in_block(const SiteTab& t, int64_t s) {
@@ -285,7 +298,10 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
                          unsigned long long* rmask, int* queues, int n_wg, int cfg,
                          const unsigned long long* wide, unsigned long long wide_thresh,
                          unsigned long long xwide_thresh, hipStream_t s,
-                         const SiteTab& tab = SiteTab{});
+                         const SiteTab& tab = SiteTab{}, const RareList& rl = RareList{});
+// after launch_correct_hist with a RareList: each site's list into its
+// histogram (hist + s * kBins), on the same stream
+void launch_rare_count(const RareList& rl, uint32_t* hist, int64_t n_sites, hipStream_t s);
 // illuminati chain (chain_kernels.hip)
 void launch_align(const void* in, void* out, int elem_bytes, int64_t n_sites, int H, int W, int oh,
                   int ow, const tmh_window* d_win, hipStream_t s);

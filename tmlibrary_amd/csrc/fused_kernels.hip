@@ -192,7 +192,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     int clip_lo, int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
     int n_bands, int* __restrict__ queues, const unsigned long long* __restrict__ wide,
     unsigned long long wide_lo, unsigned long long wide_hi, unsigned long long x_lo,
-    unsigned long long x_hi, const SiteTab tab) {
+    unsigned long long x_hi, const SiteTab tab, const RareList rl) {
   // launch-time selection (launch_correct_hist): this configuration runs only
   // when the Welford pass's counts of pixel groups with a value >= 4,096 and
   // >= 16,384 are in [wide_lo, wide_hi) and [x_lo, x_hi)
@@ -209,6 +209,12 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   static_assert(!PK || (SPU % 2 == 0 && BINS <= 16384), "packed: site pairs, u16 headroom");
   __shared__ __attribute__((aligned(16))) uint32_t bins[NSL * SLICE];
   __shared__ uint32_t pk_red[PK ? NT / 64 : 1][PK ? SPU : 1];  // packed: per-wave site sums
+  static_assert(!PK || BINS == kRareLo, "rare lists start at the packed slice size");
+  // packed with a rare list: the unit's values beyond the slices, per site
+  constexpr int kRareSh = PK ? 1024 : 1;
+  __shared__ uint16_t rstage[PK ? SPU : 1][kRareSh];
+  __shared__ unsigned int rcnt[PK ? SPU : 1], rbase[PK ? SPU : 1];
+  const bool rlist = PK && rl.v != nullptr;
   uint32_t rare[SPU];  // packed: this thread's pixels of the unit that took the global path
 #pragma unroll
   for (int k = 0; k < SPU; ++k) rare[k] = 0u;
@@ -228,6 +234,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   const int tid = threadIdx.x;
   for (int i = tid; i < NSL * SLICE; i += NT) bins[i] = 0u;
   if (tid < 2 * SPU) rm_sh[tid / SPU][tid % SPU] = 0ull;
+  if (PK && tid < SPU) rcnt[tid] = 0u;
   if (tid < 2) fix_cnt[tid] = 0u;
   __syncthreads();
 
@@ -362,7 +369,15 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
             const uint32_t p = b >> 1;
             const uint32_t word = p == 0 ? wd[0] : p == 1 ? wd[1] : p == 2 ? wd[2] : wd[3];
             const uint32_t v = (word >> ((b & 1u) << 4)) & 0xFFFFu;
-            atomicAdd(&h[v], 1u);
+            bool staged = false;
+            if (rlist) {
+              const unsigned int i = atomicAdd(&rcnt[k], 1u);  // LDS
+              if (i < (unsigned int)kRareSh) {
+                rstage[k][i] = (uint16_t)v;
+                staged = true;
+              }
+            }
+            if (!staged) atomicAdd(&h[v], 1u);
             rounds |= 1ull << (v >> 10);
           }
           atomicOr(&rm[k], rounds);  // LDS: published once per unit
@@ -432,6 +447,29 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
           sum[2 * j] += w & 0xFFFFu;
           sum[2 * j + 1] += w >> 16;
         }
+      }
+      if (rlist) {  // the unit's staged rare values to their sites' lists
+        if (tid < SPU) {
+          const unsigned int n = rcnt[tid] < (unsigned int)kRareSh ? rcnt[tid] : kRareSh;
+          rbase[tid] = (tid < un.ns && n) ? atomicAdd(&rl.cnt[un.s0 + tid], n) : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < SPU; ++k) {
+          const unsigned int n = rcnt[k] < (unsigned int)kRareSh ? rcnt[k] : kRareSh;
+          if (k >= un.ns) break;
+          uint16_t* dst = rl.v + (un.s0 + k) * (int64_t)rl.cap;
+          for (unsigned int i = tid; i < n; i += NT) {
+            const unsigned int j = rbase[k] + i;
+            const uint16_t v = rstage[k][i];
+            if (j < rl.cap)
+              dst[j] = v;
+            else
+              atomicAdd(&hs[k * (int64_t)kBins + v], 1u);  // past the list's capacity
+          }
+        }
+        __syncthreads();
+        if (tid < SPU) rcnt[tid] = 0u;
       }
       const int wv = tid >> 6;
 #pragma unroll
@@ -578,7 +616,8 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
                                     unsigned long long* rmask, int* queues, int n_wg, int cfg,
                                     const unsigned long long* wide, unsigned long long wide_lo,
                                     unsigned long long wide_hi, unsigned long long x_lo,
-                                    unsigned long long x_hi, hipStream_t s, const SiteTab& tab) {
+                                    unsigned long long x_hi, hipStream_t s, const SiteTab& tab,
+                                    const RareList& rl) {
 #define TMH_LAUNCH_CH(L_, K_, A_)                                                                \
   {                                                                                              \
     constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
@@ -588,13 +627,13 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
                          grid,                                                                   \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
                          clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
-                         wide_hi, x_lo, x_hi, tab);                                              \
+                         wide_hi, x_lo, x_hi, tab, c.packed ? rl : RareList{});                  \
     else                                                                                         \
       hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, A_, c.threads, c.lds_bins, c.packed>), \
                          grid,                                                                   \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
                          clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
-                         wide_hi, x_lo, x_hi, tab);                                              \
+                         wide_hi, x_lo, x_hi, tab, c.packed ? rl : RareList{});                  \
   }
 #define TMH_LAUNCH_CFG(L_)                                     \
   switch (cfg) {                                               \
@@ -627,7 +666,8 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
                          unsigned long long* rmask, int* queues, int n_wg, int cfg,
                          const unsigned long long* wide, unsigned long long wide_thresh,
-                         unsigned long long xwide_thresh, hipStream_t s, const SiteTab& tab) {
+                         unsigned long long xwide_thresh, hipStream_t s, const SiteTab& tab,
+                         const RareList& rl) {
   if (n_sites <= 0) return;
   ProfScope prof("correct_hist", s);
   // queues[0..8): per-XCD unit counters; queues[8..10): the union of the
@@ -639,16 +679,53 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
   if (cfg >= 0 || !wide) {
     launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo,
                             clip_hi, hist, rmask, queues, n_wg, cfg >= 0 ? cfg : kFusedNarrow,
-                            nullptr, 0, 0, 0, 0, s, tab);
+                            nullptr, 0, 0, 0, 0, s, tab, rl);
     return;
   }
   const unsigned long long X = xwide_thresh;
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedNarrow, wide, 0, wide_thresh, 0, X, s, tab);
+                          hist, rmask, queues, n_wg, kFusedNarrow, wide, 0, wide_thresh, 0, X, s, tab, rl);
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedWide, wide, wide_thresh, ~0ull, 0, X, s, tab);
+                          hist, rmask, queues, n_wg, kFusedWide, wide, wide_thresh, ~0ull, 0, X, s, tab, rl);
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedNoHist, wide, 0, ~0ull, X, ~0ull, s, tab);
+                          hist, rmask, queues, n_wg, kFusedNoHist, wide, 0, ~0ull, X, ~0ull, s, tab, rl);
+}
+
+// Each site's rare list into its histogram: one workgroup per site, the
+// values [kRareLo, 65536) counted in LDS in two halves of 24,576 bins, then
+// added to the site's bins (the fused pass has finished: plain adds).  The
+// fused pass already marked the rounds these values touch.
+constexpr int kRareHalf = (65536 - kRareLo) / 2;
+__global__ __launch_bounds__(1024) void k_rare_count(const RareList rl, uint32_t* __restrict__ hist,
+                                                     int64_t n_sites) {
+  __shared__ uint32_t c[kRareHalf];
+  for (int64_t site = blockIdx.x; site < n_sites; site += gridDim.x) {  // uniform per workgroup
+  const unsigned int cnt = rl.cnt[site];
+  const unsigned int n = cnt < rl.cap ? cnt : rl.cap;
+  if (n == 0u) continue;
+  const uint16_t* v = rl.v + site * (int64_t)rl.cap;
+  uint32_t* h = hist + site * (int64_t)kBins;
+  for (int half = 0; half < 2; ++half) {
+    const uint32_t lo = (uint32_t)kRareLo + (uint32_t)half * kRareHalf;
+    for (int i = threadIdx.x; i < kRareHalf; i += 1024) c[i] = 0u;
+    __syncthreads();
+    for (unsigned int i = threadIdx.x; i < n; i += 1024) {
+      const uint32_t u = (uint32_t)v[i] - lo;
+      if (u < (uint32_t)kRareHalf) atomicAdd(&c[u], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kRareHalf; i += 1024)
+      if (c[i]) h[lo + i] += c[i];
+    __syncthreads();
+  }
+  }
+}
+
+void launch_rare_count(const RareList& rl, uint32_t* hist, int64_t n_sites, hipStream_t s) {
+  if (n_sites <= 0 || !rl.v) return;
+  const unsigned grid = (unsigned)(n_sites < 256 ? n_sites : 256);  // one workgroup per CU (96 KB LDS)
+  hipLaunchKernelGGL(k_rare_count, dim3(grid), dim3(1024), 0, s, rl, hist, n_sites);
+  TMH_HIP(hipGetLastError());
 }
 
 }  // namespace tmh
