@@ -215,7 +215,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   __shared__ uint16_t rstage[PK ? SPU : 1][kRareSh];
   __shared__ unsigned int rcnt[PK ? SPU : 1], rbase[PK ? SPU : 1];
   const bool rlist = PK && rl.v != nullptr;
-  uint32_t rare[SPU];  // packed: this thread's pixels of the unit that took the global path
+  uint32_t rare[SPU];  // packed: this thread's pixels of the unit beyond the slices (list or atomic)
 #pragma unroll
   for (int k = 0; k < SPU; ++k) rare[k] = 0u;
   // per site of the unit: the 1,024-bin rounds holding counts (the rare
