@@ -97,11 +97,11 @@ def parse():
                    help="TMH_OPT_FUSED_CUS: CUs' worth of workgroups of the fused pass's "
                         "persistent grid (default: the library's, all CUs)")
     p.add_argument("--welford-parts", type=int, default=None,
-                   help="TMH_OPT_WELFORD_PARTS (1..4 forces that split and skips the device-side "
-                        "choice between the standard and bright passes; default: automatic)")
+                   help="TMH_OPT_WELFORD_PARTS (1..4 forces that split and the standard pass; "
+                        "default: automatic, from the job's site probe)")
     p.add_argument("--fused-config", type=int, default=None,
-                   help="fused pass (sites per unit, threads, LDS bins) configuration 0..3 "
-                        "(TMH_OPT_FUSED_CONFIG; default: the library's)")
+                   help="fused pass (sites per unit, threads, LDS bins) configuration 0..5 "
+                        "(TMH_OPT_FUSED_CONFIG; default: automatic, from the job's site probe)")
     p.add_argument("--block-sites", type=int, default=64,
                    help="sites per HBM allocation of the corrected output (a power of two >= 4; "
                         "blocked site layout); 0: one contiguous buffer")
@@ -145,9 +145,15 @@ def parse():
     p.add_argument("--resident-gb", type=float, default=160.0,
                    help="--stream-host: HBM for the two in-flight channels' resident sites; a "
                         "channel share beyond half of it is streamed twice (stats, then correct)")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
-                   help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
-    return p.parse_args()
+    p.add_argument("--traffic-json", default=None,
+                   help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py; "
+                        "default profiles/pmc_traffic.json, profiles/pmc_traffic_bright.json for "
+                        "--distribution bright)")
+    a = p.parse_args()
+    if a.traffic_json is None:
+        a.traffic_json = os.path.join(REPO, "profiles", "pmc_traffic%s.json" % (
+            "" if a.distribution == "synthetic" else "_" + a.distribution))
+    return a
 
 
 # ---------------------------------------------------------------------------
@@ -1103,6 +1109,8 @@ def main():
     S = s_end - s_begin  # this rank's sites per channel
     n_channel = S_total if sharded else world * S_total  # sites per channel job
     L = hip.lib()
+    with open(hip.LIB_PATH, "rb") as fh:  # which build ran (profiles/ summaries name it too)
+        lib_sha = hashlib.sha256(fh.read()).hexdigest()
     hip.check(L.tmh_set_device(local_rank))
     same = None
     if sharded and world > 1 and not a.no_same_workload and not staged:
@@ -1433,6 +1441,13 @@ def main():
         if len(per_channel) != CH:
             check["channels_unchecked"] = [c for c in range(CH) if c not in per_channel]
     ch0 = chans[0]
+    choice = None
+    if hasattr(L, "tmh_stats_job_choice"):  # (absent from A/B builds of earlier trees)
+        pc, wb, fc = (C.c_uint32 * 3)(), C.c_int(), C.c_int()
+        hip.check(L.tmh_stats_job_choice(ch0.h, pc, C.byref(wb), C.byref(fc)))
+        choice = {"probe_groups": list(pc), "welford_bright": wb.value,
+                  "fused_config": "no-histogram + per-site u16 pass" if fc.value == 100
+                  else fc.value}
 
     log("%.1f ms/step; check_vs_oracle %s" % (1e3 * elapsed / a.steps, check_ok))
     extras = {}
@@ -1500,19 +1515,29 @@ def main():
         if dominant:
             avg_ms = kern[dominant][0]
             ach = alg[dominant] / (avg_ms * 1e-3) / 1e9
-            traffic = None
+            # PMC traffic (tools/pmc_traffic.py) of THIS library build only:
+            # the summary names the sha256 of the library it was measured on
+            traffic, traffic_src = None, None
             try:
                 with open(a.traffic_json) as f:
                     tj = json.load(f)
                 cfg = tj.get("config", {})
                 if cfg.get("sites") == S and cfg.get("height") == H and cfg.get("width") == W \
                         and cfg.get("distribution", "synthetic") == a.distribution:
-                    traffic = tj.get("kernels", {}).get(dominant, {}).get("hbm_bytes_per_launch")
+                    if tj.get("library_sha256") == lib_sha:
+                        traffic = tj.get("kernels", {}).get(dominant, {}).get("hbm_bytes_per_launch")
+                        traffic_src = os.path.relpath(a.traffic_json, REPO)
+                    else:
+                        traffic_src = "%s was measured on another build (sha256 %s)" % (
+                            os.path.relpath(a.traffic_json, REPO), str(tj.get("library_sha256"))[:16])
             except (OSError, ValueError):
                 pass
             roofline = {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                        "traffic": traffic, "alg_bytes_per_launch": alg[dominant]}
+                        "traffic": traffic, "traffic_source": traffic_src,
+                        "alg_bytes_per_launch": alg[dominant],
+                        "timed": "HIP events around the launch of the one configuration the job "
+                                 "runs, on its stream (tmh_profile_*)"}
             if J > 1:
                 roofline["note"] = ("%d jobs in flight: this pass shares HBM with the next job's "
                                     "Welford pass, so its launches last longer than alone"
@@ -1541,6 +1566,7 @@ def main():
                         "one job per channel on its own stream" % (CH, S, H, W))
         resd = {
             "metric": METRIC,
+            "library_sha256": lib_sha,
             "value": round(value, 1),
             "unit": "sites/s",
             "n_gpus": 1 if staged else world,
@@ -1569,6 +1595,7 @@ def main():
                                              "sites' blocks" if share_out else "private"),
                        "pipeline": a.pipeline,
                        "jobs_in_flight": J,
+                       "job_choice": choice,
                        "jobs_order": a.jobs_order if J > 1 else None,
                        "hbm_layout": (("sites in one buffer, corrected output in blocks of %d "
                                        "sites" % B) if in_contig else

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define TMH_ABI_VERSION 3
+#define TMH_ABI_VERSION 4
 
 #define TMH_OK 0
 #define TMH_EINVAL (-22)  /* bad argument: maps to ValueError / TypeError */
@@ -80,25 +80,30 @@ int tmh_stats_set_stream(tmh_stats* h, void* stream);
  * handle's zero-maintained histogram slabs if a fused pass was interrupted. */
 int tmh_stats_reset(tmh_stats* h);
 
-/* Options of a handle (results never depend on them):
+/* Options of a handle (results never depend on them).  The automatic
+ * choices below come from the job's SITE PROBE: at the first Welford launch
+ * after tmh_stats_reset, one small kernel samples 16,384 8-pixel groups
+ * spread over the launch's first <= 64 sites, and the host waits for its
+ * three counts (groups sampled, holding a value >= 4,096, >= 16,384) --
+ * so that launch returns only once the probe has run on its stream.  Only
+ * the chosen kernels are queued.
  *   TMH_OPT_FUSED_CONFIG   0..5: (sites per unit, threads, LDS bins) of the
  *                          fused correct+histogram pass = (2, 1024, 32768),
  *                          (4, 1024, 32768), (2, 512, 16384), (4, 512, 16384),
  *                          (1, 1024, 32768), (4, 1024, 65536 u16 counters
- *                          packed two sites to a word).  -1 (default): chosen
- *                          per launch on the device from the Welford pass's
- *                          counts over the pending sites -- 3; or 5 when >= 2%
- *                          of the 8-pixel groups hold a value >= 4,096; or, when
- *                          >= 33% hold a value >= 16,384 ("very wide" sites,
- *                          e.g. uniform 16-bit data), the pass runs without
- *                          its histogram and a per-site u16-pair LDS
- *                          histogram pass (one more read) builds them.
- *   TMH_OPT_WELFORD_PARTS  0 (default): automatic -- a launch of >= 96 sites
- *                          probes its first site on the device and splits
- *                          into 3 site parts (merged in order) when >= 10% of
- *                          the probed 8-pixel groups hold a value >= 4,096
- *                          (bright sites: the log10 pass is VALU-bound),
- *                          else runs as one part; 1..4: that many parts where
+ *                          packed two sites to a word).  -1 (default): from
+ *                          the probe -- 3; or 5 when >= 2% of the probed
+ *                          groups hold a value >= 4,096; or, when >= 33% hold
+ *                          a value >= 16,384 ("very wide" sites, e.g. uniform
+ *                          16-bit data), the pass runs without its histogram
+ *                          and a per-site u16-pair LDS histogram pass (one
+ *                          more read) builds them.
+ *   TMH_OPT_WELFORD_PARTS  0 (default): automatic -- with the log transform,
+ *                          a launch of >= 96 sites whose job probe found >=
+ *                          10% of the groups holding a value >= 4,096 (bright
+ *                          sites: the log10 pass is VALU-bound) runs the
+ *                          16,384-entry LUT pass in 3 site parts (merged in
+ *                          order), else one part; 1..4: that many parts where
  *                          the launch has >= 32 sites a part
  *   TMH_OPT_COPY_THREADS   1..64 (default 8): host threads of the pageable <->
  *                          pinned copies of the host-buffer entry points
@@ -123,11 +128,18 @@ int tmh_stats_set_option(tmh_stats* h, int option, int value);
  * chunk k's H2D overlaps chunk k-1's kernels; returns when all are done. */
 int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites,
                      int log_transform, int64_t* zero_counts_out);
+/* Stream contract of the device update entry points: on another stream than
+ * the handle's, the work runs after everything already queued on the
+ * handle's stream, and the handle's stream waits for it before any later work
+ * on the handle (finalize, merge, ...), so results read on the handle's
+ * stream are complete. */
 int tmh_stats_update_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
                             int log_transform, void* stream);
-/* Per-site zero-pixel counts of the last tmh_stats_update_device call (its
- * first n sites; n <= 4,096), copied to host_out on `stream` after the
- * handle's queued work (asynchronous for pinned host_out). */
+/* Per-site zero-pixel counts of the LAST CHUNK of the last update call: the
+ * call's sites in chunks of 4,096, so for a call of <= 4,096 sites these are
+ * its sites' counts (n <= that chunk's size, else TMH_EINVAL).  Copied to
+ * host_out on `stream` after the handle's queued work (asynchronous for
+ * pinned host_out). */
 int tmh_stats_zero_counts(tmh_stats* h, int64_t* host_out, int64_t n, void* stream);
 
 /* Split job pipeline (one read of the sites per pass):
@@ -172,6 +184,14 @@ int tmh_stats_variance(tmh_stats* h, double* host_var);
  * pass consumed them (synchronous; diagnostics: the automatic fused
  * configuration compares it with 2% of the groups).  sites_out may be NULL. */
 int tmh_stats_wide_groups(tmh_stats* h, uint64_t* groups_out, int64_t* sites_out);
+/* The current job's site probe and the automatic choices it made (see the
+ * options above): probe_counts[3] = groups sampled, groups with a value >=
+ * 4,096, >= 16,384 (zeros before the probe ran); welford_bright = 1 / 0, -1
+ * if the job has not been probed; fused_cfg = the configuration the fused
+ * pass runs (0..5, or TMH_FUSED_NO_HIST).  Any output may be NULL. */
+#define TMH_FUSED_NO_HIST 100
+int tmh_stats_job_choice(tmh_stats* h, uint32_t* probe_counts, int* welford_bright,
+                         int* fused_cfg);
 /* Per-site histogram of the most recent update batch (debug/parity). */
 int tmh_stats_site_histogram(tmh_stats* h, int64_t site_in_last_batch, uint32_t* host_hist);
 /* Order statistics at every quantile's previous/next sorted position for one

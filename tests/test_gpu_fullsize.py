@@ -207,6 +207,9 @@ def test_bright_fullsize(L):
         return _results(L, h, H, W, N)
 
     r = job()  # automatic: wide
+    pc, wb, fc = (C.c_uint32 * 3)(), C.c_int(), C.c_int()
+    hip.check(L.tmh_stats_job_choice(h, pc, C.byref(wb), C.byref(fc)))
+    assert wb.value == 1 and fc.value == 5, (list(pc), wb.value, fc.value)  # bright: both choices
     out_auto = d_out.get(np.uint16, (N, npx))
     hist0 = np.empty(65536, np.uint32)
     hip.check(L.tmh_stats_site_histogram(h, 0, hip.ptr(hist0)))
@@ -307,6 +310,11 @@ def test_fused_multi_job_configs(L, cfg):
         assert wg.value == _wide_groups(sites), (cfg, k)
         if cfg == -1:  # the automatic choice's threshold: 2 % of the groups
             assert (wg.value >= 0.02 * groups) == bright, (k, wg.value / groups)
+        # the configuration the job runs, chosen on the host from its site probe
+        pc, wb, fc = (C.c_uint32 * 3)(), C.c_int(), C.c_int()
+        hip.check(L.tmh_stats_job_choice(h, pc, C.byref(wb), C.byref(fc)))
+        assert pc[0] == 16384 and wb.value == int(bright), (cfg, k, list(pc), wb.value)
+        assert fc.value == (cfg if cfg >= 0 else (5 if bright else 3)), (cfg, k, fc.value)
         hip.check(L.tmh_correct_u16_hist_device(c, h, d_in.p, d_out.p, n, -1, -1, None))
         r = _results(L, h, H, W, n)  # on stream 1: waits for stream 2's fused pass
         hip.check(L.tmh_stats_wide_groups(h, C.byref(wg), C.byref(ws)))

@@ -563,6 +563,53 @@ def test_run_job_end_to_end(L, tmp_path, decode, block, caplog):
     assert np.allclose(cont.mean.array, orc.smooth_reflect(g["mean"]), rtol=1e-9, atol=1e-12)
 
 
+@pytest.mark.parametrize("plain", [(), (0,), (2,), (3,)])
+def test_run_job_auto_mixed_layouts(L, tmp_path, plain):
+    """decode="auto" over a job whose files mix the reference's gzip chunks
+    with contiguous (uncompressed) ones: the GPU path runs up to the first
+    block it cannot read and the host decodes from that file on -- every site
+    counted once, in order (a fallback that restarted on the host
+    counted the GPU blocks twice).  A file of another shape raises the
+    reference's broadcast ValueError, and the calculator's next job is clean."""
+    from tmlibrary_amd.models import file as h5
+    try:
+        h5.h5lib()
+    except RuntimeError as e:
+        pytest.skip(str(e))
+    from tmlibrary_amd.workflow.corilla.api import IllumstatsCalculator
+    g = load_golden("stats_medium")
+    sites = list(g["sites"])
+    store = h5.ExperimentStore(str(tmp_path), {100 + i: (5, i, 0, 0, 0) for i in range(len(sites))})
+    (tmp_path / "channel_image_files").mkdir()
+    for i, s in enumerate(sites):
+        h5.write_channel_image(store.channel_image_file(100 + i).location, s,
+                               gzip_level=-1 if i in plain else 4)
+    batch = {"id": 1, "channel_image_files_ids": [[100 + i] for i in range(len(sites))],
+             "channel_id": 5}
+    # blocks of one file: the GPU path takes the files before the first plain one
+    calc = IllumstatsCalculator(1, store=store, batch_size=2, decode="auto", device_block=1)
+    calc.run_job(batch)
+    mean, std, keys, vals = h5.read_illumstats(store.illumstats_file(5).location)
+    assert_close_rel(mean, g["mean"])
+    assert_close_rel(std, g["std"])
+    got = dict(zip(keys.tolist(), vals.tolist()))
+    assert [got[k] for k in sorted(got)] == g["pct_values"].tolist()
+    if plain:
+        with pytest.raises(h5.RawChunksUnsupported):  # strict GPU decode refuses them
+            IllumstatsCalculator(1, store=store, batch_size=2, decode="gpu",
+                                 device_block=1).run_job(batch)
+        return
+    # a site of another shape in a later block: the reference's broadcast error
+    odd = 100 + len(sites) - 1
+    h5.write_channel_image(store.channel_image_file(odd).location, sites[-1][:-1])
+    with pytest.raises(ValueError):
+        calc.run_job(batch)
+    h5.write_channel_image(store.channel_image_file(odd).location, sites[-1])
+    calc.run_job(batch)  # the calculator's decoder carries nothing over
+    mean2, _, _, vals2 = h5.read_illumstats(store.illumstats_file(5).location)
+    assert np.array_equal(mean2, mean) and np.array_equal(vals2, vals)
+
+
 def _fused_job(L, sites, clip=(-1, -1), q=None):
     """Split pipeline through the C-ABI: Welford-only update -> finalize ->
     smooth -> corrector -> fused correct+histogram.  Returns host results."""

@@ -256,7 +256,15 @@ struct tmh_stats {
   int64_t last_batch = 0;
   int64_t pending = 0;        // Welford-updated sites whose histograms are still to come
   DBuf<unsigned long long> wide;  // pixel groups with a value >= 4,096 / >= 16,384 in the pending sites
-  DBuf<unsigned int> probe;       // bright-site probe of the Welford launch (k_wf_probe)
+  // The job's site probe (k_site_probe, first Welford launch after a reset):
+  // 8-pixel groups sampled, those with a value >= 4,096, >= 16,384.  The host
+  // reads the counts once per job and launches only the Welford pass and the
+  // fused configuration they call for (stats_choice).
+  DBuf<unsigned int> probe;
+  unsigned int* probe_host = nullptr;  // pinned copy
+  hipEvent_t ev_probe = nullptr;
+  bool probed = false;
+  unsigned int probe_cnt[3] = {0u, 0u, 0u};
   int64_t wide_sites = 0;         // sites that count covers
   bool pct_sum_external = false;
   DBuf<double> mean, m2, lut_log, gamma, acc, tmp_mean, tmp_std, rn;
@@ -417,7 +425,9 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
       h->m2.alloc(npx, true);
       h->wf_part.alloc((size_t)8 * npx);
       h->wide.alloc(2, true);  // groups with a value >= 4,096 / >= 16,384
-      h->probe.alloc(1);
+      h->probe.alloc(3);
+      TMH_HIP(hipHostMalloc((void**)&h->probe_host, 4 * sizeof(unsigned int), hipHostMallocDefault));
+      TMH_HIP(hipEventCreateWithFlags(&h->ev_probe, hipEventDisableTiming));
       h->acc.alloc(n_quantiles, true);
       h->pooled.alloc(kBins, true);
       h->lut_log.alloc(kBins);
@@ -466,6 +476,8 @@ void tmh_stats_destroy(tmh_stats* h) {
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   if (h->ev_out) (void)hipEventDestroy(h->ev_out);
+  if (h->ev_probe) (void)hipEventDestroy(h->ev_probe);
+  if (h->probe_host) (void)hipHostFree(h->probe_host);
   delete h;
   if (s) (void)hipStreamDestroy(s);
   if (side) (void)hipStreamDestroy(side);
@@ -523,7 +535,37 @@ int tmh_stats_reset(tmh_stats* h) {
     h->last_batch = 0;
     h->pending = 0;
     h->pct_sum_external = false;
+    h->probed = false;  // the next job probes its own sites
   });
+}
+
+// The job's site probe, once per job (first call after a reset): one small
+// kernel on s, its three counts copied to pinned memory, and the host waits
+// for them -- a wait for the probe itself plus whatever s had queued before
+// it.  Nothing is probed when every automatic choice is forced off.
+static void stats_probe(tmh_stats* h, const uint16_t* d, int64_t ns, const SiteTab& tab,
+                        hipStream_t s) {
+  if (h->probed || ns <= 0) return;
+  launch_site_probe(d, h->npx, ns, h->probe.p, s, tab);
+  TMH_HIP(hipMemcpyAsync(h->probe_host, h->probe.p, 3 * sizeof(unsigned int),
+                         hipMemcpyDeviceToHost, s));
+  TMH_HIP(hipEventRecord(h->ev_probe, s));
+  TMH_HIP(hipEventSynchronize(h->ev_probe));
+  for (int i = 0; i < 3; ++i) h->probe_cnt[i] = h->probe_host[i];
+  h->probed = true;
+}
+
+// The automatic choices from the probe (a job not probed: standard).
+static bool probe_bright(const tmh_stats* h) {
+  return h->probed && (double)h->probe_cnt[1] >= kBrightFrac * (double)h->probe_cnt[0];
+}
+static int probe_fused_cfg(const tmh_stats* h) {
+  if (h->fused_cfg != kFusedAuto) return h->fused_cfg;
+  if (!h->probed) return kFusedNarrow;
+  const double g = (double)h->probe_cnt[0];
+  if ((double)h->probe_cnt[2] >= kXWideFrac * g) return kFusedNoHist;
+  if ((double)h->probe_cnt[1] >= kWideFrac * g) return kFusedWide;
+  return kFusedNarrow;
 }
 
 static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int log_transform,
@@ -540,12 +582,17 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
   const int64_t chunk = 4096;
   stats_reserve_sites(h, std::min(chunk, ns));  // (re)allocate before forking
   if (h->flags & TMH_STATS_DEFERRED_PCT) stats_grow_deferred(h, ns);
+  // the bright Welford form needs a three-part split (>= 96 sites): only then
+  // is the probe worth its host wait
+  const bool vec = (h->npx & 7) == 0 && (reinterpret_cast<uintptr_t>(d) & 15) == 0;
+  if (vec && log_transform && h->wf_parts == 0 && ns >= 96) stats_probe(h, d, ns, SiteTab{}, s);
   if (!serial) {
     TMH_HIP(hipEventRecord(h->ev_fork, s));
     TMH_HIP(hipStreamWaitEvent(hs, h->ev_fork, 0));
   }
   launch_welford(d, h->npx, ns, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
-                 log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, nullptr, h->probe.p, s);
+                 log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, nullptr,
+                 probe_bright(h) ? 1 : 0, s);
   // order statistics, in chunks so the per-site slabs stay bounded
   for (int64_t c0 = 0; c0 < ns; c0 += chunk) {
     const int64_t nc = std::min(chunk, ns - c0);
@@ -568,19 +615,40 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
   h->n += ns;
 }
 
+// Stream contract of the statistics entry points that take a stream
+// (include/tmhip.h): on another stream than the handle's, the work runs after
+// everything queued on the handle's stream, and the handle's stream waits for
+// it before any later work on the handle.
+static void cross_begin(tmh_stats* h, hipStream_t s) {
+  if (s == h->stream) return;
+  TMH_HIP(hipEventRecord(h->ev_in, h->stream));
+  TMH_HIP(hipStreamWaitEvent(s, h->ev_in, 0));
+}
+static void cross_end(tmh_stats* h, hipStream_t s) {
+  if (s == h->stream) return;
+  TMH_HIP(hipEventRecord(h->ev_out, s));
+  TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
+}
+
 static void stats_welford_dev(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
                               int log_transform, void* stream, const SiteTab& tab) {
   hipStream_t s = pick(h->stream, stream);
+  cross_begin(h, s);
   if ((size_t)n_sites > h->rn.n) {
     TMH_HIP(hipStreamSynchronize(s));
     h->rn.alloc((size_t)n_sites);
   }
+  // the probe serves the fused pass's configuration and the Welford form
+  const bool vec = tab.in || ((h->npx & 7) == 0 && (reinterpret_cast<uintptr_t>(dev_sites) & 15) == 0);
+  if (vec && (h->fused_cfg == kFusedAuto || (log_transform && h->wf_parts == 0)))
+    stats_probe(h, dev_sites, n_sites, tab, s);
   launch_welford(dev_sites, h->npx, n_sites, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
-                 log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, h->wide.p, h->probe.p, s,
-                 -1, tab);
+                 log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, h->wide.p,
+                 probe_bright(h) ? 1 : 0, s, -1, tab);
   if ((h->npx & 7) == 0) h->wide_sites += n_sites;
   h->n += n_sites;
   h->pending += n_sites;
+  cross_end(h, s);
 }
 
 int tmh_stats_update_welford_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
@@ -620,7 +688,10 @@ int tmh_stats_update_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_s
                             int log_transform, void* stream) {
   return guard([&] {
     TMH_CHECK(h && (dev_sites || n_sites == 0) && n_sites >= 0, TMH_EINVAL, "bad arguments");
-    stats_update_dev(h, dev_sites, n_sites, log_transform, pick(h->stream, stream));
+    const hipStream_t s = pick(h->stream, stream);
+    cross_begin(h, s);
+    stats_update_dev(h, dev_sites, n_sites, log_transform, s);
+    cross_end(h, s);
   });
 }
 
@@ -742,6 +813,20 @@ int tmh_stats_variance(tmh_stats* h, double* host_var) {
     launch_variance(h->m2.p, h->n, h->npx, h->tmp_std.p, h->stream);
     TMH_HIP(hipMemcpyAsync(host_var, h->tmp_std.p, h->npx * 8, hipMemcpyDeviceToHost, h->stream));
     TMH_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int tmh_stats_job_choice(tmh_stats* h, uint32_t* probe_counts, int* welford_bright,
+                         int* fused_cfg) {
+  return guard([&] {
+    TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
+    if (probe_counts)
+      for (int i = 0; i < 3; ++i) probe_counts[i] = h->probed ? h->probe_cnt[i] : 0u;
+    if (welford_bright) *welford_bright = h->probed ? (probe_bright(h) ? 1 : 0) : -1;
+    if (fused_cfg) {
+      const int c = probe_fused_cfg(h);
+      *fused_cfg = c == kFusedNoHist ? TMH_FUSED_NO_HIST : c;
+    }
   });
 }
 
@@ -1254,9 +1339,9 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
     TMH_CHECK(vec || !tab.in, TMH_EINVAL,
               "a blocked site layout needs the fused pass (zero_log10 in [-37, 0])");
     if (vec) {
-      // rare lists (RareList, common.h): the auto choice or configuration 5 may
-      // run the packed configuration
-      const bool rl_on = h->fused_cfg == kFusedAuto || h->fused_cfg == kFusedWide;
+      // rare lists (RareList, common.h) for the packed configuration
+      if (h->fused_cfg == kFusedAuto) stats_probe(h, dev_in, n_sites, tab, s);
+      const bool rl_on = probe_fused_cfg(h) == kFusedWide;
       const unsigned int rl_cap =
           (unsigned int)std::min<int64_t>(65536, std::max<int64_t>(1024, h->npx / 64));
       const bool grow = (size_t)n_sites * kBins > h->hist_full.n || (size_t)n_sites > h->zeros.n ||
@@ -1299,30 +1384,28 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
       // in between, tmh_stats_reset clears them (hist_dirty)
       h->hist_dirty = true;
       uint32_t* sh = (h->flags & 2u) ? h->site_hist.p : nullptr;
-      // the wide configuration pays off once a few % of the pixel groups
-      // overflow the narrow slices (their values then take global atomics)
-      const unsigned long long wide_thresh = (unsigned long long)std::max<double>(
-          1.0, kWideFrac * (double)h->wide_sites * (double)(h->npx >> 3));
-      // very wide sites: histograms from k_hist_site_u16 instead (automatic
-      // configuration only; ~0 = never)
-      const bool autocfg = h->fused_cfg == kFusedAuto;
-      const unsigned long long xwide_thresh =
-          autocfg ? (unsigned long long)std::max<double>(
-                        1.0, kXWideFrac * (double)h->wide_sites * (double)(h->npx >> 3))
-                  : ~0ull;
+      // one configuration, chosen on the host from the job's site probe
+      // (probed at the Welford launch, or above for a job whose Welford pass
+      // did not probe)
+      const int cfg = probe_fused_cfg(h);
+      const bool very_wide = cfg == kFusedNoHist;
       const unsigned long long* rm_all = reinterpret_cast<const unsigned long long*>(c->queues.p + 8);
       const FixList fl = corrector_fixlist(c, n_sites, s);
       launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p, fl,
                           c->log_transform, clip_lo, clip_hi, h->hist_full.p, h->hist_rmask.p,
-                          c->queues.p, c->n_wg, h->fused_cfg, h->wide.p, wide_thresh, xwide_thresh,
-                          s, tab, rl);
-      launch_rare_count(rl, h->hist_full.p, n_sites, s);
+                          c->queues.p, c->n_wg, cfg, s, tab, rl);
+      if (cfg == kFusedWide) launch_rare_count(rl, h->hist_full.p, n_sites, s);
       launch_fix_correct(dev_in, dev_out, 2, c->npx, n_sites, fl, c->coef64.p, c->rc.p,
                          c->log_transform, clip_lo, clip_hi, s, tab);
-      if (autocfg)  // exits at once unless the launch is very wide
+      if (very_wide)  // the histograms from one more read of the sites
         launch_hist_site_u16(dev_in, h->npx, n_sites, h->hist_full.p, h->qp, vlh, ld, h->pooled.p,
-                             h->pooled_parts.p, kPooledParts, h->zeros.p, sh, h->wide.p,
-                             xwide_thresh, s, tab);
+                             h->pooled_parts.p, kPooledParts, h->zeros.p, sh, nullptr, 0, s, tab);
+      // the Welford pass's diagnostic wide counts restart with the next batch
+      // (reset here on s, before any later Welford launch on the handle)
+      if (h->pending - n_sites == 0) {
+        TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, s));
+        h->wide_sites = 0;
+      }
       // The histogram tail (order statistics, percentile sums) reads only the
       // handle's buffers: called on another stream than the handle's, it runs
       // on the handle's tail stream (the handle's stream waits for it), so s
@@ -1339,19 +1422,16 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
         TMH_HIP(hipStreamWaitEvent(h->tail, h->ev_out, 0));
         ts = h->tail;
       }
-      launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, n_sites, h->qp, vlh, ld,
-                           h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, sh, ts, false,
-                           rm_all, h->wide.p, xwide_thresh);
+      if (!very_wide)
+        launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, n_sites, h->qp, vlh, ld,
+                             h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, sh, ts,
+                             false, rm_all);
       if (!(h->flags & TMH_STATS_DEFERRED_PCT))
         launch_pct_accumulate(vlh, n_sites, ld, h->Q, h->gamma.p, h->acc.p, ts);
       h->hist_dirty = false;
       if (h->flags & TMH_STATS_DEFERRED_PCT) h->n_deferred += n_sites;
       h->last_batch = n_sites;
       h->pending -= n_sites;
-      if (h->pending == 0) {  // the wide counts restart with the next Welford batch
-        TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, ts));
-        h->wide_sites = 0;
-      }
       if (cross) {  // the handle's later work, and this corrector's next pass, after the tail
         TMH_HIP(hipEventRecord(h->ev_tail, ts));
         TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_tail, 0));

@@ -182,11 +182,18 @@ __device__ __forceinline__ int64_t site_in_block(const SiteTab& t, int64_t s) {
   return s & ((1ll << t.shift) - 1);
 }
 
+// bright: 1 = the host's site probe found bright sites (the 16,384-entry LUT
+// pass in three site parts where the launch allows), 0 = standard
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
                     double* part, size_t part_cap, int forced_parts,
-                    unsigned long long* wide, unsigned int* probe, hipStream_t s, int shape = -1,
+                    unsigned long long* wide, int bright, hipStream_t s, int shape = -1,
                     const SiteTab& tab = SiteTab{});
+// Site probe: out[0] = 8-pixel groups sampled (kProbeGroups, spread over the
+// launch's first <= 64 sites), out[1] / out[2] = those holding a value >=
+// 4,096 / >= 16,384 (device words; the caller copies them to the host)
+void launch_site_probe(const uint16_t* sites, int64_t npx, int64_t n_sites, unsigned int* out,
+                       hipStream_t s, const SiteTab& tab = SiteTab{});
 // vlh: the order statistics of the launch's first site (buffer + site *
 // kOsTile) in a buffer with room for vlh_ld sites (kOsTile layout above)
 void launch_hist_scatter(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* hist_hi,
@@ -199,8 +206,9 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
                           uint32_t* site_hist, hipStream_t s, bool narrow = false,
                           const unsigned long long* rm_all = nullptr,
                           const unsigned long long* wide = nullptr, unsigned long long xthr = 0);
-// very wide launches (wide[1] >= xthr): the exact per-site histogram in LDS
-// as u16 pairs from one more read of the sites, scanned into order statistics
+// very wide launches: the exact per-site histogram in LDS as u16 pairs from
+// one more read of the sites, scanned into order statistics (wide == null:
+// unconditionally; else only when wide[1] >= xthr)
 void launch_hist_site_u16(const uint16_t* sites, int64_t npx, int64_t n_sites, uint32_t* slab,
                           const QPos& p, uint32_t* vlh, int64_t vlh_ld,
                           unsigned long long* pooled, unsigned long long* pooled_parts,
@@ -273,9 +281,9 @@ void launch_correct_u8(const uint8_t* in, uint8_t* out, int64_t npx, int64_t n_s
                        const FixList& fl, int log_transform, int clip_lo, int clip_hi,
                        hipStream_t s);
 // fused pass configurations (fused_kernels.hip kFusedCfgs).  kFusedAuto picks
-// per launch, on the device: kFusedNarrow (four sites per unit, 4,096-bin
-// slices) unless the Welford pass counted at least kWideFrac of the pixel
-// groups with a value >= 4,096, then kFusedWide: four sites, 16,384 bins
+// per job on the host from the site probe: kFusedNarrow (four sites per unit,
+// 4,096-bin slices) unless at least kWideFrac of the probed pixel groups hold
+// a value >= 4,096, then kFusedWide: four sites, 16,384 bins
 // each as u16 counters packed two sites to a word (round 3: 15.95-16.11 ms
 // on 3,456 bright sites against 17.67-17.75 for configuration 0's two sites
 // x 16,384 u32 bins, profiles/r3/ab_fused_packed_bright_r3z20.jsonl; round 2:
@@ -292,13 +300,19 @@ constexpr double kWideFrac = 0.02;
 // cost more than one more read of the sites); the fused pass then runs without
 // its histogram and k_hist_site_u16 builds the histograms
 constexpr double kXWideFrac = 0.33;
+// the Welford pass's bright form: >= kBrightFrac of the probed groups hold a
+// value >= 4,096
+constexpr double kBrightFrac = 0.10;
+// the fused pass without its histogram (very wide sites: k_hist_site_u16
+// builds the histograms)
+constexpr int kFusedNoHist = 100;
+// cfg: 0 .. kFusedConfigs - 1 or kFusedNoHist -- exactly one launch
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, const FixList& fl,
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
                          unsigned long long* rmask, int* queues, int n_wg, int cfg,
-                         const unsigned long long* wide, unsigned long long wide_thresh,
-                         unsigned long long xwide_thresh, hipStream_t s,
-                         const SiteTab& tab = SiteTab{}, const RareList& rl = RareList{});
+                         hipStream_t s, const SiteTab& tab = SiteTab{},
+                         const RareList& rl = RareList{});
 // after launch_correct_hist with a RareList: each site's list into its
 // histogram (hist + s * kBins), on the same stream
 void launch_rare_count(const RareList& rl, uint32_t* hist, int64_t n_sites, hipStream_t s);

@@ -190,17 +190,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
     const float4* __restrict__ coef, const float4* __restrict__ mconst2, FixList fl,
     int clip_lo, int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
-    int n_bands, int* __restrict__ queues, const unsigned long long* __restrict__ wide,
-    unsigned long long wide_lo, unsigned long long wide_hi, unsigned long long x_lo,
-    unsigned long long x_hi, const SiteTab tab, const RareList rl) {
-  // launch-time selection (launch_correct_hist): this configuration runs only
-  // when the Welford pass's counts of pixel groups with a value >= 4,096 and
-  // >= 16,384 are in [wide_lo, wide_hi) and [x_lo, x_hi)
-  if (wide) {
-    const unsigned long long w = __builtin_nontemporal_load(wide);
-    const unsigned long long x = __builtin_nontemporal_load(wide + 1);
-    if (w < wide_lo || w >= wide_hi || x < x_lo || x >= x_hi) return;
-  }
+    int n_bands, int* __restrict__ queues, const SiteTab tab, const RareList rl) {
   constexpr int BINS = LB / SPU;
   constexpr int SLICE = BINS + 1;
   constexpr int NSL = PK ? SPU / 2 : SPU;  // word arrays (PK: two sites per array)
@@ -583,7 +573,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
 }
 
 // (sites per unit, threads, LDS bins) of the fused pass, selected per handle
-// (tmh_stats_set_option, TMH_OPT_FUSED_CONFIG) or automatically per launch
+// (tmh_stats_set_option, TMH_OPT_FUSED_CONFIG) or automatically per job
 // (kFusedAuto: kFusedNarrow, or kFusedWide when the sites are bright).
 // bands: pixel bands of the unit sweep -- 8 for the wide configuration, whose
 // 16,384-bin slices flush more counts per unit (fewer, longer units: 17.3 vs
@@ -607,17 +597,11 @@ struct FusedCfgCheck {
 static_assert(FusedCfgCheck<0>::ok && FusedCfgCheck<1>::ok && FusedCfgCheck<2>::ok &&
               FusedCfgCheck<3>::ok && FusedCfgCheck<4>::ok && FusedCfgCheck<5>::ok, "");
 
-// cfg kFusedNoHist: the narrow shape without its histogram (very wide sites:
-// k_hist_site_u16 builds the histograms)
-constexpr int kFusedNoHist = 100;
 static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                                     const float4* cf4, const float4* mconst2, const FixList& fl,
                                     int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
                                     unsigned long long* rmask, int* queues, int n_wg, int cfg,
-                                    const unsigned long long* wide, unsigned long long wide_lo,
-                                    unsigned long long wide_hi, unsigned long long x_lo,
-                                    unsigned long long x_hi, hipStream_t s, const SiteTab& tab,
-                                    const RareList& rl) {
+                                    hipStream_t s, const SiteTab& tab, const RareList& rl) {
 #define TMH_LAUNCH_CH(L_, K_, A_)                                                                \
   {                                                                                              \
     constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
@@ -626,14 +610,14 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
       hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, A_, c.threads, c.lds_bins, c.packed>), \
                          grid,                                                                   \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
-                         wide_hi, x_lo, x_hi, tab, c.packed ? rl : RareList{});                  \
+                         clip_lo, clip_hi, hist, rmask, c.bands, queues, tab,                   \
+                         c.packed ? rl : RareList{});                                       \
     else                                                                                         \
       hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, A_, c.threads, c.lds_bins, c.packed>), \
                          grid,                                                                   \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, c.bands, queues, wide, wide_lo,          \
-                         wide_hi, x_lo, x_hi, tab, c.packed ? rl : RareList{});                  \
+                         clip_lo, clip_hi, hist, rmask, c.bands, queues, tab,                   \
+                         c.packed ? rl : RareList{});                                       \
   }
 #define TMH_LAUNCH_CFG(L_)                                     \
   switch (cfg) {                                               \
@@ -655,40 +639,25 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
   TMH_HIP(hipGetLastError());
 }
 
-// cfg >= 0: that configuration.  cfg == kFusedAuto: both kFusedNarrow and
-// kFusedWide are queued and each reads the Welford pass's wide-group count
-// (*wide) on the device, so exactly one of them runs -- the choice costs no
-// host round trip, and the idle launch ends in microseconds.  wide_thresh =
-// groups at which the wide configuration is preferred.  Either way the round
-// masks name every non-empty round, so the histogram finalize is the same.
+// One launch of configuration cfg (chosen by the caller: abi.hip picks it per
+// job from the host-read site probe, so no losing configuration is queued).
+// The round masks name every non-empty round whatever the configuration, so
+// the histogram finalize is the same.  The "correct_hist" timing bracket
+// holds the kernel alone (the scratch reset is outside it), so the bench's
+// per-launch rate is the pass's own.
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, const FixList& fl,
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
                          unsigned long long* rmask, int* queues, int n_wg, int cfg,
-                         const unsigned long long* wide, unsigned long long wide_thresh,
-                         unsigned long long xwide_thresh, hipStream_t s, const SiteTab& tab,
-                         const RareList& rl) {
+                         hipStream_t s, const SiteTab& tab, const RareList& rl) {
   if (n_sites <= 0) return;
-  ProfScope prof("correct_hist", s);
   // queues[0..8): per-XCD unit counters; queues[8..10): the union of the
-  // sites' round masks (read by the pooled column sum).  Zeroed once for both
-  // configurations of an automatic launch: the one that does not run exits
-  // before touching either.
+  // sites' round masks (read by the pooled column sum)
   TMH_HIP(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), s));
   const float4* cf4 = reinterpret_cast<const float4*>(coef2);
-  if (cfg >= 0 || !wide) {
-    launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo,
-                            clip_hi, hist, rmask, queues, n_wg, cfg >= 0 ? cfg : kFusedNarrow,
-                            nullptr, 0, 0, 0, 0, s, tab, rl);
-    return;
-  }
-  const unsigned long long X = xwide_thresh;
+  ProfScope prof("correct_hist", s);
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedNarrow, wide, 0, wide_thresh, 0, X, s, tab, rl);
-  launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedWide, wide, wide_thresh, ~0ull, 0, X, s, tab, rl);
-  launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, kFusedNoHist, wide, 0, ~0ull, X, ~0ull, s, tab, rl);
+                          hist, rmask, queues, n_wg, cfg, s, tab, rl);
 }
 
 // Each site's rare list into its histogram: one workgroup per site, the

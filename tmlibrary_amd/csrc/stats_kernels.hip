@@ -213,29 +213,14 @@ __device__ __forceinline__ uint4 ld_site(gsite_t* p) {
 // BLK: blocked site layout (common.h SiteTab): site t of the launch is site
 // t & (2^shift - 1) of block t >> shift; the block base is re-read (one scalar
 // load) only when the walk enters a new block.
-// SEL (with a probe): 0 = the probe picks one part or all of gridDim.y (the
-// standard pass), 1 = run only when the probe found standard sites (one
-// part), 2 = run only when it found bright ones (LUTN = kWfLutBright)
 template <bool LOG, bool NTL, int NT, int INV, bool BLK = false, int G = kWfGroup,
-          int LUTN = kWfLut, int SEL = 0>
+          int LUTN = kWfLut>
 __global__ __launch_bounds__(NT) void k_welford_vec8(
     const uint16_t* __restrict__ sites, int64_t npx, int64_t n_total, int64_t per,
     const WfMerge mg, double* __restrict__ mean, double* __restrict__ m2,
     const double* __restrict__ lut, double* __restrict__ part,
-    unsigned long long* __restrict__ wide, const unsigned int* __restrict__ probe,
-    unsigned int probe_thr, const SiteTab tab) {
-  // probe (k_wf_probe): the site split applies only to bright sites; otherwise
-  // the part-0 workgroups walk every site and the others leave at once
-  int parts = (int)gridDim.y;
-  if (probe) {
-    const bool bright = __builtin_nontemporal_load(probe) >= probe_thr;
-    if ((SEL == 1 && bright) || (SEL == 2 && !bright)) return;
-    if (SEL == 0 && !bright) {
-      if (blockIdx.y > 0) return;
-      parts = 1;
-      per = n_total;
-    }
-  }
+    unsigned long long* __restrict__ wide, const SiteTab tab) {
+  const int parts = (int)gridDim.y;
   __shared__ double slut[LUTN], sinv[INV == 1 ? kWfLut : 1];
   __shared__ uint32_t wide_sh[2];
   if (LOG) fill_wf_tables<INV, LUTN>(lut, slut, sinv, NT);
@@ -371,9 +356,7 @@ struct WfParts {
 // Fold the parts' (mean_l, M2_l) in part order (Chan's pairwise combine),
 // then into the running state (n0 sites before this launch).
 __global__ void k_wf_merge_parts(const double* __restrict__ part, int64_t npx, const WfParts pc,
-                                 double n0, double* __restrict__ mean, double* __restrict__ m2,
-                                 const unsigned int* __restrict__ probe, unsigned int probe_thr) {
-  if (probe && __builtin_nontemporal_load(probe) < probe_thr) return;  // one-part launch
+                                 double n0, double* __restrict__ mean, double* __restrict__ m2) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= npx) return;
   double na = pc.cnt[0], ma = part[i], qa = part[npx + i];
@@ -428,20 +411,18 @@ static int welford_parts(int64_t n_sites, int64_t npx, size_t part_cap, int forc
   return forced && fits(forced) ? forced : 1;
 }
 
-template <int NT, int INV, int G = kWfGroup, int LUTN = kWfLut, int SEL = 0>
+template <int NT, int INV, int G = kWfGroup, int LUTN = kWfLut>
 static void launch_welford_vec8(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t per,
                                 int f, const WfMerge& mg, double* mean, double* m2,
                                 const double* lut, int log_transform, double* part,
                                 unsigned long long* wide, hipStream_t s,
-                                const unsigned int* probe = nullptr, unsigned int probe_thr = 0,
                                 const SiteTab& tab = SiteTab{}) {
   const dim3 grid((unsigned)cdiv(npx >> 3, NT), (unsigned)f);
   // site loads are non-temporal (streamed once; regular loads measured
   // 6.60-6.75 vs 6.19-6.34 ms at job level, profiles/r1/ab_welford_ntl.txt)
 #define TMH_WF(L_, B_)                                                                           \
-  hipLaunchKernelGGL((k_welford_vec8<L_, true, NT, INV, B_, G, LUTN, SEL>), grid, dim3(NT), 0, s, \
-                     sites, npx, \
-                     n_sites, per, mg, mean, m2, lut, part, wide, probe, probe_thr, tab)
+  hipLaunchKernelGGL((k_welford_vec8<L_, true, NT, INV, B_, G, LUTN>), grid, dim3(NT), 0, s,     \
+                     sites, npx, n_sites, per, mg, mean, m2, lut, part, wide, tab)
   if (tab.in) {
     if (log_transform)
       TMH_WF(true, true);
@@ -456,64 +437,88 @@ static void launch_welford_vec8(const uint16_t* sites, int64_t npx, int64_t n_si
 #undef TMH_WF
 }
 
-// Bright-site probe: of kProbeGroups 8-pixel groups spread over the launch's
-// first site, how many hold a value >= 4,096 (one workgroup, count to *out).
-// Bright sites make the log10 pass VALU-bound, where three site parts (three
-// times the workgroups) pay: 11.3 vs 12.4 ms on 3,456 bright sites, against
-// 6.0 vs 5.85 on standard ones (profiles/r2/mb_welford_bright_r2za.txt,
-// mb_welford_r2f.txt) -- so the split is chosen on the device, per launch.
+// Site probe of a job (tmh_stats' automatic choices, abi.hip): of kProbeGroups
+// 8-pixel groups spread over the launch's first min(n, kProbeSites) sites, how
+// many hold a value >= 4,096 (out[1]) and >= 16,384 (out[2]); out[0] = the
+// groups sampled.  One workgroup, every load in flight at once (one DRAM
+// latency).  The host reads the counts and launches only the Welford pass and
+// the fused configuration they call for: no candidate launch that waits for
+// LDS behind another job's kernels just to exit (round 4: the idle packed
+// fused candidate averaged 1.58 ms on the corrected-pass stream,
+// profiles/r4/rocprof_kernel_stats_synthetic_r4fin3.csv).
 constexpr int kProbeGroups = 16384;
+constexpr int kProbeSites = 64;
 constexpr int kWfBrightParts = 3;
-__global__ __launch_bounds__(1024) void k_wf_probe(const uint16_t* __restrict__ sites,
-                                                   int64_t ngroups, unsigned int* __restrict__ out,
-                                                   const SiteTab tab) {
-  if (tab.in) sites = tab.in[0];  // blocked layout: the first site opens block 0
-  __shared__ unsigned int cnt;
-  if (threadIdx.x == 0) cnt = 0u;
+__global__ __launch_bounds__(1024) void k_site_probe(const uint16_t* __restrict__ sites,
+                                                     int64_t ngroups, int n_probe,
+                                                     unsigned int* __restrict__ out,
+                                                     const SiteTab tab) {
+  __shared__ unsigned int cnt[2];
+  if (threadIdx.x < 2) cnt[threadIdx.x] = 0u;
   __syncthreads();
-  // all 16 loads of a thread in flight at once (one DRAM latency, not 16)
+  // sample j: site j % n_probe, its (j / n_probe)-th of R positions spread
+  // over the site
+  const int R = (kProbeGroups + n_probe - 1) / n_probe;
   uint4 v[kProbeGroups / 1024];
 #pragma unroll
   for (int k = 0; k < kProbeGroups / 1024; ++k) {
-    const int64_t g = (int64_t)(threadIdx.x + 1024 * k) * ngroups / kProbeGroups;
-    v[k] = reinterpret_cast<const uint4*>(sites)[g];
+    const int j = (int)threadIdx.x + 1024 * k;
+    const int st = j % n_probe;
+    const int64_t g = (int64_t)(j / n_probe) * ngroups / R;
+    const uint16_t* base =
+        tab.in ? tab.in[site_block(tab, st)] + site_in_block(tab, st) * ngroups * 8
+               : sites + (int64_t)st * ngroups * 8;
+    v[k] = reinterpret_cast<const uint4*>(base)[g];
   }
-  unsigned int c = 0u;
+  unsigned int w = 0u, x = 0u;
 #pragma unroll
-  for (int k = 0; k < kProbeGroups / 1024; ++k)
-    c += ((v[k].x | v[k].y | v[k].z | v[k].w) & 0xF000F000u) ? 1u : 0u;
-  if (c) atomicAdd(&cnt, c);
+  for (int k = 0; k < kProbeGroups / 1024; ++k) {
+    const uint32_t any = v[k].x | v[k].y | v[k].z | v[k].w;
+    w += (any & 0xF000F000u) ? 1u : 0u;
+    x += (any & 0xC000C000u) ? 1u : 0u;
+  }
+  if (w) atomicAdd(&cnt[0], w);
+  if (x) atomicAdd(&cnt[1], x);
   __syncthreads();
-  if (threadIdx.x == 0) out[0] = cnt;
+  if (threadIdx.x == 0) {
+    out[0] = (unsigned int)kProbeGroups;
+    out[1] = cnt[0];
+    out[2] = cnt[1];
+  }
 }
 
-// shape = -1: production (kWfThreads, kWfInv); 0..5: (256|512 threads) x
-// (f64 Newton | f64 LDS-table reciprocal | f32 small term) for the microbenchmark
+void launch_site_probe(const uint16_t* sites, int64_t npx, int64_t n_sites, unsigned int* out,
+                       hipStream_t s, const SiteTab& tab) {
+  const int np = (int)std::min<int64_t>(n_sites, kProbeSites);
+  hipLaunchKernelGGL(k_site_probe, dim3(1), dim3(1024), 0, s, sites, npx >> 3, np, out, tab);
+  TMH_HIP(hipGetLastError());
+}
+
+// shape = -1: production (kWfThreads, kWfInv); 0..8: (256|512 threads) x
+// (f64 Newton | f64 LDS-table reciprocal | f32 small term) x pipeline depth,
+// for the microbenchmark.  bright (production shape, log transform, no forced
+// split): the host's site probe found bright sites -- the 16,384-entry LUT
+// pass in kWfBrightParts site parts (the log10 pass is VALU-bound there:
+// three times the workgroups even the dispatch rounds, 11.3 vs 12.4 ms with
+// the 4,096-entry pass, profiles/r2/mb_welford_bright_r2za.txt; the 16,384
+// entries 8.0 vs 11.4 ms, profiles/r3/ab_welford_bright16k_bright_r3m.jsonl).
 void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t n0, double* rn,
                     double* mean, double* m2, const double* lut, int log_transform,
                     double* part, size_t part_cap, int forced_parts,
-                    unsigned long long* wide, unsigned int* probe, hipStream_t s, int shape,
+                    unsigned long long* wide, int bright, hipStream_t s, int shape,
                     const SiteTab& tab) {
   if (n_sites <= 0) return;
-  ProfScope prof("welford", s);
   // (a blocked layout is checked by the caller: npx % 8 == 0, 16-B aligned blocks)
   const bool vec = tab.in || ((npx & 7) == 0 && (reinterpret_cast<uintptr_t>(sites) & 15) == 0);
   if (vec) {
     int f = part ? welford_parts(n_sites, npx, part_cap, forced_parts) : 1;
-    // automatic split (no forced parts, log transform): k_wf_probe decides on
-    // the device between one part and kWfBrightParts (>= 10% of the sampled
-    // groups hold a value >= 4,096)
-    const unsigned int* pr = nullptr;
-    const unsigned int pthr = kProbeGroups / 10;
-    if (probe && part && !forced_parts && log_transform && shape < 0 &&
-        welford_parts(n_sites, npx, part_cap, kWfBrightParts) == kWfBrightParts) {
-      hipLaunchKernelGGL(k_wf_probe, dim3(1), dim3(1024), 0, s, sites, npx >> 3, probe, tab);
-      f = kWfBrightParts;
-      pr = probe;
-    }
+    const bool bpass = bright > 0 && part && !forced_parts && log_transform && shape < 0 &&
+                       welford_parts(n_sites, npx, part_cap, kWfBrightParts) == kWfBrightParts;
+    if (bpass) f = kWfBrightParts;
     const int64_t per = cdiv(n_sites, f);
     const double nl = (double)n_sites, n = (double)(n0 + n_sites);
     const WfMerge mg{1.0 / nl, nl / n, (double)n0 * nl / n, n0 == 0};
+    ProfScope prof("welford", s);  // the pass (and its part merge) only
     switch (shape) {
       case 0: launch_welford_vec8<256, 0>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       case 1: launch_welford_vec8<256, 1>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
@@ -526,17 +531,12 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
       case 7: launch_welford_vec8<256, 2, 4>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       case 8: launch_welford_vec8<512, 2, 4>(sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s); break;
       default:
-        if (pr) {  // the probe picks one of two passes on the device
-          launch_welford_vec8<kWfThreads, kWfInv, kWfGroup, kWfLut, 1>(
-              sites, npx, n_sites, n_sites, 1, mg, mean, m2, lut, log_transform, part, wide, s, pr,
-              pthr, tab);
-          launch_welford_vec8<kWfThreadsBright, kWfInv, kWfGroup, kWfLutBright, 2>(
-              sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s, pr, pthr,
-              tab);
-        } else {
+        if (bpass)
+          launch_welford_vec8<kWfThreadsBright, kWfInv, kWfGroup, kWfLutBright>(
+              sites, npx, n_sites, per, f, mg, mean, m2, lut, log_transform, part, wide, s, tab);
+        else
           launch_welford_vec8<kWfThreads, kWfInv>(sites, npx, n_sites, per, f, mg, mean, m2, lut,
-                                                  log_transform, part, wide, s, pr, pthr, tab);
-        }
+                                                  log_transform, part, wide, s, tab);
         break;
     }
     if (f > 1) {
@@ -545,7 +545,7 @@ void launch_welford(const uint16_t* sites, int64_t npx, int64_t n_sites, int64_t
       for (int p = 0; p < f; ++p)
         pc.cnt[p] = (double)std::min<int64_t>(per, n_sites - (int64_t)p * per);
       hipLaunchKernelGGL(k_wf_merge_parts, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, part,
-                         npx, pc, (double)n0, mean, m2, pr, pthr);
+                         npx, pc, (double)n0, mean, m2);
     }
   } else {  // the per-pixel Welford of odd shapes reads 1/n per site
     const dim3 grid((unsigned)cdiv(npx, kWfScalarThreads));
@@ -875,8 +875,8 @@ void launch_hist_finalize(uint32_t* hist, unsigned long long* rmask, int dense_r
 // headroom, against at most 16 waves x 15 x 64 = 15,360 LDS adds the
 // workgroup has outstanding at once.  (Spilling at the wrap itself raced: a carry
 // into the upper half, not yet undone, could make an add to the upper half
-// see -- and spill -- a wrap that was not there.)  Runs only when the Welford
-// pass's count of such groups (wide[1]) is >= xthr.
+// see -- and spill -- a wrap that was not there.)  Launched when the job's
+// site probe finds very wide sites (wide == null), or gated on a count.
 constexpr int kU16Threads = 1024;
 constexpr uint32_t kU16Spill = 0x4000u;
 __global__ __launch_bounds__(kU16Threads) void k_hist_site_u16(
@@ -885,7 +885,7 @@ __global__ __launch_bounds__(kU16Threads) void k_hist_site_u16(
     uint32_t* __restrict__ vlh_all, unsigned long long* __restrict__ pooled, int n_pooled,
     int64_t* __restrict__ zero_counts, uint32_t* __restrict__ site_hist,
     const unsigned long long* __restrict__ wide, unsigned long long xthr, const SiteTab tab) {
-  if (__builtin_nontemporal_load(wide + 1) < xthr) return;  // uniform: not a very wide launch
+  if (wide && __builtin_nontemporal_load(wide + 1) < xthr) return;  // uniform: not very wide
   constexpr int SR = 2;  // 2,048-bin super-rounds: 16 KB of ranks beside the 128 KB histogram
   __shared__ __attribute__((aligned(16))) uint32_t w16[kBins / 2];
   __shared__ uint32_t slots[32];

@@ -28,10 +28,11 @@ TMH_OPT_WELFORD_PARTS = 2
 TMH_OPT_COPY_THREADS = 4
 TMH_OPT_HOST_STAGING = 5
 TMH_OPT_FUSED_CUS = 8
+TMH_FUSED_NO_HIST = 100
 TMH_SYNTH_STANDARD = 0
 TMH_SYNTH_BRIGHT = 1
 TMH_SYNTH_UNIFORM = 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _P = C.c_void_p
 _I64 = C.c_int64
@@ -52,6 +53,7 @@ SIGNATURES = {
     "tmh_stats_set_option": (_I, [_P, _I, _I]),
     "tmh_stats_variance": (_I, [_P, _P]),
     "tmh_stats_wide_groups": (_I, [_P, _P, _P]),
+    "tmh_stats_job_choice": (_I, [_P, _P, _P, _P]),
     "tmh_stats_get_hist_device": (_I, [_P, _P, _P]),
     "tmh_stats_set_hist_device": (_I, [_P, _P, _P]),
     "tmh_stats_update": (_I, [_P, _P, _I64, _I, _P]),
@@ -153,8 +155,16 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     except ImportError:
         pass
     lib = C.CDLL(path)
+    # an A/B build of an earlier tree (TMH_LIB elsewhere, tools/gpu.sh ab) may
+    # lack entry points added since; the in-tree library must export them all
+    own = os.path.abspath(path) == os.path.join(_HERE, "libtmhip.so")
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if own:
+                raise
+            continue
         fn.restype = res
         fn.argtypes = args
     return lib

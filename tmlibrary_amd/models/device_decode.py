@@ -24,7 +24,7 @@ import time
 import numpy as np
 
 from tmlibrary_amd import hip
-from tmlibrary_amd.models.file import read_raw_chunks
+from tmlibrary_amd.models.file import RawChunksUnsupported, read_raw_chunks
 
 
 class DeviceChunkDecoder(object):
@@ -62,11 +62,16 @@ class DeviceChunkDecoder(object):
             slot[name] = t
         return t
 
-    def decode(self, paths, out_ptr, n_out=None):
+    def decode(self, paths, out_ptr, n_out=None, expect=None):
         """Decode ``paths`` into the device buffer at ``out_ptr`` ([n, H, W] of
         the files' dtype, contiguous).  Returns (H, W, elem_bytes).  The work is
         queued on ``self.stream``; the slot's buffers are reused two calls later
-        (the caller orders its consumers after ``self.stream``)."""
+        (the caller orders its consumers after ``self.stream``).
+
+        ``expect`` = (H, W, elem_bytes) the buffer was sized for: a block of
+        another shape raises ValueError (the reference's broadcast error in
+        OnlineStatistics.update), of another element size
+        RawChunksUnsupported -- both before anything is queued."""
         torch = self.torch
         L = hip.lib()
         t0 = time.perf_counter()
@@ -83,6 +88,13 @@ class DeviceChunkDecoder(object):
             None if ht is None else ht.numpy().view(hip.ZCHUNK_DTYPE))
         t2 = time.perf_counter()
         H, W, es, cr, cc = geom
+        if expect is not None:
+            eh, ew, ees = expect
+            if (H, W) != (eh, ew):
+                raise ValueError("operands could not be broadcast together with shapes (%d,%d) "
+                                 "(%d,%d)" % (H, W, eh, ew))
+            if es != ees:
+                raise RawChunksUnsupported("%d-byte pixels in a %d-byte job" % (es, ees))
         n = len(table)
         if hb is None or blob.ctypes.data != hb.data_ptr():  # grown: pin the new size
             hb = self._grow(slot, "h_blob", blob.nbytes, torch.uint8, pinned=True)
@@ -151,6 +163,19 @@ class DeviceChunkDecoder(object):
             raise IOError("%s: chunk %d: %s (%d of %d chunks failed to inflate)"
                           % (path, i, hip.Z_STATUS.get(int(st[i]), "error %d" % st[i]),
                              bad.size, n))
+
+    def reset(self):
+        """Forget every slot's pending block (after a job aborted part way):
+        waits for the queued work, drops the statuses unread, so a later job
+        never raises an earlier job's inflate error."""
+        for slot in self.slots:
+            ev = slot.get("event")
+            if ev is not None:
+                try:
+                    ev.synchronize()
+                finally:
+                    slot["event"] = None
+            slot["n"] = 0
 
     def check(self):
         """Wait for every queued block; raise if a chunk failed to inflate."""

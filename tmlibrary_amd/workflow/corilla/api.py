@@ -205,15 +205,25 @@ class IllumstatsCalculator(object):
         """The job's sites through the GPU inflate into the statistics, in order:
         block k+1's host chunk read and H2D copy overlap block k's inflate and
         statistics update (decoder stream D, statistics stream S; two device
-        site buffers, each reused once S has consumed it)."""
+        site buffers, each reused once S has consumed it).
+
+        Returns how many of ``file_ids`` (a prefix) went into ``stats``.  With
+        decode="auto" a block the GPU path cannot read (another layout or
+        element size: ``RawChunksUnsupported``, raised before anything of the
+        block is queued) ends the GPU path there, and the caller continues on
+        the host from the first file not taken -- every site is counted once,
+        in the job's order."""
         import torch
 
         from tmlibrary_amd.models.device_decode import DeviceChunkDecoder
         from tmlibrary_amd.workflow.corilla.stats import log_zero_warnings
+        strict = self.decode == "gpu"
         paths = [self.store.channel_image_file(f).location for f in file_ids]
         H, W, dt = channel_image_shape(paths[0])
         if np.dtype(dt) != np.uint16 or (H, W) != tuple(stats.image_dimensions):
-            raise RawChunksUnsupported("GPU decode takes uint16 sites of the job's shape")
+            if strict:
+                raise RawChunksUnsupported("GPU decode takes uint16 sites of the job's shape")
+            return 0
         B = self.device_block
         dev = torch.device("cuda", torch.cuda.current_device())
         st = self._dev
@@ -226,13 +236,21 @@ class IllumstatsCalculator(object):
         dec, S, bufs = st["dec"], st["S"], st["bufs"]
         zc = torch.zeros(len(file_ids), dtype=torch.int64, pin_memory=True).numpy()
         used = [None, None]
+        done, ok = 0, False
         try:
             for k in range(0, len(file_ids), B):
                 b = (k // B) % 2
                 if used[b] is not None:
                     dec.stream.wait_event(used[b])  # S has read the buffer's previous block
                 blk = paths[k:k + B]
-                dec.decode(blk, bufs[b].data_ptr())
+                try:
+                    dec.decode(blk, bufs[b].data_ptr(), expect=(H, W, 2))
+                except RawChunksUnsupported:
+                    if strict:
+                        raise
+                    logger.info("channel image files from %d on not GPU-decodable: decoding "
+                                "the rest on the host", k)
+                    break
                 ready = torch.cuda.Event()
                 ready.record(dec.stream)
                 S.wait_event(ready)
@@ -242,10 +260,16 @@ class IllumstatsCalculator(object):
                                     zero_counts=zc[k:k + len(blk)])
                 used[b] = torch.cuda.Event()
                 used[b].record(S)
-        finally:
+                done = k + len(blk)
             S.synchronize()
-        dec.check()  # a chunk that failed to inflate raises here
-        log_zero_warnings(zc)
+            dec.check()  # a chunk that failed to inflate raises here
+            ok = True
+        finally:
+            if not ok:  # aborted: nothing of this job may surface in a later one
+                S.synchronize()
+                dec.reset()
+        log_zero_warnings(zc[:done])
+        return done
 
     def run_job(self, batch, assume_clean_state=False):
         """corilla/api.py:115-146.  The reference reads the first site to learn
@@ -260,17 +284,13 @@ class IllumstatsCalculator(object):
         stats = OnlineStatistics(image_dimensions=(H, W), batch_size=self.batch_size)
         timing = {}
         try:
-            done = False
+            start = 0  # files already in the statistics (GPU path)
             if self.decode != "host":
-                try:
-                    self._update_device(file_ids, stats)
-                    done = True
-                except RawChunksUnsupported:
-                    if self.decode == "gpu":
-                        raise
+                start = self._update_device(file_ids, stats)
+                if start < len(file_ids):
                     logger.info("channel image files not GPU-decodable: decoding on the host")
-            if not done:
-                for ids, sites in self._blocks(file_ids):
+            if start < len(file_ids):
+                for ids, sites in self._blocks(file_ids[start:]):
                     for fid in ids:
                         logger.info("update statistics for image: %d", fid)
                     stats.update_batch(sites)

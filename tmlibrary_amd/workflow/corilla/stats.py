@@ -151,13 +151,20 @@ class OnlineStatistics(object):
         self._flush()
         L = hip.lib()
         sp = None if stream is None else C.c_void_p(int(stream))
-        hip.check(L.tmh_stats_update_device(self._h, C.c_void_p(int(dev_sites)), n,
-                                            int(bool(log_transform)), sp))
-        self._cache = None
         own = zero_counts is None
         if own:
             zero_counts = np.zeros(n, dtype=np.int64)
-        hip.check(L.tmh_stats_zero_counts(self._h, hip.ptr(zero_counts), n, sp))
+        # calls of <= 4,096 sites: the handle keeps one such chunk's zero
+        # counts (tmh_stats_zero_counts).  On another stream than the handle's
+        # the handle's stream waits for the work (tmhip.h stream contract).
+        site_bytes = 2 * self.image_dimensions[0] * self.image_dimensions[1]
+        for c0 in range(0, n, 4096):
+            nc = min(4096, n - c0)
+            hip.check(L.tmh_stats_update_device(self._h,
+                                                C.c_void_p(int(dev_sites) + c0 * site_bytes), nc,
+                                                int(bool(log_transform)), sp))
+            hip.check(L.tmh_stats_zero_counts(self._h, hip.ptr(zero_counts[c0:c0 + nc]), nc, sp))
+        self._cache = None
         if own:
             hip.check(L.tmh_synchronize(sp))
             if log_transform:

@@ -1,0 +1,127 @@
+#!/bin/bash
+# The one GPU-box runner: tools/gpu.sh TAG STEP [STEP ...]
+#
+# Runs the named steps in order on the box, every GPU step under its own time
+# limit; the first step that fails (a test failure excepted) ends the script,
+# so nothing more touches the GPU after a crash, abort or timeout.  Results go
+# to gpurun_out/*_TAG.*; copy the ones worth keeping into profiles/rN/.
+#
+# Steps:
+#   build          make clean + hipcc gfx950 build of libtmhip (and libtmh5
+#                  when libhdf5 is there) from the pushed sources, toolchain
+#                  and sha256 logged (build_TAG.log)
+#   tests          pytest -m gpu, then smoke (gpu_tests_TAG.log, smoke_TAG.log)
+#   bench          the default bench line, CPU baseline included (bench_TAG.json)
+#   quick          bench --steps 10 --no-extras --cpu-sample 0 (bench_quick_TAG.json)
+#   bright         quick on bright data (bench_bright_TAG.json)
+#   repeat:N       N more quick bench processes (bench_repeat_TAG.jsonl)
+#   dist432        one rank, forced-distributed, 4 channels x 432 sites: each
+#                  GPU's share of configs[2] at N = 8 (dist432_TAG.json)
+#   prof:DIST      rocprofv3 --kernel-trace --stats of a short bench on DIST
+#                  (synthetic | bright) -> rocprof_DIST_TAG/
+#   pmc:DIST       FETCH_SIZE and WRITE_SIZE passes (each its own run) of a
+#                  short bench on DIST -> pmc_traffic_DIST_TAG.json
+#   ab:R:LIB,LIB   same-box A/B of library builds (TMH_LIB), R rounds, the
+#                  order reversed every other round (ab_TAG.jsonl)
+# BENCH_ARGS adds flags to every bench run of quick/bright/repeat/ab/prof/pmc.
+set -u
+TAG=$1
+shift
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+O=gpurun_out
+QB="bench.py --steps 10 --warmup 3 --cpu-sample 0 --no-extras ${BENCH_ARGS:-}"
+SB="bench.py --steps 5 --warmup 2 --cpu-sample 0 --no-extras --no-profile ${BENCH_ARGS:-}"
+
+summ() {  # one-line summary of a bench JSON line
+  python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.strip()][-1]); r=d.get('roofline') or {}; print(sys.argv[1], d['value'], d['ms_per_step'], d.get('check_vs_oracle'), r.get('frac'), {k: v['avg_ms'] for k, v in d.get('kernels', {}).items()})" "$1"
+}
+
+for step in "$@"; do
+  IFS=: read -r name a1 a2 <<< "$step"
+  echo "== $step"
+  case $name in
+    build)
+      L=$O/build_$TAG.log
+      { /opt/rocm/bin/hipcc --version; echo; } > $L 2>&1
+      timeout -k 10 120 make -C tmlibrary_amd/csrc clean >> $L 2>&1 || exit $?
+      timeout -k 10 900 make -C tmlibrary_amd/csrc -j16 >> $L 2>&1 || exit $?
+      if [ -f /opt/conda/include/hdf5.h ]; then
+        timeout -k 10 300 make -C tmlibrary_amd/csrc h5 >> $L 2>&1 || exit $?
+      fi
+      sha256sum tmlibrary_amd/hip/*.so | tee -a $L
+      ;;
+    tests)
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -v -ra --timeout 300 --timeout-method thread > $O/gpu_tests_$TAG.log 2>&1
+      rc=$?
+      echo "pytest rc=$rc" >> $O/gpu_tests_$TAG.log
+      grep -E "passed|failed" $O/gpu_tests_$TAG.log | tail -3
+      if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+      timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > $O/smoke_$TAG.log 2>&1 || exit $?
+      tail -2 $O/smoke_$TAG.log
+      if [ $rc -ne 0 ]; then exit $rc; fi
+      ;;
+    bench)
+      timeout -k 10 900 python bench.py > $O/bench_$TAG.json 2> $O/bench_$TAG.err || exit $?
+      summ $O/bench_$TAG.json
+      ;;
+    quick)
+      timeout -k 10 300 python $QB > $O/bench_quick_$TAG.json 2> $O/bench_quick_$TAG.err || exit $?
+      summ $O/bench_quick_$TAG.json
+      ;;
+    bright)
+      timeout -k 10 300 python $QB --distribution bright > $O/bench_bright_$TAG.json 2> $O/bench_bright_$TAG.err || exit $?
+      summ $O/bench_bright_$TAG.json
+      ;;
+    repeat)
+      : > $O/bench_repeat_$TAG.jsonl
+      for i in $(seq 1 ${a1:-5}); do
+        timeout -k 10 300 python $QB > $O/b.tmp 2>> $O/bench_repeat_$TAG.err || exit $?
+        cat $O/b.tmp >> $O/bench_repeat_$TAG.jsonl
+        summ $O/b.tmp
+      done
+      ;;
+    dist432)
+      TMH_BENCH_FORCE_DIST=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \
+        timeout -k 10 300 python bench.py --layout sharded --channels 4 --sites 432 --steps 10 \
+        --warmup 3 --no-extras --cpu-sample 0 ${BENCH_ARGS:-} > $O/dist432_$TAG.json 2> $O/dist432_$TAG.err || exit $?
+      summ $O/dist432_$TAG.json
+      ;;
+    prof)
+      D=${a1:-synthetic}
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rocprof_${D}_$TAG -o run \
+        -- python3 $SB --distribution $D > $O/rocprof_${D}_$TAG.log 2>&1 || exit $?
+      ;;
+    pmc)
+      D=${a1:-synthetic}
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmc_${c}_${D}_$TAG -o run \
+          -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-extras --no-profile --distribution $D \
+          > $O/pmc_${c}_${D}_$TAG.log 2>&1 || exit $?
+      done
+      python3 tools/pmc_traffic.py $O/pmc_FETCH_SIZE_${D}_$TAG $O/pmc_WRITE_SIZE_${D}_$TAG --sites 3456 \
+        --height 2160 --width 2560 --distribution $D -o $O/pmc_traffic_${D}_$TAG.json || exit $?
+      ;;
+    ab)
+      IFS=, read -r -a LIBS <<< "$a2"
+      : > $O/ab_$TAG.jsonl
+      for i in $(seq 1 ${a1:-3}); do
+        ORDER=("${LIBS[@]}")
+        if [ $((i % 2)) -eq 0 ]; then
+          ORDER=(); for ((j=${#LIBS[@]}-1; j>=0; j--)); do ORDER+=("${LIBS[j]}"); done
+        fi
+        for L in "${ORDER[@]}"; do
+          # LIB may carry bench flags after a '+': path+--fused-config+3
+          IFS=+ read -r -a LA <<< "$L"
+          TMH_LIB=${LA[0]} timeout -k 10 300 python $QB "${LA[@]:1}" > $O/ab_$TAG.tmp 2>> $O/ab_$TAG.err || exit $?
+          python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[2]) if l.strip()][-1]); print(json.dumps({'lib': sys.argv[1], 'value': d['value'], 'ms': d['ms_per_step'], 'check': d['check_vs_oracle'], 'k': {k: v['avg_ms'] for k, v in d['kernels'].items()}}))" "$L" $O/ab_$TAG.tmp >> $O/ab_$TAG.jsonl
+          tail -1 $O/ab_$TAG.jsonl
+        done
+      done
+      ;;
+    *)
+      echo "unknown step $step"; exit 2
+      ;;
+  esac
+done
+echo "$TAG-ok"

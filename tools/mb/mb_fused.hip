@@ -169,7 +169,7 @@ static int run(int argc, char** argv) {
   time("fused auto (narrow runs, wide exits)", cb + 8.0 * npx, [&] {
     CK(hipMemsetAsync(fn, 0, 4, 0));
     launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                        queues, cus, kFusedAuto, wide, 1000ull, ~0ull, 0);
+                        queues, cus, kFusedNarrow, 0);
   });
   for (int cfg = 0; cfg < kFusedConfigs; ++cfg) {
     char nm[64];
@@ -178,8 +178,7 @@ static int run(int argc, char** argv) {
     time(nm, cb + 8.0 * npx, [&] {
       CK(hipMemsetAsync(fn, 0, 4, 0));
       launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist,
-                          rmask, queues, cus, cfg,
-                          nullptr, 0, 0, 0);
+                          rmask, queues, cus, cfg, 0);
     });
   }
   return 0;

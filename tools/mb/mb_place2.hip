@@ -134,7 +134,7 @@ int main(int argc, char** argv) {
         CK(hipMemsetAsync(fn, 0, 4, 0));
         CK(hipMemsetAsync(rmask, 0, S * 8, 0));
         launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist,
-                            rmask, queues, cus, kFusedNarrow, nullptr, 0, 0, 0, tab);
+                            rmask, queues, cus, kFusedNarrow, 0, tab);
       });
     };
     double *mean, *m2, *lut, *rn, *part;
@@ -152,7 +152,7 @@ int main(int argc, char** argv) {
     }
     auto welford = [&](const uint16_t* in, const SiteTab& tab) {
       return time([&] {
-        launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 1, wide, nullptr, 0, -1,
+        launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 1, wide, 0, 0, -1,
                        tab);
       });
     };

@@ -241,7 +241,7 @@ static int run(int argc, char** argv) {
   time("fused auto (narrow runs, wide exits)", [&] {
     CK(hipMemsetAsync(fn, 0, 4, 0));
     launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                        queues, cus, kFusedAuto, wide, 1000ull, ~0ull, 0);
+                        queues, cus, kFusedNarrow, 0);
   });
   for (int cfg = 0; cfg < kFusedConfigs; ++cfg) {
     snprintf(nm, sizeof nm, "fused cfg %d (%d,%d,%d)", cfg, kFusedCfgs[cfg].spu,
@@ -249,7 +249,7 @@ static int run(int argc, char** argv) {
     time(nm, [&] {
       CK(hipMemsetAsync(fn, 0, 4, 0));
       launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                          queues, cus, cfg, nullptr, 0, 0, 0);
+                          queues, cus, cfg, 0);
     });
   }
 #define TEAM(SPU_, NT_, ORD_, COEF_, G_, T_, NB_)                                                   \

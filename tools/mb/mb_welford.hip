@@ -399,7 +399,7 @@ static int run(int argc, char** argv) {
       char nm[80];
       snprintf(nm, sizeof nm, "welford shape %d (%s) parts %d", shape, shapes[shape], f);
       time(nm, [&] {
-        launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, f, nullptr, nullptr, 0, shape);
+        launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, f, nullptr, 0, 0, shape);
       });
     }
   time("wf f32 G2 blk16", [&] { hipLaunchKernelGGL((k_wf_f32<2, 16>), ag, dim3(256), 0, 0, in, npx, S, lut, mean); });
@@ -409,10 +409,10 @@ static int run(int argc, char** argv) {
   CK(hipMalloc(&probe, 4));
   for (int r = 0; r < 2; ++r) {
     time("welford production (parts 1)", [&] {
-      launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 1, nullptr, nullptr, 0);
+      launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 1, nullptr, 0, 0);
     });
-    time("welford automatic (probe, 1 or 3 parts)", [&] {
-      launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 0, nullptr, probe, 0);
+    time("welford bright form (16,384-entry LUT, 3 parts)", [&] {
+      launch_welford(in, npx, S, 0, rn, mean, m2, lut, 1, part, 8 * npx, 0, nullptr, 1, 0);
     });
   }
   return 0;

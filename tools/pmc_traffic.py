@@ -22,6 +22,7 @@ from __future__ import annotations
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 import re
@@ -82,8 +83,13 @@ def main():
            "correct": 2 * a.sites * site_bytes + 16 * npx,
            "correct_hist": 2 * a.sites * site_bytes + 8 * npx,
            "chain": 3 * a.sites * npx}
+    lib = os.environ.get("TMH_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                 "tmlibrary_amd", "hip", "libtmhip.so"))
+    with open(lib, "rb") as fh:
+        lib_sha = hashlib.sha256(fh.read()).hexdigest()
     res = {"config": {"sites": a.sites, "height": a.height, "width": a.width,
                       "distribution": a.distribution},
+           "library_sha256": lib_sha,
            "method": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch (separate --pmc passes; "
                      "gfx950 FETCH_SIZE halving corrected); median over the headline-sized launches "
                      "(>= 1/4 of the kernel's largest)",
