@@ -66,6 +66,17 @@ def parse():
     p.add_argument("--dry-run", action="store_true",
                    help="launcher check without a GPU: every rank joins a gloo group and rank 0 "
                         "prints the ranks' environments as its JSON line")
+    p.add_argument("--deadline", type=float, default=1500.0,
+                   help="--gpus N launcher: seconds the whole run may take; past it every rank's "
+                        "process group is killed and the launcher exits 3 naming each rank's "
+                        "last stage (the reference's failed job: exit non-zero with the cause, "
+                        "tmlib/workflow/cli.py:287-293)")
+    p.add_argument("--stall-timeout", type=float, default=300.0,
+                   help="--gpus N launcher: seconds without a heartbeat from ANY rank (every "
+                        "rank stuck, e.g. all waiting in a collective) before the ranks are "
+                        "killed and the launcher exits 3 naming each rank's last stage")
+    p.add_argument("--coll-timeout", type=float, default=600.0,
+                   help="timeout (s) of the ranks' process group (init and every collective)")
     p.add_argument("--share-gpu", action="store_true",
                    help="N > 1 ranks on GPU 0 of a one-GPU box (parity runs only): gloo group, "
                         "collectives staged through host memory (sharded.HostStagedDist)")
@@ -680,7 +691,10 @@ def bench_stream_host(a, world, rank, local_rank, dist_on):
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if dist_on:
-        dist.init_process_group("nccl", device_id=dev)
+        import datetime
+        Heartbeat(rank)("init_process_group")
+        dist.init_process_group("nccl", device_id=dev,
+                                timeout=datetime.timedelta(seconds=a.coll_timeout))
     H, W = a.height, a.width
     site_b = H * W * 2
     CH = a.stream_channels
@@ -944,6 +958,68 @@ def claim_stdout():
     return out
 
 
+class Heartbeat(object):
+    """A rank's progress for the launcher (``bench.py --gpus N``): the stage it
+    is in -- "init_process_group", "step 3", "all_reduce #41 (step 3)" -- one
+    line per stage to the file $TMH_BENCH_HEARTBEAT names (rewritten each
+    time; the launcher reads it and its mtime) and, for collectives and
+    phases, to stderr.  Inactive without that variable (a plain one-rank run
+    prints nothing more)."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.path = os.environ.get("TMH_BENCH_HEARTBEAT")
+        self.n = 0
+        self.step = ""
+
+    def __call__(self, stage, echo=True):
+        if not self.path:
+            return
+        line = "%.3f %s%s" % (time.time(), stage, self.step)
+        with open(self.path, "w") as f:
+            f.write(line + "\n")
+        if echo:
+            log("[rank %d] %s%s" % (self.rank, stage, self.step))
+
+
+class BeatingDist(object):
+    """The collectives' module with a heartbeat before every collective call:
+    a rank that never returns from one is named with it by the launcher."""
+
+    COLLECTIVES = ("all_reduce", "broadcast", "send", "recv", "barrier", "all_gather",
+                   "all_gather_object", "reduce_scatter")
+
+    def __init__(self, d, beat):
+        self._d = d
+        self._beat = beat
+
+    def __getattr__(self, name):
+        f = getattr(self._d, name)
+        if name not in self.COLLECTIVES or not callable(f):
+            return f
+        beat = self._beat
+
+        def call(*args, **kw):
+            beat.n += 1
+            beat("%s #%d" % (name, beat.n), echo=False)
+            return f(*args, **kw)
+        return call
+
+
+def read_heartbeats(paths):
+    """{rank: (seconds since the beat, stage)} from the ranks' heartbeat files."""
+    now = time.time()
+    out = {}
+    for r, p in enumerate(paths):
+        try:
+            with open(p) as f:
+                t, _, stage = f.read().strip().partition(" ")
+            out[r] = (now - float(t), stage)
+        except (OSError, ValueError):
+            out[r] = (None, "no heartbeat yet")
+    return out
+
+
 def _free_port():
     import socket
     s = socket.socket()
@@ -971,12 +1047,16 @@ def launch(a, argv):
             log("--gpus %d needs %d visible GPU(s), found %d (one process per GPU; "
                 "--share-gpu runs parity ranks on one GPU)" % (N, need, have))
             return 2
+    import shutil
+    import tempfile
     port = os.environ.get("MASTER_PORT") or str(_free_port())
+    hb_dir = tempfile.mkdtemp(prefix="tmh_bench_hb_")
+    hb = [os.path.join(hb_dir, "rank%d" % r) for r in range(N)]
     procs = []
     for r in range(N):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(0 if a.share_gpu else r),
                    WORLD_SIZE=str(N), LOCAL_WORLD_SIZE=str(N), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=port, TMH_BENCH_LAUNCHED="1")
+                   MASTER_PORT=port, TMH_BENCH_LAUNCHED="1", TMH_BENCH_HEARTBEAT=hb[r])
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
                                       start_new_session=True))
@@ -986,16 +1066,36 @@ def launch(a, argv):
     reader.start()  # rank 0's stdout, while the ranks are watched below
     rcs = [None] * N
     failed = None  # exit code of the first rank seen failing (the cause)
+    why = None
+    t_start = time.time()
     while any(rc is None for rc in rcs):
         for r, pr in enumerate(procs):
             if rcs[r] is None:
                 rcs[r] = pr.poll()
                 if rcs[r] not in (None, 0) and failed is None:
                     failed = rcs[r]
+                    why = "rank %d exited with %d" % (r, rcs[r])
         if failed is not None:
             break
+        now = time.time()
+        if now - t_start > a.deadline:
+            failed, why = 3, "deadline of %.0f s passed" % a.deadline
+            break
+        beats = read_heartbeats(hb)
+        ages = [b[0] for b in beats.values() if b[0] is not None]
+        newest = min(ages) if ages else now - t_start
+        if newest > a.stall_timeout:  # no rank has moved: every one is stuck
+            failed, why = 3, "no rank made progress for %.0f s" % newest
+            break
         time.sleep(0.2)
-    if failed is not None:  # a rank died: the others would wait forever in a collective
+    if failed is not None:  # a rank died or hangs: the others would wait forever in a collective
+        beats = read_heartbeats(hb)
+        log("launcher: %s; killing the ranks.  Last stage of each rank:" % why)
+        for r in range(N):
+            age, stage = beats[r]
+            state = "running" if procs[r].poll() is None else "exited %s" % procs[r].poll()
+            log("  rank %d (%s): %s%s" % (r, state, stage,
+                                         "" if age is None else " (%.1f s ago)" % age))
         for r, pr in enumerate(procs):
             if pr.poll() is None:
                 os.killpg(pr.pid, signal.SIGTERM)
@@ -1006,7 +1106,9 @@ def launch(a, argv):
                 os.killpg(pr.pid, signal.SIGKILL)
                 rcs[r] = pr.wait()
         log("rank exit codes: %s" % rcs)
+        shutil.rmtree(hb_dir, ignore_errors=True)
         return failed if 0 < failed < 256 else 1
+    shutil.rmtree(hb_dir, ignore_errors=True)
     reader.join(timeout=30)
     out0 = buf[0].decode(errors="replace") if buf else ""
     lines = [ln for ln in out0.splitlines() if ln.strip().startswith("{")]
@@ -1017,16 +1119,35 @@ def launch(a, argv):
     return 0
 
 
-def dry_run(world, rank):
-    """--dry-run rank body: a gloo group and the ranks' launch environment."""
+def dry_run(world, rank, a):
+    """--dry-run rank body: a gloo group, one all_reduce, and the ranks' launch
+    environment.  Launcher tests: TMH_BENCH_DRY_FAIL_RANK=r makes rank r die,
+    TMH_BENCH_DRY_STALL_RANK=r makes rank r hang before the all_reduce (the
+    others then wait inside it)."""
+    import datetime
+
+    import torch
     import torch.distributed as dist
+    beat = Heartbeat(rank)
     keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
     if os.environ.get("TMH_BENCH_DRY_FAIL_RANK") == str(rank):  # launcher test: a rank dies
         sys.exit(3)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    beat("init_process_group")
+    if world == 1:  # a lone rank needs no launcher's rendezvous address
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=a.coll_timeout))
+    D = BeatingDist(dist, beat)
+    if os.environ.get("TMH_BENCH_DRY_STALL_RANK") == str(rank):
+        beat("stalled on purpose (launcher test)")
+        time.sleep(3600)
+    t = torch.ones(1)
+    D.all_reduce(t)
     envs = [None] * world
-    dist.all_gather_object(envs, {k: os.environ.get(k) for k in keys})
+    D.all_gather_object(envs, {k: os.environ.get(k) for k in keys})
     ws = dist.get_world_size()
+    beat("done")
     dist.destroy_process_group()
     if rank == 0:
         return {"dry_run": True, "n_gpus": world, "world_size": ws, "ranks": envs}
@@ -1043,7 +1164,7 @@ def main():
         sys.exit(launch(a, sys.argv[1:]))
     out = claim_stdout()
     if a.dry_run:
-        r = dry_run(int(env_world or 1), int(os.environ.get("RANK", "0")))
+        r = dry_run(int(env_world or 1), int(os.environ.get("RANK", "0")), a)
         if r is not None:
             print(json.dumps(r), file=out, flush=True)
         return
@@ -1091,13 +1212,18 @@ def main():
     dist_on = world > 1 or os.environ.get("TMH_BENCH_FORCE_DIST") == "1"
     D = dist  # the collectives' module: RCCL, or gloo staged through host memory
     staged = a.share_gpu and world > 1
+    beat = Heartbeat(rank)
     if dist_on:
+        import datetime
+        tmo = datetime.timedelta(seconds=a.coll_timeout)
+        beat("init_process_group")
         if staged:  # parity runs: N ranks on one GPU (RCCL needs a GPU per rank)
             from tmlibrary_amd.workflow.corilla.sharded import HostStagedDist
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
             D = HostStagedDist(dist)
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
+        D = BeatingDist(D, beat)
     coll_world = dist.get_world_size() if dist_on else 1
     sharded = a.layout == "sharded" or (a.layout == "auto" and world > 1)
     CH = a.channels if a.channels else (4 if sharded else 1)
@@ -1115,6 +1241,7 @@ def main():
     same = None
     if sharded and world > 1 and not a.no_same_workload and not staged:
         if rank == 0:  # before this run's buffers exist: the GPU's whole HBM is free
+            beat("single-GPU run of the same workload")
             log("rank 0: the same %d-channel workload on this GPU alone" % CH)
             same = single_gpu_same_workload(L, dev, H, W, CH, S_total,
                                             DISTRIBUTIONS[a.distribution])
@@ -1293,6 +1420,7 @@ def main():
     jobs = {"k": 0, "applied": None, "welford": None}
 
     log("%d channel(s) x %d sites resident; warm-up" % (CH, S))
+    beat("warm-up")
 
     timing = {"on": False}
 
@@ -1333,8 +1461,10 @@ def main():
                     if timing["on"]:
                         ch.merge_ev.append(evs[id(ch)] + [e2, ch.event()])
 
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
+        beat.step = " (warm-up step %d)" % i
         step()
+    beat("synchronize after warm-up")
     torch.cuda.synchronize(dev)
 
     log("timing %d steps" % a.steps)
@@ -1346,12 +1476,16 @@ def main():
         D.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
+        beat.step = " (timed step %d)" % i
         step()
+    beat.step = ""
+    beat("synchronize after the timed steps", echo=False)
     torch.cuda.synchronize(dev)
     if dist_on:
         D.barrier()
     elapsed = time.perf_counter() - t0
+    beat("timed steps done: checks and report")
     if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         D.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -66,3 +66,39 @@ def test_gpus_must_match_world_size():
     r = _run(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0"})
     assert r.returncode == 2
     assert "disagrees with WORLD_SIZE=2" in r.stderr
+
+
+def test_launcher_stalled_collective_fails_loudly():
+    """every rank stuck (rank 1 hangs before an all_reduce,
+    rank 0 waits inside it) must not hang the run.  With no heartbeat from any
+    rank for --stall-timeout seconds the launcher kills the ranks' process
+    groups and exits 3, naming each rank's last stage -- the reference's
+    failed job exits non-zero with its cause (tmlib/workflow/cli.py:287-293)."""
+    import time
+    t0 = time.time()
+    r = _run(["--gpus", "2", "--dry-run", "--stall-timeout", "8", "--deadline", "120"],
+             {"TMH_BENCH_DRY_STALL_RANK": "1"}, timeout=170)
+    took = time.time() - t0
+    assert r.returncode == 3, (r.returncode, r.stderr[-3000:])
+    assert r.stdout.strip() == ""
+    assert "no rank made progress" in r.stderr, r.stderr[-3000:]
+    assert "rank 0 (running): all_reduce #1" in r.stderr, r.stderr[-3000:]
+    assert "rank 1 (running): stalled on purpose" in r.stderr, r.stderr[-3000:]
+    assert took < 150
+
+
+def test_launcher_deadline():
+    r = _run(["--gpus", "2", "--dry-run", "--stall-timeout", "600", "--deadline", "6"],
+             {"TMH_BENCH_DRY_STALL_RANK": "1"}, timeout=170)
+    assert r.returncode == 3, (r.returncode, r.stderr[-3000:])
+    assert "deadline of 6 s passed" in r.stderr, r.stderr[-3000:]
+    assert "rank 1 (running)" in r.stderr
+
+
+def test_one_rank_output_unchanged():
+    """--gpus 1 (and no WORLD_SIZE): no launcher, no heartbeat lines."""
+    r = _run(["--gpus", "1", "--dry-run"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    assert d["world_size"] == 1
+    assert "[rank" not in r.stderr

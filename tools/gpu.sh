@@ -31,7 +31,9 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 O=gpurun_out
 QB="bench.py --steps 10 --warmup 3 --cpu-sample 0 --no-extras ${BENCH_ARGS:-}"
-SB="bench.py --steps 5 --warmup 2 --cpu-sample 0 --no-extras --no-profile ${BENCH_ARGS:-}"
+# (the profiled bench keeps its own event timing: its line and the rocprof
+# summary then describe the same process)
+SB="bench.py --steps 5 --warmup 2 --cpu-sample 0 --no-extras ${BENCH_ARGS:-}"
 
 summ() {  # one-line summary of a bench JSON line
   python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.strip()][-1]); r=d.get('roofline') or {}; print(sys.argv[1], d['value'], d['ms_per_step'], d.get('check_vs_oracle'), r.get('frac'), {k: v['avg_ms'] for k, v in d.get('kernels', {}).items()})" "$1"
@@ -90,7 +92,8 @@ for step in "$@"; do
     prof)
       D=${a1:-synthetic}
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rocprof_${D}_$TAG -o run \
-        -- python3 $SB --distribution $D > $O/rocprof_${D}_$TAG.log 2>&1 || exit $?
+        -- python3 $SB --distribution $D > $O/rocprof_${D}_$TAG.json 2> $O/rocprof_${D}_$TAG.log || exit $?
+      summ $O/rocprof_${D}_$TAG.json
       ;;
     pmc)
       D=${a1:-synthetic}
