@@ -1644,7 +1644,11 @@ def main():
                 d["alg_GBs"] = round(gbs, 1)
                 d["frac_of_8TBs"] = round(gbs / HBM_PEAK_GBS, 4)
             kdetail[name] = d
-        dominant = max((n for n in kern if n in alg), key=lambda n: kern[n][0], default=None)
+        # the roofline's kernel: the one moving the most algorithmic bytes (the
+        # fused correct + histogram pass, 4 of the job's 6 B/px).  (By time, a
+        # Welford pass co-running with another job's kernels could be picked
+        # on bright data, where both passes stretch.)
+        dominant = max((n for n in kern if n in alg), key=lambda n: alg[n], default=None)
         roofline = None
         if dominant:
             avg_ms = kern[dominant][0]
@@ -1673,8 +1677,10 @@ def main():
                         "timed": "HIP events around the launch of the one configuration the job "
                                  "runs, on its stream (tmh_profile_*)"}
             if J > 1:
-                roofline["note"] = ("%d jobs in flight: this pass shares HBM with the next job's "
-                                    "Welford pass, so its launches last longer than alone"
+                roofline["note"] = ("%d jobs in flight: the pass holds every CU (persistent "
+                                    "grid), so the next job's Welford pass runs after it; "
+                                    "this job's histogram tail runs under that Welford pass "
+                                    "(profiles/r5/trace_jobs_synthetic_r5a.txt)"
                                     % J) if a.jobs_order == "welford" else (
                                     "%d jobs in flight (the next job's Welford pass after this "
                                     "pass)" % J)

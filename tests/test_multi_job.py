@@ -221,3 +221,67 @@ def test_single_rank_rccl_merge_path(tmp_path):
                        timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "rccl merge ok" in r.stdout
+
+
+def _gpu_decode_worker(rank, world, port, root):
+    """One rank of the sharded job on GPU 0 (ranks share it): its shard
+    through the GPU inflate into GpuChannelStats, merged over gloo with
+    host-staged device buffers."""
+    import sys
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import torch
+    from tmlibrary_amd.models.file import ExperimentStore
+    from tmlibrary_amd.workflow.corilla.multi import GpuChannelStats, run_channels_sharded
+    from tmlibrary_amd.workflow.corilla.sharded import HostStagedDist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    store = ExperimentStore(root)
+    rec = Recorder(lambda d: GpuChannelStats(d, world, device=dev, batch_size=3))
+    tm = {}
+    res = run_channels_sharded(store, _batches(), dist=HostStagedDist(dist), stats_factory=rec,
+                               block=3, device=dev, decode="gpu", device_block=2, timing=tm)
+    keys = orc.percentile_keys(3).tolist()
+    np.savez(os.path.join(root, "g%d.npz" % rank),
+             **{"mean%d" % ch: c.mean.array for ch, c in res.items()},
+             **{"std%d" % ch: c.std.array for ch, c in res.items()},
+             **{"pct%d" % ch: np.array([c.percentiles[k] for k in keys]) for ch, c in res.items()},
+             **{"hist%d" % ch: np.asarray(st.histogram, np.uint64)
+                for ch, st in zip(CHANNELS, rec.made)},
+             **{"gpu%d" % ch: np.array([t["sites"], t["gpu_decoded"]]) for ch, t in tm.items()})
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_job_gpu_decode_two_ranks(tmp_path):
+    """two ranks sharing GPU 0, each decoding its
+    contiguous shard of the reference-layout gzip files with the GPU inflate
+    and updating on the device, merged (gloo, host-staged) -- equal to the
+    single-process job with host decode: percentiles and pooled histograms
+    bit-exact, mean/std within 1e-6 (tmlib/workflow/corilla/api.py:131-136,
+    stats.py:64-121)."""
+    from test_distributed_gloo import _free_port
+    from tmlibrary_amd.workflow.corilla.multi import GpuChannelStats, run_channels_sharded
+    store, sites = _make_store(str(tmp_path))
+    rec = Recorder(lambda d: GpuChannelStats(d, 1, batch_size=3))
+    ref = run_channels_sharded(store, _batches(), dist=None, stats_factory=rec, block=3,
+                               decode="host")
+    keys = orc.percentile_keys(3).tolist()
+    world = 2
+    mp.start_processes(_gpu_decode_worker, args=(world, _free_port(), str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    for ch, ids in CHANNELS.items():
+        want_pct = np.array([ref[ch].percentiles[k] for k in keys])
+        want_hist = np.asarray(rec.made[list(CHANNELS).index(ch)].histogram, np.uint64)
+        for r in range(world):
+            z = np.load(tmp_path / ("g%d.npz" % r))
+            n_sites, n_gpu = z["gpu%d" % ch]
+            assert n_gpu == n_sites > 0, "rank %d: every site of its shard through the GPU" % r
+            assert np.array_equal(z["pct%d" % ch], want_pct)
+            assert np.array_equal(z["hist%d" % ch], want_hist)
+            assert np.allclose(z["mean%d" % ch], ref[ch].mean.array, rtol=1e-6, atol=1e-12)
+            assert np.allclose(z["std%d" % ch], ref[ch].std.array, rtol=1e-6, atol=1e-12)
+    _check(ref, sites)

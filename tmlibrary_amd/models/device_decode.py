@@ -183,3 +183,92 @@ class DeviceChunkDecoder(object):
             if slot.get("event") is not None:
                 slot["event"].synchronize()
                 self._raise_failed(slot)
+
+
+class DeviceSiteFeeder(object):
+    """A run of channel image files into a statistics object through the GPU
+    inflate, in file order (the corilla job's input path, SURVEY.md §8(f)
+    rank 1; reference: tmlib/workflow/corilla/api.py:131-136 reads and
+    updates site by site).
+
+    Two device site buffers of ``block`` sites: block k+1's host chunk read
+    and H2D copy overlap block k's inflate (decoder stream) and statistics
+    update (statistics stream S, ``stats.update_device``); a buffer is reused
+    once S has read it.  Buffers, decoder and streams are kept across calls
+    (one feeder per job runner).  ``feed`` returns how many of the files (a
+    prefix) went into ``stats``: with ``strict`` False a block the GPU path
+    cannot read (``RawChunksUnsupported``, raised before anything of the block
+    is queued) ends the GPU run there and the caller decodes the rest on the
+    host -- every site counted once, in order."""
+
+    def __init__(self, device=None, block=64, n_threads=None):
+        import torch
+        self.torch = torch
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.block = max(1, int(block))
+        self.n_threads = n_threads
+        self._key = None
+        self.dec = None
+        self.last_zero_counts = None
+
+    def _ensure(self, H, W):
+        torch = self.torch
+        if self._key != (H, W):
+            B = self.block
+            self.bufs = [torch.empty((B, H, W), dtype=torch.int16, device=self.device)
+                         for _ in range(2)]
+            self.dec = DeviceChunkDecoder(device=self.device, slots=2, n_threads=self.n_threads)
+            self.S = torch.cuda.Stream(self.device)
+            self._key = (H, W)
+
+    def feed(self, paths, stats, strict=False, on_block=None):
+        """``stats``: has ``image_dimensions`` and ``update_device(ptr, n,
+        stream=, zero_counts=)``.  ``on_block(k, n)`` (optional) is called as
+        files [k, k + n) are queued (the caller's per-site logging)."""
+        torch = self.torch
+        from tmlibrary_amd.models.file import channel_image_shape
+        from tmlibrary_amd.workflow.corilla.stats import log_zero_warnings
+        if not paths:
+            return 0
+        H, W, dt = channel_image_shape(paths[0])
+        if np.dtype(dt) != np.uint16 or (H, W) != tuple(stats.image_dimensions):
+            if strict:
+                raise RawChunksUnsupported("GPU decode takes uint16 sites of the job's shape")
+            return 0
+        self._ensure(H, W)
+        dec, S, bufs, B = self.dec, self.S, self.bufs, self.block
+        zc = torch.zeros(len(paths), dtype=torch.int64, pin_memory=True).numpy()
+        used = [None, None]
+        done, ok = 0, False
+        try:
+            for k in range(0, len(paths), B):
+                b = (k // B) % 2
+                if used[b] is not None:
+                    dec.stream.wait_event(used[b])  # S has read the buffer's previous block
+                blk = paths[k:k + B]
+                try:
+                    dec.decode(blk, bufs[b].data_ptr(), expect=(H, W, 2))
+                except RawChunksUnsupported:
+                    if strict:
+                        raise
+                    break
+                ready = torch.cuda.Event()
+                ready.record(dec.stream)
+                S.wait_event(ready)
+                if on_block is not None:
+                    on_block(k, len(blk))
+                stats.update_device(bufs[b].data_ptr(), len(blk), stream=S.cuda_stream,
+                                    zero_counts=zc[k:k + len(blk)])
+                used[b] = torch.cuda.Event()
+                used[b].record(S)
+                done = k + len(blk)
+            S.synchronize()
+            dec.check()  # a chunk that failed to inflate raises here
+            ok = True
+        finally:
+            if not ok:  # aborted: nothing of this run may surface in a later one
+                S.synchronize()
+                dec.reset()
+        log_zero_warnings(zc[:done])
+        self.last_zero_counts = zc[:done]
+        return done

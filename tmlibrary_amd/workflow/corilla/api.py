@@ -84,7 +84,7 @@ class IllumstatsCalculator(object):
             raise ValueError('decode must be "auto", "gpu" or "host"')
         self.decode = decode
         self.device_block = max(1, int(device_block))
-        self._dev = None  # device decode state, kept across jobs (buffers, decoder)
+        self._dev = None  # DeviceSiteFeeder, kept across jobs (buffers, decoder, streams)
         self.last_timing = None  # the last run_job's phases (seconds)
 
     def create_run_batches(self, args=None, channel_files=None, channel_names=None, seed=None):
@@ -202,10 +202,9 @@ class IllumstatsCalculator(object):
                 self._buffers.setdefault(key, []).append(bufs)
 
     def _update_device(self, file_ids, stats):
-        """The job's sites through the GPU inflate into the statistics, in order:
-        block k+1's host chunk read and H2D copy overlap block k's inflate and
-        statistics update (decoder stream D, statistics stream S; two device
-        site buffers, each reused once S has consumed it).
+        """The job's sites through the GPU inflate into the statistics, in order
+        (models/device_decode.py DeviceSiteFeeder: block k+1's host chunk read
+        and H2D copy overlap block k's inflate and statistics update).
 
         Returns how many of ``file_ids`` (a prefix) went into ``stats``.  With
         decode="auto" a block the GPU path cannot read (another layout or
@@ -213,62 +212,19 @@ class IllumstatsCalculator(object):
         block is queued) ends the GPU path there, and the caller continues on
         the host from the first file not taken -- every site is counted once,
         in the job's order."""
-        import torch
-
-        from tmlibrary_amd.models.device_decode import DeviceChunkDecoder
-        from tmlibrary_amd.workflow.corilla.stats import log_zero_warnings
-        strict = self.decode == "gpu"
+        from tmlibrary_amd.models.device_decode import DeviceSiteFeeder
         paths = [self.store.channel_image_file(f).location for f in file_ids]
-        H, W, dt = channel_image_shape(paths[0])
-        if np.dtype(dt) != np.uint16 or (H, W) != tuple(stats.image_dimensions):
-            if strict:
-                raise RawChunksUnsupported("GPU decode takes uint16 sites of the job's shape")
-            return 0
-        B = self.device_block
-        dev = torch.device("cuda", torch.cuda.current_device())
-        st = self._dev
-        if st is None or st["key"] != (B, H, W):
-            st = self._dev = {
-                "key": (B, H, W),
-                "bufs": [torch.empty((B, H, W), dtype=torch.int16, device=dev) for _ in range(2)],
-                "dec": DeviceChunkDecoder(device=dev, slots=2, n_threads=self.decode_threads),
-                "S": torch.cuda.Stream(dev)}
-        dec, S, bufs = st["dec"], st["S"], st["bufs"]
-        zc = torch.zeros(len(file_ids), dtype=torch.int64, pin_memory=True).numpy()
-        used = [None, None]
-        done, ok = 0, False
-        try:
-            for k in range(0, len(file_ids), B):
-                b = (k // B) % 2
-                if used[b] is not None:
-                    dec.stream.wait_event(used[b])  # S has read the buffer's previous block
-                blk = paths[k:k + B]
-                try:
-                    dec.decode(blk, bufs[b].data_ptr(), expect=(H, W, 2))
-                except RawChunksUnsupported:
-                    if strict:
-                        raise
-                    logger.info("channel image files from %d on not GPU-decodable: decoding "
-                                "the rest on the host", k)
-                    break
-                ready = torch.cuda.Event()
-                ready.record(dec.stream)
-                S.wait_event(ready)
-                for fid in file_ids[k:k + B]:
-                    logger.info("update statistics for image: %d", fid)
-                stats.update_device(bufs[b].data_ptr(), len(blk), stream=S.cuda_stream,
-                                    zero_counts=zc[k:k + len(blk)])
-                used[b] = torch.cuda.Event()
-                used[b].record(S)
-                done = k + len(blk)
-            S.synchronize()
-            dec.check()  # a chunk that failed to inflate raises here
-            ok = True
-        finally:
-            if not ok:  # aborted: nothing of this job may surface in a later one
-                S.synchronize()
-                dec.reset()
-        log_zero_warnings(zc[:done])
+        if self._dev is None:
+            self._dev = DeviceSiteFeeder(block=self.device_block, n_threads=self.decode_threads)
+
+        def on_block(k, n):
+            for fid in file_ids[k:k + n]:
+                logger.info("update statistics for image: %d", fid)
+
+        done = self._dev.feed(paths, stats, strict=self.decode == "gpu", on_block=on_block)
+        if done < len(file_ids):
+            logger.info("channel image files from %d on not GPU-decodable: decoding the rest "
+                        "on the host", done)
         return done
 
     def run_job(self, batch, assume_clean_state=False):
@@ -287,8 +243,6 @@ class IllumstatsCalculator(object):
             start = 0  # files already in the statistics (GPU path)
             if self.decode != "host":
                 start = self._update_device(file_ids, stats)
-                if start < len(file_ids):
-                    logger.info("channel image files not GPU-decodable: decoding on the host")
             if start < len(file_ids):
                 for ids, sites in self._blocks(file_ids[start:]):
                     for fid in ids:

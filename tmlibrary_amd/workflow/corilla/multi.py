@@ -10,8 +10,12 @@ channel:
 1. takes the contiguous block ``shard_bounds(n, world, rank)`` of the batch's
    file list -- the list itself is the recorded site order, so the merged
    result is the reference's sequential result over that order;
-2. decodes its block with the parallel inflate reader and accumulates it
-   (``update_batch``);
+2. decodes its block and accumulates it: with ``decode`` "auto" (default)
+   or "gpu" the rank's compressed chunks are read by the host, inflated on
+   the rank's own GPU and fed to the statistics in place
+   (models/device_decode.py ``DeviceSiteFeeder``, as ``run_job``), with
+   "host" (or files the GPU path cannot read, from the first such file on)
+   by the parallel host inflate reader (``update_batch``);
 3. merges the partial statistics (Welford all-reduce, ordered percentile
    chain, histogram all-reduce: ``sharded.merge_shards``), so every rank
    holds identical results (``stats.histogram``: the channel's pooled counts);
@@ -28,7 +32,8 @@ import logging
 import numpy as np
 
 from tmlibrary_amd.image import IllumstatsContainer
-from tmlibrary_amd.models.file import read_channel_images
+from tmlibrary_amd.models.file import (RawChunksUnsupported, channel_image_shape,
+                                       read_channel_images)
 from tmlibrary_amd.workflow.corilla.sharded import merge_shards, shard_bounds
 
 logger = logging.getLogger(__name__)
@@ -49,8 +54,16 @@ class GpuChannelStats(object):
         self.world = world
         self.device = device
 
+    @property
+    def image_dimensions(self):
+        return self.st.image_dimensions
+
     def update_batch(self, sites):
         self.st.update_batch(sites)
+
+    def update_device(self, dev_sites, n_sites, stream=None, zero_counts=None):
+        """Device-resident sites (the GPU inflate's output), in order."""
+        self.st.update_device(dev_sites, n_sites, stream=stream, zero_counts=zero_counts)
 
     def merge(self, dist, group=None):
         if not self.merging or dist is None:
@@ -79,34 +92,63 @@ class GpuChannelStats(object):
 
 
 def run_channels_sharded(store, batches, dist=None, group=None, stats_factory=None,
-                         block=32, decode_threads=None, device=None):
+                         block=32, decode_threads=None, device=None, decode="auto",
+                         device_block=64, timing=None):
     """Run every channel batch as one sharded job; returns {channel_id:
     IllumstatsContainer} (identical on every rank).  ``dist`` is
-    torch.distributed (or None for one process)."""
+    torch.distributed (or None for one process).  ``decode``: "auto" / "gpu"
+    (GPU inflate of the rank's shard, ``device_block`` files per device
+    block; "gpu" raises ``RawChunksUnsupported`` for files it cannot read)
+    or "host".  The GPU path needs statistics with ``update_device`` (the
+    default GpuChannelStats); others decode on the host.  ``timing`` (a
+    dict, optional) receives per channel the seconds of the rank's
+    input + update phase and of the merge."""
+    import time
+    if decode not in ("auto", "gpu", "host"):
+        raise ValueError('decode must be "auto", "gpu" or "host"')
     world = dist.get_world_size(group) if dist is not None else 1
     rank = dist.get_rank(group) if dist is not None else 0
     if stats_factory is None:
         def stats_factory(dims):
             return GpuChannelStats(dims, world, device=device, batch_size=block)
+    feeder = None
     results = {}
     for batch in batches:
         ids = [f[0] if isinstance(f, (list, tuple)) else f
                for f in batch["channel_image_files_ids"]]
         paths = [store.channel_image_file(i).location for i in ids]
-        first = read_channel_images(paths[:1], 1)
-        dims = first.shape[1:]
+        H, W, _ = channel_image_shape(paths[0])  # the dataset's shape: no decode needed
+        dims = (H, W)
         a, b = shard_bounds(len(paths), world, rank)
         logger.info("channel %s: rank %d of %d takes sites [%d, %d) of %d",
                     batch["channel_id"], rank, world, a, b, len(paths))
         stats = stats_factory(dims)
+        t0 = time.perf_counter()
         try:
-            for i in range(a, b, block):
+            start = a
+            if decode != "host" and b > a and hasattr(stats, "update_device"):
+                if feeder is None:
+                    from tmlibrary_amd.models.device_decode import DeviceSiteFeeder
+                    feeder = DeviceSiteFeeder(device=device, block=device_block,
+                                              n_threads=decode_threads)
+                start = a + feeder.feed(paths[a:b], stats, strict=decode == "gpu")
+                if start < b:
+                    logger.info("channel %s: files from %d on decoded on the host",
+                                batch["channel_id"], start)
+            elif decode == "gpu":
+                raise RawChunksUnsupported("decode='gpu' needs statistics with update_device")
+            for i in range(start, b, block):
                 sites = read_channel_images(paths[i:min(b, i + block)], decode_threads)
                 if sites.dtype == np.uint8:
                     sites = sites.astype(np.uint16)
                 stats.update_batch(sites)
+            t1 = time.perf_counter()
             stats.merge(dist, group)
             cont = stats.container()
+            if timing is not None:
+                timing[batch["channel_id"]] = {"sites": b - a, "gpu_decoded": start - a,
+                                               "input_update_s": t1 - t0,
+                                               "merge_s": time.perf_counter() - t1}
         finally:
             stats.close()
         if rank == 0:

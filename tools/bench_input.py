@@ -130,6 +130,25 @@ def main():
                 else:
                     d = np.abs(x.astype(np.float64) - y) / np.maximum(np.abs(x.astype(np.float64)), 1e-30)
                     cmp[str(i)] = float(d.max())
+            # the sharded multi-channel job (workflow/corilla/multi.py) on one
+            # rank: its shard through the GPU inflate vs the host reader
+            from tmlibrary_amd.workflow.corilla.multi import run_channels_sharded
+            ids = [[i] for i in range(a.sites)] * a.repeat
+            for dec in ("host", "auto"):
+                tm = {}
+                run_channels_sharded(store, [{"id": 1, "channel_id": 1,
+                                              "channel_image_files_ids": ids[:a.sites]}],
+                                     decode=dec, decode_threads=a.threads,
+                                     device_block=a.device_block)  # warm-up
+                run_channels_sharded(store, [{"id": 1, "channel_id": 1,
+                                              "channel_image_files_ids": ids}],
+                                     decode=dec, decode_threads=a.threads,
+                                     device_block=a.device_block, timing=tm)
+                t = tm[1]
+                res["sharded_job_%s_decode" % ("gpu" if dec == "auto" else "host")] = {
+                    "sites": t["sites"], "gpu_decoded": t["gpu_decoded"],
+                    "input_update_sites_per_s": round(t["sites"] / t["input_update_s"], 1),
+                    "merge_s": round(t["merge_s"], 4)}
             res["gpu_vs_host_decode_stats"] = cmp
             res["gpu_decode_same_results"] = bool(all(v == "equal" or v <= 1e-6 for v in cmp.values()))
         res["cpus_visible"] = os.cpu_count()
