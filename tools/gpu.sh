@@ -17,6 +17,10 @@
 #   repeat:N       N more quick bench processes (bench_repeat_TAG.jsonl)
 #   dist432        one rank, forced-distributed, 4 channels x 432 sites: each
 #                  GPU's share of configs[2] at N = 8 (dist432_TAG.json)
+#   pytest:EXPR    the GPU tests selected by -k EXPR (gpu_tests_k_TAG.log)
+#   input[:N]      tools/bench_input.py on N full-size gzip files (host and GPU
+#                  decode, run_job, the sharded job) -> bench_input_TAG.json
+#   prof432        rocprofv3 kernel trace of dist432 -> rocprof_dist432_TAG/
 #   prof:DIST      rocprofv3 --kernel-trace --stats of a short bench on DIST
 #                  (synthetic | bright) -> rocprof_DIST_TAG/
 #   pmc:DIST       FETCH_SIZE and WRITE_SIZE passes (each its own run) of a
@@ -88,6 +92,26 @@ for step in "$@"; do
         timeout -k 10 300 python bench.py --layout sharded --channels 4 --sites 432 --steps 10 \
         --warmup 3 --no-extras --cpu-sample 0 ${BENCH_ARGS:-} > $O/dist432_$TAG.json 2> $O/dist432_$TAG.err || exit $?
       summ $O/dist432_$TAG.json
+      ;;
+    prof432)
+      TMH_BENCH_FORCE_DIST=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rocprof_dist432_$TAG -o run \
+        -- python3 bench.py --layout sharded --channels 4 --sites 432 --steps 5 --warmup 2 \
+        --no-extras --cpu-sample 0 ${BENCH_ARGS:-} > $O/rocprof_dist432_$TAG.json 2> $O/rocprof_dist432_$TAG.log || exit $?
+      summ $O/rocprof_dist432_$TAG.json
+      ;;
+    input)
+      timeout -k 10 600 python tools/bench_input.py --sites ${a1:-256} --threads 16 --repeat 4 \
+        > $O/bench_input_$TAG.json 2> $O/bench_input_$TAG.err || exit $?
+      tail -c 1500 $O/bench_input_$TAG.json
+      ;;
+    pytest)
+      # a subset of the GPU tests: pytest:EXPR (-k expression)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v -ra --timeout 300 --timeout-method thread \
+        -k "$a1" > $O/gpu_tests_k_$TAG.log 2>&1
+      rc=$?
+      grep -E "passed|failed" $O/gpu_tests_k_$TAG.log | tail -3
+      if [ $rc -ne 0 ]; then exit $rc; fi
       ;;
     prof)
       D=${a1:-synthetic}
