@@ -78,8 +78,13 @@ class GpuChannelStats(object):
         dev = self.device if self.device is not None else torch.device("cuda",
                                                                          torch.cuda.current_device())
         ops = StatsOps(hip.lib(), st._h, h * w, len(st._q), dev)
-        n_total = merge_shards(ops, dist, group, int_device=dev)
-        torch.cuda.current_stream(dev).synchronize()
+        # one created stream for the merge's launches, copies and collectives
+        # (sharded.StatsOps: the default stream does not order against them)
+        ms = torch.cuda.Stream(dev)
+        ms.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(ms):
+            n_total = merge_shards(ops, dist, group, int_device=dev)
+        ms.synchronize()
         st.refresh()  # the handle holds the whole channel's merged state (n = n_total)
         self.histogram = st.histogram  # pooled over every rank's sites
         return n_total

@@ -45,7 +45,16 @@ class StatsOps(object):
         self.device = device
 
     def _stream(self):
-        return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+        # torch's collectives and copies and these launches must share one
+        # ordered stream: the default (null) stream cannot be named through
+        # the C-ABI (NULL there means the handle's own stream, which does not
+        # synchronise with it), so the merge must run under a created stream
+        h = self.torch.cuda.current_stream(self.device).cuda_stream
+        if not h:
+            raise RuntimeError("StatsOps: run the merge under a non-default torch stream "
+                               "(with torch.cuda.stream(...)): the default stream does not "
+                               "order against the statistics handle's stream")
+        return C.c_void_p(h)
 
     def _chk(self, rc):
         from tmlibrary_amd import hip
