@@ -134,6 +134,13 @@ def parse():
                         "(sharing HBM with job k's corrected pass, hiding job k's small kernels "
                         "and tail) or after job k's corrected pass (hiding only the tail); a "
                         "third, pipelined order measured no better (DESIGN.md 9.5)")
+    p.add_argument("--planes", choices=["multi", "per-job"], default="multi",
+                   help="finalize -> smoothing -> coefficients: every channel's in one launch per "
+                        "kernel (tmh_job_planes_multi_device) or per channel (finalize, "
+                        "smooth2, corrector update)")
+    p.add_argument("--merge", choices=["batched", "per-channel"], default="batched",
+                   help="N > 1 / forced distributed: the channels' merges with one collective per "
+                        "quantity for all channels (sharded.merge_*_multi) or per channel")
     p.add_argument("--channel-streams", choices=["per-channel", "one"], default="per-channel",
                    help="several channels: each on its own stream (its merges overlap the "
                         "others' kernels), or all on one stream")
@@ -1202,8 +1209,9 @@ def main():
     from tmlibrary_amd.image import ZERO_LOG10
     from tmlibrary_amd.synth import DISTRIBUTIONS
     from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
-    from tmlibrary_amd.workflow.corilla.sharded import (StatsOps, merge_counts, merge_welford,
-                                                         shard_bounds)
+    from tmlibrary_amd.workflow.corilla.sharded import (StatsOps, merge_counts,
+                                                         merge_counts_multi, merge_welford,
+                                                         merge_welford_multi, shard_bounds)
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -1371,8 +1379,17 @@ def main():
             self.ops = StatsOps(L, self.h, npx, Q, dev)
             self.merge_ev = []  # (welford start, end, counts start, end) per timed step
 
-        def stats(self):
+        def reset_probe(self):
+            """The job's reset, and its site probe queued at once (no wait):
+            with several channels every probe is in flight before any
+            channel's Welford launch waits for its own."""
             hip.check(L.tmh_stats_reset(self.h))
+            if fused and B and not in_contig:
+                hip.check(L.tmh_stats_probe_blocks_device(self.h, self.T_in, shift, S, self.sp))
+            else:
+                hip.check(L.tmh_stats_probe_device(self.h, self.S_ptr, S, self.sp))
+
+        def welford(self):
             if fused and B and not in_contig:  # Welford pass; histograms from the correction's read
                 hip.check(L.tmh_stats_update_welford_blocks_device(self.h, self.T_in, shift, S, 1,
                                                                    self.sp))
@@ -1381,14 +1398,28 @@ def main():
             else:
                 hip.check(L.tmh_stats_update_device(self.h, self.S_ptr, S, 1, self.sp))
 
-        def apply(self):
+        def stats(self):
+            self.reset_probe()
+            self.welford()
+
+        def planes(self):
+            """finalize -> smoothing -> coefficients of this job alone"""
             p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+            if a.planes == "multi":
+                planes_multi([self])
+                return
             hip.check(L.tmh_stats_finalize_device(self.h, p(self.mean), p(self.std), self.sp))
             hip.check(L.tmh_smooth2_f64_device(p(self.mean), p(self.std), p(self.smean),
                                                p(self.sstd), p(self.tmp), p(self.tmp2), H, W, 5.0,
                                                self.sp))
             hip.check(L.tmh_corrector_update_device(self.corr, p(self.smean), p(self.sstd),
                                                     self.sp))
+
+        def apply(self):
+            self.planes()
+            self.corrected()
+
+        def corrected(self):
             if fused and B:
                 hip.check(L.tmh_correct_u16_hist_blocks_device(self.corr, self.h, self.T_in,
                                                                self.T_out, shift, S, -1, -1,
@@ -1408,6 +1439,19 @@ def main():
         def close(self):
             L.tmh_corrector_destroy(self.corr)
             L.tmh_stats_destroy(self.h)
+
+    def planes_multi(jobs):
+        """The planes step of several jobs (a rank's channels) in one launch per
+        kernel (tmh_job_planes_multi_device), on the first job's stream: the
+        library orders it after every job's stream and every job's stream
+        after it."""
+        n = len(jobs)
+        arr = lambda xs: (C.c_void_p * n)(*[C.c_void_p(x) for x in xs])  # noqa: E731
+        hip.check(L.tmh_job_planes_multi_device(
+            arr([j.h.value for j in jobs]), arr([j.corr.value for j in jobs]), n,
+            arr([j.mean.data_ptr() for j in jobs]), arr([j.std.data_ptr() for j in jobs]),
+            arr([j.smean.data_ptr() for j in jobs]), arr([j.sstd.data_ptr() for j in jobs]),
+            5.0, jobs[0].sp))
 
     # jobs in flight (one channel, one rank): lanes share the sites and the
     # output blocks; job k runs on lane k % J after job k-1's corrected pass
@@ -1442,18 +1486,39 @@ def main():
             ev.record(ch.cstream)
             jobs["applied"] = ev
             return
+        for ch in chans:  # every channel's probe queued before any Welford launch waits
+            ch.reset_probe()
         for ch in chans:
-            ch.stats()
+            ch.welford()
         evs = {}
-        if dist_on:
+        if dist_on and a.merge == "batched":
+            # every channel's merge on the main stream, one collective per
+            # quantity for all channels (the library orders each handle's
+            # stream against it: tmhip.h stream contract)
+            with torch.cuda.stream(stream):
+                e0 = chans[0].event() if timing["on"] else None
+                merge_welford_multi([ch.ops for ch in chans], D, n_totals=[n_channel] * CH)
+                evs["batched"] = [e0, chans[0].event() if timing["on"] else None]
+        elif dist_on:
             for ch in chans:
                 with torch.cuda.stream(ch.stream):
                     e0 = ch.event() if timing["on"] else None
                     merge_welford(ch.ops, D, n_total=n_channel)
                     evs[id(ch)] = [e0, ch.event() if timing["on"] else None]
+        if a.planes == "multi":
+            planes_multi(chans)
+        else:
+            for ch in chans:
+                ch.planes()
         for ch in chans:
-            ch.apply()
-        if dist_on:
+            ch.corrected()
+        if dist_on and a.merge == "batched":
+            with torch.cuda.stream(stream):
+                e2 = chans[0].event() if timing["on"] else None
+                merge_counts_multi([ch.ops for ch in chans], D)
+                if timing["on"]:
+                    chans[0].merge_ev.append(evs["batched"] + [e2, chans[0].event()])
+        elif dist_on:
             for ch in chans:
                 with torch.cuda.stream(ch.stream):
                     e2 = ch.event() if timing["on"] else None
@@ -1506,19 +1571,30 @@ def main():
         ct = CollectiveTimer(torch, dev)
         for ch in chans:
             ch.stats()
-        for ch in chans:
-            with torch.cuda.stream(ch.stream):
-                merge_welford(ch.ops, D, n_total=n_channel, timer=ct)
+        if a.merge == "batched":
+            with torch.cuda.stream(stream):
+                merge_welford_multi([ch.ops for ch in chans], D, n_totals=[n_channel] * CH,
+                                    timer=ct)
+        else:
+            for ch in chans:
+                with torch.cuda.stream(ch.stream):
+                    merge_welford(ch.ops, D, n_total=n_channel, timer=ct)
         for ch in chans:
             ch.apply()
-        for ch in chans:
-            with torch.cuda.stream(ch.stream):
-                merge_counts(ch.ops, D, timer=ct)
+        if a.merge == "batched":
+            with torch.cuda.stream(stream):
+                merge_counts_multi([ch.ops for ch in chans], D, timer=ct)
+        else:
+            for ch in chans:
+                with torch.cuda.stream(ch.stream):
+                    merge_counts(ch.ops, D, timer=ct)
         collectives = ct.summary()
     merge_ms = None
     if dist_on and prof:
         merge_ms = []
         for ch in chans:
+            if not ch.merge_ev:  # batched merges: timed on channel 0 for all channels
+                continue
             w = [e[0].elapsed_time(e[1]) for e in ch.merge_ev]
             m = [e[2].elapsed_time(e[3]) for e in ch.merge_ev]
             merge_ms.append({"welford_allreduce_ms": round(float(np.mean(w)), 4),
@@ -1735,6 +1811,8 @@ def main():
                                              "sites' blocks" if share_out else "private"),
                        "pipeline": a.pipeline,
                        "jobs_in_flight": J,
+                       "planes": a.planes,
+                       "merge": a.merge if dist_on else None,
                        "job_choice": choice,
                        "jobs_order": a.jobs_order if J > 1 else None,
                        "hbm_layout": (("sites in one buffer, corrected output in blocks of %d "
@@ -1747,7 +1825,11 @@ def main():
             "kernels": kdetail,
         }
         if merge_ms is not None:
-            resd["merge_per_channel"] = merge_ms
+            if a.merge == "batched":
+                resd["merge_all_channels"] = dict(merge_ms[0], note=(
+                    "batched: one collective per quantity for the %d channels" % CH))
+            else:
+                resd["merge_per_channel"] = merge_ms
         if collectives is not None:
             resd["collectives_isolated"] = {
                 "note": "one extra step, the device synchronised before each collective: its own "

@@ -153,6 +153,18 @@ int tmh_stats_zero_counts(tmh_stats* h, int64_t* host_out, int64_t n, void* stre
 int tmh_stats_update_welford_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
                                     int log_transform, void* stream);
 
+/* The job's site probe (see the options above), queued now on `stream`
+ * without waiting for it: the first Welford launch of the job then only
+ * waits for the probe's counts.  A caller running several jobs on several
+ * streams (a rank's channels) queues every job's probe first, so that no
+ * launch waits for another job's kernels to drain before its probe can run.
+ * Optional: a job not probed this way is probed by its first Welford launch.
+ * Same stream contract as the updates (below). */
+int tmh_stats_probe_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
+                           void* stream);
+int tmh_stats_probe_blocks_device(tmh_stats* h, const uint16_t* const* dev_blocks, int block_shift,
+                                  int64_t n_sites, void* stream);
+
 /* Blocked site layout (device entry points below): the n_sites sites, in
  * site order, live in blocks of 2^block_shift consecutive sites (2 <= shift
  * <= 24; the last block may be partial), block b at dev_blocks[b] -- a DEVICE
@@ -200,7 +212,11 @@ int tmh_stats_site_order_stats(tmh_stats* h, int64_t site, uint16_t* host_vlo,
                                uint16_t* host_vhi);
 
 /* ---- multi-GPU merge (one process per GPU; collectives done by the caller
- * over RCCL on the device buffers these functions fill/consume) --------- */
+ * over RCCL on the device buffers these functions fill/consume).  Every
+ * entry point below that takes a stream follows the updates' stream
+ * contract: on another stream than the handle's it runs after the handle's
+ * queued work and the handle's stream waits for it (so one stream can merge
+ * several handles -- a rank's channels -- with batched collectives). ---- */
 int tmh_stats_get_n(tmh_stats* h, int64_t* n);
 /* The reference's plain attribute OnlineStatistics.n (stats.py:53): the count
  * later Welford updates continue from and percentiles / var divide by. */
@@ -288,6 +304,30 @@ int tmh_corrector_update_device(tmh_corrector* c, const double* dev_mean, const 
 int tmh_corrector_set_option(tmh_corrector* c, int option, int value);
 /* The two global means (np.mean(std), np.mean(mean), image.py:627). */
 int tmh_corrector_means(tmh_corrector* c, double* mean_of_std, double* mean_of_mean);
+/* tmh_corrector_update_device for n <= 8 correctors (a rank's channels) in
+ * one launch per kernel (the plane sums, every coefficient form, the launch
+ * constants), on `stream` (NULL: the first corrector's); results identical
+ * to n separate calls. */
+int tmh_corrector_update_multi_device(tmh_corrector* const* cs, int n, const double* const* dev_mean,
+                                      const double* const* dev_std, void* stream);
+/* The planes step of n <= 8 jobs at once (a rank's channels, configs[2]/[3];
+ * reference: one corilla job per channel, tmlib/workflow/corilla/api.py:64-105):
+ * per job k, statistics finalize (stats.py:94-112) -> IllumstatsContainer
+ * smoothing of mean and std (image.py:1172-1193, sigma) -> corrector k's
+ * coefficients from the smoothed planes (image.py:599-631).  One launch per
+ * kernel for all jobs: the smoothing reads each handle's mean and M2 and
+ * finalizes std as it reads it (sigma 5; other sigmas finalize into scratch
+ * first), then the coefficient launches of tmh_corrector_update_multi_device.
+ * dev_smean / dev_sstd [n]: the smoothed planes (device, f64 [height*width]);
+ * dev_mean / dev_std (may be NULL, or hold NULL entries): the unsmoothed
+ * planes, written only where asked for.  Runs on `stream` (NULL: the first
+ * handle's) after everything queued on every handle's stream, and every
+ * handle's stream waits for it.  Results identical to finalize + smooth2 +
+ * corrector update per job. */
+int tmh_job_planes_multi_device(tmh_stats* const* hs, tmh_corrector* const* cs, int n,
+                                double* const* dev_mean, double* const* dev_std,
+                                double* const* dev_smean, double* const* dev_sstd, double sigma,
+                                void* stream);
 /* Host buffers: chunks of <= 16 sites, H2D / kernel / D2H on three streams
  * with two device and two pinned output slots (TMH_OPT_HOST_STAGING).  Returns when host_out is
  * complete; host_out must not overlap host_in. */

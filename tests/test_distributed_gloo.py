@@ -156,3 +156,63 @@ def test_shard_bounds_cover_in_order():
             spans = [shard_bounds(n, w, r) for r in range(w)]
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+
+
+def _multi_worker(rank, world, port, name, out_dir, whole):
+    """Two jobs sharded over the same ranks (a rank's channels), merged with
+    the batched collectives (sharded.merge_welford_multi / merge_counts_multi):
+    job 0 = the golden's sites, job 1 = the same sites in reverse order."""
+    import sys
+    sys.path.insert(0, REPO)
+    from oracle import corilla_oracle as orc
+    from tmlibrary_amd.workflow.corilla.sharded import (merge_counts_multi, merge_welford_multi,
+                                                         shard_bounds)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = load_golden(name)
+    jobs = [list(g["sites"]), list(g["sites"])[::-1]]
+    q = np.linspace(0, 100, 10 ** (int(g["decimals"]) + 2))
+    ops_list = []
+    for sites in jobs:
+        a, b = shard_bounds(len(sites), world, rank)
+        mine = sites[a:b]
+        st = orc.OracleOnlineStatistics(sites[0].shape, int(g["decimals"]))
+        for s in mine:
+            st.update(s)
+        local_hist = sum((orc.histogram_u16(s) for s in mine), np.zeros(65536, np.uint64))
+        cls = WholeOps if whole else HostOps
+        ops_list.append(cls(st.n, st.mean, st._M2, [orc.percentile_linear(s, q) for s in mine],
+                            local_hist))
+    n_totals = merge_welford_multi(ops_list, dist)
+    merge_counts_multi(ops_list, dist)
+    np.savez(os.path.join(out_dir, "m%d.npz" % rank), n=np.array(n_totals),
+             **{"mean%d" % j: o.mean.numpy() for j, o in enumerate(ops_list)},
+             **{"m2%d" % j: o.m2.numpy() for j, o in enumerate(ops_list)},
+             **{"acc%d" % j: o.acc.numpy() for j, o in enumerate(ops_list)},
+             **{"hist%d" % j: o.hist.numpy().astype(np.uint64) for j, o in enumerate(ops_list)})
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,whole", [(2, False), (3, False), (2, True)])
+def test_merge_multi_jobs_gloo(tmp_path, world, whole):
+    """Batched multi-job merges: each job's results equal its own sequential
+    oracle -- Welford within 1e-6, percentile sums bit-exact (each job's sites
+    in its own order through the shared chain), pooled histograms exact."""
+    name = "stats_medium"
+    mp.start_processes(_multi_worker, args=(world, _free_port(), name, str(tmp_path), whole),
+                       nprocs=world, join=True, start_method="spawn")
+    g = load_golden(name)
+    jobs = [list(g["sites"]), list(g["sites"])[::-1]]
+    refs = [orc.run_illumstats(s) for s in jobs]
+    want_hist = sum((orc.histogram_u16(s) for s in g["sites"]), np.zeros(65536, np.uint64))
+    for r in range(world):
+        z = np.load(tmp_path / ("m%d.npz" % r))
+        assert z["n"].tolist() == [len(jobs[0])] * 2
+        for j, ref in enumerate(refs):
+            assert np.allclose(z["mean%d" % j].reshape(ref.mean.shape), ref.mean, rtol=1e-6,
+                               atol=1e-12)
+            var = z["m2%d" % j].reshape(ref.mean.shape) / (len(jobs[j]) - 1)
+            assert np.allclose(var, ref.std ** 2, rtol=1e-6, atol=1e-12)
+            assert np.array_equal(z["acc%d" % j], ref.percentile_sums), (r, j)
+            assert np.array_equal(z["hist%d" % j], want_hist)

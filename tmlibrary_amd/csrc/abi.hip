@@ -264,6 +264,7 @@ struct tmh_stats {
   unsigned int* probe_host = nullptr;  // pinned copy
   hipEvent_t ev_probe = nullptr;
   bool probed = false;
+  bool probe_queued = false;  // tmh_stats_probe_device: launched, not yet read
   unsigned int probe_cnt[3] = {0u, 0u, 0u};
   int64_t wide_sites = 0;         // sites that count covers
   bool pct_sum_external = false;
@@ -313,6 +314,21 @@ struct tmh_corrector {
 };
 
 static hipStream_t pick(hipStream_t own, void* s) { return s ? (hipStream_t)s : own; }
+
+// Stream contract of the statistics entry points that take a stream
+// (include/tmhip.h): on another stream than the handle's, the work runs after
+// everything queued on the handle's stream, and the handle's stream waits for
+// it before any later work on the handle.
+static void cross_begin(tmh_stats* h, hipStream_t s) {
+  if (s == h->stream) return;
+  TMH_HIP(hipEventRecord(h->ev_in, h->stream));
+  TMH_HIP(hipStreamWaitEvent(s, h->ev_in, 0));
+}
+static void cross_end(tmh_stats* h, hipStream_t s) {
+  if (s == h->stream) return;
+  TMH_HIP(hipEventRecord(h->ev_out, s));
+  TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
+}
 
 constexpr int kPooledParts = 16;
 
@@ -535,7 +551,9 @@ int tmh_stats_reset(tmh_stats* h) {
     h->last_batch = 0;
     h->pending = 0;
     h->pct_sum_external = false;
+    if (h->probe_queued) TMH_HIP(hipEventSynchronize(h->ev_probe));  // its buffers are reused
     h->probed = false;  // the next job probes its own sites
+    h->probe_queued = false;
   });
 }
 
@@ -545,14 +563,29 @@ int tmh_stats_reset(tmh_stats* h) {
 // it.  Nothing is probed when every automatic choice is forced off.
 static void stats_probe(tmh_stats* h, const uint16_t* d, int64_t ns, const SiteTab& tab,
                         hipStream_t s) {
-  if (h->probed || ns <= 0) return;
+  if (h->probed || (ns <= 0 && !h->probe_queued)) return;
+  if (!h->probe_queued) {
+    launch_site_probe(d, h->npx, ns, h->probe.p, s, tab);
+    TMH_HIP(hipMemcpyAsync(h->probe_host, h->probe.p, 3 * sizeof(unsigned int),
+                           hipMemcpyDeviceToHost, s));
+    TMH_HIP(hipEventRecord(h->ev_probe, s));
+  }
+  TMH_HIP(hipEventSynchronize(h->ev_probe));
+  for (int i = 0; i < 3; ++i) h->probe_cnt[i] = h->probe_host[i];
+  h->probed = true;
+  h->probe_queued = false;
+}
+
+// The probe queued ahead of the job's Welford launch (tmh_stats_probe_device):
+// stats_probe then only waits for it.
+static void stats_probe_queue(tmh_stats* h, const uint16_t* d, int64_t ns, const SiteTab& tab,
+                              hipStream_t s) {
+  if (h->probed || h->probe_queued || ns <= 0) return;
   launch_site_probe(d, h->npx, ns, h->probe.p, s, tab);
   TMH_HIP(hipMemcpyAsync(h->probe_host, h->probe.p, 3 * sizeof(unsigned int),
                          hipMemcpyDeviceToHost, s));
   TMH_HIP(hipEventRecord(h->ev_probe, s));
-  TMH_HIP(hipEventSynchronize(h->ev_probe));
-  for (int i = 0; i < 3; ++i) h->probe_cnt[i] = h->probe_host[i];
-  h->probed = true;
+  h->probe_queued = true;
 }
 
 // The automatic choices from the probe (a job not probed: standard).
@@ -615,21 +648,6 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
   h->n += ns;
 }
 
-// Stream contract of the statistics entry points that take a stream
-// (include/tmhip.h): on another stream than the handle's, the work runs after
-// everything queued on the handle's stream, and the handle's stream waits for
-// it before any later work on the handle.
-static void cross_begin(tmh_stats* h, hipStream_t s) {
-  if (s == h->stream) return;
-  TMH_HIP(hipEventRecord(h->ev_in, h->stream));
-  TMH_HIP(hipStreamWaitEvent(s, h->ev_in, 0));
-}
-static void cross_end(tmh_stats* h, hipStream_t s) {
-  if (s == h->stream) return;
-  TMH_HIP(hipEventRecord(h->ev_out, s));
-  TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
-}
-
 static void stats_welford_dev(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
                               int log_transform, void* stream, const SiteTab& tab) {
   hipStream_t s = pick(h->stream, stream);
@@ -649,6 +667,33 @@ static void stats_welford_dev(tmh_stats* h, const uint16_t* dev_sites, int64_t n
   h->n += n_sites;
   h->pending += n_sites;
   cross_end(h, s);
+}
+
+static SiteTab blocked_tab(const uint16_t* const* dev_in_blocks, uint16_t* const* dev_out_blocks,
+                          int block_shift, int64_t npx);
+
+int tmh_stats_probe_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
+                           void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && (dev_sites || n_sites == 0) && n_sites >= 0, TMH_EINVAL, "bad arguments");
+    if ((h->npx & 7) || (reinterpret_cast<uintptr_t>(dev_sites) & 15)) return;  // no vector path
+    const hipStream_t s = pick(h->stream, stream);
+    cross_begin(h, s);
+    stats_probe_queue(h, dev_sites, n_sites, SiteTab{}, s);
+    cross_end(h, s);
+  });
+}
+
+int tmh_stats_probe_blocks_device(tmh_stats* h, const uint16_t* const* dev_blocks, int block_shift,
+                                  int64_t n_sites, void* stream) {
+  return guard([&] {
+    TMH_CHECK(h && n_sites >= 0, TMH_EINVAL, "bad arguments");
+    const SiteTab tab = blocked_tab(dev_blocks, nullptr, block_shift, h->npx);
+    const hipStream_t s = pick(h->stream, stream);
+    cross_begin(h, s);
+    stats_probe_queue(h, nullptr, n_sites, tab, s);
+    cross_end(h, s);
+  });
 }
 
 int tmh_stats_update_welford_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
@@ -844,16 +889,20 @@ int tmh_stats_wide_groups(tmh_stats* h, uint64_t* groups_out, int64_t* sites_out
 int tmh_stats_get_hist_device(tmh_stats* h, uint64_t* dev_hist, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_hist, TMH_EINVAL, "bad arguments");
-    TMH_HIP(hipMemcpyAsync(dev_hist, h->pooled.p, (size_t)kBins * 8, hipMemcpyDeviceToDevice,
-                           pick(h->stream, stream)));
+    const hipStream_t s = pick(h->stream, stream);
+    cross_begin(h, s);
+    TMH_HIP(hipMemcpyAsync(dev_hist, h->pooled.p, (size_t)kBins * 8, hipMemcpyDeviceToDevice, s));
+    cross_end(h, s);
   });
 }
 
 int tmh_stats_set_hist_device(tmh_stats* h, const uint64_t* dev_hist, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_hist, TMH_EINVAL, "bad arguments");
-    TMH_HIP(hipMemcpyAsync(h->pooled.p, dev_hist, (size_t)kBins * 8, hipMemcpyDeviceToDevice,
-                           pick(h->stream, stream)));
+    const hipStream_t s = pick(h->stream, stream);
+    cross_begin(h, s);
+    TMH_HIP(hipMemcpyAsync(h->pooled.p, dev_hist, (size_t)kBins * 8, hipMemcpyDeviceToDevice, s));
+    cross_end(h, s);
   });
 }
 
@@ -906,7 +955,10 @@ int tmh_stats_set_n(tmh_stats* h, int64_t n) {
 int tmh_stats_merge_stage1(tmh_stats* h, double* dev_nmean, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_nmean, TMH_EINVAL, "bad arguments");
-    launch_merge1(h->mean.p, h->n, h->npx, dev_nmean, pick(h->stream, stream));
+    const hipStream_t s = pick(h->stream, stream);
+    cross_begin(h, s);
+    launch_merge1(h->mean.p, h->n, h->npx, dev_nmean, s);
+    cross_end(h, s);
   });
 }
 
@@ -914,15 +966,20 @@ int tmh_stats_merge_stage2(tmh_stats* h, const double* dev_sum_nmean, int64_t n_
                            double* dev_m2c, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_sum_nmean && dev_m2c && n_total > 0, TMH_EINVAL, "bad arguments");
-    launch_merge2(h->mean.p, h->m2.p, h->n, dev_sum_nmean, n_total, h->npx, dev_m2c,
-                  pick(h->stream, stream));
+    const hipStream_t s = pick(h->stream, stream);
+    cross_begin(h, s);
+    launch_merge2(h->mean.p, h->m2.p, h->n, dev_sum_nmean, n_total, h->npx, dev_m2c, s);
+    cross_end(h, s);
   });
 }
 
 int tmh_stats_merge_stage3(tmh_stats* h, int64_t n_total, const double* dev_sum_m2c, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_sum_m2c && n_total >= 0, TMH_EINVAL, "bad arguments");
-    launch_copy_f64(dev_sum_m2c, h->m2.p, h->npx, pick(h->stream, stream));
+    const hipStream_t s = pick(h->stream, stream);
+    cross_begin(h, s);
+    launch_copy_f64(dev_sum_m2c, h->m2.p, h->npx, s);
+    cross_end(h, s);
     h->n = n_total;
   });
 }
@@ -932,8 +989,10 @@ int tmh_stats_pct_accumulate(tmh_stats* h, double* dev_acc, void* stream) {
     TMH_CHECK(h && dev_acc, TMH_EINVAL, "bad arguments");
     TMH_CHECK(h->flags & TMH_STATS_DEFERRED_PCT, TMH_ESTATE,
               "percentile chain needs a TMH_STATS_DEFERRED_PCT handle");
-    launch_pct_accumulate(h->vlh.p, h->n_deferred, h->vlh_cap, h->Q, h->gamma.p, dev_acc,
-                          pick(h->stream, stream));
+    const hipStream_t s = pick(h->stream, stream);
+    cross_begin(h, s);
+    launch_pct_accumulate(h->vlh.p, h->n_deferred, h->vlh_cap, h->Q, h->gamma.p, dev_acc, s);
+    cross_end(h, s);
   });
 }
 
@@ -945,15 +1004,21 @@ int tmh_stats_pct_accumulate_range(tmh_stats* h, double* dev_acc_range, int q_be
               "percentile chain needs a TMH_STATS_DEFERRED_PCT handle");
     TMH_CHECK(q_begin >= 0 && q_count >= 0 && (int64_t)q_begin + q_count <= h->Q, TMH_EINVAL,
               "quantile range out of bounds");
+    const hipStream_t s = pick(h->stream, stream);
+    cross_begin(h, s);
     launch_pct_accumulate_range(h->vlh.p, h->n_deferred, h->vlh_cap, q_begin, q_count, h->gamma.p,
-                                dev_acc_range, pick(h->stream, stream));
+                                dev_acc_range, s);
+    cross_end(h, s);
   });
 }
 
 int tmh_stats_set_pct_sum(tmh_stats* h, const double* dev_acc, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_acc, TMH_EINVAL, "bad arguments");
-    launch_copy_f64(dev_acc, h->acc.p, h->Q, pick(h->stream, stream));
+    const hipStream_t s = pick(h->stream, stream);
+    cross_begin(h, s);
+    launch_copy_f64(dev_acc, h->acc.p, h->Q, s);
+    cross_end(h, s);
     h->pct_sum_external = true;
   });
 }
@@ -1070,18 +1135,36 @@ int tmh_smooth_f64(const double* host_in, double* host_out, int height, int widt
 // correction
 // ---------------------------------------------------------------------------
 
+constexpr int kCoefPartials = 1024;  // blocks of the deterministic plane sums
+
+static void coef_job(CoefJobs& J, int k, tmh_corrector* c, const double* d_mean,
+                     const double* d_std) {
+  J.mean[k] = d_mean;
+  J.std[k] = d_std;
+  J.partial[k] = c->partial.p;
+  J.sums[k] = c->sums.p;
+  J.coef[k] = c->coef.p;
+  J.coef2[k] = c->coef2.p;
+  J.coef_lin[k] = c->coef_lin.p;
+  J.coef64[k] = c->coef64.p;
+  J.mconst[k] = c->mconst.p;
+  J.mconst2[k] = c->mconst2.p;
+  J.rc[k] = c->rc.p;
+  J.log_transform[k] = c->log_transform;
+  J.zero_log10[k] = c->zero_log10;
+}
+
 static void corrector_coeffs(tmh_corrector* c, const double* d_mean, const double* d_std,
                              hipStream_t s) {
   ProfScope prof("coeffs", s);
-  const int np = 1024;
-  launch_reduce_sum2(d_std, d_mean, c->npx, c->partial.p, np, c->sums.p, s);
-  launch_coeffs_all(d_mean, d_std, c->sums.p, c->npx, c->log_transform, c->zero_log10, c->coef.p,
-                    c->mconst.p, c->coef2.p, c->mconst2.p, c->coef_lin.p, c->coef64.p, c->rc.p, s);
+  CoefJobs J{};
+  coef_job(J, 0, c, d_mean, d_std);
+  launch_coeffs_jobs(J, 1, c->npx, kCoefPartials, s);
 }
 
 static void corrector_init(tmh_corrector* c, const double* d_mean, const double* d_std) {
   c->sums.alloc(3);
-  c->partial.alloc(3 * 1024);
+  c->partial.alloc(3 * kCoefPartials);
   c->coef.alloc(c->npx);
   c->coef2.alloc(c->npx);
   c->coef_lin.alloc(c->npx);
@@ -1182,6 +1265,92 @@ int tmh_corrector_update_device(tmh_corrector* c, const double* dev_mean, const 
   return guard([&] {
     TMH_CHECK(c && dev_mean && dev_std, TMH_EINVAL, "bad arguments");
     corrector_coeffs(c, dev_mean, dev_std, pick(c->stream, stream));
+  });
+}
+
+int tmh_corrector_update_multi_device(tmh_corrector* const* cs, int n, const double* const* dev_mean,
+                                      const double* const* dev_std, void* stream) {
+  return guard([&] {
+    TMH_CHECK(cs && dev_mean && dev_std && n >= 1 && n <= kMaxJobs, TMH_EINVAL,
+              "bad arguments (1 <= n <= 8 correctors)");
+    CoefJobs J{};
+    for (int k = 0; k < n; ++k) {
+      TMH_CHECK(cs[k] && dev_mean[k] && dev_std[k], TMH_EINVAL, "bad arguments");
+      TMH_CHECK(cs[k]->npx == cs[0]->npx, TMH_EINVAL, "correctors of different image sizes");
+      coef_job(J, k, cs[k], dev_mean[k], dev_std[k]);
+    }
+    const hipStream_t s = pick(cs[0]->stream, stream);
+    ProfScope prof("coeffs", s);
+    launch_coeffs_jobs(J, n, cs[0]->npx, kCoefPartials, s);
+  });
+}
+
+int tmh_job_planes_multi_device(tmh_stats* const* hs, tmh_corrector* const* cs, int n,
+                                double* const* dev_mean, double* const* dev_std,
+                                double* const* dev_smean, double* const* dev_sstd, double sigma,
+                                void* stream) {
+  return guard([&] {
+    TMH_CHECK(hs && cs && dev_smean && dev_sstd && n >= 1 && n <= kMaxJobs, TMH_EINVAL,
+              "bad arguments (1 <= n <= 8 jobs)");
+    TMH_CHECK(sigma >= 0.125, TMH_EINVAL, "sigma must be >= 0.125");
+    for (int k = 0; k < n; ++k) {
+      TMH_CHECK(hs[k] && cs[k] && dev_smean[k] && dev_sstd[k], TMH_EINVAL, "bad arguments");
+      TMH_CHECK(hs[k]->H == hs[0]->H && hs[k]->W == hs[0]->W && cs[k]->npx == hs[0]->npx,
+                TMH_EINVAL, "jobs of different image sizes");
+      TMH_CHECK(dev_smean[k] != dev_sstd[k], TMH_EINVAL, "smoothed planes must differ");
+      for (int j = 0; j < k; ++j)
+        TMH_CHECK(hs[j] != hs[k] && cs[j] != cs[k], TMH_EINVAL, "a handle listed twice");
+    }
+    const int H = hs[0]->H, W = hs[0]->W;
+    const int64_t npx = hs[0]->npx;
+    const hipStream_t s = pick(hs[0]->stream, stream);
+    for (int k = 0; k < n; ++k) cross_begin(hs[k], s);
+    // stats.py:94-112 as asked for (the unsmoothed planes: what the
+    // illumstats file keeps); the smoothing reads the handles' state itself
+    for (int k = 0; k < n; ++k) {
+      const bool m = dev_mean && dev_mean[k], d = dev_std && dev_std[k];
+      if (m || d)
+        launch_finalize(hs[k]->mean.p, hs[k]->m2.p, hs[k]->n, npx, m ? dev_mean[k] : nullptr,
+                        d ? dev_std[k] : nullptr, s);
+    }
+    // IllumstatsContainer.smooth (image.py:1172-1193), every job's mean and
+    // std in one launch; the std planes finalized as they are read
+    const auto t = taps_for(sigma);
+    const double* in[kMaxPlanes];
+    double* out[kMaxPlanes];
+    double sq[kMaxPlanes];
+    DBuf<double> scratch;
+    const bool onepass = t.second == 20 && W >= 41 && !getenv("TMH_SMOOTH_2PASS");
+    if (!onepass) scratch.alloc((size_t)3 * n * npx);  // finalized std + axis-0 temps
+    double* tmp[kMaxPlanes];
+    for (int k = 0; k < n; ++k) {
+      tmh_stats* h = hs[k];
+      in[2 * k] = h->mean.p;
+      out[2 * k] = dev_smean[k];
+      sq[2 * k] = 0.0;
+      out[2 * k + 1] = dev_sstd[k];
+      if (onepass) {
+        in[2 * k + 1] = h->m2.p;
+        sq[2 * k + 1] = h->n >= 2 ? (double)(h->n - 1) : -1.0;
+      } else {
+        double* sd = scratch.p + (size_t)(3 * k) * npx;
+        launch_finalize(h->mean.p, h->m2.p, h->n, npx, nullptr, sd, s);
+        in[2 * k + 1] = sd;
+        sq[2 * k + 1] = 0.0;
+        tmp[2 * k] = scratch.p + (size_t)(3 * k + 1) * npx;
+        tmp[2 * k + 1] = scratch.p + (size_t)(3 * k + 2) * npx;
+      }
+    }
+    launch_smooth_planes(in, out, onepass ? out : tmp, sq, 2 * n, H, W, t.first, t.second, s);
+    // the correctors' coefficients (image.py:599-631) from the smoothed planes
+    CoefJobs J{};
+    for (int k = 0; k < n; ++k) coef_job(J, k, cs[k], dev_smean[k], dev_sstd[k]);
+    {
+      ProfScope prof("coeffs", s);
+      launch_coeffs_jobs(J, n, npx, kCoefPartials, s);
+    }
+    for (int k = 0; k < n; ++k) cross_end(hs[k], s);
+    if (!onepass) TMH_HIP(hipStreamSynchronize(s));  // the scratch is freed on return
   });
 }
 

@@ -30,13 +30,25 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
   return (i < n) ? i : p - 1 - i;
 }
 
-// Planes of one launch (gridDim.z = 1 or 2): the mean and std planes of a
-// job are smoothed by the same two launches, half the launches of plane by
-// plane (each ~0.035 ms at 2160x2560: launch and tail dominated).
+// Planes of one launch (gridDim.z = the planes): the mean and std planes of
+// one job -- or of several jobs (tmh_job_planes_multi_device: a rank's
+// channels) -- are smoothed by the same launches, instead of a launch per
+// plane (each ~0.035 ms at 2160x2560: launch and tail dominated).  A plane
+// with sq[z] != 0 is read through the statistics finalize (stats.py:94-112):
+// sqrt(in / sq) -- in = M2, sq = n - 1 -- or NaN (sq < 0: n < 2), the same
+// expression k_finalize evaluates, so the std plane is never written out.
 struct SmPlanes {
-  const double* in[2];
-  double* out[2];
+  const double* in[kMaxPlanes];
+  double* out[kMaxPlanes];
+  double sq[kMaxPlanes];
 };
+
+__device__ __forceinline__ double sm_in(const SmPlanes& pl, const double* __restrict__ in, int64_t i) {
+  const double v = in[i];
+  const double q = pl.sq[blockIdx.z];
+  if (q == 0.0) return v;
+  return q > 0.0 ? sqrt(v / q) : __builtin_nan("");
+}
 
 // axis 0 (rows of the plane vary): out[y][x] = sum_j w[j] in[refl(y+j-r)][x]
 __global__ __launch_bounds__(256) void k_smooth_axis0(const SmPlanes pl, int H, int W,
@@ -136,7 +148,7 @@ __global__ __launch_bounds__(256) void k_smooth_2d(const SmPlanes pl, int H, int
     for (int t = 0; t < TH; ++t) acc[t] = 0.0;
 #pragma unroll
     for (int u = 0; u < TH + 2 * R; ++u) {
-      const double v = in[(int64_t)reflect_idx(y0 + u - R, H) * W + x];
+      const double v = sm_in(pl, in, (int64_t)reflect_idx(y0 + u - R, H) * W + x);
 #pragma unroll
       for (int t = 0; t < TH; ++t) {
         const int k = u - t;
@@ -159,23 +171,36 @@ __global__ __launch_bounds__(256) void k_smooth_2d(const SmPlanes pl, int H, int
   }
 }
 
-// np planes (1 or 2): in[k] -> tmp[k] (axis 0) -> out[k] (axis 1)
-static void launch_smooth_planes(const double* const* in, double* const* out, double* const* tmp,
-                                 int np, int H, int W, const double* d_w, int radius,
-                                 hipStream_t s) {
+// np planes: in[k] -> tmp[k] (axis 0) -> out[k] (axis 1); sq[k] != 0: plane k
+// is read as a finalized std (SmPlanes), which needs the one-pass form
+// (radius 20) -- the caller finalizes into a plane of its own otherwise
+void launch_smooth_planes(const double* const* in, double* const* out, double* const* tmp,
+                          const double* sq, int np, int H, int W, const double* d_w, int radius,
+                          hipStream_t s) {
   ProfScope prof("smooth", s);
-  SmPlanes a0{{in[0], np > 1 ? in[1] : nullptr}, {tmp[0], np > 1 ? tmp[1] : nullptr}};
-  SmPlanes a1{{tmp[0], np > 1 ? tmp[1] : nullptr}, {out[0], np > 1 ? out[1] : nullptr}};
-  const dim3 grid((unsigned)cdiv(W, 256), (unsigned)H, (unsigned)np);
+  if (np <= 0) return;
+  auto planes = [&](const double* const* a, double* const* b) {
+    SmPlanes p{};
+    for (int k = 0; k < np; ++k) {
+      p.in[k] = a[k];
+      p.out[k] = b[k];
+      p.sq[k] = sq ? sq[k] : 0.0;
+    }
+    return p;
+  };
   if (radius == 20 && W >= 2 * radius + 1 && !getenv("TMH_SMOOTH_2PASS")) {
     // sigma = 5, the reference's default (image.py:1172): one pass, both axes
     constexpr int TH = 16, TW = 256 - 2 * 20;
-    SmPlanes a{{in[0], np > 1 ? in[1] : nullptr}, {out[0], np > 1 ? out[1] : nullptr}};
+    const SmPlanes a = planes(in, out);
     const dim3 g((unsigned)cdiv(W, TW), (unsigned)cdiv(H, TH), (unsigned)np);
     hipLaunchKernelGGL((k_smooth_2d<TH, 20>), g, dim3(256), 0, s, a, H, W, d_w);
     TMH_HIP(hipGetLastError());
     return;
   }
+  for (int k = 0; k < np; ++k)
+    if (sq && sq[k] != 0.0) throw Error{TMH_EINVAL, "finalize-on-read smoothing needs sigma 5"};
+  const SmPlanes a0 = planes(in, tmp), a1 = planes(tmp, out);
+  const dim3 grid((unsigned)cdiv(W, 256), (unsigned)H, (unsigned)np);
   if (radius == 20) {  // sigma = 5, the reference's default (image.py:1172)
     // 16 rows per thread: 1,350 workgroups per plane at 2160x2560 (8 / 32 measured slower)
     const dim3 g2((unsigned)cdiv(W, 256), (unsigned)cdiv(H, 16), (unsigned)np);
@@ -193,7 +218,7 @@ static void launch_smooth_planes(const double* const* in, double* const* out, do
 
 void launch_smooth(const double* in, double* out, double* tmp, int H, int W, const double* d_w,
                    int radius, hipStream_t s) {
-  launch_smooth_planes(&in, &out, &tmp, 1, H, W, d_w, radius, s);
+  launch_smooth_planes(&in, &out, &tmp, nullptr, 1, H, W, d_w, radius, s);
 }
 
 void launch_smooth2(const double* in0, const double* in1, double* out0, double* out1,
@@ -202,7 +227,7 @@ void launch_smooth2(const double* in0, const double* in1, double* out0, double* 
   const double* in[2] = {in0, in1};
   double* out[2] = {out0, out1};
   double* tmp[2] = {tmp0, tmp1};
-  launch_smooth_planes(in, out, tmp, 2, H, W, d_w, radius, s);
+  launch_smooth_planes(in, out, tmp, nullptr, 2, H, W, d_w, radius, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -251,14 +276,15 @@ __device__ __forceinline__ double block_min256(double v, double* red) {
 }
 
 // sums of two planes at once (np.mean(std), np.mean(mean) of image.py:627):
-// blockIdx.y selects the plane, fixed partition -> deterministic.  The std
-// plane's blocks also take the smallest positive finite value (the largest
-// mean(std)/std, which sets the refinement threshold, common.h).
-__global__ __launch_bounds__(256) void k_reduce_partial2(const double* __restrict__ x0,
-                                                         const double* __restrict__ x1, int64_t n,
-                                                         double* __restrict__ partial) {
+// blockIdx.y selects the plane, blockIdx.z the job (CoefJobs), fixed
+// partition -> deterministic.  The std plane's blocks also take the smallest
+// positive finite value (the largest mean(std)/std, which sets the
+// refinement threshold, common.h).
+__global__ __launch_bounds__(256) void k_reduce_partial2(const CoefJobs J, int64_t n) {
   __shared__ double red[256];
-  const double* x = blockIdx.y ? x1 : x0;
+  const int j = blockIdx.z;
+  const double* x = blockIdx.y ? J.mean[j] : J.std[j];
+  double* partial = J.partial[j];
   const int64_t chunk = cdiv(n, gridDim.x);
   const int64_t b = (int64_t)blockIdx.x * chunk;
   const int64_t e = (b + chunk < n) ? b + chunk : n;
@@ -277,10 +303,13 @@ __global__ __launch_bounds__(256) void k_reduce_partial2(const double* __restric
   }
 }
 
-__global__ __launch_bounds__(256) void k_reduce_final2(const double* __restrict__ partial, int n,
-                                                       double* __restrict__ out) {
+// blockIdx.y = job: sums[0] = sum(std), sums[1] = sum(mean), sums[2] = min
+// positive std
+__global__ __launch_bounds__(256) void k_reduce_final2(const CoefJobs J, int n) {
   __shared__ double red[256];
-  const double* p = partial + (int64_t)blockIdx.x * n;
+  const int j = blockIdx.y;
+  const double* p = J.partial[j] + (int64_t)blockIdx.x * n;
+  double* out = J.sums[j];
   if (blockIdx.x == 2) {
     double mn = __builtin_inf();
     for (int i = threadIdx.x; i < n; i += 256) mn = fmin(mn, p[i]);
@@ -292,13 +321,6 @@ __global__ __launch_bounds__(256) void k_reduce_final2(const double* __restrict_
   for (int i = threadIdx.x; i < n; i += 256) acc += p[i];
   const double t = block_sum256(acc, red);
   if (threadIdx.x == 0) out[blockIdx.x] = t;
-}
-
-void launch_reduce_sum2(const double* x0, const double* x1, int64_t n, double* partial,
-                        int n_partial, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_partial2, dim3(n_partial, 2), dim3(256), 0, s, x0, x1, n, partial);
-  hipLaunchKernelGGL(k_reduce_final2, dim3(3), dim3(256), 0, s, partial, n_partial, out);
-  TMH_HIP(hipGetLastError());
 }
 
 void launch_reduce_sum(const double* x, int64_t n, double* partial, int n_partial, double* out,
@@ -331,46 +353,46 @@ void launch_build_corr_lut(float2* lut, int log_transform, double zero_log10, hi
 
 constexpr double kLog2_10d = 3.32192809488736234787;
 
-// Every coefficient form of one (mean, std) pair, one thread per pixel i:
+// Every coefficient form of one (mean, std) pair, one thread per pixel i
+// (blockIdx.y = job, CoefJobs):
 //   coef[i]    = (mean hi, mean lo, a = mean(std)/std, 0)      LUT path
 //   coef2      = (mean [* log2 10], a) as f32, for npx % 8 == 0 pixel 8g+j in
 //                plane j/2 as float4 (mu_2p, mu_2p+1, a_2p, a_2p+1) at g: one
 //                16-B load gives a pixel pair its packed-f32 operands (fused pass)
 //   coef_lin[i] = the same pair in pixel order (the chain's shifted gathers)
 //   coef64[i]  = (mean, std) in f64 (the refinement, common.h)
-__global__ void k_coeffs_all(const double* __restrict__ mean, const double* __restrict__ std,
-                             const double* __restrict__ sums, int64_t npx, int log_transform,
-                             float4* __restrict__ coef, float* __restrict__ coef2,
-                             float2* __restrict__ coef_lin, double2* __restrict__ coef64) {
+__global__ void k_coeffs_all(const CoefJobs J, int64_t npx) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= npx) return;
-  const double S = sums[0] / (double)npx;  // np.mean(std)
-  const double mu = mean[i], sd = std[i];
+  const int j = blockIdx.y;
+  const double S = J.sums[j][0] / (double)npx;  // np.mean(std)
+  const double mu = J.mean[j][i], sd = J.std[j][i];
   const double a = S / sd;
   const float mh = (float)mu;
-  coef[i] = make_float4(mh, (float)(mu - (double)mh), (float)a, 0.0f);
-  const double K = log_transform ? kLog2_10d : 1.0;
+  J.coef[j][i] = make_float4(mh, (float)(mu - (double)mh), (float)a, 0.0f);
+  const double K = J.log_transform[j] ? kLog2_10d : 1.0;
   int64_t om = 2 * i, oa = 2 * i + 1;
   if ((npx & 7) == 0) {
-    const int64_t g = i >> 3, j = i & 7;
-    const int64_t base = (j >> 1) * (npx >> 1) + 4 * g + (j & 1);
+    const int64_t g = i >> 3, jj = i & 7;
+    const int64_t base = (jj >> 1) * (npx >> 1) + 4 * g + (jj & 1);
     om = base;
     oa = base + 2;
   }
   const float mu2 = (float)(mu * K), af = (float)a;
+  float* coef2 = reinterpret_cast<float*>(J.coef2[j]);
   coef2[om] = mu2;
   coef2[oa] = af;
-  coef_lin[i] = make_float2(mu2, af);
-  coef64[i] = make_double2(mu, sd);
+  J.coef_lin[j][i] = make_float2(mu2, af);
+  J.coef64[j][i] = make_double2(mu, sd);
 }
 
-// Launch constants: mconst = (M hi, M lo, T, 0) (LUT path), mconst2 = (M' hi,
-// M' lo, 10**zero_log10 as f32 (a zero pixel's floor), T) with M' = M [* log2
-// 10], and the refinement constants; a_max = S / (smallest positive std), T
-// rounded down to f32.
-__global__ void k_refine_const(const double* __restrict__ sums, int64_t npx, int log_transform,
-                               double zero_log10, float4* __restrict__ mconst,
-                               float4* __restrict__ mconst2, RefineConst* __restrict__ rc) {
+// Launch constants (blockIdx.x = job): mconst = (M hi, M lo, T, 0) (LUT
+// path), mconst2 = (M' hi, M' lo, 10**zero_log10 as f32 (a zero pixel's
+// floor), T) with M' = M [* log2 10], and the refinement constants; a_max =
+// S / (smallest positive std), T rounded down to f32.
+__global__ void k_refine_const(const CoefJobs J, int64_t npx) {
+  const int j = blockIdx.x;
+  const double* sums = J.sums[j];
   const double S = sums[0] / (double)npx, M = sums[1] / (double)npx;
   double am = fabs(S / sums[2]);  // sums[2] = +inf (no positive std): 0
   if (!(am <= 1.7976931348623157e308)) am = 0.0;  // S inf/NaN: every pixel is inf/NaN anyway
@@ -378,21 +400,21 @@ __global__ void k_refine_const(const double* __restrict__ sums, int64_t npx, int
   float Tf = (float)T;
   if ((double)Tf > T) Tf = __uint_as_float(__float_as_uint(Tf) - 1u);  // T > 0: one f32 step down
   const float mh = (float)M;
-  mconst[0] = make_float4(mh, (float)(M - (double)mh), Tf, 0.0f);
-  const double M2 = M * (log_transform ? kLog2_10d : 1.0);
+  J.mconst[j][0] = make_float4(mh, (float)(M - (double)mh), Tf, 0.0f);
+  const double M2 = M * (J.log_transform[j] ? kLog2_10d : 1.0);
   const float m2h = (float)M2;
-  mconst2[0] = make_float4(m2h, (float)(M2 - (double)m2h), (float)exp10(zero_log10), Tf);
-  rc[0] = RefineConst{S, M, zero_log10, (double)Tf};
+  J.mconst2[j][0] = make_float4(m2h, (float)(M2 - (double)m2h), (float)exp10(J.zero_log10[j]), Tf);
+  J.rc[j][0] = RefineConst{S, M, J.zero_log10[j], (double)Tf};
 }
 
-void launch_coeffs_all(const double* mean, const double* std, const double* sums, int64_t npx,
-                       int log_transform, double zero_log10, float4* coef, float4* mconst,
-                       float2* coef2, float4* mconst2, float2* coef_lin, double2* coef64,
-                       RefineConst* rc, hipStream_t s) {
-  hipLaunchKernelGGL(k_coeffs_all, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, mean, std, sums,
-                     npx, log_transform, coef, reinterpret_cast<float*>(coef2), coef_lin, coef64);
-  hipLaunchKernelGGL(k_refine_const, dim3(1), dim3(1), 0, s, sums, npx, log_transform, zero_log10,
-                     mconst, mconst2, rc);
+// The jobs' sums (two fixed-order passes, deterministic), then every
+// coefficient form and the launch constants: four launches for all jobs.
+void launch_coeffs_jobs(const CoefJobs& J, int n_jobs, int64_t npx, int n_partial, hipStream_t s) {
+  if (n_jobs <= 0) return;
+  hipLaunchKernelGGL(k_reduce_partial2, dim3(n_partial, 2, n_jobs), dim3(256), 0, s, J, npx);
+  hipLaunchKernelGGL(k_reduce_final2, dim3(3, n_jobs), dim3(256), 0, s, J, n_partial);
+  hipLaunchKernelGGL(k_coeffs_all, dim3((unsigned)cdiv(npx, 256), n_jobs), dim3(256), 0, s, J, npx);
+  hipLaunchKernelGGL(k_refine_const, dim3(n_jobs), dim3(1), 0, s, J, npx);
   TMH_HIP(hipGetLastError());
 }
 

@@ -246,26 +246,44 @@ struct ZeroList {
 };
 void launch_zero_u64(const ZeroList& z, hipStream_t s);
 
+constexpr int kMaxJobs = 8;          // jobs (a rank's channels) of one multi-job launch
+constexpr int kMaxPlanes = 2 * kMaxJobs;
 void launch_smooth(const double* in, double* out, double* tmp, int H, int W, const double* d_w,
                    int radius, hipStream_t s);
+// np <= kMaxPlanes planes; sq (may be null): per plane 0 = read as is, else
+// the plane is M2 read as the finalized std sqrt(M2 / sq) (sq = n - 1; < 0:
+// NaN), sigma 5 only
+void launch_smooth_planes(const double* const* in, double* const* out, double* const* tmp,
+                          const double* sq, int np, int H, int W, const double* d_w, int radius,
+                          hipStream_t s);
 void launch_smooth2(const double* in0, const double* in1, double* out0, double* out1,
                     double* tmp0, double* tmp1, int H, int W, const double* d_w, int radius,
                     hipStream_t s);
-// out[0] = sum(x0), out[1] = sum(x1), out[2] = smallest positive finite x0
-// (+inf if none); partial holds 3 * n_partial
-void launch_reduce_sum2(const double* x0, const double* x1, int64_t n, double* partial,
-                        int n_partial, double* out, hipStream_t s);
 void launch_reduce_sum(const double* x, int64_t n, double* partial, int n_partial, double* out,
                        hipStream_t s);
 void launch_build_corr_lut(float2* lut, int log_transform, double zero_log10, hipStream_t s);
-// Every coefficient form of one (mean, std) pair in one pass: coef (LUT path,
-// mconst = (M hi, M lo, T, 0)), coef2 / coef_lin / mconst2 (packed log2-domain
-// path, fused_kernels.hip), coef64 (f64 (mean, std) for the refinement) and
-// rc (RefineConst).  sums = (sum(std), sum(mean), min positive std).
-void launch_coeffs_all(const double* mean, const double* std, const double* sums, int64_t npx,
-                       int log_transform, double zero_log10, float4* coef, float4* mconst,
-                       float2* coef2, float4* mconst2, float2* coef_lin, double2* coef64,
-                       RefineConst* rc, hipStream_t s);
+// Per job (a corrector) of a coefficient launch: its (smoothed) mean / std
+// planes, the reduction scratch (3 x n_partial) and sums (sum(std),
+// sum(mean), min positive std), and every coefficient form (apply_kernels.hip
+// k_coeffs_all: coef (LUT path, mconst = (M hi, M lo, T, 0)), coef2 / coef_lin
+// / mconst2 (packed log2-domain path, fused_kernels.hip), coef64 (f64 (mean,
+// std) for the refinement) and rc (RefineConst)).
+struct CoefJobs {
+  const double* mean[kMaxJobs];
+  const double* std[kMaxJobs];
+  double* partial[kMaxJobs];
+  double* sums[kMaxJobs];
+  float4* coef[kMaxJobs];
+  float2* coef2[kMaxJobs];
+  float2* coef_lin[kMaxJobs];
+  double2* coef64[kMaxJobs];
+  float4* mconst[kMaxJobs];
+  float4* mconst2[kMaxJobs];
+  RefineConst* rc[kMaxJobs];
+  int log_transform[kMaxJobs];
+  double zero_log10[kMaxJobs];
+};
+void launch_coeffs_jobs(const CoefJobs& J, int n_jobs, int64_t npx, int n_partial, hipStream_t s);
 // Refinement of the pixels a correct launch flagged (fl), written into out
 // (u16 or u8 of in's type; clip as the launch); launched on the same stream.
 void launch_fix_correct(const void* in, void* out, int elem_bytes, int64_t npx, int64_t n_sites,

@@ -60,6 +60,10 @@ SIGNATURES = {
     "tmh_stats_update_device": (_I, [_P, _P, _I64, _I, _P]),
     "tmh_stats_zero_counts": (_I, [_P, _P, _I64, _P]),
     "tmh_stats_update_welford_device": (_I, [_P, _P, _I64, _I, _P]),
+    "tmh_stats_probe_device": (_I, [_P, _P, _I64, _P]),
+    "tmh_stats_probe_blocks_device": (_I, [_P, _P, _I, _I64, _P]),
+    "tmh_corrector_update_multi_device": (_I, [_P, _I, _P, _P, _P]),
+    "tmh_job_planes_multi_device": (_I, [_P, _P, _I, _P, _P, _P, _P, _D, _P]),
     "tmh_stats_update_welford_blocks_device": (_I, [_P, _P, _I, _I64, _I, _P]),
     "tmh_stats_finalize": (_I, [_P, _P, _P, _P, _P, _P]),
     "tmh_stats_finalize_device": (_I, [_P, _P, _P, _P]),
