@@ -103,7 +103,7 @@ def test_job_planes_multi_bit_identical(L, sigma, ns):
         a, b = res["per-job"][j], res["multi"][j]
         for k in range(4):  # mean, std, smoothed mean, smoothed std: bit for bit (NaN too)
             assert np.array_equal(a["planes"][k], b["planes"][k], equal_nan=True), (j, k)
-        assert a["means"] == b["means"] or (np.isnan(a["means"]).all() and np.isnan(b["means"]).all())
+        assert np.array_equal(a["means"], b["means"], equal_nan=True), (a["means"], b["means"])
         assert np.array_equal(a["corrected"], b["corrected"]), j
     if ns[0] == 1:
         assert np.isnan(res["multi"][0]["planes"][1]).all()  # one site: std is NaN (stats.py:108)
