@@ -141,6 +141,12 @@ def parse():
     p.add_argument("--merge", choices=["batched", "per-channel"], default="batched",
                    help="N > 1 / forced distributed: the channels' merges with one collective per "
                         "quantity for all channels (sharded.merge_*_multi) or per channel")
+    p.add_argument("--channel-order", choices=["serial", "concurrent"], default="serial",
+                   help="several channels: their Welford passes, then their corrected passes, "
+                        "one after another on one stream (serial), or each channel's on its own "
+                        "stream at once (concurrent)")
+    p.add_argument("--fused-bands", type=int, default=None,
+                   help="TMH_OPT_FUSED_BANDS: pixel bands of the fused pass (default: automatic)")
     p.add_argument("--channel-streams", choices=["per-channel", "one"], default="per-channel",
                    help="several channels: each on its own stream (its merges overlap the "
                         "others' kernels), or all on one stream")
@@ -1376,6 +1382,9 @@ def main():
                                                     ZERO_LOG10, self.sp, C.byref(self.corr)))
             if a.fused_cus is not None:
                 hip.check(L.tmh_corrector_set_option(self.corr, hip.TMH_OPT_FUSED_CUS, a.fused_cus))
+            if a.fused_bands is not None:
+                hip.check(L.tmh_corrector_set_option(self.corr, hip.TMH_OPT_FUSED_BANDS,
+                                                     a.fused_bands))
             self.ops = StatsOps(L, self.h, npx, Q, dev)
             self.merge_ev = []  # (welford start, end, counts start, end) per timed step
 
@@ -1389,14 +1398,15 @@ def main():
             else:
                 hip.check(L.tmh_stats_probe_device(self.h, self.S_ptr, S, self.sp))
 
-        def welford(self):
+        def welford(self, sp=None):
+            sp = sp or self.sp  # another stream: the library orders it against the handle's
             if fused and B and not in_contig:  # Welford pass; histograms from the correction's read
                 hip.check(L.tmh_stats_update_welford_blocks_device(self.h, self.T_in, shift, S, 1,
-                                                                   self.sp))
+                                                                   sp))
             elif fused:
-                hip.check(L.tmh_stats_update_welford_device(self.h, self.S_ptr, S, 1, self.sp))
+                hip.check(L.tmh_stats_update_welford_device(self.h, self.S_ptr, S, 1, sp))
             else:
-                hip.check(L.tmh_stats_update_device(self.h, self.S_ptr, S, 1, self.sp))
+                hip.check(L.tmh_stats_update_device(self.h, self.S_ptr, S, 1, sp))
 
         def stats(self):
             self.reset_probe()
@@ -1419,14 +1429,15 @@ def main():
             self.planes()
             self.corrected()
 
-        def corrected(self):
+        def corrected(self, sp=None):
+            csp = sp or self.csp
             if fused and B:
                 hip.check(L.tmh_correct_u16_hist_blocks_device(self.corr, self.h, self.T_in,
                                                                self.T_out, shift, S, -1, -1,
-                                                               self.csp))
+                                                               csp))
             elif fused:
                 hip.check(L.tmh_correct_u16_hist_device(self.corr, self.h, self.S_ptr, self.O_ptr,
-                                                        S, -1, -1, self.csp))
+                                                        S, -1, -1, csp))
             else:
                 hip.check(L.tmh_correct_u16_device(self.corr, self.S_ptr, self.O_ptr, S, -1, -1,
                                                    self.sp))
@@ -1461,6 +1472,13 @@ def main():
     J = jobs_in_flight = max(1, a.jobs_in_flight) if (CH == 1 and not dist_on and fused) else 1
     chans = [Channel(c) for c in range(CH)]
     lanes = chans + [Channel(0, lane=j) for j in range(1, J)]
+    # several channels, --channel-order serial: every channel's Welford pass,
+    # then every channel's corrected pass, one after another on one stream of
+    # their own (each streaming pass alone on the GPU; the library orders it
+    # against the channel's handle stream, and each channel's histogram tail
+    # runs on its handle's tail stream under the next channel's pass)
+    pass_stream = torch.cuda.Stream(dev) if CH > 1 and a.channel_order == "serial" else None
+    pass_sp = C.c_void_p(pass_stream.cuda_stream) if pass_stream is not None else None
     jobs = {"k": 0, "applied": None, "welford": None}
 
     log("%d channel(s) x %d sites resident; warm-up" % (CH, S))
@@ -1488,8 +1506,11 @@ def main():
             return
         for ch in chans:  # every channel's probe queued before any Welford launch waits
             ch.reset_probe()
+        if CH > 1:  # ... and run: no probe waits behind another channel's pass for CUs
+            for ch in chans:
+                ch.stream.synchronize()
         for ch in chans:
-            ch.welford()
+            ch.welford(pass_sp)
         evs = {}
         if dist_on and a.merge == "batched":
             # every channel's merge on the main stream, one collective per
@@ -1511,7 +1532,7 @@ def main():
             for ch in chans:
                 ch.planes()
         for ch in chans:
-            ch.corrected()
+            ch.corrected(pass_sp)
         if dist_on and a.merge == "batched":
             with torch.cuda.stream(stream):
                 e2 = chans[0].event() if timing["on"] else None
@@ -1812,6 +1833,7 @@ def main():
                        "pipeline": a.pipeline,
                        "jobs_in_flight": J,
                        "planes": a.planes,
+                       "channel_order": a.channel_order if CH > 1 else None,
                        "merge": a.merge if dist_on else None,
                        "job_choice": choice,
                        "jobs_order": a.jobs_order if J > 1 else None,

@@ -301,6 +301,11 @@ int tmh_corrector_update_device(tmh_corrector* c, const double* dev_mean, const 
  * CU count, default: all) -- fewer leave room for other streams' kernels
  * (several channel jobs sharing a GPU).  Results never depend on them. */
 #define TMH_OPT_FUSED_CUS 8
+/* TMH_OPT_FUSED_BANDS: pixel bands of the fused pass's unit sweep, 0
+ * (default: the configuration's, doubled up to 64 while a launch has fewer
+ * than 8 units per workgroup -- short launches, e.g. a rank's 432-site share
+ * of a channel at N = 8), or 8 / 16 / 32 / 64. */
+#define TMH_OPT_FUSED_BANDS 9
 int tmh_corrector_set_option(tmh_corrector* c, int option, int value);
 /* The two global means (np.mean(std), np.mean(mean), image.py:627). */
 int tmh_corrector_means(tmh_corrector* c, double* mean_of_std, double* mean_of_mean);

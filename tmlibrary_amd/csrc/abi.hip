@@ -301,6 +301,7 @@ struct tmh_corrector {
   DBuf<tmh_window> win;  // per-site alignment windows of the chain pass
   DBuf<uint8_t> lut8;    // the chain pass's 16-bit clip + scale table (64 KB)
   int n_wg = 256;
+  int bands = 0;     // TMH_OPT_FUSED_BANDS (0: automatic)
   DBuf<int> queues;  // fused pass: per-XCD unit counters (dynamic deal)
   DBuf<double> sums, partial;
   DBuf<uint16_t> stage_in, stage_out;
@@ -1249,6 +1250,12 @@ void tmh_corrector_destroy(tmh_corrector* c) {
 int tmh_corrector_set_option(tmh_corrector* c, int option, int value) {
   return guard([&] {
     TMH_CHECK(c, TMH_EINVAL, "corrector is NULL");
+    if (option == TMH_OPT_FUSED_BANDS) {
+      TMH_CHECK(value == 0 || value == 8 || value == 16 || value == 32 || value == 64, TMH_EINVAL,
+                "fused bands must be 0 (automatic), 8, 16, 32 or 64");
+      c->bands = value;
+      return;
+    }
     if (option == TMH_OPT_FUSED_CUS) {
       int cus = 256;
       TMH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
@@ -1562,7 +1569,7 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
       const FixList fl = corrector_fixlist(c, n_sites, s);
       launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p, fl,
                           c->log_transform, clip_lo, clip_hi, h->hist_full.p, h->hist_rmask.p,
-                          c->queues.p, c->n_wg, cfg, s, tab, rl);
+                          c->queues.p, c->n_wg, cfg, c->bands, s, tab, rl);
       if (cfg == kFusedWide) launch_rare_count(rl, h->hist_full.p, n_sites, s);
       launch_fix_correct(dev_in, dev_out, 2, c->npx, n_sites, fl, c->coef64.p, c->rc.p,
                          c->log_transform, clip_lo, clip_hi, s, tab);

@@ -324,11 +324,13 @@ constexpr double kBrightFrac = 0.10;
 // the fused pass without its histogram (very wide sites: k_hist_site_u16
 // builds the histograms)
 constexpr int kFusedNoHist = 100;
-// cfg: 0 .. kFusedConfigs - 1 or kFusedNoHist -- exactly one launch
+// cfg: 0 .. kFusedConfigs - 1 or kFusedNoHist -- exactly one launch; bands:
+// pixel bands of the unit sweep (0: the configuration's, more for a short
+// launch -- fused_kernels.hip fused_bands)
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, const FixList& fl,
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
-                         unsigned long long* rmask, int* queues, int n_wg, int cfg,
+                         unsigned long long* rmask, int* queues, int n_wg, int cfg, int bands,
                          hipStream_t s, const SiteTab& tab = SiteTab{},
                          const RareList& rl = RareList{});
 // after launch_correct_hist with a RareList: each site's list into its

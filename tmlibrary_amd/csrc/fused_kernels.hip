@@ -597,26 +597,41 @@ struct FusedCfgCheck {
 static_assert(FusedCfgCheck<0>::ok && FusedCfgCheck<1>::ok && FusedCfgCheck<2>::ok &&
               FusedCfgCheck<3>::ok && FusedCfgCheck<4>::ok && FusedCfgCheck<5>::ok, "");
 
+// Pixel bands of a launch: the configuration's, doubled (up to 64) while the
+// launch has fewer than 8 units per workgroup -- a short launch (a rank's
+// 432-site share of a channel at N = 8: 108 site groups x 16 bands over 512
+// workgroups) otherwise ends with most workgroups idle for a unit's time.
+// bands > 0: that many (TMH_OPT_FUSED_BANDS).
+static int fused_bands(int cfg_bands, int64_t n_sites, int spu, int64_t n_wgs, int bands) {
+  if (bands > 0) return bands;
+  int b = cfg_bands;
+  const int64_t groups = (n_sites + spu - 1) / spu;
+  while (b < 64 && groups * b < 8 * n_wgs) b *= 2;
+  return b;
+}
+
 static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                                     const float4* cf4, const float4* mconst2, const FixList& fl,
                                     int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
                                     unsigned long long* rmask, int* queues, int n_wg, int cfg,
-                                    hipStream_t s, const SiteTab& tab, const RareList& rl) {
+                                    int bands_opt, hipStream_t s, const SiteTab& tab,
+                                    const RareList& rl) {
 #define TMH_LAUNCH_CH(L_, K_, A_)                                                                \
   {                                                                                              \
     constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
     const dim3 grid(n_wg * (1024 / c.threads));                                                  \
+    const int nbands = fused_bands(c.bands, n_sites, c.spu, grid.x, bands_opt);                  \
     if (clip_lo >= 0)                                                                            \
       hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, A_, c.threads, c.lds_bins, c.packed>), \
                          grid,                                                                   \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, c.bands, queues, tab,                   \
+                         clip_lo, clip_hi, hist, rmask, nbands, queues, tab,                    \
                          c.packed ? rl : RareList{});                                       \
     else                                                                                         \
       hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, A_, c.threads, c.lds_bins, c.packed>), \
                          grid,                                                                   \
                          dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, c.bands, queues, tab,                   \
+                         clip_lo, clip_hi, hist, rmask, nbands, queues, tab,                    \
                          c.packed ? rl : RareList{});                                       \
   }
 #define TMH_LAUNCH_CFG(L_)                                     \
@@ -648,7 +663,7 @@ static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t n
 void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                          const float2* coef2, const float4* mconst2, const FixList& fl,
                          int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
-                         unsigned long long* rmask, int* queues, int n_wg, int cfg,
+                         unsigned long long* rmask, int* queues, int n_wg, int cfg, int bands,
                          hipStream_t s, const SiteTab& tab, const RareList& rl) {
   if (n_sites <= 0) return;
   // queues[0..8): per-XCD unit counters; queues[8..10): the union of the
@@ -657,7 +672,7 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
   const float4* cf4 = reinterpret_cast<const float4*>(coef2);
   ProfScope prof("correct_hist", s);
   launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, cfg, s, tab, rl);
+                          hist, rmask, queues, n_wg, cfg, bands, s, tab, rl);
 }
 
 // Each site's rare list into its histogram: one workgroup per site, the

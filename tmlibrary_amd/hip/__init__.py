@@ -28,6 +28,7 @@ TMH_OPT_WELFORD_PARTS = 2
 TMH_OPT_COPY_THREADS = 4
 TMH_OPT_HOST_STAGING = 5
 TMH_OPT_FUSED_CUS = 8
+TMH_OPT_FUSED_BANDS = 9
 TMH_FUSED_NO_HIST = 100
 TMH_SYNTH_STANDARD = 0
 TMH_SYNTH_BRIGHT = 1

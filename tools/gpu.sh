@@ -20,6 +20,7 @@
 #   pytest:EXPR    the GPU tests selected by -k EXPR (gpu_tests_k_TAG.log)
 #   input[:N]      tools/bench_input.py on N full-size gzip files (host and GPU
 #                  decode, run_job, the sharded job) -> bench_input_TAG.json
+#   dist432v:ARGS  dist432 with extra flags ('+' for spaces) -> dist432_v_TAG.jsonl
 #   prof432        rocprofv3 kernel trace of dist432 -> rocprof_dist432_TAG/
 #   prof:DIST      rocprofv3 --kernel-trace --stats of a short bench on DIST
 #                  (synthetic | bright) -> rocprof_DIST_TAG/
@@ -92,6 +93,14 @@ for step in "$@"; do
         timeout -k 10 300 python bench.py --layout sharded --channels 4 --sites 432 --steps 10 \
         --warmup 3 --no-extras --cpu-sample 0 ${BENCH_ARGS:-} > $O/dist432_$TAG.json 2> $O/dist432_$TAG.err || exit $?
       summ $O/dist432_$TAG.json
+      ;;
+    dist432v)
+      # one variant: dist432v:--flag+value+--flag2 ('+' for spaces), appended to dist432_v_TAG.jsonl
+      V=$(echo "$a1" | tr '+' ' ')
+      TMH_BENCH_FORCE_DIST=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \
+        timeout -k 10 300 python bench.py --layout sharded --channels 4 --sites 432 --steps 10 \
+        --warmup 3 --no-extras --cpu-sample 0 ${BENCH_ARGS:-} $V > $O/dist432v.tmp 2>> $O/dist432_v_$TAG.err || exit $?
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.strip()][-1]); print(json.dumps({'variant': sys.argv[2], 'value': d['value'], 'ms': d['ms_per_step'], 'check': d['check_vs_oracle'], 'k': {k: v['avg_ms'] for k, v in d['kernels'].items()}}))" $O/dist432v.tmp "$V" | tee -a $O/dist432_v_$TAG.jsonl
       ;;
     prof432)
       TMH_BENCH_FORCE_DIST=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \

@@ -127,7 +127,7 @@ static int run(int argc, char** argv) {
       // zero-maintained slab: the production finalize resets it; here a memset
       CK(hipMemsetAsync(rmask, 0, S * 8, 0));
       launch_correct_hist(buf[i], buf[o], npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist,
-                          rmask, queues, cus, kFusedNarrow, 0);
+                          rmask, queues, cus, kFusedNarrow, 0, 0);
     });
   };
   // output written at buf[o] + delta bytes: does the read/write address
@@ -138,7 +138,7 @@ static int run(int argc, char** argv) {
       CK(hipMemsetAsync(rmask, 0, S * 8, 0));
       launch_correct_hist(buf[i], reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(buf[o]) + delta),
                           npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask, queues,
-                          cus, kFusedNarrow, 0);
+                          cus, kFusedNarrow, 0, 0);
     });
   };
   auto welford = [&](int i) {

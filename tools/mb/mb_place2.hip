@@ -134,7 +134,7 @@ int main(int argc, char** argv) {
         CK(hipMemsetAsync(fn, 0, 4, 0));
         CK(hipMemsetAsync(rmask, 0, S * 8, 0));
         launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist,
-                            rmask, queues, cus, kFusedNarrow, 0, tab);
+                            rmask, queues, cus, kFusedNarrow, 0, 0, tab);
       });
     };
     double *mean, *m2, *lut, *rn, *part;

@@ -120,7 +120,7 @@ static int run(int argc, char** argv) {
   int* queues;  // per-XCD unit counters + round-mask union
   CK(hipMalloc(&queues, kFusedQueueInts * sizeof(int)));
   launch_correct_hist(in, out, npx, S, (const float2*)coef, mconst2, fl, 1, -1, -1, hist, rmask,
-                      queues, cus, dist == 0 ? kFusedNarrow : kFusedWide, 0);
+                      queues, cus, dist == 0 ? kFusedNarrow : kFusedWide, 0, 0);
   CK(hipDeviceSynchronize());
   {
     std::vector<unsigned long long> rm(S);
