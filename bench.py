@@ -1506,9 +1506,6 @@ def main():
             return
         for ch in chans:  # every channel's probe queued before any Welford launch waits
             ch.reset_probe()
-        if CH > 1:  # ... and run: no probe waits behind another channel's pass for CUs
-            for ch in chans:
-                ch.stream.synchronize()
         for ch in chans:
             ch.welford(pass_sp)
         evs = {}

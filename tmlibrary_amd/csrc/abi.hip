@@ -302,6 +302,7 @@ struct tmh_corrector {
   DBuf<uint8_t> lut8;    // the chain pass's 16-bit clip + scale table (64 KB)
   int n_wg = 256;
   int bands = 0;     // TMH_OPT_FUSED_BANDS (0: automatic)
+  bool forms_stale = false;  // coef / coef_lin not made since the last coefficient update
   DBuf<int> queues;  // fused pass: per-XCD unit counters (dynamic deal)
   DBuf<double> sums, partial;
   DBuf<uint16_t> stage_in, stage_out;
@@ -1144,15 +1145,26 @@ static void coef_job(CoefJobs& J, int k, tmh_corrector* c, const double* d_mean,
   J.std[k] = d_std;
   J.partial[k] = c->partial.p;
   J.sums[k] = c->sums.p;
-  J.coef[k] = c->coef.p;
+  // the LUT path's coef and the chain's coef_lin are made when a call needs
+  // them (corrector_forms): the fused job path reads only coef2 and coef64
+  // (24 of the 48 B/px the full set writes)
+  J.coef[k] = nullptr;
   J.coef2[k] = c->coef2.p;
-  J.coef_lin[k] = c->coef_lin.p;
+  J.coef_lin[k] = nullptr;
+  c->forms_stale = true;
   J.coef64[k] = c->coef64.p;
   J.mconst[k] = c->mconst.p;
   J.mconst2[k] = c->mconst2.p;
   J.rc[k] = c->rc.p;
   J.log_transform[k] = c->log_transform;
   J.zero_log10[k] = c->zero_log10;
+}
+
+// coef / coef_lin for the calls that read them, from the last update
+static void corrector_forms(tmh_corrector* c, hipStream_t s) {
+  if (!c->forms_stale) return;
+  launch_coeffs_forms(c->coef64.p, c->sums.p, c->npx, c->log_transform, c->coef.p, c->coef_lin.p, s);
+  c->forms_stale = false;
 }
 
 static void corrector_coeffs(tmh_corrector* c, const double* d_mean, const double* d_std,
@@ -1384,6 +1396,7 @@ int tmh_correct_u16_device(tmh_corrector* c, const uint16_t* dev_in, uint16_t* d
     check_clip(clip_lo, clip_hi, 65535);
     hipStream_t s = pick(c->stream, stream);
     const FixList fl = corrector_fixlist(c, n_sites, s);
+    corrector_forms(c, s);
     launch_correct_u16(dev_in, dev_out, c->npx, n_sites, c->coef.p, c->lut.p, c->mconst.p, fl,
                        c->log_transform, clip_lo, clip_hi, s);
     launch_fix_correct(dev_in, dev_out, 2, c->npx, n_sites, fl, c->coef64.p, c->rc.p,
@@ -1443,6 +1456,7 @@ int tmh_correct_u16(tmh_corrector* c, const uint16_t* host_in, uint16_t* host_ou
         TMH_HIP(hipEventRecord(p.ev_in[slot], p.h2d));
         TMH_HIP(hipStreamWaitEvent(c->stream, p.ev_in[slot], 0));
         const FixList fl = corrector_fixlist(c, ns, c->stream);
+        corrector_forms(c, c->stream);
         launch_correct_u16(din, dout, c->npx, ns, c->coef.p, c->lut.p, c->mconst.p, fl,
                            c->log_transform, clip_lo, clip_hi, c->stream);
         launch_fix_correct(din, dout, 2, c->npx, ns, fl, c->coef64.p, c->rc.p, c->log_transform,
@@ -1476,6 +1490,7 @@ int tmh_correct_u8(tmh_corrector* c, const uint8_t* host_in, uint8_t* host_out, 
     c->stage8_out.ensure(bytes);
     TMH_HIP(hipMemcpyAsync(c->stage8_in.p, host_in, bytes, hipMemcpyHostToDevice, c->stream));
     const FixList fl = corrector_fixlist(c, n_sites, c->stream);
+    corrector_forms(c, c->stream);
     launch_correct_u8(c->stage8_in.p, c->stage8_out.p, c->npx, n_sites, c->coef.p, c->lut.p,
                       c->mconst.p, fl, c->log_transform, clip_lo, clip_hi, c->stream);
     launch_fix_correct(c->stage8_in.p, c->stage8_out.p, 1, c->npx, n_sites, fl, c->coef64.p,
@@ -1647,6 +1662,7 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
       h->vlh_ld = ld;
       stats_reserve_sites(h, nc);
       const FixList fl = corrector_fixlist(c, nc, s);
+      corrector_forms(c, s);
       launch_correct_u16(din, dout, c->npx, nc, c->coef.p, c->lut.p, c->mconst.p, fl,
                          c->log_transform, clip_lo, clip_hi, s);
       launch_fix_correct(din, dout, 2, c->npx, nc, fl, c->coef64.p, c->rc.p, c->log_transform,
@@ -1782,6 +1798,7 @@ int tmh_correct_chain_u8_device(tmh_corrector* c, const uint16_t* dev_in, uint8_
                            hipMemcpyHostToDevice, s));
     const FixList fl = corrector_fixlist(c, n_sites, s);
     if (!c->lut8.n) c->lut8.alloc(65536);
+    corrector_forms(c, s);
     launch_chain_u8(dev_in, dev_out, c->H, c->W, n_sites, c->coef_lin.p, c->mconst2.p, fl,
                     c->coef64.p, c->rc.p, c->log_transform, c->win.p, clip_lo, clip_hi,
                     c->lut8.p, s, c->zero_log10);

@@ -369,7 +369,7 @@ __global__ void k_coeffs_all(const CoefJobs J, int64_t npx) {
   const double mu = J.mean[j][i], sd = J.std[j][i];
   const double a = S / sd;
   const float mh = (float)mu;
-  J.coef[j][i] = make_float4(mh, (float)(mu - (double)mh), (float)a, 0.0f);
+  if (J.coef[j]) J.coef[j][i] = make_float4(mh, (float)(mu - (double)mh), (float)a, 0.0f);
   const double K = J.log_transform[j] ? kLog2_10d : 1.0;
   int64_t om = 2 * i, oa = 2 * i + 1;
   if ((npx & 7) == 0) {
@@ -382,8 +382,32 @@ __global__ void k_coeffs_all(const CoefJobs J, int64_t npx) {
   float* coef2 = reinterpret_cast<float*>(J.coef2[j]);
   coef2[om] = mu2;
   coef2[oa] = af;
-  J.coef_lin[j][i] = make_float2(mu2, af);
+  if (J.coef_lin[j]) J.coef_lin[j][i] = make_float2(mu2, af);
   J.coef64[j][i] = make_double2(mu, sd);
+}
+
+// The LUT path's coef and the chain's coef_lin from coef64 and the sums, for
+// a corrector whose coefficient update skipped them (the fused job path needs
+// only coef2 / coef64): the same values k_coeffs_all writes.
+__global__ void k_coeffs_forms(const double2* __restrict__ coef64, const double* __restrict__ sums,
+                               int64_t npx, int log_transform, float4* __restrict__ coef,
+                               float2* __restrict__ coef_lin) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npx) return;
+  const double S = sums[0] / (double)npx;
+  const double2 ms = coef64[i];
+  const double mu = ms.x, a = S / ms.y;
+  const float mh = (float)mu;
+  coef[i] = make_float4(mh, (float)(mu - (double)mh), (float)a, 0.0f);
+  const double K = log_transform ? kLog2_10d : 1.0;
+  coef_lin[i] = make_float2((float)(mu * K), (float)a);
+}
+
+void launch_coeffs_forms(const double2* coef64, const double* sums, int64_t npx, int log_transform,
+                         float4* coef, float2* coef_lin, hipStream_t s) {
+  hipLaunchKernelGGL(k_coeffs_forms, dim3((unsigned)cdiv(npx, 256)), dim3(256), 0, s, coef64, sums,
+                     npx, log_transform, coef, coef_lin);
+  TMH_HIP(hipGetLastError());
 }
 
 // Launch constants (blockIdx.x = job): mconst = (M hi, M lo, T, 0) (LUT

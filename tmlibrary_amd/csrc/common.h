@@ -264,7 +264,8 @@ void launch_reduce_sum(const double* x, int64_t n, double* partial, int n_partia
 void launch_build_corr_lut(float2* lut, int log_transform, double zero_log10, hipStream_t s);
 // Per job (a corrector) of a coefficient launch: its (smoothed) mean / std
 // planes, the reduction scratch (3 x n_partial) and sums (sum(std),
-// sum(mean), min positive std), and every coefficient form (apply_kernels.hip
+// sum(mean), min positive std), and every coefficient form (coef / coef_lin
+// null: left out, launch_coeffs_forms makes them when needed; apply_kernels.hip
 // k_coeffs_all: coef (LUT path, mconst = (M hi, M lo, T, 0)), coef2 / coef_lin
 // / mconst2 (packed log2-domain path, fused_kernels.hip), coef64 (f64 (mean,
 // std) for the refinement) and rc (RefineConst)).
@@ -284,6 +285,10 @@ struct CoefJobs {
   double zero_log10[kMaxJobs];
 };
 void launch_coeffs_jobs(const CoefJobs& J, int n_jobs, int64_t npx, int n_partial, hipStream_t s);
+// coef (LUT path) and coef_lin (chain) from coef64 + sums, for a job whose
+// coefficient launch left them out (CoefJobs entries null)
+void launch_coeffs_forms(const double2* coef64, const double* sums, int64_t npx, int log_transform,
+                         float4* coef, float2* coef_lin, hipStream_t s);
 // Refinement of the pixels a correct launch flagged (fl), written into out
 // (u16 or u8 of in's type; clip as the launch); launched on the same stream.
 void launch_fix_correct(const void* in, void* out, int elem_bytes, int64_t npx, int64_t n_sites,

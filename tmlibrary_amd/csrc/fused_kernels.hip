@@ -201,7 +201,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   __shared__ uint32_t pk_red[PK ? NT / 64 : 1][PK ? SPU : 1];  // packed: per-wave site sums
   static_assert(!PK || BINS == kRareLo, "rare lists start at the packed slice size");
   // packed with a rare list: the unit's values beyond the slices, per site
-  constexpr int kRareSh = PK ? 1024 : 1;
+  constexpr int kRareSh = PK ? 3072 : 1;  // the rest of the 160 KB of LDS (r4: 1,024)
   __shared__ uint16_t rstage[PK ? SPU : 1][kRareSh];
   __shared__ unsigned int rcnt[PK ? SPU : 1], rbase[PK ? SPU : 1];
   const bool rlist = PK && rl.v != nullptr;
