@@ -141,10 +141,14 @@ def parse():
     p.add_argument("--merge", choices=["batched", "per-channel"], default="batched",
                    help="N > 1 / forced distributed: the channels' merges with one collective per "
                         "quantity for all channels (sharded.merge_*_multi) or per channel")
-    p.add_argument("--channel-order", choices=["serial", "concurrent"], default="serial",
+    p.add_argument("--channel-order", choices=["pipelined", "serial", "concurrent"],
+                   default="pipelined",
                    help="several channels: their Welford passes, then their corrected passes, "
-                        "one after another on one stream (serial), or each channel's on its own "
-                        "stream at once (concurrent)")
+                        "one after another on one pass stream, each channel's merges and planes "
+                        "on its own stream under the other channels' passes (pipelined); the "
+                        "same with every channel's merge and planes batched between the two "
+                        "sweeps (serial); or each channel's passes on its own stream at once "
+                        "(concurrent)")
     p.add_argument("--fused-bands", type=int, default=None,
                    help="TMH_OPT_FUSED_BANDS: pixel bands of the fused pass (default: automatic)")
     p.add_argument("--channel-streams", choices=["per-channel", "one"], default="per-channel",
@@ -1477,7 +1481,12 @@ def main():
     # their own (each streaming pass alone on the GPU; the library orders it
     # against the channel's handle stream, and each channel's histogram tail
     # runs on its handle's tail stream under the next channel's pass)
-    pass_stream = torch.cuda.Stream(dev) if CH > 1 and a.channel_order == "serial" else None
+    pass_stream = (torch.cuda.Stream(dev) if CH > 1 and a.channel_order in ("serial", "pipelined")
+                   else None)
+    evs_p = {}
+    # the pipelined order merges each channel on its own stream as soon as its
+    # pass is done (one collective per quantity and channel)
+    merge_mode = "per-channel" if a.channel_order == "pipelined" and CH > 1 else a.merge
     pass_sp = C.c_void_p(pass_stream.cuda_stream) if pass_stream is not None else None
     jobs = {"k": 0, "applied": None, "welford": None}
 
@@ -1504,12 +1513,41 @@ def main():
             ev.record(ch.cstream)
             jobs["applied"] = ev
             return
+        if a.channel_order == "pipelined":
+            # every channel's probe queued, then the Welford passes one after
+            # another on the pass stream; channel c's merge and planes on its
+            # own stream as soon as its pass is done (under the next channel's
+            # Welford pass); the corrected passes one after another on the pass
+            # stream (each after its channel's planes: the library's stream
+            # contract), each channel's tail and count merge under the next
+            # channel's corrected pass
+            for ch in chans:
+                ch.reset_probe()
+            for ch in chans:
+                ch.welford(pass_sp)
+            for ch in chans:
+                with torch.cuda.stream(ch.stream):
+                    if dist_on:
+                        e0 = ch.event() if timing["on"] else None
+                        merge_welford(ch.ops, D, n_total=n_channel)
+                        evs_p[id(ch)] = [e0, ch.event() if timing["on"] else None]
+                ch.planes()
+            for ch in chans:
+                ch.corrected(pass_sp)
+            if dist_on:
+                for ch in chans:
+                    with torch.cuda.stream(ch.stream):
+                        e2 = ch.event() if timing["on"] else None
+                        merge_counts(ch.ops, D)
+                        if timing["on"]:
+                            ch.merge_ev.append(evs_p[id(ch)] + [e2, ch.event()])
+            return
         for ch in chans:  # every channel's probe queued before any Welford launch waits
             ch.reset_probe()
         for ch in chans:
             ch.welford(pass_sp)
         evs = {}
-        if dist_on and a.merge == "batched":
+        if dist_on and merge_mode == "batched":
             # every channel's merge on the main stream, one collective per
             # quantity for all channels (the library orders each handle's
             # stream against it: tmhip.h stream contract)
@@ -1530,7 +1568,7 @@ def main():
                 ch.planes()
         for ch in chans:
             ch.corrected(pass_sp)
-        if dist_on and a.merge == "batched":
+        if dist_on and merge_mode == "batched":
             with torch.cuda.stream(stream):
                 e2 = chans[0].event() if timing["on"] else None
                 merge_counts_multi([ch.ops for ch in chans], D)
@@ -1589,7 +1627,7 @@ def main():
         ct = CollectiveTimer(torch, dev)
         for ch in chans:
             ch.stats()
-        if a.merge == "batched":
+        if merge_mode == "batched":
             with torch.cuda.stream(stream):
                 merge_welford_multi([ch.ops for ch in chans], D, n_totals=[n_channel] * CH,
                                     timer=ct)
@@ -1599,7 +1637,7 @@ def main():
                     merge_welford(ch.ops, D, n_total=n_channel, timer=ct)
         for ch in chans:
             ch.apply()
-        if a.merge == "batched":
+        if merge_mode == "batched":
             with torch.cuda.stream(stream):
                 merge_counts_multi([ch.ops for ch in chans], D, timer=ct)
         else:
@@ -1831,7 +1869,7 @@ def main():
                        "jobs_in_flight": J,
                        "planes": a.planes,
                        "channel_order": a.channel_order if CH > 1 else None,
-                       "merge": a.merge if dist_on else None,
+                       "merge": merge_mode if dist_on else None,
                        "job_choice": choice,
                        "jobs_order": a.jobs_order if J > 1 else None,
                        "hbm_layout": (("sites in one buffer, corrected output in blocks of %d "
@@ -1844,7 +1882,7 @@ def main():
             "kernels": kdetail,
         }
         if merge_ms is not None:
-            if a.merge == "batched":
+            if merge_mode == "batched":
                 resd["merge_all_channels"] = dict(merge_ms[0], note=(
                     "batched: one collective per quantity for the %d channels" % CH))
             else:
