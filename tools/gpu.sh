@@ -114,6 +114,12 @@ for step in "$@"; do
         > $O/bench_input_$TAG.json 2> $O/bench_input_$TAG.err || exit $?
       tail -c 1500 $O/bench_input_$TAG.json
       ;;
+    inflate)
+      # GPU inflate kernels: inflate[:MODES] (comma list of TMH_INFLATE_MODE) -> bench_inflate_TAG.json
+      timeout -k 10 600 python tools/bench_inflate.py --block 128 --modes ${a1:-wave,lane} \
+        > $O/bench_inflate_$TAG.json 2> $O/bench_inflate_$TAG.err || exit $?
+      grep mode $O/bench_inflate_$TAG.err
+      ;;
     pytest)
       # a subset of the GPU tests: pytest:EXPR (-k expression)
       timeout -k 10 900 python -u -m pytest tests -m gpu -v -ra --timeout 300 --timeout-method thread \
