@@ -141,14 +141,20 @@ def parse():
     p.add_argument("--merge", choices=["batched", "per-channel"], default="batched",
                    help="N > 1 / forced distributed: the channels' merges with one collective per "
                         "quantity for all channels (sharded.merge_*_multi) or per channel")
-    p.add_argument("--channel-order", choices=["pipelined", "serial", "concurrent"],
+    p.add_argument("--channel-order", choices=["pipelined", "deep", "serial", "concurrent"],
                    default="pipelined",
                    help="several channels: their Welford passes, then their corrected passes, "
                         "one after another on one pass stream, each channel's merges and planes "
                         "on its own stream under the other channels' passes (pipelined); the "
                         "same with every channel's merge and planes batched between the two "
                         "sweeps (serial); or each channel's passes on its own stream at once "
-                        "(concurrent)")
+                        "(concurrent); or job p+1's Welford passes before job p's corrected "
+                        "pass, every small step of the jobs in flight under a Welford pass (deep, "
+                        "three channel sets: measured slower, DESIGN.md 10.3)")
+    p.add_argument("--pass-launch", choices=["multi", "per-channel"], default="multi",
+                   help="several channels, serial or pipelined order: every channel's corrected "
+                        "pass in ONE fused launch (tmh_correct_u16_hist_multi_blocks_device) or "
+                        "one launch per channel")
     p.add_argument("--fused-bands", type=int, default=None,
                    help="TMH_OPT_FUSED_BANDS: pixel bands of the fused pass (default: automatic)")
     p.add_argument("--channel-streams", choices=["per-channel", "one"], default="per-channel",
@@ -1336,6 +1342,8 @@ def main():
     fused = a.pipeline == "fused"
     prof = not a.no_profile
 
+    probe_sp = [None]  # several channels: the site probes' own stream (set below)
+
     class Channel(object):
         """One channel's job: its sites, statistics handle, corrector and
         stream (channel 0 runs on the main stream; with several channels the
@@ -1395,12 +1403,15 @@ def main():
         def reset_probe(self):
             """The job's reset, and its site probe queued at once (no wait):
             with several channels every probe is in flight before any
-            channel's Welford launch waits for its own."""
+            channel's Welford launch waits for its own.  The probe reads only
+            the (resident) sites: on the probe stream it need not wait for
+            the handle's queued work (tmhip.h)."""
             hip.check(L.tmh_stats_reset(self.h))
+            sp = probe_sp[0] or self.sp
             if fused and B and not in_contig:
-                hip.check(L.tmh_stats_probe_blocks_device(self.h, self.T_in, shift, S, self.sp))
+                hip.check(L.tmh_stats_probe_blocks_device(self.h, self.T_in, shift, S, sp))
             else:
-                hip.check(L.tmh_stats_probe_device(self.h, self.S_ptr, S, self.sp))
+                hip.check(L.tmh_stats_probe_device(self.h, self.S_ptr, S, sp))
 
         def welford(self, sp=None):
             sp = sp or self.sp  # another stream: the library orders it against the handle's
@@ -1455,18 +1466,38 @@ def main():
             L.tmh_corrector_destroy(self.corr)
             L.tmh_stats_destroy(self.h)
 
-    def planes_multi(jobs):
+    def planes_multi(jobs, sp=None, unsmoothed=True):
         """The planes step of several jobs (a rank's channels) in one launch per
-        kernel (tmh_job_planes_multi_device), on the first job's stream: the
-        library orders it after every job's stream and every job's stream
-        after it."""
+        kernel (tmh_job_planes_multi_device), on the first job's stream (or
+        sp): the library orders it after every job's stream and every job's
+        stream after it.  unsmoothed=False: only the smoothed planes the
+        correction needs (no finalize launch)."""
         n = len(jobs)
         arr = lambda xs: (C.c_void_p * n)(*[C.c_void_p(x) for x in xs])  # noqa: E731
         hip.check(L.tmh_job_planes_multi_device(
             arr([j.h.value for j in jobs]), arr([j.corr.value for j in jobs]), n,
-            arr([j.mean.data_ptr() for j in jobs]), arr([j.std.data_ptr() for j in jobs]),
+            arr([j.mean.data_ptr() for j in jobs]) if unsmoothed else None,
+            arr([j.std.data_ptr() for j in jobs]) if unsmoothed else None,
             arr([j.smean.data_ptr() for j in jobs]), arr([j.sstd.data_ptr() for j in jobs]),
-            5.0, jobs[0].sp))
+            5.0, sp or jobs[0].sp))
+
+    def corrected_multi(jobs, sp):
+        """Every job's corrected pass in one fused launch on sp (the library
+        orders it after each job's handle stream; each job's histogram tail on
+        its handle's tail stream)."""
+        n = len(jobs)
+        arr = lambda xs: (C.c_void_p * n)(*[C.c_void_p(x) for x in xs])  # noqa: E731
+        ns = (C.c_int64 * n)(*[S] * n)
+        if B:
+            hip.check(L.tmh_correct_u16_hist_multi_blocks_device(
+                arr([j.corr.value for j in jobs]), arr([j.h.value for j in jobs]), n,
+                arr([j.T_in.value for j in jobs]), arr([j.T_out.value for j in jobs]), shift, ns,
+                -1, -1, sp))
+        else:
+            hip.check(L.tmh_correct_u16_hist_multi_device(
+                arr([j.corr.value for j in jobs]), arr([j.h.value for j in jobs]), n,
+                arr([j.S_ptr.value for j in jobs]), arr([j.O_ptr.value for j in jobs]), ns,
+                -1, -1, sp))
 
     # jobs in flight (one channel, one rank): lanes share the sites and the
     # output blocks; job k runs on lane k % J after job k-1's corrected pass
@@ -1481,21 +1512,105 @@ def main():
     # their own (each streaming pass alone on the GPU; the library orders it
     # against the channel's handle stream, and each channel's histogram tail
     # runs on its handle's tail stream under the next channel's pass)
-    pass_stream = (torch.cuda.Stream(dev) if CH > 1 and a.channel_order in ("serial", "pipelined")
+    pass_stream = (torch.cuda.Stream(dev) if CH > 1 and a.channel_order in ("serial", "pipelined",
+                                                                         "deep")
                    else None)
     evs_p = {}
     # the pipelined order merges each channel on its own stream as soon as its
     # pass is done (one collective per quantity and channel)
-    merge_mode = "per-channel" if a.channel_order == "pipelined" and CH > 1 else a.merge
+    merge_mode = ("per-channel" if a.channel_order == "pipelined" and CH > 1 else
+                  "batched" if a.channel_order == "deep" and CH > 1 else a.merge)
     pass_sp = C.c_void_p(pass_stream.cuda_stream) if pass_stream is not None else None
-    jobs = {"k": 0, "applied": None, "welford": None}
+    multi_pass = pass_sp is not None and fused and a.pass_launch == "multi"
+    # several channels on the pass stream: consecutive jobs (steps) alternate
+    # between --jobs-in-flight sets of channel handles / correctors, so the
+    # next job's reset and site probe are queued under this job's passes and
+    # its first Welford pass needs nothing of this job's histogram tails and
+    # count merges (the same jobs in flight as the one-channel headline)
+    CJ = max(1, a.jobs_in_flight) if (pass_sp is not None and fused) else 1
+    # --channel-order deep: job p+1's Welford passes run before job p's
+    # corrected pass, so job p's merges and planes (and job p-1's count
+    # merges, histogram tails and the next job's probe) all run under Welford
+    # passes; three channel sets (jobs p-1, p, p+1 in flight)
+    deep = a.channel_order == "deep" and pass_sp is not None and fused and B
+    if pass_sp is not None:
+        probe_stream = torch.cuda.Stream(dev)
+        probe_sp[0] = C.c_void_p(probe_stream.cuda_stream)
+    if deep:
+        CJ = max(3, CJ)
+        small_stream = torch.cuda.Stream(dev)
+        small_sp = C.c_void_p(small_stream.cuda_stream)
+    sets = [chans] + [[Channel(c, lane=j) for c in range(CH)] for j in range(1, CJ)]
+
+    def corrected_all(X):
+        if multi_pass:
+            corrected_multi(X, pass_sp)
+        else:
+            for ch in X:
+                ch.corrected(pass_sp)
+    jobs = {"k": 0, "applied": None, "welford": None, "probed": set(), "p": None,
+            "counts": None}
+
+    def deep_step(last=False):
+        """One period of the deep order (job p): job p+1's Welford passes,
+        job p-1's count merges, job p+2's reset and probe, job p's merges and
+        planes, job p's corrected pass.  Per period exactly one job's passes;
+        the first period's job p+1 Welford passes follow a prologue (job p's)."""
+        S_ = lambda j: sets[j % CJ]  # noqa: E731
+        if jobs["p"] is None:  # prologue (warm-up): job 0's reset, probe and Welford passes
+            jobs["p"] = 0
+            for ch in S_(0):
+                ch.reset_probe()
+            for ch in S_(0):
+                ch.welford(pass_sp)
+            for ch in S_(1):
+                ch.reset_probe()
+        p = jobs["p"]
+        for ch in S_(p + 1):  # probed a period ago: no host wait
+            ch.welford(pass_sp)
+        if jobs["counts"] is not None:  # job p-1's count merges (after its tails)
+            if dist_on:
+                with torch.cuda.stream(small_stream):
+                    merge_counts_multi([ch.ops for ch in jobs["counts"]], D)
+            jobs["counts"] = None
+        if not last:  # job p+2 reuses job p-1's set: after its count merges
+            for ch in S_(p + 2):
+                ch.reset_probe()
+        X = S_(p)
+        if dist_on:
+            with torch.cuda.stream(small_stream):
+                merge_welford_multi([ch.ops for ch in X], D, n_totals=[n_channel] * CH)
+        planes_multi(X, sp=small_sp, unsmoothed=False)
+        corrected_all(X)
+        jobs["counts"] = X
+        jobs["p"] = p + 1
+
+    def deep_drain():
+        """Untimed, after the timed periods: the in-flight jobs completed
+        (job p-1's count merges; job p's merges, planes and corrected pass)."""
+        if jobs["counts"] is not None and dist_on:
+            with torch.cuda.stream(small_stream):
+                merge_counts_multi([ch.ops for ch in jobs["counts"]], D)
+        X = sets[jobs["p"] % CJ]
+        if dist_on:
+            with torch.cuda.stream(small_stream):
+                merge_welford_multi([ch.ops for ch in X], D, n_totals=[n_channel] * CH)
+        planes_multi(X, sp=small_sp, unsmoothed=False)
+        corrected_all(X)
+        if dist_on:
+            with torch.cuda.stream(small_stream):
+                merge_counts_multi([ch.ops for ch in X], D)
+        jobs["counts"] = None
 
     log("%d channel(s) x %d sites resident; warm-up" % (CH, S))
     beat("warm-up")
 
     timing = {"on": False}
 
-    def step():
+    def step(last=False):
+        if deep:
+            deep_step(last)
+            return
         if J > 1:
             ch = lanes[jobs["k"] % J]
             jobs["k"] += 1
@@ -1513,6 +1628,23 @@ def main():
             ev.record(ch.cstream)
             jobs["applied"] = ev
             return
+        X = sets[jobs["k"] % CJ]
+        Y = sets[(jobs["k"] + 1) % CJ]
+        jobs["k"] += 1
+
+        def reset_probe(Z):
+            if id(Z) not in jobs["probed"]:
+                for ch in Z:
+                    ch.reset_probe()
+            jobs["probed"].discard(id(Z))
+
+        def prefetch():
+            # the next job's reset and site probe (channel set Y), queued on
+            # Y's streams now: they run under this job's passes
+            if CJ > 1 and not last:
+                for ch in Y:
+                    ch.reset_probe()
+                jobs["probed"].add(id(Y))
         if a.channel_order == "pipelined":
             # every channel's probe queued, then the Welford passes one after
             # another on the pass stream; channel c's merge and planes on its
@@ -1521,61 +1653,59 @@ def main():
             # stream (each after its channel's planes: the library's stream
             # contract), each channel's tail and count merge under the next
             # channel's corrected pass
-            for ch in chans:
-                ch.reset_probe()
-            for ch in chans:
+            reset_probe(X)
+            for ch in X:
                 ch.welford(pass_sp)
-            for ch in chans:
+            prefetch()
+            for ch in X:
                 with torch.cuda.stream(ch.stream):
                     if dist_on:
                         e0 = ch.event() if timing["on"] else None
                         merge_welford(ch.ops, D, n_total=n_channel)
                         evs_p[id(ch)] = [e0, ch.event() if timing["on"] else None]
                 ch.planes()
-            for ch in chans:
-                ch.corrected(pass_sp)
+            corrected_all(X)
             if dist_on:
-                for ch in chans:
+                for ch in X:
                     with torch.cuda.stream(ch.stream):
                         e2 = ch.event() if timing["on"] else None
                         merge_counts(ch.ops, D)
                         if timing["on"]:
                             ch.merge_ev.append(evs_p[id(ch)] + [e2, ch.event()])
             return
-        for ch in chans:  # every channel's probe queued before any Welford launch waits
-            ch.reset_probe()
-        for ch in chans:
+        reset_probe(X)  # every channel's probe queued before any Welford launch waits
+        for ch in X:
             ch.welford(pass_sp)
+        prefetch()
         evs = {}
         if dist_on and merge_mode == "batched":
             # every channel's merge on the main stream, one collective per
             # quantity for all channels (the library orders each handle's
             # stream against it: tmhip.h stream contract)
             with torch.cuda.stream(stream):
-                e0 = chans[0].event() if timing["on"] else None
-                merge_welford_multi([ch.ops for ch in chans], D, n_totals=[n_channel] * CH)
-                evs["batched"] = [e0, chans[0].event() if timing["on"] else None]
+                e0 = X[0].event() if timing["on"] else None
+                merge_welford_multi([ch.ops for ch in X], D, n_totals=[n_channel] * CH)
+                evs["batched"] = [e0, X[0].event() if timing["on"] else None]
         elif dist_on:
-            for ch in chans:
+            for ch in X:
                 with torch.cuda.stream(ch.stream):
                     e0 = ch.event() if timing["on"] else None
                     merge_welford(ch.ops, D, n_total=n_channel)
                     evs[id(ch)] = [e0, ch.event() if timing["on"] else None]
         if a.planes == "multi":
-            planes_multi(chans)
+            planes_multi(X)
         else:
-            for ch in chans:
+            for ch in X:
                 ch.planes()
-        for ch in chans:
-            ch.corrected(pass_sp)
+        corrected_all(X)
         if dist_on and merge_mode == "batched":
             with torch.cuda.stream(stream):
-                e2 = chans[0].event() if timing["on"] else None
-                merge_counts_multi([ch.ops for ch in chans], D)
+                e2 = X[0].event() if timing["on"] else None
+                merge_counts_multi([ch.ops for ch in X], D)
                 if timing["on"]:
-                    chans[0].merge_ev.append(evs["batched"] + [e2, chans[0].event()])
+                    X[0].merge_ev.append(evs["batched"] + [e2, X[0].event()])
         elif dist_on:
-            for ch in chans:
+            for ch in X:
                 with torch.cuda.stream(ch.stream):
                     e2 = ch.event() if timing["on"] else None
                     merge_counts(ch.ops, D)
@@ -1599,7 +1729,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         beat.step = " (timed step %d)" % i
-        step()
+        step(last=i == a.steps - 1)
     beat.step = ""
     beat("synchronize after the timed steps", echo=False)
     torch.cuda.synchronize(dev)
@@ -1622,6 +1752,9 @@ def main():
             if k.value:
                 kern[name] = (ms.value / k.value, k.value)
         L.tmh_profile_enable(0)
+    if deep:  # the jobs in flight completed (untimed) before the checks
+        deep_drain()
+        torch.cuda.synchronize(dev)
     collectives = None
     if dist_on and prof:  # one more step with every collective timed on its own
         ct = CollectiveTimer(torch, dev)
@@ -1660,7 +1793,8 @@ def main():
     # against its oracle fingerprint (tests/golden/make_bench_fingerprint.py)
     check, check_ok = {}, None
     per_channel = {}
-    for c, ch in list(enumerate(chans)) + [(0, ln) for ln in lanes[len(chans):]]:
+    for c, ch in (list(enumerate(chans)) + [(0, ln) for ln in lanes[len(chans):]] +
+                  [(c, ch) for X in sets[1:] for c, ch in enumerate(X)]):
         nn = C.c_int64()
         res = {"mean": np.empty(npx), "std": np.empty(npx), "acc": np.empty(Q),
                "hist": np.empty(65536, np.uint64)}
@@ -1696,7 +1830,7 @@ def main():
                 "wrap_flips": int(cnt[4])}
             per_channel[c] = per_channel.get(c, True) and all(oks.values())
         if ch.lane > 0:  # the other jobs-in-flight lane(s): their own statistics, same outputs
-            check.setdefault("lanes", {})["lane%d" % ch.lane] = chk
+            check.setdefault("lanes", {})["lane%d" % ch.lane + ("_c%d" % c if c else "")] = chk
         elif c == 0:
             check = chk
         else:
@@ -1783,8 +1917,11 @@ def main():
         dominant = max((n for n in kern if n in alg), key=lambda n: alg[n], default=None)
         roofline = None
         if dominant:
-            avg_ms = kern[dominant][0]
-            ach = alg[dominant] / (avg_ms * 1e-3) / 1e9
+            avg_ms, k_launch = kern[dominant]
+            # one launch may carry several channels' jobs (--pass-launch multi)
+            jobs_per_launch = max(1, int(round(a.steps * CH / k_launch)))
+            alg_launch = alg[dominant] * jobs_per_launch
+            ach = alg_launch / (avg_ms * 1e-3) / 1e9
             # PMC traffic (tools/pmc_traffic.py) of THIS library build only:
             # the summary names the sha256 of the library it was measured on
             traffic, traffic_src = None, None
@@ -1805,7 +1942,7 @@ def main():
             roofline = {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                         "traffic": traffic, "traffic_source": traffic_src,
-                        "alg_bytes_per_launch": alg[dominant],
+                        "alg_bytes_per_launch": alg_launch, "jobs_per_launch": jobs_per_launch,
                         "timed": "HIP events around the launch of the one configuration the job "
                                  "runs, on its stream (tmh_profile_*)"}
             if J > 1:
@@ -1866,9 +2003,10 @@ def main():
                        "corrected_outputs": ("channels share output blocks except the checked "
                                              "sites' blocks" if share_out else "private"),
                        "pipeline": a.pipeline,
-                       "jobs_in_flight": J,
+                       "jobs_in_flight": J if CH == 1 else CJ,
                        "planes": a.planes,
                        "channel_order": a.channel_order if CH > 1 else None,
+                       "pass_launch": ("multi" if multi_pass else "per-channel") if CH > 1 else None,
                        "merge": merge_mode if dist_on else None,
                        "job_choice": choice,
                        "jobs_order": a.jobs_order if J > 1 else None,
@@ -1881,7 +2019,7 @@ def main():
             "roofline": roofline,
             "kernels": kdetail,
         }
-        if merge_ms is not None:
+        if merge_ms:
             if merge_mode == "batched":
                 resd["merge_all_channels"] = dict(merge_ms[0], note=(
                     "batched: one collective per quantity for the %d channels" % CH))

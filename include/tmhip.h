@@ -132,7 +132,11 @@ int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites,
  * the handle's, the work runs after everything already queued on the
  * handle's stream, and the handle's stream waits for it before any later work
  * on the handle (finalize, merge, ...), so results read on the handle's
- * stream are complete. */
+ * stream are complete.  The wait is queued with the handle's next work (a
+ * wait queued at once would hold up every stream sharing the handle stream's
+ * hardware queue until the awaited pass ended): work a caller queues on the
+ * handle's stream itself, outside this library, is not ordered after it --
+ * order such work against the caller's stream, or synchronise. */
 int tmh_stats_update_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
                             int log_transform, void* stream);
 /* Per-site zero-pixel counts of the LAST CHUNK of the last update call: the
@@ -159,7 +163,12 @@ int tmh_stats_update_welford_device(tmh_stats* h, const uint16_t* dev_sites, int
  * streams (a rank's channels) queues every job's probe first, so that no
  * launch waits for another job's kernels to drain before its probe can run.
  * Optional: a job not probed this way is probed by its first Welford launch.
- * Same stream contract as the updates (below). */
+ * Stream: the probe reads only the sites and its counts go to the host, so
+ * it is ordered after `stream`'s queued work alone (the sites must be ready
+ * there; NULL: the handle's stream) and nothing of the handle waits for it:
+ * on a stream of its own it runs as soon as the sites are, whatever the
+ * handle still has queued (the previous job's merges and tails).  Call it
+ * after tmh_stats_reset. */
 int tmh_stats_probe_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
                            void* stream);
 int tmh_stats_probe_blocks_device(tmh_stats* h, const uint16_t* const* dev_blocks, int block_shift,
@@ -364,6 +373,27 @@ int tmh_correct_u16_hist_blocks_device(tmh_corrector* c, tmh_stats* h,
                                        const uint16_t* const* dev_in_blocks,
                                        uint16_t* const* dev_out_blocks, int block_shift,
                                        int64_t n_sites, int clip_lo, int clip_hi, void* stream);
+/* n <= 8 jobs' tmh_correct_u16_hist_device (the same image size and
+ * transform, each job its own corrector and statistics handle, n_sites[k]
+ * pending sites of handle k) in ONE fused launch when their configurations
+ * agree (a rank's channels: a short job's launch otherwise pays the pass's
+ * fill and drain on its own); a job whose configuration differs, or which
+ * needs the two-pass path, gets its own launch on the same stream.  Runs on
+ * `stream` (NULL: the first corrector's); the stream contract of the
+ * single-job call holds for every job (each after its handle's queued work,
+ * each handle's stream after its job's tail).  Results identical to the
+ * per-job calls. */
+int tmh_correct_u16_hist_multi_device(tmh_corrector* const* cs, tmh_stats* const* hs, int n,
+                                      const uint16_t* const* dev_in, uint16_t* const* dev_out,
+                                      const int64_t* n_sites, int clip_lo, int clip_hi,
+                                      void* stream);
+/* The same on the blocked layout: per job an input and an output block table
+ * (device arrays of block pointers), one block_shift for all. */
+int tmh_correct_u16_hist_multi_blocks_device(tmh_corrector* const* cs, tmh_stats* const* hs,
+                                             int n, const uint16_t* const* const* dev_in_blocks,
+                                             uint16_t* const* const* dev_out_blocks,
+                                             int block_shift, const int64_t* n_sites, int clip_lo,
+                                             int clip_hi, void* stream);
 int tmh_correct_u8(tmh_corrector* c, const uint8_t* host_in, uint8_t* host_out, int64_t n_sites,
                    int clip_lo, int clip_hi);
 /* ---- illuminati chain ------------------------------

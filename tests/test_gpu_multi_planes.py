@@ -10,12 +10,16 @@ results must be BIT-identical to finalize + smooth2 + corrector update per
 job -- unsmoothed and smoothed planes, the correctors' global means and the
 corrected pixels -- for sigma 5 (one-pass smoothing) and another sigma
 (finalize into scratch, two passes), and for a job of one site (std NaN).
+The jobs' corrected passes share one fused launch
+(tmh_correct_u16_hist_multi_device): per-site histograms, percentile sums and
+corrected pixels bit-identical to one launch per job.
 """
 import ctypes as C
 
 import numpy as np
 import pytest
 
+from oracle import corilla_oracle as orc
 from test_gpu_parity import Dev
 
 pytestmark = pytest.mark.gpu
@@ -71,6 +75,7 @@ def test_job_planes_multi_bit_identical(L, sigma, ns):
             for j in range(n):
                 m, sd, sm, ss, t, t2 = pl[j]
                 hip.check(L.tmh_stats_finalize_device(hs[j], m.p, sd.p, None))
+                L.tmh_synchronize(None)  # handle's stream -> null stream
                 hip.check(L.tmh_smooth2_f64_device(m.p, sd.p, sm.p, ss.p, t.p, t2.p, H, W, sigma,
                                                    None))
                 hip.check(L.tmh_corrector_update_device(cs[j], sm.p, ss.p, None))
@@ -161,3 +166,144 @@ def test_corrector_update_multi_equals_single(L):
         ds.free()
     d_in.free()
     d_out.free()
+
+
+@pytest.mark.parametrize("layout", ["contiguous", "blocks"])
+def test_correct_hist_multi_equals_per_job(L, layout):
+    """tmh_correct_u16_hist_multi(_blocks)_device against one
+    tmh_correct_u16_hist(_blocks)_device per job: corrected pixels, per-site
+    histograms, pooled histogram, order statistics (percentile sums) and
+    moments bit for bit.  Jobs 0 and 2 share the narrow configuration (one
+    launch); job 1 is bright (packed configuration: its own launch)."""
+    import torch
+
+    from tmlibrary_amd import hip, synth
+    from tmlibrary_amd.image import ZERO_LOG10
+    from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
+    H, W = 216, 256
+    npx = H * W
+    ns = (9, 8, 5)
+    n = len(ns)
+    kinds = (synth.STANDARD, synth.BRIGHT, synth.STANDARD)
+    sites = [np.stack([synth.synth_exact_host(H, W, 500 + j, j, i, kinds[j]) for i in range(k)])
+             for j, k in enumerate(ns)]
+    sites[1][:, :3, :40] = 60000  # values beyond the packed slices (rare lists)
+    lo, hi, gamma = quantile_table(npx, np.linspace(0, 100, 1000))
+    lut = stats_log10_lut()
+    d_in = [Dev(L, s.nbytes) for s in sites]
+    for d, s in zip(d_in, sites):
+        d.put(s)
+    shift = 2  # blocks of 4 sites
+    dev = torch.device("cuda", 0)
+    res = {}
+    for mode in ("per-job", "multi"):
+        d_out = [Dev(L, s.nbytes) for s in sites]
+        hs, cs, planes = [], [], []
+        for j in range(n):
+            h = C.c_void_p()
+            hip.check(L.tmh_stats_create(H, W, len(lo), hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
+                                         hip.ptr(lut), 1, hip.TMH_STATS_KEEP_SITE_HIST,
+                                         C.byref(h)))
+            hs.append(h)
+            planes.append([Dev(L, npx * 8) for _ in range(6)])
+        L.tmh_synchronize(None)
+        for j in range(n):
+            c = C.c_void_p()
+            hip.check(L.tmh_corrector_create_device(planes[j][0].p, planes[j][1].p, H, W, 1,
+                                                    ZERO_LOG10, None, C.byref(c)))
+            cs.append(c)
+        tabs = []
+        if layout == "blocks":
+            for j in range(n):
+                nb = (ns[j] + 3) >> shift
+                ti = torch.tensor([d_in[j].p.value + b * 4 * npx * 2 for b in range(nb)],
+                                  dtype=torch.int64, device=dev)
+                to = torch.tensor([d_out[j].p.value + b * 4 * npx * 2 for b in range(nb)],
+                                  dtype=torch.int64, device=dev)
+                tabs.append((ti, to))
+        L.tmh_synchronize(None)
+        torch.cuda.synchronize()
+        for j in range(n):
+            m, sd, sm, ss, t, t2 = planes[j]
+            hip.check(L.tmh_stats_reset(hs[j]))
+            hip.check(L.tmh_stats_update_welford_device(hs[j], d_in[j].p, ns[j], 1, None))
+            hip.check(L.tmh_stats_finalize_device(hs[j], m.p, sd.p, None))
+            # (the handle's stream, the null stream and the corrector's: one
+            # device synchronisation between them; the stream contract of the
+            # corrected passes is what is under test below)
+            L.tmh_synchronize(None)
+            hip.check(L.tmh_smooth2_f64_device(m.p, sd.p, sm.p, ss.p, t.p, t2.p, H, W, 5.0, None))
+            hip.check(L.tmh_corrector_update_device(cs[j], sm.p, ss.p, None))
+            L.tmh_synchronize(None)
+        ps = torch.cuda.Stream(dev)
+        sp = C.c_void_p(ps.cuda_stream)
+        arr = lambda xs: (C.c_void_p * n)(*[C.c_void_p(x) for x in xs])  # noqa: E731
+        if mode == "per-job":
+            for j in range(n):
+                if layout == "blocks":
+                    hip.check(L.tmh_correct_u16_hist_blocks_device(
+                        cs[j], hs[j], C.c_void_p(tabs[j][0].data_ptr()),
+                        C.c_void_p(tabs[j][1].data_ptr()), shift, ns[j], -1, -1, sp))
+                else:
+                    hip.check(L.tmh_correct_u16_hist_device(cs[j], hs[j], d_in[j].p, d_out[j].p,
+                                                            ns[j], -1, -1, sp))
+        else:
+            nn = (C.c_int64 * n)(*ns)
+            if layout == "blocks":
+                hip.check(L.tmh_correct_u16_hist_multi_blocks_device(
+                    arr([c.value for c in cs]), arr([h.value for h in hs]), n,
+                    arr([t[0].data_ptr() for t in tabs]), arr([t[1].data_ptr() for t in tabs]),
+                    shift, nn, -1, -1, sp))
+            else:
+                hip.check(L.tmh_correct_u16_hist_multi_device(
+                    arr([c.value for c in cs]), arr([h.value for h in hs]), n,
+                    arr([d.p.value for d in d_in]), arr([d.p.value for d in d_out]), nn, -1, -1, sp))
+        cfg = []
+        for j in range(n):
+            fc = C.c_int()
+            hip.check(L.tmh_stats_job_choice(hs[j], None, None, C.byref(fc)))
+            cfg.append(fc.value)
+        assert cfg == [3, 5, 3], cfg
+        L.tmh_synchronize(None)
+        torch.cuda.synchronize()
+        out = []
+        for j in range(n):
+            nn_ = C.c_int64()
+            mean, std = np.empty(npx), np.empty(npx)
+            acc = np.empty(len(lo))
+            hist = np.empty(65536, np.uint64)
+            hip.check(L.tmh_stats_finalize(hs[j], C.byref(nn_), hip.ptr(mean), hip.ptr(std),
+                                           hip.ptr(acc), hip.ptr(hist)))
+            sh = []
+            for i in range(ns[j]):
+                x = np.empty(65536, np.uint32)
+                hip.check(L.tmh_stats_site_histogram(hs[j], i, hip.ptr(x)))
+                sh.append(x)
+            out.append({"n": nn_.value, "mean": mean, "std": std, "acc": acc, "hist": hist,
+                        "site_hist": np.stack(sh),
+                        "corrected": d_out[j].get(np.uint16, sites[j].shape)})
+        res[mode] = out
+        for c in cs:
+            L.tmh_corrector_destroy(c)
+        for h in hs:
+            L.tmh_stats_destroy(h)
+        for p in planes:
+            for d in p:
+                d.free()
+        for d in d_out:
+            d.free()
+    for j in range(n):
+        a, b = res["per-job"][j], res["multi"][j]
+        assert a["n"] == b["n"] == ns[j]
+        for k in ("mean", "std", "acc", "hist", "site_hist", "corrected"):
+            if not np.array_equal(a[k], b[k], equal_nan=True):
+                bad = np.argwhere(a[k] != b[k])
+                raise AssertionError("job %d %s: %d of %d differ, first at %s (%s vs %s)" % (
+                    j, k, len(bad), a[k].size, bad[0].tolist(), a[k][tuple(bad[0])],
+                    b[k][tuple(bad[0])]))
+        assert np.array_equal(b["hist"], sum(orc.histogram_u16(x) for x in sites[j])), j
+        for i in (0, ns[j] - 1):
+            assert np.array_equal(b["site_hist"][i].astype(np.uint64),
+                                  orc.histogram_u16(sites[j][i])), (j, i)
+    for d in d_in:
+        d.free()

@@ -70,6 +70,15 @@ def _assert_all_channels(d):
         assert cv["beyond_1DN"] == 0 and cv["wrap_flips"] == 0
         assert cv["sampled_pixels"] == 3 * 65536
     assert d["check_vs_oracle"] is True
+    # consecutive jobs rotate over channel sets (jobs in flight, three in the
+    # default deep order): every set's last job is checked
+    lanes = chk.get("lanes", {})
+    sets = d["config"]["jobs_in_flight"]
+    assert sets == (3 if d["config"]["channel_order"] == "deep" else 2), d["config"]
+    assert len(lanes) == 4 * (sets - 1), sorted(lanes)
+    for name, cc in lanes.items():
+        assert all(v for k, v in cc["vs_oracle"].items() if k != "fingerprint"), (name, cc)
+        assert cc["corrected_vs_oracle"]["beyond_1DN"] == 0
 
 
 @pytest.mark.timeout(600)

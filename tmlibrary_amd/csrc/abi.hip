@@ -247,6 +247,14 @@ struct tmh_stats {
   hipEvent_t ev_tail = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;  // ordering against a caller's stream
+  // work on other streams the handle's stream must wait for, joined lazily
+  // (hstream): a wait enqueued at once would sit in the stream's hardware
+  // queue ahead of unrelated work of every stream sharing that queue until
+  // the awaited pass had finished
+  static constexpr int kJoins = 8;
+  hipEvent_t join_ev[kJoins]{};
+  hipStream_t join_s[kJoins]{};  // one entry per stream: a later record supersedes
+  int join_n = 0;
   int fused_cfg = kFusedAuto;     // TMH_OPT_FUSED_CONFIG (-1: per launch, on the device)
   int wf_parts = 0;               // TMH_OPT_WELFORD_PARTS (0: automatic)
   HostOpts host;                  // TMH_OPT_COPY_THREADS / TMH_OPT_HOST_STAGING
@@ -317,19 +325,55 @@ struct tmh_corrector {
 
 static hipStream_t pick(hipStream_t own, void* s) { return s ? (hipStream_t)s : own; }
 
+// The handle's stream for new work: first it waits for the work on other
+// streams joined since its last use (defer_join).
+static hipStream_t hstream(tmh_stats* h) {
+  for (int i = 0; i < h->join_n; ++i) TMH_HIP(hipStreamWaitEvent(h->stream, h->join_ev[i], 0));
+  h->join_n = 0;
+  return h->stream;
+}
+
+// The stream of an entry point: the caller's, or the handle's (joins first).
+static hipStream_t hpick(tmh_stats* h, void* stream) {
+  return stream ? (hipStream_t)stream : hstream(h);
+}
+
+// The handle's stream must wait for the work queued on s so far: recorded
+// now, waited for when the handle's stream is next used (or by the next
+// cross-stream call, directly).  One entry per stream.
+static void defer_join(tmh_stats* h, hipStream_t s) {
+  int i = 0;
+  while (i < h->join_n && h->join_s[i] != s) ++i;
+  if (i == tmh_stats::kJoins) {  // full: join them now
+    hstream(h);
+    i = 0;
+  }
+  hipEvent_t& e = h->join_ev[i];
+  if (!e) TMH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  TMH_HIP(hipEventRecord(e, s));
+  h->join_s[i] = s;
+  if (i == h->join_n) ++h->join_n;
+}
+
 // Stream contract of the statistics entry points that take a stream
 // (include/tmhip.h): on another stream than the handle's, the work runs after
-// everything queued on the handle's stream, and the handle's stream waits for
-// it before any later work on the handle.
+// everything queued on the handle's stream (and the work joined to it), and
+// the handle's stream waits for it before any later work on the handle.
+// Nothing is queued on the handle's stream here: s waits for the joined
+// work's events itself.
 static void cross_begin(tmh_stats* h, hipStream_t s) {
-  if (s == h->stream) return;
+  if (s == h->stream) {
+    hstream(h);
+    return;
+  }
   TMH_HIP(hipEventRecord(h->ev_in, h->stream));
   TMH_HIP(hipStreamWaitEvent(s, h->ev_in, 0));
+  for (int i = 0; i < h->join_n; ++i)
+    if (h->join_s[i] != s) TMH_HIP(hipStreamWaitEvent(s, h->join_ev[i], 0));
 }
 static void cross_end(tmh_stats* h, hipStream_t s) {
   if (s == h->stream) return;
-  TMH_HIP(hipEventRecord(h->ev_out, s));
-  TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
+  defer_join(h, s);
 }
 
 constexpr int kPooledParts = 16;
@@ -372,7 +416,7 @@ static void stats_reserve_sites(tmh_stats* h, int64_t n_sites) {
                     ((h->flags & 2u) && (size_t)n_sites * kBins > h->site_hist.n) ||
                     (!(h->flags & TMH_STATS_DEFERRED_PCT) && os_words(h, n_sites) > h->vlh.n);
   if (grow) {
-    TMH_HIP(hipStreamSynchronize(h->stream));
+    TMH_HIP(hipStreamSynchronize(hstream(h)));
     TMH_HIP(hipStreamSynchronize(h->side));
   }
   // per-site slabs: hist_hi stays all-zero between launches (the kernel
@@ -401,9 +445,9 @@ static void stats_grow_deferred(tmh_stats* h, int64_t extra) {
     const size_t row = (size_t)kOsTile * 4;
     TMH_HIP(hipMemcpy2DAsync(nb.p, (size_t)cap * row, h->vlh.p, (size_t)h->vlh_cap * row,
                              (size_t)h->n_deferred * row, (size_t)os_tiles(h->Q),
-                             hipMemcpyDeviceToDevice, h->stream));
+                             hipMemcpyDeviceToDevice, hstream(h)));
   }
-  TMH_HIP(hipStreamSynchronize(h->stream));
+  TMH_HIP(hipStreamSynchronize(hstream(h)));
   TMH_HIP(hipStreamSynchronize(h->side));
   std::swap(h->vlh.p, nb.p);
   std::swap(h->vlh.n, nb.n);
@@ -484,6 +528,7 @@ int tmh_stats_create(int height, int width, int n_quantiles, const int64_t* q_lo
 
 void tmh_stats_destroy(tmh_stats* h) {
   if (!h) return;
+  for (int i = 0; i < h->join_n; ++i) (void)hipEventSynchronize(h->join_ev[i]);
   if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
   if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
   hipStream_t s = h->own_stream, side = h->side, tail = h->tail;
@@ -495,6 +540,8 @@ void tmh_stats_destroy(tmh_stats* h) {
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   if (h->ev_out) (void)hipEventDestroy(h->ev_out);
   if (h->ev_probe) (void)hipEventDestroy(h->ev_probe);
+  for (hipEvent_t e : h->join_ev)
+    if (e) (void)hipEventDestroy(e);
   if (h->probe_host) (void)hipHostFree(h->probe_host);
   delete h;
   if (s) (void)hipStreamDestroy(s);
@@ -534,10 +581,10 @@ int tmh_stats_reset(tmh_stats* h) {
     if (h->hist_dirty) {  // an interrupted fused launch: restore the zero-maintained slabs
       TMH_HIP(hipDeviceSynchronize());  // it may have been queued on any stream
       if (h->hist_full.n)
-        TMH_HIP(hipMemsetAsync(h->hist_full.p, 0, h->hist_full.n * 4, h->stream));
+        TMH_HIP(hipMemsetAsync(h->hist_full.p, 0, h->hist_full.n * 4, hstream(h)));
       if (h->hist_rmask.n)
-        TMH_HIP(hipMemsetAsync(h->hist_rmask.p, 0, h->hist_rmask.n * 8, h->stream));
-      TMH_HIP(hipMemsetAsync(h->pooled_parts.p, 0, h->pooled_parts.n * 8, h->stream));
+        TMH_HIP(hipMemsetAsync(h->hist_rmask.p, 0, h->hist_rmask.n * 8, hstream(h)));
+      TMH_HIP(hipMemsetAsync(h->pooled_parts.p, 0, h->pooled_parts.n * 8, hstream(h)));
       h->hist_dirty = false;
     }
     ZeroList z;  // one launch for the job's fresh state
@@ -546,7 +593,7 @@ int tmh_stats_reset(tmh_stats* h) {
     z.add(h->acc.p, h->Q);
     z.add(h->pooled.p, kBins);
     z.add(h->wide.p, 2);
-    launch_zero_u64(z, h->stream);
+    launch_zero_u64(z, hstream(h));
     h->wide_sites = 0;
     h->n = 0;
     h->n_deferred = 0;
@@ -652,7 +699,7 @@ static void stats_update_dev(tmh_stats* h, const uint16_t* d, int64_t ns, int lo
 
 static void stats_welford_dev(tmh_stats* h, const uint16_t* dev_sites, int64_t n_sites,
                               int log_transform, void* stream, const SiteTab& tab) {
-  hipStream_t s = pick(h->stream, stream);
+  hipStream_t s = hpick(h, stream);
   cross_begin(h, s);
   if ((size_t)n_sites > h->rn.n) {
     TMH_HIP(hipStreamSynchronize(s));
@@ -679,10 +726,8 @@ int tmh_stats_probe_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_si
   return guard([&] {
     TMH_CHECK(h && (dev_sites || n_sites == 0) && n_sites >= 0, TMH_EINVAL, "bad arguments");
     if ((h->npx & 7) || (reinterpret_cast<uintptr_t>(dev_sites) & 15)) return;  // no vector path
-    const hipStream_t s = pick(h->stream, stream);
-    cross_begin(h, s);
-    stats_probe_queue(h, dev_sites, n_sites, SiteTab{}, s);
-    cross_end(h, s);
+    // ordered after stream's work only (include/tmhip.h): the counts go to the host
+    stats_probe_queue(h, dev_sites, n_sites, SiteTab{}, hpick(h, stream));
   });
 }
 
@@ -691,10 +736,7 @@ int tmh_stats_probe_blocks_device(tmh_stats* h, const uint16_t* const* dev_block
   return guard([&] {
     TMH_CHECK(h && n_sites >= 0, TMH_EINVAL, "bad arguments");
     const SiteTab tab = blocked_tab(dev_blocks, nullptr, block_shift, h->npx);
-    const hipStream_t s = pick(h->stream, stream);
-    cross_begin(h, s);
-    stats_probe_queue(h, nullptr, n_sites, tab, s);
-    cross_end(h, s);
+    stats_probe_queue(h, nullptr, n_sites, tab, hpick(h, stream));
   });
 }
 
@@ -735,7 +777,7 @@ int tmh_stats_update_device(tmh_stats* h, const uint16_t* dev_sites, int64_t n_s
                             int log_transform, void* stream) {
   return guard([&] {
     TMH_CHECK(h && (dev_sites || n_sites == 0) && n_sites >= 0, TMH_EINVAL, "bad arguments");
-    const hipStream_t s = pick(h->stream, stream);
+    const hipStream_t s = hpick(h, stream);
     cross_begin(h, s);
     stats_update_dev(h, dev_sites, n_sites, log_transform, s);
     cross_end(h, s);
@@ -748,11 +790,8 @@ int tmh_stats_zero_counts(tmh_stats* h, int64_t* host_out, int64_t n, void* stre
     TMH_CHECK(n <= h->last_batch && (size_t)n <= h->zeros.n, TMH_EINVAL,
               "more sites than the last update held");
     if (n == 0) return;
-    hipStream_t s = pick(h->stream, stream);
-    if (s != h->stream) {
-      TMH_HIP(hipEventRecord(h->ev_in, h->stream));
-      TMH_HIP(hipStreamWaitEvent(s, h->ev_in, 0));
-    }
+    hipStream_t s = hpick(h, stream);
+    cross_begin(h, s);
     TMH_HIP(hipMemcpyAsync(host_out, h->zeros.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
   });
 }
@@ -766,7 +805,7 @@ int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites, 
     const int64_t per = h->batch_cap;
     const size_t slot_px = (size_t)per * h->npx;
     if (2 * slot_px > h->stage.n) {
-      TMH_HIP(hipStreamSynchronize(h->stream));
+      TMH_HIP(hipStreamSynchronize(hstream(h)));
       h->stage.ensure(2 * slot_px);
     }
     p.init();
@@ -796,12 +835,12 @@ int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites, 
         uint16_t* dev = h->stage.p + (size_t)slot * slot_px;
         TMH_HIP(hipMemcpyAsync(dev, src, bytes, hipMemcpyHostToDevice, p.h2d));
         TMH_HIP(hipEventRecord(p.ev_in[slot], p.h2d));
-        TMH_HIP(hipStreamWaitEvent(h->stream, p.ev_in[slot], 0));
-        stats_update_dev(h, dev, ns, log_transform, h->stream);
+        TMH_HIP(hipStreamWaitEvent(hstream(h), p.ev_in[slot], 0));
+        stats_update_dev(h, dev, ns, log_transform, hstream(h));
         if (zero_counts_out)
           TMH_HIP(hipMemcpyAsync(p.out[slot].p, h->zeros.p, (size_t)ns * 8, hipMemcpyDeviceToHost,
-                                 h->stream));
-        TMH_HIP(hipEventRecord(p.ev_done[slot], h->stream));
+                                 hstream(h)));
+        TMH_HIP(hipEventRecord(p.ev_done[slot], hstream(h)));
         p.busy[slot] = true;
         p.s0[slot] = s0;
         p.ns[slot] = ns;
@@ -809,7 +848,7 @@ int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites, 
       retire((int)(k & 1));
       retire((int)((k + 1) & 1));
     } catch (...) {
-      p.abandon(h->stream);
+      p.abandon(hstream(h));
       throw;
     }
   });
@@ -817,9 +856,9 @@ int tmh_stats_update(tmh_stats* h, const uint16_t* host_sites, int64_t n_sites, 
 
 static void stats_pct_sum_device(tmh_stats* h) {
   if ((h->flags & TMH_STATS_DEFERRED_PCT) && !h->pct_sum_external) {
-    TMH_HIP(hipMemsetAsync(h->acc.p, 0, (size_t)h->Q * 8, h->stream));
+    TMH_HIP(hipMemsetAsync(h->acc.p, 0, (size_t)h->Q * 8, hstream(h)));
     launch_pct_accumulate(h->vlh.p, h->n_deferred, h->vlh_cap, h->Q, h->gamma.p, h->acc.p,
-                          h->stream);
+                          hstream(h));
   }
 }
 
@@ -830,26 +869,29 @@ int tmh_stats_finalize(tmh_stats* h, int64_t* n, double* mean, double* std, doub
     if (n) *n = h->n;
     if (mean || std) {
       h->tmp_std.ensure(h->npx);
-      launch_finalize(h->mean.p, h->m2.p, h->n, h->npx, nullptr, h->tmp_std.p, h->stream);
+      launch_finalize(h->mean.p, h->m2.p, h->n, h->npx, nullptr, h->tmp_std.p, hstream(h));
       if (mean)
-        TMH_HIP(hipMemcpyAsync(mean, h->mean.p, h->npx * 8, hipMemcpyDeviceToHost, h->stream));
+        TMH_HIP(hipMemcpyAsync(mean, h->mean.p, h->npx * 8, hipMemcpyDeviceToHost, hstream(h)));
       if (std)
-        TMH_HIP(hipMemcpyAsync(std, h->tmp_std.p, h->npx * 8, hipMemcpyDeviceToHost, h->stream));
+        TMH_HIP(hipMemcpyAsync(std, h->tmp_std.p, h->npx * 8, hipMemcpyDeviceToHost, hstream(h)));
     }
     if (pct_sum) {
       stats_pct_sum_device(h);
-      TMH_HIP(hipMemcpyAsync(pct_sum, h->acc.p, (size_t)h->Q * 8, hipMemcpyDeviceToHost, h->stream));
+      TMH_HIP(hipMemcpyAsync(pct_sum, h->acc.p, (size_t)h->Q * 8, hipMemcpyDeviceToHost, hstream(h)));
     }
     if (hist)
-      TMH_HIP(hipMemcpyAsync(hist, h->pooled.p, (size_t)kBins * 8, hipMemcpyDeviceToHost, h->stream));
-    TMH_HIP(hipStreamSynchronize(h->stream));
+      TMH_HIP(hipMemcpyAsync(hist, h->pooled.p, (size_t)kBins * 8, hipMemcpyDeviceToHost, hstream(h)));
+    TMH_HIP(hipStreamSynchronize(hstream(h)));
   });
 }
 
 int tmh_stats_finalize_device(tmh_stats* h, double* dev_mean, double* dev_std, void* stream) {
   return guard([&] {
     TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
-    launch_finalize(h->mean.p, h->m2.p, h->n, h->npx, dev_mean, dev_std, pick(h->stream, stream));
+    const hipStream_t s = hpick(h, stream);
+    cross_begin(h, s);
+    launch_finalize(h->mean.p, h->m2.p, h->n, h->npx, dev_mean, dev_std, s);
+    cross_end(h, s);
   });
 }
 
@@ -857,9 +899,9 @@ int tmh_stats_variance(tmh_stats* h, double* host_var) {
   return guard([&] {
     TMH_CHECK(h && host_var, TMH_EINVAL, "bad arguments");
     h->tmp_std.ensure(h->npx);
-    launch_variance(h->m2.p, h->n, h->npx, h->tmp_std.p, h->stream);
-    TMH_HIP(hipMemcpyAsync(host_var, h->tmp_std.p, h->npx * 8, hipMemcpyDeviceToHost, h->stream));
-    TMH_HIP(hipStreamSynchronize(h->stream));
+    launch_variance(h->m2.p, h->n, h->npx, h->tmp_std.p, hstream(h));
+    TMH_HIP(hipMemcpyAsync(host_var, h->tmp_std.p, h->npx * 8, hipMemcpyDeviceToHost, hstream(h)));
+    TMH_HIP(hipStreamSynchronize(hstream(h)));
   });
 }
 
@@ -881,8 +923,8 @@ int tmh_stats_wide_groups(tmh_stats* h, uint64_t* groups_out, int64_t* sites_out
   return guard([&] {
     TMH_CHECK(h && groups_out, TMH_EINVAL, "bad arguments");
     unsigned long long w = 0;
-    TMH_HIP(hipMemcpyAsync(&w, h->wide.p, 8, hipMemcpyDeviceToHost, h->stream));
-    TMH_HIP(hipStreamSynchronize(h->stream));
+    TMH_HIP(hipMemcpyAsync(&w, h->wide.p, 8, hipMemcpyDeviceToHost, hstream(h)));
+    TMH_HIP(hipStreamSynchronize(hstream(h)));
     *groups_out = w;
     if (sites_out) *sites_out = h->wide_sites;
   });
@@ -891,7 +933,7 @@ int tmh_stats_wide_groups(tmh_stats* h, uint64_t* groups_out, int64_t* sites_out
 int tmh_stats_get_hist_device(tmh_stats* h, uint64_t* dev_hist, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_hist, TMH_EINVAL, "bad arguments");
-    const hipStream_t s = pick(h->stream, stream);
+    const hipStream_t s = hpick(h, stream);
     cross_begin(h, s);
     TMH_HIP(hipMemcpyAsync(dev_hist, h->pooled.p, (size_t)kBins * 8, hipMemcpyDeviceToDevice, s));
     cross_end(h, s);
@@ -901,7 +943,7 @@ int tmh_stats_get_hist_device(tmh_stats* h, uint64_t* dev_hist, void* stream) {
 int tmh_stats_set_hist_device(tmh_stats* h, const uint64_t* dev_hist, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_hist, TMH_EINVAL, "bad arguments");
-    const hipStream_t s = pick(h->stream, stream);
+    const hipStream_t s = hpick(h, stream);
     cross_begin(h, s);
     TMH_HIP(hipMemcpyAsync(h->pooled.p, dev_hist, (size_t)kBins * 8, hipMemcpyDeviceToDevice, s));
     cross_end(h, s);
@@ -914,8 +956,8 @@ int tmh_stats_site_histogram(tmh_stats* h, int64_t site, uint32_t* host_hist) {
     TMH_CHECK(h->flags & 2u, TMH_ESTATE, "handle was created without TMH_STATS_KEEP_SITE_HIST (2)");
     TMH_CHECK(site >= 0 && site < h->last_batch, TMH_EINVAL, "site outside the last batch");
     TMH_HIP(hipMemcpyAsync(host_hist, h->site_hist.p + (size_t)site * kBins, (size_t)kBins * 4,
-                           hipMemcpyDeviceToHost, h->stream));
-    TMH_HIP(hipStreamSynchronize(h->stream));
+                           hipMemcpyDeviceToHost, hstream(h)));
+    TMH_HIP(hipStreamSynchronize(hstream(h)));
   });
 }
 
@@ -930,13 +972,13 @@ int tmh_stats_site_order_stats(tmh_stats* h, int64_t site, uint16_t* host_vlo, u
     std::vector<uint32_t> w((size_t)os_tiles(h->Q) * kOsTile);
     TMH_HIP(hipMemcpy2DAsync(w.data(), row, h->vlh.p + (size_t)site * kOsTile,
                              (size_t)h->vlh_ld * row, row, (size_t)os_tiles(h->Q),
-                             hipMemcpyDeviceToHost, h->stream));
-    TMH_HIP(hipStreamSynchronize(h->stream));
+                             hipMemcpyDeviceToHost, hstream(h)));
+    TMH_HIP(hipStreamSynchronize(hstream(h)));
     for (int64_t q = 0; q < h->Q; ++q) {
       host_vlo[q] = (uint16_t)(w[q] & 0xFFFFu);
       host_vhi[q] = (uint16_t)(w[q] >> 16);
     }
-    TMH_HIP(hipStreamSynchronize(h->stream));
+    TMH_HIP(hipStreamSynchronize(hstream(h)));
   });
 }
 
@@ -957,7 +999,7 @@ int tmh_stats_set_n(tmh_stats* h, int64_t n) {
 int tmh_stats_merge_stage1(tmh_stats* h, double* dev_nmean, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_nmean, TMH_EINVAL, "bad arguments");
-    const hipStream_t s = pick(h->stream, stream);
+    const hipStream_t s = hpick(h, stream);
     cross_begin(h, s);
     launch_merge1(h->mean.p, h->n, h->npx, dev_nmean, s);
     cross_end(h, s);
@@ -968,7 +1010,7 @@ int tmh_stats_merge_stage2(tmh_stats* h, const double* dev_sum_nmean, int64_t n_
                            double* dev_m2c, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_sum_nmean && dev_m2c && n_total > 0, TMH_EINVAL, "bad arguments");
-    const hipStream_t s = pick(h->stream, stream);
+    const hipStream_t s = hpick(h, stream);
     cross_begin(h, s);
     launch_merge2(h->mean.p, h->m2.p, h->n, dev_sum_nmean, n_total, h->npx, dev_m2c, s);
     cross_end(h, s);
@@ -978,7 +1020,7 @@ int tmh_stats_merge_stage2(tmh_stats* h, const double* dev_sum_nmean, int64_t n_
 int tmh_stats_merge_stage3(tmh_stats* h, int64_t n_total, const double* dev_sum_m2c, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_sum_m2c && n_total >= 0, TMH_EINVAL, "bad arguments");
-    const hipStream_t s = pick(h->stream, stream);
+    const hipStream_t s = hpick(h, stream);
     cross_begin(h, s);
     launch_copy_f64(dev_sum_m2c, h->m2.p, h->npx, s);
     cross_end(h, s);
@@ -991,7 +1033,7 @@ int tmh_stats_pct_accumulate(tmh_stats* h, double* dev_acc, void* stream) {
     TMH_CHECK(h && dev_acc, TMH_EINVAL, "bad arguments");
     TMH_CHECK(h->flags & TMH_STATS_DEFERRED_PCT, TMH_ESTATE,
               "percentile chain needs a TMH_STATS_DEFERRED_PCT handle");
-    const hipStream_t s = pick(h->stream, stream);
+    const hipStream_t s = hpick(h, stream);
     cross_begin(h, s);
     launch_pct_accumulate(h->vlh.p, h->n_deferred, h->vlh_cap, h->Q, h->gamma.p, dev_acc, s);
     cross_end(h, s);
@@ -1006,7 +1048,7 @@ int tmh_stats_pct_accumulate_range(tmh_stats* h, double* dev_acc_range, int q_be
               "percentile chain needs a TMH_STATS_DEFERRED_PCT handle");
     TMH_CHECK(q_begin >= 0 && q_count >= 0 && (int64_t)q_begin + q_count <= h->Q, TMH_EINVAL,
               "quantile range out of bounds");
-    const hipStream_t s = pick(h->stream, stream);
+    const hipStream_t s = hpick(h, stream);
     cross_begin(h, s);
     launch_pct_accumulate_range(h->vlh.p, h->n_deferred, h->vlh_cap, q_begin, q_count, h->gamma.p,
                                 dev_acc_range, s);
@@ -1017,7 +1059,7 @@ int tmh_stats_pct_accumulate_range(tmh_stats* h, double* dev_acc_range, int q_be
 int tmh_stats_set_pct_sum(tmh_stats* h, const double* dev_acc, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_acc, TMH_EINVAL, "bad arguments");
-    const hipStream_t s = pick(h->stream, stream);
+    const hipStream_t s = hpick(h, stream);
     cross_begin(h, s);
     launch_copy_f64(dev_acc, h->acc.p, h->Q, s);
     cross_end(h, s);
@@ -1028,22 +1070,16 @@ int tmh_stats_set_pct_sum(tmh_stats* h, const double* dev_acc, void* stream) {
 int tmh_stats_get_pct_sum_device(tmh_stats* h, double* dev_acc, void* stream) {
   return guard([&] {
     TMH_CHECK(h && dev_acc, TMH_EINVAL, "bad arguments");
-    hipStream_t s = pick(h->stream, stream);
+    hipStream_t s = hpick(h, stream);
     const bool cross = s != h->stream;
-    if (cross) {  // after the handle's queued work, and the handle waits for the copy
-      TMH_HIP(hipEventRecord(h->ev_in, h->stream));
-      TMH_HIP(hipStreamWaitEvent(s, h->ev_in, 0));
-    }
+    cross_begin(h, s);  // after the handle's queued work, and the handle waits for the copy
     if ((h->flags & TMH_STATS_DEFERRED_PCT) && !h->pct_sum_external) {
       TMH_HIP(hipMemsetAsync(dev_acc, 0, (size_t)h->Q * 8, s));
       launch_pct_accumulate(h->vlh.p, h->n_deferred, h->vlh_cap, h->Q, h->gamma.p, dev_acc, s);
     } else {
       TMH_HIP(hipMemcpyAsync(dev_acc, h->acc.p, (size_t)h->Q * 8, hipMemcpyDeviceToDevice, s));
     }
-    if (cross) {
-      TMH_HIP(hipEventRecord(h->ev_out, s));
-      TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
-    }
+    if (cross) defer_join(h, s);
   });
 }
 
@@ -1500,136 +1536,184 @@ int tmh_correct_u8(tmh_corrector* c, const uint8_t* host_in, uint8_t* host_out, 
   });
 }
 
+// One job's fused pass (correct + per-site histograms, then the histogram
+// tail), in three steps so several jobs can share the launch in between
+// (tmh_correct_u16_hist_multi_device): fused_prepare -> launch -> fused_finish.
+struct FusedPass {
+  tmh_corrector* c;
+  tmh_stats* h;
+  const uint16_t* in;
+  uint16_t* out;
+  int64_t n;
+  SiteTab tab;
+  hipStream_t s;
+  bool cross;
+  int clip_lo, clip_hi;
+  int cfg;
+  RareList rl;
+  FixList fl;
+  uint32_t* vlh;
+  int64_t ld;
+  uint32_t* sh;
+};
+
+// the fused pass floors zero pixels at 10**zero_log10 in f32 and reads 8-pixel
+// groups: false = the two-pass path for odd shapes
+static bool fused_vec(const tmh_corrector* c, const tmh_stats* h, const uint16_t* dev_in,
+                      const uint16_t* dev_out, const SiteTab& tab) {
+  const bool zl_ok = !c->log_transform || (c->zero_log10 >= -37.0 && c->zero_log10 <= 0.0);
+  const bool vec = zl_ok && (h->npx & 7) == 0 &&
+                   (tab.in || ((reinterpret_cast<uintptr_t>(dev_in) & 15) == 0 &&
+                               (reinterpret_cast<uintptr_t>(dev_out) & 15) == 0));
+  TMH_CHECK(vec || !tab.in, TMH_EINVAL,
+            "a blocked site layout needs the fused pass (zero_log10 in [-37, 0])");
+  return vec;
+}
+
+static void fused_check(const tmh_corrector* c, const tmh_stats* h, int64_t n_sites) {
+  TMH_CHECK(c->npx == h->npx, TMH_EINVAL, "corrector and statistics image sizes differ");
+  TMH_CHECK(n_sites <= h->pending, TMH_ESTATE,
+            "more sites than were passed to tmh_stats_update_welford_device");
+}
+
+// Stream contract (include/tmhip.h): the job's launches run on s, after
+// everything already queued on the statistics handle's stream (and after the
+// corrector's pending tail, which still reads its round masks).
+static bool fused_begin(tmh_corrector* c, tmh_stats* h, hipStream_t s) {
+  const bool cross = s != h->stream;
+  cross_begin(h, s);
+  if (c->tail_pending) {
+    TMH_HIP(hipStreamWaitEvent(s, c->ev_tail, 0));
+    c->tail_pending = false;
+  }
+  return cross;
+}
+
+// buffers, rare lists, fixup list and the configuration of one job's pass
+static void fused_prepare(FusedPass& p) {
+  tmh_stats* h = p.h;
+  tmh_corrector* c = p.c;
+  const int64_t n_sites = p.n;
+  hipStream_t s = p.s;
+  // rare lists (RareList, common.h) for the packed configuration
+  if (h->fused_cfg == kFusedAuto) stats_probe(h, p.in, n_sites, p.tab, s);
+  const bool rl_on = probe_fused_cfg(h) == kFusedWide;
+  const unsigned int rl_cap =
+      (unsigned int)std::min<int64_t>(65536, std::max<int64_t>(1024, h->npx / 64));
+  const bool grow = (size_t)n_sites * kBins > h->hist_full.n || (size_t)n_sites > h->zeros.n ||
+                    (size_t)n_sites > h->hist_rmask.n ||
+                    (rl_on && ((size_t)n_sites * rl_cap > h->rare_v.n ||
+                               (size_t)n_sites > h->rare_n.n)) ||
+                    ((h->flags & 2u) && (size_t)n_sites * kBins > h->site_hist.n) ||
+                    (!(h->flags & TMH_STATS_DEFERRED_PCT) && os_words(h, n_sites) > h->vlh.n);
+  if (grow) {
+    TMH_HIP(hipStreamSynchronize(s));
+    TMH_HIP(hipStreamSynchronize(hstream(h)));
+    TMH_HIP(hipStreamSynchronize(h->side));
+  }
+  if ((size_t)n_sites * kBins > h->hist_full.n) h->hist_full.alloc((size_t)n_sites * kBins, true);
+  if ((size_t)n_sites > h->hist_rmask.n) h->hist_rmask.alloc((size_t)n_sites, true);
+  p.rl = RareList{};
+  if (rl_on) {
+    h->rare_v.ensure((size_t)n_sites * rl_cap);
+    h->rare_n.ensure((size_t)n_sites);
+    TMH_HIP(hipMemsetAsync(h->rare_n.p, 0, (size_t)n_sites * sizeof(unsigned int), s));
+    p.rl = RareList{h->rare_v.p, h->rare_n.p, rl_cap};
+  }
+  h->zeros.ensure((size_t)n_sites);
+  if (h->flags & 2u) h->site_hist.ensure((size_t)n_sites * kBins);
+  if (h->flags & TMH_STATS_DEFERRED_PCT) {
+    stats_grow_deferred(h, n_sites);
+    p.vlh = h->vlh.p + (size_t)h->n_deferred * kOsTile;
+    p.ld = h->vlh_cap;
+  } else {
+    h->vlh.ensure(os_words(h, n_sites));
+    p.vlh = h->vlh.p;
+    p.ld = n_sites;
+  }
+  h->vlh_ld = p.ld;
+  // the histogram slab and round masks are zero-maintained: the fused pass
+  // fills them and k_hist_finalize resets what it read; if anything fails in
+  // between, tmh_stats_reset clears them (hist_dirty)
+  h->hist_dirty = true;
+  p.sh = (h->flags & 2u) ? h->site_hist.p : nullptr;
+  // one configuration, chosen on the host from the job's site probe (probed
+  // at the Welford launch, or above for a job whose Welford pass did not)
+  p.cfg = probe_fused_cfg(h);
+  p.fl = corrector_fixlist(c, n_sites, s);
+}
+
+// what follows the job's fused launch: rare lists, f64 fixups, the very wide
+// configuration's histograms, and the histogram tail
+static void fused_finish(FusedPass& p) {
+  tmh_stats* h = p.h;
+  tmh_corrector* c = p.c;
+  const int64_t n_sites = p.n;
+  hipStream_t s = p.s;
+  const bool very_wide = p.cfg == kFusedNoHist;
+  const unsigned long long* rm_all = reinterpret_cast<const unsigned long long*>(c->queues.p + 8);
+  if (p.cfg == kFusedWide) launch_rare_count(p.rl, h->hist_full.p, n_sites, s);
+  launch_fix_correct(p.in, p.out, 2, c->npx, n_sites, p.fl, c->coef64.p, c->rc.p,
+                     c->log_transform, p.clip_lo, p.clip_hi, s, p.tab);
+  if (very_wide)  // the histograms from one more read of the sites
+    launch_hist_site_u16(p.in, h->npx, n_sites, h->hist_full.p, h->qp, p.vlh, p.ld, h->pooled.p,
+                         h->pooled_parts.p, kPooledParts, h->zeros.p, p.sh, nullptr, 0, s, p.tab);
+  // the Welford pass's diagnostic wide counts restart with the next batch
+  // (reset here on s, before any later Welford launch on the handle)
+  if (h->pending - n_sites == 0) {
+    TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, s));
+    h->wide_sites = 0;
+  }
+  // The histogram tail (order statistics, percentile sums) reads only the
+  // handle's buffers: called on another stream than the handle's, it runs on
+  // the handle's tail stream (the handle's stream waits for it), so s is free
+  // as soon as the corrected sites are written (a caller pipelining jobs
+  // starts the next one's Welford pass under this one's tail).
+  hipStream_t ts = s;
+  if (p.cross) {
+    if (!h->tail) {  // created on first use: every stream takes a hardware queue slot
+      TMH_HIP(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
+      TMH_HIP(hipEventCreateWithFlags(&h->ev_tail, hipEventDisableTiming));
+    }
+    TMH_HIP(hipEventRecord(h->ev_out, s));
+    TMH_HIP(hipStreamWaitEvent(h->tail, h->ev_out, 0));
+    ts = h->tail;
+  }
+  if (!very_wide)
+    launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, n_sites, h->qp, p.vlh, p.ld,
+                         h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, p.sh, ts,
+                         false, rm_all);
+  if (!(h->flags & TMH_STATS_DEFERRED_PCT))
+    launch_pct_accumulate(p.vlh, n_sites, p.ld, h->Q, h->gamma.p, h->acc.p, ts);
+  h->hist_dirty = false;
+  if (h->flags & TMH_STATS_DEFERRED_PCT) h->n_deferred += n_sites;
+  h->last_batch = n_sites;
+  h->pending -= n_sites;
+  if (p.cross) {  // the handle's later work, and this corrector's next pass, after the tail
+    defer_join(h, ts);
+    if (!c->ev_tail) TMH_HIP(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
+    TMH_HIP(hipEventRecord(c->ev_tail, ts));
+    c->tail_pending = true;
+  }
+}
+
 static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev_in,
                              uint16_t* dev_out, int64_t n_sites, int clip_lo, int clip_hi,
                              void* stream, const SiteTab& tab) {
   {
-    TMH_CHECK(c->npx == h->npx, TMH_EINVAL, "corrector and statistics image sizes differ");
-    TMH_CHECK(n_sites <= h->pending, TMH_ESTATE,
-              "more sites than were passed to tmh_stats_update_welford_device");
+    fused_check(c, h, n_sites);
     check_clip(clip_lo, clip_hi, 65535);
     if (n_sites == 0) return;
     hipStream_t s = pick(c->stream, stream);
-    // Stream contract (include/tmhip.h): the launches below run on s, after
-    // everything already queued on the statistics handle's stream, and the
-    // handle's stream waits for them before any later work on the handle.
-    const bool cross = s != h->stream;
-    if (cross) {
-      TMH_HIP(hipEventRecord(h->ev_in, h->stream));
-      TMH_HIP(hipStreamWaitEvent(s, h->ev_in, 0));
-    }
-    if (c->tail_pending) {  // an earlier call's tail still reads this corrector's round masks
-      TMH_HIP(hipStreamWaitEvent(s, c->ev_tail, 0));
-      c->tail_pending = false;
-    }
-    // the fused pass floors zero pixels at 10**zero_log10 in f32
-    const bool zl_ok = !c->log_transform || (c->zero_log10 >= -37.0 && c->zero_log10 <= 0.0);
-    const bool vec = zl_ok && (h->npx & 7) == 0 &&
-                     (tab.in || ((reinterpret_cast<uintptr_t>(dev_in) & 15) == 0 &&
-                                 (reinterpret_cast<uintptr_t>(dev_out) & 15) == 0));
-    TMH_CHECK(vec || !tab.in, TMH_EINVAL,
-              "a blocked site layout needs the fused pass (zero_log10 in [-37, 0])");
+    const bool vec = fused_vec(c, h, dev_in, dev_out, tab);
+    const bool cross = fused_begin(c, h, s);
     if (vec) {
-      // rare lists (RareList, common.h) for the packed configuration
-      if (h->fused_cfg == kFusedAuto) stats_probe(h, dev_in, n_sites, tab, s);
-      const bool rl_on = probe_fused_cfg(h) == kFusedWide;
-      const unsigned int rl_cap =
-          (unsigned int)std::min<int64_t>(65536, std::max<int64_t>(1024, h->npx / 64));
-      const bool grow = (size_t)n_sites * kBins > h->hist_full.n || (size_t)n_sites > h->zeros.n ||
-                        (size_t)n_sites > h->hist_rmask.n ||
-                        (rl_on && ((size_t)n_sites * rl_cap > h->rare_v.n ||
-                                   (size_t)n_sites > h->rare_n.n)) ||
-                        ((h->flags & 2u) && (size_t)n_sites * kBins > h->site_hist.n) ||
-                        (!(h->flags & TMH_STATS_DEFERRED_PCT) && os_words(h, n_sites) > h->vlh.n);
-      if (grow) {
-        TMH_HIP(hipStreamSynchronize(s));
-        TMH_HIP(hipStreamSynchronize(h->stream));
-        TMH_HIP(hipStreamSynchronize(h->side));
-      }
-      if ((size_t)n_sites * kBins > h->hist_full.n)
-        h->hist_full.alloc((size_t)n_sites * kBins, true);
-      if ((size_t)n_sites > h->hist_rmask.n) h->hist_rmask.alloc((size_t)n_sites, true);
-      RareList rl{};
-      if (rl_on) {
-        h->rare_v.ensure((size_t)n_sites * rl_cap);
-        h->rare_n.ensure((size_t)n_sites);
-        TMH_HIP(hipMemsetAsync(h->rare_n.p, 0, (size_t)n_sites * sizeof(unsigned int), s));
-        rl = RareList{h->rare_v.p, h->rare_n.p, rl_cap};
-      }
-      h->zeros.ensure((size_t)n_sites);
-      if (h->flags & 2u) h->site_hist.ensure((size_t)n_sites * kBins);
-      uint32_t* vlh;
-      int64_t ld;
-      if (h->flags & TMH_STATS_DEFERRED_PCT) {
-        stats_grow_deferred(h, n_sites);
-        vlh = h->vlh.p + (size_t)h->n_deferred * kOsTile;
-        ld = h->vlh_cap;
-      } else {
-        h->vlh.ensure(os_words(h, n_sites));
-        vlh = h->vlh.p;
-        ld = n_sites;
-      }
-      h->vlh_ld = ld;
-      // the histogram slab and round masks are zero-maintained: the fused pass
-      // fills them and k_hist_finalize resets what it read; if anything fails
-      // in between, tmh_stats_reset clears them (hist_dirty)
-      h->hist_dirty = true;
-      uint32_t* sh = (h->flags & 2u) ? h->site_hist.p : nullptr;
-      // one configuration, chosen on the host from the job's site probe
-      // (probed at the Welford launch, or above for a job whose Welford pass
-      // did not probe)
-      const int cfg = probe_fused_cfg(h);
-      const bool very_wide = cfg == kFusedNoHist;
-      const unsigned long long* rm_all = reinterpret_cast<const unsigned long long*>(c->queues.p + 8);
-      const FixList fl = corrector_fixlist(c, n_sites, s);
-      launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p, fl,
+      FusedPass p{c, h, dev_in, dev_out, n_sites, tab, s, cross, clip_lo, clip_hi};
+      fused_prepare(p);
+      launch_correct_hist(dev_in, dev_out, c->npx, n_sites, c->coef2.p, c->mconst2.p, p.fl,
                           c->log_transform, clip_lo, clip_hi, h->hist_full.p, h->hist_rmask.p,
-                          c->queues.p, c->n_wg, cfg, c->bands, s, tab, rl);
-      if (cfg == kFusedWide) launch_rare_count(rl, h->hist_full.p, n_sites, s);
-      launch_fix_correct(dev_in, dev_out, 2, c->npx, n_sites, fl, c->coef64.p, c->rc.p,
-                         c->log_transform, clip_lo, clip_hi, s, tab);
-      if (very_wide)  // the histograms from one more read of the sites
-        launch_hist_site_u16(dev_in, h->npx, n_sites, h->hist_full.p, h->qp, vlh, ld, h->pooled.p,
-                             h->pooled_parts.p, kPooledParts, h->zeros.p, sh, nullptr, 0, s, tab);
-      // the Welford pass's diagnostic wide counts restart with the next batch
-      // (reset here on s, before any later Welford launch on the handle)
-      if (h->pending - n_sites == 0) {
-        TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, s));
-        h->wide_sites = 0;
-      }
-      // The histogram tail (order statistics, percentile sums) reads only the
-      // handle's buffers: called on another stream than the handle's, it runs
-      // on the handle's tail stream (the handle's stream waits for it), so s
-      // is free as soon as the corrected sites are written (a caller
-      // pipelining jobs starts the next one's Welford pass under this one's
-      // tail).
-      hipStream_t ts = s;
-      if (cross) {
-        if (!h->tail) {  // created on first use: every stream takes a hardware queue slot
-          TMH_HIP(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
-          TMH_HIP(hipEventCreateWithFlags(&h->ev_tail, hipEventDisableTiming));
-        }
-        TMH_HIP(hipEventRecord(h->ev_out, s));
-        TMH_HIP(hipStreamWaitEvent(h->tail, h->ev_out, 0));
-        ts = h->tail;
-      }
-      if (!very_wide)
-        launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, n_sites, h->qp, vlh, ld,
-                             h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, sh, ts,
-                             false, rm_all);
-      if (!(h->flags & TMH_STATS_DEFERRED_PCT))
-        launch_pct_accumulate(vlh, n_sites, ld, h->Q, h->gamma.p, h->acc.p, ts);
-      h->hist_dirty = false;
-      if (h->flags & TMH_STATS_DEFERRED_PCT) h->n_deferred += n_sites;
-      h->last_batch = n_sites;
-      h->pending -= n_sites;
-      if (cross) {  // the handle's later work, and this corrector's next pass, after the tail
-        TMH_HIP(hipEventRecord(h->ev_tail, ts));
-        TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_tail, 0));
-        if (!c->ev_tail) TMH_HIP(hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
-        TMH_HIP(hipEventRecord(c->ev_tail, ts));
-        c->tail_pending = true;
-      }
+                          c->queues.p, c->n_wg, p.cfg, c->bands, s, tab, p.rl);
+      fused_finish(p);
       return;
     }
     const int64_t chunk = 4096;  // odd shapes: correct and histogram in two passes
@@ -1643,7 +1727,7 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
                         (!(h->flags & TMH_STATS_DEFERRED_PCT) && os_words(h, nc) > h->vlh.n);
       if (grow) {
         TMH_HIP(hipStreamSynchronize(s));
-        TMH_HIP(hipStreamSynchronize(h->stream));
+        TMH_HIP(hipStreamSynchronize(hstream(h)));
         TMH_HIP(hipStreamSynchronize(h->side));
       }
       h->zeros.ensure((size_t)nc);
@@ -1680,10 +1764,7 @@ static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev
       TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, s));
       h->wide_sites = 0;
     }
-    if (cross) {
-      TMH_HIP(hipEventRecord(h->ev_out, s));
-      TMH_HIP(hipStreamWaitEvent(h->stream, h->ev_out, 0));
-    }
+    if (cross) defer_join(h, s);
   }
 }
 
@@ -1712,6 +1793,118 @@ int tmh_correct_u16_hist_blocks_device(tmh_corrector* c, tmh_stats* h,
               "input and output block tables must differ");
     const SiteTab tab = blocked_tab(dev_in_blocks, dev_out_blocks, block_shift, h->npx);
     correct_hist_dev(c, h, nullptr, nullptr, n_sites, clip_lo, clip_hi, stream, tab);
+  });
+}
+
+// Several jobs' fused passes in ONE launch (a rank's channels): a short job's
+// launch ends with most workgroups idle for a unit's time and starts with the
+// pipeline filling; one sweep over every job's units pays that once.  Jobs
+// whose configuration differs from the first's, or that need the two-pass
+// path, run their own passes on the same stream; results are the per-job
+// calls' in every case.
+static void correct_hist_multi(tmh_corrector* const* cs, tmh_stats* const* hs, int n_jobs,
+                               const uint16_t* const* ins, uint16_t* const* outs,
+                               const SiteTab* tabs, const int64_t* n_sites, int clip_lo,
+                               int clip_hi, void* stream) {
+  TMH_CHECK(cs && hs && n_sites && n_jobs >= 1 && n_jobs <= kMaxJobs, TMH_EINVAL,
+            "bad arguments (1 to 8 jobs)");
+  check_clip(clip_lo, clip_hi, 65535);
+  for (int j = 0; j < n_jobs; ++j) {
+    TMH_CHECK(cs[j] && hs[j] && n_sites[j] >= 0, TMH_EINVAL, "bad arguments");
+    fused_check(cs[j], hs[j], n_sites[j]);
+    TMH_CHECK(cs[j]->npx == cs[0]->npx && cs[j]->log_transform == cs[0]->log_transform,
+              TMH_EINVAL, "the jobs of one call need the same image size and transform");
+    for (int k = 0; k < j; ++k)
+      TMH_CHECK(cs[k] != cs[j] && hs[k] != hs[j], TMH_EINVAL,
+                "each job needs its own corrector and statistics handle");
+  }
+  hipStream_t s = pick(cs[0]->stream, stream);
+  bool all_vec = true;
+  for (int j = 0; j < n_jobs; ++j)
+    all_vec = all_vec && fused_vec(cs[j], hs[j], ins ? ins[j] : nullptr,
+                                   outs ? outs[j] : nullptr, tabs[j]);
+  if (!all_vec) {
+    for (int j = 0; j < n_jobs; ++j)
+      correct_hist_dev(cs[j], hs[j], ins ? ins[j] : nullptr, outs ? outs[j] : nullptr, n_sites[j],
+                       clip_lo, clip_hi, s, tabs[j]);
+    return;
+  }
+  FusedPass p[kMaxJobs];
+  int np = 0;
+  for (int j = 0; j < n_jobs; ++j) {
+    if (n_sites[j] == 0) continue;
+    const bool cross = fused_begin(cs[j], hs[j], s);
+    p[np] = FusedPass{cs[j], hs[j], ins ? ins[j] : nullptr, outs ? outs[j] : nullptr, n_sites[j],
+                      tabs[j], s, cross, clip_lo, clip_hi};
+    fused_prepare(p[np]);
+    ++np;
+  }
+  if (np == 0) return;
+  FusedJobs J{};
+  for (int j = 0; j < np; ++j) {
+    if (p[j].cfg != p[0].cfg) {  // its own launch
+      tmh_corrector* c = p[j].c;
+      launch_correct_hist(p[j].in, p[j].out, c->npx, p[j].n, c->coef2.p, c->mconst2.p, p[j].fl,
+                          c->log_transform, clip_lo, clip_hi, p[j].h->hist_full.p,
+                          p[j].h->hist_rmask.p, c->queues.p, c->n_wg, p[j].cfg, c->bands, s,
+                          p[j].tab, p[j].rl);
+      continue;
+    }
+    tmh_corrector* c = p[j].c;
+    // the launch's unit counters are the first job's queues[0..8); every
+    // job's round-mask union is its own corrector's queues + 8
+    TMH_HIP(hipMemsetAsync(c->queues.p, 0, kFusedQueueInts * sizeof(int), s));
+    J.j[J.n++] = FusedJob{p[j].in, p[j].out, p[j].n,
+                          reinterpret_cast<const float4*>(c->coef2.p), c->mconst2.p, p[j].fl,
+                          p[j].h->hist_full.p, p[j].h->hist_rmask.p,
+                          reinterpret_cast<unsigned long long*>(c->queues.p + 8), p[j].tab,
+                          p[j].rl};
+  }
+  tmh_corrector* c0 = p[0].c;
+  launch_correct_hist_jobs(J, c0->npx, c0->log_transform, clip_lo, clip_hi, c0->queues.p, c0->n_wg,
+                           p[0].cfg, c0->bands, s);
+  for (int j = 0; j < np; ++j) fused_finish(p[j]);
+}
+
+int tmh_correct_u16_hist_multi_device(tmh_corrector* const* correctors, tmh_stats* const* handles,
+                                      int n_jobs, const uint16_t* const* dev_in,
+                                      uint16_t* const* dev_out, const int64_t* n_sites,
+                                      int clip_lo, int clip_hi, void* stream) {
+  return guard([&] {
+    TMH_CHECK(dev_in && dev_out && n_jobs >= 1 && n_jobs <= kMaxJobs && n_sites, TMH_EINVAL,
+              "bad arguments");
+    SiteTab tabs[kMaxJobs];
+    for (int j = 0; j < n_jobs; ++j) {
+      TMH_CHECK(n_sites[j] >= 0 && (n_sites[j] == 0 || (dev_in[j] && dev_out[j])), TMH_EINVAL,
+                "bad arguments");
+      const int64_t npx = handles && handles[j] ? handles[j]->npx : 0;
+      TMH_CHECK(n_sites[j] == 0 || dev_in[j] + n_sites[j] * npx <= dev_out[j] ||
+                    dev_out[j] + n_sites[j] * npx <= dev_in[j],
+                TMH_EINVAL, "input and output sites must not overlap");
+    }
+    correct_hist_multi(correctors, handles, n_jobs, dev_in, dev_out, tabs, n_sites, clip_lo,
+                       clip_hi, stream);
+  });
+}
+
+int tmh_correct_u16_hist_multi_blocks_device(tmh_corrector* const* correctors,
+                                             tmh_stats* const* handles, int n_jobs,
+                                             const uint16_t* const* const* dev_in_blocks,
+                                             uint16_t* const* const* dev_out_blocks,
+                                             int block_shift, const int64_t* n_sites, int clip_lo,
+                                             int clip_hi, void* stream) {
+  return guard([&] {
+    TMH_CHECK(dev_in_blocks && dev_out_blocks && handles && n_jobs >= 1 && n_jobs <= kMaxJobs,
+              TMH_EINVAL, "bad arguments");
+    SiteTab tabs[kMaxJobs];
+    for (int j = 0; j < n_jobs; ++j) {
+      TMH_CHECK(handles[j] && dev_out_blocks[j], TMH_EINVAL, "bad arguments");
+      TMH_CHECK(dev_in_blocks[j] != (const uint16_t* const*)dev_out_blocks[j], TMH_EINVAL,
+                "input and output block tables must differ");
+      tabs[j] = blocked_tab(dev_in_blocks[j], dev_out_blocks[j], block_shift, handles[j]->npx);
+    }
+    correct_hist_multi(correctors, handles, n_jobs, nullptr, nullptr, tabs, n_sites, clip_lo,
+                       clip_hi, stream);
   });
 }
 

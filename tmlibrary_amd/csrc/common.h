@@ -338,6 +338,31 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
                          unsigned long long* rmask, int* queues, int n_wg, int cfg, int bands,
                          hipStream_t s, const SiteTab& tab = SiteTab{},
                          const RareList& rl = RareList{});
+// One fused pass over several jobs (a rank's channels, same image size,
+// configuration and transform): job j's units follow job j-1's in one sweep,
+// each unit with its own job's sites, coefficients, histograms, round masks
+// and fixup list.  uni: the job's round-mask union (its corrector's
+// queues + 8, zeroed by the caller); queues: the launch's unit counters.
+struct FusedJob {
+  const uint16_t* in;
+  uint16_t* out;
+  int64_t n_sites;
+  const float4* coef;     // coef2 as float4 planes
+  const float4* mconst2;
+  FixList fl;
+  uint32_t* hist;
+  unsigned long long* rmask;
+  unsigned long long* uni;
+  SiteTab tab;
+  RareList rl;
+};
+struct FusedJobs {
+  FusedJob j[kMaxJobs];
+  int n;
+};
+void launch_correct_hist_jobs(const FusedJobs& J, int64_t npx, int log_transform, int clip_lo,
+                              int clip_hi, int* queues, int n_wg, int cfg, int bands,
+                              hipStream_t s);
 // after launch_correct_hist with a RareList: each site's list into its
 // histogram (hist + s * kBins), on the same stream
 void launch_rare_count(const RareList& rl, uint32_t* hist, int64_t n_sites, hipStream_t s);

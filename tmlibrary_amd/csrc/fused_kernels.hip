@@ -187,10 +187,8 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // instead of flushed.
 template <bool LOG, bool CLIP, int SPU, int ABL, int NT, int LB, bool PK = false>
 __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void k_correct_hist(
-    const uint16_t* __restrict__ in, uint16_t* __restrict__ out, int64_t npx, int64_t n_sites,
-    const float4* __restrict__ coef, const float4* __restrict__ mconst2, FixList fl,
-    int clip_lo, int clip_hi, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
-    int n_bands, int* __restrict__ queues, const SiteTab tab, const RareList rl) {
+    const FusedJobs J, int64_t npx, int clip_lo, int clip_hi, int n_bands,
+    int* __restrict__ queues) {
   constexpr int BINS = LB / SPU;
   constexpr int SLICE = BINS + 1;
   constexpr int NSL = PK ? SPU / 2 : SPU;  // word arrays (PK: two sites per array)
@@ -204,7 +202,6 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   constexpr int kRareSh = PK ? 3072 : 1;  // the rest of the 160 KB of LDS (r4: 1,024)
   __shared__ uint16_t rstage[PK ? SPU : 1][kRareSh];
   __shared__ unsigned int rcnt[PK ? SPU : 1], rbase[PK ? SPU : 1];
-  const bool rlist = PK && rl.v != nullptr;
   uint32_t rare[SPU];  // packed: this thread's pixels of the unit beyond the slices (list or atomic)
 #pragma unroll
   for (int k = 0; k < SPU; ++k) rare[k] = 0u;
@@ -228,31 +225,21 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   if (tid < 2) fix_cnt[tid] = 0u;
   __syncthreads();
 
-  const float4 m = mconst2[0];
   const uint32_t clo2 = (uint32_t)clip_lo * 0x00010001u, chi2 = (uint32_t)clip_hi * 0x00010001u;
   const int ngroups = (int)(npx >> 3);
   const int site_bytes = (int)(npx * 2);
-  const int n_groups_s = (int)((n_sites + SPU - 1) / SPU);
-  const int n_units = n_bands * n_groups_s;
-  // coefficient planes: plane k holds (mu, mu, a, a) of pixels 8g+2k, 8g+2k+1
-  // of group g, so each of a lane's four coefficient loads is one contiguous
-  // 1 KiB per wave
-  const __amdgpu_buffer_rsrc_t rcf =
-      __builtin_amdgcn_make_buffer_rsrc((void*)coef, 0, (int)(npx * 8), 0x00020000);
+  int n_units = 0;  // every job's units, job after job
+  for (int j = 0; j < J.n; ++j) n_units += n_bands * (int)((J.j[j].n_sites + SPU - 1) / SPU);
   const float4 cc = make_float4(2.5f, 2.4f, 1.1f, 0.9f);
 
-  // Unit order: the sweep i = 0, 1, ... is band-major with the 8 XCDs two
-  // bands apart -- unit i is site group i % n_groups_s of band
-  // (i / n_groups_s + 2 * (i % 8)) % n_bands -- and XCD x deals the units
-  // i = x + 8 j from its own counter (queues[x]), stealing from the next
-  // queue once its own is drained.  The next unit is grabbed while the
-  // current one streams.
+  // Unit order: the sweep i = 0, 1, ... runs job by job; within a job it is
+  // band-major with the 8 XCDs two bands apart -- the job's unit i' is site
+  // group i' % n_groups_s of band (i' / n_groups_s + 2 * (i' % 8)) % n_bands
+  // -- and XCD x deals the units i = x + 8 j from its own counter
+  // (queues[x]), stealing from the next queue once its own is drained.  The
+  // next unit is grabbed while the current one streams.
   __shared__ int unit_sh;
   int q = xcc_id(), exhausted = 0;
-  auto unit_of = [&](int i) -> int {
-    const int band = (i / n_groups_s + 2 * (i % 8)) % n_bands;
-    return band * n_groups_s + i % n_groups_s;
-  };
   auto grab = [&]() -> int {
     while (exhausted < 8) {
       if (tid == 0) unit_sh = atomicAdd(&queues[q], 1);
@@ -262,7 +249,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
       const int i = q + 8 * j;
       if (i < n_units) {
         exhausted = 0;
-        return unit_of(i);
+        return i;
       }
       q = (q + 1) & 7;  // this queue is drained: steal from the next
       ++exhausted;
@@ -270,28 +257,41 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     return -1;
   };
   struct Unit {
-    int g0, g1, ns;
+    int job, g0, g1, ns;
     int64_t s0;
     __amdgpu_buffer_rsrc_t rin, rout;  // the unit's SPU sites; loads past ns read 0
+    // coefficient planes: plane k holds (mu, mu, a, a) of pixels 8g+2k,
+    // 8g+2k+1 of group g, so each of a lane's four coefficient loads is one
+    // contiguous 1 KiB per wave
+    __amdgpu_buffer_rsrc_t rcf;
   };
-  auto decode = [&](int code) -> Unit {
-    const int band = code / n_groups_s;
+  auto decode = [&](int i) -> Unit {
     Unit r;
-    r.s0 = (int64_t)(code % n_groups_s) * SPU;
-    r.ns = (int)(n_sites - r.s0 < SPU ? n_sites - r.s0 : SPU);
+    int job = 0, n_groups_s = 0;
+    for (;; ++job) {  // the sweep index's job (uniform: every lane the same)
+      n_groups_s = (int)((J.j[job].n_sites + SPU - 1) / SPU);
+      if (job + 1 >= J.n || i < n_bands * n_groups_s) break;
+      i -= n_bands * n_groups_s;
+    }
+    const FusedJob& jb = J.j[job];
+    const int band = (i / n_groups_s + 2 * (i % 8)) % n_bands;
+    r.job = job;
+    r.s0 = (int64_t)(i % n_groups_s) * SPU;
+    r.ns = (int)(jb.n_sites - r.s0 < SPU ? jb.n_sites - r.s0 : SPU);
     r.g0 = (int)((int64_t)band * ngroups / n_bands);
     r.g1 = (int)((int64_t)(band + 1) * ngroups / n_bands);
-    const uint16_t* ib = in + r.s0 * npx;
-    uint16_t* ob = out + r.s0 * npx;
-    if (tab.in) {  // blocked layout: the unit's sites lie inside one block
-      const int64_t b = site_block(tab, r.s0), o = site_in_block(tab, r.s0) * npx;
-      ib = tab.in[b] + o;
-      ob = tab.out[b] + o;
+    const uint16_t* ib = jb.in + r.s0 * npx;
+    uint16_t* ob = jb.out + r.s0 * npx;
+    if (jb.tab.in) {  // blocked layout: the unit's sites lie inside one block
+      const int64_t b = site_block(jb.tab, r.s0), o = site_in_block(jb.tab, r.s0) * npx;
+      ib = jb.tab.in[b] + o;
+      ob = jb.tab.out[b] + o;
     }
     r.rin = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(ib), 0, r.ns * site_bytes,
                                               0x00020000);
     r.rout = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(ob), 0, r.ns * site_bytes,
                                                0x00020000);
+    r.rcf = __builtin_amdgcn_make_buffer_rsrc((void*)jb.coef, 0, (int)(npx * 8), 0x00020000);
     return r;
   };
   // a lane whose group lies past the unit's band loads from past the buffers'
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
 #pragma unroll
       for (int p = 0; p < 4; ++p)
         c[p] = __builtin_bit_cast(float4,
-                                  __builtin_amdgcn_raw_buffer_load_b128(rcf, off, p * ngroups * 16, 0));
+                                  __builtin_amdgcn_raw_buffer_load_b128(un.rcf, off, p * ngroups * 16, 0));
     }
   };
 
@@ -326,7 +326,12 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     const Unit un = decode(cur);
     Unit nu = un;
     if (nxt >= 0) nu = decode(nxt);
-    uint32_t* hs = hist + un.s0 * (int64_t)kBins;
+    const FusedJob& jb = J.j[un.job];
+    const float4 m = jb.mconst2[0];
+    const FixList fl = jb.fl;
+    const RareList rl = jb.rl;
+    const bool rlist = PK && rl.v != nullptr;
+    uint32_t* hs = jb.hist + un.s0 * (int64_t)kBins;
 
     auto process = [&](const uint4 w, const int k, const float4 (&cf)[4], const int g) -> u32x4_t {
       const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
@@ -507,8 +512,8 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
         if (lm1) atomicOr(&rm[2 * j + 1], lm1);
       }
       if (bad) {  // rare: recount those sites' band pixels below BINS exactly
-        const uint16_t* ib = in + un.s0 * npx;
-        if (tab.in) ib = tab.in[site_block(tab, un.s0)] + site_in_block(tab, un.s0) * npx;
+        const uint16_t* ib = jb.in + un.s0 * npx;
+        if (jb.tab.in) ib = jb.tab.in[site_block(jb.tab, un.s0)] + site_in_block(jb.tab, un.s0) * npx;
         for (int k = 0; k < SPU; ++k) {
           if (!((bad >> k) & 1u)) continue;
           uint32_t* h = hs + k * (int64_t)kBins;
@@ -550,8 +555,8 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     if (tid < un.ns) {
       const unsigned long long r = rm[tid];
       if (r) {
-        atomicOr(&rmask[un.s0 + tid], r);
-        atomicOr(reinterpret_cast<unsigned long long*>(queues + 8), r);  // launch-wide union
+        atomicOr(&jb.rmask[un.s0 + tid], r);
+        atomicOr(jb.uni, r);  // the job's union
       }
       rm[tid] = 0ull;
     }
@@ -610,29 +615,25 @@ static int fused_bands(int cfg_bands, int64_t n_sites, int spu, int64_t n_wgs, i
   return b;
 }
 
-static void launch_correct_hist_cfg(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
-                                    const float4* cf4, const float4* mconst2, const FixList& fl,
-                                    int log_transform, int clip_lo, int clip_hi, uint32_t* hist,
-                                    unsigned long long* rmask, int* queues, int n_wg, int cfg,
-                                    int bands_opt, hipStream_t s, const SiteTab& tab,
-                                    const RareList& rl) {
+static void launch_correct_hist_cfg(const FusedJobs& J, int64_t npx, int log_transform,
+                                    int clip_lo, int clip_hi, int* queues, int n_wg, int cfg,
+                                    int bands_opt, hipStream_t s) {
+  int64_t n_sites = 0;  // the bands see the launch's site groups, every job's
 #define TMH_LAUNCH_CH(L_, K_, A_)                                                                \
   {                                                                                              \
     constexpr FusedCfg c = kFusedCfgs[K_];                                                       \
     const dim3 grid(n_wg * (1024 / c.threads));                                                  \
+    for (int j = 0; j < J.n; ++j) n_sites += (J.j[j].n_sites + c.spu - 1) / c.spu * c.spu;      \
     const int nbands = fused_bands(c.bands, n_sites, c.spu, grid.x, bands_opt);                  \
+    FusedJobs Jc = J;                                                                            \
+    if (!c.packed)                                                                               \
+      for (int j = 0; j < J.n; ++j) Jc.j[j].rl = RareList{};                                     \
     if (clip_lo >= 0)                                                                            \
       hipLaunchKernelGGL((k_correct_hist<L_, true, c.spu, A_, c.threads, c.lds_bins, c.packed>), \
-                         grid,                                                                   \
-                         dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, nbands, queues, tab,                    \
-                         c.packed ? rl : RareList{});                                       \
+                         grid, dim3(c.threads), 0, s, Jc, npx, clip_lo, clip_hi, nbands, queues); \
     else                                                                                         \
       hipLaunchKernelGGL((k_correct_hist<L_, false, c.spu, A_, c.threads, c.lds_bins, c.packed>), \
-                         grid,                                                                   \
-                         dim3(c.threads), 0, s, in, out, npx, n_sites, cf4, mconst2, fl,           \
-                         clip_lo, clip_hi, hist, rmask, nbands, queues, tab,                    \
-                         c.packed ? rl : RareList{});                                       \
+                         grid, dim3(c.threads), 0, s, Jc, npx, clip_lo, clip_hi, nbands, queues); \
   }
 #define TMH_LAUNCH_CFG(L_)                                     \
   switch (cfg) {                                               \
@@ -669,10 +670,21 @@ void launch_correct_hist(const uint16_t* in, uint16_t* out, int64_t npx, int64_t
   // queues[0..8): per-XCD unit counters; queues[8..10): the union of the
   // sites' round masks (read by the pooled column sum)
   TMH_HIP(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), s));
-  const float4* cf4 = reinterpret_cast<const float4*>(coef2);
+  FusedJobs J{};
+  J.n = 1;
+  J.j[0] = FusedJob{in, out, n_sites, reinterpret_cast<const float4*>(coef2), mconst2, fl, hist,
+                    rmask, reinterpret_cast<unsigned long long*>(queues + 8), tab, rl};
   ProfScope prof("correct_hist", s);
-  launch_correct_hist_cfg(in, out, npx, n_sites, cf4, mconst2, fl, log_transform, clip_lo, clip_hi,
-                          hist, rmask, queues, n_wg, cfg, bands, s, tab, rl);
+  launch_correct_hist_cfg(J, npx, log_transform, clip_lo, clip_hi, queues, n_wg, cfg, bands, s);
+}
+
+// Several jobs in one launch (the caller zeroed queues and every job's uni).
+void launch_correct_hist_jobs(const FusedJobs& J, int64_t npx, int log_transform, int clip_lo,
+                              int clip_hi, int* queues, int n_wg, int cfg, int bands,
+                              hipStream_t s) {
+  if (J.n <= 0) return;
+  ProfScope prof("correct_hist", s);
+  launch_correct_hist_cfg(J, npx, log_transform, clip_lo, clip_hi, queues, n_wg, cfg, bands, s);
 }
 
 // Each site's rare list into its histogram: one workgroup per site, the

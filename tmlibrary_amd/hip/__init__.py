@@ -92,6 +92,8 @@ SIGNATURES = {
     "tmh_correct_u16_device": (_I, [_P, _P, _P, _I64, _I, _I, _P]),
     "tmh_correct_u16_hist_device": (_I, [_P, _P, _P, _P, _I64, _I, _I, _P]),
     "tmh_correct_u16_hist_blocks_device": (_I, [_P, _P, _P, _P, _I, _I64, _I, _I, _P]),
+    "tmh_correct_u16_hist_multi_device": (_I, [_P, _P, _I, _P, _P, _P, _I, _I, _P]),
+    "tmh_correct_u16_hist_multi_blocks_device": (_I, [_P, _P, _I, _P, _P, _I, _P, _I, _I, _P]),
     "tmh_correct_u8": (_I, [_P, _P, _P, _I64, _I, _I]),
     "tmh_clip_u16": (_I, [_P, _P, _I64, _I, _I]),
     "tmh_align": (_I, [_P, _P, _I, _I64, _I, _I, _P, _I, _I]),

@@ -17,7 +17,7 @@
 #   repeat:N       N more quick bench processes (bench_repeat_TAG.jsonl)
 #   dist432        one rank, forced-distributed, 4 channels x 432 sites: each
 #                  GPU's share of configs[2] at N = 8 (dist432_TAG.json)
-#   pytest:EXPR    the GPU tests selected by -k EXPR (gpu_tests_k_TAG.log)
+#   pytest:EXPR    the GPU tests selected by -k EXPR, '+' for spaces (gpu_tests_k_TAG.log)
 #   input[:N]      tools/bench_input.py on N full-size gzip files (host and GPU
 #                  decode, run_job, the sharded job) -> bench_input_TAG.json
 #   dist432v:ARGS  dist432 with extra flags ('+' for spaces) -> dist432_v_TAG.jsonl
@@ -109,6 +109,17 @@ for step in "$@"; do
         --no-extras --cpu-sample 0 ${BENCH_ARGS:-} > $O/rocprof_dist432_$TAG.json 2> $O/rocprof_dist432_$TAG.log || exit $?
       summ $O/rocprof_dist432_$TAG.json
       ;;
+    prof432h)
+      # prof432 with the HIP runtime calls (host waits) on the kernels' clock:
+      # prof432h[:ARGS] ('+' for spaces) -> rocprof_dist432h_TAG/
+      V=$(echo "${a1:-}" | tr '+' ' ')
+      TMH_BENCH_FORCE_DIST=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \
+        timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-trace \
+        --output-format csv -d $O/rocprof_dist432h_$TAG -o run \
+        -- python3 bench.py --layout sharded --channels 4 --sites 432 --steps 5 --warmup 2 \
+        --no-extras --cpu-sample 0 ${BENCH_ARGS:-} $V > $O/rocprof_dist432h_$TAG.json 2> $O/rocprof_dist432h_$TAG.log || exit $?
+      summ $O/rocprof_dist432h_$TAG.json
+      ;;
     input)
       timeout -k 10 600 python tools/bench_input.py --sites ${a1:-256} --threads 16 --repeat 4 \
         > $O/bench_input_$TAG.json 2> $O/bench_input_$TAG.err || exit $?
@@ -121,9 +132,10 @@ for step in "$@"; do
       grep mode $O/bench_inflate_$TAG.err
       ;;
     pytest)
-      # a subset of the GPU tests: pytest:EXPR (-k expression)
+      # a subset of the GPU tests: pytest:EXPR (-k expression, '+' for spaces)
+      K=$(echo "$a1" | tr '+' ' ')
       timeout -k 10 900 python -u -m pytest tests -m gpu -v -ra --timeout 300 --timeout-method thread \
-        -k "$a1" > $O/gpu_tests_k_$TAG.log 2>&1
+        -k "$K" > $O/gpu_tests_k_$TAG.log 2>&1
       rc=$?
       grep -E "passed|failed" $O/gpu_tests_k_$TAG.log | tail -3
       if [ $rc -ne 0 ]; then exit $rc; fi
