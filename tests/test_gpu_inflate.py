@@ -162,7 +162,7 @@ def _files(tmp_path, n, H, W, dtype, chunks, level, seed=1):
 
 
 @pytest.mark.parametrize("H,W,dtype,chunks,level", [
-    (300, 500, np.uint16, None, 4),        # whole-row chunks, last one padded
+    (300, 500, np.uint16, None, 4),        # h5py's default chunks (38 x 125), last row padded
     (300, 500, np.uint16, (64, 96), 1),    # 2-D chunks, right and bottom edges padded
     (257, 333, np.uint8, (50, 50), 9),
     (128, 256, np.uint16, (128, 256), 6),  # one chunk per file
@@ -196,7 +196,7 @@ def test_device_decode_channel_image_files(L, tmp_path, H, W, dtype, chunks, lev
 @pytest.mark.timeout(300)
 def test_device_decode_fullsize_sites(L, tmp_path):
     """Eight 2160x2560 synthetic sites, written as the reference-layout files
-    (gzip level 4, whole-row chunks), decoded on the GPU = the host read."""
+    (gzip level 4, h5py's default 135 x 160 chunks), decoded on the GPU = the host read."""
     import torch
 
     from tmlibrary_amd.models.device_decode import DeviceChunkDecoder

@@ -641,12 +641,16 @@ int64_t inflate_scratch_bytes(int64_t n_chunks, int64_t raw_max) {
   return n_chunks * match_words(raw_max) * 4;
 }
 
-// The decode form: "wave" (default: one wave per stream, speculative
-// tokens, resolve + Adler-32 in the same kernel) or "lane" (one lane per
-// stream, two kernels).  TMH_INFLATE_MODE selects one for A/B measurements.
+// The decode form: "lane" (default: one lane per stream, two kernels) or
+// "wave" (one wave per stream, speculative tokens, resolve + Adler-32 in the
+// same kernel).  The wave form measured slower on the site images' 32 KB
+// streams: 68.4 against 35.2 + 4.6 ms per 128 sites (one 64-bit window per
+// round covers ~7 literal tokens of near-incompressible data, and each
+// round's chain walk is a serial readlane chain; profiles/r5/
+// bench_inflate_modes_r5i.json).  TMH_INFLATE_MODE selects one.
 static bool inflate_wave_mode() {
-  if (const char* e = getenv("TMH_INFLATE_MODE")) return strcmp(e, "lane") != 0;
-  return true;
+  if (const char* e = getenv("TMH_INFLATE_MODE")) return strcmp(e, "wave") == 0;
+  return false;
 }
 
 // Streams per phase-1 workgroup.  A lane's decode is a serial chain of

@@ -2,7 +2,7 @@
 """Site-image input path on the GPU box: host inflate vs GPU inflate.
 
 Writes D distinct full-size synthetic sites as channel image files (gzip
-level 4, libtmh5's whole-row chunks -- the reference's ChannelImageFile
+level 4, h5py's default 135 x 160 chunks -- the reference's ChannelImageFile
 layout, tmlib/models/file.py:353-363), then decodes a block of B files (the
 D files cycled) R times each way:
   host:  read_channel_images (libhdf5 metadata + zlib inflate on the granted cores)
