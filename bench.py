@@ -1729,9 +1729,12 @@ def main():
         D.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    host_ms = []  # the host's time to queue each step (it runs ahead unless it waits)
     for i in range(a.steps):
         beat.step = " (timed step %d)" % i
+        th = time.perf_counter()
         step(last=i == a.steps - 1)
+        host_ms.append(1e3 * (time.perf_counter() - th))
     beat.step = ""
     beat("synchronize after the timed steps", echo=False)
     torch.cuda.synchronize(dev)
@@ -1985,6 +1988,8 @@ def main():
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(1e3 * elapsed / a.steps, 3),
+            "host_queue_ms_per_step": [round(float(np.median(host_ms)), 3),
+                                       round(float(np.max(host_ms)), 3)],
             "higher_is_better": True,
             "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,

@@ -100,7 +100,7 @@ for step in "$@"; do
       TMH_BENCH_FORCE_DIST=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \
         timeout -k 10 300 python bench.py --layout sharded --channels 4 --sites 432 --steps 10 \
         --warmup 3 --no-extras --cpu-sample 0 ${BENCH_ARGS:-} $V > $O/dist432v.tmp 2>> $O/dist432_v_$TAG.err || exit $?
-      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.strip()][-1]); print(json.dumps({'variant': sys.argv[2], 'value': d['value'], 'ms': d['ms_per_step'], 'check': d['check_vs_oracle'], 'k': {k: v['avg_ms'] for k, v in d['kernels'].items()}}))" $O/dist432v.tmp "$V" | tee -a $O/dist432_v_$TAG.jsonl
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.strip()][-1]); print(json.dumps({'variant': sys.argv[2], 'value': d['value'], 'ms': d['ms_per_step'], 'host_ms': d.get('host_queue_ms_per_step'), 'check': d['check_vs_oracle'], 'k': {k: v['avg_ms'] for k, v in d['kernels'].items()}}))" $O/dist432v.tmp "$V" | tee -a $O/dist432_v_$TAG.jsonl
       ;;
     prof432)
       TMH_BENCH_FORCE_DIST=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \
