@@ -1433,7 +1433,7 @@ def main():
             """finalize -> smoothing -> coefficients of this job alone"""
             p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
             if a.planes == "multi":
-                planes_multi([self])
+                planes_multi([self], unsmoothed=False)
                 return
             hip.check(L.tmh_stats_finalize_device(self.h, p(self.mean), p(self.std), self.sp))
             hip.check(L.tmh_smooth2_f64_device(p(self.mean), p(self.std), p(self.smean),
@@ -1468,7 +1468,7 @@ def main():
             L.tmh_corrector_destroy(self.corr)
             L.tmh_stats_destroy(self.h)
 
-    def planes_multi(jobs, sp=None, unsmoothed=True):
+    def planes_multi(jobs, sp=None, unsmoothed=False):
         """The planes step of several jobs (a rank's channels) in one launch per
         kernel (tmh_job_planes_multi_device), on the first job's stream (or
         sp): the library orders it after every job's stream and every job's
@@ -1695,7 +1695,7 @@ def main():
                     merge_welford(ch.ops, D, n_total=n_channel)
                     evs[id(ch)] = [e0, ch.event() if timing["on"] else None]
         if a.planes == "multi":
-            planes_multi(X)
+            planes_multi(X, unsmoothed=False)
         else:
             for ch in X:
                 ch.planes()

@@ -1173,8 +1173,6 @@ int tmh_smooth_f64(const double* host_in, double* host_out, int height, int widt
 // correction
 // ---------------------------------------------------------------------------
 
-constexpr int kCoefPartials = 1024;  // blocks of the deterministic plane sums
-
 static void coef_job(CoefJobs& J, int k, tmh_corrector* c, const double* d_mean,
                      const double* d_std) {
   J.mean[k] = d_mean;
@@ -1208,12 +1206,12 @@ static void corrector_coeffs(tmh_corrector* c, const double* d_mean, const doubl
   ProfScope prof("coeffs", s);
   CoefJobs J{};
   coef_job(J, 0, c, d_mean, d_std);
-  launch_coeffs_jobs(J, 1, c->npx, kCoefPartials, s);
+  launch_coeffs_jobs(J, 1, c->H, c->W, false, s);
 }
 
 static void corrector_init(tmh_corrector* c, const double* d_mean, const double* d_std) {
   c->sums.alloc(3);
-  c->partial.alloc(3 * kCoefPartials);
+  c->partial.alloc(3 * (size_t)coef_tiles(c->H, c->W));
   c->coef.alloc(c->npx);
   c->coef2.alloc(c->npx);
   c->coef_lin.alloc(c->npx);
@@ -1334,9 +1332,12 @@ int tmh_corrector_update_multi_device(tmh_corrector* const* cs, int n, const dou
       TMH_CHECK(cs[k]->npx == cs[0]->npx, TMH_EINVAL, "correctors of different image sizes");
       coef_job(J, k, cs[k], dev_mean[k], dev_std[k]);
     }
+    for (int k = 0; k < n; ++k)
+      TMH_CHECK(cs[k]->H == cs[0]->H && cs[k]->W == cs[0]->W, TMH_EINVAL,
+                "correctors of different image shapes");
     const hipStream_t s = pick(cs[0]->stream, stream);
     ProfScope prof("coeffs", s);
-    launch_coeffs_jobs(J, n, cs[0]->npx, kCoefPartials, s);
+    launch_coeffs_jobs(J, n, cs[0]->H, cs[0]->W, false, s);
   });
 }
 
@@ -1396,13 +1397,27 @@ int tmh_job_planes_multi_device(tmh_stats* const* hs, tmh_corrector* const* cs, 
         tmp[2 * k + 1] = scratch.p + (size_t)(3 * k + 2) * npx;
       }
     }
-    launch_smooth_planes(in, out, onepass ? out : tmp, sq, 2 * n, H, W, t.first, t.second, s);
+    // the coefficient tiles' sums of the smoothed planes come with them
+    // (psum / pmin: std sums, mean sums, std minima in each corrector's
+    // partial buffer)
+    const int nt = coef_tiles(H, W);
+    double* psum[kMaxPlanes];
+    double* pmin[kMaxPlanes];
+    for (int k = 0; k < n; ++k) {
+      TMH_CHECK(cs[k]->H == H && cs[k]->W == W, TMH_EINVAL, "jobs of different image shapes");
+      psum[2 * k] = cs[k]->partial.p + nt;  // mean
+      pmin[2 * k] = nullptr;
+      psum[2 * k + 1] = cs[k]->partial.p;  // std
+      pmin[2 * k + 1] = cs[k]->partial.p + 2 * nt;
+    }
+    launch_smooth_planes(in, out, onepass ? out : tmp, sq, 2 * n, H, W, t.first, t.second, s,
+                         psum, pmin);
     // the correctors' coefficients (image.py:599-631) from the smoothed planes
     CoefJobs J{};
     for (int k = 0; k < n; ++k) coef_job(J, k, cs[k], dev_smean[k], dev_sstd[k]);
     {
       ProfScope prof("coeffs", s);
-      launch_coeffs_jobs(J, n, npx, kCoefPartials, s);
+      launch_coeffs_jobs(J, n, H, W, true, s);
     }
     for (int k = 0; k < n; ++k) cross_end(hs[k], s);
     if (!onepass) TMH_HIP(hipStreamSynchronize(s));  // the scratch is freed on return
@@ -1644,8 +1659,9 @@ static void fused_prepare(FusedPass& p) {
 }
 
 // what follows the job's fused launch: rare lists, f64 fixups, the very wide
-// configuration's histograms, and the histogram tail
-static void fused_finish(FusedPass& p) {
+// configuration's histograms, and the histogram tail.  fixed: the caller
+// launched the fixups (and the wide counters' reset) for several jobs at once.
+static void fused_finish(FusedPass& p, bool fixed = false) {
   tmh_stats* h = p.h;
   tmh_corrector* c = p.c;
   const int64_t n_sites = p.n;
@@ -1653,15 +1669,16 @@ static void fused_finish(FusedPass& p) {
   const bool very_wide = p.cfg == kFusedNoHist;
   const unsigned long long* rm_all = reinterpret_cast<const unsigned long long*>(c->queues.p + 8);
   if (p.cfg == kFusedWide) launch_rare_count(p.rl, h->hist_full.p, n_sites, s);
-  launch_fix_correct(p.in, p.out, 2, c->npx, n_sites, p.fl, c->coef64.p, c->rc.p,
-                     c->log_transform, p.clip_lo, p.clip_hi, s, p.tab);
+  if (!fixed)
+    launch_fix_correct(p.in, p.out, 2, c->npx, n_sites, p.fl, c->coef64.p, c->rc.p,
+                       c->log_transform, p.clip_lo, p.clip_hi, s, p.tab);
   if (very_wide)  // the histograms from one more read of the sites
     launch_hist_site_u16(p.in, h->npx, n_sites, h->hist_full.p, h->qp, p.vlh, p.ld, h->pooled.p,
                          h->pooled_parts.p, kPooledParts, h->zeros.p, p.sh, nullptr, 0, s, p.tab);
   // the Welford pass's diagnostic wide counts restart with the next batch
   // (reset here on s, before any later Welford launch on the handle)
   if (h->pending - n_sites == 0) {
-    TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, s));
+    if (!fixed) TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, s));
     h->wide_sites = 0;
   }
   // The histogram tail (order statistics, percentile sums) reads only the
@@ -1863,7 +1880,15 @@ static void correct_hist_multi(tmh_corrector* const* cs, tmh_stats* const* hs, i
   tmh_corrector* c0 = p[0].c;
   launch_correct_hist_jobs(J, c0->npx, c0->log_transform, clip_lo, clip_hi, c0->queues.p, c0->n_wg,
                            p[0].cfg, c0->bands, s);
-  for (int j = 0; j < np; ++j) fused_finish(p[j]);
+  // every job's fixups (and Welford wide-counter reset) in one launch
+  FixJobs F{};
+  for (int j = 0; j < np; ++j) {
+    tmh_corrector* c = p[j].c;
+    F.j[F.n++] = FixJob{p[j].in, p[j].out, p[j].n, p[j].fl, c->coef64.p, c->rc.p, p[j].tab,
+                        p[j].h->pending - p[j].n == 0 ? p[j].h->wide.p : nullptr};
+  }
+  launch_fix_correct_jobs(F, c0->npx, c0->log_transform, clip_lo, clip_hi, s);
+  for (int j = 0; j < np; ++j) fused_finish(p[j], true);
 }
 
 int tmh_correct_u16_hist_multi_device(tmh_corrector* const* correctors, tmh_stats* const* handles,

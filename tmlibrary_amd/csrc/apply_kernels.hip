@@ -41,7 +41,50 @@ struct SmPlanes {
   const double* in[kMaxPlanes];
   double* out[kMaxPlanes];
   double sq[kMaxPlanes];
+  // optional (k_smooth_2d): the plane's partial sums per coefficient tile
+  // (kSumTH x kSumTW outputs, tile = blockIdx.y * gridDim.x + blockIdx.x) and
+  // its smallest positive value per tile -- the coefficient step's np.mean
+  // and refinement bound without a pass of their own (k_tile_sums computes
+  // the same partials from a plane in memory)
+  double* psum[kMaxPlanes];
+  double* pmin[kMaxPlanes];
 };
+
+__device__ __forceinline__ double block_sum256(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  return red[0];
+}
+
+__device__ __forceinline__ double block_min256(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = fmin(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  return red[0];
+}
+
+// A thread's column of a coefficient tile, summed in row order, then the
+// tile's 256 threads (idle ones adding 0) in a fixed tree: the partition and
+// order k_smooth_2d's fused sums and k_tile_sums share, so the sums do not
+// depend on which of the two made them.
+__device__ __forceinline__ void tile_partials(double sum, double mn, double* psum, double* pmin,
+                                              double* red) {
+  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+  const double t = block_sum256(sum, red);
+  if (threadIdx.x == 0) psum[tile] = t;
+  if (pmin) {
+    __syncthreads();
+    const double m = block_min256(mn, red);
+    if (threadIdx.x == 0) pmin[tile] = m;
+  }
+}
 
 __device__ __forceinline__ double sm_in(const SmPlanes& pl, const double* __restrict__ in, int64_t i) {
   const double v = in[i];
@@ -160,23 +203,54 @@ __global__ __launch_bounds__(256) void k_smooth_2d(const SmPlanes pl, int H, int
   }
   __syncthreads();
   const int x = x0 + (int)threadIdx.x;
-  if ((int)threadIdx.x >= TW || x >= W) return;
+  double sum = 0.0, mn = __builtin_inf();
+  if ((int)threadIdx.x < TW && x < W) {
 #pragma unroll 4
-  for (int t = 0; t < TH; ++t) {
-    if (y0 + t >= H) break;
-    double a = 0.0;
+    for (int t = 0; t < TH; ++t) {
+      if (y0 + t >= H) break;
+      double a = 0.0;
 #pragma unroll
-    for (int j = 0; j <= 2 * R; ++j) a = fma(w[j], vt[t][threadIdx.x + j], a);
-    out[(int64_t)(y0 + t) * W + x] = a;
+      for (int j = 0; j <= 2 * R; ++j) a = fma(w[j], vt[t][threadIdx.x + j], a);
+      out[(int64_t)(y0 + t) * W + x] = a;
+      sum += a;
+      if (a > 0.0 && a < mn) mn = a;  // NaN fails both; +inf never below mn
+    }
+  }
+  double* ps = pl.psum[blockIdx.z];
+  if (ps) {  // uniform per workgroup
+    __shared__ double red[256];
+    tile_partials(sum, mn, ps, pl.pmin[blockIdx.z], red);
   }
 }
+
+static_assert(kSumTW == 256 - 2 * 20, "coefficient tiles are the sigma-5 smoothing's tiles");
+
+// The coefficient tiles' partial sums (and smallest positive values) of
+// planes in memory, in k_smooth_2d's partition and order.
+__global__ __launch_bounds__(256) void k_tile_sums(const SmPlanes pl, int H, int W) {
+  __shared__ double red[256];
+  const double* __restrict__ in = pl.in[blockIdx.z];
+  const int x = blockIdx.x * kSumTW + (int)threadIdx.x, y0 = blockIdx.y * kSumTH;
+  double sum = 0.0, mn = __builtin_inf();
+  if ((int)threadIdx.x < kSumTW && x < W) {
+    for (int t = 0; t < kSumTH; ++t) {
+      if (y0 + t >= H) break;
+      const double a = in[(int64_t)(y0 + t) * W + x];
+      sum += a;
+      if (a > 0.0 && a < mn) mn = a;
+    }
+  }
+  tile_partials(sum, mn, pl.psum[blockIdx.z], pl.pmin[blockIdx.z], red);
+}
+
+int coef_tiles(int H, int W) { return (int)(cdiv(W, kSumTW) * cdiv(H, kSumTH)); }
 
 // np planes: in[k] -> tmp[k] (axis 0) -> out[k] (axis 1); sq[k] != 0: plane k
 // is read as a finalized std (SmPlanes), which needs the one-pass form
 // (radius 20) -- the caller finalizes into a plane of its own otherwise
 void launch_smooth_planes(const double* const* in, double* const* out, double* const* tmp,
                           const double* sq, int np, int H, int W, const double* d_w, int radius,
-                          hipStream_t s) {
+                          hipStream_t s, double* const* psum, double* const* pmin) {
   ProfScope prof("smooth", s);
   if (np <= 0) return;
   auto planes = [&](const double* const* a, double* const* b) {
@@ -189,11 +263,15 @@ void launch_smooth_planes(const double* const* in, double* const* out, double* c
     return p;
   };
   if (radius == 20 && W >= 2 * radius + 1 && !getenv("TMH_SMOOTH_2PASS")) {
-    // sigma = 5, the reference's default (image.py:1172): one pass, both axes
-    constexpr int TH = 16, TW = 256 - 2 * 20;
-    const SmPlanes a = planes(in, out);
-    const dim3 g((unsigned)cdiv(W, TW), (unsigned)cdiv(H, TH), (unsigned)np);
-    hipLaunchKernelGGL((k_smooth_2d<TH, 20>), g, dim3(256), 0, s, a, H, W, d_w);
+    // sigma = 5, the reference's default (image.py:1172): one pass, both
+    // axes, the coefficient tiles' sums as the outputs are written
+    SmPlanes a = planes(in, out);
+    for (int k = 0; k < np && psum; ++k) {
+      a.psum[k] = psum[k];
+      a.pmin[k] = pmin ? pmin[k] : nullptr;
+    }
+    const dim3 g((unsigned)cdiv(W, kSumTW), (unsigned)cdiv(H, kSumTH), (unsigned)np);
+    hipLaunchKernelGGL((k_smooth_2d<kSumTH, 20>), g, dim3(256), 0, s, a, H, W, d_w);
     TMH_HIP(hipGetLastError());
     return;
   }
@@ -213,12 +291,27 @@ void launch_smooth_planes(const double* const* in, double* const* out, double* c
                        dim3(256), 0, s, a1, H, W, d_w, radius);
   else
     hipLaunchKernelGGL(k_smooth_axis1_wide, grid, dim3(256), 0, s, a1, H, W, d_w, radius);
+  if (psum) launch_tile_sums(out, psum, pmin, np, H, W, s);
+  TMH_HIP(hipGetLastError());
+}
+
+void launch_tile_sums(const double* const* x, double* const* psum, double* const* pmin, int np,
+                      int H, int W, hipStream_t s) {
+  if (np <= 0) return;
+  SmPlanes p{};
+  for (int k = 0; k < np; ++k) {
+    p.in[k] = x[k];
+    p.psum[k] = psum[k];
+    p.pmin[k] = pmin ? pmin[k] : nullptr;
+  }
+  const dim3 g((unsigned)cdiv(W, kSumTW), (unsigned)cdiv(H, kSumTH), (unsigned)np);
+  hipLaunchKernelGGL(k_tile_sums, g, dim3(256), 0, s, p, H, W);
   TMH_HIP(hipGetLastError());
 }
 
 void launch_smooth(const double* in, double* out, double* tmp, int H, int W, const double* d_w,
                    int radius, hipStream_t s) {
-  launch_smooth_planes(&in, &out, &tmp, nullptr, 1, H, W, d_w, radius, s);
+  launch_smooth_planes(&in, &out, &tmp, nullptr, 1, H, W, d_w, radius, s, nullptr, nullptr);
 }
 
 void launch_smooth2(const double* in0, const double* in1, double* out0, double* out1,
@@ -227,22 +320,12 @@ void launch_smooth2(const double* in0, const double* in1, double* out0, double* 
   const double* in[2] = {in0, in1};
   double* out[2] = {out0, out1};
   double* tmp[2] = {tmp0, tmp1};
-  launch_smooth_planes(in, out, tmp, nullptr, 2, H, W, d_w, radius, s);
+  launch_smooth_planes(in, out, tmp, nullptr, 2, H, W, d_w, radius, s, nullptr, nullptr);
 }
 
 // ---------------------------------------------------------------------------
 // deterministic f64 sum (two fixed-order passes)
 // ---------------------------------------------------------------------------
-
-__device__ __forceinline__ double block_sum256(double v, double* red) {
-  red[threadIdx.x] = v;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
-  return red[0];
-}
 
 __global__ __launch_bounds__(256) void k_reduce_partial(const double* __restrict__ x, int64_t n,
                                                         double* __restrict__ partial) {
@@ -263,64 +346,6 @@ __global__ __launch_bounds__(256) void k_reduce_final(const double* __restrict__
   for (int i = threadIdx.x; i < n; i += 256) acc += partial[i];
   const double t = block_sum256(acc, red);
   if (threadIdx.x == 0) *out = t;
-}
-
-__device__ __forceinline__ double block_min256(double v, double* red) {
-  red[threadIdx.x] = v;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] = fmin(red[threadIdx.x], red[threadIdx.x + o]);
-    __syncthreads();
-  }
-  return red[0];
-}
-
-// sums of two planes at once (np.mean(std), np.mean(mean) of image.py:627):
-// blockIdx.y selects the plane, blockIdx.z the job (CoefJobs), fixed
-// partition -> deterministic.  The std plane's blocks also take the smallest
-// positive finite value (the largest mean(std)/std, which sets the
-// refinement threshold, common.h).
-__global__ __launch_bounds__(256) void k_reduce_partial2(const CoefJobs J, int64_t n) {
-  __shared__ double red[256];
-  const int j = blockIdx.z;
-  const double* x = blockIdx.y ? J.mean[j] : J.std[j];
-  double* partial = J.partial[j];
-  const int64_t chunk = cdiv(n, gridDim.x);
-  const int64_t b = (int64_t)blockIdx.x * chunk;
-  const int64_t e = (b + chunk < n) ? b + chunk : n;
-  double acc = 0.0, mn = __builtin_inf();
-  for (int64_t i = b + threadIdx.x; i < e; i += 256) {
-    const double v = x[i];
-    acc += v;
-    if (v > 0.0 && v < mn) mn = v;  // NaN fails both; +inf never below mn
-  }
-  const double t = block_sum256(acc, red);
-  if (threadIdx.x == 0) partial[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = t;
-  if (blockIdx.y == 0) {
-    __syncthreads();
-    const double m = block_min256(mn, red);
-    if (threadIdx.x == 0) partial[(int64_t)2 * gridDim.x + blockIdx.x] = m;
-  }
-}
-
-// blockIdx.y = job: sums[0] = sum(std), sums[1] = sum(mean), sums[2] = min
-// positive std
-__global__ __launch_bounds__(256) void k_reduce_final2(const CoefJobs J, int n) {
-  __shared__ double red[256];
-  const int j = blockIdx.y;
-  const double* p = J.partial[j] + (int64_t)blockIdx.x * n;
-  double* out = J.sums[j];
-  if (blockIdx.x == 2) {
-    double mn = __builtin_inf();
-    for (int i = threadIdx.x; i < n; i += 256) mn = fmin(mn, p[i]);
-    const double m = block_min256(mn, red);
-    if (threadIdx.x == 0) out[2] = m;
-    return;
-  }
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) acc += p[i];
-  const double t = block_sum256(acc, red);
-  if (threadIdx.x == 0) out[blockIdx.x] = t;
 }
 
 void launch_reduce_sum(const double* x, int64_t n, double* partial, int n_partial, double* out,
@@ -410,15 +435,35 @@ void launch_coeffs_forms(const double2* coef64, const double* sums, int64_t npx,
   TMH_HIP(hipGetLastError());
 }
 
-// Launch constants (blockIdx.x = job): mconst = (M hi, M lo, T, 0) (LUT
-// path), mconst2 = (M' hi, M' lo, 10**zero_log10 as f32 (a zero pixel's
-// floor), T) with M' = M [* log2 10], and the refinement constants; a_max =
-// S / (smallest positive std), T rounded down to f32.
-__global__ void k_refine_const(const CoefJobs J, int64_t npx) {
+// Per job (blockIdx.x): the planes' sums from the coefficient tiles'
+// partials -- sums[0] = sum(std), sums[1] = sum(mean), sums[2] = the smallest
+// positive std (np.mean(std), np.mean(mean) of image.py:627; each a fixed
+// order, deterministic) -- then the launch constants: mconst = (M hi, M lo,
+// T, 0) (LUT path), mconst2 = (M' hi, M' lo, 10**zero_log10 as f32 (a zero
+// pixel's floor), T) with M' = M [* log2 10], and the refinement constants;
+// a_max = S / (smallest positive std), T rounded down to f32.
+__global__ __launch_bounds__(256) void k_sums_const(const CoefJobs J, int n, int64_t npx) {
+  __shared__ double red[256];
   const int j = blockIdx.x;
-  const double* sums = J.sums[j];
-  const double S = sums[0] / (double)npx, M = sums[1] / (double)npx;
-  double am = fabs(S / sums[2]);  // sums[2] = +inf (no positive std): 0
+  const double* p = J.partial[j];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) acc += p[i];
+  const double s_std = block_sum256(acc, red);
+  __syncthreads();
+  acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) acc += p[n + i];
+  const double s_mean = block_sum256(acc, red);
+  __syncthreads();
+  double mn = __builtin_inf();
+  for (int i = threadIdx.x; i < n; i += 256) mn = fmin(mn, p[2 * n + i]);
+  const double s_min = block_min256(mn, red);
+  if (threadIdx.x != 0) return;
+  double* sums = J.sums[j];
+  sums[0] = s_std;
+  sums[1] = s_mean;
+  sums[2] = s_min;
+  const double S = s_std / (double)npx, M = s_mean / (double)npx;
+  double am = fabs(S / s_min);  // s_min = +inf (no positive std): 0
   if (!(am <= 1.7976931348623157e308)) am = 0.0;  // S inf/NaN: every pixel is inf/NaN anyway
   const double T = 1.0 / (kRefineK1 * am + kRefineK2);
   float Tf = (float)T;
@@ -431,14 +476,31 @@ __global__ void k_refine_const(const CoefJobs J, int64_t npx) {
   J.rc[j][0] = RefineConst{S, M, J.zero_log10[j], (double)Tf};
 }
 
-// The jobs' sums (two fixed-order passes, deterministic), then every
-// coefficient form and the launch constants: four launches for all jobs.
-void launch_coeffs_jobs(const CoefJobs& J, int n_jobs, int64_t npx, int n_partial, hipStream_t s) {
+// The jobs' tile partials (unless the smoothing already wrote them), their
+// sums and launch constants, then every coefficient form: one to three
+// launches for all jobs.  J.partial[j] holds 3 x coef_tiles(H, W) doubles:
+// std sums, mean sums, std minima.
+void launch_coeffs_jobs(const CoefJobs& J, int n_jobs, int H, int W, bool partials_ready,
+                        hipStream_t s) {
   if (n_jobs <= 0) return;
-  hipLaunchKernelGGL(k_reduce_partial2, dim3(n_partial, 2, n_jobs), dim3(256), 0, s, J, npx);
-  hipLaunchKernelGGL(k_reduce_final2, dim3(3, n_jobs), dim3(256), 0, s, J, n_partial);
+  const int nt = coef_tiles(H, W);
+  const int64_t npx = (int64_t)H * W;
+  if (!partials_ready) {
+    const double* x[kMaxPlanes];
+    double* ps[kMaxPlanes];
+    double* pm[kMaxPlanes];
+    for (int j = 0; j < n_jobs; ++j) {
+      x[2 * j] = J.std[j];
+      ps[2 * j] = J.partial[j];
+      pm[2 * j] = J.partial[j] + 2 * nt;
+      x[2 * j + 1] = J.mean[j];
+      ps[2 * j + 1] = J.partial[j] + nt;
+      pm[2 * j + 1] = nullptr;
+    }
+    launch_tile_sums(x, ps, pm, 2 * n_jobs, H, W, s);
+  }
+  hipLaunchKernelGGL(k_sums_const, dim3(n_jobs), dim3(256), 0, s, J, nt, npx);
   hipLaunchKernelGGL(k_coeffs_all, dim3((unsigned)cdiv(npx, 256), n_jobs), dim3(256), 0, s, J, npx);
-  hipLaunchKernelGGL(k_refine_const, dim3(n_jobs), dim3(1), 0, s, J, npx);
   TMH_HIP(hipGetLastError());
 }
 
@@ -446,11 +508,11 @@ void launch_coeffs_jobs(const CoefJobs& J, int n_jobs, int64_t npx, int n_partia
 // common.h), written as the launch would (low BITS bits, clip).  If the list
 // overflowed, every pixel of the launch is recomputed in f64.
 template <bool LOG, typename T, int BITS>
-__global__ __launch_bounds__(256) void k_fix_correct(const T* __restrict__ in, T* __restrict__ out,
-                                                     int64_t npx, int64_t n_sites, FixList fl,
-                                                     const double2* __restrict__ c64,
-                                                     const RefineConst* __restrict__ rc,
-                                                     int clip_lo, int clip_hi, const SiteTab tab) {
+__device__ __forceinline__ void fix_correct_body(const T* __restrict__ in, T* __restrict__ out,
+                                                 int64_t npx, int64_t n_sites, const FixList& fl,
+                                                 const double2* __restrict__ c64,
+                                                 const RefineConst* __restrict__ rc, int clip_lo,
+                                                 int clip_hi, const SiteTab& tab) {
   const unsigned int n = *fl.n;
   const bool all = n > fl.cap;
   const int64_t total = all ? n_sites * ((npx + 7) / 8) : (int64_t)n;
@@ -482,6 +544,37 @@ __global__ __launch_bounds__(256) void k_fix_correct(const T* __restrict__ in, T
       so[p] = (T)r;
     }
   }
+}
+
+template <bool LOG, typename T, int BITS>
+__global__ __launch_bounds__(256) void k_fix_correct(const T* __restrict__ in, T* __restrict__ out,
+                                                     int64_t npx, int64_t n_sites, FixList fl,
+                                                     const double2* __restrict__ c64,
+                                                     const RefineConst* __restrict__ rc,
+                                                     int clip_lo, int clip_hi, const SiteTab tab) {
+  fix_correct_body<LOG, T, BITS>(in, out, npx, n_sites, fl, c64, rc, clip_lo, clip_hi, tab);
+}
+
+// Several jobs' fixups in one launch (blockIdx.y = job, uint16 sites), each
+// job's Welford wide counters reset on the way (FixJob::wide, may be null)
+template <bool LOG>
+__global__ __launch_bounds__(256) void k_fix_correct_jobs(const FixJobs J, int64_t npx, int clip_lo,
+                                                          int clip_hi) {
+  const FixJob& f = J.j[blockIdx.y];
+  if (f.wide && blockIdx.x == 0 && threadIdx.x < 2) f.wide[threadIdx.x] = 0ull;
+  fix_correct_body<LOG, uint16_t, 16>(f.in, f.out, npx, f.n_sites, f.fl, f.c64, f.rc, clip_lo,
+                                      clip_hi, f.tab);
+}
+
+void launch_fix_correct_jobs(const FixJobs& J, int64_t npx, int log_transform, int clip_lo,
+                             int clip_hi, hipStream_t s) {
+  if (J.n <= 0) return;
+  const dim3 grid(512, (unsigned)J.n), block(256);
+  if (log_transform)
+    hipLaunchKernelGGL(k_fix_correct_jobs<true>, grid, block, 0, s, J, npx, clip_lo, clip_hi);
+  else
+    hipLaunchKernelGGL(k_fix_correct_jobs<false>, grid, block, 0, s, J, npx, clip_lo, clip_hi);
+  TMH_HIP(hipGetLastError());
 }
 
 void launch_fix_correct(const void* in, void* out, int elem_bytes, int64_t npx, int64_t n_sites,

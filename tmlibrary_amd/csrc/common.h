@@ -253,9 +253,19 @@ void launch_smooth(const double* in, double* out, double* tmp, int H, int W, con
 // np <= kMaxPlanes planes; sq (may be null): per plane 0 = read as is, else
 // the plane is M2 read as the finalized std sqrt(M2 / sq) (sq = n - 1; < 0:
 // NaN), sigma 5 only
+// psum / pmin (may be null): per plane the coefficient tiles' partial sums
+// and smallest positive values (k_tile_sums' partition), written as the
+// sigma-5 pass stores its outputs, or by k_tile_sums after the two-pass form
 void launch_smooth_planes(const double* const* in, double* const* out, double* const* tmp,
                           const double* sq, int np, int H, int W, const double* d_w, int radius,
-                          hipStream_t s);
+                          hipStream_t s, double* const* psum, double* const* pmin);
+// Coefficient tiles: kSumTH rows x kSumTW columns of a plane (the sigma-5
+// smoothing's workgroup tile); a plane's sums are fixed-order sums of its
+// tiles' partials (deterministic, whichever kernel made them)
+constexpr int kSumTH = 16, kSumTW = 216;
+int coef_tiles(int H, int W);
+void launch_tile_sums(const double* const* x, double* const* psum, double* const* pmin, int np,
+                      int H, int W, hipStream_t s);
 void launch_smooth2(const double* in0, const double* in1, double* out0, double* out1,
                     double* tmp0, double* tmp1, int H, int W, const double* d_w, int radius,
                     hipStream_t s);
@@ -284,7 +294,9 @@ struct CoefJobs {
   int log_transform[kMaxJobs];
   double zero_log10[kMaxJobs];
 };
-void launch_coeffs_jobs(const CoefJobs& J, int n_jobs, int64_t npx, int n_partial, hipStream_t s);
+// partials_ready: J.partial already holds the tiles' sums (the smoothing wrote them)
+void launch_coeffs_jobs(const CoefJobs& J, int n_jobs, int H, int W, bool partials_ready,
+                        hipStream_t s);
 // coef (LUT path) and coef_lin (chain) from coef64 + sums, for a job whose
 // coefficient launch left them out (CoefJobs entries null)
 void launch_coeffs_forms(const double2* coef64, const double* sums, int64_t npx, int log_transform,
@@ -295,6 +307,23 @@ void launch_fix_correct(const void* in, void* out, int elem_bytes, int64_t npx, 
                         const FixList& fl, const double2* coef64, const RefineConst* rc,
                         int log_transform, int clip_lo, int clip_hi, hipStream_t s,
                         const SiteTab& tab = SiteTab{});
+// Several uint16 jobs' fixups in one launch (the multi-job fused pass)
+struct FixJob {
+  const uint16_t* in;
+  uint16_t* out;
+  int64_t n_sites;
+  FixList fl;
+  const double2* c64;
+  const RefineConst* rc;
+  SiteTab tab;
+  unsigned long long* wide;  // the job's Welford wide counters to reset, or null
+};
+struct FixJobs {
+  FixJob j[kMaxJobs];
+  int n;
+};
+void launch_fix_correct_jobs(const FixJobs& J, int64_t npx, int log_transform, int clip_lo,
+                             int clip_hi, hipStream_t s);
 void launch_correct_u16(const uint16_t* in, uint16_t* out, int64_t npx, int64_t n_sites,
                         const float4* coef, const float2* lut, const float4* mconst,
                         const FixList& fl, int log_transform, int clip_lo, int clip_hi,
