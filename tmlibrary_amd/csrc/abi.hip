@@ -244,7 +244,6 @@ struct tmh_stats {
   // above it, a two-jobs-in-flight bench ran 4-6% slower: profiles/r4/
   // ab_jobs_in_flight_priority_r4y.txt.)
   hipStream_t tail = nullptr;
-  hipEvent_t ev_tail = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;  // ordering against a caller's stream
   // work on other streams the handle's stream must wait for, joined lazily
@@ -534,7 +533,6 @@ void tmh_stats_destroy(tmh_stats* h) {
   hipStream_t s = h->own_stream, side = h->side, tail = h->tail;
   if (side) (void)hipStreamSynchronize(side);
   if (tail) (void)hipStreamSynchronize(tail);
-  if (h->ev_tail) (void)hipEventDestroy(h->ev_tail);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
@@ -1690,7 +1688,6 @@ static void fused_finish(FusedPass& p, bool fixed = false) {
   if (p.cross) {
     if (!h->tail) {  // created on first use: every stream takes a hardware queue slot
       TMH_HIP(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
-      TMH_HIP(hipEventCreateWithFlags(&h->ev_tail, hipEventDisableTiming));
     }
     TMH_HIP(hipEventRecord(h->ev_out, s));
     TMH_HIP(hipStreamWaitEvent(h->tail, h->ev_out, 0));

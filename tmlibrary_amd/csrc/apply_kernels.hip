@@ -324,38 +324,6 @@ void launch_smooth2(const double* in0, const double* in1, double* out0, double* 
 }
 
 // ---------------------------------------------------------------------------
-// deterministic f64 sum (two fixed-order passes)
-// ---------------------------------------------------------------------------
-
-__global__ __launch_bounds__(256) void k_reduce_partial(const double* __restrict__ x, int64_t n,
-                                                        double* __restrict__ partial) {
-  __shared__ double red[256];
-  const int64_t chunk = cdiv(n, gridDim.x);
-  const int64_t b = (int64_t)blockIdx.x * chunk;
-  const int64_t e = (b + chunk < n) ? b + chunk : n;
-  double acc = 0.0;
-  for (int64_t i = b + threadIdx.x; i < e; i += 256) acc += x[i];
-  const double t = block_sum256(acc, red);
-  if (threadIdx.x == 0) partial[blockIdx.x] = t;
-}
-
-__global__ __launch_bounds__(256) void k_reduce_final(const double* __restrict__ partial, int n,
-                                                      double* __restrict__ out) {
-  __shared__ double red[256];
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) acc += partial[i];
-  const double t = block_sum256(acc, red);
-  if (threadIdx.x == 0) *out = t;
-}
-
-void launch_reduce_sum(const double* x, int64_t n, double* partial, int n_partial, double* out,
-                       hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_partial, dim3(n_partial), dim3(256), 0, s, x, n, partial);
-  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(256), 0, s, partial, n_partial, out);
-  TMH_HIP(hipGetLastError());
-}
-
-// ---------------------------------------------------------------------------
 // correction coefficients
 // ---------------------------------------------------------------------------
 

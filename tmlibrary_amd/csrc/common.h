@@ -269,8 +269,6 @@ void launch_tile_sums(const double* const* x, double* const* psum, double* const
 void launch_smooth2(const double* in0, const double* in1, double* out0, double* out1,
                     double* tmp0, double* tmp1, int H, int W, const double* d_w, int radius,
                     hipStream_t s);
-void launch_reduce_sum(const double* x, int64_t n, double* partial, int n_partial, double* out,
-                       hipStream_t s);
 void launch_build_corr_lut(float2* lut, int log_transform, double zero_log10, hipStream_t s);
 // Per job (a corrector) of a coefficient launch: its (smoothed) mean / std
 // planes, the reduction scratch (3 x n_partial) and sums (sum(std),
