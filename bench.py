@@ -129,11 +129,12 @@ def parse():
                         "this many statistics handles / correctors / streams, so job k+1's "
                         "Welford pass runs while job k's histogram tail finishes (each job "
                         "still complete and checked; 1 = one job at a time)")
-    p.add_argument("--jobs-order", choices=["welford", "corrected"], default="welford",
+    p.add_argument("--jobs-order", choices=["welford", "planes", "corrected"], default="welford",
                    help="jobs in flight: job k+1's Welford pass starts after job k's Welford pass "
                         "(sharing HBM with job k's corrected pass, hiding job k's small kernels "
-                        "and tail) or after job k's corrected pass (hiding only the tail); a "
-                        "third, pipelined order measured no better (DESIGN.md 9.5)")
+                        "and tail), after job k's planes, or after job k's corrected pass "
+                        "(hiding only the tail); a pipelined order measured no better "
+                        "(DESIGN.md 9.5, 10.7)")
     p.add_argument("--planes", choices=["multi", "per-job"], default="multi",
                    help="finalize -> smoothing -> coefficients: every channel's in one launch per "
                         "kernel (tmh_job_planes_multi_device) or per channel (finalize, "
@@ -151,6 +152,11 @@ def parse():
                         "(concurrent); or job p+1's Welford passes before job p's corrected "
                         "pass, every small step of the jobs in flight under a Welford pass (deep, "
                         "three channel sets: measured slower, DESIGN.md 10.3)")
+    p.add_argument("--prefetch-probe", choices=["on", "off"], default="off",
+                   help="jobs in flight: queue the next job's reset and site probe right after "
+                        "this job's Welford pass (on): its Welford launch then does not wait "
+                        "for the probe behind this job's corrected pass (measured 0.5-1%% "
+                        "slower, profiles/r5/ab_jobs_order_prefetch_r6j.jsonl)")
     p.add_argument("--pass-launch", choices=["multi", "per-channel"], default="multi",
                    help="several channels, serial or pipelined order: every channel's corrected "
                         "pass in ONE fused launch (tmh_correct_u16_hist_multi_blocks_device) or "
@@ -1535,7 +1541,7 @@ def main():
     # merges, histogram tails and the next job's probe) all run under Welford
     # passes; three channel sets (jobs p-1, p, p+1 in flight)
     deep = a.channel_order == "deep" and pass_sp is not None and fused and B
-    if pass_sp is not None:
+    if pass_sp is not None or (J > 1 and a.prefetch_probe == "on"):
         probe_stream = torch.cuda.Stream(dev)
         probe_sp[0] = C.c_void_p(probe_stream.cuda_stream)
     if deep:
@@ -1615,17 +1621,35 @@ def main():
             return
         if J > 1:
             ch = lanes[jobs["k"] % J]
+            nxt = lanes[(jobs["k"] + 1) % J]
             jobs["k"] += 1
-            gate = jobs["welford"] if a.jobs_order == "welford" else jobs["applied"]
+            gate = {"welford": jobs["welford"], "planes": jobs.get("planes"),
+                    "corrected": jobs["applied"]}[a.jobs_order]
             if gate is not None:  # after the previous job's Welford (or corrected) pass
                 ch.stream.wait_event(gate)
-            ch.stats()
+            if id(ch) in jobs["probed"]:  # reset and probed one step ago
+                jobs["probed"].discard(id(ch))
+                ch.welford()
+            else:
+                ch.stats()
             ev_w = torch.cuda.Event()
             ev_w.record(ch.stream)
             jobs["welford"] = ev_w
+            if a.prefetch_probe == "on" and not last and nxt is not ch:
+                # the next job's reset (after its lane's previous job) and site
+                # probe (on the probe stream, sites resident) now: they run
+                # under this job's passes, so the next Welford launch finds
+                # its probe done instead of waiting for it behind this job's
+                # corrected pass
+                nxt.reset_probe()
+                jobs["probed"].add(id(nxt))
+            ch.planes()
+            ev_p = torch.cuda.Event()
+            ev_p.record(ch.stream)
+            jobs["planes"] = ev_p
             if jobs["applied"] is not None:  # corrected passes in job order (shared outputs)
                 ch.cstream.wait_event(jobs["applied"])
-            ch.apply()
+            ch.corrected()
             ev = torch.cuda.Event()
             ev.record(ch.cstream)
             jobs["applied"] = ev
@@ -2011,6 +2035,7 @@ def main():
                                              "sites' blocks" if share_out else "private"),
                        "pipeline": a.pipeline,
                        "jobs_in_flight": J if CH == 1 else CJ,
+                       "prefetch_probe": a.prefetch_probe if J > 1 else None,
                        "planes": a.planes,
                        "channel_order": a.channel_order if CH > 1 else None,
                        "pass_launch": ("multi" if multi_pass else "per-channel") if CH > 1 else None,

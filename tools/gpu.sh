@@ -24,6 +24,7 @@
 #   prof432        rocprofv3 kernel trace of dist432 -> rocprof_dist432_TAG/
 #   prof:DIST      rocprofv3 --kernel-trace --stats of a short bench on DIST
 #                  (synthetic | bright) -> rocprof_DIST_TAG/
+#   profh[:DIST]   prof with the HIP runtime trace (host waits) -> rocprof_h_DIST_TAG/
 #   pmc:DIST       FETCH_SIZE and WRITE_SIZE passes (each its own run) of a
 #                  short bench on DIST -> pmc_traffic_DIST_TAG.json
 #   ab:R:LIB,LIB   same-box A/B of library builds (TMH_LIB), R rounds, the
@@ -145,6 +146,14 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rocprof_${D}_$TAG -o run \
         -- python3 $SB --distribution $D > $O/rocprof_${D}_$TAG.json 2> $O/rocprof_${D}_$TAG.log || exit $?
       summ $O/rocprof_${D}_$TAG.json
+      ;;
+    profh)
+      # prof with the HIP runtime calls on the kernels' clock: profh[:DIST]
+      D=${a1:-synthetic}
+      timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-trace \
+        --output-format csv -d $O/rocprof_h_${D}_$TAG -o run \
+        -- python3 $SB --distribution $D > $O/rocprof_h_${D}_$TAG.json 2> $O/rocprof_h_${D}_$TAG.log || exit $?
+      summ $O/rocprof_h_${D}_$TAG.json
       ;;
     pmc)
       D=${a1:-synthetic}
