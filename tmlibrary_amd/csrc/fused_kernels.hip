@@ -36,6 +36,15 @@
 namespace tmh {
 
 constexpr int kFusedBands = 16;  // pixel bands of the unit sweep
+// cache policy bits of the site loads and corrected stores (2: streamed,
+// non-temporal); overridable at build time for A/B builds
+#ifndef TMH_FUSED_LOAD_AUX
+#define TMH_FUSED_LOAD_AUX 2
+#endif
+#ifndef TMH_FUSED_STORE_AUX
+#define TMH_FUSED_STORE_AUX 2
+#endif
+constexpr int kFusedLoadAux = TMH_FUSED_LOAD_AUX, kFusedStoreAux = TMH_FUSED_STORE_AUX;
 
 // A pointer every lane holds the same value of, moved to scalar registers: a
 // buffer resource built from a pointer loaded with a vector load (a block
@@ -303,7 +312,8 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     const int off = g < un.g1 ? g * 16 : kOOB;
 #pragma unroll
     for (int k = 0; k < SPU; ++k) {
-      const u32x4_t w = __builtin_amdgcn_raw_buffer_load_b128(un.rin, off, k * site_bytes, 2);
+      const u32x4_t w =
+          __builtin_amdgcn_raw_buffer_load_b128(un.rin, off, k * site_bytes, kFusedLoadAux);
       v[k] = make_uint4(w.x, w.y, w.z, w.w);
     }
     if (!(ABL & 2)) {
@@ -404,7 +414,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
         for (int k = 0; k < SPU; ++k)
           if (k < un.ns)
             __builtin_amdgcn_raw_buffer_store_b128(process(v[k], k, cf, g), un.rout, g * 16,
-                                                   k * site_bytes, 2);
+                                                   k * site_bytes, kFusedStoreAux);
       }
     };
     const int iters = (un.g1 - un.g0 + NT - 1) / NT;
