@@ -1656,21 +1656,19 @@ static void fused_prepare(FusedPass& p) {
   p.fl = corrector_fixlist(c, n_sites, s);
 }
 
-// what follows the job's fused launch: rare lists, f64 fixups, the very wide
-// configuration's histograms, and the histogram tail.  fixed: the caller
+// what follows the job's fused launch up to its histogram tail: rare lists,
+// f64 fixups and the very wide configuration's histograms.  fixed: the caller
 // launched the fixups (and the wide counters' reset) for several jobs at once.
-static void fused_finish(FusedPass& p, bool fixed = false) {
+static void fused_post(FusedPass& p, bool fixed) {
   tmh_stats* h = p.h;
   tmh_corrector* c = p.c;
   const int64_t n_sites = p.n;
   hipStream_t s = p.s;
-  const bool very_wide = p.cfg == kFusedNoHist;
-  const unsigned long long* rm_all = reinterpret_cast<const unsigned long long*>(c->queues.p + 8);
   if (p.cfg == kFusedWide) launch_rare_count(p.rl, h->hist_full.p, n_sites, s);
   if (!fixed)
     launch_fix_correct(p.in, p.out, 2, c->npx, n_sites, p.fl, c->coef64.p, c->rc.p,
                        c->log_transform, p.clip_lo, p.clip_hi, s, p.tab);
-  if (very_wide)  // the histograms from one more read of the sites
+  if (p.cfg == kFusedNoHist)  // the histograms from one more read of the sites
     launch_hist_site_u16(p.in, h->npx, n_sites, h->hist_full.p, h->qp, p.vlh, p.ld, h->pooled.p,
                          h->pooled_parts.p, kPooledParts, h->zeros.p, p.sh, nullptr, 0, s, p.tab);
   // the Welford pass's diagnostic wide counts restart with the next batch
@@ -1679,24 +1677,30 @@ static void fused_finish(FusedPass& p, bool fixed = false) {
     if (!fixed) TMH_HIP(hipMemsetAsync(h->wide.p, 0, 16, s));
     h->wide_sites = 0;
   }
-  // The histogram tail (order statistics, percentile sums) reads only the
-  // handle's buffers: called on another stream than the handle's, it runs on
-  // the handle's tail stream (the handle's stream waits for it), so s is free
-  // as soon as the corrected sites are written (a caller pipelining jobs
-  // starts the next one's Welford pass under this one's tail).
-  hipStream_t ts = s;
-  if (p.cross) {
-    if (!h->tail) {  // created on first use: every stream takes a hardware queue slot
-      TMH_HIP(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
-    }
-    TMH_HIP(hipEventRecord(h->ev_out, s));
-    TMH_HIP(hipStreamWaitEvent(h->tail, h->ev_out, 0));
-    ts = h->tail;
+}
+
+// The histogram tail (order statistics, percentile sums) reads only the
+// handle's buffers: called on another stream than the handle's, it runs on
+// the handle's tail stream (the handle's stream waits for it), so s is free
+// as soon as the corrected sites are written (a caller pipelining jobs
+// starts the next one's Welford pass under this one's tail).
+static hipStream_t fused_tail_stream(const FusedPass& p) {
+  tmh_stats* h = p.h;
+  if (!p.cross) return p.s;
+  if (!h->tail) {  // created on first use: every stream takes a hardware queue slot
+    TMH_HIP(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
   }
-  if (!very_wide)
-    launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, n_sites, h->qp, p.vlh, p.ld,
-                         h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, p.sh, ts,
-                         false, rm_all);
+  TMH_HIP(hipEventRecord(h->ev_out, p.s));
+  TMH_HIP(hipStreamWaitEvent(h->tail, h->ev_out, 0));
+  return h->tail;
+}
+
+// the tail's percentile sums and the handle's bookkeeping; ts: the stream
+// the job's order statistics were queued on
+static void fused_tail_end(FusedPass& p, hipStream_t ts) {
+  tmh_stats* h = p.h;
+  tmh_corrector* c = p.c;
+  const int64_t n_sites = p.n;
   if (!(h->flags & TMH_STATS_DEFERRED_PCT))
     launch_pct_accumulate(p.vlh, n_sites, p.ld, h->Q, h->gamma.p, h->acc.p, ts);
   h->hist_dirty = false;
@@ -1709,6 +1713,17 @@ static void fused_finish(FusedPass& p, bool fixed = false) {
     TMH_HIP(hipEventRecord(c->ev_tail, ts));
     c->tail_pending = true;
   }
+}
+
+static void fused_finish(FusedPass& p) {
+  fused_post(p, false);
+  hipStream_t ts = fused_tail_stream(p);
+  tmh_stats* h = p.h;
+  if (p.cfg != kFusedNoHist)
+    launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, p.n, h->qp, p.vlh, p.ld, h->pooled.p,
+                         h->pooled_parts.p, kPooledParts, h->zeros.p, p.sh, ts, false,
+                         reinterpret_cast<const unsigned long long*>(p.c->queues.p + 8));
+  fused_tail_end(p, ts);
 }
 
 static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev_in,
@@ -1885,7 +1900,38 @@ static void correct_hist_multi(tmh_corrector* const* cs, tmh_stats* const* hs, i
                         p[j].h->pending - p[j].n == 0 ? p[j].h->wide.p : nullptr};
   }
   launch_fix_correct_jobs(F, c0->npx, c0->log_transform, clip_lo, clip_hi, s);
-  for (int j = 0; j < np; ++j) fused_finish(p[j], true);
+  for (int j = 0; j < np; ++j) fused_post(p[j], true);
+  // every job's histogram tail (column sums, order statistics) in two
+  // launches on one stream: the first job's tail stream when the jobs run
+  // off their handles' streams, else s
+  bool same_cross = true;
+  for (int j = 1; j < np; ++j) same_cross = same_cross && p[j].cross == p[0].cross;
+  if (!same_cross) {  // mixed: per-job tails
+    for (int j = 0; j < np; ++j) {
+      hipStream_t ts = fused_tail_stream(p[j]);
+      tmh_stats* h = p[j].h;
+      if (p[j].cfg != kFusedNoHist)
+        launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, p[j].n, h->qp, p[j].vlh, p[j].ld,
+                             h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, p[j].sh, ts,
+                             false,
+                             reinterpret_cast<const unsigned long long*>(p[j].c->queues.p + 8));
+      fused_tail_end(p[j], ts);
+    }
+    return;
+  }
+  hipStream_t ts = fused_tail_stream(p[0]);
+  TailJobs T{};
+  for (int j = 0; j < np; ++j) {
+    if (p[j].cfg == kFusedNoHist) continue;  // its order statistics are written
+    tmh_stats* h = p[j].h;
+    QPos qp = h->qp;
+    qp.tstride = p[j].ld * kOsTile;
+    T.j[T.n++] = TailJob{h->hist_full.p, h->hist_rmask.p,
+                         reinterpret_cast<const unsigned long long*>(p[j].c->queues.p + 8), qp,
+                         p[j].vlh, h->pooled.p, h->zeros.p, p[j].sh, p[j].n};
+  }
+  launch_hist_finalize_jobs(T, ts);
+  for (int j = 0; j < np; ++j) fused_tail_end(p[j], ts);
 }
 
 int tmh_correct_u16_hist_multi_device(tmh_corrector* const* correctors, tmh_stats* const* handles,

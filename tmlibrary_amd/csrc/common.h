@@ -247,6 +247,23 @@ struct ZeroList {
 void launch_zero_u64(const ZeroList& z, hipStream_t s);
 
 constexpr int kMaxJobs = 8;          // jobs (a rank's channels) of one multi-job launch
+// Several fused jobs' histogram tails (same image size)
+struct TailJob {
+  uint32_t* hist;                  // the job's histogram slab (zero-maintained)
+  unsigned long long* rmask;       // per site: rounds holding counts (zero-maintained)
+  const unsigned long long* rm_all;  // the union of the masks
+  QPos qp;                         // the handle's quantile table (tstride set)
+  uint32_t* vlh;                   // order statistics of the job's first site
+  unsigned long long* pooled;
+  int64_t* zero_counts;
+  uint32_t* site_hist;             // may be null
+  int64_t n_sites;
+};
+struct TailJobs {
+  TailJob j[kMaxJobs];
+  int n;
+};
+void launch_hist_finalize_jobs(const TailJobs& J, hipStream_t s);
 constexpr int kMaxPlanes = 2 * kMaxJobs;
 void launch_smooth(const double* in, double* out, double* tmp, int H, int W, const double* d_w,
                    int radius, hipStream_t s);

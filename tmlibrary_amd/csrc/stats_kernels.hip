@@ -733,6 +733,31 @@ struct FinSR {
   static constexpr int value = NT >= 1024 ? 4 : 1;
 };
 
+template <int ABL, int NT>
+__device__ __forceinline__ void hist_finalize_site(
+    int64_t s, uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask,
+    int dense_rounds, const QPos& p, uint32_t* __restrict__ vlh_all,
+    unsigned long long* __restrict__ pooled, int n_pooled, int64_t* __restrict__ zero_counts,
+    uint32_t* __restrict__ site_hist) {
+  constexpr int SR = FinSR<NT>::value;
+  __shared__ uint32_t slots[32];
+  __shared__ int32_t starts[2 * SR * kRound];
+  const unsigned long long rm = rmask ? rmask[s] : ~0ull;
+  __syncthreads();
+  if (rmask && !(ABL & 8) && threadIdx.x == 0) rmask[s] = 0ull;  // every thread has read it
+  uint32_t* h = hist + s * (int64_t)kBins;
+  // sites spread their pooled-histogram adds over n_pooled copies (fewer
+  // same-address atomic collisions); k_pooled_fold sums the copies
+  unsigned long long* pl = pooled ? pooled + (int64_t)(s % n_pooled) * kBins : nullptr;
+  const unsigned long long dense = dense_rounds >= 64 ? ~0ull : ((1ull << dense_rounds) - 1ull);
+  hist_tail_rounds<ABL & 7, NT, SR>(
+      dense | rm, [&](uint32_t b) -> uint32_t { return h[b]; },
+      [&](uint32_t b, uint32_t c) {
+        if (!(ABL & 8) && c) h[b] = 0u;
+      },
+      s, p, vlh_all, pl, zero_counts, site_hist, slots, starts);
+}
+
 template <int ABL = 0, int NT = kHistThreads>
 __global__ __launch_bounds__(NT, 8) void k_hist_finalize(
     uint32_t* __restrict__ hist, unsigned long long* __restrict__ rmask, int dense_rounds,
@@ -742,24 +767,18 @@ __global__ __launch_bounds__(NT, 8) void k_hist_finalize(
     const unsigned long long* __restrict__ wide = nullptr, unsigned long long xthr = 0) {
   // a very wide launch: k_hist_site_u16 has written this site's outputs
   if (wide && __builtin_nontemporal_load(wide + 1) >= xthr) return;
-  constexpr int SR = FinSR<NT>::value;
-  __shared__ uint32_t slots[32];
-  __shared__ int32_t starts[2 * SR * kRound];
-  const int64_t s = blockIdx.x;
-  const unsigned long long rm = rmask ? rmask[s] : ~0ull;
-  __syncthreads();
-  if (rmask && !(ABL & 8) && threadIdx.x == 0) rmask[s] = 0ull;  // every thread has read it
-  uint32_t* h = hist + s * (int64_t)kBins;
-  // sites spread their pooled-histogram adds over n_pooled copies (fewer
-  // same-address atomic collisions); k_pooled_fold sums the copies
-  unsigned long long* pl = pooled ? pooled + (int64_t)(blockIdx.x % n_pooled) * kBins : nullptr;
-  const unsigned long long dense = dense_rounds >= 64 ? ~0ull : ((1ull << dense_rounds) - 1ull);
-  hist_tail_rounds<ABL & 7, NT, SR>(
-      dense | rm, [&](uint32_t b) -> uint32_t { return h[b]; },
-      [&](uint32_t b, uint32_t c) {
-        if (!(ABL & 8) && c) h[b] = 0u;
-      },
-      s, p, vlh_all, pl, zero_counts, site_hist, slots, starts);
+  hist_finalize_site<ABL, NT>(blockIdx.x, hist, rmask, dense_rounds, p, vlh_all, pooled, n_pooled,
+                              zero_counts, site_hist);
+}
+
+// Several jobs' finalize in one launch (blockIdx.y = job): each site's order
+// statistics from its job's histogram slab and round mask (the pooled
+// histograms come from the column sum)
+__global__ __launch_bounds__(kHistThreads, 8) void k_hist_finalize_jobs(const TailJobs J) {
+  const TailJob& t = J.j[blockIdx.y];
+  if ((int64_t)blockIdx.x >= t.n_sites) return;  // uniform per workgroup
+  hist_finalize_site<0, kHistThreads>(blockIdx.x, t.hist, t.rmask, 0, t.qp, t.vlh, nullptr, 1,
+                                      t.zero_counts, t.site_hist);
 }
 
 // Pooled histogram of a fused launch's sites without per-site atomics:
@@ -771,11 +790,11 @@ __global__ __launch_bounds__(NT, 8) void k_hist_finalize(
 // this replaced ~30,000 per-site atomics per site in the finalize (1.2 ms of
 // its 2.4 ms at 3,456 sites: profiles/r2/mb_tail_bright_r2y.txt).
 constexpr int kColSites = 32;
-__global__ __launch_bounds__(256) void k_pooled_colsum(const uint32_t* __restrict__ hist,
-                                                       const unsigned long long* __restrict__ rmask,
-                                                       const unsigned long long* __restrict__ rm_all,
-                                                       int64_t n_sites,
-                                                       unsigned long long* __restrict__ pooled) {
+__device__ __forceinline__ void pooled_colsum_chunk(const uint32_t* __restrict__ hist,
+                                                    const unsigned long long* __restrict__ rmask,
+                                                    const unsigned long long* __restrict__ rm_all,
+                                                    int64_t n_sites,
+                                                    unsigned long long* __restrict__ pooled) {
   static_assert(kColSites <= 256, "one mask per thread");
   __shared__ uint32_t use[kColSites];  // per site of the chunk: this round holds counts
   __shared__ int any;
@@ -800,6 +819,37 @@ __global__ __launch_bounds__(256) void k_pooled_colsum(const uint32_t* __restric
   for (int s = 0; s < ns; ++s)
     if (use[s]) t += h[(int64_t)s * kBins];
   if (t) atomicAdd(&pooled[b], t);
+}
+
+__global__ __launch_bounds__(256) void k_pooled_colsum(const uint32_t* __restrict__ hist,
+                                                       const unsigned long long* __restrict__ rmask,
+                                                       const unsigned long long* __restrict__ rm_all,
+                                                       int64_t n_sites,
+                                                       unsigned long long* __restrict__ pooled) {
+  pooled_colsum_chunk(hist, rmask, rm_all, n_sites, pooled);
+}
+
+// blockIdx.z = job (TailJobs)
+__global__ __launch_bounds__(256) void k_pooled_colsum_jobs(const TailJobs J) {
+  const TailJob& t = J.j[blockIdx.z];
+  if ((int64_t)blockIdx.y * kColSites >= t.n_sites) return;  // uniform per workgroup
+  pooled_colsum_chunk(t.hist, t.rmask, t.rm_all, t.n_sites, t.pooled);
+}
+
+// Several fused jobs' histogram tails (pooled column sums, then every site's
+// order statistics) in two launches
+void launch_hist_finalize_jobs(const TailJobs& J, hipStream_t s) {
+  if (J.n <= 0) return;
+  ProfScope prof("hist_finalize", s);
+  int64_t nmax = 0;
+  for (int j = 0; j < J.n; ++j) nmax = std::max(nmax, J.j[j].n_sites);
+  if (nmax <= 0) return;
+  hipLaunchKernelGGL(k_pooled_colsum_jobs,
+                     dim3(kBins / 256, (unsigned)cdiv(nmax, kColSites), (unsigned)J.n), dim3(256), 0,
+                     s, J);
+  hipLaunchKernelGGL(k_hist_finalize_jobs, dim3((unsigned)nmax, (unsigned)J.n), dim3(kHistThreads),
+                     0, s, J);
+  TMH_HIP(hipGetLastError());
 }
 
 // pooled[b] += sum of the copies; copies reset to zero (zero-maintained)
