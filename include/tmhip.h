@@ -97,7 +97,7 @@ int tmh_stats_reset(tmh_stats* h);
  *                          a value >= 16,384 ("very wide" sites, e.g. uniform
  *                          16-bit data), the pass runs without its histogram
  *                          and a per-site u16-pair LDS histogram pass (one
- *                          more read) builds them.
+ *                          more read) builds them; 100 forces that form.
  *   TMH_OPT_WELFORD_PARTS  0 (default): automatic -- with the log transform,
  *                          a launch of >= 96 sites whose job probe found >=
  *                          10% of the groups holding a value >= 4,096 (bright

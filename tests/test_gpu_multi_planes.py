@@ -168,13 +168,19 @@ def test_corrector_update_multi_equals_single(L):
     d_out.free()
 
 
-@pytest.mark.parametrize("layout", ["contiguous", "blocks"])
-def test_correct_hist_multi_equals_per_job(L, layout):
+@pytest.mark.parametrize("layout,streams", [("contiguous", "cross"), ("blocks", "cross"),
+                                            ("contiguous", "own"), ("contiguous", "mixed")])
+def test_correct_hist_multi_equals_per_job(L, layout, streams):
     """tmh_correct_u16_hist_multi(_blocks)_device against one
     tmh_correct_u16_hist(_blocks)_device per job: corrected pixels, per-site
     histograms, pooled histogram, order statistics (percentile sums) and
     moments bit for bit.  Jobs 0 and 2 share the narrow configuration (one
-    launch); job 1 is bright (packed configuration: its own launch)."""
+    launch); job 1 is bright (packed configuration: its own launch); job 3 is
+    forced to the very wide configuration (histograms from a second read, no
+    finalize in the batched histogram tail).  streams: the call's stream is
+    none of the handles' streams (cross: the tails batched on the first
+    handle's tail stream), all of them (own: batched on the call's stream), or
+    only the first's (mixed: per-job tails)."""
     import torch
 
     from tmlibrary_amd import hip, synth
@@ -182,9 +188,9 @@ def test_correct_hist_multi_equals_per_job(L, layout):
     from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
     H, W = 216, 256
     npx = H * W
-    ns = (9, 8, 5)
+    ns = (9, 8, 5, 6)
     n = len(ns)
-    kinds = (synth.STANDARD, synth.BRIGHT, synth.STANDARD)
+    kinds = (synth.STANDARD, synth.BRIGHT, synth.STANDARD, synth.STANDARD)
     sites = [np.stack([synth.synth_exact_host(H, W, 500 + j, j, i, kinds[j]) for i in range(k)])
              for j, k in enumerate(ns)]
     sites[1][:, :3, :40] = 60000  # values beyond the packed slices (rare lists)
@@ -199,11 +205,17 @@ def test_correct_hist_multi_equals_per_job(L, layout):
     for mode in ("per-job", "multi"):
         d_out = [Dev(L, s.nbytes) for s in sites]
         hs, cs, planes = [], [], []
+        ps = torch.cuda.Stream(dev)
+        sp = C.c_void_p(ps.cuda_stream)
         for j in range(n):
             h = C.c_void_p()
             hip.check(L.tmh_stats_create(H, W, len(lo), hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
                                          hip.ptr(lut), 1, hip.TMH_STATS_KEEP_SITE_HIST,
                                          C.byref(h)))
+            if streams == "own" or (streams == "mixed" and j == 0):
+                hip.check(L.tmh_stats_set_stream(h, sp))
+            if j == 3:
+                hip.check(L.tmh_stats_set_option(h, hip.TMH_OPT_FUSED_CONFIG, 100))
             hs.append(h)
             planes.append([Dev(L, npx * 8) for _ in range(6)])
         L.tmh_synchronize(None)
@@ -235,8 +247,6 @@ def test_correct_hist_multi_equals_per_job(L, layout):
             hip.check(L.tmh_smooth2_f64_device(m.p, sd.p, sm.p, ss.p, t.p, t2.p, H, W, 5.0, None))
             hip.check(L.tmh_corrector_update_device(cs[j], sm.p, ss.p, None))
             L.tmh_synchronize(None)
-        ps = torch.cuda.Stream(dev)
-        sp = C.c_void_p(ps.cuda_stream)
         arr = lambda xs: (C.c_void_p * n)(*[C.c_void_p(x) for x in xs])  # noqa: E731
         if mode == "per-job":
             for j in range(n):
@@ -263,7 +273,7 @@ def test_correct_hist_multi_equals_per_job(L, layout):
             fc = C.c_int()
             hip.check(L.tmh_stats_job_choice(hs[j], None, None, C.byref(fc)))
             cfg.append(fc.value)
-        assert cfg == [3, 5, 3], cfg
+        assert cfg == [3, 5, 3, 100], cfg
         L.tmh_synchronize(None)
         torch.cuda.synchronize()
         out = []

@@ -559,8 +559,8 @@ int tmh_stats_set_option(tmh_stats* h, int option, int value) {
     TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
     switch (option) {
       case TMH_OPT_FUSED_CONFIG:
-        TMH_CHECK(value >= kFusedAuto && value < kFusedConfigs, TMH_EINVAL,
-                  "fused configuration out of range");
+        TMH_CHECK((value >= kFusedAuto && value < kFusedConfigs) || value == kFusedNoHist,
+                  TMH_EINVAL, "fused configuration out of range");
         h->fused_cfg = value;
         break;
       case TMH_OPT_WELFORD_PARTS:
