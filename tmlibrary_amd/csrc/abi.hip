@@ -1715,15 +1715,20 @@ static void fused_tail_end(FusedPass& p, hipStream_t ts) {
   }
 }
 
-static void fused_finish(FusedPass& p) {
-  fused_post(p, false);
+// one job's histogram tail, on its handle's tail stream (or s)
+static void fused_tail(FusedPass& p) {
   hipStream_t ts = fused_tail_stream(p);
   tmh_stats* h = p.h;
-  if (p.cfg != kFusedNoHist)
+  if (p.cfg != kFusedNoHist)  // (very wide: k_hist_site_u16 wrote the order statistics)
     launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, p.n, h->qp, p.vlh, p.ld, h->pooled.p,
                          h->pooled_parts.p, kPooledParts, h->zeros.p, p.sh, ts, false,
                          reinterpret_cast<const unsigned long long*>(p.c->queues.p + 8));
   fused_tail_end(p, ts);
+}
+
+static void fused_finish(FusedPass& p) {
+  fused_post(p, false);
+  fused_tail(p);
 }
 
 static void correct_hist_dev(tmh_corrector* c, tmh_stats* h, const uint16_t* dev_in,
@@ -1907,16 +1912,7 @@ static void correct_hist_multi(tmh_corrector* const* cs, tmh_stats* const* hs, i
   bool same_cross = true;
   for (int j = 1; j < np; ++j) same_cross = same_cross && p[j].cross == p[0].cross;
   if (!same_cross) {  // mixed: per-job tails
-    for (int j = 0; j < np; ++j) {
-      hipStream_t ts = fused_tail_stream(p[j]);
-      tmh_stats* h = p[j].h;
-      if (p[j].cfg != kFusedNoHist)
-        launch_hist_finalize(h->hist_full.p, h->hist_rmask.p, 0, p[j].n, h->qp, p[j].vlh, p[j].ld,
-                             h->pooled.p, h->pooled_parts.p, kPooledParts, h->zeros.p, p[j].sh, ts,
-                             false,
-                             reinterpret_cast<const unsigned long long*>(p[j].c->queues.p + 8));
-      fused_tail_end(p[j], ts);
-    }
+    for (int j = 0; j < np; ++j) fused_tail(p[j]);
     return;
   }
   hipStream_t ts = fused_tail_stream(p[0]);
