@@ -121,6 +121,9 @@ def parse():
                         "takes its contiguous path, the fused pass a block table into it) or in "
                         "B-site blocks allocated alternately with the output blocks")
     p.add_argument("--no-profile", action="store_true", help="skip per-kernel event timing")
+    p.add_argument("--no-box", action="store_true",
+                   help="skip the box probe (the box's copy / read rate and shader clock over "
+                        "the job's own buffers, reported as 'box')")
     p.add_argument("--hbm-skip-gb", type=float, default=0.0,
                    help="hold an allocation of this many GB before the sites' buffers "
                         "(placement study: which HBM region the first buffer lands in)")
@@ -442,6 +445,51 @@ def bench_input_path(H, W, dev, distinct=8, block=64, reps=2):
                 "gpu_equals_host": same}
     finally:
         shutil.rmtree(d, ignore_errors=True)
+
+
+def sysfs_clocks(torch, dev):
+    """The GPU's current sclk / mclk DPM levels from sysfs (best effort: the
+    levels the driver selected, '*' in pp_dpm_*), or the reason they are not
+    readable."""
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        path = "/sys/bus/pci/devices/%04x:%02x:%02x.0" % (
+            getattr(pr, "pci_domain_id", 0), pr.pci_bus_id, pr.pci_device_id)
+    except Exception as e:  # noqa: BLE001 -- report, never fail the line
+        return {"error": "%s: %s" % (type(e).__name__, e)}
+    out = {"device": path}
+    for k in ("sclk", "mclk", "fclk"):
+        try:
+            with open(os.path.join(path, "pp_dpm_%s" % k)) as f:
+                lines = [ln.strip() for ln in f if ln.strip()]
+            cur = [ln for ln in lines if ln.endswith("*")]
+            out[k] = cur[0].split(":", 1)[1].rstrip("*").strip() if cur else lines
+        except OSError as e:
+            out[k] = "unreadable (%s)" % e.strerror
+    return out
+
+
+def box_probe(L, hip, ch, S, H, W, sp, reps=3):
+    """The box's own copy and read rates over the job's buffers (the fused
+    pass's 2 + 2 B/px and the Welford pass's 2 B/px; tmh_box_probe_device) in
+    two shapes (persistent grid-strided, one thread per 16 B), the shader
+    clock measured inside the persistent probe kernel.  The box's rate for a
+    pass's bytes is the faster shape's."""
+    res = {}
+    npx = H * W
+    for kind, nbytes, modes in (("copy", 4 * S * npx, (0, 2)), ("read", 2 * S * npx, (1, 3))):
+        shapes = {}
+        for mode in modes:
+            ms, mhz = C.c_double(), C.c_double()
+            hip.check(L.tmh_box_probe_device(ch["t_in"], ch["t_out"], ch["shift"], S, H, W, mode,
+                                             reps, sp, C.byref(ms), C.byref(mhz)))
+            d = {"ms": round(ms.value, 4), "GBs": round(nbytes / (ms.value * 1e-3) / 1e9, 1)}
+            if mhz.value > 0:
+                d["sclk_mhz_measured"] = round(mhz.value, 1)
+            shapes["persistent" if mode < 2 else "flat"] = d
+        best = max(shapes.values(), key=lambda d: d["GBs"])
+        res[kind] = {"ms": best["ms"], "GBs": best["GBs"], "bytes": nbytes, "shapes": shapes}
+    return res
 
 
 def link_rates(dev, nbytes=2 << 30):
@@ -1176,11 +1224,135 @@ def dry_run(world, rank, a):
     envs = [None] * world
     D.all_gather_object(envs, {k: os.environ.get(k) for k in keys})
     ws = dist.get_world_size()
+    merges = rehearse_merges(a, world, rank, D, torch) if world > 1 else None
     beat("done")
     dist.destroy_process_group()
     if rank == 0:
-        return {"dry_run": True, "n_gpus": world, "world_size": ws, "ranks": envs}
+        r = {"dry_run": True, "n_gpus": world, "world_size": ws, "ranks": envs}
+        if merges is not None:
+            r["merges"] = merges
+        return r
     return None
+
+
+class DryOps(object):
+    """Synthetic per-rank state for the dry run's merge rehearsal (no
+    statistics are computed): channel c's local site i contributes the
+    percentile vector p(c, i) below, its Welford state and histogram are
+    seeded by (c, rank).  Same interface as sharded.StatsOps, on CPU tensors,
+    so the dry run moves the real collectives' shapes through the real
+    sequencing code (sharded.merge_*)."""
+
+    def __init__(self, torch, c, rank, world, S_total, npx, Q):
+        from tmlibrary_amd.workflow.corilla.sharded import shard_bounds
+        self.torch, self.c, self.Q = torch, c, Q
+        self.a, self.b = shard_bounds(S_total, world, rank)
+        rng = np.random.default_rng([c, rank])
+        self.n = self.b - self.a
+        self.mean = torch.from_numpy(rng.random(npx) * 4.0)
+        self.m2 = torch.from_numpy(rng.random(npx) * self.n)
+        self.hist = torch.from_numpy(rng.integers(0, 1000, 65536).astype(np.int64))
+        self.acc = None
+        self.device = "cpu"
+
+    @staticmethod
+    def pcts(c, i, q0, qn):
+        """site i's synthetic percentiles [q0, q0 + qn): inexact products, so a
+        reassociated sum differs in its last bits"""
+        q = np.arange(q0, q0 + qn, dtype=np.int64)
+        return ((q * 40503 + i * 2654435761 + c * 97) % 65536).astype(np.float64) * 1.0000001
+
+    def n_local(self):
+        return self.n
+
+    def empty_plane(self):
+        return self.torch.empty(self.mean.numel(), dtype=self.torch.float64)
+
+    def empty_acc(self):
+        return self.torch.zeros(self.Q, dtype=self.torch.float64)
+
+    def stage1(self, buf):
+        buf.copy_(self.n * self.mean)
+
+    def stage2(self, sum_nmean, n_total, m2c):
+        mu = sum_nmean / n_total
+        d = self.mean - mu
+        m2c.copy_(self.m2 + self.n * d * d)
+        self.mean = mu.clone()
+
+    def stage3(self, n_total, sum_m2c):
+        self.m2, self.n = sum_m2c.clone(), n_total
+
+    def pct_accumulate_range(self, part, q0, qn):
+        acc = part.numpy().copy()
+        for i in range(self.a, self.b):  # the rank's sites in order
+            acc += self.pcts(self.c, i, q0, qn)
+        part.copy_(self.torch.from_numpy(acc))
+
+    def pct_accumulate(self, acc):
+        self.pct_accumulate_range(acc, 0, self.Q)
+
+    def set_pct_sum(self, acc):
+        self.acc = acc.clone()
+
+    def empty_hist(self):
+        return self.torch.empty(65536, dtype=self.torch.int64)
+
+    def get_hist(self, buf):
+        buf.copy_(self.hist)
+
+    def set_hist(self, buf):
+        self.hist = buf.clone()
+
+
+def rehearse_merges(a, world, rank, D, torch):
+    """The N > 1 bench's exchange at its own geometry, on CPU (gloo): every
+    channel's sites sharded over the ranks, the Welford all-reduce merges, the
+    pipelined ordered percentile chain (chain_chunks(Q, N) chunks, N hops) and
+    the histogram all-reduce, in the order --channel-order / --merge give the
+    GPU run (per-channel merges for the default pipelined order, one batched
+    collective per quantity for 'deep' / --merge batched); rank 0 then checks
+    every channel against the sequential result (site-order sum bit for bit,
+    pooled Welford and histogram)."""
+    from tmlibrary_amd.workflow.corilla.sharded import (chain_chunks, merge_counts,
+                                                         merge_counts_multi, merge_welford,
+                                                         merge_welford_multi, shard_bounds)
+    CH = a.channels if a.channels else 4
+    S_total, Q, npx = a.sites, 100000, a.height * a.width
+    batched = a.channel_order == "deep" or (a.channel_order != "pipelined" and a.merge == "batched")
+    ops = [DryOps(torch, c, rank, world, S_total, npx, Q) for c in range(CH)]
+    if batched:
+        merge_welford_multi(ops, D, n_totals=[S_total] * CH)
+        merge_counts_multi(ops, D)
+    else:
+        for o in ops:
+            merge_welford(o, D, n_total=S_total)
+        for o in ops:
+            merge_counts(o, D)
+    if rank != 0:
+        return None
+    out = {"channels": CH, "sites_per_channel": S_total, "height": a.height, "width": a.width,
+           "n_quantiles": Q, "chain_chunks": len(chain_chunks(Q, world)),
+           "merge": "batched" if batched else "per-channel", "check": {}}
+    for c, o in enumerate(ops):
+        want_acc = np.zeros(Q)
+        for i in range(S_total):  # the reference's sequential += in site order
+            want_acc += DryOps.pcts(c, i, 0, Q)
+        parts = [DryOps(torch, c, r, world, S_total, npx, Q) for r in range(world)]
+        n = sum(p.n for p in parts)
+        mean = sum(p.n * p.mean for p in parts) / n
+        m2 = sum(p.m2 + p.n * (p.mean - mean) ** 2 for p in parts)
+        hist = sum(p.hist for p in parts)
+        out["check"]["c%d" % c] = {
+            "sites_per_rank": [shard_bounds(S_total, world, r)[1] - shard_bounds(S_total, world, r)[0]
+                               for r in range(world)],
+            "pct_sum_bit_exact": bool(np.array_equal(o.acc.numpy(), want_acc)),
+            "welford_close": bool(torch.allclose(o.mean, mean, rtol=1e-12, atol=0) and
+                                  torch.allclose(o.m2, m2, rtol=1e-12, atol=0) and o.n == n),
+            "hist_equal": bool(torch.equal(o.hist, hist))}
+    out["ok"] = all(all(v for k, v in d.items() if k != "sites_per_rank")
+                    for d in out["check"].values())
+    return out
 
 
 def main():
@@ -1237,6 +1409,7 @@ def main():
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    clocks_start = sysfs_clocks(torch, dev)
     # TMH_BENCH_FORCE_DIST=1 runs the multi-GPU code path (RCCL merges,
     # deferred percentiles, pipelined chain) even with one rank
     dist_on = world > 1 or os.environ.get("TMH_BENCH_FORCE_DIST") == "1"
@@ -1918,6 +2091,22 @@ def main():
             extras["input_path"] = bench_input_path(H, W, dev)
         except Exception as e:  # libhdf5 missing on the box: report, never fail the headline
             extras["input_path"] = {"error": "%s: %s" % (type(e).__name__, e)}
+    box = None
+    if not a.no_box and not staged and hasattr(L, "tmh_box_probe_device"):
+        # (absent from A/B builds of earlier trees) the box's own copy / read rates over channel 0's buffers (after the
+        # checks: the copy overwrites the corrected outputs), so the passes'
+        # rates can be read against this box rather than the 8 TB/s spec
+        torch.cuda.synchronize(dev)
+        if B:
+            tab = {"t_in": ch0.T_in, "t_out": ch0.T_out, "shift": shift}
+        else:
+            t_one = torch.tensor([ch0.S_ptr.value], dtype=torch.int64, device=dev)
+            o_one = torch.tensor([ch0.O_ptr.value], dtype=torch.int64, device=dev)
+            tab = {"t_in": C.c_void_p(t_one.data_ptr()), "t_out": C.c_void_p(o_one.data_ptr()),
+                   "shift": 24}
+        log("box probe: copy and read over the job's buffers")
+        box = box_probe(L, hip, tab, S, H, W, sp)
+        box["sysfs_clocks"] = {"start": clocks_start, "end": sysfs_clocks(torch, dev)}
 
     if rank == 0:
         site_bytes = npx * 2
@@ -2051,6 +2240,23 @@ def main():
             "roofline": roofline,
             "kernels": kdetail,
         }
+        if box is not None:
+            # each pass's algorithmic rate over the box's own rate for its bytes
+            # (copy: 2 + 2 B/px like the fused pass, read: 2 B/px like Welford)
+            fr = {}
+            for name, probe, alg_name in (("correct_hist", "copy", "correct_hist"),
+                                          ("welford", "read", "welford")):
+                if name in kdetail and kdetail[name].get("alg_GBs"):
+                    fr[name] = round(kdetail[name]["alg_GBs"] / box[probe]["GBs"], 4)
+                if name in solo_kern:
+                    solo = alg[alg_name] / (solo_kern[name] * 1e-3) / 1e9
+                    fr[name + "_one_job_at_a_time"] = round(solo / box[probe]["GBs"], 4)
+            box["frac_of_box_copy"] = fr
+            box["note"] = ("tmh_box_probe_device: 16-B non-temporal loads (+ stores) over the "
+                           "job's own input and output blocks, %d sites, the faster of two "
+                           "shapes; sclk_mhz_measured = clock64 / wall_clock64 ticks in the "
+                           "persistent probe kernel" % S)
+            resd["box"] = box
         if merge_ms:
             if merge_mode == "batched":
                 resd["merge_all_channels"] = dict(merge_ms[0], note=(

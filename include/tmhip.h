@@ -441,6 +441,24 @@ int tmh_synth_sites_device(uint16_t* dev_out, int64_t n_sites, int height, int w
 int tmh_synth_tables(int distribution, int height, int width, int32_t* ln16, int32_t* nz16,
                      int32_t* ey, int32_t* ex);
 
+/* ---- box probe (bench support; no reference counterpart) ------------------
+ * The box's own stream rates for the two passes' bytes, so a bench line can
+ * tell a slow box from a slow kernel: even modes copy -- read every site's 2
+ * B/px and write them to its output block (the fused correct+histogram pass's
+ * bytes) --, odd modes read every site once (the Welford pass's); 16-byte
+ * non-temporal loads and stores as the passes move them, over the caller's
+ * blocked layout (device block tables as in
+ * tmh_stats_update_welford_blocks_device; shift 24 with one entry: one
+ * contiguous run; dev_out_blocks unused when reading).  Modes 0 / 1: one
+ * persistent grid-strided launch; 2 / 3: one thread per 16 bytes, one launch
+ * per block.  reps repetitions on `stream`; ms_out = their average (HIP
+ * events), sclk_mhz_out (may be NULL) = the shader clock during the last
+ * persistent launch (clock64 ticks per 100 MHz wall_clock64 tick in
+ * workgroup 0; 0 for modes 2 / 3).  Synchronous. */
+int tmh_box_probe_device(const uint16_t* const* dev_in_blocks, uint16_t* const* dev_out_blocks,
+                         int block_shift, int64_t n_sites, int height, int width, int mode,
+                         int reps, void* stream, double* ms_out, double* sclk_mhz_out);
+
 /* ---- site-image input: GPU inflate of HDF5 gzip chunks ------------------
  * Replaces the deflate filter libhdf5 runs under h5py for every chunk of a
  * ChannelImageFile's /array (tmlib/models/file.py:322-351,

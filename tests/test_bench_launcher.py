@@ -102,3 +102,50 @@ def test_one_rank_output_unchanged():
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
     assert d["world_size"] == 1
     assert "[rank" not in r.stderr
+
+
+def test_launcher_dry_run_eight_ranks_rehearses_the_merges():
+    """the N = 8 launch and its exchange before any 8-GPU
+    run.  Eight ranks each take their contiguous 432-site share of four
+    3,456-site channels (configs[2]) and run the bench's merges at that
+    geometry -- per-channel Welford all-reduces, the 8-hop ordered chain in
+    chain_chunks(100,000, 8) pieces, the histogram all-reduce (the default
+    pipelined order), through the heartbeat-wrapped collectives -- on
+    synthetic per-rank state; rank 0 checks every channel: the chained sums
+    bit-equal to the site-order sum, the pooled Welford state and histograms
+    (reference: corilla/api.py:64-105, stats.py:75-76).  Plane size reduced
+    (216 x 256) to keep eight CPU ranks light; the chain carries the full Q."""
+    r = _run(["--gpus", "8", "--dry-run", "--sites", "3456", "--height", "216", "--width", "256",
+              "--deadline", "400", "--stall-timeout", "120"], timeout=420)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    assert d["world_size"] == 8 and [e["RANK"] for e in d["ranks"]] == [str(i) for i in range(8)]
+    m = d["merges"]
+    assert m["ok"], m
+    assert m["channels"] == 4 and m["chain_chunks"] == 8 and m["merge"] == "per-channel"
+    for c in range(4):
+        chk = m["check"]["c%d" % c]
+        assert chk["sites_per_rank"] == [432] * 8
+        assert chk["pct_sum_bit_exact"] and chk["welford_close"] and chk["hist_equal"]
+    # every rank's heartbeat went through the collectives (the launcher's
+    # watchdog read them against --deadline / --stall-timeout and let them run)
+    for i in range(8):
+        assert "[rank %d]" % i in r.stderr, r.stderr[-2000:]
+
+
+def test_launcher_dry_run_eight_ranks_batched_merges():
+    r = _run(["--gpus", "8", "--dry-run", "--sites", "100", "--height", "24", "--width", "32",
+              "--merge", "batched", "--channel-order", "concurrent", "--deadline", "300"],
+             timeout=320)
+    assert r.returncode == 0, r.stderr[-3000:]
+    m = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])["merges"]
+    assert m["ok"] and m["merge"] == "batched", m
+    assert m["check"]["c0"]["sites_per_rank"] == [13] * 4 + [12] * 4
+
+
+def test_launcher_eight_ranks_one_stalled():
+    r = _run(["--gpus", "8", "--dry-run", "--stall-timeout", "10", "--deadline", "200"],
+             {"TMH_BENCH_DRY_STALL_RANK": "7"}, timeout=230)
+    assert r.returncode == 3, (r.returncode, r.stderr[-3000:])
+    assert r.stdout.strip() == ""
+    assert "rank 7 (running): stalled on purpose" in r.stderr, r.stderr[-3000:]

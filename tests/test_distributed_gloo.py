@@ -21,13 +21,13 @@ from oracle import corilla_oracle as orc
 class HostOps(object):
     """Test double of sharded.StatsOps on numpy/torch CPU state."""
 
-    def __init__(self, n, mean, m2, site_pcts, hist):
+    def __init__(self, n, mean, m2, site_pcts, hist, Q=None):
         self.n = int(n)
         self.hist = torch.tensor(np.asarray(hist, dtype=np.uint64).astype(np.int64))
         self.mean = torch.tensor(np.asarray(mean, dtype=np.float64).ravel())
         self.m2 = torch.tensor(np.asarray(m2, dtype=np.float64).ravel())
         self.site_pcts = [np.asarray(p, dtype=np.float64) for p in site_pcts]
-        self.Q = self.site_pcts[0].size
+        self.Q = self.site_pcts[0].size if Q is None else int(Q)  # Q: an empty shard's
         self.acc = None
         self.device = "cpu"
 
@@ -216,3 +216,71 @@ def test_merge_multi_jobs_gloo(tmp_path, world, whole):
             assert np.allclose(var, ref.std ** 2, rtol=1e-6, atol=1e-12)
             assert np.array_equal(z["acc%d" % j], ref.percentile_sums), (r, j)
             assert np.array_equal(z["hist%d" % j], want_hist)
+
+
+# The N = 8 geometry of configs[2] (VERDICT r5 "next round" item 3): four
+# channels, each channel's sites in 8 contiguous shards of the recorded site
+# order (uneven, and one channel with fewer sites than ranks: empty shards),
+# decimals 3 (Q = 100,000), merged with the batched collectives and the
+# default chain (chain_chunks(Q, 8): 8 quantile chunks flowing down an 8-hop
+# chain, [C, chunk] messages) -- the transport the first 8-GPU run uses,
+# rehearsed on CPU (reference: corilla/api.py:64-105, one job per channel;
+# stats.py:75-76, the sequential percentile sum the chain must keep).
+W8_SITES = (19, 8, 5, 11)  # per channel
+W8_SHAPE = (24, 40)
+
+
+def _w8_sites(c):
+    from tmlibrary_amd.synth import synth_sites_host
+    return synth_sites_host(W8_SITES[c], *W8_SHAPE, seed=900 + c, channel=c)
+
+
+def _w8_worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, REPO)
+    from oracle import corilla_oracle as orc
+    from tmlibrary_amd.workflow.corilla.sharded import (chain_chunks, merge_counts_multi,
+                                                         merge_welford_multi, shard_bounds)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    q = np.linspace(0, 100, 100000)
+    ops_list = []
+    for c in range(len(W8_SITES)):
+        sites = _w8_sites(c)
+        a, b = shard_bounds(len(sites), world, rank)
+        mine = sites[a:b]
+        st = orc.OracleOnlineStatistics(W8_SHAPE, 3)
+        for s in mine:
+            st.update(s)
+        local_hist = sum((orc.histogram_u16(s) for s in mine), np.zeros(65536, np.uint64))
+        ops_list.append(HostOps(st.n, st.mean, st._M2, [orc.percentile_linear(s, q) for s in mine],
+                                local_hist, Q=q.size))
+    n_totals = merge_welford_multi(ops_list, dist)
+    merge_counts_multi(ops_list, dist)
+    np.savez(os.path.join(out_dir, "w8_%d.npz" % rank), n=np.array(n_totals),
+             chunks=np.array(len(chain_chunks(q.size, world))),
+             **{"mean%d" % j: o.mean.numpy() for j, o in enumerate(ops_list)},
+             **{"m2%d" % j: o.m2.numpy() for j, o in enumerate(ops_list)},
+             **{"acc%d" % j: o.acc.numpy() for j, o in enumerate(ops_list)},
+             **{"hist%d" % j: o.hist.numpy().astype(np.uint64) for j, o in enumerate(ops_list)})
+    dist.destroy_process_group()
+
+
+def test_merge_multi_world8_geometry(tmp_path):
+    world = 8
+    mp.start_processes(_w8_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    refs = [orc.run_illumstats(_w8_sites(c)) for c in range(len(W8_SITES))]
+    hists = [sum((orc.histogram_u16(s) for s in _w8_sites(c)), np.zeros(65536, np.uint64))
+             for c in range(len(W8_SITES))]
+    for r in range(world):
+        z = np.load(tmp_path / ("w8_%d.npz" % r))
+        assert int(z["chunks"]) == 8
+        assert z["n"].tolist() == list(W8_SITES)
+        for c, ref in enumerate(refs):
+            assert np.allclose(z["mean%d" % c].reshape(W8_SHAPE), ref.mean, rtol=1e-6, atol=1e-12)
+            std = np.sqrt(z["m2%d" % c].reshape(W8_SHAPE) / (W8_SITES[c] - 1))
+            assert np.allclose(std, ref.std, rtol=1e-6, atol=1e-12)
+            assert np.array_equal(z["acc%d" % c], ref.percentile_sums), (r, c)
+            assert np.array_equal(z["hist%d" % c], hists[c]), (r, c)

@@ -2115,6 +2115,72 @@ int tmh_synth_sites_device(uint16_t* dev_out, int64_t n_sites, int height, int w
   });
 }
 
+int tmh_box_probe_device(const uint16_t* const* dev_in_blocks, uint16_t* const* dev_out_blocks,
+                         int block_shift, int64_t n_sites, int height, int width, int mode,
+                         int reps, void* stream, double* ms_out, double* sclk_mhz_out) {
+  return guard([&] {
+    TMH_CHECK(dev_in_blocks && n_sites > 0 && n_sites < (int64_t(1) << 24) && height > 0 &&
+                  width > 0 && ((int64_t)height * width) % 8 == 0 && block_shift >= 0 &&
+                  block_shift <= 24 && mode >= 0 && mode <= 3 && reps > 0 && ms_out,
+              TMH_EINVAL, "bad arguments");
+    const bool write = (mode & 1) == 0, flat = mode >= 2;
+    TMH_CHECK(!write || dev_out_blocks, TMH_EINVAL, "the copy probe needs output blocks");
+    const hipStream_t s = (hipStream_t)stream;
+    int dev = 0, cus = 0;
+    TMH_HIP(hipGetDevice(&dev));
+    TMH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    DBuf<unsigned long long> clk;
+    DBuf<unsigned int> sink;
+    clk.alloc(4);
+    sink.alloc(1);
+    hipEvent_t e0, e1;
+    TMH_HIP(hipEventCreate(&e0));
+    TMH_HIP(hipEventCreate(&e1));
+    const int64_t npx = (int64_t)height * width;
+    const int64_t per = (int64_t)1 << block_shift, nb = (n_sites + per - 1) / per;
+    std::vector<const uint16_t*> hin;
+    std::vector<uint16_t*> hout;
+    if (flat) {  // the flat shape launches per block: the block pointers on the host
+      hin.resize(nb);
+      TMH_HIP(hipMemcpy(hin.data(), dev_in_blocks, nb * sizeof(void*), hipMemcpyDeviceToHost));
+      if (write) {
+        hout.resize(nb);
+        TMH_HIP(hipMemcpy(hout.data(), dev_out_blocks, nb * sizeof(void*), hipMemcpyDeviceToHost));
+      }
+    }
+    TMH_HIP(hipMemsetAsync(clk.p, 0, 4 * sizeof(unsigned long long), s));
+    float ms = 0.0f;
+    try {
+      TMH_HIP(hipEventRecord(e0, s));
+      for (int r = 0; r < reps; ++r) {
+        if (!flat) {
+          launch_box_probe(dev_in_blocks, const_cast<uint16_t* const*>(dev_out_blocks),
+                           block_shift, n_sites, npx, write, clk.p, sink.p, cus, s);
+          continue;
+        }
+        for (int64_t b = 0; b < nb; ++b)
+          launch_box_probe_flat(hin[b], write ? hout[b] : nullptr,
+                                std::min<int64_t>(per, n_sites - b * per), npx, write, sink.p, s);
+      }
+      TMH_HIP(hipEventRecord(e1, s));
+      TMH_HIP(hipEventSynchronize(e1));
+      TMH_HIP(hipEventElapsedTime(&ms, e0, e1));
+    } catch (...) {
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      throw;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *ms_out = (double)ms / reps;
+    if (sclk_mhz_out) {
+      unsigned long long t[4];
+      TMH_HIP(hipMemcpy(t, clk.p, sizeof(t), hipMemcpyDeviceToHost));
+      *sclk_mhz_out = t[3] > t[1] ? 100.0 * (double)(t[2] - t[0]) / (double)(t[3] - t[1]) : 0.0;
+    }
+  });
+}
+
 int tmh_synth_tables(int distribution, int height, int width, int32_t* ln16, int32_t* nz16,
                      int32_t* ey, int32_t* ex) {
   return guard([&] {

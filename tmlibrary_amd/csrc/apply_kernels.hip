@@ -349,10 +349,13 @@ constexpr double kLog2_10d = 3.32192809488736234787;
 // Every coefficient form of one (mean, std) pair, one thread per pixel i
 // (blockIdx.y = job, CoefJobs):
 //   coef[i]    = (mean hi, mean lo, a = mean(std)/std, 0)      LUT path
-//   coef2      = (mean [* log2 10], a) as f32, for npx % 8 == 0 pixel 8g+j in
-//                plane j/2 as float4 (mu_2p, mu_2p+1, a_2p, a_2p+1) at g: one
-//                16-B load gives a pixel pair its packed-f32 operands (fused pass)
-//   coef_lin[i] = the same pair in pixel order (the chain's shifted gathers)
+//   coef2      = (c, a) as f32, a rounded first and c = (M - mean * a) [* log2
+//                10] from it in f64 (M = np.mean(mean)), so the fused pass's
+//                t2 = log2(x) * a + c is one fma; for npx % 8 == 0 pixel 8g+j
+//                in plane j/2 as float4 (c_2p, c_2p+1, a_2p, a_2p+1) at g: one
+//                16-B load gives a pixel pair its packed-f32 operands
+//   coef_lin[i] = (mean [* log2 10], a) in pixel order (the chain's shifted
+//                gathers)
 //   coef64[i]  = (mean, std) in f64 (the refinement, common.h)
 __global__ void k_coeffs_all(const CoefJobs J, int64_t npx) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -372,8 +375,9 @@ __global__ void k_coeffs_all(const CoefJobs J, int64_t npx) {
     oa = base + 2;
   }
   const float mu2 = (float)(mu * K), af = (float)a;
+  const double M = J.sums[j][1] / (double)npx;  // np.mean(mean)
   float* coef2 = reinterpret_cast<float*>(J.coef2[j]);
-  coef2[om] = mu2;
+  coef2[om] = (float)((M - mu * (double)af) * K);
   coef2[oa] = af;
   if (J.coef_lin[j]) J.coef_lin[j][i] = make_float2(mu2, af);
   J.coef64[j][i] = make_double2(mu, sd);

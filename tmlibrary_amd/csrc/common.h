@@ -433,6 +433,15 @@ void launch_clip_u16(const uint16_t* in, uint16_t* out, int64_t n, int lo, int h
 void launch_synth(uint16_t* out, int64_t n_sites, int H, int W, uint64_t seed, int channel,
                   int64_t first_site, int dist, hipStream_t s);
 void synth_tables_host(int dist, int H, int W, int32_t* ln, int32_t* nz, int32_t* ey, int32_t* ex);
+// box probe (bench support, synth_kernels.hip): write = copy the sites to the
+// output blocks, else read them; clk[4] = (clock64, wall_clock64) at workgroup
+// 0's start and end
+void launch_box_probe(const uint16_t* const* in_blocks, uint16_t* const* out_blocks, int shift,
+                      int64_t n_sites, int64_t npx, int write, unsigned long long* clk,
+                      unsigned int* sink, int n_cus, hipStream_t s);
+// the flat shape: one 16-byte group per thread over one contiguous run of sites
+void launch_box_probe_flat(const uint16_t* in, uint16_t* out, int64_t n_sites, int64_t npx,
+                           int write, unsigned int* sink, hipStream_t s);
 
 __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

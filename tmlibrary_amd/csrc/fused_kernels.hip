@@ -26,11 +26,12 @@
 //
 // Arithmetic (ChannelImage._correct_illumination, tmlib/image.py:599-631), in
 // the log2 domain so 10**t is one v_exp_f32:
-//   t2 = (log2(img) - mean*log2(10)) * mean(std)/std + mean(mean)*log2(10)
+//   t2 = (log2(img) - mean*log2(10)) * a + mean(mean)*log2(10),  a = mean(std)/std
+//      = log2(img) * a + c,  c = (mean(mean) - mean*a)*log2(10)  (per pixel, f32)
 //   out = astype_uint16_x86(2**t2)
-// log2 is v_log_f32 (<= 1 ulp: <= 0.1 DN at 65535); mean*log2(10) and
-// mean(std)/std are f32 (mean's rounding adds <= 0.05*a DN at 65535); zero
-// pixels take the reference's log10(1e-10) = -10.  Parity bar: +-1 DN.
+// log2 is v_log_f32 (<= 1 ulp: <= 0.1 DN at 65535); a and c are f32 (c's
+// rounding adds <= 0.05*a DN at 65535); zero pixels take the reference's
+// log10(1e-10) = -10.  Parity bar: +-1 DN.
 #include "common.h"
 
 namespace tmh {
@@ -66,27 +67,45 @@ __device__ __forceinline__ int xcc_id() {
 
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
-// Largest f32 below 2^31 whose low 16 bits are 0: min(o, kCastTop) then
-// v_cvt_i32_f32 reproduces the x86 astype(uint16) rule for every o the f32
-// path can resolve -- o >= 2^31, +inf and NaN (minNum drops it) give 0,
-// o < -2^31 saturates to INT32_MIN whose low half is 0.  Only the f32 values in
-// [2^31 - 2^16, 2^31), where f32 already carries 128-DN steps, differ.
-constexpr float kCastTop = 2147418112.0f;
+// The f32 error bound (common.h): |o| (K1 a + K2) < 1 keeps the truncated
+// value within 1 DN of the f64 one; K1, K2 carry a 0.2% margin for the f32
+// evaluation of the bound itself.
+constexpr float kBoundK1 = (float)(kRefineK1 * 1.002), kBoundK2 = (float)(kRefineK2 * 1.002);
+
+// The bound factor K1 a + K2 of a pixel group's largest a (monotone in a, so
+// no pixel of the group has a larger one): computed once per group for all
+// the unit's sites.  NaN a's drop out of the max (their pixels are not
+// flagged, as before).
+__device__ __forceinline__ float group_bound(const float4 (&k)[4]) {
+  float am = __builtin_fmaxf(__builtin_fmaxf(k[0].z, k[0].w), __builtin_fmaxf(k[1].z, k[1].w));
+  am = __builtin_fmaxf(am, __builtin_fmaxf(__builtin_fmaxf(k[2].z, k[2].w),
+                                           __builtin_fmaxf(k[3].z, k[3].w)));
+  return __builtin_fmaf(am, kBoundK1, kBoundK2);
+}
 
 // Eight pixels (four packed u16 words) -> their corrected u16 values packed
-// the same way.  k[p] = (mu_lo, mu_hi, a_lo, a_hi) of word p's two pixels: the
-// subtract / fma / add run as v_pk_*_f32 on the pair, and each stage is issued
+// the same way.  k[p] = (c_lo, c_hi, a_lo, a_hi) of word p's two pixels, c =
+// (M - mean * a) [* log2 10] with a already rounded to f32 (k_coeffs_all), so
+//   t2 = log2(x) * a + c
+// is one v_pk_fma_f32 per pair (the reference's (log x - mean) * a + M with
+// one rounding of c instead of the rounded mean, the subtraction and the
+// rounded M: the error stays within the bound below).  Each stage is issued
 // for all four pairs before the next so dependent packed ops do not stall on
 // their one-pass hazard.  A zero pixel takes log2(zf), zf = 10**zero_log10 as
 // f32 (1e-10f: v_log_f32 is within 1 ulp of the reference's log10(1e-10) =
 // -10, scaled): one v_max instead of a compare + select.  The caller keeps zf
 // in [FLT_MIN, 1].  Returns the mask of the pixels whose f32 result may be
-// more than 1 DN off (their own error bound, below): the caller flags them for
-// the f64 refinement (common.h) -- rare, saturated pixels in dim corners.
+// more than 1 DN off (their own error bound): the caller flags them for the
+// f64 refinement (common.h) -- rare, saturated pixels in dim corners.  The
+// common path tests the group once: its largest |o| against bmax (the group's
+// largest bound factor, group_bound); only a group that passes that test
+// (the return value) has its pixels' own bounds evaluated, by the caller
+// (far_mask, inside a branch that also stages the fixups, so the compiler
+// cannot if-convert the per-pixel work into the common path).
 template <bool LOG, bool CLIP>
-__device__ __forceinline__ uint32_t fcorrect8(const uint32_t (&w)[4], const float4 (&k)[4],
-                                              float mh, float zf, float T, uint32_t clip_lo2,
-                                              uint32_t clip_hi2, uint32_t (&r)[4]) {
+__device__ __forceinline__ bool fcorrect8(const uint32_t (&w)[4], const float4 (&k)[4], float zf,
+                                          float bmax, uint32_t clip_lo2, uint32_t clip_hi2,
+                                          uint32_t (&r)[4], float (&o)[8]) {
   f32x2_t t[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -100,48 +119,26 @@ __device__ __forceinline__ uint32_t fcorrect8(const uint32_t (&w)[4], const floa
       t[p].y = __builtin_amdgcn_logf(__builtin_fmaxf(t[p].y, zf));
     }
   }
-  const f32x2_t M = {mh, mh};
 #pragma unroll
-  for (int p = 0; p < 4; ++p) t[p] -= (f32x2_t){k[p].x, k[p].y};
-#pragma unroll
-  for (int p = 0; p < 4; ++p) t[p] = __builtin_elementwise_fma(t[p], (f32x2_t){k[p].z, k[p].w}, M);
-  float o[8];
+  for (int p = 0; p < 4; ++p)
+    t[p] = __builtin_elementwise_fma(t[p], (f32x2_t){k[p].z, k[p].w}, (f32x2_t){k[p].x, k[p].y});
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     o[2 * p] = LOG ? __builtin_amdgcn_exp2f(t[p].x) : t[p].x;  // v_exp_f32
     o[2 * p + 1] = LOG ? __builtin_amdgcn_exp2f(t[p].y) : t[p].y;
   }
-  // the pixel's own f32 error bound (common.h): |o| (K1 a + K2) < 1 keeps the
-  // truncated value within 1 DN of the f64 one; K1, K2 carry a 0.2% margin
-  // for the f32 evaluation of the bound itself.  (The launch-wide threshold T
-  // = 1 / (K1 a_max + K2) flagged every bright pixel of an image with one
-  // low-variance pixel; the per-pixel bound flags only the pixels that need
-  // it.)  One compare per 8 pixels; the mask only if needed.
-  (void)T;
-  constexpr float K1 = (float)(kRefineK1 * 1.002), K2 = (float)(kRefineK2 * 1.002);
-  float e[8];
+  auto mag = [](float v) { return LOG ? v : __builtin_fabsf(v); };  // log: o = 2**t >= 0 (or NaN)
+  float mx = __builtin_fmaxf(mag(o[0]), mag(o[1]));
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const f32x2_t b = __builtin_elementwise_fma((f32x2_t){k[p].z, k[p].w}, (f32x2_t){K1, K1},
-                                                (f32x2_t){K2, K2});
-    e[2 * p] = __builtin_fabsf(o[2 * p]) * b.x;
-    e[2 * p + 1] = __builtin_fabsf(o[2 * p + 1]) * b.y;
-  }
-  float mx = e[0];
-#pragma unroll
-  for (int j = 1; j < 8; ++j) mx = __builtin_fmaxf(mx, e[j]);
-  uint32_t far = 0;  // pixels beyond their f32 bound
-  if (mx >= 0.998f) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) far |= (e[j] >= 0.998f ? 1u : 0u) << j;
-  }
+  for (int j = 2; j < 8; ++j) mx = __builtin_fmaxf(mx, mag(o[j]));
+  // No clamp before the cast: an unflagged |o| is below 1 / K2 < 2^18, where
+  // v_cvt_i32_f32 truncates exactly as the reference's x86 cast does, and a
+  // flagged pixel's value is rewritten by the f64 refinement (every |o| >=
+  // 1 / K2, +-inf included, is flagged; NaN -- never flagged -- converts to 0,
+  // the low half of the reference's INT32_MIN).
   int32_t iv[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    o[j] = __builtin_fminf(o[j], kCastTop);
-    if (!LOG) o[j] = __builtin_fmaxf(o[j], -2147483648.0f);  // t may be negative: stay in range
-    iv[j] = (int32_t)o[j];
-  }
+  for (int j = 0; j < 8; ++j) iv[j] = (int32_t)o[j];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     r[p] = __builtin_amdgcn_perm((uint32_t)iv[2 * p + 1], (uint32_t)iv[2 * p], 0x05040100u);
@@ -152,6 +149,19 @@ __device__ __forceinline__ uint32_t fcorrect8(const uint32_t (&w)[4], const floa
                                     __builtin_bit_cast(u16x2_t, clip_hi2));
       r[p] = __builtin_bit_cast(uint32_t, v);
     }
+  }
+  return mx * bmax >= 0.998f;
+}
+
+// The pixels of a flagged group beyond their own f32 bound (bit j: pixel j)
+__device__ __forceinline__ uint32_t far_mask(const float4 (&k)[4], const float (&o)[8]) {
+  uint32_t far = 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float b0 = __builtin_fmaf(k[p].z, kBoundK1, kBoundK2);
+    const float b1 = __builtin_fmaf(k[p].w, kBoundK1, kBoundK2);
+    far |= (__builtin_fabsf(o[2 * p]) * b0 >= 0.998f ? 1u : 0u) << (2 * p);
+    far |= (__builtin_fabsf(o[2 * p + 1]) * b1 >= 0.998f ? 2u : 0u) << (2 * p);
   }
   return far;
 }
@@ -343,7 +353,8 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     const bool rlist = PK && rl.v != nullptr;
     uint32_t* hs = jb.hist + un.s0 * (int64_t)kBins;
 
-    auto process = [&](const uint4 w, const int k, const float4 (&cf)[4], const int g) -> u32x4_t {
+    auto process = [&](const uint4 w, const int k, const float4 (&cf)[4], const float bmax,
+                       const int g) -> u32x4_t {
       const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
       if (!(ABL & 1)) {
         uint32_t* sl = bins + (PK ? k >> 1 : k) * SLICE;
@@ -394,13 +405,16 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
                            w.z ^ (__float_as_uint(cf[2].z) & 1u), w.w ^ (__float_as_uint(cf[3].w) & 1u)};
         return r;
       }
-      const uint32_t far = fcorrect8<LOG, CLIP>(wd, cf, m.x, m.z, m.w, clo2, chi2, o);
-      if (far) {
-        const unsigned int i = atomicAdd(&fix_cnt[par], 1u);
-        if (i < (unsigned int)kFixSh)
-          fix_sh[par][i] = fix_code8(far, un.s0 + k, (int64_t)g * 8);
-        else
-          fix_push8(fl, far, un.s0 + k, (int64_t)g * 8);  // rare: the unit's LDS set is full
+      float of[8];
+      if (fcorrect8<LOG, CLIP>(wd, cf, m.z, bmax, clo2, chi2, o, of)) {  // rare
+        const uint32_t far = far_mask(cf, of);
+        if (far) {
+          const unsigned int i = atomicAdd(&fix_cnt[par], 1u);
+          if (i < (unsigned int)kFixSh)
+            fix_sh[par][i] = fix_code8(far, un.s0 + k, (int64_t)g * 8);
+          else
+            fix_push8(fl, far, un.s0 + k, (int64_t)g * 8);  // rare: the unit's LDS set is full
+        }
       }
       const u32x4_t r = {o[0], o[1], o[2], o[3]};
       return r;
@@ -410,10 +424,11 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
     // steps; A holds the unit's first group when the previous unit loaded it
     auto stage = [&](const uint4 (&v)[SPU], const float4 (&cf)[4], int g) {
       if (g < un.g1) {
+        const float bmax = group_bound(cf);  // once per group for the unit's sites
 #pragma unroll
         for (int k = 0; k < SPU; ++k)
           if (k < un.ns)
-            __builtin_amdgcn_raw_buffer_store_b128(process(v[k], k, cf, g), un.rout, g * 16,
+            __builtin_amdgcn_raw_buffer_store_b128(process(v[k], k, cf, bmax, g), un.rout, g * 16,
                                                    k * site_bytes, kFusedStoreAux);
       }
     };

@@ -102,6 +102,8 @@ SIGNATURES = {
     "tmh_correct_chain_u8": (_I, [_P, _P, _P, _I64, _P, _I, _I]),
     "tmh_synth_sites_device": (_I, [_P, _I64, _I, _I, C.c_uint64, _I, _I64, _I, _P]),
     "tmh_synth_tables": (_I, [_I, _I, _I, _P, _P, _P, _P]),
+    "tmh_box_probe_device": (_I, [_P, _P, _I, _I64, _I, _I, _I, _I, _P, C.POINTER(_D),
+                                  C.POINTER(_D)]),
     "tmh_inflate_scratch_bytes": (_I64, [_I64, _I64]),
     "tmh_inflate_device": (_I, [_P, _I64, _P, _I64, _I64, _P, _I64, _P, _I64, _P, _P]),
     "tmh_place_chunks_device": (_I, [_P, _P, _I64, _I, _I, _I, _I, _I, _P, _P]),

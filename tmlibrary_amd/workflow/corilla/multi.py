@@ -140,7 +140,9 @@ def run_channels_sharded(store, batches, dist=None, group=None, stats_factory=No
                 if start < b:
                     logger.info("channel %s: files from %d on decoded on the host",
                                 batch["channel_id"], start)
-            elif decode == "gpu":
+            elif decode == "gpu" and not hasattr(stats, "update_device"):
+                # (an empty shard -- more ranks than files -- has nothing to
+                # decode and goes straight to the merge its peers wait in)
                 raise RawChunksUnsupported("decode='gpu' needs statistics with update_device")
             for i in range(start, b, block):
                 sites = read_channel_images(paths[i:min(b, i + block)], decode_threads)

@@ -165,6 +165,27 @@ for step in "$@"; do
       python3 tools/pmc_traffic.py $O/pmc_FETCH_SIZE_${D}_$TAG $O/pmc_WRITE_SIZE_${D}_$TAG --sites 3456 \
         --height 2160 --width 2560 --distribution $D -o $O/pmc_traffic_${D}_$TAG.json || exit $?
       ;;
+    avail)
+      timeout -k 10 60 rocprofv3 --list-avail > $O/pmc_avail_$TAG.txt 2>&1 || exit $?
+      grep -cE "SQ_|GRBM_" $O/pmc_avail_$TAG.txt || true
+      ;;
+    pmcsq)
+      # SQ / GRBM counters of a short bench on DIST, two passes (each <= 8 SQ
+      # and <= 2 GRBM counters, its own run): pmcsq[:DIST] -> pmc_sq_DIST_TAG.json
+      D=${a1:-synthetic}
+      PA="SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE"
+      PB="SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
+      n=0
+      for P in "$PA" "$PB"; do
+        n=$((n + 1))
+        timeout -s KILL 240 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $O/pmcsq${n}_${D}_$TAG -o run \
+          -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-extras --no-profile --no-box \
+          --jobs-in-flight 1 --distribution $D > $O/pmcsq${n}_${D}_$TAG.log 2>&1 || exit $?
+      done
+      python3 tools/pmc_sq.py $O/pmcsq1_${D}_$TAG $O/pmcsq2_${D}_$TAG --pixels $((3456 * 2160 * 2560)) \
+        -o $O/pmc_sq_${D}_$TAG.json > /dev/null || exit $?
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); [print(k[:60], v['derived']) for k, v in d['kernels'].items()]" $O/pmc_sq_${D}_$TAG.json
+      ;;
     ab)
       IFS=, read -r -a LIBS <<< "$a2"
       : > $O/ab_$TAG.jsonl
