@@ -110,6 +110,10 @@ def parse():
     p.add_argument("--welford-parts", type=int, default=None,
                    help="TMH_OPT_WELFORD_PARTS (1..4 forces that split and the standard pass; "
                         "default: automatic, from the job's site probe)")
+    p.add_argument("--welford-cus", type=int, default=None,
+                   help="(experiment) run each job lane's stream -- its Welford pass and planes "
+                        "-- on a stream CU-masked to this many CUs, leaving the rest to the "
+                        "previous job's histogram tail")
     p.add_argument("--fused-config", type=int, default=None,
                    help="fused pass (sites per unit, threads, LDS bins) configuration 0..5 "
                         "(TMH_OPT_FUSED_CONFIG; default: automatic, from the job's site probe)")
@@ -467,6 +471,36 @@ def sysfs_clocks(torch, dev):
         except OSError as e:
             out[k] = "unreadable (%s)" % e.strerror
     return out
+
+
+def cu_masked_stream(torch, dev, n_cus):
+    """A HIP stream restricted to n_cus of the device's CUs
+    (hipExtStreamCreateWithCUMask; the CUs left out spread evenly over the CU
+    indices), wrapped for torch.  The mask call goes to the HIP runtime torch
+    already loaded (one runtime per process)."""
+    total = torch.cuda.get_device_properties(dev).multi_processor_count
+    n_cus = max(1, min(int(n_cus), total))
+    keep = [True] * total
+    drop = total - n_cus
+    for j in range(drop):
+        keep[(j * total) // drop] = False
+    words = [0] * ((total + 31) // 32)
+    for i, k in enumerate(keep):
+        if k:
+            words[i // 32] |= 1 << (i % 32)
+    path = None
+    with open("/proc/self/maps") as f:
+        for ln in f:
+            if "libamdhip64.so" in ln:
+                path = ln.split()[-1]
+                break
+    rt = C.CDLL(path or "libamdhip64.so")
+    h = C.c_void_p()
+    rc = rt.hipExtStreamCreateWithCUMask(C.byref(h), C.c_uint32(len(words)),
+                                         (C.c_uint32 * len(words))(*words))
+    if rc != 0:
+        raise RuntimeError("hipExtStreamCreateWithCUMask failed (%d)" % rc)
+    return torch.cuda.ExternalStream(h.value, device=dev)
 
 
 def box_probe(L, hip, ch, S, H, W, sp, reps=3):
@@ -1534,6 +1568,8 @@ def main():
             # for 4 x 432 sites, profiles/r5/dist432_stream_priority_r5y.jsonl)
             self.stream = (stream if (c == 0 and lane == 0) or a.channel_streams == "one"
                            else torch.cuda.Stream(dev))
+            if a.welford_cus:  # (experiment) this lane's Welford pass and planes on fewer CUs
+                self.stream = cu_masked_stream(torch, dev, a.welford_cus)
             self.sp = C.c_void_p(self.stream.cuda_stream)
             # jobs in flight: the corrected pass on a stream of its own, so the
             # histogram tail runs on the statistics handle's stream after it

@@ -86,7 +86,13 @@ int tmh_stats_reset(tmh_stats* h);
  * spread over the launch's first <= 64 sites, and the host waits for its
  * three counts (groups sampled, holding a value >= 4,096, >= 16,384) --
  * so that launch returns only once the probe has run on its stream.  Only
- * the chosen kernels are queued.
+ * the chosen kernels are queued.  The choice assumes the first <= 64 sites
+ * stand for the job: a job whose first sites are dark and later sites very
+ * wide runs the narrow configurations, its wide values taking their global-
+ * atomic path -- results identical, the pass slower (uniform 16-bit sites
+ * that way: ~0.5 s per 3,456 sites, against ~36 ms chosen right;
+ * test_gpu_parity.py dark_prefix_wide_tail).  Force a configuration
+ * (TMH_OPT_FUSED_CONFIG) for such jobs.
  *   TMH_OPT_FUSED_CONFIG   0..5: (sites per unit, threads, LDS bins) of the
  *                          fused correct+histogram pass = (2, 1024, 32768),
  *                          (4, 1024, 32768), (2, 512, 16384), (4, 512, 16384),

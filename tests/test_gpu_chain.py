@@ -96,6 +96,54 @@ def test_chain_fused_vs_reference(L):
     assert (d == 0).mean() > 0.99
 
 
+def _layer_percentiles(sites):
+    """the channel's percentile dict (stats.py:114-121) from the pinned oracle"""
+    st = orc.run_illumstats(sites)
+    keys, vals = orc.percentile_keys(3), orc.percentile_values(st.percentile_sums, st.n)
+    return dict(zip(keys.tolist(), vals.tolist()))
+
+
+def test_chain_with_derived_clip_bounds(L):
+    """illuminati's layer (api.py:119-164, 389-405): the clip bounds derived
+    from the channel's percentiles (workflow/illuminati.clip_bounds) fed to
+    the fused chain -- the chain fixture's layer, whose bounds the reference
+    took from the same statistics sites (make_goldens.py)."""
+    from tmlibrary_amd.image import IllumstatsContainer, IllumstatsImage
+    from tmlibrary_amd.synth import synth_sites_host
+    from tmlibrary_amd.workflow.illuminati import correct_chain_u8
+    g, wins = _chain_inputs()
+    pct = _layer_percentiles(synth_sites_host(6, 96, 128, seed=1111))
+    stats = IllumstatsContainer(IllumstatsImage(g["smooth_mean"].copy()),
+                                IllumstatsImage(g["smooth_std"].copy()), pct)
+    got, bounds = correct_chain_u8(stats, g["images"], wins)
+    stats.release()
+    assert bounds == (int(g["clip_lo"]), int(g["clip_hi"]))
+    d = np.abs(got.astype(np.int32) - g["scaled"].astype(np.int32))
+    assert d.max() <= 1 and (d == 0).mean() > 0.99
+
+
+def test_chain_dim_channel_floor(L):
+    """A dim channel's layer: clip_max raised to 700 (api.py:142-153), the
+    chain against the oracle at those bounds."""
+    from tmlibrary_amd.image import IllumstatsContainer, IllumstatsImage
+    from tmlibrary_amd.synth import synth_sites_host
+    from tmlibrary_amd.workflow.illuminati import correct_chain_u8
+    g, wins = _chain_inputs()
+    dim = [(s // 8).astype(np.uint16) for s in synth_sites_host(6, 96, 128, seed=1111)]
+    st = orc.run_illumstats(dim)
+    sm_mean, sm_std = orc.smooth_reflect(st.mean), orc.smooth_reflect(st.std)
+    pct = _layer_percentiles(dim)
+    stats = IllumstatsContainer(IllumstatsImage(sm_mean), IllumstatsImage(sm_std), pct)
+    imgs = np.stack([(s // 8).astype(np.uint16) for s in g["images"]])
+    got, (lo, hi) = correct_chain_u8(stats, imgs, wins)
+    stats.release()
+    assert hi == 700 and lo == orc.get_closest_percentile(pct, 0.001)
+    for img, (y, x), o in zip(imgs, g["shifts"], got):
+        want = orc.illuminati_chain(img, sm_mean, sm_std, (int(y), int(x)),
+                                    tuple(int(v) for v in g["residues"]), lo, hi)
+        assert np.abs(o.astype(np.int32) - want.astype(np.int32)).max() <= 1
+
+
 def test_chain_by_steps_vs_reference(L):
     """The same chain through the drop-in API, one method at a time."""
     from tmlibrary_amd.image import ChannelImage, IllumstatsContainer, IllumstatsImage

@@ -652,7 +652,10 @@ def _fused_job(L, sites, clip=(-1, -1), q=None):
         hip.check(L.tmh_stats_site_histogram(h, i, hip.ptr(sh)))
         site_h.append(sh)
     out = d_out.get(np.uint16, sites.shape)
+    pc, wb, fc = (C.c_uint32 * 3)(), C.c_int(), C.c_int()
+    hip.check(L.tmh_stats_job_choice(h, pc, C.byref(wb), C.byref(fc)))
     res = dict(n=nn.value, mean=m_h, std=s_h, acc=acc, hist=hist, site_hist=site_h, out=out,
+               fused_cfg=fc.value,
                smean=smean.get(np.float64, (H, W)), sstd=sstd.get(np.float64, (H, W)),
                order_stats=site_order_stats(L, h, range(n), Q))
     L.tmh_corrector_destroy(c)
@@ -663,11 +666,14 @@ def _fused_job(L, sites, clip=(-1, -1), q=None):
 
 
 @pytest.mark.parametrize("kind", ["synth", "extremes", "uniform", "tiny", "many", "saturated",
-                                  "constant", "two_values"])
+                                  "constant", "two_values", "dark_prefix_wide_tail"])
 def test_fused_correct_hist_pipeline(L, kind):
     """The fused pass and its percentile tail: one-bin sites, Q > pixel
     count, sparse tails, the very wide path of the uniform case, each
-    bit-exact."""
+    bit-exact.  dark_prefix_wide_tail: the job's site probe sees only the
+    first 64 sites (dark), so the narrow configuration runs and the wide
+    tail's values take its global-atomic path (tmhip.h, the probe's first-sites
+    assumption): slower, and still bit-exact."""
     from tmlibrary_amd.synth import synth_exact_sites_host, synth_sites_host
     rng = np.random.default_rng(97)
     if kind == "saturated":  # corrected values far above 2**16 (f64 refinement, common.h)
@@ -687,6 +693,11 @@ def test_fused_correct_hist_pipeline(L, kind):
         sites[::5, 3, :] = 65000
     elif kind == "constant":  # one bin per site (one compact-CDF entry)
         sites = np.stack([np.full((48, 64), v, np.uint16) for v in (0, 777, 65535, 4096)])
+    elif kind == "dark_prefix_wide_tail":
+        dark = np.stack(synth_sites_host(64, 48, 64, seed=12))
+        assert dark.max() < 4096 or (dark >= 4096).mean() < 1e-3
+        wide = rng.integers(0, 65536, size=(6, 48, 64), dtype=np.uint16)
+        sites = np.concatenate([dark, wide])
     elif kind == "two_values":  # every quantile chunk inside one of two entries
         sites = np.stack([np.where(rng.random((48, 64)) < 0.3, 3, 60000).astype(np.uint16)
                           for _ in range(5)])
@@ -695,6 +706,8 @@ def test_fused_correct_hist_pipeline(L, kind):
     r = _fused_job(L, sites)
     ref = orc.run_illumstats(list(sites))
     assert r["n"] == len(sites)
+    if kind == "dark_prefix_wide_tail":
+        assert r["fused_cfg"] == 3, "the probe saw only the dark prefix: narrow configuration"
     assert_close_rel(r["mean"], ref.mean)
     assert_close_rel(r["std"], ref.std)
     assert np.array_equal(r["acc"], ref.percentile_sums), "fused percentile sums not bit-exact"

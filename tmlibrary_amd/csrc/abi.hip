@@ -791,6 +791,7 @@ int tmh_stats_zero_counts(tmh_stats* h, int64_t* host_out, int64_t n, void* stre
     hipStream_t s = hpick(h, stream);
     cross_begin(h, s);
     TMH_HIP(hipMemcpyAsync(host_out, h->zeros.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+    cross_end(h, s);  // a later update (on any stream) writes h->zeros after this copy
   });
 }
 
@@ -1351,6 +1352,10 @@ int tmh_job_planes_multi_device(tmh_stats* const* hs, tmh_corrector* const* cs, 
       TMH_CHECK(hs[k] && cs[k] && dev_smean[k] && dev_sstd[k], TMH_EINVAL, "bad arguments");
       TMH_CHECK(hs[k]->H == hs[0]->H && hs[k]->W == hs[0]->W && cs[k]->npx == hs[0]->npx,
                 TMH_EINVAL, "jobs of different image sizes");
+      // (every check before the first cross_begin / launch: a rejected call
+      // leaves nothing queued that reads scratch freed on the way out)
+      TMH_CHECK(cs[k]->H == hs[0]->H && cs[k]->W == hs[0]->W, TMH_EINVAL,
+                "jobs of different image shapes");
       TMH_CHECK(dev_smean[k] != dev_sstd[k], TMH_EINVAL, "smoothed planes must differ");
       for (int j = 0; j < k; ++j)
         TMH_CHECK(hs[j] != hs[k] && cs[j] != cs[k], TMH_EINVAL, "a handle listed twice");
@@ -1402,7 +1407,6 @@ int tmh_job_planes_multi_device(tmh_stats* const* hs, tmh_corrector* const* cs, 
     double* psum[kMaxPlanes];
     double* pmin[kMaxPlanes];
     for (int k = 0; k < n; ++k) {
-      TMH_CHECK(cs[k]->H == H && cs[k]->W == W, TMH_EINVAL, "jobs of different image shapes");
       psum[2 * k] = cs[k]->partial.p + nt;  // mean
       pmin[2 * k] = nullptr;
       psum[2 * k + 1] = cs[k]->partial.p;  // std

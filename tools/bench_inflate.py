@@ -35,7 +35,6 @@ def main():
     ap.add_argument("--level", type=int, default=4)
     ap.add_argument("--dir", default=None)
     ap.add_argument("--lanes", default="", help="comma list of TMH_INFLATE_LANES to sweep")
-    ap.add_argument("--modes", default="", help="comma list of TMH_INFLATE_MODE (wave, lane) to sweep")
     a = ap.parse_args()
     import torch
 
@@ -133,18 +132,6 @@ def main():
             print(json.dumps({"lanes": w, **sweep[str(w)]}), file=sys.stderr, flush=True)
         res["lanes_sweep"] = sweep
         os.environ.pop("TMH_INFLATE_LANES", None)
-    if a.modes:
-        msw = {}
-        for m in a.modes.split(","):
-            os.environ["TMH_INFLATE_MODE"] = m
-            g, sps, kern = timed(0)
-            ok = ok and g
-            tot = kern.get("inflate", 0.0) + kern.get("inflate_matches", 0.0)
-            msw[m] = {"gpu_sites_per_s": sps, "kernel_ms": kern, "equal": g,
-                      "inflate_kernels_sites_per_s": round(a.block / (tot * 1e-3), 1) if tot else None}
-            print(json.dumps({"mode": m, **msw[m]}), file=sys.stderr, flush=True)
-        res["modes_sweep"] = msw
-        os.environ.pop("TMH_INFLATE_MODE", None)
     res["gpu_equals_host"] = ok
     print(json.dumps(res), flush=True)
     if a.dir is None:

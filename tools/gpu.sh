@@ -127,10 +127,10 @@ for step in "$@"; do
       tail -c 1500 $O/bench_input_$TAG.json
       ;;
     inflate)
-      # GPU inflate kernels: inflate[:MODES] (comma list of TMH_INFLATE_MODE) -> bench_inflate_TAG.json
-      timeout -k 10 600 python tools/bench_inflate.py --block 128 --modes ${a1:-wave,lane} \
+      # GPU inflate kernels -> bench_inflate_TAG.json
+      timeout -k 10 600 python tools/bench_inflate.py --block 128 \
         > $O/bench_inflate_$TAG.json 2> $O/bench_inflate_$TAG.err || exit $?
-      grep mode $O/bench_inflate_$TAG.err
+      tail -c 600 $O/bench_inflate_$TAG.json
       ;;
     pytest)
       # a subset of the GPU tests: pytest:EXPR (-k expression, '+' for spaces)
