@@ -85,6 +85,36 @@ __global__ __launch_bounds__(256) void k_flat_copy2(const u32x4* __restrict__ a,
   }
 }
 
+// flat with K consecutive 4 KB chunks per workgroup (thread t: groups t,
+// t + 256, ...; U loads in flight): how long-lived may a workgroup be?
+template <int K, int U>
+__global__ __launch_bounds__(256) void k_flatk_copy(const u32x4* __restrict__ a, u32x4* __restrict__ c,
+                                                    int64_t n) {
+  const int64_t base = (int64_t)blockIdx.x * 256 * K + threadIdx.x;
+#pragma unroll 1
+  for (int k = 0; k < K; k += U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + (int64_t)(k + u) * 256;
+      if (i < n) v[u] = __builtin_nontemporal_load(a + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + (int64_t)(k + u) * 256;
+      if (i < n) __builtin_nontemporal_store(v[u], c + i);
+    }
+  }
+}
+
+// persistent grid-stride, one group per iteration
+__global__ __launch_bounds__(256) void k_grid1_copy(const u32x4* __restrict__ a, u32x4* __restrict__ c,
+                                                    int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), c + i);
+}
+
 // persistent, chunks of K x 4 KB in address order from one counter; the
 // chunk's block: in / out tables of nb blocks of per_blk groups (16 B)
 template <int K>
@@ -233,16 +263,6 @@ int main(int argc, char** argv) {
       time("copy grid4", cbytes, [&] {
         launch_box_probe(tin, tout, shift, S, npx, 1, (unsigned long long*)fe, sink, cus, 0);
       });
-      time("copy queue1 (4 KB)", cbytes, [&] {
-        CK(hipMemsetAsync(ctr, 0, 4, 0));
-        hipLaunchKernelGGL(k_queue_copy<1>, dim3(cus * 8), dim3(256), 0, 0,
-                           (const u32x4* const*)tin, (u32x4* const*)tout, per_blk, S * ng, ctr);
-      });
-      time("copy queue4 (16 KB)", cbytes, [&] {
-        CK(hipMemsetAsync(ctr, 0, 4, 0));
-        hipLaunchKernelGGL(k_queue_copy<4>, dim3(cus * 8), dim3(256), 0, 0,
-                           (const u32x4* const*)tin, (u32x4* const*)tout, per_blk, S * ng, ctr);
-      });
       time("fused abl33 (copy)", cbytes, [&] {
         fused(k_correct_hist<true, false, 4, 33, 512, 16384, false>, 2, 16);
       });
@@ -262,27 +282,29 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(k_flat_scatter, dim3((unsigned)(S * ((ng + 255) / 256))), dim3(256), 0, 0,
                            (const u32x4*)in, (u32x4* const*)tout, shift, S, ng);
       });
-      time("copy flat 2x16B", cbytes, [&] {
+      auto flatk = [&](const char* name, auto kern, int K) {
+        time(name, cbytes, [&] {
+          for (int k = 0; k < nblk; ++k) {
+            const int64_t n = std::min<int64_t>(B, S - (int64_t)k * B) * ng;
+            hipLaunchKernelGGL(kern, dim3((unsigned)((n + 256 * K - 1) / (256 * K))), dim3(256), 0, 0,
+                               (const u32x4*)ib[k], (u32x4*)ob[k], n);
+          }
+        });
+      };
+      flatk("copy flatK4 U1", k_flatk_copy<4, 1>, 4);
+      flatk("copy flatK16 U1", k_flatk_copy<16, 1>, 16);
+      flatk("copy flatK16 U4", k_flatk_copy<16, 4>, 16);
+      flatk("copy flatK256 U1", k_flatk_copy<256, 1>, 256);
+      flatk("copy flatK256 U4", k_flatk_copy<256, 4>, 256);
+      time("copy grid1 (per block)", cbytes, [&] {
         for (int k = 0; k < nblk; ++k) {
           const int64_t n = std::min<int64_t>(B, S - (int64_t)k * B) * ng;
-          hipLaunchKernelGGL(k_flat_copy2, dim3((unsigned)((n + 511) / 512)), dim3(256), 0, 0,
-                             (const u32x4*)ib[k], (u32x4*)ob[k], n);
+          hipLaunchKernelGGL(k_grid1_copy, dim3(cus * 8), dim3(256), 0, 0, (const u32x4*)ib[k],
+                             (u32x4*)ob[k], n);
         }
-      });
-      time("fused abl33 128 bands", cbytes, [&] {
-        fused(k_correct_hist<true, false, 4, 33, 512, 16384, false>, 2, 128);
       });
       time("fused abl33 cfg1 4x1024", cbytes, [&] {
         fused(k_correct_hist<true, false, 4, 33, 1024, 32768, false>, 1, 16, 1024);
-      });
-      time("fused abl33 cfg0 2x1024", cbytes, [&] {
-        fused(k_correct_hist<true, false, 2, 33, 1024, 32768, false>, 1, 8, 1024);
-      });
-      time("fused abl33 cfg2 2x512", cbytes, [&] {
-        fused(k_correct_hist<true, false, 2, 33, 512, 16384, false>, 2, 16);
-      });
-      time("fused abl33 cfg4 1x1024", cbytes, [&] {
-        fused(k_correct_hist<true, false, 1, 33, 1024, 32768, false>, 1, 16, 1024);
       });
       time("read flat", rbytes, [&] {
         hipLaunchKernelGGL(k_flat_read, dim3((unsigned)((S * ng + 255) / 256)), dim3(256), 0, 0,
