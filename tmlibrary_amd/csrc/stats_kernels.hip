@@ -726,11 +726,15 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_scatter(
 // at or above dense_rounds that hold counts; the others are known empty and
 // are not read (a microscopy site touches a handful of the 64).  The mask is
 // zero-maintained like the counts.
-// super-round width of the finalize: 4 rounds (4,096 bins, 16 KB of ranks
-// per buffer) for the 1,024-thread form, 1 for the narrow side-stream form
+// super-round width of the finalize: 8 rounds (8,192 bins, 32 KB of ranks
+// per buffer) for the 1,024-thread form, 1 for the narrow side-stream form.
+// Round 6: 8 instead of 4 -- bright sites (45 of 64 rounds in use) scan in 6
+// super-rounds instead of 12: bright job 136.1k / 136.7k vs 135.5k / 134.5k,
+// standard 166.9k / 165.4k vs 166.5k / 166.6k, same box ABBA
+// (profiles/r6/ab_finalize_sr8_*_r6g.jsonl).
 template <int NT>
 struct FinSR {
-  static constexpr int value = NT >= 1024 ? 4 : 1;
+  static constexpr int value = NT >= 1024 ? 8 : 1;
 };
 
 template <int ABL, int NT>
