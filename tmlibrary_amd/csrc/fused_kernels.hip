@@ -8,10 +8,12 @@
 // their own: HBM traffic is then the algorithmic 2 + 4 B/px per site.
 //
 // Layout of the work: the image is cut into n_bands = 16 pixel bands, and a
-// unit is SPU sites of one band.  The units form one band-major sweep with
-// the 8 XCDs two bands apart (each XCD's L2 holds the coefficients of the
-// band it is on -- 8 B/px: 2.76 MB per band at 2160x2560 -- while the site
-// groups stream through), dealt from per-XCD counters with stealing.
+// unit is SPU sites of one band.  XCD x owns bands 2x and 2x+1 and deals
+// their units band-major from its own counter (its L2 holds the coefficients
+// of the band it is on -- 8 B/px: 2.76 MB per band at 2160x2560 -- while the
+// site groups of every job of the launch stream through, the XCDs an eighth
+// of the site groups apart), stealing from the next XCD's counter once its
+// own is drained.
 // Same-box job A/B (profiles/r2/ab_fused_sched_r2pqr.txt, ab_fused_dyn_r2zd.jsonl):
 // this deal against round 1's per-XCD queues that each owned two whole bands,
 // 13.8 vs 14.3 ms on one box, 14.5 vs 14.7 on another; against the same
@@ -247,16 +249,24 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   const uint32_t clo2 = (uint32_t)clip_lo * 0x00010001u, chi2 = (uint32_t)clip_hi * 0x00010001u;
   const int ngroups = (int)(npx >> 3);
   const int site_bytes = (int)(npx * 2);
-  int n_units = 0;  // every job's units, job after job
-  for (int j = 0; j < J.n; ++j) n_units += n_bands * (int)((J.j[j].n_sites + SPU - 1) / SPU);
+  int n_groups_all = 0;  // every job's site groups
+  for (int j = 0; j < J.n; ++j) n_groups_all += (int)((J.j[j].n_sites + SPU - 1) / SPU);
+  const int n_units = n_bands * n_groups_all;
   const float4 cc = make_float4(2.5f, 2.4f, 1.1f, 0.9f);
 
-  // Unit order: the sweep i = 0, 1, ... runs job by job; within a job it is
-  // band-major with the 8 XCDs two bands apart -- the job's unit i' is site
-  // group i' % n_groups_s of band (i' / n_groups_s + 2 * (i' % 8)) % n_bands
-  // -- and XCD x deals the units i = x + 8 j from its own counter
-  // (queues[x]), stealing from the next queue once its own is drained.  The
-  // next unit is grabbed while the current one streams.
+  // Unit order: XCD x deals the units i = x + 8 j from its own counter
+  // (queues[x]), stealing from the next queue once its own is drained, and
+  // owns the bands [x * n_bands / 8, (x + 1) * n_bands / 8): its j-th unit is
+  // band x * n_bands / 8 + j / G, site group (j + x * (G / 8)) % G of the G
+  // site groups of every job of the launch (job after job).  So each XCD's L2
+  // holds one band of coefficients at a time and reads each job's band once
+  // per launch (round 5's sweep walked every XCD over every band: a
+  // multi-job launch re-read each job's 44 MB of coefficient planes once per
+  // XCD, ~1.4 GB per 4 x 432-site step), and the XCDs stay G/8 site groups
+  // apart: with every XCD on the same or neighbouring site groups (different
+  // bands of the same sites at once) the single-job pass ran 4% slower
+  // (profiles/r6/ab_fused_sweep_xcd_bands_r6j.jsonl).  The next unit is
+  // grabbed while the current one streams.
   __shared__ int unit_sh;
   int q = xcc_id(), exhausted = 0;
   auto grab = [&]() -> int {
@@ -286,16 +296,17 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
   };
   auto decode = [&](int i) -> Unit {
     Unit r;
-    int job = 0, n_groups_s = 0;
-    for (;; ++job) {  // the sweep index's job (uniform: every lane the same)
-      n_groups_s = (int)((J.j[job].n_sites + SPU - 1) / SPU);
-      if (job + 1 >= J.n || i < n_bands * n_groups_s) break;
-      i -= n_bands * n_groups_s;
+    const int j8 = i >> 3;
+    const int band = (i & 7) * (n_bands >> 3) + j8 / n_groups_all;
+    int job = 0, grp = (j8 + (i & 7) * (n_groups_all >> 3)) % n_groups_all;
+    for (;; ++job) {  // the unit's job (uniform: every lane the same)
+      const int n_groups_s = (int)((J.j[job].n_sites + SPU - 1) / SPU);
+      if (job + 1 >= J.n || grp < n_groups_s) break;
+      grp -= n_groups_s;
     }
     const FusedJob& jb = J.j[job];
-    const int band = (i / n_groups_s + 2 * (i % 8)) % n_bands;
     r.job = job;
-    r.s0 = (int64_t)(i % n_groups_s) * SPU;
+    r.s0 = (int64_t)grp * SPU;
     r.ns = (int)(jb.n_sites - r.s0 < SPU ? jb.n_sites - r.s0 : SPU);
     r.g0 = (int)((int64_t)band * ngroups / n_bands);
     r.g1 = (int)((int64_t)(band + 1) * ngroups / n_bands);

@@ -29,6 +29,7 @@
 #                  short bench on DIST -> pmc_traffic_DIST_TAG.json
 #   ab:R:LIB,LIB   same-box A/B of library builds (TMH_LIB), R rounds, the
 #                  order reversed every other round (ab_TAG.jsonl)
+#   ab432:R:LIB,.. the same over dist432 runs (ab432_TAG.jsonl)
 # BENCH_ARGS adds flags to every bench run of quick/bright/repeat/ab/prof/pmc.
 set -u
 TAG=$1
@@ -102,6 +103,25 @@ for step in "$@"; do
         timeout -k 10 300 python bench.py --layout sharded --channels 4 --sites 432 --steps 10 \
         --warmup 3 --no-extras --cpu-sample 0 ${BENCH_ARGS:-} $V > $O/dist432v.tmp 2>> $O/dist432_v_$TAG.err || exit $?
       python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.strip()][-1]); print(json.dumps({'variant': sys.argv[2], 'value': d['value'], 'ms': d['ms_per_step'], 'host_ms': d.get('host_queue_ms_per_step'), 'check': d['check_vs_oracle'], 'k': {k: v['avg_ms'] for k, v in d['kernels'].items()}}))" $O/dist432v.tmp "$V" | tee -a $O/dist432_v_$TAG.jsonl
+      ;;
+    ab432)
+      # dist432 A/B over libraries: ab432:ROUNDS:LIB1,LIB2 (LIB may carry '+'-joined flags)
+      IFS=, read -r -a LIBS <<< "$a2"
+      : > $O/ab432_$TAG.jsonl
+      for i in $(seq 1 ${a1:-3}); do
+        ORDER=("${LIBS[@]}")
+        if [ $((i % 2)) -eq 0 ]; then
+          ORDER=(); for ((j=${#LIBS[@]}-1; j>=0; j--)); do ORDER+=("${LIBS[j]}"); done
+        fi
+        for L in "${ORDER[@]}"; do
+          IFS=+ read -r -a LA <<< "$L"
+          TMH_LIB=${LA[0]} TMH_BENCH_FORCE_DIST=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 \
+            MASTER_PORT=29517 timeout -k 10 300 python bench.py --layout sharded --channels 4 --sites 432 \
+            --steps 10 --warmup 3 --no-extras --cpu-sample 0 "${LA[@]:1}" > $O/ab432_$TAG.tmp 2>> $O/ab432_$TAG.err || exit $?
+          python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[2]) if l.strip()][-1]); print(json.dumps({'lib': sys.argv[1], 'value': d['value'], 'ms': d['ms_per_step'], 'check': d['check_vs_oracle'], 'k': {k: v['avg_ms'] for k, v in d['kernels'].items()}}))" "$L" $O/ab432_$TAG.tmp >> $O/ab432_$TAG.jsonl
+          tail -1 $O/ab432_$TAG.jsonl
+        done
+      done
       ;;
     prof432)
       TMH_BENCH_FORCE_DIST=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \

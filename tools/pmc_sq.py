@@ -7,19 +7,23 @@ and prints, per kernel (full name), the per-dispatch median of every counter
 over the headline-sized dispatches (>= 1/4 of the kernel's largest
 SQ_WAVE_CYCLES or first counter), plus derived ratios:
 
-  valu_busy       SQ_ACTIVE_INST_VALU * 4 / (n_simd * GRBM_GUI_ACTIVE)
+  gui_per_xcd     GRBM_GUI_ACTIVE / n_xcd (the counter is summed over the 8
+                  XCDs' GRBMs on gfx950: 222.0M over a 12.82 ms dispatch is
+                  8 x 2.16 GHz; SQ_BUSY_CYCLES / 32 SEs agrees)
+  valu_busy       SQ_ACTIVE_INST_VALU * 4 / (n_simd * gui_per_xcd)
                   (ACTIVE_INST_* count quad-cycles, summed over waves; a
                   SIMD issues for one wave at a time)
-  lds_busy        SQ_LDS_IDX_ACTIVE * 4 / (n_cu * GRBM_GUI_ACTIVE)
+  lds_busy        SQ_LDS_IDX_ACTIVE / (n_cu * gui_per_xcd)
   lds_conflict    SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   wait_any        SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves waiting on anything)
   wait_inst_any   SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (waiting for an
                   instruction's dependency: vmcnt / lgkmcnt)
   *_per_px        instructions (wave-level) per pixel of the dispatch
-  clock_mhz       GRBM_GUI_ACTIVE / dispatch duration (when the csv has
+  clock_mhz       gui_per_xcd / dispatch duration (when the csv has
                   timestamps)
 
     python tools/pmc_sq.py DIR [DIR ...] --pixels N -o out.json
+    python tools/pmc_sq.py --rederive OLD.json -o out.json   (counters kept, ratios recomputed)
 """
 from __future__ import annotations
 
@@ -51,16 +55,53 @@ def read_dirs(dirs):
     return out
 
 
+def derive(med, pixels, n_cu, n_xcd):
+    g = med.get("GRBM_GUI_ACTIVE")
+    dv = {}
+    if g:
+        g = g / n_xcd
+        if "SQ_ACTIVE_INST_VALU" in med:
+            dv["valu_busy"] = med["SQ_ACTIVE_INST_VALU"] * 4 / (4 * n_cu * g)
+        if "SQ_LDS_IDX_ACTIVE" in med:
+            dv["lds_busy"] = med["SQ_LDS_IDX_ACTIVE"] / (n_cu * g)
+        if "_ns" in med and med["_ns"] > 0:
+            dv["clock_mhz"] = g / med["_ns"] * 1e3
+    if med.get("SQ_LDS_IDX_ACTIVE"):
+        dv["lds_conflict"] = med.get("SQ_LDS_BANK_CONFLICT", 0.0) / med["SQ_LDS_IDX_ACTIVE"]
+    if med.get("SQ_WAVE_CYCLES"):
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS"):
+            if c in med:
+                dv[c.lower()[3:]] = med[c] / med["SQ_WAVE_CYCLES"]
+    for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD",
+              "SQ_INSTS_VMEM_WR"):
+        if c in med:
+            dv[c.lower()[3:] + "_per_px"] = med[c] / pixels
+    return {k: round(v, 4) for k, v in dv.items()}
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("dirs", nargs="+")
-    p.add_argument("--pixels", type=float, required=True,
+    p.add_argument("dirs", nargs="*")
+    p.add_argument("--pixels", type=float,
                    help="pixels one headline dispatch of the kernels of interest processes")
     p.add_argument("--n-cu", type=int, default=256)
+    p.add_argument("--n-xcd", type=int, default=8)
+    p.add_argument("--rederive", help="recompute the ratios of an earlier output's counters")
     p.add_argument("--kernels", default="k_correct_hist,k_welford_vec8",
                    help="comma list of kernel-name substrings to report")
     p.add_argument("-o", "--out", required=True)
     a = p.parse_args()
+    if a.rederive:
+        with open(a.rederive) as fh:
+            res = json.load(fh)
+        res["note"] = __doc__.split("\n\n")[1]
+        for v in res["kernels"].values():
+            v["derived"] = derive(v["counters"], res["pixels_per_dispatch"], a.n_cu, a.n_xcd)
+        with open(a.out, "w") as fh:
+            json.dump(res, fh, indent=1)
+        return
+    if not a.dirs or a.pixels is None:
+        p.error("DIR ... and --pixels are required")
     data = read_dirs(a.dirs)
     want = [k for k in a.kernels.split(",") if k]
     lib = os.environ.get("TMH_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
@@ -92,26 +133,7 @@ def main():
         for c, vs in per_counter.items():
             vs = sorted(vs)
             med[c] = vs[len(vs) // 2]
-        g = med.get("GRBM_GUI_ACTIVE")
-        dv = {}
-        if g:
-            if "SQ_ACTIVE_INST_VALU" in med:
-                dv["valu_busy"] = med["SQ_ACTIVE_INST_VALU"] * 4 / (4 * a.n_cu * g)
-            if "SQ_LDS_IDX_ACTIVE" in med:
-                dv["lds_busy"] = med["SQ_LDS_IDX_ACTIVE"] * 4 / (a.n_cu * g)
-            if "_ns" in med and med["_ns"] > 0:
-                dv["clock_mhz"] = g / med["_ns"] * 1e3
-        if med.get("SQ_LDS_IDX_ACTIVE"):
-            dv["lds_conflict"] = med.get("SQ_LDS_BANK_CONFLICT", 0.0) / med["SQ_LDS_IDX_ACTIVE"]
-        if med.get("SQ_WAVE_CYCLES"):
-            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS"):
-                if c in med:
-                    dv[c.lower()[3:]] = med[c] / med["SQ_WAVE_CYCLES"]
-        for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD",
-                  "SQ_INSTS_VMEM_WR"):
-            if c in med:
-                dv[c.lower()[3:] + "_per_px"] = med[c] / a.pixels
-        res["kernels"][name] = {"counters": med, "derived": {k: round(v, 4) for k, v in dv.items()},
+        res["kernels"][name] = {"counters": med, "derived": derive(med, a.pixels, a.n_cu, a.n_xcd),
                                 "dispatches": len(disps)}
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as fh:
