@@ -285,3 +285,72 @@ def test_sharded_job_gpu_decode_two_ranks(tmp_path):
             assert np.allclose(z["mean%d" % ch], ref[ch].mean.array, rtol=1e-6, atol=1e-12)
             assert np.allclose(z["std%d" % ch], ref[ch].std.array, rtol=1e-6, atol=1e-12)
     _check(ref, sites)
+
+
+class _HostFeeder(object):
+    """CPU stand-in for DeviceSiteFeeder: host decode, then the statistics'
+    update (the orchestration around the GPU inflate, without a GPU)."""
+
+    def __init__(self, **kw):
+        self.fed = 0
+
+    def feed(self, paths, stats, strict=False):
+        from tmlibrary_amd.models.file import read_channel_images
+        stats.update_batch(read_channel_images(paths, 2).astype(np.uint16))
+        self.fed += len(paths)
+        return len(paths)
+
+
+class OracleDeviceDouble(OracleChannelStats):
+    """The oracle double with the attribute that selects the GPU decode path."""
+
+    def update_device(self, *a, **k):  # never reached: the stand-in feeder updates on the host
+        raise AssertionError("update_device")
+
+
+def _empty_shard_worker(rank, world, port, root):
+    import sys
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import tmlibrary_amd.models.device_decode as dd
+    from tmlibrary_amd.models.file import ExperimentStore
+    from tmlibrary_amd.workflow.corilla.multi import run_channels_sharded
+    from test_multi_job import _HostFeeder as feeder_cls, OracleDeviceDouble as double
+    dd.DeviceSiteFeeder = feeder_cls
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tm = {}
+    res = run_channels_sharded(ExperimentStore(root), _batches(), dist=dist, stats_factory=double,
+                               block=2, decode_threads=2, decode="gpu", timing=tm)
+    np.savez(os.path.join(root, "e%d.npz" % rank),
+             **{"mean%d" % ch: c.mean.array for ch, c in res.items()},
+             **{"std%d" % ch: c.std.array for ch, c in res.items()},
+             **{"n%d" % ch: np.array([tm[ch]["sites"], tm[ch]["gpu_decoded"]]) for ch in res})
+    dist.destroy_process_group()
+
+
+def test_sharded_job_empty_shard_gpu_decode(tmp_path):
+    """with decode="gpu" and more ranks than a channel's
+    files, the rank with an empty shard goes straight to the merge (no
+    RawChunksUnsupported, no peer left waiting in a collective).  World 6
+    over channels of 7 and 5 files: channel 2 leaves one rank empty."""
+    from test_distributed_gloo import _free_port
+    store, sites = _make_store(str(tmp_path))
+    world = 6
+    mp.start_processes(_empty_shard_worker, args=(world, _free_port(), str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    empty = 0
+    for ch, ids in CHANNELS.items():
+        ref = orc.run_illumstats([sites[i] for i in ids])
+        got = 0
+        for r in range(world):
+            z = np.load(tmp_path / ("e%d.npz" % r))
+            n_sites, n_fed = z["n%d" % ch]
+            assert n_fed == n_sites, "every site of the shard through the (stand-in) GPU feeder"
+            got += n_sites
+            empty += n_sites == 0
+            assert np.allclose(z["mean%d" % ch], ref.mean, rtol=1e-6, atol=1e-12)
+            assert np.allclose(z["std%d" % ch], ref.std, rtol=1e-6, atol=1e-12)
+        assert got == len(ids)
+    assert empty >= 1
