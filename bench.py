@@ -2287,6 +2287,13 @@ def main():
                 if name in solo_kern:
                     solo = alg[alg_name] / (solo_kern[name] * 1e-3) / 1e9
                     fr[name + "_one_job_at_a_time"] = round(solo / box[probe]["GBs"], 4)
+                    # against the probe's persistent shape (a grid-strided
+                    # loop, the passes' own shape): one-launch-per-block flat
+                    # copies outrun every long-lived shape measured
+                    # (profiles/r6/mb_stream_r6k.txt)
+                    pers = box[probe].get("shapes", {}).get("persistent", {}).get("GBs")
+                    if pers:
+                        fr[name + "_one_job_at_a_time_vs_persistent_shape"] = round(solo / pers, 4)
             box["frac_of_box_copy"] = fr
             box["note"] = ("tmh_box_probe_device: 16-B non-temporal loads (+ stores) over the "
                            "job's own input and output blocks, %d sites, the faster of two "
