@@ -111,9 +111,11 @@ def parse():
                    help="TMH_OPT_WELFORD_PARTS (1..4 forces that split and the standard pass; "
                         "default: automatic, from the job's site probe)")
     p.add_argument("--welford-cus", type=int, default=None,
-                   help="(experiment) run each job lane's stream -- its Welford pass and planes "
-                        "-- on a stream CU-masked to this many CUs, leaving the rest to the "
-                        "previous job's histogram tail")
+                   help="(experiment) one channel: run each job lane's stream -- its Welford "
+                        "pass and planes -- on a stream CU-masked to this many CUs, leaving the "
+                        "rest to the previous job's histogram tail; several channels "
+                        "(pipelined order): the Welford passes on a stream so masked, the "
+                        "channels' merges and plane chains beside them on the rest")
     p.add_argument("--fused-config", type=int, default=None,
                    help="fused pass (sites per unit, threads, LDS bins) configuration 0..5 "
                         "(TMH_OPT_FUSED_CONFIG; default: automatic, from the job's site probe)")
@@ -1568,7 +1570,7 @@ def main():
             # for 4 x 432 sites, profiles/r5/dist432_stream_priority_r5y.jsonl)
             self.stream = (stream if (c == 0 and lane == 0) or a.channel_streams == "one"
                            else torch.cuda.Stream(dev))
-            if a.welford_cus:  # (experiment) this lane's Welford pass and planes on fewer CUs
+            if a.welford_cus and CH == 1:  # (experiment) the lane's Welford pass and planes on fewer CUs
                 self.stream = cu_masked_stream(torch, dev, a.welford_cus)
             self.sp = C.c_void_p(self.stream.cuda_stream)
             # jobs in flight: the corrected pass on a stream of its own, so the
@@ -1738,6 +1740,13 @@ def main():
     merge_mode = ("per-channel" if a.channel_order == "pipelined" and CH > 1 else
                   "batched" if a.channel_order == "deep" and CH > 1 else a.merge)
     pass_sp = C.c_void_p(pass_stream.cuda_stream) if pass_stream is not None else None
+    # (experiment, --welford-cus with several channels) the Welford passes on
+    # a CU-masked stream of their own, so the channels' plane chains queued
+    # beside them find free CUs; the corrected passes stay on the pass stream
+    wf_sp = pass_sp
+    if a.welford_cus and pass_stream is not None:
+        wf_stream = cu_masked_stream(torch, dev, a.welford_cus)
+        wf_sp = C.c_void_p(wf_stream.cuda_stream)
     multi_pass = pass_sp is not None and fused and a.pass_launch == "multi"
     # several channels on the pass stream: consecutive jobs (steps) alternate
     # between --jobs-in-flight sets of channel handles / correctors, so the
@@ -1779,12 +1788,12 @@ def main():
             for ch in S_(0):
                 ch.reset_probe()
             for ch in S_(0):
-                ch.welford(pass_sp)
+                ch.welford(wf_sp)
             for ch in S_(1):
                 ch.reset_probe()
         p = jobs["p"]
         for ch in S_(p + 1):  # probed a period ago: no host wait
-            ch.welford(pass_sp)
+            ch.welford(wf_sp)
         if jobs["counts"] is not None:  # job p-1's count merges (after its tails)
             if dist_on:
                 with torch.cuda.stream(small_stream):
@@ -1890,7 +1899,7 @@ def main():
             # channel's corrected pass
             reset_probe(X)
             for ch in X:
-                ch.welford(pass_sp)
+                ch.welford(wf_sp)
             prefetch()
             for ch in X:
                 with torch.cuda.stream(ch.stream):
@@ -1910,7 +1919,7 @@ def main():
             return
         reset_probe(X)  # every channel's probe queued before any Welford launch waits
         for ch in X:
-            ch.welford(pass_sp)
+            ch.welford(wf_sp)
         prefetch()
         evs = {}
         if dist_on and merge_mode == "batched":
