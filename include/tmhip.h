@@ -460,7 +460,9 @@ int tmh_synth_tables(int distribution, int height, int width, int32_t* ln16, int
  * per block.  reps repetitions on `stream`; ms_out = their average (HIP
  * events), sclk_mhz_out (may be NULL) = the shader clock during the last
  * persistent launch (clock64 ticks per 100 MHz wall_clock64 tick in
- * workgroup 0; 0 for modes 2 / 3).  Synchronous. */
+ * workgroup 0; 0 for modes 2 / 3).  Synchronous.  The copy modes overwrite
+ * the output blocks with the sites: probe before the outputs are produced or
+ * after they have been checked. */
 int tmh_box_probe_device(const uint16_t* const* dev_in_blocks, uint16_t* const* dev_out_blocks,
                          int block_shift, int64_t n_sites, int height, int width, int mode,
                          int reps, void* stream, double* ms_out, double* sclk_mhz_out);

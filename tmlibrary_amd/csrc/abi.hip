@@ -2170,6 +2170,7 @@ int tmh_box_probe_device(const uint16_t* const* dev_in_blocks, uint16_t* const* 
       TMH_HIP(hipEventSynchronize(e1));
       TMH_HIP(hipEventElapsedTime(&ms, e0, e1));
     } catch (...) {
+      (void)hipStreamSynchronize(s);  // no launch left using clk / sink as they unwind
       (void)hipEventDestroy(e0);
       (void)hipEventDestroy(e1);
       throw;
