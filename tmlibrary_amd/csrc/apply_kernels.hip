@@ -225,6 +225,156 @@ __global__ __launch_bounds__(256) void k_smooth_2d(const SmPlanes pl, int H, int
 
 static_assert(kSumTW == 256 - 2 * 20, "coefficient tiles are the sigma-5 smoothing's tiles");
 
+// block_sum256's tree (red[i] += red[i + o], o = 128, 64, ..., 1) and the
+// matching min, with two LDS exchanges and in-wave shuffles instead of eight
+// barriers each: the same additions of the same operands, so the same sum.
+// red: 2 x (128 + 64) doubles.  Thread 0 writes the tile's partials.
+__device__ __forceinline__ void tile_partials_wave(double s, double m, double* red, double* ps,
+                                                   double* pm) {
+  const int t = threadIdx.x;
+  double* rs1 = red;
+  double* rm1 = red + 128;
+  double* rs2 = red + 256;
+  double* rm2 = red + 320;
+  if (t >= 128) {
+    rs1[t - 128] = s;
+    rm1[t - 128] = m;
+  }
+  __syncthreads();
+  if (t < 128) {
+    s += rs1[t];
+    m = fmin(m, rm1[t]);
+    if (t >= 64) {
+      rs2[t - 64] = s;
+      rm2[t - 64] = m;
+    }
+  }
+  __syncthreads();
+  if (t < 64) {
+    s += rs2[t];
+    m = fmin(m, rm2[t]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s += __shfl_down(s, o, 64);
+      m = fmin(m, __shfl_down(m, o, 64));
+    }
+    if (t == 0) {
+      *ps = s;
+      if (pm) *pm = m;
+    }
+  }
+}
+
+template <bool STD>
+__device__ __forceinline__ double sm_xf(double v, double q) {
+  if (!STD) return v;
+  return q > 0.0 ? sqrt(v / q) : __builtin_nan("");
+}
+
+// Both axes in one pass, axis 1 register-blocked (sigma 5, R = 20): the
+// production form.  A workgroup owns one coefficient tile, kSumTW output
+// columns x 16 rows.  Axis 0 as k_smooth_2d: each of the 256 threads runs one
+// input column (the tile's 216 plus the reflected 2R halo) over the tile's
+// 16 + 2R input rows into 16 register accumulators.  Axis 1 differs: a thread
+// runs 18 consecutive outputs of one row from 58 LDS reads (k_smooth_2d: one
+// output from 41 reads, a serial chain of 41 FMAs per output), i.e. 18
+// independent chains; the outputs go back through LDS for coalesced stores
+// and the tile's column sums.  Every output's taps are added in k_smooth_2d's
+// order (axis 0 k = 0..2R, then axis 1 j = 0..2R, each from 0.0) and the tile
+// partials in tile_partials' tree: bit-identical outputs and partials
+// (tools/mb/mb_smooth.hip checks both; 0.086-0.091 vs 0.147 ms for a job's
+// two planes, 0.32 vs 0.60 ms for four jobs' eight,
+// profiles/r6/mb_smooth_r6s4.txt).  Rows rolled through the registers from one
+// 16-row chunk to the next (each input row read once per workgroup) measured
+// slower at every depth (56 live accumulators: half the occupancy;
+// mb_smooth_variants_r6s3.txt).
+constexpr int kVtS = 257;  // LDS row stride in doubles (odd: rows land on different banks)
+template <bool STD>
+__device__ __forceinline__ void smooth2d_blk_body(const double* __restrict__ in,
+                                                  double* __restrict__ out, double q,
+                                                  const double* __restrict__ w, double* ps,
+                                                  double* pm, int H, int W, double* vt,
+                                                  double* red) {
+  constexpr int R = 20, K = 2 * R + 1, CH = kSumTH, OX = 18, NG = kSumTW / OX;
+  static_assert(CH == 16 && NG * OX == kSumTW && NG * CH <= 256, "axis-1 work split");
+  const int tid = threadIdx.x;
+  const int x0 = blockIdx.x * kSumTW, y0 = blockIdx.y * CH;
+  // (-n <= i < 2n: one reflection; the launcher asks H, W > R)
+  auto refl = [](int i, int n) { return i < 0 ? -1 - i : (i >= n ? 2 * n - 1 - i : i); };
+  const double* __restrict__ col = in + refl(x0 - R + tid, W);
+  // the taps are symmetric bit for bit (abi.hip gaussian_taps writes w[R + i]
+  // and w[R - i] from one value): 21 scalar registers' worth, not 41
+  double wk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) wk[k] = w[k <= R ? k : 2 * R - k];
+  {  // axis 0: input rows y0 - R .. y0 + CH + R - 1 of this column
+    double acc[CH], v[CH + 2 * R];
+#pragma unroll
+    for (int t = 0; t < CH; ++t) acc[t] = 0.0;
+#pragma unroll
+    for (int u = 0; u < CH + 2 * R; ++u) v[u] = col[(int64_t)refl(y0 - R + u, H) * W];
+#pragma unroll
+    for (int u = 0; u < CH + 2 * R; ++u) {
+      const double x = sm_xf<STD>(v[u], q);
+#pragma unroll
+      for (int t = 0; t < CH; ++t)
+        if (u - t >= 0 && u - t <= 2 * R) acc[t] = fma(wk[u - t], x, acc[t]);
+    }
+#pragma unroll
+    for (int r = 0; r < CH; ++r) vt[r * kVtS + tid] = acc[r];
+  }
+  __syncthreads();
+  const int r1 = tid & (CH - 1), g1 = tid >> 4;  // axis-1 item: row r1, columns 18 g1 ..
+  const bool act1 = g1 < NG;
+  double o[OX];
+  if (act1) {
+    const double* row = vt + r1 * kVtS + OX * g1;
+#pragma unroll
+    for (int i = 0; i < OX; ++i) o[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < OX + 2 * R; ++j) {
+      const double v = row[j];
+#pragma unroll
+      for (int i = (j > 2 * R ? j - 2 * R : 0); i <= (j < OX - 1 ? j : OX - 1); ++i)
+        o[i] = fma(wk[j - i], v, o[i]);
+    }
+  }
+  __syncthreads();
+  if (act1) {
+#pragma unroll
+    for (int i = 0; i < OX; ++i) vt[r1 * kVtS + OX * g1 + i] = o[i];
+  }
+  __syncthreads();
+  const int x = x0 + tid;
+  double sum = 0.0, mn = __builtin_inf();
+  if (tid < kSumTW && x < W) {
+#pragma unroll
+    for (int r = 0; r < CH; ++r) {
+      if (y0 + r >= H) break;
+      const double a = vt[r * kVtS + tid];
+      out[(int64_t)(y0 + r) * W + x] = a;
+      sum += a;
+      if (a > 0.0 && a < mn) mn = a;  // NaN fails both; +inf never below mn
+    }
+  }
+  if (ps) {  // uniform per workgroup
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    tile_partials_wave(sum, mn, red, ps + tile, pm ? pm + tile : nullptr);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_smooth_2d_blk(const SmPlanes pl, int H, int W,
+                                                       const double* __restrict__ w) {
+  __shared__ double vt[kSumTH * kVtS];
+  __shared__ double red[384];
+  const int z = blockIdx.z;
+  const double q = pl.sq[z];
+  if (q == 0.0)
+    smooth2d_blk_body<false>(pl.in[z], pl.out[z], q, w, pl.psum[z], pl.pmin[z], H, W, vt, red);
+  else
+    smooth2d_blk_body<true>(pl.in[z], pl.out[z], q, w, pl.psum[z], pl.pmin[z], H, W, vt, red);
+}
+
 // The coefficient tiles' partial sums (and smallest positive values) of
 // planes in memory, in k_smooth_2d's partition and order.
 __global__ __launch_bounds__(256) void k_tile_sums(const SmPlanes pl, int H, int W) {
@@ -270,8 +420,17 @@ void launch_smooth_planes(const double* const* in, double* const* out, double* c
       a.psum[k] = psum[k];
       a.pmin[k] = pmin ? pmin[k] : nullptr;
     }
+    // k_smooth_2d_blk needs H, W > R (one reflection); TMH_SMOOTH_FORM=0 picks
+    // the round-5 form (A/B)
+    static const bool blk = [] {
+      const char* e = getenv("TMH_SMOOTH_FORM");
+      return !(e && atoi(e) == 0);
+    }();
     const dim3 g((unsigned)cdiv(W, kSumTW), (unsigned)cdiv(H, kSumTH), (unsigned)np);
-    hipLaunchKernelGGL((k_smooth_2d<kSumTH, 20>), g, dim3(256), 0, s, a, H, W, d_w);
+    if (blk && H > 20)
+      hipLaunchKernelGGL(k_smooth_2d_blk, g, dim3(256), 0, s, a, H, W, d_w);
+    else
+      hipLaunchKernelGGL((k_smooth_2d<kSumTH, 20>), g, dim3(256), 0, s, a, H, W, d_w);
     TMH_HIP(hipGetLastError());
     return;
   }

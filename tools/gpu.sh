@@ -223,6 +223,38 @@ for step in "$@"; do
         done
       done
       ;;
+    mb)
+      # a microbenchmark built here: mb:NAME[:ARGS] ('+' for spaces) -> mb_NAME_TAG.txt
+      V=$(echo "${a2:-}" | tr '+' ' ')
+      timeout -k 10 180 ./tools/mb/$a1 $V > $O/mb_${a1}_$TAG.txt 2>&1 || { tail -5 $O/mb_${a1}_$TAG.txt; exit 1; }
+      tail -20 $O/mb_${a1}_$TAG.txt
+      ;;
+    abenv|abenvb|abenv432)
+      # A/B over environment settings of one library: abenv:R:VAR=a,VAR=b (each
+      # entry may join several VAR=value with '+'), order reversed every other
+      # round; abenv = quick bench, abenvb = quick bench on bright data,
+      # abenv432 = the dist432 run
+      IFS=, read -r -a ENVS <<< "$a2"
+      : > $O/${name}_$TAG.jsonl
+      case $name in
+        abenv) CMD="python $QB"; DE="" ;;
+        abenvb) CMD="python $QB --distribution bright"; DE="" ;;
+        abenv432) CMD="python bench.py --layout sharded --channels 4 --sites 432 --steps 10 --warmup 3 --no-extras --cpu-sample 0 ${BENCH_ARGS:-}"
+          DE="TMH_BENCH_FORCE_DIST=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29517" ;;
+      esac
+      for i in $(seq 1 ${a1:-3}); do
+        ORDER=("${ENVS[@]}")
+        if [ $((i % 2)) -eq 0 ]; then
+          ORDER=(); for ((j=${#ENVS[@]}-1; j>=0; j--)); do ORDER+=("${ENVS[j]}"); done
+        fi
+        for E in "${ORDER[@]}"; do
+          EV=$(echo "$E" | tr '+' ' ')
+          env $EV $DE timeout -k 10 300 $CMD > $O/${name}_$TAG.tmp 2>> $O/${name}_$TAG.err || exit $?
+          python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[2]) if l.strip()][-1]); print(json.dumps({'env': sys.argv[1], 'value': d['value'], 'ms': d['ms_per_step'], 'check': d['check_vs_oracle'], 'k': {k: v['avg_ms'] for k, v in d['kernels'].items()}}))" "$E" $O/${name}_$TAG.tmp >> $O/${name}_$TAG.jsonl
+          tail -1 $O/${name}_$TAG.jsonl
+        done
+      done
+      ;;
     *)
       echo "unknown step $step"; exit 2
       ;;
