@@ -138,11 +138,6 @@ def parse():
                         "this many statistics handles / correctors / streams, so job k+1's "
                         "Welford pass runs while job k's histogram tail finishes (each job "
                         "still complete and checked; 1 = one job at a time)")
-    p.add_argument("--own-queues", action="store_true",
-                   help="(experiment) the corrected-pass, pass and probe streams and the library's "
-                        "histogram-tail streams each on a hardware queue of its own (a CU-masked "
-                        "stream with every CU set), so packets waiting for one pass block no "
-                        "other stream's work (TMH_TAIL_OWN_QUEUE=1 for the library)")
     p.add_argument("--jobs-order", choices=["welford", "planes", "corrected"], default="welford",
                    help="jobs in flight: job k+1's Welford pass starts after job k's Welford pass "
                         "(sharing HBM with job k's corrected pass, hiding job k's small kernels "
@@ -204,8 +199,6 @@ def parse():
                         "default profiles/pmc_traffic.json, profiles/pmc_traffic_bright.json for "
                         "--distribution bright)")
     a = p.parse_args()
-    if a.own_queues:  # read by the library when it creates a handle's tail stream
-        os.environ["TMH_TAIL_OWN_QUEUE"] = "1"
     if a.traffic_json is None:
         a.traffic_json = os.path.join(REPO, "profiles", "pmc_traffic%s.json" % (
             "" if a.distribution == "synthetic" else "_" + a.distribution))
@@ -1566,13 +1559,6 @@ def main():
 
     probe_sp = [None]  # several channels: the site probes' own stream (set below)
 
-    def new_stream():
-        """A stream for one role of the step; --own-queues: on a hardware
-        queue of its own (cu_masked_stream with every CU)"""
-        if a.own_queues:
-            return cu_masked_stream(torch, dev, torch.cuda.get_device_properties(dev).multi_processor_count)
-        return torch.cuda.Stream(dev)
-
     class Channel(object):
         """One channel's job: its sites, statistics handle, corrector and
         stream (channel 0 runs on the main stream; with several channels the
@@ -1592,7 +1578,7 @@ def main():
             # (tmhip.h stream contract) and the next job need not wait for it
             # (one stream for every lane's corrected pass: they run in job order)
             if jobs_in_flight > 1 and "cstream" not in shared_streams:
-                shared_streams["cstream"] = new_stream()
+                shared_streams["cstream"] = torch.cuda.Stream(dev)
             self.cstream = shared_streams["cstream"] if jobs_in_flight > 1 else self.stream
             self.csp = C.c_void_p(self.cstream.cuda_stream)
             blk_in, blk_out = chan_sites[c]
@@ -1745,7 +1731,8 @@ def main():
     # their own (each streaming pass alone on the GPU; the library orders it
     # against the channel's handle stream, and each channel's histogram tail
     # runs on its handle's tail stream under the next channel's pass)
-    pass_stream = (new_stream() if CH > 1 and a.channel_order in ("serial", "pipelined", "deep")
+    pass_stream = (torch.cuda.Stream(dev) if CH > 1 and a.channel_order in ("serial", "pipelined",
+                                                                         "deep")
                    else None)
     evs_p = {}
     # the pipelined order merges each channel on its own stream as soon as its
@@ -1773,7 +1760,7 @@ def main():
     # passes; three channel sets (jobs p-1, p, p+1 in flight)
     deep = a.channel_order == "deep" and pass_sp is not None and fused and B
     if pass_sp is not None or (J > 1 and a.prefetch_probe == "on"):
-        probe_stream = new_stream()
+        probe_stream = torch.cuda.Stream(dev)
         probe_sp[0] = C.c_void_p(probe_stream.cuda_stream)
     if deep:
         CJ = max(3, CJ)
@@ -2289,7 +2276,6 @@ def main():
                        "merge": merge_mode if dist_on else None,
                        "job_choice": choice,
                        "jobs_order": a.jobs_order if J > 1 else None,
-                       "own_queues": bool(a.own_queues),
                        "hbm_layout": (("sites in one buffer, corrected output in blocks of %d "
                                        "sites" % B) if in_contig else
                                       ("blocks of %d sites, input and output blocks allocated "

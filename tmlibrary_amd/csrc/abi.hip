@@ -1688,31 +1688,12 @@ static void fused_post(FusedPass& p, bool fixed) {
 // the handle's tail stream (the handle's stream waits for it), so s is free
 // as soon as the corrected sites are written (a caller pipelining jobs
 // starts the next one's Welford pass under this one's tail).
-// TMH_TAIL_OWN_QUEUE=1 (experiment): the tail stream on a hardware queue of
-// its own -- a stream with a CU mask (every CU set) is not one of the
-// runtime's shared queues, so the tail's packets, which wait for the
-// corrected pass, block no other stream's packets queued behind them.
-static void create_tail_stream(hipStream_t* s) {
-  static const bool own = [] {
-    const char* e = getenv("TMH_TAIL_OWN_QUEUE");
-    return e && atoi(e) != 0;
-  }();
-  if (!own) {
-    TMH_HIP(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
-    return;
-  }
-  int dev = 0, ncu = 0;
-  TMH_HIP(hipGetDevice(&dev));
-  TMH_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-  for (int i = 0; i < ncu; ++i) mask[i / 32] |= 1u << (i % 32);
-  TMH_HIP(hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()));
-}
-
 static hipStream_t fused_tail_stream(const FusedPass& p) {
   tmh_stats* h = p.h;
   if (!p.cross) return p.s;
-  if (!h->tail) create_tail_stream(&h->tail);  // on first use: every stream takes a queue slot
+  if (!h->tail) {  // created on first use: every stream takes a hardware queue slot
+    TMH_HIP(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
+  }
   TMH_HIP(hipEventRecord(h->ev_out, p.s));
   TMH_HIP(hipStreamWaitEvent(h->tail, h->ev_out, 0));
   return h->tail;
