@@ -86,13 +86,7 @@ int tmh_stats_reset(tmh_stats* h);
  * spread over the launch's first <= 64 sites, and the host waits for its
  * three counts (groups sampled, holding a value >= 4,096, >= 16,384) --
  * so that launch returns only once the probe has run on its stream.  Only
- * the chosen kernels are queued.  Once one job of the handle has been
- * probed, a later job's Welford launch takes the Welford form of the
- * handle's last probed job and only queues its own probe (no host wait;
- * TMH_WELFORD_PREDICT=0 in the environment turns this off); the fused pass,
- * which waits for the probe, still chooses from the job's own counts, and a
- * mispredicted form is slower, never different (test_gpu_parity.py
- * dark_then_bright_jobs).  The choice assumes the first <= 64 sites
+ * the chosen kernels are queued.  The choice assumes the first <= 64 sites
  * stand for the job: a job whose first sites are dark and later sites very
  * wide runs the narrow configurations, its wide values taking their global-
  * atomic path -- results identical, the pass slower (uniform 16-bit sites
@@ -219,9 +213,8 @@ int tmh_stats_variance(tmh_stats* h, double* host_var);
 int tmh_stats_wide_groups(tmh_stats* h, uint64_t* groups_out, int64_t* sites_out);
 /* The current job's site probe and the automatic choices it made (see the
  * options above): probe_counts[3] = groups sampled, groups with a value >=
- * 4,096, >= 16,384 (zeros before the probe ran); welford_bright = the form
- * the job's Welford pass took (1 / 0; before it ran, the probe's choice; -1 if
- * neither); fused_cfg = the configuration the fused
+ * 4,096, >= 16,384 (zeros before the probe ran); welford_bright = 1 / 0, -1
+ * if the job has not been probed; fused_cfg = the configuration the fused
  * pass runs (0..5, or TMH_FUSED_NO_HIST).  Any output may be NULL. */
 #define TMH_FUSED_NO_HIST 100
 int tmh_stats_job_choice(tmh_stats* h, uint32_t* probe_counts, int* welford_bright,

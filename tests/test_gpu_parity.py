@@ -828,66 +828,3 @@ def test_pipelined_chain_ranges_bit_exact(L):
     for h in hs:
         L.tmh_stats_destroy(h)
     acc.free()
-
-
-def test_welford_form_prediction_dark_then_bright_jobs(L):
-    """One handle, three jobs (tmhip.h, the site probe): job 1 (dark sites)
-    is probed before its Welford launch -> standard form; job 2 (bright
-    sites) takes job 1's form without waiting for its own probe -- the
-    mispredicted standard form, which must give the same statistics; job 3
-    (bright again) takes job 2's probed form, the bright one.  Every job is
-    checked against the oracle (percentile sums bit-exact)."""
-    from tmlibrary_amd import hip
-    from tmlibrary_amd.image import ZERO_LOG10
-    from tmlibrary_amd.synth import BRIGHT, STANDARD, synth_exact_sites_host
-    from tmlibrary_amd.workflow.corilla.quantiles import quantile_table, stats_log10_lut
-    n, H, W = 100, 32, 64  # >= 96 sites: the bright form's site parts apply
-    npx = H * W
-    q = np.linspace(0, 100, 1000)  # decimals 1 (stats.py:59-60)
-    lo, hi, gamma = quantile_table(npx, q)
-    lut = stats_log10_lut()
-    h = C.c_void_p()
-    hip.check(L.tmh_stats_create(H, W, len(q), hip.ptr(lo), hip.ptr(hi), hip.ptr(gamma),
-                                 hip.ptr(lut), 4, 0, C.byref(h)))
-    d_in = Dev(L, n * npx * 2)
-    d_out = Dev(L, n * npx * 2)
-    planes = [Dev(L, npx * 8) for _ in range(5)]
-    mean, std, smean, sstd, tmp = planes
-    try:
-        for job, (dist, want_form) in enumerate([(STANDARD, 0), (BRIGHT, 0), (BRIGHT, 1)]):
-            sites = synth_exact_sites_host(n, H, W, seed=40 + job, distribution=dist)
-            d_in.put(sites)
-            hip.check(L.tmh_stats_reset(h))
-            hip.check(L.tmh_stats_update_welford_device(h, d_in.p, n, 1, None))
-            pc, wb, fc = (C.c_uint32 * 3)(), C.c_int(), C.c_int()
-            hip.check(L.tmh_stats_job_choice(h, pc, C.byref(wb), C.byref(fc)))
-            assert wb.value == want_form, "job %d ran Welford form %d" % (job, wb.value)
-            hip.check(L.tmh_stats_finalize_device(h, mean.p, std.p, None))
-            L.tmh_synchronize(None)
-            hip.check(L.tmh_smooth_f64_device(mean.p, smean.p, tmp.p, H, W, 5.0, None))
-            hip.check(L.tmh_smooth_f64_device(std.p, sstd.p, tmp.p, H, W, 5.0, None))
-            L.tmh_synchronize(None)
-            c = C.c_void_p()
-            hip.check(L.tmh_corrector_create_device(smean.p, sstd.p, H, W, 1, ZERO_LOG10, None,
-                                                    C.byref(c)))
-            hip.check(L.tmh_correct_u16_hist_device(c, h, d_in.p, d_out.p, n, -1, -1, None))
-            L.tmh_synchronize(None)
-            L.tmh_corrector_destroy(c)
-            hip.check(L.tmh_stats_job_choice(h, pc, C.byref(wb), C.byref(fc)))
-            bright_probe = pc[1] >= 0.10 * pc[0]
-            assert bright_probe == (dist == BRIGHT), "the job's own probe"
-            acc = np.empty(len(q))
-            nn = C.c_int64()
-            m_h, s_h = np.empty((H, W)), np.empty((H, W))
-            hist = np.empty(65536, np.uint64)
-            hip.check(L.tmh_stats_finalize(h, C.byref(nn), hip.ptr(m_h), hip.ptr(s_h),
-                                           hip.ptr(acc), hip.ptr(hist)))
-            ref = orc.run_illumstats(list(sites), decimals=1)
-            assert nn.value == n
-            assert_close_rel(m_h, ref.mean)
-            assert_close_rel(s_h, ref.std)
-            assert np.array_equal(acc, ref.percentile_sums), "job %d percentile sums" % job
-    finally:
-        L.tmh_stats_destroy(h)
-        for b in planes + [d_in, d_out]:
-            b.free()

@@ -273,10 +273,6 @@ struct tmh_stats {
   bool probed = false;
   bool probe_queued = false;  // tmh_stats_probe_device: launched, not yet read
   unsigned int probe_cnt[3] = {0u, 0u, 0u};
-  // the Welford form the handle's last probed job took (-1: none yet): a
-  // later job's Welford launch takes it without waiting for its own probe
-  int last_bright = -1;
-  int wf_bright_ran = -1;  // the form this job's Welford pass took (-1: none yet)
   int64_t wide_sites = 0;         // sites that count covers
   bool pct_sum_external = false;
   DBuf<double> mean, m2, lut_log, gamma, acc, tmp_mean, tmp_std, rn;
@@ -577,23 +573,6 @@ int tmh_stats_set_option(tmh_stats* h, int option, int value) {
   });
 }
 
-// the probe's counts, once it has run (its event waited for)
-static void probe_take(tmh_stats* h) {
-  for (int i = 0; i < 3; ++i) h->probe_cnt[i] = h->probe_host[i];
-  h->probed = true;
-  h->probe_queued = false;
-  h->last_bright = (double)h->probe_cnt[1] >= kBrightFrac * (double)h->probe_cnt[0] ? 1 : 0;
-}
-
-// TMH_WELFORD_PREDICT=0 turns the prediction below off (A/B)
-static bool wf_predict() {
-  static const bool on = [] {
-    const char* e = getenv("TMH_WELFORD_PREDICT");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-
 int tmh_stats_reset(tmh_stats* h) {
   return guard([&] {
     TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
@@ -619,11 +598,7 @@ int tmh_stats_reset(tmh_stats* h) {
     h->last_batch = 0;
     h->pending = 0;
     h->pct_sum_external = false;
-    if (h->probe_queued) {  // its buffers are reused; its choice informs the next job
-      TMH_HIP(hipEventSynchronize(h->ev_probe));
-      probe_take(h);
-    }
-    h->wf_bright_ran = -1;
+    if (h->probe_queued) TMH_HIP(hipEventSynchronize(h->ev_probe));  // its buffers are reused
     h->probed = false;  // the next job probes its own sites
     h->probe_queued = false;
   });
@@ -643,7 +618,9 @@ static void stats_probe(tmh_stats* h, const uint16_t* d, int64_t ns, const SiteT
     TMH_HIP(hipEventRecord(h->ev_probe, s));
   }
   TMH_HIP(hipEventSynchronize(h->ev_probe));
-  probe_take(h);
+  for (int i = 0; i < 3; ++i) h->probe_cnt[i] = h->probe_host[i];
+  h->probed = true;
+  h->probe_queued = false;
 }
 
 // The probe queued ahead of the job's Welford launch (tmh_stats_probe_device):
@@ -728,27 +705,11 @@ static void stats_welford_dev(tmh_stats* h, const uint16_t* dev_sites, int64_t n
   }
   // the probe serves the fused pass's configuration and the Welford form
   const bool vec = tab.in || ((h->npx & 7) == 0 && (reinterpret_cast<uintptr_t>(dev_sites) & 15) == 0);
-  // A handle whose last job was probed takes that job's Welford form and
-  // only queues this job's probe (the fused pass waits for it): no host wait
-  // here, so a caller's next launches are queued at once (a rank's channels:
-  // the Welford passes follow the previous corrected pass without a gap for
-  // the probe).  Results do not depend on the form.
-  int bright = 0;
-  if (vec && (h->fused_cfg == kFusedAuto || (log_transform && h->wf_parts == 0))) {
-    if (h->last_bright >= 0 && !h->probed && wf_predict()) {
-      stats_probe_queue(h, dev_sites, n_sites, tab, s);
-      bright = h->last_bright;
-    } else {
-      stats_probe(h, dev_sites, n_sites, tab, s);
-      bright = probe_bright(h) ? 1 : 0;
-    }
-  } else {
-    bright = probe_bright(h) ? 1 : 0;
-  }
+  if (vec && (h->fused_cfg == kFusedAuto || (log_transform && h->wf_parts == 0)))
+    stats_probe(h, dev_sites, n_sites, tab, s);
   launch_welford(dev_sites, h->npx, n_sites, h->n, h->rn.p, h->mean.p, h->m2.p, h->lut_log.p,
-                 log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, h->wide.p, bright, s, -1,
-                 tab);
-  h->wf_bright_ran = bright;
+                 log_transform, h->wf_part.p, h->wf_part.n, h->wf_parts, h->wide.p,
+                 probe_bright(h) ? 1 : 0, s, -1, tab);
   if ((h->npx & 7) == 0) h->wide_sites += n_sites;
   h->n += n_sites;
   h->pending += n_sites;
@@ -949,9 +910,7 @@ int tmh_stats_job_choice(tmh_stats* h, uint32_t* probe_counts, int* welford_brig
     TMH_CHECK(h, TMH_EINVAL, "handle is NULL");
     if (probe_counts)
       for (int i = 0; i < 3; ++i) probe_counts[i] = h->probed ? h->probe_cnt[i] : 0u;
-    if (welford_bright)
-      *welford_bright = h->wf_bright_ran >= 0 ? h->wf_bright_ran
-                                              : h->probed ? (probe_bright(h) ? 1 : 0) : -1;
+    if (welford_bright) *welford_bright = h->probed ? (probe_bright(h) ? 1 : 0) : -1;
     if (fused_cfg) {
       const int c = probe_fused_cfg(h);
       *fused_cfg = c == kFusedNoHist ? TMH_FUSED_NO_HIST : c;
