@@ -1228,7 +1228,8 @@ static void corrector_init(tmh_corrector* c, const double* d_mean, const double*
 // capacity for 1/1024 of the launch's pixels (an overflow makes the fixup
 // recompute every pixel in f64: slow but exact), count reset on s.  One
 // launch at a time per corrector (the list is reused).
-static FixList corrector_fixlist(tmh_corrector* c, int64_t n_sites, hipStream_t s) {
+static FixList corrector_fixlist(tmh_corrector* c, int64_t n_sites, hipStream_t s,
+                                 bool reset = true) {
   TMH_CHECK(n_sites < ((int64_t)1 << 24), TMH_EINVAL, "at most 2^24 - 1 sites per correct call");
   const int64_t want = std::min<int64_t>(std::max<int64_t>((int64_t)1 << 20, n_sites * c->npx / 1024),
                                          (int64_t)1 << 30);
@@ -1236,7 +1237,7 @@ static FixList corrector_fixlist(tmh_corrector* c, int64_t n_sites, hipStream_t 
     TMH_HIP(hipDeviceSynchronize());  // the list may be in use on any stream
     c->fix_e.alloc((size_t)want);
   }
-  TMH_HIP(hipMemsetAsync(c->fix_n.p, 0, sizeof(unsigned int), s));
+  if (reset) TMH_HIP(hipMemsetAsync(c->fix_n.p, 0, sizeof(unsigned int), s));
   return FixList{c->fix_e.p, c->fix_n.p, (unsigned int)c->fix_e.n};
 }
 
@@ -1607,7 +1608,8 @@ static bool fused_begin(tmh_corrector* c, tmh_stats* h, hipStream_t s) {
 }
 
 // buffers, rare lists, fixup list and the configuration of one job's pass
-static void fused_prepare(FusedPass& p) {
+// (batched: the caller zeroes the fixup counter with its other jobs')
+static void fused_prepare(FusedPass& p, bool batched = false) {
   tmh_stats* h = p.h;
   tmh_corrector* c = p.c;
   const int64_t n_sites = p.n;
@@ -1657,7 +1659,7 @@ static void fused_prepare(FusedPass& p) {
   // one configuration, chosen on the host from the job's site probe (probed
   // at the Welford launch, or above for a job whose Welford pass did not)
   p.cfg = probe_fused_cfg(h);
-  p.fl = corrector_fixlist(c, n_sites, s);
+  p.fl = corrector_fixlist(c, n_sites, s, !batched);
 }
 
 // what follows the job's fused launch up to its histogram tail: rare lists,
@@ -1874,10 +1876,19 @@ static void correct_hist_multi(tmh_corrector* const* cs, tmh_stats* const* hs, i
     const bool cross = fused_begin(cs[j], hs[j], s);
     p[np] = FusedPass{cs[j], hs[j], ins ? ins[j] : nullptr, outs ? outs[j] : nullptr, n_sites[j],
                       tabs[j], s, cross, clip_lo, clip_hi};
-    fused_prepare(p[np]);
+    fused_prepare(p[np], true);
     ++np;
   }
   if (np == 0) return;
+  // every job's fixup counter, and the unit queues of the jobs sharing the
+  // first job's launch, zeroed by one kernel (a fill per array cost ~10 us
+  // each on the pass stream, 8 of them ahead of a four-job launch)
+  ZeroList32 Z;
+  for (int j = 0; j < np; ++j) {
+    Z.add(p[j].c->fix_n.p, 1);
+    if (p[j].cfg == p[0].cfg) Z.add(p[j].c->queues.p, kFusedQueueInts);
+  }
+  launch_zero_u32(Z, s);
   FusedJobs J{};
   for (int j = 0; j < np; ++j) {
     if (p[j].cfg != p[0].cfg) {  // its own launch
@@ -1890,8 +1901,7 @@ static void correct_hist_multi(tmh_corrector* const* cs, tmh_stats* const* hs, i
     }
     tmh_corrector* c = p[j].c;
     // the launch's unit counters are the first job's queues[0..8); every
-    // job's round-mask union is its own corrector's queues + 8
-    TMH_HIP(hipMemsetAsync(c->queues.p, 0, kFusedQueueInts * sizeof(int), s));
+    // job's round-mask union is its own corrector's queues + 8 (zeroed above)
     J.j[J.n++] = FusedJob{p[j].in, p[j].out, p[j].n,
                           reinterpret_cast<const float4*>(c->coef2.p), c->mconst2.p, p[j].fl,
                           p[j].h->hist_full.p, p[j].h->hist_rmask.p,

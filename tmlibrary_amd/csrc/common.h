@@ -245,6 +245,18 @@ struct ZeroList {
   }
 };
 void launch_zero_u64(const ZeroList& z, hipStream_t s);
+// Small u32 arrays zeroed in one launch (a multi-job corrected pass's
+// per-job fixup counters and unit queues: one kernel, not a fill per array)
+struct ZeroList32 {
+  unsigned int* p[16];
+  int count[16];  // u32 elements
+  int n = 0;
+  void add(void* ptr, int elems) {
+    p[n] = static_cast<unsigned int*>(ptr);
+    count[n++] = elems;
+  }
+};
+void launch_zero_u32(const ZeroList32& z, hipStream_t s);
 
 constexpr int kMaxJobs = 8;          // jobs (a rank's channels) of one multi-job launch
 // Several fused jobs' histogram tails (same image size)

@@ -1228,6 +1228,17 @@ void launch_zero_u64(const ZeroList& z, hipStream_t s) {
   TMH_HIP(hipGetLastError());
 }
 
+__global__ __launch_bounds__(256) void k_zero_u32(const ZeroList32 z) {
+  for (int k = 0; k < z.n; ++k)
+    for (int i = threadIdx.x; i < z.count[k]; i += 256) z.p[k][i] = 0u;
+}
+
+void launch_zero_u32(const ZeroList32& z, hipStream_t s) {
+  if (z.n == 0) return;
+  hipLaunchKernelGGL(k_zero_u32, dim3(1), dim3(256), 0, s, z);
+  TMH_HIP(hipGetLastError());
+}
+
 __global__ void k_copy_f64(const double* __restrict__ src, double* __restrict__ dst, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) dst[i] = src[i];
