@@ -185,6 +185,14 @@ for step in "$@"; do
       python3 tools/pmc_traffic.py $O/pmc_FETCH_SIZE_${D}_$TAG $O/pmc_WRITE_SIZE_${D}_$TAG --sites 3456 \
         --height 2160 --width 2560 --distribution $D -o $O/pmc_traffic_${D}_$TAG.json || exit $?
       ;;
+    pmcinstall)
+      # the pmc:DIST result of this call as the bench's traffic file (so a
+      # bench later in the same call reports roofline.traffic for this build)
+      D=${a1:-synthetic}
+      SUF=""; [ "$D" != "synthetic" ] && SUF="_$D"
+      cp $O/pmc_traffic_${D}_$TAG.json profiles/pmc_traffic${SUF}.json || exit $?
+      mkdir -p $O/profiles && cp $O/pmc_traffic_${D}_$TAG.json $O/profiles/pmc_traffic${SUF}.json
+      ;;
     avail)
       timeout -k 10 60 rocprofv3 --list-avail > $O/pmc_avail_$TAG.txt 2>&1 || exit $?
       grep -cE "SQ_|GRBM_" $O/pmc_avail_$TAG.txt || true
