@@ -219,11 +219,14 @@ def test_smooth_and_correct_vs_golden(L, name):
 
 
 @pytest.mark.parametrize("shape", [(2160, 2560), (300, 217), (37, 53), (20, 30), (1, 300),
-                                   (300, 1), (5, 5)])
+                                   (300, 1), (5, 5), (21, 41), (34, 41), (35, 234), (48, 64),
+                                   (100, 235), (53, 433)])
 def test_smooth_one_pass_bit_identical(L, shape, monkeypatch):
-    """The one-pass 2-D smoothing kernel (k_smooth_2d, sigma 5) equals the
-    two separable passes bit for bit, edges and planes narrower than the
-    kernel included, and matches the oracle."""
+    """The one-pass 2-D smoothing kernel (k_smooth_2d_blk, sigma 5; planes of
+    <= 20 rows: k_smooth_2d) equals the two separable passes bit for bit,
+    edges and planes narrower than the kernel included, and matches the
+    oracle.  21 / 34 rows and 41 / 64 / 234 / 235 columns: tiles whose halo
+    threads and rows reach past one reflection (clamped, apply_kernels.hip)."""
     from tmlibrary_amd.image import smooth_f64
     rng = np.random.default_rng(shape[0] * 7 + shape[1])
     plane = rng.random(shape) * 4.0 + 1.0

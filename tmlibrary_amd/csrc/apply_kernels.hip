@@ -299,8 +299,14 @@ __device__ __forceinline__ void smooth2d_blk_body(const double* __restrict__ in,
   static_assert(CH == 16 && NG * OX == kSumTW && NG * CH <= 256, "axis-1 work split");
   const int tid = threadIdx.x;
   const int x0 = blockIdx.x * kSumTW, y0 = blockIdx.y * CH;
-  // (-n <= i < 2n: one reflection; the launcher asks H, W > R)
-  auto refl = [](int i, int n) { return i < 0 ? -1 - i : (i >= n ? 2 * n - 1 - i : i); };
+  // One reflection: -n <= i < 2n.  The launcher asks H, W > R, so i >= -R
+  // holds; indices past n - 1 + R feed no output inside the plane (the
+  // tile's last threads and rows on narrow or short planes), so they are
+  // clamped there first -- every load stays inside the plane.
+  auto refl = [](int i, int n) {
+    i = i < n + R - 1 ? i : n + R - 1;
+    return i < 0 ? -1 - i : (i >= n ? 2 * n - 1 - i : i);
+  };
   const double* __restrict__ col = in + refl(x0 - R + tid, W);
   // the taps are symmetric bit for bit (abi.hip gaussian_taps writes w[R + i]
   // and w[R - i] from one value): 21 scalar registers' worth, not 41
