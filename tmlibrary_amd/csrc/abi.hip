@@ -530,7 +530,7 @@ void tmh_stats_destroy(tmh_stats* h) {
   for (int i = 0; i < h->join_n; ++i) (void)hipEventSynchronize(h->join_ev[i]);
   if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
   if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
-  hipStream_t s = h->own_stream, side = h->side, tail = h->tail == h->side ? nullptr : h->tail;
+  hipStream_t s = h->own_stream, side = h->side, tail = h->tail;
   if (side) (void)hipStreamSynchronize(side);
   if (tail) (void)hipStreamSynchronize(tail);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
@@ -1694,14 +1694,7 @@ static hipStream_t fused_tail_stream(const FusedPass& p) {
   tmh_stats* h = p.h;
   if (!p.cross) return p.s;
   if (!h->tail) {  // created on first use: every stream takes a hardware queue slot
-    static const bool on_side = [] {  // (A/B) the handle's side stream as its tail stream
-      const char* e = getenv("TMH_TAIL_ON_SIDE");
-      return e && atoi(e) != 0;
-    }();
-    if (on_side)
-      h->tail = h->side;
-    else
-      TMH_HIP(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
+    TMH_HIP(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
   }
   TMH_HIP(hipEventRecord(h->ev_out, p.s));
   TMH_HIP(hipStreamWaitEvent(h->tail, h->ev_out, 0));
