@@ -124,6 +124,28 @@ __global__ void k_rn_table(double* __restrict__ rn, int64_t n0, int64_t n) {
   if (i < n) rn[i] = 1.0 / (double)(n0 + i + 1);
 }
 
+// LDS byte offsets of a packed word's two table entries (8-B entries, indices
+// masked to the table): one v_and keeps both halves' index bits, then one SDWA
+// shift per half selects and scales it -- three VALU ops per word where the
+// compiler's shift-and-mask pairs took four (the standard pass issues 2 such
+// ops per pixel beside its 3 f64 ops).  `three` is a VGPR holding 3 (an SDWA
+// shift amount is a register operand).
+__device__ __forceinline__ void lut_offsets(uint32_t w, uint32_t idx_mask2, uint32_t three,
+                                            uint32_t& lo, uint32_t& hi) {
+  const uint32_t m = w & idx_mask2;
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "
+      "src1_sel:WORD_0"
+      : "=v"(lo)
+      : "v"(three), "v"(m));
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "
+      "src1_sel:WORD_1"
+      : "=v"(hi)
+      : "v"(three), "v"(m));
+}
+__device__ __forceinline__ double lds_at(const double* base, uint32_t byte_off) {
+  return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
 // Stats transform of eight pixels: LDS LUT gather of each value's low 12
 // bits (no clamp: the index stays in the table), then -- only when a word has
 // a value >= 4,096 -- those slots recomputed with log10_big (wc counts such
@@ -137,10 +159,20 @@ __device__ __forceinline__ void xform8(const uint4 v, const double* slut, const 
                          v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
   const uint32_t any = v.x | v.y | v.z | v.w;
   const bool wide = (any & 0xF000F000u) != 0;
+  if (LOG) {  // the table entries of every pixel's low index bits
+    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t three = 3u;
+    constexpr uint32_t kMask2 = (uint32_t)(LUTN - 1) * 0x00010001u;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      uint32_t lo, hi;
+      lut_offsets(wd[p], kMask2, three, lo, hi);
+      x[2 * p] = lds_at(slut, lo);
+      x[2 * p + 1] = lds_at(slut, hi);
+    }
+  }
   if (LOG && LUTN == kWfLutBright) {  // exact below 16,384
     constexpr uint32_t kIdx = LUTN - 1;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = slut[u[k] & kIdx];
     wc += wide ? 1u : 0u;
     if (any & 0xC000C000u) {  // a value >= 16,384
       ++xc;
@@ -150,8 +182,6 @@ __device__ __forceinline__ void xform8(const uint4 v, const double* slut, const 
     }
   } else if (LOG) {
     constexpr uint32_t kIdx = kWfLut - 1;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = slut[u[k] & kIdx];
     if (wide) {
       ++wc;
       xc += (any & 0xC000C000u) ? 1u : 0u;  // a value >= 16,384
@@ -268,17 +298,14 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
   // (gfx9 has no 64-bit scalar less-than; an int64 test costs two VALU ops
   // per site in a VALU-issue-bound loop)
   const int ns = (int)n_sites;
-  for (int s = 0; s < ns; s += G) {
-#pragma unroll
-    for (int k = 0; k < G; ++k) {
-      const int t = s + G + k;
-      nxt[k] = ld_site<NTL>(site(t < (int)last ? t : (int)last));
-    }
+  // stage of G sites starting at s: the next stage's loads are issued first;
+  // two register sets used in turn (no copy of the next set into the current)
+  auto fold = [&](const uint4 (&v)[G], int s) {
 #pragma unroll
     for (int k = 0; k < G; ++k) {
       if (s + k < ns) {
         double x[8];
-        xform8<LOG, INV, LUTN>(cur[k], slut, sinv, x, wc, xc);
+        xform8<LOG, INV, LUTN>(v[k], slut, sinv, x, wc, xc);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const double d = x[j] - K[j];
@@ -287,8 +314,20 @@ __global__ __launch_bounds__(NT) void k_welford_vec8(
         }
       }
     }
+  };
+  auto issue = [&](uint4 (&v)[G], int s) {
 #pragma unroll
-    for (int k = 0; k < G; ++k) cur[k] = nxt[k];
+    for (int k = 0; k < G; ++k) {
+      const int t = s + k;
+      v[k] = ld_site<NTL>(site(t < (int)last ? t : (int)last));
+    }
+  };
+  for (int s = 0; s < ns; s += 2 * G) {
+    issue(nxt, s + G);
+    fold(cur, s);
+    if (s + G >= ns) break;
+    issue(cur, s + 2 * G);
+    fold(nxt, s + G);
   }
 
   if (wide) {  // one global add per counter and workgroup (thread 0's group always exists)
