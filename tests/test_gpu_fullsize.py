@@ -170,7 +170,7 @@ def test_bright_fullsize(L):
     adds for every pixel >= 4,096) must give identical results, and both
     match the oracle.  (64 sites: below the 96 the bright Welford pass needs,
     so this covers the standard pass's rare log10 path; tests/test_gpu_blocked.py
-    runs 100 bright sites through the 16,384-entry bright pass.)"""
+    runs 100 bright sites through the bright pass and its 20,472-entry table.)"""
     import torch
 
     from tmlibrary_amd import hip

@@ -78,21 +78,39 @@ __device__ __forceinline__ double log10_big(uint32_t u, const double* slut, cons
 // set (one OR/AND over the four packed words).
 constexpr int kWfLut = 4096;
 
+// The fill issues up to 8 of a thread's loads before its LDS stores (one L2
+// round trip per 8 entries instead of one per entry: a 1,024-thread bright
+// workgroup, alone on its CU, waits out its whole fill).
 template <int INV, int LUTN = kWfLut>
 __device__ __forceinline__ void fill_wf_tables(const double* __restrict__ lut, double* slut,
                                                double* sinv, int nt) {
-  for (int i = threadIdx.x; i < LUTN; i += nt) {
-    slut[i] = lut[i];
-    if (INV == 1 && i < kWfLut) sinv[i] = i ? 1.0 / (16.0 * (double)i) : 0.0;
+  constexpr int U = 8;
+  for (int i0 = threadIdx.x; i0 < LUTN; i0 += U * nt) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * nt;
+      v[u] = i < LUTN ? lut[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * nt;
+      if (i < LUTN) slut[i] = v[u];
+      if (INV == 1 && i < kWfLut) sinv[i] = i ? 1.0 / (16.0 * (double)i) : 0.0;
+    }
   }
 }
 
-// Bright sites: the host LUT's first kWfLutBright entries (128 KB of LDS, one
-// 1,024-thread workgroup per CU) -- values below 16,384 take the exact table
-// like the standard pass's values below 4,096, and only the ~2% of bright
-// pixels >= 16,384 the log10_big path (with 4,096 entries most bright pixels
-// took it: the pass was VALU-bound, 11.3-12.3 ms against 6.0 on standard sites)
-constexpr int kWfLutBright = 16384;
+// Bright sites: the host LUT's first kWfLutBright entries (160 KB of LDS less
+// the pass's two counters and reciprocal slot, one 1,024-thread workgroup per
+// CU) -- values below it take the exact table like the standard pass's values
+// below 4,096, and only the bright pixels above it the log10_big path (with
+// 4,096 entries most bright pixels took it: the pass was VALU-bound, 11.3-12.3
+// ms against 6.0 on standard sites).  A wave runs that path for a pixel slot
+// when any of its 64 lanes needs it: at 16,384 entries (round 3-6) ~1.5% of the
+// bright values did, i.e. most slots of most waves; at 20,472 about half as
+// many.  Not a power of two: indices are clamped (v_pk_min_u16), not masked.
+constexpr int kWfLutBright = 20472;
 constexpr int kWfThreadsBright = 1024;
 
 template <bool LOG>
@@ -124,15 +142,15 @@ __global__ void k_rn_table(double* __restrict__ rn, int64_t n0, int64_t n) {
   if (i < n) rn[i] = 1.0 / (double)(n0 + i + 1);
 }
 
-// LDS byte offsets of a packed word's two table entries (8-B entries, indices
-// masked to the table): one v_and keeps both halves' index bits, then one SDWA
-// shift per half selects and scales it -- three VALU ops per word where the
-// compiler's shift-and-mask pairs took four (the standard pass issues 2 such
-// ops per pixel beside its 3 f64 ops).  `three` is a VGPR holding 3 (an SDWA
-// shift amount is a register operand).
-__device__ __forceinline__ void lut_offsets(uint32_t w, uint32_t idx_mask2, uint32_t three,
-                                            uint32_t& lo, uint32_t& hi) {
-  const uint32_t m = w & idx_mask2;
+// LDS byte offsets of a packed word's two table entries (8-B entries): the
+// caller brings both halves' indices into the table (one v_and with the
+// 4,096-entry mask, or one v_pk_min_u16 clamp for the bright table), then one
+// SDWA shift per half selects and scales it -- three VALU ops per word where
+// the compiler's shift-and-mask pairs took four (the standard pass issues 2
+// such ops per pixel beside its 3 f64 ops).  `three` is a VGPR holding 3 (an
+// SDWA shift amount is a register operand).
+__device__ __forceinline__ void lut_offsets(uint32_t m, uint32_t three, uint32_t& lo,
+                                            uint32_t& hi) {
   asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "
       "src1_sel:WORD_0"
       : "=v"(lo)
@@ -142,15 +160,24 @@ __device__ __forceinline__ void lut_offsets(uint32_t w, uint32_t idx_mask2, uint
       : "=v"(hi)
       : "v"(three), "v"(m));
 }
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t w, uint32_t c2) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, w),
+                                                                __builtin_bit_cast(u16x2_t, c2)));
+}
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, a),
+                                                                __builtin_bit_cast(u16x2_t, b)));
+}
 __device__ __forceinline__ double lds_at(const double* base, uint32_t byte_off) {
   return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + byte_off);
 }
 
-// Stats transform of eight pixels: LDS LUT gather of each value's low 12
-// bits (no clamp: the index stays in the table), then -- only when a word has
-// a value >= 4,096 -- those slots recomputed with log10_big (wc counts such
-// groups, xc the groups with a value >= 16,384: the fused pass picks its
-// histogram configuration from them).  The inner loop is VALU-issue bound (3 f64 ops per
+// Stats transform of eight pixels: LDS LUT gather of each value's table
+// index (the low 12 bits, or for the bright table the value clamped to it),
+// then -- only when a word has a value past the table -- those slots
+// recomputed with log10_big (wc counts the groups with a value >= 4,096, xc
+// those with a value >= 16,384: diagnostics since round 5).  The inner loop is VALU-issue bound (3 f64 ops per
 // pixel), so the integer work per pixel is kept to the gather address.
 template <bool LOG, int INV, int LUTN = kWfLut>
 __device__ __forceinline__ void xform8(const uint4 v, const double* slut, const double* sinv,
@@ -159,29 +186,30 @@ __device__ __forceinline__ void xform8(const uint4 v, const double* slut, const 
                          v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
   const uint32_t any = v.x | v.y | v.z | v.w;
   const bool wide = (any & 0xF000F000u) != 0;
-  if (LOG) {  // the table entries of every pixel's low index bits
+  constexpr bool kPow2 = (LUTN & (LUTN - 1)) == 0;
+  constexpr uint32_t kIdx = LUTN - 1;
+  if (LOG) {  // the table entries of every pixel (index masked or clamped)
     const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
     const uint32_t three = 3u;
-    constexpr uint32_t kMask2 = (uint32_t)(LUTN - 1) * 0x00010001u;
+    constexpr uint32_t kIdx2 = kIdx * 0x00010001u;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       uint32_t lo, hi;
-      lut_offsets(wd[p], kMask2, three, lo, hi);
+      lut_offsets(kPow2 ? wd[p] & kIdx2 : pk_min_u16(wd[p], kIdx2), three, lo, hi);
       x[2 * p] = lds_at(slut, lo);
       x[2 * p + 1] = lds_at(slut, hi);
     }
   }
-  if (LOG && LUTN == kWfLutBright) {  // exact below 16,384
-    constexpr uint32_t kIdx = LUTN - 1;
+  if (LOG && LUTN == kWfLutBright) {  // exact below kWfLutBright
     wc += wide ? 1u : 0u;
-    if (any & 0xC000C000u) {  // a value >= 16,384
-      ++xc;
+    xc += (any & 0xC000C000u) ? 1u : 0u;  // a value >= 16,384
+    const uint32_t mx = pk_max_u16(pk_max_u16(v.x, v.y), pk_max_u16(v.z, v.w));
+    if ((mx & 0xFFFFu) > kIdx || (mx >> 16) > kIdx) {  // a value beyond the table
 #pragma unroll
       for (int k = 0; k < 8; ++k)
         if (u[k] > kIdx) x[k] = log10_big<INV>(u[k], slut, sinv);
     }
   } else if (LOG) {
-    constexpr uint32_t kIdx = kWfLut - 1;
     if (wide) {
       ++wc;
       xc += (any & 0xC000C000u) ? 1u : 0u;  // a value >= 16,384
