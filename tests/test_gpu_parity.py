@@ -658,7 +658,7 @@ def _fused_job(L, sites, clip=(-1, -1), q=None):
     pc, wb, fc = (C.c_uint32 * 3)(), C.c_int(), C.c_int()
     hip.check(L.tmh_stats_job_choice(h, pc, C.byref(wb), C.byref(fc)))
     res = dict(n=nn.value, mean=m_h, std=s_h, acc=acc, hist=hist, site_hist=site_h, out=out,
-               fused_cfg=fc.value,
+               fused_cfg=fc.value, welford_bright=wb.value,
                smean=smean.get(np.float64, (H, W)), sstd=sstd.get(np.float64, (H, W)),
                order_stats=site_order_stats(L, h, range(n), Q))
     L.tmh_corrector_destroy(c)
@@ -721,6 +721,32 @@ def test_fused_correct_hist_pipeline(L, kind):
         want = orc.correct_illumination(s, r["smean"], r["sstd"])
         assert_dn(o, want)
     check_order_stats(sites, r["order_stats"])
+
+
+def test_bright_welford_table_edges(L):
+    """The bright Welford form's table covers values below 20,472 (160 KB of
+    LDS, stats_kernels.hip kWfLutBright; indices clamped, not masked): values
+    on both sides of its end and of round 6's 16,384-entry end, in every
+    site and as constant columns (std exactly 0 on either path), against the
+    oracle at the 1e-6 bar everywhere and 1e-9 on the edge pixels (the
+    log10_big path past the table is within 3e-10 of numpy's log10)."""
+    from tmlibrary_amd.synth import BRIGHT, synth_exact_host
+    n, H, W = 100, 48, 64  # >= 96 sites: the bright form's three site parts
+    sites = np.stack([synth_exact_host(H, W, 77, 1, i, BRIGHT) for i in range(n)])
+    edges = np.array([16383, 16384, 20470, 20471, 20472, 20473, 32768, 65535], np.uint16)
+    for i in range(n):
+        sites[i, 0, :16] = np.roll(np.tile(edges, 2), i)
+    sites[:, 1, 0] = 20471  # constant columns: table / log10_big path
+    sites[:, 1, 1] = 20472
+    r = _fused_job(L, sites)
+    assert r["welford_bright"] == 1, "the probe should pick the bright Welford form"
+    ref = orc.run_illumstats(list(sites))
+    assert_close_rel(r["mean"], ref.mean)
+    assert_close_rel(r["std"], ref.std)
+    assert_close_rel(r["mean"][0, :16], ref.mean[0, :16], rtol=1e-9)
+    assert_close_rel(r["std"][0, :16], ref.std[0, :16], rtol=1e-9)
+    assert r["std"][1, 0] == 0.0 and r["std"][1, 1] == 0.0
+    assert np.array_equal(r["acc"], ref.percentile_sums)
 
 
 @pytest.mark.parametrize("kind", ["lognormal_tails", "uniform", "constant", "two_values",
