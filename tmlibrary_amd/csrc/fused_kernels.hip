@@ -190,7 +190,8 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 }
 
 // ABL: development ablations (tools/mb), 0 in production: 1 = no histogram,
-// 2 = constant coefficients, 8 = no flush, 32 = no arithmetic.
+// 2 = constant coefficients, 8 = no flush, 32 = no arithmetic, 64 = values
+// beyond the slices not staged (the rare path's loop skipped).
 // NT threads per workgroup, LB LDS bins per workgroup (split into SPU slices
 // of BINS counters plus one overflow counter each: a pixel >= BINS adds to the
 // overflow counter -- never read -- and to its global bin, so the common path
@@ -391,6 +392,7 @@ __global__ __launch_bounds__(NT, (LB * 4 > 80 * 1024 && NT <= 512) ? 2 : 4) void
             msk |= ((t >> 16) ? 2u : 0u) << (2 * p);
           }
           if (PK) rare[k] += __builtin_popcount(msk);
+          if (ABL & 64) msk = 0u;  // (ablation: counted for the wrap check, not staged)
           while (msk) {
             const uint32_t b = __builtin_ctz(msk);
             msk &= msk - 1u;

@@ -13,7 +13,9 @@
 //                       A (33: no histogram, no arithmetic; 1: no histogram;
 //                       32: no arithmetic; 0: the real pass)
 //   read  flat, welford (production), wfread (its access shape, no compute)
-// Usage: mb_stream [n_sites=3456] [reps=3]
+// Usage: mb_stream [n_sites=3456] [reps=3] [dist=0 standard | 1 bright]
+// (bright: the packed configuration's ablations -- cfg 5, rare lists on --
+// beside the copies)
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -169,13 +171,14 @@ int main(int argc, char** argv) {
   try {
     const int64_t S = argc > 1 ? atoll(argv[1]) : 3456;
     const int reps = argc > 2 ? atoi(argv[2]) : 3;
+    const int dist = argc > 3 ? atoi(argv[3]) : 0;
     const int H = 2160, W = 2560, B = 64, shift = 6;
     const int64_t npx = (int64_t)H * W, ng = npx / 8;
     const size_t bytes = (size_t)S * npx * 2;
     const int nblk = (int)((S + B - 1) / B);
     uint16_t* in;
     CK(hipMalloc(&in, bytes));
-    launch_synth(in, S, H, W, 12345, 0, 0, 0, 0);
+    launch_synth(in, S, H, W, 12345, 0, 0, dist, 0);
     std::vector<uint16_t*> ib(nblk), ob(nblk);
     for (int k = 0; k < nblk; ++k) {
       ib[k] = in + (size_t)k * B * npx;
@@ -205,6 +208,11 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&sink, 4));
     CK(hipMalloc(&queues, kFusedQueueInts * sizeof(int)));
     CK(hipMalloc(&ctr, 4));
+    uint16_t* rare_v;
+    unsigned int* rare_n;
+    const unsigned int rare_cap = 65536;
+    CK(hipMalloc(&rare_v, (size_t)S * rare_cap * 2));
+    CK(hipMalloc(&rare_n, (size_t)S * 4));
     {
       // (c, a) planes of a plausible correction: c = 0.02 * log2 10, a = 1.02
       std::vector<float> c(npx * 2);
@@ -251,6 +259,53 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL(kern, dim3(cus * n_wg_mult), dim3(nt), 0, 0, J, npx, -1, -1, bands,
                          queues);
     };
+    // the packed configuration (cfg 5: 4 sites, 1,024 threads, u16 counters,
+    // rare lists), as abi.hip launches it for bright jobs
+    auto fusedp = [&](auto kern, int bands) {
+      CK(hipMemsetAsync(fn, 0, 4, 0));
+      CK(hipMemsetAsync(rmask, 0, S * 8, 0));
+      CK(hipMemsetAsync(queues, 0, kFusedQueueInts * sizeof(int), 0));
+      CK(hipMemsetAsync(rare_n, 0, (size_t)S * 4, 0));
+      FusedJobs J{};
+      J.n = 1;
+      J.j[0] = FusedJob{nullptr, nullptr, S, coef, mconst2, fl, hist, rmask,
+                        reinterpret_cast<unsigned long long*>(queues + 8), tab,
+                        RareList{rare_v, rare_n, rare_cap}};
+      hipLaunchKernelGGL(kern, dim3(cus), dim3(1024), 0, 0, J, npx, -1, -1, bands, queues);
+    };
+    if (dist == 1) {
+      for (int pass = 0; pass < 2; ++pass) {
+        printf("-- bright pass %d\n", pass);
+        time("copy flat", cbytes, [&] {
+          for (int k = 0; k < nblk; ++k) {
+            const int64_t n = std::min<int64_t>(B, S - (int64_t)k * B) * ng;
+            hipLaunchKernelGGL(k_flat_copy, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
+                               (const u32x4*)ib[k], (u32x4*)ob[k], n);
+          }
+        });
+        time("copy grid4", cbytes, [&] {
+          launch_box_probe(tin, tout, shift, S, npx, 1, (unsigned long long*)fe, sink, cus, 0);
+        });
+        time("packed abl33 (copy)", cbytes,
+             [&] { fusedp(k_correct_hist<true, false, 4, 33, 1024, 65536, true>, 8); });
+        time("packed abl1 (no hist)", cbytes,
+             [&] { fusedp(k_correct_hist<true, false, 4, 1, 1024, 65536, true>, 8); });
+        time("packed abl32 (no arith)", cbytes,
+             [&] { fusedp(k_correct_hist<true, false, 4, 32, 1024, 65536, true>, 8); });
+        time("packed abl0 (real)", cbytes,
+             [&] { fusedp(k_correct_hist<true, false, 4, 0, 1024, 65536, true>, 8); });
+        time("packed abl0 16 bands", cbytes,
+             [&] { fusedp(k_correct_hist<true, false, 4, 0, 1024, 65536, true>, 16); });
+        time("packed abl8 (no flush)", cbytes,
+             [&] { fusedp(k_correct_hist<true, false, 4, 8, 1024, 65536, true>, 8); });
+        time("packed abl64 (no rare path)", cbytes,
+             [&] { fusedp(k_correct_hist<true, false, 4, 64, 1024, 65536, true>, 8); });
+        time("packed abl96 (no rare, no arith)", cbytes,
+             [&] { fusedp(k_correct_hist<true, false, 4, 96, 1024, 65536, true>, 8); });
+      }
+      printf("done\n");
+      return 0;
+    }
     for (int pass = 0; pass < 2; ++pass) {  // twice: the order of the variants should not matter
       printf("-- pass %d\n", pass);
       time("copy flat", cbytes, [&] {
